@@ -1,0 +1,258 @@
+"""ctypes binding of libbcp.so (include/bcp.h) for tests, the bench and
+Python callers.  Thin: every call goes straight to the C ABI; there is no
+Python or CPU compute path here.  A missing library or GPU raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import errno
+import os
+import subprocess
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG_DIR, "lib", "libbcp.so")
+HEADER_DIR = os.path.join(os.path.dirname(PKG_DIR), "include")
+
+MAX_SOURCES = 56
+WINDOW_BYTES = 10 * 1024 * 1024
+
+
+class BcpError(RuntimeError):
+    def __init__(self, fn: str, rc: int):
+        super().__init__(f"{fn} failed: rc={rc} ({os.strerror(-rc) if rc < 0 else rc})")
+        self.rc = rc
+
+
+class Source(ctypes.Structure):
+    _fields_ = [("ptr", ctypes.c_uint64), ("len", ctypes.c_uint64)]
+
+
+class Stripe(ctypes.Structure):
+    _fields_ = [("dst", ctypes.c_uint64), ("out_len", ctypes.c_uint64), ("first_src", ctypes.c_uint32),
+                ("nsrc", ctypes.c_uint32), ("window", ctypes.c_uint64)]
+
+
+_lib = None
+
+_V = ctypes.c_void_p
+_SIGS = {
+    "bcp_abi_version": ([], ctypes.c_int),
+    "bcp_device_count": ([ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
+    "bcp_strerror": ([ctypes.c_int], ctypes.c_char_p),
+    "bcp_engine_create": ([ctypes.c_int, ctypes.POINTER(_V)], ctypes.c_int),
+    "bcp_engine_destroy": ([_V], ctypes.c_int),
+    "bcp_engine_info": ([_V, ctypes.POINTER(ctypes.c_int), ctypes.c_char_p, ctypes.c_size_t], ctypes.c_int),
+    "bcp_queue_create": ([_V, ctypes.POINTER(_V)], ctypes.c_int),
+    "bcp_queue_destroy": ([_V], ctypes.c_int),
+    "bcp_queue_sync": ([_V], ctypes.c_int),
+    "bcp_queue_query": ([_V], ctypes.c_int),
+    "bcp_event_create": ([_V, ctypes.POINTER(_V)], ctypes.c_int),
+    "bcp_event_destroy": ([_V], ctypes.c_int),
+    "bcp_event_record": ([_V, _V], ctypes.c_int),
+    "bcp_queue_wait_event": ([_V, _V], ctypes.c_int),
+    "bcp_event_sync": ([_V], ctypes.c_int),
+    "bcp_event_query": ([_V], ctypes.c_int),
+    "bcp_dev_alloc": ([_V, ctypes.c_size_t, ctypes.POINTER(_V)], ctypes.c_int),
+    "bcp_dev_free": ([_V, _V], ctypes.c_int),
+    "bcp_host_alloc": ([_V, ctypes.c_size_t, ctypes.POINTER(_V)], ctypes.c_int),
+    "bcp_host_free": ([_V, _V], ctypes.c_int),
+    "bcp_h2d_async": ([_V, _V, _V, ctypes.c_size_t], ctypes.c_int),
+    "bcp_d2h_async": ([_V, _V, _V, ctypes.c_size_t], ctypes.c_int),
+    "bcp_d2d_async": ([_V, _V, _V, ctypes.c_size_t], ctypes.c_int),
+    "bcp_h2d_2d_async": ([_V, _V, ctypes.c_size_t, _V, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t],
+                         ctypes.c_int),
+    "bcp_memset_async": ([_V, _V, ctypes.c_int, ctypes.c_size_t], ctypes.c_int),
+    "bcp_xor_uniform_async": ([_V, _V, _V, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64], ctypes.c_int),
+    "bcp_xor_strided_async": ([_V, _V, ctypes.c_uint64, _V, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
+                               ctypes.c_uint32, ctypes.c_uint64], ctypes.c_int),
+    "bcp_xor_stripes_async": ([_V, ctypes.POINTER(Stripe), ctypes.c_uint32, ctypes.POINTER(Source), ctypes.c_uint32],
+                              ctypes.c_int),
+    "bcp_xor_parity": ([_V, ctypes.c_size_t, _V, ctypes.c_int], ctypes.c_int),
+    "bcp_dev_fill_synthetic_async": ([_V, _V, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64], ctypes.c_int),
+    "bcp_dev_xor_fold_async": ([_V, _V, ctypes.c_uint64, _V], ctypes.c_int),
+    "bcp_dev_compare_async": ([_V, _V, _V, ctypes.c_uint64, _V], ctypes.c_int),
+    "bcp_queue_mark": ([_V, ctypes.c_int], ctypes.c_int),
+    "bcp_queue_elapsed_ms": ([_V, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_float)], ctypes.c_int),
+    "bcp_set_tuning": ([_V, ctypes.c_int, ctypes.c_int], ctypes.c_int),
+}
+
+
+def build() -> str:
+    subprocess.run(["make", "-s", "-j8", "-C", PKG_DIR], check=True)
+    return LIB_PATH
+
+
+def lib() -> ctypes.CDLL:
+    """Load libbcp.so (raises if it is missing: there is no fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise OSError(f"libbcp.so not built: {LIB_PATH} (run make -C {PKG_DIR})")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (args, res) in _SIGS.items():
+            fn = getattr(L, name)
+            fn.argtypes = args
+            fn.restype = res
+        _lib = L
+    return _lib
+
+
+def check(fn: str, rc: int) -> int:
+    if rc != 0:
+        raise BcpError(fn, rc)
+    return rc
+
+
+def call(fn: str, *args) -> int:
+    return check(fn, getattr(lib(), fn)(*args))
+
+
+def device_count() -> int:
+    n = ctypes.c_int(0)
+    call("bcp_device_count", ctypes.byref(n))
+    return n.value
+
+
+class Engine:
+    """One engine per device (bcp_engine_create)."""
+
+    def __init__(self, device: int = 0):
+        h = _V()
+        call("bcp_engine_create", device, ctypes.byref(h))
+        self.h = h
+        self.device = device
+        self._allocs: list[int] = []
+
+    def info(self):
+        cus = ctypes.c_int(0)
+        name = ctypes.create_string_buffer(256)
+        call("bcp_engine_info", self.h, ctypes.byref(cus), name, 256)
+        return cus.value, name.value.decode()
+
+    def tune(self, blocks_per_cu: int = 0, vecs_per_thread: int = 0):
+        call("bcp_set_tuning", self.h, blocks_per_cu, vecs_per_thread)
+
+    def queue(self) -> "Queue":
+        return Queue(self)
+
+    def event(self) -> "Event":
+        return Event(self)
+
+    def alloc(self, nbytes: int) -> int:
+        p = _V()
+        call("bcp_dev_alloc", self.h, nbytes, ctypes.byref(p))
+        return p.value
+
+    def free(self, ptr: int):
+        call("bcp_dev_free", self.h, _V(ptr))
+
+    def host_alloc(self, nbytes: int) -> int:
+        p = _V()
+        call("bcp_host_alloc", self.h, nbytes, ctypes.byref(p))
+        return p.value
+
+    def host_free(self, ptr: int):
+        call("bcp_host_free", self.h, _V(ptr))
+
+    def close(self):
+        if self.h:
+            call("bcp_engine_destroy", self.h)
+            self.h = None
+
+
+class Event:
+    def __init__(self, eng: Engine):
+        h = _V()
+        call("bcp_event_create", eng.h, ctypes.byref(h))
+        self.h = h
+
+    def record(self, q: "Queue"):
+        call("bcp_event_record", self.h, q.h)
+
+    def sync(self):
+        call("bcp_event_sync", self.h)
+
+    def close(self):
+        if self.h:
+            call("bcp_event_destroy", self.h)
+            self.h = None
+
+
+class Queue:
+    """One in-order HIP stream (bcp_queue_create)."""
+
+    def __init__(self, eng: Engine):
+        h = _V()
+        call("bcp_queue_create", eng.h, ctypes.byref(h))
+        self.h = h
+        self.eng = eng
+
+    def sync(self):
+        call("bcp_queue_sync", self.h)
+
+    def wait(self, ev: Event):
+        call("bcp_queue_wait_event", self.h, ev.h)
+
+    def h2d(self, dptr: int, host, nbytes: int | None = None):
+        """host: numpy array / bytes / int address."""
+        addr, n = _host_addr(host, nbytes)
+        call("bcp_h2d_async", self.h, _V(dptr), _V(addr), n)
+
+    def d2h(self, host, dptr: int, nbytes: int | None = None):
+        addr, n = _host_addr(host, nbytes)
+        call("bcp_d2h_async", self.h, _V(addr), _V(dptr), n)
+
+    def memset(self, dptr: int, value: int, nbytes: int):
+        call("bcp_memset_async", self.h, _V(dptr), value, nbytes)
+
+    def xor_uniform(self, dst: int, src: int, nstripes: int, nsrc: int, chunk: int):
+        call("bcp_xor_uniform_async", self.h, _V(dst), _V(src), nstripes, nsrc, chunk)
+
+    def xor_strided(self, dst: int, dst_stride: int, src: int, stripe_stride: int, src_stride: int,
+                    nstripes: int, nsrc: int, chunk: int):
+        call("bcp_xor_strided_async", self.h, _V(dst), dst_stride, _V(src), stripe_stride, src_stride,
+             nstripes, nsrc, chunk)
+
+    def xor_stripes(self, stripes, sources):
+        """stripes: list of (dst, out_len, first_src, nsrc, window); sources: list of (ptr, len)."""
+        st = (Stripe * max(len(stripes), 1))(*[Stripe(*s) for s in stripes])
+        so = (Source * max(len(sources), 1))(*[Source(*s) for s in sources])
+        call("bcp_xor_stripes_async", self.h, st, len(stripes), so, len(sources))
+
+    def fill_synthetic(self, dptr: int, nbytes: int, seed: int, byte_offset: int = 0):
+        call("bcp_dev_fill_synthetic_async", self.h, _V(dptr), nbytes, seed, byte_offset)
+
+    def xor_fold(self, src: int, nbytes: int, out16: int):
+        call("bcp_dev_xor_fold_async", self.h, _V(src), nbytes, _V(out16))
+
+    def compare(self, a: int, b: int, nbytes: int, out8: int):
+        call("bcp_dev_compare_async", self.h, _V(a), _V(b), nbytes, _V(out8))
+
+    def mark(self, slot: int):
+        call("bcp_queue_mark", self.h, slot)
+
+    def elapsed_ms(self, a: int, b: int) -> float:
+        ms = ctypes.c_float(0)
+        call("bcp_queue_elapsed_ms", self.h, a, b, ctypes.byref(ms))
+        return ms.value
+
+    def close(self):
+        if self.h:
+            call("bcp_queue_destroy", self.h)
+            self.h = None
+
+
+def _host_addr(host, nbytes):
+    import numpy as np
+    if isinstance(host, int):
+        assert nbytes is not None
+        return host, nbytes
+    if isinstance(host, (bytes, bytearray)):
+        arr = np.frombuffer(host, dtype=np.uint8)
+        return arr.ctypes.data, len(host) if nbytes is None else nbytes
+    return host.ctypes.data, host.nbytes if nbytes is None else nbytes
+
+
+def xor_parity(dst, nbytes: int, data, nsources: int):
+    """Drop-in for task_processing.c:96-109 on numpy buffers (GPU)."""
+    call("bcp_xor_parity", _V(dst.ctypes.data), nbytes, _V(data.ctypes.data), nsources)

@@ -1,0 +1,572 @@
+// bcp_engine.hip -- C ABI of libbcp.so (include/bcp.h): engine, queues,
+// events, memory, XOR submission and the xor_parity drop-in.
+//
+// The engine replaces the CPU fold at task_processing.c:211 (xor_parity,
+// :96-109).  Design points (MI355X):
+//  * one in-order HIP stream per queue; lanes (gen/main.c:821-845) each own a
+//    queue, so twelve lanes overlap their copies and kernels on the device;
+//  * descriptor batches are staged through a per-queue ring of pinned slots
+//    so submission never synchronises with earlier work of the same queue;
+//  * grids are persistent: CUs x blocks_per_cu workgroups of 256 threads.
+#include <errno.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <new>
+#include <vector>
+
+#include "bcp_internal.h"
+
+using namespace bcp;
+
+struct bcp_engine {
+  int device = 0;
+  int num_cus = 0;
+  char name[256] = {0};
+  Tuning tuning;
+  pthread_mutex_t lock = PTHREAD_MUTEX_INITIALIZER;
+};
+
+namespace {
+
+constexpr int kRingSlots = 4;
+constexpr int kTimerSlots = 8;
+
+struct DescSlot {
+  void *host = nullptr;   // pinned staging
+  void *dev = nullptr;    // device copy
+  size_t cap = 0;
+  hipEvent_t done = nullptr;  // recorded after the kernel that read `dev`
+  bool used = false;
+};
+
+}  // namespace
+
+struct bcp_queue {
+  bcp_engine *eng = nullptr;
+  hipStream_t stream = nullptr;
+  DescSlot ring[kRingSlots];
+  int next_slot = 0;
+  hipEvent_t timer[kTimerSlots] = {};
+};
+
+struct bcp_event {
+  bcp_engine *eng = nullptr;
+  hipEvent_t ev = nullptr;
+};
+
+// ---------------------------------------------------------------------------
+// helpers
+// ---------------------------------------------------------------------------
+#define HIP_RC(expr)                                                            \
+  do {                                                                          \
+    hipError_t e_ = (expr);                                                     \
+    if (e_ != hipSuccess) {                                                     \
+      if (getenv("BCP_VERBOSE"))                                                \
+        fprintf(stderr, "bcp: %s failed: %s (%s:%d)\n", #expr,                 \
+                hipGetErrorString(e_), __FILE__, __LINE__);                     \
+      return hip_to_errno(e_);                                                  \
+    }                                                                           \
+  } while (0)
+
+static int hip_to_errno(hipError_t e) {
+  switch (e) {
+    case hipSuccess: return 0;
+    case hipErrorOutOfMemory: return -ENOMEM;
+    case hipErrorNoDevice:
+    case hipErrorInvalidDevice: return -ENODEV;
+    case hipErrorInvalidValue: return -EINVAL;
+    case hipErrorNotReady: return -EAGAIN;
+    default: return -EIO;
+  }
+}
+
+static int set_device(bcp_engine *e) {
+  HIP_RC(hipSetDevice(e->device));
+  return 0;
+}
+
+static int grid_for(const bcp_engine *e) {
+  int g = e->num_cus * e->tuning.blocks_per_cu;
+  return g > 0 ? g : 256;
+}
+
+static bool aligned16(uint64_t x) { return (x & 15u) == 0; }
+
+// Reserve a ring slot of at least `bytes`; waits only if that slot's
+// previous kernel has not finished (kRingSlots submissions ago).
+static int ring_acquire(bcp_queue *q, size_t bytes, DescSlot **out) {
+  DescSlot *s = &q->ring[q->next_slot];
+  q->next_slot = (q->next_slot + 1) % kRingSlots;
+  if (s->used) HIP_RC(hipEventSynchronize(s->done));
+  if (s->cap < bytes) {
+    if (s->host) HIP_RC(hipHostFree(s->host));
+    if (s->dev) HIP_RC(hipFree(s->dev));
+    s->host = s->dev = nullptr;
+    size_t cap = 64 * 1024;
+    while (cap < bytes) cap *= 2;
+    HIP_RC(hipHostMalloc(&s->host, cap, hipHostMallocDefault));
+    HIP_RC(hipMalloc(&s->dev, cap));
+    s->cap = cap;
+  }
+  if (!s->done) HIP_RC(hipEventCreateWithFlags(&s->done, hipEventDisableTiming));
+  *out = s;
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// library / device
+// ---------------------------------------------------------------------------
+extern "C" int bcp_abi_version(void) { return BCP_ABI_VERSION; }
+
+extern "C" int bcp_device_count(int *count) {
+  if (!count) return -EINVAL;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+  *count = n;
+  return 0;
+}
+
+extern "C" const char *bcp_strerror(int rc) {
+  switch (rc) {
+    case 0: return "ok";
+    case -EINVAL: return "invalid argument";
+    case -ENOMEM: return "out of memory";
+    case -ENODEV: return "no usable HIP device";
+    case -EAGAIN: return "work pending";
+    case -EIO: return "HIP runtime error";
+    default: return "unknown error";
+  }
+}
+
+// ---------------------------------------------------------------------------
+// engine
+// ---------------------------------------------------------------------------
+extern "C" int bcp_engine_create(int device, bcp_engine **out) {
+  if (!out) return -EINVAL;
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return -ENODEV;
+  if (device < 0 || device >= n) return -ENODEV;
+  hipDeviceProp_t prop;
+  HIP_RC(hipGetDeviceProperties(&prop, device));
+  bcp_engine *e = new (std::nothrow) bcp_engine();
+  if (!e) return -ENOMEM;
+  e->device = device;
+  e->num_cus = prop.multiProcessorCount;
+  snprintf(e->name, sizeof(e->name), "%s (%s)", prop.name, prop.gcnArchName);
+  if (const char *v = getenv("BCP_BLOCKS_PER_CU")) e->tuning.blocks_per_cu = atoi(v);
+  if (const char *v = getenv("BCP_VECS_PER_THREAD")) e->tuning.vecs_per_thread = atoi(v);
+  if (e->tuning.blocks_per_cu < 1 || e->tuning.blocks_per_cu > 32) e->tuning.blocks_per_cu = 8;
+  if (e->tuning.vecs_per_thread != 1 && e->tuning.vecs_per_thread != 2 && e->tuning.vecs_per_thread != 4)
+    e->tuning.vecs_per_thread = 2;
+  *out = e;
+  return 0;
+}
+
+extern "C" int bcp_engine_destroy(bcp_engine *eng) {
+  if (!eng) return -EINVAL;
+  delete eng;
+  return 0;
+}
+
+extern "C" int bcp_engine_info(bcp_engine *eng, int *num_cus, char *name, size_t name_cap) {
+  if (!eng) return -EINVAL;
+  if (num_cus) *num_cus = eng->num_cus;
+  if (name && name_cap) snprintf(name, name_cap, "%s", eng->name);
+  return 0;
+}
+
+extern "C" int bcp_set_tuning(bcp_engine *eng, int blocks_per_cu, int vecs_per_thread) {
+  if (!eng) return -EINVAL;
+  if (blocks_per_cu < 0 || blocks_per_cu > 32) return -EINVAL;
+  if (vecs_per_thread != 0 && vecs_per_thread != 1 && vecs_per_thread != 2 && vecs_per_thread != 4) return -EINVAL;
+  pthread_mutex_lock(&eng->lock);
+  eng->tuning.blocks_per_cu = blocks_per_cu ? blocks_per_cu : 8;
+  eng->tuning.vecs_per_thread = vecs_per_thread ? vecs_per_thread : 2;
+  pthread_mutex_unlock(&eng->lock);
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// queues / events
+// ---------------------------------------------------------------------------
+extern "C" int bcp_queue_create(bcp_engine *eng, bcp_queue **out) {
+  if (!eng || !out) return -EINVAL;
+  *out = nullptr;
+  int rc = set_device(eng);
+  if (rc) return rc;
+  bcp_queue *q = new (std::nothrow) bcp_queue();
+  if (!q) return -ENOMEM;
+  q->eng = eng;
+  hipError_t e = hipStreamCreateWithFlags(&q->stream, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    delete q;
+    return hip_to_errno(e);
+  }
+  *out = q;
+  return 0;
+}
+
+extern "C" int bcp_queue_destroy(bcp_queue *q) {
+  if (!q) return -EINVAL;
+  set_device(q->eng);
+  (void)hipStreamSynchronize(q->stream);
+  for (auto &s : q->ring) {
+    if (s.host) (void)hipHostFree(s.host);
+    if (s.dev) (void)hipFree(s.dev);
+    if (s.done) (void)hipEventDestroy(s.done);
+  }
+  for (auto &t : q->timer)
+    if (t) (void)hipEventDestroy(t);
+  (void)hipStreamDestroy(q->stream);
+  delete q;
+  return 0;
+}
+
+extern "C" int bcp_queue_sync(bcp_queue *q) {
+  if (!q) return -EINVAL;
+  HIP_RC(hipStreamSynchronize(q->stream));
+  return 0;
+}
+
+extern "C" int bcp_queue_query(bcp_queue *q) {
+  if (!q) return -EINVAL;
+  hipError_t e = hipStreamQuery(q->stream);
+  if (e == hipErrorNotReady) return -EAGAIN;
+  return hip_to_errno(e);
+}
+
+extern "C" int bcp_event_create(bcp_engine *eng, bcp_event **out) {
+  if (!eng || !out) return -EINVAL;
+  int rc = set_device(eng);
+  if (rc) return rc;
+  bcp_event *ev = new (std::nothrow) bcp_event();
+  if (!ev) return -ENOMEM;
+  ev->eng = eng;
+  hipError_t e = hipEventCreateWithFlags(&ev->ev, hipEventDisableTiming);
+  if (e != hipSuccess) {
+    delete ev;
+    return hip_to_errno(e);
+  }
+  *out = ev;
+  return 0;
+}
+
+extern "C" int bcp_event_destroy(bcp_event *ev) {
+  if (!ev) return -EINVAL;
+  (void)hipEventDestroy(ev->ev);
+  delete ev;
+  return 0;
+}
+
+extern "C" int bcp_event_record(bcp_event *ev, bcp_queue *q) {
+  if (!ev || !q) return -EINVAL;
+  HIP_RC(hipEventRecord(ev->ev, q->stream));
+  return 0;
+}
+
+extern "C" int bcp_queue_wait_event(bcp_queue *q, bcp_event *ev) {
+  if (!ev || !q) return -EINVAL;
+  HIP_RC(hipStreamWaitEvent(q->stream, ev->ev, 0));
+  return 0;
+}
+
+extern "C" int bcp_event_sync(bcp_event *ev) {
+  if (!ev) return -EINVAL;
+  HIP_RC(hipEventSynchronize(ev->ev));
+  return 0;
+}
+
+extern "C" int bcp_event_query(bcp_event *ev) {
+  if (!ev) return -EINVAL;
+  hipError_t e = hipEventQuery(ev->ev);
+  if (e == hipErrorNotReady) return -EAGAIN;
+  return hip_to_errno(e);
+}
+
+extern "C" int bcp_queue_mark(bcp_queue *q, int slot) {
+  if (!q || slot < 0 || slot >= kTimerSlots) return -EINVAL;
+  if (!q->timer[slot]) HIP_RC(hipEventCreate(&q->timer[slot]));
+  HIP_RC(hipEventRecord(q->timer[slot], q->stream));
+  return 0;
+}
+
+extern "C" int bcp_queue_elapsed_ms(bcp_queue *q, int a, int b, float *ms) {
+  if (!q || !ms || a < 0 || b < 0 || a >= kTimerSlots || b >= kTimerSlots) return -EINVAL;
+  if (!q->timer[a] || !q->timer[b]) return -EINVAL;
+  HIP_RC(hipEventSynchronize(q->timer[b]));
+  HIP_RC(hipEventElapsedTime(ms, q->timer[a], q->timer[b]));
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// memory
+// ---------------------------------------------------------------------------
+extern "C" int bcp_dev_alloc(bcp_engine *eng, size_t bytes, void **dptr) {
+  if (!eng || !dptr) return -EINVAL;
+  *dptr = nullptr;
+  int rc = set_device(eng);
+  if (rc) return rc;
+  HIP_RC(hipMalloc(dptr, bytes ? bytes : 16));
+  return 0;
+}
+
+extern "C" int bcp_dev_free(bcp_engine *eng, void *dptr) {
+  if (!eng) return -EINVAL;
+  if (!dptr) return 0;
+  set_device(eng);
+  HIP_RC(hipFree(dptr));
+  return 0;
+}
+
+extern "C" int bcp_host_alloc(bcp_engine *eng, size_t bytes, void **hptr) {
+  if (!eng || !hptr) return -EINVAL;
+  *hptr = nullptr;
+  int rc = set_device(eng);
+  if (rc) return rc;
+  HIP_RC(hipHostMalloc(hptr, bytes ? bytes : 16, hipHostMallocDefault));
+  return 0;
+}
+
+extern "C" int bcp_host_free(bcp_engine *eng, void *hptr) {
+  if (!eng) return -EINVAL;
+  if (!hptr) return 0;
+  HIP_RC(hipHostFree(hptr));
+  return 0;
+}
+
+extern "C" int bcp_h2d_async(bcp_queue *q, void *dst, const void *src, size_t bytes) {
+  if (!q || (bytes && (!dst || !src))) return -EINVAL;
+  if (!bytes) return 0;
+  HIP_RC(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, q->stream));
+  return 0;
+}
+
+extern "C" int bcp_d2h_async(bcp_queue *q, void *dst, const void *src, size_t bytes) {
+  if (!q || (bytes && (!dst || !src))) return -EINVAL;
+  if (!bytes) return 0;
+  HIP_RC(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, q->stream));
+  return 0;
+}
+
+extern "C" int bcp_d2d_async(bcp_queue *q, void *dst, const void *src, size_t bytes) {
+  if (!q || (bytes && (!dst || !src))) return -EINVAL;
+  if (!bytes) return 0;
+  HIP_RC(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, q->stream));
+  return 0;
+}
+
+extern "C" int bcp_h2d_2d_async(bcp_queue *q, void *dst, size_t dpitch, const void *src, size_t hpitch,
+                                size_t row_bytes, size_t rows) {
+  if (!q || row_bytes > dpitch || row_bytes > hpitch) return -EINVAL;
+  if (!rows || !row_bytes) return 0;
+  if (!dst || !src) return -EINVAL;
+  HIP_RC(hipMemcpy2DAsync(dst, dpitch, src, hpitch, row_bytes, rows, hipMemcpyHostToDevice, q->stream));
+  return 0;
+}
+
+extern "C" int bcp_memset_async(bcp_queue *q, void *dst, int value, size_t bytes) {
+  if (!q || (bytes && !dst)) return -EINVAL;
+  if (!bytes) return 0;
+  HIP_RC(hipMemsetAsync(dst, value, bytes, q->stream));
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// XOR submission
+// ---------------------------------------------------------------------------
+
+// Submit a descriptor batch (host arrays) on q.
+static int submit_desc(bcp_queue *q, const bcp_stripe *stripes, uint32_t nstripes, const bcp_source *sources,
+                       uint32_t nsources) {
+  bcp_engine *e = q->eng;
+  const int vecs = e->tuning.vecs_per_thread;
+  const uint32_t tile_bytes = desc_tile_bytes(vecs);
+  // Validate and count tiles.
+  uint64_t ntiles = 0;
+  for (uint32_t i = 0; i < nstripes; i++) {
+    const bcp_stripe &s = stripes[i];
+    if ((uint64_t)s.first_src + s.nsrc > nsources) return -EINVAL;
+    if (s.nsrc > BCP_MAX_SOURCES) return -EINVAL;
+    if (s.out_len && !s.dst) return -EINVAL;
+    if (s.window && (s.window & 15u)) return -EINVAL;
+    for (uint32_t k = 0; k < s.nsrc; k++)
+      if (sources[s.first_src + k].len && !sources[s.first_src + k].ptr) return -EINVAL;
+    ntiles += (s.out_len + tile_bytes - 1) / tile_bytes;
+  }
+  if (ntiles == 0) return 0;
+  if (ntiles > 0xFFFFFFF0ull) return -EINVAL;
+  const size_t off_src = (size_t)nstripes * sizeof(bcp_stripe);
+  const size_t off_tiles = (off_src + (size_t)nsources * sizeof(bcp_source) + 15) & ~(size_t)15;
+  const size_t bytes = off_tiles + ((size_t)nstripes + 1) * sizeof(uint32_t);
+  DescSlot *slot = nullptr;
+  int rc = ring_acquire(q, bytes, &slot);
+  if (rc) return rc;
+  char *h = (char *)slot->host;
+  memcpy(h, stripes, off_src);
+  if (nsources) memcpy(h + off_src, sources, (size_t)nsources * sizeof(bcp_source));
+  uint32_t *ts = (uint32_t *)(h + off_tiles);
+  uint32_t acc = 0;
+  for (uint32_t i = 0; i < nstripes; i++) {
+    ts[i] = acc;
+    acc += (uint32_t)((stripes[i].out_len + tile_bytes - 1) / tile_bytes);
+  }
+  ts[nstripes] = acc;
+  HIP_RC(hipMemcpyAsync(slot->dev, slot->host, bytes, hipMemcpyHostToDevice, q->stream));
+  DescBatch b;
+  char *d = (char *)slot->dev;
+  b.stripes = (const bcp_stripe *)d;
+  b.sources = (const bcp_source *)(d + off_src);
+  b.tile_start = (const uint32_t *)(d + off_tiles);
+  b.nstripes = nstripes;
+  b.ntiles = acc;
+  b.tile_bytes = tile_bytes;
+  HIP_RC(launch_xor_desc(q->stream, grid_for(e), vecs, b));
+  HIP_RC(hipEventRecord(slot->done, q->stream));
+  slot->used = true;
+  return 0;
+}
+
+extern "C" int bcp_xor_stripes_async(bcp_queue *q, const bcp_stripe *stripes, uint32_t nstripes,
+                                     const bcp_source *sources, uint32_t nsources) {
+  if (!q || (nstripes && !stripes) || (nsources && !sources)) return -EINVAL;
+  if (!nstripes) return 0;
+  int rc = set_device(q->eng);
+  if (rc) return rc;
+  return submit_desc(q, stripes, nstripes, sources, nsources);
+}
+
+extern "C" int bcp_xor_strided_async(bcp_queue *q, void *dst, uint64_t dst_stride, const void *src,
+                                     uint64_t stripe_stride, uint64_t src_stride, uint64_t nstripes,
+                                     uint32_t nsrc, uint64_t chunk_bytes) {
+  if (!q || nsrc == 0 || nsrc > BCP_MAX_SOURCES) return -EINVAL;
+  if (!nstripes || !chunk_bytes) return 0;
+  if (!dst || !src) return -EINVAL;
+  bcp_engine *e = q->eng;
+  int rc = set_device(e);
+  if (rc) return rc;
+  const bool fast = aligned16((uint64_t)dst) && aligned16((uint64_t)src) && aligned16(dst_stride) &&
+                    aligned16(stripe_stride) && aligned16(src_stride) && aligned16(chunk_bytes) &&
+                    chunk_bytes / 16 <= 0xFFFFFFFFull;
+  if (fast) {
+    HIP_RC(launch_xor_strided_fast(q->stream, grid_for(e), e->tuning.vecs_per_thread, (char *)dst, dst_stride,
+                                   (const char *)src, stripe_stride, src_stride, nstripes, nsrc, chunk_bytes));
+    return 0;
+  }
+  // General geometry: express as descriptors (any alignment / tail).
+  if (nstripes * nsrc > 0xFFFFFFFFull || nstripes > 0xFFFFFFFFull) return -EINVAL;
+  std::vector<bcp_stripe> st(nstripes);
+  std::vector<bcp_source> so(nstripes * nsrc);
+  for (uint64_t s = 0; s < nstripes; s++) {
+    st[s].dst = (uint64_t)dst + s * dst_stride;
+    st[s].out_len = chunk_bytes;
+    st[s].first_src = (uint32_t)(s * nsrc);
+    st[s].nsrc = nsrc;
+    st[s].window = 0;
+    for (uint32_t k = 0; k < nsrc; k++) {
+      so[s * nsrc + k].ptr = (uint64_t)src + s * stripe_stride + k * src_stride;
+      so[s * nsrc + k].len = chunk_bytes;
+    }
+  }
+  return submit_desc(q, st.data(), (uint32_t)nstripes, so.data(), (uint32_t)so.size());
+}
+
+extern "C" int bcp_xor_uniform_async(bcp_queue *q, void *dst, const void *src, uint64_t nstripes, uint32_t nsrc,
+                                     uint64_t chunk_bytes) {
+  return bcp_xor_strided_async(q, dst, chunk_bytes, src, chunk_bytes * nsrc, chunk_bytes, nstripes, nsrc,
+                               chunk_bytes);
+}
+
+// ---------------------------------------------------------------------------
+// verification / synthetic data
+// ---------------------------------------------------------------------------
+extern "C" int bcp_dev_fill_synthetic_async(bcp_queue *q, void *dst, uint64_t bytes, uint64_t seed,
+                                            uint64_t byte_offset) {
+  if (!q || (bytes && !dst)) return -EINVAL;
+  int rc = set_device(q->eng);
+  if (rc) return rc;
+  HIP_RC(launch_fill_synthetic(q->stream, grid_for(q->eng), (char *)dst, bytes, seed, byte_offset));
+  return 0;
+}
+
+extern "C" int bcp_dev_xor_fold_async(bcp_queue *q, const void *src, uint64_t bytes, void *out16_dev) {
+  if (!q || !out16_dev || (bytes && !src)) return -EINVAL;
+  if (!aligned16((uint64_t)src)) return -EINVAL;
+  int rc = set_device(q->eng);
+  if (rc) return rc;
+  HIP_RC(hipMemsetAsync(out16_dev, 0, 16, q->stream));
+  HIP_RC(launch_xor_fold(q->stream, grid_for(q->eng), (const char *)src, bytes, (uint32_t *)out16_dev));
+  return 0;
+}
+
+extern "C" int bcp_dev_compare_async(bcp_queue *q, const void *a, const void *b, uint64_t bytes, void *out_dev) {
+  if (!q || !out_dev || (bytes && (!a || !b))) return -EINVAL;
+  if (!aligned16((uint64_t)a) || !aligned16((uint64_t)b)) return -EINVAL;
+  int rc = set_device(q->eng);
+  if (rc) return rc;
+  HIP_RC(hipMemsetAsync(out_dev, 0, 8, q->stream));
+  HIP_RC(launch_compare(q->stream, grid_for(q->eng), (const char *)a, (const char *)b, bytes,
+                        (unsigned long long *)out_dev));
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// xor_parity drop-in (task_processing.c:96-109)
+// ---------------------------------------------------------------------------
+namespace {
+
+pthread_once_t g_once = PTHREAD_ONCE_INIT;
+bcp_engine *g_engine = nullptr;
+int g_engine_rc = 0;
+
+void init_global_engine() {
+  int dev = 0;
+  if (const char *v = getenv("BCP_DEVICE")) dev = atoi(v);
+  g_engine_rc = bcp_engine_create(dev, &g_engine);
+}
+
+struct DropinState {
+  bcp_queue *q = nullptr;
+  void *dev = nullptr;
+  size_t cap = 0;
+  ~DropinState() {
+    if (q) {
+      if (dev) bcp_dev_free(g_engine, dev);
+      bcp_queue_destroy(q);
+    }
+  }
+};
+thread_local DropinState t_dropin;
+
+}  // namespace
+
+extern "C" int bcp_xor_parity(uint8_t *dst, size_t nbytes, const uint8_t *data, int nsources) {
+  if (nsources < 1 || nsources > BCP_MAX_SOURCES) return -EINVAL;
+  if (!nbytes) return 0;
+  if (!dst || !data) return -EINVAL;
+  pthread_once(&g_once, init_global_engine);
+  if (g_engine_rc) return g_engine_rc;
+  DropinState &st = t_dropin;
+  int rc = 0;
+  if (!st.q && (rc = bcp_queue_create(g_engine, &st.q))) return rc;
+  // Device layout: sources at a 256-byte pitch so every row is aligned, then
+  // the output row.
+  const size_t pitch = (nbytes + 255) & ~(size_t)255;
+  const size_t need = pitch * ((size_t)nsources + 1);
+  if (st.cap < need) {
+    if (st.dev) bcp_dev_free(g_engine, st.dev);
+    st.dev = nullptr;
+    st.cap = 0;
+    if ((rc = bcp_dev_alloc(g_engine, need, &st.dev))) return rc;
+    st.cap = need;
+  }
+  char *dv = (char *)st.dev;
+  if ((rc = bcp_h2d_2d_async(st.q, dv, pitch, data, nbytes, nbytes, (size_t)nsources))) return rc;
+  char *dout = dv + pitch * (size_t)nsources;
+  if ((rc = bcp_xor_strided_async(st.q, dout, pitch, dv, pitch * nsources, pitch, 1, (uint32_t)nsources, nbytes)))
+    return rc;
+  if ((rc = bcp_d2h_async(st.q, dst, dout, nbytes))) return rc;
+  return bcp_queue_sync(st.q);
+}

@@ -1,0 +1,263 @@
+#!/usr/bin/env python3
+"""bench.py -- device-resident chunk-XOR parity throughput on MI355X.
+
+Workload (BASELINE.json configs[1], "config 2"): 12,500 stripes x 8 sources
+x 512 KiB (100,000 data chunks = 48.8 GiB) resident in HBM per GPU; one step
+= one pass of the parity kernel over all stripes (xor_strided_fast<8,U>,
+the reference's xor_parity, task_processing.c:96-109, batched).
+`--mode rebuild` times config 3 instead (7 survivors + parity body ->
+rebuilt chunk, descriptor kernel).
+
+value = algorithmic bytes of all ranks / max-over-ranks wall time, with
+algorithmic bytes = sum of source lengths + output length per stripe
+((N+1) x 512 KiB = 4,718,592 B for config 2).  N>1 (torchrun): each rank owns
+its own stripe shard on its own GPU (no data-path collective; gloo only for
+the start barrier and the max-time reduction), scaling "weak".
+
+roofline.achieved uses the kernel's HIP-event time on the stream it runs on;
+roofline.traffic comes from the committed rocprofv3 PMC pass
+(profiles/*pmc*.json) when it matches this workload, else null.
+cpu_baseline: rank 0 at N=1 times the oracle's C restatement of xor_parity
+(-std=gnu99 -Os, the reference flags) on a bounded sample of the same
+stripes, 1 thread ("port").
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "beegfs-chunk-parity_amd"))
+
+import bcp_ctypes as bcp  # noqa: E402
+
+KiB = 1024
+GiB = 1024 ** 3
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, MI355X_MICROARCH.md chip table
+METRIC = "GiB/s device-resident XOR parity, 512 KiB chunks, 8-wide stripe; % HBM peak"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--mode", choices=["gen", "rebuild"], default="gen")
+    ap.add_argument("--stripes", type=int, default=12500, help="stripes per GPU")
+    ap.add_argument("--nsrc", type=int, default=8)
+    ap.add_argument("--chunk", type=int, default=512 * KiB)
+    ap.add_argument("--blocks-per-cu", type=int, default=0)
+    ap.add_argument("--vecs", type=int, default=0)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-stripes", type=int, default=256, help="stripes in the CPU sample pool")
+    ap.add_argument("--no-cpu", action="store_true")
+    return ap.parse_args()
+
+
+class Dist:
+    def __init__(self):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+        self.pg = None
+        if self.world > 1:
+            import torch.distributed as dist
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            dist.init_process_group("gloo", rank=self.rank, world_size=self.world)
+            self.pg = dist
+
+    def barrier(self):
+        if self.pg:
+            self.pg.barrier()
+
+    def max(self, x: float) -> float:
+        if not self.pg:
+            return x
+        import torch
+        t = torch.tensor([x], dtype=torch.float64)
+        self.pg.all_reduce(t, op=self.pg.ReduceOp.MAX)
+        return float(t.item())
+
+    def sum(self, x: float) -> float:
+        if not self.pg:
+            return x
+        import torch
+        t = torch.tensor([x], dtype=torch.float64)
+        self.pg.all_reduce(t, op=self.pg.ReduceOp.SUM)
+        return float(t.item())
+
+    def close(self):
+        if self.pg:
+            self.pg.destroy_process_group()
+
+
+def pmc_traffic(workload_key: str):
+    """Per-launch HBM bytes from the committed PMC summary, if it matches."""
+    best = None
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
+        try:
+            doc = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        if doc.get("workload_key") == workload_key and doc.get("hbm_bytes_per_launch"):
+            best = doc
+    return best
+
+
+def main():
+    a = parse()
+    d = Dist()
+    eng = bcp.Engine(d.local_rank)
+    if a.blocks_per_cu or a.vecs:
+        eng.tune(a.blocks_per_cu, a.vecs)
+    cus, devname = eng.info()
+    q = eng.queue()
+    S, N, C = a.stripes, a.nsrc, a.chunk
+    src = eng.alloc(S * N * C)
+    out = eng.alloc(S * C)
+    chk = eng.alloc(64)
+    q.fill_synthetic(src, S * N * C, seed=1 + d.rank)
+
+    if a.mode == "gen":
+        def step():
+            q.xor_uniform(out, src, S, N, C)
+        bytes_per_step = S * (N + 1) * C
+        kernel = f"xor_strided_fast<{N},U>"
+        workload = f"config2: parity gen, {S} stripes x {N} x {C // KiB} KiB device-resident"
+    else:
+        # config 3: parity first, then rebuild source index 3 from the other
+        # N-1 chunks + parity body (descriptor kernel; truncation to 512 KiB).
+        par = eng.alloc(S * C)
+        q.xor_uniform(par, src, S, N, C)
+        victim = min(3, N - 1)
+        stripes, sources = [], []
+        for s in range(S):
+            first = len(sources)
+            for k in range(N):
+                if k != victim:
+                    sources.append((src + (s * N + k) * C, C))
+            sources.append((par + s * C, C))
+            stripes.append((out + s * C, C, first, N, 0))
+        import ctypes
+        st = (bcp.Stripe * len(stripes))(*[bcp.Stripe(*x) for x in stripes])
+        so = (bcp.Source * len(sources))(*[bcp.Source(*x) for x in sources])
+        L = bcp.lib()
+
+        def step():
+            bcp.check("bcp_xor_stripes_async", L.bcp_xor_stripes_async(q.h, st, len(stripes), so, len(sources)))
+        bytes_per_step = S * (N + 1) * C
+        kernel = "xor_desc<U>"
+        workload = f"config3: rebuild, {S} stripes x ({N - 1} survivors + parity) x {C // KiB} KiB device-resident"
+
+    for _ in range(a.warmup):
+        step()
+    q.sync()
+
+    d.barrier()
+    q.sync()
+    t0 = time.perf_counter()
+    q.mark(0)
+    for _ in range(a.steps):
+        step()
+    q.mark(1)
+    q.sync()
+    t1 = time.perf_counter()
+    d.barrier()
+    wall = t1 - t0
+    kern_ms = q.elapsed_ms(0, 1) / a.steps  # avg launch duration on the kernel's stream
+
+    # device-side property check (no oracle here): fold(output) == fold(inputs)
+    verified = None
+    if a.mode == "gen":
+        q.xor_fold(out, S * C, chk)
+        q.xor_fold(src, S * N * C, chk + 16)
+        import numpy as np
+        f = np.empty(32, dtype=np.uint8)
+        q.d2h(f, chk, 32)
+        q.sync()
+        verified = bool(np.array_equal(f[:16], f[16:]))
+    else:
+        import numpy as np
+        victim = min(3, N - 1)
+        gathered = eng.alloc(S * C)
+        q.xor_strided(gathered, C, src + victim * C, N * C, C, S, 1, C)
+        q.compare(out, gathered, S * C, chk)
+        f = np.empty(8, dtype=np.uint8)
+        q.d2h(f, chk, 8)
+        q.sync()
+        verified = int(f.view("<u8")[0]) == 0
+
+    wall_max = d.max(wall)
+    total_bytes = d.sum(float(bytes_per_step * a.steps))
+    ok_all = d.sum(1.0 if verified else 0.0) == d.world
+    kern_ms_max = d.max(kern_ms)
+
+    cpu = None
+    if d.rank == 0 and d.world == 1 and not a.no_cpu:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle  # cpu_baseline leg only
+        bps = oracle.bench_xor(1, a.cpu_stripes, N, C, a.cpu_seconds)
+        cpu = {"value": round(bps / GiB, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
+               "sample": f"oracle_xor_parity (-std=gnu99 -Os) over a {a.cpu_stripes}-stripe pool of {N} x "
+                         f"{C // KiB} KiB synthetic chunks, looped >= {a.cpu_seconds:g} s on 1 host thread; "
+                         f"(N+1)*S bytes per stripe"}
+
+    if d.rank == 0:
+        value = total_bytes / wall_max / GiB
+        achieved = bytes_per_step / (kern_ms_max * 1e-3) / 1e9
+        wkey = f"{a.mode}:{S}x{N}x{C}"
+        pmc = pmc_traffic(wkey)
+        line = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "GiB/s",
+            "n_gpus": d.world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(wall_max / a.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (splitmix64 stream, seed 1+rank), generated on device",
+            "config": {
+                "workload": workload,
+                "mode": a.mode,
+                "stripes_per_gpu": S,
+                "nsrc": N,
+                "chunk_bytes": C,
+                "bytes_per_step_per_gpu": bytes_per_step,
+                "data_rate_GiBps": round(value * N / (N + 1), 2),
+                "pct_hbm_peak": round(100.0 * achieved / HBM_PEAK_GBS, 2),
+                "parallelism": f"shard{d.world} (stripes per GPU, no collective)",
+                "device": devname,
+                "cus": cus,
+                "verified_on_device": ok_all,
+            },
+            "roofline": {
+                "bound": "hbm",
+                "kernel": kernel,
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "kernel_ms": round(kern_ms_max, 4),
+                "traffic": pmc["hbm_bytes_per_launch"] if pmc else None,
+                "traffic_source": pmc["source"] if pmc else None,
+            },
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    q.close()
+    eng.close()
+    d.close()
+    if not ok_all:
+        sys.exit(3)
+
+
+if __name__ == "__main__":
+    main()

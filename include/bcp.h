@@ -1,0 +1,173 @@
+/*
+ * bcp.h -- C ABI of the MI355X chunk-XOR parity engine (libbcp.so).
+ *
+ * Drop-in boundary for the arithmetic seam of runefriborg/beegfs-chunk-parity:
+ *
+ *   static void xor_parity(uint8_t *restrict dst, size_t nbytes,
+ *                          const uint8_t *data, int nsources);
+ *       -- src/beegfs-raid5/common/task_processing.c:96-109
+ *
+ * which the P role (parity_generator, task_processing.c:117-245) calls once
+ * per 10 MiB window.  This ABI replaces it with
+ *   (1) bcp_xor_parity(): the same signature and semantics, on the GPU;
+ *   (2) an engine/queue lifecycle (one queue = one HIP stream pair, one per
+ *       lane thread, gen/main.c:821-845 runs 12 lanes per rank);
+ *   (3) batched asynchronous submission of stripe descriptors, because one
+ *       512 KiB x 8 stripe is ~1 us of HBM time -- far below a launch;
+ *   (4) query / wait on completion, and HIP-event timing for the bench.
+ *
+ * Conventions: plain C types only; every function returns 0 or a negative
+ * errno value (-EINVAL, -ENOMEM, -ENODEV, -EIO, -EAGAIN); nothing throws
+ * across the ABI.  An engine is thread-safe; a queue belongs to one thread
+ * at a time.  There is no CPU fallback: without a usable gfx950 device every
+ * compute entry point returns -ENODEV.
+ *
+ * Semantics of every XOR entry point (bit-exact with the reference,
+ * SURVEY.md §8(a)):
+ *   out[j] = XOR_k  src_k'[j]         for 0 <= j < out_len
+ * where src_k'[j] = src_k[j] if j < len_k else 0 (zero padding), except when
+ * a stripe carries window W != 0: then byte j of window w = j / W of a source
+ * with last readable window lw_k = (len_k - 1) / W and w > lw_k replays
+ * window lw_k (chunk_sender never refills its buffer after EOF,
+ * task_processing.c:291-308, quirk A3-q1).  len_k = 0 always reads zeros.
+ */
+#ifndef BCP_H
+#define BCP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BCP_ABI_VERSION 1
+#define BCP_MAX_SOURCES 56                  /* MAX_STORAGE_TARGETS, common.h:18 */
+#define BCP_WINDOW_BYTES (10u * 1024u * 1024u) /* FILE_TRANSFER_BUFFER_SIZE, task_processing.c:20 */
+
+typedef struct bcp_engine bcp_engine;
+typedef struct bcp_queue bcp_queue;
+
+/* One source of a stripe: device address and readable length in bytes. */
+typedef struct bcp_source {
+    uint64_t ptr;
+    uint64_t len;
+} bcp_source;
+
+/* One stripe: out[0..out_len) = XOR of sources[first_src .. first_src+nsrc).
+ * window = 0 for plain zero padding, or the transfer window (normally
+ * BCP_WINDOW_BYTES, must be a multiple of 16) when the stream exceeded one
+ * window and the reference's replay semantics apply. */
+typedef struct bcp_stripe {
+    uint64_t dst;
+    uint64_t out_len;
+    uint32_t first_src;
+    uint32_t nsrc;
+    uint64_t window;
+} bcp_stripe;
+
+/* ---- library / device ------------------------------------------------- */
+int bcp_abi_version(void);
+/* Number of visible HIP devices (0 without a GPU; never fails for that). */
+int bcp_device_count(int *count);
+/* Human-readable message for a return code. */
+const char *bcp_strerror(int rc);
+
+/* ---- engine lifecycle ------------------------------------------------- */
+/* Create an engine bound to `device` (HIP ordinal). */
+int bcp_engine_create(int device, bcp_engine **out);
+int bcp_engine_destroy(bcp_engine *eng);
+/* Device properties the bench reports: CU count and the name string. */
+int bcp_engine_info(bcp_engine *eng, int *num_cus, char *name, size_t name_cap);
+
+/* ---- queues (one in-order HIP stream each) ----------------------------- */
+/* Work on one queue runs in submission order.  Overlap (copy beside compute)
+ * comes from using two queues ordered by events, as the pipeline does. */
+int bcp_queue_create(bcp_engine *eng, bcp_queue **out);
+int bcp_queue_destroy(bcp_queue *q);
+/* Block until everything submitted to q has finished. */
+int bcp_queue_sync(bcp_queue *q);
+/* 0 if idle, -EAGAIN if work is pending. */
+int bcp_queue_query(bcp_queue *q);
+
+/* ---- completion handles (HIP events) ---------------------------------- */
+typedef struct bcp_event bcp_event;
+int bcp_event_create(bcp_engine *eng, bcp_event **out);
+int bcp_event_destroy(bcp_event *ev);
+/* Mark the current tail of q; later bcp_queue_wait_event() / bcp_event_sync()
+ * see everything submitted to q before this call. */
+int bcp_event_record(bcp_event *ev, bcp_queue *q);
+/* Make later work on q wait (on the device) for ev. */
+int bcp_queue_wait_event(bcp_queue *q, bcp_event *ev);
+/* Host wait; bcp_event_query: 0 done, -EAGAIN pending. */
+int bcp_event_sync(bcp_event *ev);
+int bcp_event_query(bcp_event *ev);
+
+/* ---- memory ----------------------------------------------------------- */
+int bcp_dev_alloc(bcp_engine *eng, size_t bytes, void **dptr);
+int bcp_dev_free(bcp_engine *eng, void *dptr);
+/* Pinned (page-locked) host memory for staging. */
+int bcp_host_alloc(bcp_engine *eng, size_t bytes, void **hptr);
+int bcp_host_free(bcp_engine *eng, void *hptr);
+/* Async copies, in order on q. */
+int bcp_h2d_async(bcp_queue *q, void *dst, const void *src, size_t bytes);
+int bcp_d2h_async(bcp_queue *q, void *dst, const void *src, size_t bytes);
+int bcp_d2d_async(bcp_queue *q, void *dst, const void *src, size_t bytes);
+/* Pitched H2D: `rows` rows of `row_bytes`, host pitch hpitch, device pitch dpitch. */
+int bcp_h2d_2d_async(bcp_queue *q, void *dst, size_t dpitch, const void *src,
+                     size_t hpitch, size_t row_bytes, size_t rows);
+int bcp_memset_async(bcp_queue *q, void *dst, int value, size_t bytes);
+
+/* ---- XOR kernels (device pointers, asynchronous on q) ------------------ */
+/* Uniform stripes: src is [nstripes][nsrc][chunk_bytes] contiguous, dst is
+ * [nstripes][chunk_bytes].  Any alignment / length is accepted; 16-byte
+ * aligned pointers with chunk_bytes % 16 == 0 take the streaming fast path. */
+int bcp_xor_uniform_async(bcp_queue *q, void *dst, const void *src,
+                          uint64_t nstripes, uint32_t nsrc,
+                          uint64_t chunk_bytes);
+/* Same, but sources given by a stride: source k of stripe s starts at
+ * src + s*stripe_stride + k*src_stride; output s at dst + s*dst_stride. */
+int bcp_xor_strided_async(bcp_queue *q, void *dst, uint64_t dst_stride,
+                          const void *src, uint64_t stripe_stride,
+                          uint64_t src_stride, uint64_t nstripes,
+                          uint32_t nsrc, uint64_t chunk_bytes);
+/* Descriptor batch (variable lengths, zero padding, rebuild truncation,
+ * window replay).  Host arrays are copied before return. */
+int bcp_xor_stripes_async(bcp_queue *q, const bcp_stripe *stripes,
+                          uint32_t nstripes, const bcp_source *sources,
+                          uint32_t nsources);
+
+/* ---- drop-in for xor_parity (task_processing.c:96-109) ----------------- */
+/* Host pointers, synchronous, same contract as the reference: dst gets
+ * XOR of the nsources rows of `data` ([nsources][nbytes]).  Runs on a
+ * process-wide engine (device from $BCP_DEVICE, default 0) and a per-thread
+ * queue with pinned staging; returns -ENODEV without a GPU. */
+int bcp_xor_parity(uint8_t *dst, size_t nbytes, const uint8_t *data,
+                   int nsources);
+
+/* ---- verification / synthetic data (device) --------------------------- */
+/* Fill with the splitmix64 byte stream: byte b = byte (b&7) of
+ * splitmix64(seed + (byte_offset + b)/8).  Same stream as the oracle's
+ * oracle_fill_synthetic, so checks need no bulk host copy. */
+int bcp_dev_fill_synthetic_async(bcp_queue *q, void *dst, uint64_t bytes,
+                                 uint64_t seed, uint64_t byte_offset);
+/* XOR-fold of a buffer into 16 bytes (out16_dev is device memory). */
+int bcp_dev_xor_fold_async(bcp_queue *q, const void *src, uint64_t bytes,
+                           void *out16_dev);
+/* Count of differing bytes between two device buffers into *out_dev (u64). */
+int bcp_dev_compare_async(bcp_queue *q, const void *a, const void *b,
+                          uint64_t bytes, void *out_dev);
+
+/* ---- timing (HIP events on the queue's stream) ------------------------- */
+int bcp_queue_mark(bcp_queue *q, int slot);           /* slot 0..7 */
+int bcp_queue_elapsed_ms(bcp_queue *q, int slot_from, int slot_to,
+                         float *ms);
+
+/* Tuning knobs for the fast path (bench / autotune only; 0 = default). */
+int bcp_set_tuning(bcp_engine *eng, int blocks_per_cu, int vecs_per_thread);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* BCP_H */

@@ -1,0 +1,47 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "beegfs-chunk-parity_amd")
+for p in (PKG, os.path.join(ROOT, "oracle"), ROOT):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs through libbcp.so on the device)")
+
+
+@pytest.fixture(scope="session")
+def oracle():
+    import oracle as O
+    O.build()
+    return O
+
+
+@pytest.fixture(scope="session")
+def bcp():
+    """libbcp ctypes module; GPU tests fail (not skip) when the device or library is missing."""
+    import bcp_ctypes
+    if not os.path.exists(bcp_ctypes.LIB_PATH):
+        bcp_ctypes.build()
+    bcp_ctypes.lib()
+    return bcp_ctypes
+
+
+@pytest.fixture(scope="session")
+def engine(bcp):
+    n = bcp.device_count()
+    assert n > 0, "gpu test needs a HIP device (no CPU fallback exists)"
+    eng = bcp.Engine(0)
+    yield eng
+    eng.close()
+
+
+@pytest.fixture(scope="session")
+def queue(engine):
+    q = engine.queue()
+    yield q
+    q.close()

@@ -1,0 +1,342 @@
+"""GPU parity tests: every XOR entry point of libbcp.so (through the C ABI)
+against the oracle restatement, the committed golden vectors and, at the
+BASELINE sizes, size-independent properties (XOR-fold conservation, sampled
+oracle stripes, rebuild round trip)."""
+import concurrent.futures as cf
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+GOLD = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "kats.json")))
+KiB, MiB = 1024, 1024 * 1024
+
+
+class Dev:
+    """Scratch device allocations freed at test end."""
+
+    def __init__(self, eng, q):
+        self.eng, self.q, self.ptrs = eng, q, []
+
+    def alloc(self, n):
+        p = self.eng.alloc(max(n, 16))
+        self.ptrs.append(p)
+        return p
+
+    def put(self, arr, pad=0):
+        """Upload arr at byte offset `pad` inside a fresh allocation; returns device address."""
+        arr = np.ascontiguousarray(arr, dtype=np.uint8)
+        base = self.alloc(arr.size + pad + 16)
+        if arr.size:
+            self.q.h2d(base + pad, arr)
+        return base + pad
+
+    def get(self, ptr, n):
+        out = np.empty(max(n, 1), dtype=np.uint8)
+        if n:
+            self.q.d2h(out, ptr, n)
+        self.q.sync()
+        return out[:n]
+
+    def free(self):
+        self.q.sync()
+        for p in self.ptrs:
+            self.eng.free(p)
+        self.ptrs = []
+
+
+@pytest.fixture
+def dev(engine, queue):
+    d = Dev(engine, queue)
+    yield d
+    d.free()
+
+
+def gpu_stripes(dev, queue, stripes):
+    """stripes: list of dict(chunks=[np arrays or None], out_len, window, pads) -> list of outputs."""
+    descs, sources, outs = [], [], []
+    for st in stripes:
+        pads = st.get("pads") or [0] * len(st["chunks"])
+        first = len(sources)
+        for c, pad in zip(st["chunks"], pads):
+            if c is None or len(c) == 0:
+                sources.append((0, 0))
+            else:
+                sources.append((dev.put(c, pad), len(c)))
+        dptr = dev.alloc(st["out_len"] + 32) + st.get("dst_pad", 0)
+        outs.append((dptr, st["out_len"]))
+        descs.append((dptr, st["out_len"], first, len(st["chunks"]), st.get("window", 0)))
+    queue.xor_stripes(descs, sources)
+    queue.sync()
+    return [dev.get(p, n) for p, n in outs]
+
+
+# --------------------------------------------------------------------------
+# drop-in xor_parity (task_processing.c:96-109)
+# --------------------------------------------------------------------------
+@pytest.mark.parametrize("n", [1, 2, 3, 5, 8, 13, 56])
+@pytest.mark.parametrize("nbytes", [1, 7, 8, 9, 15, 16, 17, 4095, 65536, 524288, 524289])
+def test_dropin_xor_parity(bcp, oracle, engine, n, nbytes):
+    rng = np.random.default_rng(n * 1000003 + nbytes)
+    data = rng.integers(0, 256, size=n * nbytes, dtype=np.uint8)
+    dst = np.full(nbytes, 0xA5, dtype=np.uint8)
+    bcp.xor_parity(dst, nbytes, data, n)
+    assert np.array_equal(dst, oracle.xor_parity(data, nbytes, n))
+
+
+def test_dropin_golden_edge_vectors(bcp, oracle, engine):
+    for fx in GOLD["edge"]:
+        if fx["kind"] != "xor_parity":
+            continue
+        data = oracle.kat1_data(fx["n"], fx["s"])
+        dst = np.empty(fx["s"], dtype=np.uint8)
+        bcp.xor_parity(dst, fx["s"], data, fx["n"])
+        assert hashlib.sha256(dst.tobytes()).hexdigest() == fx["sha256"], fx
+
+
+def test_dropin_kat1(bcp, oracle, engine):
+    k = GOLD["survey_kats"]["KAT-1"]
+    data = oracle.kat1_data(k["n"], k["s"])
+    dst = np.full(k["s"], 7, dtype=np.uint8)
+    bcp.xor_parity(dst, k["s"], data, k["n"])
+    assert hashlib.sha256(dst.tobytes()).hexdigest() == k["sha256"]
+
+
+def test_dropin_concurrent_lanes(bcp, oracle, engine):
+    """Twelve lane threads (gen/main.c:821) calling the drop-in at once."""
+    def lane(i):
+        rng = np.random.default_rng(i)
+        for it in range(5):
+            n, nb = int(rng.integers(2, 10)), int(rng.integers(1, 300000))
+            data = rng.integers(0, 256, size=n * nb, dtype=np.uint8)
+            dst = np.empty(nb, dtype=np.uint8)
+            bcp.xor_parity(dst, nb, data, n)
+            if not np.array_equal(dst, oracle.xor_parity(data, nb, n)):
+                return False
+        return True
+    with cf.ThreadPoolExecutor(12) as ex:
+        assert all(ex.map(lane, range(12)))
+
+
+# --------------------------------------------------------------------------
+# uniform / strided fast path
+# --------------------------------------------------------------------------
+@pytest.mark.parametrize("nsrc", [1, 2, 3, 7, 8, 9, 13, 16, 17, 56])
+@pytest.mark.parametrize("chunk", [16, 4096, 8192 + 16, 524288, 524289, 1000])
+def test_uniform_vs_oracle(oracle, dev, queue, nsrc, chunk):
+    nstripes = 3
+    rng = np.random.default_rng(nsrc * 7 + chunk)
+    data = rng.integers(0, 256, size=nstripes * nsrc * chunk, dtype=np.uint8)
+    src = dev.put(data)
+    dst = dev.alloc(nstripes * chunk)
+    queue.xor_uniform(dst, src, nstripes, nsrc, chunk)
+    out = dev.get(dst, nstripes * chunk)
+    for s in range(nstripes):
+        ref = oracle.xor_parity(data[s * nsrc * chunk:(s + 1) * nsrc * chunk], chunk, nsrc)
+        assert np.array_equal(out[s * chunk:(s + 1) * chunk], ref), (s, nsrc, chunk)
+
+
+def test_strided_layout(oracle, dev, queue):
+    """Sources interleaved [k][s] instead of [s][k]; outputs at a padded pitch."""
+    nstripes, nsrc, chunk = 5, 8, 65536
+    rng = np.random.default_rng(11)
+    data = rng.integers(0, 256, size=nsrc * nstripes * chunk, dtype=np.uint8)  # [k][s][chunk]
+    src = dev.put(data)
+    pitch = chunk + 4096
+    dst = dev.alloc(nstripes * pitch)
+    queue.xor_strided(dst, pitch, src, chunk, nstripes * chunk, nstripes, nsrc, chunk)
+    out = dev.get(dst, nstripes * pitch)
+    d = data.reshape(nsrc, nstripes, chunk)
+    for s in range(nstripes):
+        ref = np.bitwise_xor.reduce(d[:, s, :], axis=0)
+        assert np.array_equal(out[s * pitch:s * pitch + chunk], ref)
+
+
+@pytest.mark.parametrize("bpc,vecs", [(1, 1), (2, 4), (4, 2), (8, 1), (16, 4)])
+def test_tuning_variants_agree(oracle, engine, dev, queue, bpc, vecs):
+    nstripes, nsrc, chunk = 7, 8, 524288 + 4096
+    rng = np.random.default_rng(bpc * 10 + vecs)
+    data = rng.integers(0, 256, size=nstripes * nsrc * chunk, dtype=np.uint8)
+    src = dev.put(data)
+    dst = dev.alloc(nstripes * chunk)
+    engine.tune(bpc, vecs)
+    try:
+        queue.xor_uniform(dst, src, nstripes, nsrc, chunk)
+        out = dev.get(dst, nstripes * chunk)
+        # variable-length path with the same tuning
+        res = gpu_stripes(dev, queue, [dict(chunks=[data[:1000], data[5:70000], None], out_len=70000 - 5)])
+    finally:
+        engine.tune(0, 0)
+    ref = np.bitwise_xor.reduce(data.reshape(nstripes, nsrc, chunk), axis=1).reshape(-1)
+    assert np.array_equal(out, ref)
+    assert np.array_equal(res[0], oracle.xor_padded_np([data[:1000], data[5:70000]]))
+
+
+# --------------------------------------------------------------------------
+# descriptor path: variable lengths, padding, alignment, windows, rebuild
+# --------------------------------------------------------------------------
+@pytest.mark.parametrize("seed", range(8))
+def test_descriptor_mixed_lengths_and_alignment(oracle, dev, queue, seed):
+    rng = np.random.default_rng(100 + seed)
+    stripes, refs = [], []
+    for _ in range(int(rng.integers(1, 12))):
+        n = int(rng.integers(1, 10))
+        lens = [int(x) for x in rng.integers(0, 300000, size=n)]
+        chunks = [rng.integers(0, 256, size=L, dtype=np.uint8) for L in lens]
+        pads = [int(x) for x in rng.integers(0, 16, size=n)]
+        m = max(lens)
+        stripes.append(dict(chunks=chunks, out_len=m, pads=pads, dst_pad=int(rng.integers(0, 16))))
+        refs.append(np.frombuffer(oracle.gen_parity_file(chunks)[8 * n:], np.uint8))
+    outs = gpu_stripes(dev, queue, stripes)
+    for o, r in zip(outs, refs):
+        assert np.array_equal(o, r)
+
+
+def test_golden_gen_files_on_gpu(oracle, dev, queue):
+    for fx in GOLD["edge"]:
+        if fx["kind"] != "gen_file":
+            continue
+        lens, W = fx["lens"], fx.get("window", 0)
+        chunks = [oracle.synthetic(L, 1000 + k) for k, L in enumerate(lens)]
+        m = max(lens)
+        window = W if (W and m > W) else 0
+        out = gpu_stripes(dev, queue, [dict(chunks=chunks, out_len=m, window=window)])[0]
+        hdr = np.array(lens, dtype="<u8").tobytes()
+        assert hashlib.sha256(hdr + out.tobytes()).hexdigest() == fx["sha256"], fx
+
+
+def test_survey_kats_on_gpu(oracle, dev, queue):
+    for name in ("KAT-2", "KAT-3", "KAT-4"):
+        k = GOLD["survey_kats"][name]
+        chunks = [oracle.kat_chunk(i, L) for i, L in enumerate(k["lens"])]
+        m = max(k["lens"])
+        window = oracle.WINDOW if m > oracle.WINDOW else 0
+        out = gpu_stripes(dev, queue, [dict(chunks=chunks, out_len=m, window=window)])[0]
+        hdr = np.array(k["lens"], dtype="<u8").tobytes()
+        assert hashlib.sha256(hdr + out.tobytes()).hexdigest() == k["sha256"], name
+
+
+@pytest.mark.parametrize("lens", [[10485760, 26214405], [26214405, 1, 15 * MiB + 3], [21 * MiB, 0, 10 * MiB + 17]])
+def test_window_replay_random_data(oracle, dev, queue, lens):
+    rng = np.random.default_rng(sum(lens))
+    chunks = [rng.integers(0, 256, size=L, dtype=np.uint8) for L in lens]
+    ref = oracle.gen_parity_file(chunks)[8 * len(lens):]
+    out = gpu_stripes(dev, queue, [dict(chunks=chunks, out_len=max(lens), window=oracle.WINDOW)])[0]
+    assert out.tobytes() == ref
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_rebuild_truncates_to_victim(oracle, dev, queue, seed):
+    """Rebuild (task_processing.c:146-174,228-230): survivors + parity body,
+    output truncated to header[victim]; max_cs from the header."""
+    rng = np.random.default_rng(200 + seed)
+    n = int(rng.integers(2, 9))
+    lens = [int(x) for x in rng.integers(1, 600000, size=n)]
+    chunks = [rng.integers(0, 256, size=L, dtype=np.uint8) for L in lens]
+    pf = oracle.gen_parity_file(chunks)
+    v = int(rng.integers(0, n))
+    survivors = [c for i, c in enumerate(chunks) if i != v]
+    body = np.frombuffer(pf[8 * n:], np.uint8)
+    out = gpu_stripes(dev, queue, [dict(chunks=survivors + [body], out_len=lens[v])])[0]
+    assert out.tobytes() == chunks[v].tobytes()
+    assert out.tobytes() == oracle.rebuild_chunk(pf, survivors, v)
+
+
+def test_empty_and_degenerate_stripes(oracle, dev, queue):
+    a = np.arange(100, dtype=np.uint8)
+    outs = gpu_stripes(dev, queue, [
+        dict(chunks=[a], out_len=0),                 # nothing to write
+        dict(chunks=[None, None], out_len=64),       # unreadable sources -> zeros
+        dict(chunks=[a, a], out_len=100),            # cancels
+        dict(chunks=[a], out_len=37),                # truncated copy
+        dict(chunks=[], out_len=20),                 # no sources -> zeros
+    ])
+    assert outs[0].size == 0
+    assert not outs[1].any() and outs[1].size == 64
+    assert not outs[2].any()
+    assert np.array_equal(outs[3], a[:37])
+    assert not outs[4].any()
+
+
+def test_invalid_descriptors_rejected(bcp, dev, queue):
+    with pytest.raises(bcp.BcpError):
+        queue.xor_stripes([(dev.alloc(64), 64, 0, 3, 0)], [(dev.alloc(64), 64)])   # sources out of range
+    with pytest.raises(bcp.BcpError):
+        queue.xor_stripes([(dev.alloc(64), 64, 0, 1, 7)], [(dev.alloc(64), 64)])   # window % 16
+    with pytest.raises(bcp.BcpError):
+        queue.xor_stripes([(dev.alloc(64), 64, 0, 1, 0)], [(0, 64)])               # null source
+    queue.sync()
+
+
+# --------------------------------------------------------------------------
+# synthetic data / fold / compare utilities
+# --------------------------------------------------------------------------
+@pytest.mark.parametrize("n,off", [(1, 0), (17, 0), (4096, 8), (100003, 3), (1 << 20, 16)])
+def test_fill_synthetic_matches_oracle(oracle, dev, queue, n, off):
+    p = dev.alloc(n + 16)
+    queue.fill_synthetic(p, n, 77, off)
+    assert np.array_equal(dev.get(p, n), oracle.synthetic(n, 77, off))
+
+
+def test_fold_and_compare(dev, queue):
+    rng = np.random.default_rng(5)
+    a = rng.integers(0, 256, size=1000003, dtype=np.uint8)
+    b = a.copy()
+    b[[0, 17, 999999, 1000002]] ^= 0x5A
+    pa, pb = dev.put(a), dev.put(b)
+    res = dev.alloc(32)
+    queue.xor_fold(pa, a.size, res)
+    fold = dev.get(res, 16)
+    ref = np.zeros(16, np.uint8)
+    for i in range(16):
+        ref[i] = np.bitwise_xor.reduce(a[i::16])
+    assert np.array_equal(fold, ref)
+    queue.compare(pa, pb, a.size, res)
+    assert int(dev.get(res, 8).view("<u8")[0]) == 4
+
+
+# --------------------------------------------------------------------------
+# BASELINE sizes: config 2 (gen) and config 3 (rebuild), 12,500 stripes of
+# 8 x 512 KiB device-resident -- size-independent properties
+# --------------------------------------------------------------------------
+def test_config2_and_config3_full_size(oracle, dev, queue):
+    nstripes, nsrc, chunk = 12500, 8, 512 * KiB
+    total = nstripes * nsrc * chunk
+    src = dev.alloc(total)
+    par = dev.alloc(nstripes * chunk)
+    reb = dev.alloc(nstripes * chunk)
+    res = dev.alloc(64)
+    queue.fill_synthetic(src, total, 1)
+    queue.xor_uniform(par, src, nstripes, nsrc, chunk)
+    # (1) XOR-fold conservation: fold(parity) == fold(all sources)
+    queue.xor_fold(par, nstripes * chunk, res)
+    queue.xor_fold(src, total, res + 16)
+    f = dev.get(res, 32)
+    assert np.array_equal(f[:16], f[16:]) and f[:16].any()
+    # (2) sampled stripes against the oracle
+    rng = np.random.default_rng(2)
+    for s in [0, nstripes - 1] + [int(x) for x in rng.integers(0, nstripes, size=6)]:
+        data = dev.get(src + s * nsrc * chunk, nsrc * chunk)
+        assert np.array_equal(data, oracle.synthetic(nsrc * chunk, 1, s * nsrc * chunk))
+        assert np.array_equal(dev.get(par + s * chunk, chunk), oracle.xor_parity(data, chunk, nsrc))
+    # (3) config 3: rebuild target 3 of every stripe from 7 survivors + parity
+    victim = 3
+    stripes, sources = [], []
+    for s in range(nstripes):
+        first = len(sources)
+        for k in range(nsrc):
+            if k != victim:
+                sources.append((src + (s * nsrc + k) * chunk, chunk))
+        sources.append((par + s * chunk, chunk))
+        stripes.append((reb + s * chunk, chunk, first, nsrc, 0))
+    queue.xor_stripes(stripes, sources)
+    # gather the original victims with a 1-source strided XOR (a copy), then
+    # compare all 6.1 GiB on the device
+    gathered = dev.alloc(nstripes * chunk)
+    queue.xor_strided(gathered, chunk, src + victim * chunk, nsrc * chunk, chunk, nstripes, 1, chunk)
+    queue.compare(reb, gathered, nstripes * chunk, res)
+    bad = int(dev.get(res, 8).view("<u8")[0])
+    assert bad == 0
