@@ -74,6 +74,7 @@ _SIGS = {
     "bcp_queue_mark": ([_V, ctypes.c_int], ctypes.c_int),
     "bcp_queue_elapsed_ms": ([_V, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_float)], ctypes.c_int),
     "bcp_set_tuning": ([_V, ctypes.c_int, ctypes.c_int], ctypes.c_int),
+    "bcp_set_option": ([_V, ctypes.c_char_p, ctypes.c_int], ctypes.c_int),
 }
 
 
@@ -131,6 +132,9 @@ class Engine:
 
     def tune(self, blocks_per_cu: int = 0, vecs_per_thread: int = 0):
         call("bcp_set_tuning", self.h, blocks_per_cu, vecs_per_thread)
+
+    def option(self, key: str, value: int):
+        call("bcp_set_option", self.h, key.encode(), value)
 
     def queue(self) -> "Queue":
         return Queue(self)

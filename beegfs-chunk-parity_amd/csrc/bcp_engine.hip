@@ -31,7 +31,7 @@ struct bcp_engine {
 namespace {
 
 constexpr int kRingSlots = 4;
-constexpr int kTimerSlots = 8;
+constexpr int kTimerSlots = 64;
 
 struct DescSlot {
   void *host = nullptr;   // pinned staging
@@ -158,9 +158,11 @@ extern "C" int bcp_engine_create(int device, bcp_engine **out) {
   snprintf(e->name, sizeof(e->name), "%s (%s)", prop.name, prop.gcnArchName);
   if (const char *v = getenv("BCP_BLOCKS_PER_CU")) e->tuning.blocks_per_cu = atoi(v);
   if (const char *v = getenv("BCP_VECS_PER_THREAD")) e->tuning.vecs_per_thread = atoi(v);
-  if (e->tuning.blocks_per_cu < 1 || e->tuning.blocks_per_cu > 32) e->tuning.blocks_per_cu = 8;
+  const Tuning defaults;
+  if (e->tuning.blocks_per_cu < 1 || e->tuning.blocks_per_cu > 32) e->tuning.blocks_per_cu = defaults.blocks_per_cu;
   if (e->tuning.vecs_per_thread != 1 && e->tuning.vecs_per_thread != 2 && e->tuning.vecs_per_thread != 4)
-    e->tuning.vecs_per_thread = 2;
+    e->tuning.vecs_per_thread = defaults.vecs_per_thread;
+  if (const char *v = getenv("BCP_POLICY")) e->tuning.policy = atoi(v) & 7;
   *out = e;
   return 0;
 }
@@ -178,13 +180,26 @@ extern "C" int bcp_engine_info(bcp_engine *eng, int *num_cus, char *name, size_t
   return 0;
 }
 
+extern "C" int bcp_set_option(bcp_engine *eng, const char *key, int value) {
+  if (!eng || !key) return -EINVAL;
+  int rc = 0;
+  pthread_mutex_lock(&eng->lock);
+  if (!strcmp(key, "blocks_per_cu") && value >= 1 && value <= 32) eng->tuning.blocks_per_cu = value;
+  else if (!strcmp(key, "vecs_per_thread") && (value == 1 || value == 2 || value == 4)) eng->tuning.vecs_per_thread = value;
+  else if (!strcmp(key, "policy") && value >= 0 && value <= 7) eng->tuning.policy = value;
+  else rc = -EINVAL;
+  pthread_mutex_unlock(&eng->lock);
+  return rc;
+}
+
 extern "C" int bcp_set_tuning(bcp_engine *eng, int blocks_per_cu, int vecs_per_thread) {
   if (!eng) return -EINVAL;
   if (blocks_per_cu < 0 || blocks_per_cu > 32) return -EINVAL;
   if (vecs_per_thread != 0 && vecs_per_thread != 1 && vecs_per_thread != 2 && vecs_per_thread != 4) return -EINVAL;
+  const Tuning defaults;
   pthread_mutex_lock(&eng->lock);
-  eng->tuning.blocks_per_cu = blocks_per_cu ? blocks_per_cu : 8;
-  eng->tuning.vecs_per_thread = vecs_per_thread ? vecs_per_thread : 2;
+  eng->tuning.blocks_per_cu = blocks_per_cu ? blocks_per_cu : defaults.blocks_per_cu;
+  eng->tuning.vecs_per_thread = vecs_per_thread ? vecs_per_thread : defaults.vecs_per_thread;
   pthread_mutex_unlock(&eng->lock);
   return 0;
 }
@@ -451,7 +466,7 @@ extern "C" int bcp_xor_strided_async(bcp_queue *q, void *dst, uint64_t dst_strid
                     aligned16(stripe_stride) && aligned16(src_stride) && aligned16(chunk_bytes) &&
                     chunk_bytes / 16 <= 0xFFFFFFFFull;
   if (fast) {
-    HIP_RC(launch_xor_strided_fast(q->stream, grid_for(e), e->tuning.vecs_per_thread, (char *)dst, dst_stride,
+    HIP_RC(launch_xor_strided_fast(q->stream, grid_for(e), e->tuning.vecs_per_thread, e->tuning.policy, (char *)dst, dst_stride,
                                    (const char *)src, stripe_stride, src_stride, nstripes, nsrc, chunk_bytes));
     return 0;
   }

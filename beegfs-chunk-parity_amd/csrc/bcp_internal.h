@@ -13,9 +13,18 @@ namespace bcp {
 constexpr int kBlock = 256;        // threads per workgroup (4 waves of 64)
 constexpr int kMaxVecsPerThread = 4;
 
+// Fast-path policy bits (8-wide stripes only; other widths use 0).
+constexpr int kPolPlainLoad = 1;   // default-policy loads instead of non-temporal
+constexpr int kPolPlainStore = 2;  // default-policy stores instead of non-temporal
+constexpr int kPolContig = 4;      // contiguous tile range per workgroup instead of grid-stride
+
+// Defaults from the r01 interleaved sweep on MI355X (profiles/r01/sweep_fast.jsonl):
+// 16 x 256-thread workgroups per CU (8 resident, the rest queue behind them),
+// 4 vectors per lane, contiguous tile runs, non-temporal loads and stores.
 struct Tuning {
-    int blocks_per_cu = 8;      // resident 256-thread workgroups per CU
-    int vecs_per_thread = 2;    // 16-byte vectors per lane per tile
+    int blocks_per_cu = 16;     // 256-thread workgroups launched per CU
+    int vecs_per_thread = 4;    // 16-byte vectors per lane per tile
+    int policy = kPolContig;    // kPol* bits for the 8-wide fast path
 };
 
 // Device-side form of one stripe descriptor batch.
@@ -29,7 +38,7 @@ struct DescBatch {
 };
 
 // Kernel launchers (bcp_kernels.hip).  All return hipError_t.
-hipError_t launch_xor_strided_fast(hipStream_t st, int grid, int vecs,
+hipError_t launch_xor_strided_fast(hipStream_t st, int grid, int vecs, int pol,
                                    char *dst, uint64_t dst_stride,
                                    const char *src, uint64_t stripe_stride,
                                    uint64_t src_stride, uint64_t nstripes,

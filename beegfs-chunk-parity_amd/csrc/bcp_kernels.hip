@@ -21,64 +21,89 @@ typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 typedef v4u v4u_u __attribute__((aligned(1)));  // unaligned 16-byte view
 
 __device__ __forceinline__ v4u ld_nt(const v4u *p) { return __builtin_nontemporal_load(p); }
-__device__ __forceinline__ void st_nt(v4u *p, v4u v) { __builtin_nontemporal_store(v, p); }
 __device__ __forceinline__ v4u zero4() { return v4u{0u, 0u, 0u, 0u}; }
 
 // ---------------------------------------------------------------------------
 // Fast path.  Stripe s, source k starts at src + s*stripe_stride + k*src_stride
 // and holds vps 16-byte vectors; output s at dst + s*dst_stride.  A tile is
-// kBlock*U vectors of one stripe; workgroups walk tiles grid-stride.  Lane l of
-// a tile owns vectors l, l+256, ... so each wave-instruction moves 1 KiB
-// contiguous per source.  NSRC == 0 means "runtime nsrc".
+// kBlock*U vectors of one stripe.  Lane l of a tile owns vectors l, l+256, ...
+// so each wave-instruction moves 1 KiB contiguous per source, and all
+// NSRC*U loads of a lane are issued before its XORs.  NSRC == 0 means
+// "runtime nsrc".  POL selects the cache policy and the tile schedule
+// (kPolPlainLoad / kPolPlainStore / kPolContig bits, see bcp_internal.h).
 // ---------------------------------------------------------------------------
-template <int NSRC, int U>
+template <int POL>
+__device__ __forceinline__ v4u ld_pol(const v4u *p) {
+  if constexpr (POL & kPolPlainLoad) return *p;
+  else return __builtin_nontemporal_load(p);
+}
+template <int POL>
+__device__ __forceinline__ void st_pol(v4u *p, v4u v) {
+  if constexpr (POL & kPolPlainStore) *p = v;
+  else __builtin_nontemporal_store(v, p);
+}
+
+template <int NSRC, int U, int POL>
+__device__ __forceinline__ void fast_tile(char *__restrict__ dst, uint64_t dst_stride, const char *__restrict__ src,
+                                          uint64_t stripe_stride, uint64_t src_stride, uint32_t vps, uint32_t tps,
+                                          uint32_t nsrc, uint32_t t) {
+  constexpr uint32_t tile_v = kBlock * U;
+  const uint32_t s = t / tps;
+  const uint32_t tin = t - s * tps;
+  const char *sb = src + (uint64_t)s * stripe_stride;
+  v4u *db = reinterpret_cast<v4u *>(dst + (uint64_t)s * dst_stride);
+  const uint32_t v0 = tin * tile_v + threadIdx.x;
+  v4u acc[U];
+  if (tin * tile_v + tile_v <= vps) {
+    const v4u *p0 = reinterpret_cast<const v4u *>(sb) + v0;
+#pragma unroll
+    for (int u = 0; u < U; u++) acc[u] = ld_pol<POL>(p0 + u * kBlock);
+    if constexpr (NSRC > 0) {
+#pragma unroll
+      for (int k = 1; k < NSRC; k++) {
+        const v4u *pk = reinterpret_cast<const v4u *>(sb + k * src_stride) + v0;
+#pragma unroll
+        for (int u = 0; u < U; u++) acc[u] ^= ld_pol<POL>(pk + u * kBlock);
+      }
+    } else {
+#pragma unroll 4
+      for (uint32_t k = 1; k < nsrc; k++) {
+        const v4u *pk = reinterpret_cast<const v4u *>(sb + k * src_stride) + v0;
+#pragma unroll
+        for (int u = 0; u < U; u++) acc[u] ^= ld_pol<POL>(pk + u * kBlock);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) st_pol<POL>(db + v0 + u * kBlock, acc[u]);
+  } else {
+    // Last, partial tile of a stripe: per-vector bounds.
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint32_t v = v0 + u * kBlock;
+      if (v < vps) {
+        v4u a = ld_pol<POL>(reinterpret_cast<const v4u *>(sb) + v);
+        for (uint32_t k = 1; k < nsrc; k++) a ^= ld_pol<POL>(reinterpret_cast<const v4u *>(sb + k * src_stride) + v);
+        st_pol<POL>(db + v, a);
+      }
+    }
+  }
+}
+
+template <int NSRC, int U, int POL>
 __global__ __launch_bounds__(kBlock) void xor_strided_fast(
     char *__restrict__ dst, uint64_t dst_stride, const char *__restrict__ src,
     uint64_t stripe_stride, uint64_t src_stride, uint32_t vps, uint32_t tps,
     uint32_t ntiles, uint32_t nsrc_rt) {
-  constexpr uint32_t tile_v = kBlock * U;
   const uint32_t nsrc = NSRC > 0 ? (uint32_t)NSRC : nsrc_rt;
-  for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
-    const uint32_t s = t / tps;
-    const uint32_t tin = t - s * tps;
-    const char *sb = src + (uint64_t)s * stripe_stride;
-    v4u *db = reinterpret_cast<v4u *>(dst + (uint64_t)s * dst_stride);
-    const uint32_t v0 = tin * tile_v + threadIdx.x;
-    v4u acc[U];
-    if (tin * tile_v + tile_v <= vps) {
-      const v4u *p0 = reinterpret_cast<const v4u *>(sb) + v0;
-#pragma unroll
-      for (int u = 0; u < U; u++) acc[u] = ld_nt(p0 + u * kBlock);
-      if constexpr (NSRC > 0) {
-#pragma unroll
-        for (int k = 1; k < NSRC; k++) {
-          const v4u *pk = reinterpret_cast<const v4u *>(sb + k * src_stride) + v0;
-#pragma unroll
-          for (int u = 0; u < U; u++) acc[u] ^= ld_nt(pk + u * kBlock);
-        }
-      } else {
-#pragma unroll 4
-        for (uint32_t k = 1; k < nsrc; k++) {
-          const v4u *pk = reinterpret_cast<const v4u *>(sb + k * src_stride) + v0;
-#pragma unroll
-          for (int u = 0; u < U; u++) acc[u] ^= ld_nt(pk + u * kBlock);
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < U; u++) st_nt(db + v0 + u * kBlock, acc[u]);
-    } else {
-      // Last, partial tile of a stripe: per-vector bounds.
-#pragma unroll
-      for (int u = 0; u < U; u++) {
-        const uint32_t v = v0 + u * kBlock;
-        if (v < vps) {
-          v4u a = ld_nt(reinterpret_cast<const v4u *>(sb) + v);
-          for (uint32_t k = 1; k < nsrc; k++)
-            a ^= ld_nt(reinterpret_cast<const v4u *>(sb + k * src_stride) + v);
-          st_nt(db + v, a);
-        }
-      }
-    }
+  if constexpr (POL & kPolContig) {
+    // Workgroup b owns tiles [b*T/G, (b+1)*T/G): one contiguous run each.
+    const uint32_t t0 = (uint32_t)(((uint64_t)blockIdx.x * ntiles) / gridDim.x);
+    const uint32_t t1 = (uint32_t)(((uint64_t)(blockIdx.x + 1) * ntiles) / gridDim.x);
+    for (uint32_t t = t0; t < t1; t++)
+      fast_tile<NSRC, U, POL>(dst, dst_stride, src, stripe_stride, src_stride, vps, tps, nsrc, t);
+  } else {
+    for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x)
+      fast_tile<NSRC, U, POL>(dst, dst_stride, src, stripe_stride, src_stride, vps, tps, nsrc, t);
   }
 }
 
@@ -311,32 +336,48 @@ __global__ __launch_bounds__(kBlock) void compare_bytes(const unsigned char *a, 
 // ---------------------------------------------------------------------------
 // Launchers.
 // ---------------------------------------------------------------------------
-template <int NSRC, int U>
+template <int NSRC, int U, int POL>
 static hipError_t launch_fast_nu(hipStream_t st, int grid, char *dst, uint64_t dst_stride, const char *src,
                                  uint64_t stripe_stride, uint64_t src_stride, uint32_t vps, uint32_t tps,
                                  uint32_t ntiles, uint32_t nsrc) {
-  hipLaunchKernelGGL((xor_strided_fast<NSRC, U>), dim3(grid), dim3(kBlock), 0, st, dst, dst_stride, src,
+  hipLaunchKernelGGL((xor_strided_fast<NSRC, U, POL>), dim3(grid), dim3(kBlock), 0, st, dst, dst_stride, src,
                      stripe_stride, src_stride, vps, tps, ntiles, nsrc);
   return hipGetLastError();
 }
 
+// The hot 8-wide stripe gets every policy variant; other widths use the
+// default policy (non-temporal loads and stores, grid-stride tiles).
 template <int U>
-static hipError_t launch_fast_u(hipStream_t st, int grid, char *dst, uint64_t dst_stride, const char *src,
+static hipError_t launch_fast_u(hipStream_t st, int grid, int pol, char *dst, uint64_t dst_stride, const char *src,
                                 uint64_t stripe_stride, uint64_t src_stride, uint32_t vps, uint32_t tps,
                                 uint32_t ntiles, uint32_t nsrc) {
+#define BCP_ARGS st, grid, dst, dst_stride, src, stripe_stride, src_stride, vps, tps, ntiles, nsrc
 #define BCP_NSRC_CASE(n) \
-  case n: return launch_fast_nu<n, U>(st, grid, dst, dst_stride, src, stripe_stride, src_stride, vps, tps, ntiles, nsrc);
+  case n: return launch_fast_nu<n, U, 0>(BCP_ARGS);
+  if (nsrc == 8) {
+    switch (pol & 7) {
+      case 1: return launch_fast_nu<8, U, 1>(BCP_ARGS);
+      case 2: return launch_fast_nu<8, U, 2>(BCP_ARGS);
+      case 3: return launch_fast_nu<8, U, 3>(BCP_ARGS);
+      case 4: return launch_fast_nu<8, U, 4>(BCP_ARGS);
+      case 5: return launch_fast_nu<8, U, 5>(BCP_ARGS);
+      case 6: return launch_fast_nu<8, U, 6>(BCP_ARGS);
+      case 7: return launch_fast_nu<8, U, 7>(BCP_ARGS);
+      default: return launch_fast_nu<8, U, 0>(BCP_ARGS);
+    }
+  }
   switch (nsrc) {
     BCP_NSRC_CASE(1) BCP_NSRC_CASE(2) BCP_NSRC_CASE(3) BCP_NSRC_CASE(4) BCP_NSRC_CASE(5)
-    BCP_NSRC_CASE(6) BCP_NSRC_CASE(7) BCP_NSRC_CASE(8) BCP_NSRC_CASE(9) BCP_NSRC_CASE(10)
+    BCP_NSRC_CASE(6) BCP_NSRC_CASE(7) BCP_NSRC_CASE(9) BCP_NSRC_CASE(10)
     BCP_NSRC_CASE(11) BCP_NSRC_CASE(12) BCP_NSRC_CASE(16)
     default:
-      return launch_fast_nu<0, U>(st, grid, dst, dst_stride, src, stripe_stride, src_stride, vps, tps, ntiles, nsrc);
+      return launch_fast_nu<0, U, 0>(BCP_ARGS);
   }
 #undef BCP_NSRC_CASE
+#undef BCP_ARGS
 }
 
-hipError_t launch_xor_strided_fast(hipStream_t st, int grid, int vecs, char *dst, uint64_t dst_stride,
+hipError_t launch_xor_strided_fast(hipStream_t st, int grid, int vecs, int pol, char *dst, uint64_t dst_stride,
                                    const char *src, uint64_t stripe_stride, uint64_t src_stride,
                                    uint64_t nstripes, uint32_t nsrc, uint64_t chunk_bytes) {
   const uint32_t vps = (uint32_t)(chunk_bytes / 16);
@@ -347,9 +388,9 @@ hipError_t launch_xor_strided_fast(hipStream_t st, int grid, int vecs, char *dst
   if (ntiles > 0x7FFFFFFFull) return hipErrorInvalidValue;
   if ((uint64_t)grid > ntiles) grid = (int)ntiles;
   switch (vecs) {
-    case 1: return launch_fast_u<1>(st, grid, dst, dst_stride, src, stripe_stride, src_stride, vps, tps, (uint32_t)ntiles, nsrc);
-    case 4: return launch_fast_u<4>(st, grid, dst, dst_stride, src, stripe_stride, src_stride, vps, tps, (uint32_t)ntiles, nsrc);
-    default: return launch_fast_u<2>(st, grid, dst, dst_stride, src, stripe_stride, src_stride, vps, tps, (uint32_t)ntiles, nsrc);
+    case 1: return launch_fast_u<1>(st, grid, pol, dst, dst_stride, src, stripe_stride, src_stride, vps, tps, (uint32_t)ntiles, nsrc);
+    case 4: return launch_fast_u<4>(st, grid, pol, dst, dst_stride, src, stripe_stride, src_stride, vps, tps, (uint32_t)ntiles, nsrc);
+    default: return launch_fast_u<2>(st, grid, pol, dst, dst_stride, src, stripe_stride, src_stride, vps, tps, (uint32_t)ntiles, nsrc);
   }
 }
 

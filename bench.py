@@ -95,15 +95,16 @@ class Dist:
             self.pg.destroy_process_group()
 
 
-def pmc_traffic(workload_key: str):
+def pmc_traffic(workload_key: str, kernel_tag: str):
     """Per-launch HBM bytes from the committed PMC summary, if it matches."""
     best = None
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "**", "*pmc*.json"), recursive=True)):
         try:
             doc = json.load(open(path))
         except (OSError, ValueError):
             continue
-        if doc.get("workload_key") == workload_key and doc.get("hbm_bytes_per_launch"):
+        if (doc.get("workload_key") == workload_key and doc.get("hbm_bytes_per_launch")
+                and kernel_tag in doc.get("kernel", "")):
             best = doc
     return best
 
@@ -126,7 +127,8 @@ def main():
         def step():
             q.xor_uniform(out, src, S, N, C)
         bytes_per_step = S * (N + 1) * C
-        kernel = f"xor_strided_fast<{N},U>"
+        kernel = f"xor_strided_fast<{N},U,POL>"
+        kernel_tag = "xor_strided_fast<"
         workload = f"config2: parity gen, {S} stripes x {N} x {C // KiB} KiB device-resident"
     else:
         # config 3: parity first, then rebuild source index 3 from the other
@@ -151,6 +153,7 @@ def main():
             bcp.check("bcp_xor_stripes_async", L.bcp_xor_stripes_async(q.h, st, len(stripes), so, len(sources)))
         bytes_per_step = S * (N + 1) * C
         kernel = "xor_desc<U>"
+        kernel_tag = "xor_desc<"
         workload = f"config3: rebuild, {S} stripes x ({N - 1} survivors + parity) x {C // KiB} KiB device-resident"
 
     for _ in range(a.warmup):
@@ -210,7 +213,7 @@ def main():
         value = total_bytes / wall_max / GiB
         achieved = bytes_per_step / (kern_ms_max * 1e-3) / 1e9
         wkey = f"{a.mode}:{S}x{N}x{C}"
-        pmc = pmc_traffic(wkey)
+        pmc = pmc_traffic(wkey, kernel_tag)
         line = {
             "metric": METRIC,
             "value": round(value, 2),

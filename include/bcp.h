@@ -159,12 +159,18 @@ int bcp_dev_compare_async(bcp_queue *q, const void *a, const void *b,
                           uint64_t bytes, void *out_dev);
 
 /* ---- timing (HIP events on the queue's stream) ------------------------- */
-int bcp_queue_mark(bcp_queue *q, int slot);           /* slot 0..7 */
+int bcp_queue_mark(bcp_queue *q, int slot);           /* slot 0..63 */
 int bcp_queue_elapsed_ms(bcp_queue *q, int slot_from, int slot_to,
                          float *ms);
 
 /* Tuning knobs for the fast path (bench / autotune only; 0 = default). */
 int bcp_set_tuning(bcp_engine *eng, int blocks_per_cu, int vecs_per_thread);
+/* Named knob: "blocks_per_cu" (1..32), "vecs_per_thread" (1,2,4),
+ * "policy" (bits: 1 default-policy loads, 2 default-policy stores,
+ * 4 contiguous tile ranges; 8-wide stripes only). */
+int bcp_set_option(bcp_engine *eng, const char *key, int value);
+/* Timer slots for bcp_queue_mark / bcp_queue_elapsed_ms. */
+#define BCP_TIMER_SLOTS 64
 
 #ifdef __cplusplus
 }

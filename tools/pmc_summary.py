@@ -1,0 +1,64 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 PMC passes (FETCH_SIZE and WRITE_SIZE, collected in
+separate runs) into HBM bytes per launch of one kernel.
+
+gfx950 corrections (MI355X_MICROARCH.md §HBM): FETCH_SIZE reads exactly half
+the bytes of a wide coalesced 16-B-per-lane stream, so it is doubled;
+WRITE_SIZE is exact for 16-B streaming stores.  Both are in KiB.
+
+    python tools/pmc_summary.py --fetch DIR/run_counter_collection.csv \
+        --write DIR2/run_counter_collection.csv --kernel xor_strided_fast \
+        --workload-key gen:12500x8x524288 --algorithmic 58982400000 --out profiles/r01_pmc_gen.json
+"""
+import argparse
+import csv
+import json
+import statistics
+
+
+def per_dispatch(path, counter, kernel):
+    vals = {}
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            if row["Counter_Name"] != counter or kernel not in row["Kernel_Name"]:
+                continue
+            vals[row["Dispatch_Id"]] = (float(row["Counter_Value"]), row["Kernel_Name"],
+                                        int(row["End_Timestamp"]) - int(row["Start_Timestamp"]))
+    return vals
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--fetch", required=True)
+    ap.add_argument("--write", required=True)
+    ap.add_argument("--kernel", required=True)
+    ap.add_argument("--workload-key", required=True)
+    ap.add_argument("--algorithmic", type=float, required=True, help="algorithmic bytes per launch")
+    ap.add_argument("--out", required=True)
+    a = ap.parse_args()
+    fe = per_dispatch(a.fetch, "FETCH_SIZE", a.kernel)
+    wr = per_dispatch(a.write, "WRITE_SIZE", a.kernel)
+    assert fe and wr, "no matching dispatches"
+    fetch_b = statistics.median(v[0] for v in fe.values()) * 1024 * 2
+    write_b = statistics.median(v[0] for v in wr.values()) * 1024
+    doc = {
+        "workload_key": a.workload_key,
+        "kernel": next(iter(fe.values()))[1],
+        "dispatches": {"fetch_pass": len(fe), "write_pass": len(wr)},
+        "fetch_bytes_per_launch": round(fetch_b),
+        "write_bytes_per_launch": round(write_b),
+        "hbm_bytes_per_launch": round(fetch_b + write_b),
+        "algorithmic_bytes_per_launch": round(a.algorithmic),
+        "traffic_over_algorithmic": round((fetch_b + write_b) / a.algorithmic, 5),
+        "profiled_kernel_ns_median": statistics.median(v[2] for v in fe.values()),
+        "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes); FETCH_SIZE x2 (gfx950 "
+                  "wide-read correction), WRITE_SIZE x1; KiB->B x1024",
+    }
+    with open(a.out, "w") as f:
+        json.dump(doc, f, indent=1)
+        f.write("\n")
+    print(json.dumps(doc))
+
+
+if __name__ == "__main__":
+    main()
