@@ -32,6 +32,35 @@ class Stripe(ctypes.Structure):
                 ("nsrc", ctypes.c_uint32), ("window", ctypes.c_uint64)]
 
 
+class FileInfo(ctypes.Structure):
+    _fields_ = [("timestamp", ctypes.c_int64), ("locations", ctypes.c_uint64)]
+
+
+class WorkItem(ctypes.Structure):
+    _fields_ = [("path", ctypes.c_char_p), ("fi", FileInfo)]
+
+
+class RunStats(ctypes.Structure):
+    _fields_ = [("seconds", ctypes.c_double), ("tasks", ctypes.c_uint64), ("bytes_read", ctypes.c_uint64),
+                ("bytes_written", ctypes.c_uint64), ("errors", ctypes.c_int)]
+
+
+XOR_HOOK = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t,
+                            ctypes.c_int, ctypes.c_void_p)
+
+L_MASK = (1 << 56) - 1
+NO_P = 0xFF
+
+
+def with_p(locations: int, p: int) -> int:
+    """WITH_P (common.h:22)."""
+    return (locations & L_MASK) | ((p & 0xFF) << 56)
+
+
+def get_p(locations: int) -> int:
+    return locations >> 56
+
+
 _lib = None
 
 _V = ctypes.c_void_p
@@ -75,6 +104,16 @@ _SIGS = {
     "bcp_queue_elapsed_ms": ([_V, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_float)], ctypes.c_int),
     "bcp_set_tuning": ([_V, ctypes.c_int, ctypes.c_int], ctypes.c_int),
     "bcp_set_option": ([_V, ctypes.c_char_p, ctypes.c_int], ctypes.c_int),
+    "bcp_task_set_device_map": ([ctypes.POINTER(ctypes.c_int), ctypes.c_int], ctypes.c_int),
+    "bcp_task_shutdown": ([], ctypes.c_int),
+    "bcp_task_set_xor_hook": ([_V, _V], None),
+    "bcp_assign_lanes": ([ctypes.c_int, ctypes.c_uint64, ctypes.POINTER(FileInfo), ctypes.POINTER(ctypes.c_int)], None),
+    "bcp_gen_run": ([ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(WorkItem), ctypes.c_size_t, ctypes.c_int,
+                     ctypes.POINTER(ctypes.c_int), _V, ctypes.POINTER(RunStats)], ctypes.c_int),
+    "bcp_rebuild_run": ([ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.POINTER(WorkItem), ctypes.c_size_t,
+                         ctypes.c_char_p, _V, ctypes.POINTER(RunStats)], ctypes.c_int),
+    "bcp_lb_init": ([ctypes.c_int], ctypes.c_int),
+    "bcp_lb_finalize": ([], ctypes.c_int),
 }
 
 
@@ -260,3 +299,60 @@ def _host_addr(host, nbytes):
 def xor_parity(dst, nbytes: int, data, nsources: int):
     """Drop-in for task_processing.c:96-109 on numpy buffers (GPU)."""
     call("bcp_xor_parity", _V(dst.ctypes.data), nbytes, _V(data.ctypes.data), nsources)
+
+
+# ---------------------------------------------------------------------------
+# host layer: loopback gen / rebuild drivers (include/bcp_task.h)
+# ---------------------------------------------------------------------------
+def _items(items):
+    """items: list of (path, timestamp, locations)."""
+    arr = (WorkItem * max(len(items), 1))()
+    keep = []
+    for i, (path, ts, loc) in enumerate(items):
+        b = path.encode() if isinstance(path, str) else path
+        keep.append(b)
+        arr[i].path = b
+        arr[i].fi.timestamp = ts
+        arr[i].fi.locations = loc
+    return arr, keep
+
+
+def assign_lanes(nlanes: int, locations) -> list:
+    n = len(locations)
+    fis = (FileInfo * max(n, 1))(*[FileInfo(0, loc) for loc in locations])
+    out = (ctypes.c_int * max(n, 1))()
+    lib().bcp_assign_lanes(nlanes, n, fis, out)
+    return list(out)[:n]
+
+
+def gen_run(store_root: str, ntargets: int, items, nlanes: int = 12, lanes=None, log=None) -> RunStats:
+    """Parity generation over loopback ranks (bcp_gen_run).  log: a C FILE* or None."""
+    arr, keep = _items(items)
+    st = RunStats()
+    ln = None
+    if lanes is not None:
+        ln = (ctypes.c_int * max(len(lanes), 1))(*lanes)
+    rc = lib().bcp_gen_run(store_root.encode(), ntargets, arr, len(items), nlanes, ln, log, ctypes.byref(st))
+    check("bcp_gen_run", rc)
+    del keep
+    return st
+
+
+def rebuild_run(store_root: str, ntargets: int, rebuild_target: int, items, corrupt_list: str | None = None,
+                log=None) -> RunStats:
+    arr, keep = _items(items)
+    st = RunStats()
+    rc = lib().bcp_rebuild_run(store_root.encode(), ntargets, rebuild_target, arr, len(items),
+                               corrupt_list.encode() if corrupt_list else None, log, ctypes.byref(st))
+    check("bcp_rebuild_run", rc)
+    del keep
+    return st
+
+
+def set_xor_hook(fn_addr: int | None, ctx: int | None = None):
+    """Test injection point: route the P role's fold to a C function (address)."""
+    lib().bcp_task_set_xor_hook(_V(fn_addr) if fn_addr else None, _V(ctx) if ctx else None)
+
+
+def task_shutdown():
+    call("bcp_task_shutdown")

@@ -1,0 +1,388 @@
+/*
+ * bcp_runner.c -- the callers of process_task, as loopback ranks.
+ *
+ *   bcp_assign_lanes  gen/assign_lanes.c:12-46
+ *   bcp_gen_run       gen/main.c:116-164 (process_list) + the lane launch at
+ *                     :821-889 and the per-rank HostState setup at :723-743
+ *   bcp_rebuild_run   rebuild/main.c:40-89 (do_file) + setup at :200-225
+ *
+ * Every storage target k is loopback rank k+1 (rank 0 is the coordinator,
+ * idle here as in the reference's phase 2), with its store at
+ * <root>/st<k>/{chunks,parity}.  The worklist is shared memory instead of an
+ * MPI_Bcast (gen/main.c:794-797); every rank still walks it in the same order,
+ * which is what keeps the per-(pair, tag) message order consistent.
+ */
+#define _GNU_SOURCE
+#include <errno.h>
+#include <fcntl.h>
+#include <pthread.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/stat.h>
+#include <time.h>
+#include <unistd.h>
+
+#include "bcp_task.h"
+
+#define PER_LANE 16
+#define LANE_MASK 15
+
+void bcp_assign_lanes(int nlanes, uint64_t njobs, const FileInfo *jobs, int *lane)
+{
+    if (nlanes <= 0 || !lane)
+        return;
+    uint64_t *prev = calloc((size_t)nlanes * PER_LANE, sizeof(uint64_t));
+    int *offsets = calloc((size_t)nlanes, sizeof(int));
+    if (!prev || !offsets) {
+        for (uint64_t i = 0; i < njobs; i++)
+            lane[i] = (int)(i % (uint64_t)nlanes);
+        free(prev);
+        free(offsets);
+        return;
+    }
+    for (uint64_t i = 0; i < njobs; i++) {
+        /* The reference forms the P bit as (1 << GET_P(x)) with an int: on
+         * x86-64 the shift count is taken mod 32 and the int sign-extends
+         * into the u64 mask.  Reproduced so lanes match for every P,
+         * including NO_P items (assigned, then skipped by process_list). */
+        const uint32_t p = (uint32_t)GET_P(jobs[i].locations);
+        const uint64_t pbit = (uint64_t)(int64_t)(int32_t)(UINT32_C(1) << (p & 31u));
+        const uint64_t target = (jobs[i].locations & L_MASK) | pbit;
+        const int lane_offset = (int)(i % (uint64_t)nlanes);
+        int best_idx = lane_offset;
+        int best_so_far = 0;
+        for (int j0 = 0; j0 < nlanes; j0++) {
+            const int j = (lane_offset + j0) % nlanes;
+            int dist = PER_LANE;
+            const int off = offsets[j];
+            /* distance to the most recent task in lane j that shares a target */
+            for (int k = 0; k < PER_LANE; k++)
+                if (target & prev[j * PER_LANE + ((off + k) & LANE_MASK)])
+                    dist = PER_LANE - k;
+            if (dist > best_so_far) {
+                best_so_far = dist;
+                best_idx = j;
+            }
+        }
+        lane[i] = best_idx;
+        prev[best_idx * PER_LANE + offsets[best_idx]] = target;
+        offsets[best_idx] = (offsets[best_idx] + 1) & LANE_MASK;
+    }
+    free(offsets);
+    free(prev);
+}
+
+static double now_s(void)
+{
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return (double)t.tv_sec + (double)t.tv_nsec * 1e-9;
+}
+
+/* ---- per-target host state -------------------------------------------- */
+
+static int open_store(const char *root, int st, int rebuilding, int corrupt_fd, FILE *log, HostState *hs)
+{
+    char path[4096];
+    memset(hs, 0, sizeof(*hs));
+    hs->storage_target = st;
+    hs->log = log;
+    hs->corrupt_files_fd = corrupt_fd;
+    snprintf(path, sizeof(path), "%s/st%d", root, st);
+    int store_fd = open(path, O_DIRECTORY | O_RDONLY);
+    if (store_fd < 0)
+        return -errno;
+    if (mkdirat(store_fd, "parity", 0700) == -1 && errno != EEXIST) {
+        close(store_fd);
+        return -errno;
+    }
+    hs->fd_null = open("/dev/null", O_WRONLY);
+    hs->fd_zero = open("/dev/zero", O_RDONLY);
+    int chunks = openat(store_fd, "chunks", O_DIRECTORY | O_RDONLY);
+    int parity = openat(store_fd, "parity", O_DIRECTORY | O_RDONLY);
+    close(store_fd);
+    if (chunks < 0 || parity < 0 || hs->fd_null < 0 || hs->fd_zero < 0)
+        return -ENOENT;
+    if (rebuilding) {
+        /* rebuild/main.c:210-212: rebuilt chunks are written into chunks/ */
+        hs->write_dir = chunks;
+        hs->read_chunk_dir = chunks;
+        hs->read_parity_dir = parity;
+    } else {
+        /* gen/main.c:740-742 */
+        hs->write_dir = parity;
+        hs->read_chunk_dir = chunks;
+        hs->read_parity_dir = -1;
+        /* keep the parity fd open through write_dir only */
+    }
+    return 0;
+}
+
+static void close_store(HostState *hs, int rebuilding)
+{
+    if (hs->fd_null > 0)
+        close(hs->fd_null);
+    if (hs->fd_zero > 0)
+        close(hs->fd_zero);
+    if (hs->read_chunk_dir > 0)
+        close(hs->read_chunk_dir);
+    if (rebuilding) {
+        if (hs->read_parity_dir > 0)
+            close(hs->read_parity_dir);
+    } else if (hs->write_dir > 0) {
+        close(hs->write_dir);
+    }
+    if (hs->error && hs->log)
+        fprintf(hs->log, "started using zero/null after '%s' gave error %d (%s) on st %d\n",
+                hs->error_path ? hs->error_path : "?", hs->error, strerror(hs->error), hs->storage_target);
+}
+
+/* ---- generation lanes --------------------------------------------------- */
+
+typedef struct {
+    HostState *hs;
+    const bcp_work_item *items;
+    size_t nitems;
+    const int *lanes;
+    int lane;
+    int rank;
+    ProgressSample sample;
+    uint64_t tasks;
+} lane_arg;
+
+/* process_list (gen/main.c:116-164) for one lane of one rank. */
+static void *gen_lane(void *p)
+{
+    lane_arg *a = p;
+    bcp_lb_set_rank(a->rank);
+    TaskInfo ti = {a->hs->read_chunk_dir, 0, -1, a->lane, &a->sample};
+    for (size_t i = 0; i < a->nitems; i++) {
+        if (a->lanes[i] != a->lane)
+            continue;
+        if ((uint64_t)GET_P(a->items[i].fi.locations) == NO_P)
+            continue;
+        double t0 = now_s();
+        int report = process_task(a->hs, a->items[i].path, &a->items[i].fi, ti);
+        if (report) {
+            a->sample.dt += now_s() - t0;
+            a->sample.nfiles += 1;
+            a->tasks++;
+        }
+    }
+    bcp_task_thread_release();
+    return NULL;
+}
+
+static int check_items(int ntargets, const bcp_work_item *items, size_t nitems)
+{
+    for (size_t i = 0; i < nitems; i++) {
+        uint64_t loc = items[i].fi.locations;
+        if (!items[i].path || strlen(items[i].path) == 0)
+            return -EINVAL;
+        if ((loc & L_MASK) >> ntargets)
+            return -EINVAL; /* chunk on a target outside the world */
+        int P = GET_P(loc);
+        if ((uint64_t)P != NO_P && (P >= ntargets || TEST_BIT(loc, P)))
+            return -EINVAL; /* process_task asserts P_IS_INVALID == 0 */
+    }
+    return 0;
+}
+
+int bcp_gen_run(const char *store_root, int ntargets, const bcp_work_item *items, size_t nitems, int nlanes,
+                const int *lanes_in, FILE *log, bcp_run_stats *stats)
+{
+    if (!store_root || ntargets < 1 || ntargets > MAX_STORAGE_TARGETS || nlanes < 1 || nlanes > 64 ||
+        (nitems && !items))
+        return -EINVAL;
+    int rc = check_items(ntargets, items, nitems);
+    if (rc)
+        return rc;
+    int *lanes = NULL;
+    if (!lanes_in) {
+        FileInfo *fis = malloc((nitems ? nitems : 1) * sizeof(FileInfo));
+        lanes = malloc((nitems ? nitems : 1) * sizeof(int));
+        if (!fis || !lanes) {
+            free(fis);
+            free(lanes);
+            return -ENOMEM;
+        }
+        for (size_t i = 0; i < nitems; i++)
+            fis[i] = items[i].fi;
+        bcp_assign_lanes(nlanes, nitems, fis, lanes);
+        free(fis);
+    }
+    const int *use_lanes = lanes_in ? lanes_in : lanes;
+    for (int k = 0; k < MAX_STORAGE_TARGETS; k++)
+        st2rank[k] = k < ntargets ? k + 1 : -1;
+    if ((rc = bcp_lb_init(ntargets + 1))) {
+        free(lanes);
+        return rc;
+    }
+    HostState *hs = calloc((size_t)ntargets, sizeof(HostState));
+    lane_arg *args = calloc((size_t)ntargets * nlanes, sizeof(lane_arg));
+    pthread_t *th = calloc((size_t)ntargets * nlanes, sizeof(pthread_t));
+    if (!hs || !args || !th) {
+        rc = -ENOMEM;
+        goto out;
+    }
+    for (int k = 0; k < ntargets; k++)
+        if ((rc = open_store(store_root, k, 0, -1, log, &hs[k])))
+            goto out;
+    double t0 = now_s();
+    int started = 0;
+    for (int k = 0; k < ntargets; k++)
+        for (int l = 0; l < nlanes; l++) {
+            lane_arg *a = &args[k * nlanes + l];
+            a->hs = &hs[k];
+            a->items = items;
+            a->nitems = nitems;
+            a->lanes = use_lanes;
+            a->lane = l;
+            a->rank = k + 1;
+            if (pthread_create(&th[started], NULL, gen_lane, a) != 0) {
+                /* cannot leave partner lanes blocked: give up loudly */
+                fprintf(stderr, "bcp_gen_run: thread create failed\n");
+                abort();
+            }
+            started++;
+        }
+    for (int i = 0; i < started; i++)
+        pthread_join(th[i], NULL);
+    if (stats) {
+        memset(stats, 0, sizeof(*stats));
+        stats->seconds = now_s() - t0;
+        for (int i = 0; i < started; i++) {
+            stats->tasks += args[i].tasks;
+            stats->bytes_read += args[i].sample.bytes_read;
+            stats->bytes_written += args[i].sample.bytes_written;
+        }
+        for (int k = 0; k < ntargets; k++)
+            stats->errors += hs[k].error != 0;
+    }
+out:
+    if (hs)
+        for (int k = 0; k < ntargets; k++)
+            close_store(&hs[k], 0);
+    {
+        int frc = bcp_lb_finalize();
+        if (!rc && frc)
+            rc = frc; /* unmatched messages: a protocol bug */
+    }
+    free(th);
+    free(args);
+    free(hs);
+    free(lanes);
+    return rc;
+}
+
+/* ---- rebuild ------------------------------------------------------------ */
+
+typedef struct {
+    HostState *hs;
+    const bcp_work_item *items;
+    size_t nitems;
+    int rebuild_target;
+    int rank;
+    ProgressSample sample;
+    uint64_t tasks;
+} rebuild_arg;
+
+/* do_file (rebuild/main.c:40-89) over the whole item list, one lane. */
+static void *rebuild_rank(void *p)
+{
+    rebuild_arg *a = p;
+    bcp_lb_set_rank(a->rank);
+    const int my_st = a->hs->storage_target;
+    const int victim = a->rebuild_target;
+    for (size_t i = 0; i < a->nitems; i++) {
+        const FileInfo *fi = &a->items[i].fi;
+        const int P = GET_P(fi->locations);
+        if ((uint64_t)P == NO_P || P == victim || TEST_BIT(fi->locations, victim) == 0)
+            continue;
+        FileInfo mod = *fi;
+        /* the parity holder becomes a source, the victim the new "P" */
+        mod.locations |= UINT64_C(1) << P;
+        mod.locations &= ~(UINT64_C(1) << victim);
+        mod.locations = WITH_P(mod.locations, (uint64_t)victim);
+        const int rdir = (P == my_st) ? a->hs->read_parity_dir : a->hs->read_chunk_dir;
+        TaskInfo ti = {rdir, 1, P, 0, &a->sample};
+        double t0 = now_s();
+        if (process_task(a->hs, a->items[i].path, &mod, ti)) {
+            a->sample.dt += now_s() - t0;
+            a->sample.nfiles += 1;
+            a->tasks++;
+        }
+    }
+    bcp_task_thread_release();
+    return NULL;
+}
+
+int bcp_rebuild_run(const char *store_root, int ntargets, int rebuild_target, const bcp_work_item *items,
+                    size_t nitems, const char *corrupt_list_path, FILE *log, bcp_run_stats *stats)
+{
+    if (!store_root || ntargets < 2 || ntargets > MAX_STORAGE_TARGETS || rebuild_target < 0 ||
+        rebuild_target >= ntargets || (nitems && !items))
+        return -EINVAL;
+    int rc = check_items(ntargets, items, nitems);
+    if (rc)
+        return rc;
+    for (int k = 0; k < MAX_STORAGE_TARGETS; k++)
+        st2rank[k] = k < ntargets ? k + 1 : -1;
+    int corrupt_fd = -1;
+    if (corrupt_list_path) {
+        corrupt_fd = open(corrupt_list_path, O_WRONLY | O_CREAT | O_TRUNC | O_APPEND, S_IRUSR | S_IWUSR);
+        if (corrupt_fd < 0)
+            return -errno;
+    } else {
+        corrupt_fd = open("/dev/null", O_WRONLY);
+    }
+    if ((rc = bcp_lb_init(ntargets + 1))) {
+        close(corrupt_fd);
+        return rc;
+    }
+    HostState *hs = calloc((size_t)ntargets, sizeof(HostState));
+    rebuild_arg *args = calloc((size_t)ntargets, sizeof(rebuild_arg));
+    pthread_t *th = calloc((size_t)ntargets, sizeof(pthread_t));
+    if (!hs || !args || !th) {
+        rc = -ENOMEM;
+        goto out;
+    }
+    for (int k = 0; k < ntargets; k++)
+        if ((rc = open_store(store_root, k, 1, corrupt_fd, log, &hs[k])))
+            goto out;
+    double t0 = now_s();
+    for (int k = 0; k < ntargets; k++) {
+        args[k] = (rebuild_arg){&hs[k], items, nitems, rebuild_target, k + 1, PROGRESS_SAMPLE_INIT, 0};
+        if (pthread_create(&th[k], NULL, rebuild_rank, &args[k]) != 0) {
+            fprintf(stderr, "bcp_rebuild_run: thread create failed\n");
+            abort();
+        }
+    }
+    for (int k = 0; k < ntargets; k++)
+        pthread_join(th[k], NULL);
+    if (stats) {
+        memset(stats, 0, sizeof(*stats));
+        stats->seconds = now_s() - t0;
+        for (int k = 0; k < ntargets; k++) {
+            stats->tasks += args[k].tasks;
+            stats->bytes_read += args[k].sample.bytes_read;
+            stats->bytes_written += args[k].sample.bytes_written;
+            stats->errors += hs[k].error != 0;
+        }
+    }
+out:
+    if (hs)
+        for (int k = 0; k < ntargets; k++)
+            close_store(&hs[k], 1);
+    {
+        int frc = bcp_lb_finalize();
+        if (!rc && frc)
+            rc = frc;
+    }
+    close(corrupt_fd);
+    free(th);
+    free(args);
+    free(hs);
+    return rc;
+}

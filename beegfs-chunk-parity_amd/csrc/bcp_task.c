@@ -1,0 +1,553 @@
+/*
+ * bcp_task.c -- the per-rank chunk-streaming protocol (process_task) with the
+ * P role's fold on the GPU.
+ *
+ * Follows the reference's roles and message flow
+ * (src/beegfs-raid5/common/task_processing.c):
+ *   process_task      :325-340  dispatch by role
+ *   parity_generator  :117-245  P role: sizes -> max_cs -> windows -> parity
+ *   chunk_sender      :247-322  source role: size -> windows (zero padded)
+ * over the loopback transport (bcp_loopback.c) instead of MPI.  The window
+ * fold (xor_parity at :211) becomes: pinned window rows (256-byte pitch, so
+ * every row is 16-byte aligned for the fast kernel) -> H2D -> XOR kernel ->
+ * D2H on the calling lane's own HIP queue.  Twelve lanes per rank therefore
+ * keep twelve queues of copies and kernels in flight on the device.
+ */
+#define _GNU_SOURCE
+#include <assert.h>
+#include <errno.h>
+#include <fcntl.h>
+#include <pthread.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/stat.h>
+#include <sys/types.h>
+#include <unistd.h>
+
+#include "bcp_task.h"
+
+#define WINDOW ((uint64_t)BCP_WINDOW_BYTES)
+#define ROW_ALIGN 256u
+#define MAX_DEVICES 64
+
+__attribute__((weak)) int st2rank[MAX_STORAGE_TARGETS];
+
+#define LOGERR(format, ...)                                                                      \
+    do {                                                                                        \
+        if (hs->log) {                                                                          \
+            fprintf(hs->log, "%s:%d (%s): " format, __FILE__, __LINE__, __func__, __VA_ARGS__); \
+            fflush(hs->log);                                                                    \
+        }                                                                                       \
+    } while (0)
+
+#define MIN_(a, b) ((a) < (b) ? (a) : (b))
+#define MAX_(a, b) ((a) > (b) ? (a) : (b))
+
+/* ---- engines / device map / test hook ---------------------------------- */
+static pthread_mutex_t g_lock = PTHREAD_MUTEX_INITIALIZER;
+static bcp_engine *g_engines[MAX_DEVICES];
+static int g_engine_rc[MAX_DEVICES];
+static int g_devmap[MAX_STORAGE_TARGETS];
+static int g_devmap_n = 0;
+static bcp_xor_hook_fn g_hook = NULL;
+static void *g_hook_ctx = NULL;
+
+int bcp_task_set_device_map(const int *devices, int ntargets)
+{
+    if (ntargets < 0 || ntargets > MAX_STORAGE_TARGETS || (ntargets && !devices))
+        return -EINVAL;
+    pthread_mutex_lock(&g_lock);
+    for (int i = 0; i < ntargets; i++)
+        g_devmap[i] = devices[i];
+    g_devmap_n = ntargets;
+    pthread_mutex_unlock(&g_lock);
+    return 0;
+}
+
+void bcp_task_set_xor_hook(bcp_xor_hook_fn fn, void *ctx)
+{
+    pthread_mutex_lock(&g_lock);
+    g_hook = fn;
+    g_hook_ctx = ctx;
+    pthread_mutex_unlock(&g_lock);
+}
+
+static int engine_for_target(int st, bcp_engine **out, int *device)
+{
+    int ndev = 0;
+    bcp_device_count(&ndev);
+    if (ndev <= 0)
+        return -ENODEV;
+    int dev = st % ndev;
+    pthread_mutex_lock(&g_lock);
+    if (st < g_devmap_n)
+        dev = g_devmap[st];
+    if (dev < 0 || dev >= ndev || dev >= MAX_DEVICES) {
+        pthread_mutex_unlock(&g_lock);
+        return -ENODEV;
+    }
+    if (!g_engines[dev] && !g_engine_rc[dev])
+        g_engine_rc[dev] = bcp_engine_create(dev, &g_engines[dev]);
+    int rc = g_engine_rc[dev];
+    *out = g_engines[dev];
+    pthread_mutex_unlock(&g_lock);
+    *device = dev;
+    return rc;
+}
+
+/* ---- per-lane resources (thread-local, reused across tasks) ------------- */
+typedef struct {
+    int device;
+    bcp_engine *eng;
+    bcp_queue *q;
+    uint8_t *h_win[2];  /* pinned window rows [n][pitch] */
+    uint8_t *h_par;     /* pinned fold output */
+    size_t h_cap, hp_cap;
+    int h_pinned;
+    void *d_src, *d_out;
+    size_t d_cap, dout_cap;
+    uint8_t *send_buf;  /* chunk_sender window buffer */
+    size_t send_cap;
+} lane_res;
+
+static __thread lane_res t_res = {.device = -1};
+
+static void free_host(lane_res *L, void *p)
+{
+    if (!p)
+        return;
+    if (L->h_pinned)
+        bcp_host_free(L->eng, p);
+    else
+        free(p);
+}
+
+void bcp_task_thread_release(void)
+{
+    lane_res *L = &t_res;
+    free_host(L, L->h_win[0]);
+    free_host(L, L->h_win[1]);
+    free_host(L, L->h_par);
+    if (L->eng) {
+        if (L->d_src)
+            bcp_dev_free(L->eng, L->d_src);
+        if (L->d_out)
+            bcp_dev_free(L->eng, L->d_out);
+    }
+    if (L->q)
+        bcp_queue_destroy(L->q);
+    free(L->send_buf);
+    memset(L, 0, sizeof(*L));
+    L->device = -1;
+}
+
+int bcp_task_shutdown(void)
+{
+    bcp_task_thread_release();
+    pthread_mutex_lock(&g_lock);
+    for (int d = 0; d < MAX_DEVICES; d++) {
+        if (g_engines[d])
+            bcp_engine_destroy(g_engines[d]);
+        g_engines[d] = NULL;
+        g_engine_rc[d] = 0;
+    }
+    pthread_mutex_unlock(&g_lock);
+    return 0;
+}
+
+/* Window buffers for n rows of `pitch` plus a fold output of `nbytes`.
+ * Pinned through the engine when the GPU folds, plain memory under the hook. */
+static int lane_windows(lane_res *L, HostState *hs, int use_gpu, size_t rows_bytes, size_t nbytes)
+{
+    int rc = 0;
+    if (use_gpu && (!L->eng || L->device < 0)) {
+        int dev = -1;
+        bcp_engine *e = NULL;
+        if ((rc = engine_for_target(hs->storage_target, &e, &dev)))
+            return rc;
+        if (L->eng && L->device != dev)
+            bcp_task_thread_release();
+        L->eng = e;
+        L->device = dev;
+    }
+    if (use_gpu && !L->q && (rc = bcp_queue_create(L->eng, &L->q)))
+        return rc;
+    int want_pinned = use_gpu;
+    if (L->h_cap && L->h_pinned != want_pinned) {
+        free_host(L, L->h_win[0]);
+        free_host(L, L->h_win[1]);
+        free_host(L, L->h_par);
+        L->h_win[0] = L->h_win[1] = L->h_par = NULL;
+        L->h_cap = L->hp_cap = 0;
+    }
+    L->h_pinned = want_pinned;
+    if (L->h_cap < rows_bytes) {
+        free_host(L, L->h_win[0]);
+        free_host(L, L->h_win[1]);
+        L->h_win[0] = L->h_win[1] = NULL;
+        L->h_cap = 0;
+        size_t cap = MAX_(rows_bytes, (size_t)1 << 20);
+        for (int i = 0; i < 2; i++) {
+            if (want_pinned)
+                rc = bcp_host_alloc(L->eng, cap, (void **)&L->h_win[i]);
+            else
+                L->h_win[i] = malloc(cap), rc = L->h_win[i] ? 0 : -ENOMEM;
+            if (rc)
+                return rc;
+        }
+        L->h_cap = cap;
+    }
+    if (L->hp_cap < nbytes || !L->h_par) {
+        free_host(L, L->h_par);
+        L->h_par = NULL;
+        size_t cap = MAX_(nbytes, (size_t)1 << 20);
+        if (want_pinned)
+            rc = bcp_host_alloc(L->eng, cap, (void **)&L->h_par);
+        else
+            L->h_par = malloc(cap), rc = L->h_par ? 0 : -ENOMEM;
+        if (rc)
+            return rc;
+        L->hp_cap = cap;
+    }
+    if (use_gpu) {
+        if (L->d_cap < rows_bytes) {
+            if (L->d_src)
+                bcp_dev_free(L->eng, L->d_src);
+            L->d_src = NULL;
+            L->d_cap = 0;
+            if ((rc = bcp_dev_alloc(L->eng, MAX_(rows_bytes, (size_t)1 << 20), &L->d_src)))
+                return rc;
+            L->d_cap = MAX_(rows_bytes, (size_t)1 << 20);
+        }
+        if (L->dout_cap < nbytes || !L->d_out) {
+            if (L->d_out)
+                bcp_dev_free(L->eng, L->d_out);
+            L->d_out = NULL;
+            L->dout_cap = 0;
+            if ((rc = bcp_dev_alloc(L->eng, MAX_(nbytes, (size_t)1 << 20), &L->d_out)))
+                return rc;
+            L->dout_cap = MAX_(nbytes, (size_t)1 << 20);
+        }
+    }
+    return 0;
+}
+
+/* The fold of one window (replaces xor_parity at task_processing.c:211):
+ * out = XOR of n rows of `pitch` bytes, nbytes each. */
+static int fold_window(lane_res *L, HostState *hs, bcp_xor_hook_fn hook, void *ctx, const uint8_t *rows,
+                       size_t pitch, size_t nbytes, int n, uint8_t *out)
+{
+    if (hook) {
+        static int warned = 0;
+        if (!warned) {
+            warned = 1;
+            LOGERR("XOR test hook active on st %d (no GPU fold)\n", hs->storage_target);
+        }
+        return hook(out, nbytes, rows, pitch, n, ctx);
+    }
+    int rc;
+    if ((rc = bcp_h2d_async(L->q, L->d_src, rows, pitch * (size_t)n)))
+        return rc;
+    if ((rc = bcp_xor_strided_async(L->q, L->d_out, pitch, L->d_src, pitch * (size_t)n, pitch, 1, (uint32_t)n,
+                                    nbytes)))
+        return rc;
+    if ((rc = bcp_d2h_async(L->q, out, L->d_out, nbytes)))
+        return rc;
+    return bcp_queue_sync(L->q);
+}
+
+/* ---- file helpers (task_processing.c:29-79) ----------------------------- */
+
+/* mkdir -p for the directories of `filename` under wdir. */
+static void mkdir_for_file(int wdir, const char *filename)
+{
+    size_t len = strlen(filename);
+    char *tmp = malloc(len + 1);
+    if (!tmp)
+        return;
+    memcpy(tmp, filename, len + 1);
+    for (char *p = tmp + 1; *p; p++) {
+        if (*p == '/') {
+            *p = 0;
+            mkdirat(wdir, tmp, S_IRWXU);
+            *p = '/';
+        }
+    }
+    free(tmp);
+}
+
+static int open_chunk_readonly(int rdir, const char *path)
+{
+    int fd = openat(rdir, path, O_RDONLY);
+    if (fd > 0)
+        posix_fadvise(fd, 0, 0, POSIX_FADV_SEQUENTIAL);
+    return fd;
+}
+
+static int open_new_parity(int wdir, const char *path, off_t expected_size)
+{
+    mkdir_for_file(wdir, path);
+    int fd = openat(wdir, path, O_CREAT | O_WRONLY | O_TRUNC, S_IRUSR | S_IWUSR);
+    if (fd > 0 && expected_size > 0)
+        posix_fallocate(fd, 0, expected_size);
+    return fd;
+}
+
+/* Corrupt list entry (task_processing.c:54-60); written whole, one line. */
+static void push_corrupt_path(HostState *hs, const char *path)
+{
+    size_t len = strlen(path);
+    char *line = malloc(len + 2);
+    if (!line)
+        return;
+    memcpy(line, path, len);
+    line[len] = '\n';
+    ssize_t w = write(hs->corrupt_files_fd, line, len + 1);
+    (void)w;
+    free(line);
+}
+
+static int active_ranks(uint64_t locations) { return __builtin_popcountll(locations & L_MASK); }
+
+/* ---- roles ------------------------------------------------------------- */
+
+static void parity_generator(const char *path, const FileInfo *task, TaskInfo ti, HostState *hs)
+{
+    const int n = active_ranks(task->locations);
+    int ranks[MAX_STORAGE_TARGETS];
+    for (int i = 0, j = 0; i < MAX_STORAGE_TARGETS; i++)
+        if (TEST_BIT(task->locations, i))
+            ranks[j++] = st2rank[i];
+
+    /* nobody holds a chunk any more: the parity chunk goes too (:141-144) */
+    if (n == 0) {
+        unlinkat(hs->write_dir, path, 0);
+        return;
+    }
+
+    bcp_lb_req *req[MAX_STORAGE_TARGETS];
+    uint64_t chunk_sizes[MAX_STORAGE_TARGETS] = {0};
+    if (ti.is_rebuilding) {
+        bcp_lb_recv(chunk_sizes, (size_t)n * sizeof(uint64_t), st2rank[ti.actual_P_st], ti.tag, NULL);
+    } else {
+        for (int j = 0; j < n; j++)
+            bcp_lb_irecv(&chunk_sizes[j], sizeof(uint64_t), ranks[j], ti.tag, &req[j]);
+        bcp_lb_waitall(n, req);
+    }
+
+    uint64_t max_cs = 0;
+    for (int j = 0; j < n; j++)
+        max_cs = MAX_(max_cs, chunk_sizes[j]);
+    for (int j = 0; j < n; j++)
+        bcp_lb_isend(&max_cs, sizeof(max_cs), ranks[j], ti.tag, &req[j]);
+    bcp_lb_waitall(n, req);
+
+    uint64_t final_parity_chunk_size = max_cs + (uint64_t)n * sizeof(uint64_t);
+    if (ti.is_rebuilding) {
+        /* index of this (rebuilt) target in the stored header (:169-174) */
+        uint64_t loc = task->locations & ~(UINT64_C(1) << ti.actual_P_st) & L_MASK;
+        uint64_t my_mask = (UINT64_C(1) << hs->storage_target) - 1;
+        final_parity_chunk_size = chunk_sizes[active_ranks(loc & my_mask)];
+    }
+
+    const size_t buffer_size = (size_t)MIN_(WINDOW, max_cs);
+    const size_t pitch = (buffer_size + ROW_ALIGN - 1) / ROW_ALIGN * ROW_ALIGN;
+    const uint64_t final_size = max_cs + (uint64_t)n * 8u;
+    const uint64_t expected_messages = (max_cs + WINDOW - 1) / WINDOW;
+    uint64_t data_left = max_cs;
+
+    pthread_mutex_lock(&g_lock);
+    bcp_xor_hook_fn hook = g_hook;
+    void *hook_ctx = g_hook_ctx;
+    pthread_mutex_unlock(&g_lock);
+
+    lane_res *L = &t_res;
+    int have_had_error = hs->error;
+    int res_rc = expected_messages ? lane_windows(L, hs, hook == NULL, pitch * (size_t)n, buffer_size) : 0;
+    uint8_t *scratch = NULL; /* receive space if staging could not be set up */
+    uint8_t *win_a, *win_b, *pblk;
+    if (res_rc) {
+        LOGERR("no parity engine for '%s' on st %d: %s\n", path, hs->storage_target, bcp_strerror(res_rc));
+        if (!have_had_error)
+            have_had_error = res_rc == -ENODEV ? ENODEV : (res_rc == -ENOMEM ? ENOMEM : EIO);
+        scratch = malloc(2 * pitch * (size_t)n + buffer_size + 1);
+        if (!scratch)
+            abort(); /* cannot even drain the senders */
+        win_a = scratch;
+        win_b = scratch + pitch * (size_t)n;
+        pblk = scratch + 2 * pitch * (size_t)n;
+    } else if (expected_messages) {
+        win_a = L->h_win[0];
+        win_b = L->h_win[1];
+        pblk = L->h_par;
+    } else {
+        win_a = win_b = pblk = NULL; /* header-only parity chunk */
+    }
+
+    int P_fd = hs->fd_null;
+    if (have_had_error == 0) {
+        P_fd = open_new_parity(hs->write_dir, path, (off_t)final_size);
+        if (P_fd <= 0) {
+            have_had_error = errno;
+            LOGERR("opened parity chunk '%s' with error = '%s'\n", path, strerror(errno));
+            P_fd = hs->fd_null;
+        }
+    } else {
+        LOGERR("using null for '%s', we already have global errno %d\n", path, have_had_error);
+    }
+
+    /* gen: the chunk sizes head the parity chunk (:199-201) */
+    if (!ti.is_rebuilding)
+        if (write(P_fd, chunk_sizes, sizeof(uint64_t) * (size_t)n) <= 0)
+            have_had_error = errno;
+
+    for (uint64_t msg_i = 0; msg_i < expected_messages; msg_i++) {
+        if (msg_i == 0)
+            for (int j = 0; j < n; j++)
+                bcp_lb_irecv(win_a + (size_t)j * pitch, buffer_size, ranks[j], ti.tag, &req[j]);
+        bcp_lb_waitall(n, req);
+        if (msg_i + 1 != expected_messages)
+            for (int j = 0; j < n; j++)
+                bcp_lb_irecv(win_b + (size_t)j * pitch, buffer_size, ranks[j], ti.tag, &req[j]);
+        /* fold window msg_i on the GPU while the senders fill win_b */
+        if (!have_had_error) {
+            int frc = fold_window(L, hs, hook, hook_ctx, win_a, pitch, buffer_size, n, pblk);
+            if (frc) {
+                have_had_error = EIO;
+                LOGERR("GPU fold of '%s' failed: %s\n", path, bcp_strerror(frc));
+            }
+        }
+        if (!have_had_error) {
+            size_t wsize = (size_t)MIN_((uint64_t)buffer_size, data_left);
+            ssize_t w = write(P_fd, pblk, wsize);
+            if (w <= 0) {
+                have_had_error = errno;
+                LOGERR("writing '%s' caused new error %d (%s) after %llu bytes\n", path, errno, strerror(errno),
+                       (unsigned long long)(final_size - data_left));
+            }
+            data_left -= wsize;
+        }
+        if (ti.sample)
+            ti.sample->bytes_written += buffer_size;
+        uint8_t *t = win_a;
+        win_a = win_b;
+        win_b = t;
+    }
+
+    if (ti.is_rebuilding && P_fd != hs->fd_null)
+        if (ftruncate(P_fd, (off_t)final_parity_chunk_size) != 0 && !have_had_error)
+            have_had_error = errno;
+
+    if (hs->error == 0 && have_had_error != 0) {
+        LOGERR("local error on '%s' elevated to global error\n", path);
+        hs->error = have_had_error;
+        hs->error_path = strdup(path);
+    }
+    free(scratch);
+    if (P_fd != hs->fd_null)
+        close(P_fd);
+}
+
+static uint8_t *sender_buffer(size_t need)
+{
+    lane_res *L = &t_res;
+    if (L->send_cap < need || !L->send_buf) {
+        free(L->send_buf);
+        L->send_cap = MAX_(need, (size_t)1 << 20);
+        L->send_buf = malloc(L->send_cap);
+        if (!L->send_buf)
+            L->send_cap = 0;
+    }
+    return L->send_buf;
+}
+
+static void chunk_sender(const char *path, const FileInfo *task, TaskInfo ti, HostState *hs)
+{
+    const int my_st = hs->storage_target;
+    const int coordinator = st2rank[GET_P(task->locations)];
+    const int ntargets = active_ranks(task->locations);
+    uint64_t fd_size = 0;
+    int have_had_error = 0;
+    int fd = open_chunk_readonly(ti.read_dir, path);
+    if (fd <= 0) {
+        have_had_error = errno;
+        fd = hs->fd_zero;
+        LOGERR("opening '%s' caused new error %d (%s)\n", path, errno, strerror(errno));
+    } else {
+        struct stat st;
+        fstat(fd, &st);
+        fd_size = (uint64_t)st.st_size;
+        if (ti.is_rebuilding && ti.actual_P_st == my_st)
+            fd_size -= (uint64_t)ntargets * sizeof(uint64_t);
+        if (ti.is_rebuilding && ti.actual_P_st != my_st && st.st_mtime > task->timestamp)
+            push_corrupt_path(hs, path);
+    }
+
+    if (ti.is_rebuilding && ti.actual_P_st == my_st) {
+        /* the parity holder forwards the stored header instead of a size */
+        uint64_t chunk_sizes[MAX_STORAGE_TARGETS] = {0};
+        ssize_t r = read(fd, chunk_sizes, (size_t)ntargets * sizeof(uint64_t));
+        (void)r;
+        bcp_lb_send(chunk_sizes, (size_t)ntargets * sizeof(uint64_t), coordinator, ti.tag);
+    } else if (!ti.is_rebuilding) {
+        bcp_lb_send(&fd_size, sizeof(fd_size), coordinator, ti.tag);
+    }
+
+    uint64_t data_to_send = 0;
+    bcp_lb_recv(&data_to_send, sizeof(data_to_send), coordinator, ti.tag, NULL);
+
+    const size_t buffer_size = (size_t)MIN_(WINDOW, data_to_send);
+    uint8_t *data = sender_buffer(buffer_size);
+    if (!data)
+        abort();
+    /* A buffer that is never filled is sent as zeros: the reference sends
+     * uninitialised memory for a zero-length chunk (quirk A3-q2). */
+    if (have_had_error != 0 || fd_size == 0)
+        memset(data, 0, buffer_size);
+
+    uint64_t data_sent = 0;
+    while (data_sent < data_to_send) {
+        uint64_t left = data_to_send - data_sent;
+        /* once the file is exhausted the previous window is re-sent (A3-q1) */
+        if (have_had_error == 0 && data_sent < fd_size) {
+            ssize_t r = read(fd, data, (size_t)MIN_((uint64_t)buffer_size, left));
+            if (r < 0) {
+                have_had_error = errno;
+                memset(data, 0, buffer_size);
+                LOGERR("reading '%s' caused new error %d (%s) after %llu bytes\n", path, errno, strerror(errno),
+                       (unsigned long long)data_sent);
+            }
+            if (r >= 0 && (size_t)r < buffer_size)
+                memset(data + r, 0, buffer_size - (size_t)r);
+        }
+        if (ti.sample)
+            ti.sample->bytes_read += buffer_size;
+        data_sent += buffer_size;
+        bcp_lb_send(data, buffer_size, coordinator, ti.tag);
+    }
+
+    /* ENOENT: the chunk vanished after planning; an unlink event follows. */
+    if (hs->error == 0 && have_had_error != 0 && have_had_error != ENOENT) {
+        LOGERR("local error on '%s' elevated to global error\n", path);
+        hs->error = have_had_error;
+        hs->error_path = strdup(path);
+    }
+    if (fd != hs->fd_zero)
+        close(fd);
+}
+
+int process_task(HostState *hs, const char *path, const FileInfo *fi, TaskInfo ti)
+{
+    assert(GET_P(fi->locations) != (int)NO_P);
+    assert(P_IS_INVALID(fi->locations) == 0);
+    assert(hs->storage_target >= 0);
+
+    if (GET_P(fi->locations) == hs->storage_target)
+        parity_generator(path, fi, ti, hs);
+    else if (TEST_BIT(fi->locations, hs->storage_target))
+        chunk_sender(path, fi, ti, hs);
+    else
+        return 0;
+    return active_ranks(fi->locations) != 0;
+}

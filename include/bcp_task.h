@@ -1,0 +1,172 @@
+/*
+ * bcp_task.h -- per-rank chunk-streaming interface of the parity engine
+ * (host C layer of libbcp.so).
+ *
+ * Drop-in for the reference's task layer:
+ *   int process_task(HostState *hs, const char *path, const FileInfo *fi,
+ *                    TaskInfo ti);
+ *       -- src/beegfs-raid5/common/task_processing.h:20-24
+ * with the reference's types (common.h:15-48, task_processing.h:7-18,
+ * progress_reporting.h:10-20) kept field for field, so the callers
+ * process_list (gen/main.c:116-164) and do_file (rebuild/main.c:40-89) bind
+ * unchanged.  What differs is underneath:
+ *   - the P role folds the received windows on the GPU through the engine
+ *     (include/bcp.h) instead of the CPU xor_parity;
+ *   - ranks are loopback ranks (threads of one process) talking through an
+ *     MPI-like point-to-point transport (bcp_lb_*) matched by
+ *     (source, tag) in FIFO order, in place of MPI_COMM_WORLD.
+ * Behaviour kept from the reference: message flow and sizes, 10 MiB windows
+ * with the replay-after-EOF quirk, parity chunk file format (u64 chunk_size[n]
+ * header in ascending storage-target order + max_cs XOR bytes), rebuild
+ * truncation, the corrupt list, sticky per-rank errors (/dev/zero, /dev/null).
+ */
+#ifndef BCP_TASK_H
+#define BCP_TASK_H
+
+#include <stddef.h>
+#include <stdint.h>
+#include <stdio.h>
+
+#include "bcp.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- shared types and bit layout (common.h:15-48) ---------------------- */
+#define MODIFY_EVENT 'm'
+#define UNLINK_EVENT 'd'
+#define MAX_STORAGE_TARGETS 56
+#define TEST_BIT(x, i) ((x) & (1ULL << (i)))
+#define GET_P(loc) ((int)((loc) >> 56))
+#define P_MASK UINT64_C(0xFF00000000000000)
+#define L_MASK UINT64_C(0x00FFFFFFFFFFFFFF)
+#define WITH_P(loc, P) (((loc) & L_MASK) | (((uint64_t)(P) << 56) & P_MASK))
+#define NO_P UINT64_C(0xFF)
+#define P_IS_INVALID(loc) (GET_P(loc) == NO_P || TEST_BIT((loc), GET_P(loc)))
+#define DB_VERSION 1
+
+typedef struct {
+    int64_t timestamp;
+    uint64_t locations; /* bits 0..55 chunk holders, bits 56..63 parity target P */
+} FileInfo;
+
+/* progress_reporting.h:10-20 */
+typedef struct {
+    double dt;
+    size_t nfiles;
+    size_t bytes_read;
+    size_t bytes_written;
+    double total_time;
+    size_t total_nfiles;
+    size_t total_bytes_read;
+    size_t total_bytes_written;
+} ProgressSample;
+#define PROGRESS_SAMPLE_INIT {0.0, 0, 0, 0, 0.0, 0, 0, 0}
+
+typedef struct {
+    int read_dir;
+    int is_rebuilding;
+    int actual_P_st; /* only valid when rebuilding */
+    int tag;
+    ProgressSample *sample;
+} TaskInfo;
+
+/* task_processing.h:7-18 */
+typedef struct {
+    int storage_target;
+    int corrupt_files_fd;
+    int error;
+    const char *error_path;
+    int fd_null;
+    int fd_zero;
+    int write_dir;
+    int read_chunk_dir;
+    int read_parity_dir;
+    FILE *log;
+} HostState;
+
+/* storage target -> rank map, defined by the caller (gen/main.c:48,
+ * rebuild/main.c:34 define it the same way). */
+extern int st2rank[MAX_STORAGE_TARGETS];
+
+/* Returns non-zero if this rank took part in the task and it is not a delete
+ * task.  Errors are logged to hs->log and made sticky in hs->error. */
+int process_task(HostState *hs, const char *path, const FileInfo *fi, TaskInfo ti);
+
+/* ---- GPU binding of the P role ----------------------------------------- */
+/* Device used by the P role of storage target st: devices[st] if a map was
+ * given, else st % device_count.  Engines are created lazily, one per device. */
+int bcp_task_set_device_map(const int *devices, int ntargets);
+/* Release the engines and every lane's queues / staging (call after all
+ * lanes have joined). */
+int bcp_task_shutdown(void);
+/* Release the calling thread's queue and staging buffers. */
+void bcp_task_thread_release(void);
+
+/* Test injection point: when set, the P role calls fn instead of the GPU
+ * (host logic tests on machines without a GPU).  The product never sets it;
+ * every use is logged to hs->log. fn gets n rows of `pitch` bytes. */
+typedef int (*bcp_xor_hook_fn)(uint8_t *dst, size_t nbytes, const uint8_t *data, size_t pitch, int nsrc,
+                               void *ctx);
+void bcp_task_set_xor_hook(bcp_xor_hook_fn fn, void *ctx);
+
+/* ---- loopback rank transport (replaces the MPI subset of §2) ----------- */
+/* A world of `world_size` ranks inside this process.  Every thread acting
+ * for rank r calls bcp_lb_set_rank(r) first.  Semantics follow MPI
+ * point-to-point: blocking send (rendezvous: returns once a receiver has the
+ * data), non-blocking send (eager copy), posted receives matched in order by
+ * (source, tag), non-overtaking per (source, destination, tag). */
+typedef struct bcp_lb_req bcp_lb_req;
+int bcp_lb_init(int world_size);
+int bcp_lb_finalize(void);
+int bcp_lb_world_size(void);
+void bcp_lb_set_rank(int rank);
+int bcp_lb_rank(void);
+int bcp_lb_send(const void *buf, size_t n, int dst, int tag);
+int bcp_lb_recv(void *buf, size_t n, int src, int tag, size_t *received);
+int bcp_lb_isend(const void *buf, size_t n, int dst, int tag, bcp_lb_req **req);
+int bcp_lb_irecv(void *buf, size_t n, int src, int tag, bcp_lb_req **req);
+int bcp_lb_wait(bcp_lb_req *req, size_t *received);
+int bcp_lb_waitall(int n, bcp_lb_req **reqs);
+
+/* ---- callers: generation lanes and rebuild (loopback drivers) ---------- */
+typedef struct {
+    const char *path;   /* chunk path relative to <store>/chunks and /parity */
+    FileInfo fi;
+} bcp_work_item;
+
+typedef struct {
+    double seconds;
+    uint64_t tasks;            /* process_task calls that returned non-zero */
+    uint64_t bytes_read;       /* ProgressSample totals over every rank/lane */
+    uint64_t bytes_written;
+    int errors;                /* ranks that ended with a sticky error */
+} bcp_run_stats;
+
+/* Greedy lane assignment of gen/assign_lanes.c:12-46 (16-deep history per
+ * lane, tasks sharing targets kept apart).  Identical output to the
+ * reference on x86-64, including its int-shift of P. */
+void bcp_assign_lanes(int nlanes, uint64_t njobs, const FileInfo *jobs, int *lane);
+
+/* Parity generation over loopback ranks: storage target k (0..ntargets-1) is
+ * rank k+1 with store <root>/st<k>/{chunks,parity}; every rank runs nlanes
+ * lane threads that walk the same worklist (process_list, gen/main.c:116-164:
+ * own lane only, NO_P skipped, MPI tag = lane).  Lanes come from
+ * bcp_assign_lanes when lanes == NULL. */
+int bcp_gen_run(const char *store_root, int ntargets, const bcp_work_item *items, size_t nitems, int nlanes,
+                const int *lanes, FILE *log, bcp_run_stats *stats);
+
+/* Rebuild of one lost target over loopback ranks (do_file, rebuild/main.c:
+ * 40-89): items in DB key order, skip rules, re-roled locations, the
+ * P-holder reads <store>/parity, single lane with tag 0.  Survivors whose
+ * chunk mtime is newer than FileInfo.timestamp are appended (one path per
+ * line) to corrupt_list_path. */
+int bcp_rebuild_run(const char *store_root, int ntargets, int rebuild_target, const bcp_work_item *items,
+                    size_t nitems, const char *corrupt_list_path, FILE *log, bcp_run_stats *stats);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* BCP_TASK_H */

@@ -1,0 +1,90 @@
+"""The host protocol with the real GPU fold: process_task over loopback ranks
+(bcp_gen_run / bcp_rebuild_run), parity files compared with the oracle and
+the survey KATs, rebuilds compared with the lost chunks."""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+import bcp_store as S
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLD = json.load(open(os.path.join(HERE, "golden", "kats.json")))
+KiB = 1024
+
+
+@pytest.fixture(autouse=True)
+def gpu_fold(bcp, engine):
+    bcp.set_xor_hook(None)  # the product path: fold on the device
+    yield
+    bcp.task_shutdown()
+
+
+@pytest.mark.parametrize("name", ["KAT-2", "KAT-3", "KAT-4"])
+def test_survey_kats_end_to_end(bcp, oracle, tmp_path, name):
+    k = GOLD["survey_kats"][name]
+    n = len(k["lens"])
+    p = 8 if n == 8 else 4
+    nt = max(9, p + 1)
+    root = str(tmp_path)
+    S.make_store(root, nt)
+    chunks = [oracle.kat_chunk(i, L) for i, L in enumerate(k["lens"])]
+    for i, c in enumerate(chunks):
+        S.write_chunk(root, i, "a/b/chunk1", c)
+    items = [("a/b/chunk1", 2**40, S.with_p((1 << n) - 1, p))]
+    st = bcp.gen_run(root, nt, items)
+    assert st.errors == 0
+    pf = S.read_file(S.parity_path(root, p, "a/b/chunk1"))
+    assert len(pf) == k["file_len"] and hashlib.sha256(pf).hexdigest() == k["sha256"]
+    v = k["rebuild_victim"]
+    os.remove(S.chunk_path(root, v, "a/b/chunk1"))
+    st = bcp.rebuild_run(root, nt, v, items)
+    assert st.errors == 0
+    assert S.read_file(S.chunk_path(root, v, "a/b/chunk1")) == chunks[v].tobytes()
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_random_worklists_end_to_end(bcp, oracle, tmp_path, seed):
+    rng = np.random.default_rng(50 + seed)
+    ntargets = int(rng.integers(5, 14))
+    files = []
+    for i in range(60):
+        width = int(rng.integers(1, min(8, ntargets - 1) + 1))
+        holders, p = S.random_layout(rng, ntargets, width)
+        lens = [int(x) for x in rng.integers(0, 700_000, size=width)]
+        files.append((f"u{i % 7}/{i:04x}/chunk{i}", holders, p, lens))
+    root = str(tmp_path)
+    items, contents = S.populate(root, ntargets, files, seed=seed)
+    st = bcp.gen_run(root, ntargets, items, nlanes=12)
+    assert st.errors == 0
+    for (path, holders, p, lens) in files:
+        assert S.read_file(S.parity_path(root, p, path)) == oracle.gen_parity_file(contents[path]), path
+    victim = int(rng.integers(0, ntargets))
+    lost = {}
+    for (path, holders, p, lens) in files:
+        if victim in holders:
+            lost[path] = S.read_file(S.chunk_path(root, victim, path))
+            os.remove(S.chunk_path(root, victim, path))
+    st = bcp.rebuild_run(root, ntargets, victim, items)
+    assert st.errors == 0
+    for path, data in lost.items():
+        assert S.read_file(S.chunk_path(root, victim, path)) == data, path
+
+
+def test_config1_shape_small(bcp, oracle, tmp_path):
+    """Config 1's layout at reduced size: 4 targets, 3-wide stripes, P
+    rotating over the target left out, 512 KiB chunks."""
+    root = str(tmp_path)
+    files = []
+    for i in range(48):
+        p = i % 4
+        holders = [t for t in range(4) if t != p]
+        files.append((f"c1/f{i}", holders, p, [512 * KiB] * 3))
+    items, contents = S.populate(root, 4, files, seed=9)
+    st = bcp.gen_run(root, 4, items)
+    assert st.errors == 0 and st.tasks == 48 * 4
+    for (path, holders, p, lens) in files:
+        assert S.read_file(S.parity_path(root, p, path)) == oracle.gen_parity_file(contents[path])
