@@ -34,6 +34,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "beegfs-chunk-parity_amd"))
 
 import bcp_ctypes as bcp  # noqa: E402
+from bcp_dist import Dist  # noqa: E402
 
 KiB = 1024
 GiB = 1024 ** 3
@@ -58,43 +59,6 @@ def parse():
     return ap.parse_args()
 
 
-class Dist:
-    def __init__(self):
-        self.world = int(os.environ.get("WORLD_SIZE", "1"))
-        self.rank = int(os.environ.get("RANK", "0"))
-        self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-        self.pg = None
-        if self.world > 1:
-            import torch.distributed as dist
-            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-            dist.init_process_group("gloo", rank=self.rank, world_size=self.world)
-            self.pg = dist
-
-    def barrier(self):
-        if self.pg:
-            self.pg.barrier()
-
-    def max(self, x: float) -> float:
-        if not self.pg:
-            return x
-        import torch
-        t = torch.tensor([x], dtype=torch.float64)
-        self.pg.all_reduce(t, op=self.pg.ReduceOp.MAX)
-        return float(t.item())
-
-    def sum(self, x: float) -> float:
-        if not self.pg:
-            return x
-        import torch
-        t = torch.tensor([x], dtype=torch.float64)
-        self.pg.all_reduce(t, op=self.pg.ReduceOp.SUM)
-        return float(t.item())
-
-    def close(self):
-        if self.pg:
-            self.pg.destroy_process_group()
-
-
 def pmc_traffic(workload_key: str, kernel_tag: str):
     """Per-launch HBM bytes from the committed PMC summary, if it matches."""
     best = None
@@ -112,7 +76,9 @@ def pmc_traffic(workload_key: str, kernel_tag: str):
 def main():
     a = parse()
     d = Dist()
-    eng = bcp.Engine(d.local_rank)
+    ndev = bcp.device_count()
+    assert ndev > 0, "bench.py needs a HIP device (there is no CPU path)"
+    eng = bcp.Engine(d.local_rank % ndev)
     if a.blocks_per_cu or a.vecs:
         eng.tune(a.blocks_per_cu, a.vecs)
     cus, devname = eng.info()
