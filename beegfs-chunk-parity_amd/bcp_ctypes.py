@@ -45,6 +45,11 @@ class RunStats(ctypes.Structure):
                 ("bytes_written", ctypes.c_uint64), ("errors", ctypes.c_int)]
 
 
+class PipelineOpts(ctypes.Structure):
+    _fields_ = [("device", ctypes.c_int), ("slab_bytes", ctypes.c_size_t), ("io_threads", ctypes.c_int),
+                ("nslots", ctypes.c_int)]
+
+
 XOR_HOOK = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t,
                             ctypes.c_int, ctypes.c_void_p)
 
@@ -112,7 +117,21 @@ _SIGS = {
                      ctypes.POINTER(ctypes.c_int), _V, ctypes.POINTER(RunStats)], ctypes.c_int),
     "bcp_rebuild_run": ([ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.POINTER(WorkItem), ctypes.c_size_t,
                          ctypes.c_char_p, _V, ctypes.POINTER(RunStats)], ctypes.c_int),
+    "bcp_pipeline_gen": ([ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(WorkItem), ctypes.c_size_t,
+                          ctypes.POINTER(PipelineOpts), _V, ctypes.POINTER(RunStats)], ctypes.c_int),
     "bcp_lb_init": ([ctypes.c_int], ctypes.c_int),
+    "bcp_eventset_create": ([ctypes.POINTER(_V)], ctypes.c_int),
+    "bcp_eventset_destroy": ([_V], None),
+    "bcp_eventset_feed": ([_V, ctypes.c_int, _V, ctypes.c_size_t], ctypes.c_int),
+    "bcp_eventset_feed_file": ([_V, ctypes.c_int, ctypes.c_char_p], ctypes.c_int),
+    "bcp_eventset_count": ([_V], ctypes.c_size_t),
+    "bcp_eventset_get": ([_V, ctypes.c_size_t, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_int64),
+                          ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),
+                          ctypes.POINTER(ctypes.c_uint64)], ctypes.c_int),
+    "bcp_path_hash": ([ctypes.c_char_p, ctypes.c_size_t], ctypes.c_uint32),
+    "bcp_store_weight": ([ctypes.c_int], ctypes.c_int),
+    "bcp_plan_worklist": ([_V, ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(WorkItem), ctypes.c_size_t,
+                           ctypes.POINTER(WorkItem), ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
     "bcp_lb_finalize": ([], ctypes.c_int),
 }
 
@@ -349,6 +368,19 @@ def rebuild_run(store_root: str, ntargets: int, rebuild_target: int, items, corr
     return st
 
 
+def pipeline_gen(store_root: str, ntargets: int, items, device: int = 0, slab_bytes: int = 256 << 20,
+                 io_threads: int = 8, nslots: int = 3, log=None) -> RunStats:
+    """Batched end-to-end parity generation (bcp_pipeline_gen)."""
+    arr, keep = _items(items)
+    st = RunStats()
+    opts = PipelineOpts(device, slab_bytes, io_threads, nslots)
+    rc = lib().bcp_pipeline_gen(store_root.encode(), ntargets, arr, len(items), ctypes.byref(opts), log,
+                                ctypes.byref(st))
+    check("bcp_pipeline_gen", rc)
+    del keep
+    return st
+
+
 def set_xor_hook(fn_addr: int | None, ctx: int | None = None):
     """Test injection point: route the P role's fold to a C function (address)."""
     lib().bcp_task_set_xor_hook(_V(fn_addr) if fn_addr else None, _V(ctx) if ctx else None)
@@ -356,3 +388,65 @@ def set_xor_hook(fn_addr: int | None, ctx: int | None = None):
 
 def task_shutdown():
     call("bcp_task_shutdown")
+
+
+# ---------------------------------------------------------------------------
+# chunk-event records and worklist planning
+# ---------------------------------------------------------------------------
+def pack_records(records) -> bytes:
+    """records: (timestamp, size, event 'm'|'d', path) -> the binary stream
+    of bp-find-all-chunks/main.c:25-33."""
+    import struct
+    out = bytearray()
+    for ts, size, ev, path in records:
+        b = path.encode() if isinstance(path, str) else path
+        out += struct.pack("<qQQQ", ts, size, ord(ev), len(b)) + b
+    return bytes(out)
+
+
+class EventSet:
+    def __init__(self):
+        h = _V()
+        call("bcp_eventset_create", ctypes.byref(h))
+        self.h = h
+
+    def feed(self, st: int, data: bytes):
+        buf = ctypes.create_string_buffer(bytes(data), len(data))
+        call("bcp_eventset_feed", self.h, st, buf, len(data))
+
+    def feed_file(self, st: int, path: str):
+        call("bcp_eventset_feed_file", self.h, st, path.encode())
+
+    def __len__(self):
+        return lib().bcp_eventset_count(self.h)
+
+    def entries(self):
+        out = []
+        for i in range(len(self)):
+            p, ts, m, d, sz = ctypes.c_char_p(), ctypes.c_int64(), ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+            call("bcp_eventset_get", self.h, i, ctypes.byref(p), ctypes.byref(ts), ctypes.byref(m), ctypes.byref(d),
+                 ctypes.byref(sz))
+            out.append((p.value.decode(), ts.value, m.value, d.value, sz.value))
+        return out
+
+    def plan(self, ntargets: int, cum_weight, prev=()):
+        """prev: iterable of (path, timestamp, locations); returns [(path, timestamp, locations)]."""
+        prev = sorted(prev, key=lambda x: x[0].encode())
+        parr, keep = _items(prev)
+        cw = (ctypes.c_int * ntargets)(*cum_weight)
+        n = ctypes.c_size_t(0)
+        call("bcp_plan_worklist", self.h, ntargets, cw, parr, len(prev), None, 0, ctypes.byref(n))
+        out = (WorkItem * max(n.value, 1))()
+        call("bcp_plan_worklist", self.h, ntargets, cw, parr, len(prev), out, n.value, ctypes.byref(n))
+        del keep
+        return [(out[i].path.decode(), out[i].fi.timestamp, out[i].fi.locations) for i in range(n.value)]
+
+    def close(self):
+        if self.h:
+            lib().bcp_eventset_destroy(self.h)
+            self.h = None
+
+
+def path_hash(path: str) -> int:
+    b = path.encode()
+    return lib().bcp_path_hash(b, len(b))

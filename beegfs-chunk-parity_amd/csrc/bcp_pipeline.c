@@ -1,0 +1,619 @@
+/*
+ * bcp_pipeline.c -- batched end-to-end parity generation on one node.
+ *
+ * The per-task protocol (bcp_task.c) moves one stripe per round trip; this
+ * is the throughput form of the same computation for loopback stores, where
+ * every chunk file is local: stripes are batched into pinned slabs and the
+ * device does one descriptor-kernel launch per batch (SURVEY.md §7 "hard
+ * parts": batching vs the per-task interface).
+ *
+ *   readers (io thread pool)  chunk files -> pinned input slab   [slot s]
+ *   h2d queue                 pinned -> device slab, event H
+ *   compute queue             wait H, xor_desc over the batch, event K
+ *   d2h queue                 wait K, parity bodies -> pinned output slab, event D
+ *   writers (io thread pool)  wait D, parity files = u64 sizes[n] + body
+ *
+ * Slots are recycled round-robin, so batch b+1 is read while batch b is on
+ * the device and batch b-1 is being written; H2D and D2H run on their own
+ * queues beside the kernel (PCIe is full duplex).
+ *
+ * Output files are byte-identical to parity_generator's
+ * (task_processing.c:146-226): header in ascending storage-target order, then
+ * the windowed XOR (replay semantics past one 10 MiB window); a missing chunk
+ * counts as size 0 / zeros; an item with no holders unlinks its parity chunk.
+ */
+#define _GNU_SOURCE
+#include <errno.h>
+#include <fcntl.h>
+#include <pthread.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/stat.h>
+#include <sys/uio.h>
+#include <time.h>
+#include <unistd.h>
+
+#include "bcp_task.h"
+
+#define ROW 256u
+#define WINDOW ((uint64_t)BCP_WINDOW_BYTES)
+#define RUP(x) (((x) + ROW - 1) / ROW * ROW)
+
+static double now_s(void)
+{
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return (double)t.tv_sec + (double)t.tv_nsec * 1e-9;
+}
+
+/* ---- a small job pool --------------------------------------------------- */
+typedef struct job {
+    struct job *next;
+    void (*fn)(void *);
+    void *arg;
+} job;
+
+typedef struct {
+    pthread_mutex_t lock;
+    pthread_cond_t cv;
+    job *head, *tail;
+    int stop;
+    int nthreads;
+    pthread_t *th;
+} pool;
+
+static void *pool_main(void *p)
+{
+    pool *P = p;
+    for (;;) {
+        pthread_mutex_lock(&P->lock);
+        while (!P->head && !P->stop)
+            pthread_cond_wait(&P->cv, &P->lock);
+        job *j = P->head;
+        if (!j) {
+            pthread_mutex_unlock(&P->lock);
+            return NULL;
+        }
+        P->head = j->next;
+        if (!P->head)
+            P->tail = NULL;
+        pthread_mutex_unlock(&P->lock);
+        j->fn(j->arg);
+        free(j);
+    }
+}
+
+static int pool_start(pool *P, int n)
+{
+    memset(P, 0, sizeof(*P));
+    pthread_mutex_init(&P->lock, NULL);
+    pthread_cond_init(&P->cv, NULL);
+    P->th = calloc((size_t)n, sizeof(pthread_t));
+    if (!P->th)
+        return -ENOMEM;
+    for (int i = 0; i < n; i++) {
+        if (pthread_create(&P->th[i], NULL, pool_main, P) != 0)
+            return -EAGAIN;
+        P->nthreads++;
+    }
+    return 0;
+}
+
+static int pool_push(pool *P, void (*fn)(void *), void *arg)
+{
+    job *j = malloc(sizeof(*j));
+    if (!j)
+        return -ENOMEM;
+    j->fn = fn;
+    j->arg = arg;
+    j->next = NULL;
+    pthread_mutex_lock(&P->lock);
+    if (P->tail)
+        P->tail->next = j;
+    else
+        P->head = j;
+    P->tail = j;
+    pthread_cond_signal(&P->cv);
+    pthread_mutex_unlock(&P->lock);
+    return 0;
+}
+
+static void pool_stop(pool *P)
+{
+    pthread_mutex_lock(&P->lock);
+    P->stop = 1;
+    pthread_cond_broadcast(&P->cv);
+    pthread_mutex_unlock(&P->lock);
+    for (int i = 0; i < P->nthreads; i++)
+        pthread_join(P->th[i], NULL);
+    free(P->th);
+    pthread_mutex_destroy(&P->lock);
+    pthread_cond_destroy(&P->cv);
+}
+
+/* countdown latch */
+typedef struct {
+    pthread_mutex_t lock;
+    pthread_cond_t cv;
+    long left;
+} latch;
+
+static void latch_init(latch *l, long n)
+{
+    pthread_mutex_init(&l->lock, NULL);
+    pthread_cond_init(&l->cv, NULL);
+    l->left = n;
+}
+static void latch_down(latch *l)
+{
+    pthread_mutex_lock(&l->lock);
+    if (--l->left == 0)
+        pthread_cond_broadcast(&l->cv);
+    pthread_mutex_unlock(&l->lock);
+}
+static void latch_wait(latch *l)
+{
+    pthread_mutex_lock(&l->lock);
+    while (l->left > 0)
+        pthread_cond_wait(&l->cv, &l->lock);
+    pthread_mutex_unlock(&l->lock);
+}
+static void latch_destroy(latch *l)
+{
+    pthread_mutex_destroy(&l->lock);
+    pthread_cond_destroy(&l->cv);
+}
+
+/* ---- plan --------------------------------------------------------------- */
+typedef struct {
+    const char *path;
+    int p;                               /* parity target */
+    int n;                               /* holders */
+    int holders[MAX_STORAGE_TARGETS];
+    uint64_t size[MAX_STORAGE_TARGETS];  /* chunk sizes at stat time (0 = missing) */
+    uint64_t max_cs;
+    uint64_t in_off[MAX_STORAGE_TARGETS];/* offsets in the input slab */
+    uint64_t out_off;                    /* offset in the output slab */
+    int batch;
+} task;
+
+typedef struct {
+    const char *root;
+    task *t;
+    latch *done;
+} stat_arg;
+
+typedef struct {
+    uint8_t *h_in, *h_out;
+    void *d_in, *d_out;
+    size_t in_cap, out_cap;
+    bcp_event *ev_h, *ev_k, *ev_d;
+    latch reads, writes;
+    int busy;             /* writes of the previous batch pending */
+} slot;
+
+typedef struct {
+    const char *root;
+    task *t;
+    int k;
+    uint8_t *dst;
+    uint64_t *bytes;      /* accumulated under lock */
+    latch *done;
+} read_arg;
+
+typedef struct {
+    const char *root;
+    task *t;
+    const uint8_t *body;
+    latch *done;
+    FILE *log;
+    int *errors;
+} write_arg;
+
+typedef struct {
+    slot *S;
+    const char *root;
+    task *tasks;
+    size_t first, last;
+    pool *writers;
+    FILE *log;
+    int *errors;
+    int *dev_rc;
+} complete_arg;
+
+static pthread_mutex_t g_stat_lock = PTHREAD_MUTEX_INITIALIZER;
+
+static void chunk_file(char *buf, size_t cap, const char *root, int st, const char *dir, const char *path)
+{
+    snprintf(buf, cap, "%s/st%d/%s/%s", root, st, dir, path);
+}
+
+static void do_stat(void *p)
+{
+    stat_arg *a = p;
+    task *t = a->t;
+    char fn[4352];
+    t->max_cs = 0;
+    for (int k = 0; k < t->n; k++) {
+        chunk_file(fn, sizeof(fn), a->root, t->holders[k], "chunks", t->path);
+        struct stat st;
+        t->size[k] = stat(fn, &st) == 0 ? (uint64_t)st.st_size : 0;
+        if (t->size[k] > t->max_cs)
+            t->max_cs = t->size[k];
+    }
+    latch_down(a->done);
+}
+
+static void do_read(void *p)
+{
+    read_arg *a = p;
+    task *t = a->t;
+    uint64_t want = t->size[a->k], got = 0;
+    if (want) {
+        char fn[4352];
+        chunk_file(fn, sizeof(fn), a->root, t->holders[a->k], "chunks", t->path);
+        int fd = open(fn, O_RDONLY);
+        if (fd >= 0) {
+            posix_fadvise(fd, 0, 0, POSIX_FADV_SEQUENTIAL);
+            while (got < want) {
+                ssize_t r = read(fd, a->dst + got, (size_t)(want - got));
+                if (r <= 0)
+                    break;
+                got += (uint64_t)r;
+            }
+            close(fd);
+        }
+        /* a short read is zero padded, as chunk_sender does (:302-303) */
+        if (got < want)
+            memset(a->dst + got, 0, (size_t)(want - got));
+    }
+    pthread_mutex_lock(&g_stat_lock);
+    *a->bytes += got;
+    pthread_mutex_unlock(&g_stat_lock);
+    latch_down(a->done);
+    free(a);
+}
+
+static void mkdir_parents(char *fn)
+{
+    for (char *q = fn + 1; *q; q++)
+        if (*q == '/') {
+            *q = 0;
+            mkdir(fn, S_IRWXU);
+            *q = '/';
+        }
+}
+
+static void do_write(void *p)
+{
+    write_arg *a = p;
+    task *t = a->t;
+    char fn[4352];
+    chunk_file(fn, sizeof(fn), a->root, t->p, "parity", t->path);
+    mkdir_parents(fn);
+    int fd = open(fn, O_CREAT | O_WRONLY | O_TRUNC, S_IRUSR | S_IWUSR);
+    int bad = fd < 0;
+    if (!bad) {
+        uint64_t total = 8u * (uint64_t)t->n + t->max_cs;
+        posix_fallocate(fd, 0, (off_t)total);
+        struct iovec iov[2] = {{t->size, 8u * (size_t)t->n}, {(void *)a->body, (size_t)t->max_cs}};
+        uint64_t done = 0;
+        int idx = 0;
+        while (idx < 2 && !bad) {
+            ssize_t w = writev(fd, iov + idx, 2 - idx);
+            if (w <= 0) {
+                bad = 1;
+                break;
+            }
+            done += (uint64_t)w;
+            size_t left = (size_t)w;
+            while (idx < 2 && left >= iov[idx].iov_len) {
+                left -= iov[idx].iov_len;
+                idx++;
+            }
+            if (idx < 2) {
+                iov[idx].iov_base = (uint8_t *)iov[idx].iov_base + left;
+                iov[idx].iov_len -= left;
+            }
+        }
+        (void)done;
+        close(fd);
+    }
+    if (bad) {
+        pthread_mutex_lock(&g_stat_lock);
+        (*a->errors)++;
+        if (a->log)
+            fprintf(a->log, "bcp_pipeline: writing parity '%s' failed: %s\n", fn, strerror(errno));
+        pthread_mutex_unlock(&g_stat_lock);
+    }
+    latch_down(a->done);
+    free(a);
+}
+
+static void do_write(void *p);
+
+/* Completion stage (one thread, batches in order): wait for the batch's D2H,
+ * then hand its parity files to the writer pool. */
+static void do_complete(void *p)
+{
+    complete_arg *a = p;
+    int rc = bcp_event_sync(a->S->ev_d);
+    if (rc) {
+        pthread_mutex_lock(&g_stat_lock);
+        *a->dev_rc = rc;
+        pthread_mutex_unlock(&g_stat_lock);
+        for (size_t i = a->first; i < a->last; i++)
+            latch_down(&a->S->writes);
+    } else {
+        for (size_t i = a->first; i < a->last; i++) {
+            write_arg *w = malloc(sizeof(*w));
+            *w = (write_arg){a->root, &a->tasks[i], a->S->h_out + a->tasks[i].out_off, &a->S->writes, a->log,
+                             a->errors};
+            pool_push(a->writers, do_write, w);
+        }
+    }
+    free(a);
+}
+
+static int slot_alloc(bcp_engine *e, slot *s, size_t in_cap, size_t out_cap)
+{
+    int rc;
+    memset(s, 0, sizeof(*s));
+    if ((rc = bcp_host_alloc(e, in_cap, (void **)&s->h_in)) || (rc = bcp_host_alloc(e, out_cap, (void **)&s->h_out)) ||
+        (rc = bcp_dev_alloc(e, in_cap, &s->d_in)) || (rc = bcp_dev_alloc(e, out_cap, &s->d_out)) ||
+        (rc = bcp_event_create(e, &s->ev_h)) || (rc = bcp_event_create(e, &s->ev_k)) ||
+        (rc = bcp_event_create(e, &s->ev_d)))
+        return rc;
+    s->in_cap = in_cap;
+    s->out_cap = out_cap;
+    return 0;
+}
+
+static void slot_free(bcp_engine *e, slot *s)
+{
+    bcp_host_free(e, s->h_in);
+    bcp_host_free(e, s->h_out);
+    bcp_dev_free(e, s->d_in);
+    bcp_dev_free(e, s->d_out);
+    if (s->ev_h)
+        bcp_event_destroy(s->ev_h);
+    if (s->ev_k)
+        bcp_event_destroy(s->ev_k);
+    if (s->ev_d)
+        bcp_event_destroy(s->ev_d);
+}
+
+int bcp_pipeline_gen(const char *store_root, int ntargets, const bcp_work_item *items, size_t nitems,
+                     const bcp_pipeline_opts *opts_in, FILE *log, bcp_run_stats *stats)
+{
+    if (!store_root || ntargets < 1 || ntargets > MAX_STORAGE_TARGETS || (nitems && !items))
+        return -EINVAL;
+    bcp_pipeline_opts o = {0, 256u << 20, 8, 3};
+    if (opts_in)
+        o = *opts_in;
+    if (o.slab_bytes < (1u << 20))
+        o.slab_bytes = 1u << 20;
+    if (o.io_threads < 1)
+        o.io_threads = 1;
+    if (o.nslots < 2)
+        o.nslots = 2;
+    if (o.nslots > 8)
+        o.nslots = 8;
+
+    double t0 = now_s();
+    int rc = 0, errors = 0;
+    uint64_t bytes_read = 0, bytes_written = 0, ntasks = 0;
+
+    /* tasks: skip NO_P, unlink deletes now (no data moves for them) */
+    task *tasks = calloc(nitems ? nitems : 1, sizeof(task));
+    if (!tasks)
+        return -ENOMEM;
+    size_t nt = 0;
+    for (size_t i = 0; i < nitems; i++) {
+        uint64_t loc = items[i].fi.locations;
+        int P = GET_P(loc);
+        if ((uint64_t)P == NO_P)
+            continue;
+        if (P >= ntargets || TEST_BIT(loc, P) || ((loc & L_MASK) >> ntargets)) {
+            free(tasks);
+            return -EINVAL;
+        }
+        if ((loc & L_MASK) == 0) {
+            char fn[4352];
+            chunk_file(fn, sizeof(fn), store_root, P, "parity", items[i].path);
+            unlink(fn);
+            continue;
+        }
+        task *t = &tasks[nt++];
+        t->path = items[i].path;
+        t->p = P;
+        for (int k = 0; k < MAX_STORAGE_TARGETS; k++)
+            if (TEST_BIT(loc, k))
+                t->holders[t->n++] = k;
+    }
+
+    bcp_engine *eng = NULL;
+    bcp_queue *qh = NULL, *qk = NULL, *qd = NULL;
+    slot *slots = NULL;
+    pool readers, writers, completer;
+    int pools = 0, dev_rc = 0;
+    if ((rc = bcp_engine_create(o.device, &eng)))
+        goto out;
+    if ((rc = bcp_queue_create(eng, &qh)) || (rc = bcp_queue_create(eng, &qk)) || (rc = bcp_queue_create(eng, &qd)))
+        goto out;
+    if ((rc = pool_start(&readers, o.io_threads)) || (rc = pool_start(&writers, o.io_threads)) ||
+        (rc = pool_start(&completer, 1)))
+        goto out;
+    pools = 1;
+
+    /* 1. stat every chunk (parallel) */
+    {
+        latch l;
+        latch_init(&l, (long)nt);
+        stat_arg *args = calloc(nt ? nt : 1, sizeof(stat_arg));
+        if (!args) {
+            rc = -ENOMEM;
+            goto out;
+        }
+        for (size_t i = 0; i < nt; i++) {
+            args[i] = (stat_arg){store_root, &tasks[i], &l};
+            pool_push(&readers, do_stat, &args[i]);
+        }
+        latch_wait(&l);
+        latch_destroy(&l);
+        free(args);
+    }
+
+    /* 2. plan batches: inputs at 256-byte pitch, outputs likewise */
+    size_t in_cap = o.slab_bytes, out_cap = o.slab_bytes;
+    for (size_t i = 0; i < nt; i++) {
+        uint64_t in = 0;
+        for (int k = 0; k < tasks[i].n; k++)
+            in += RUP(tasks[i].size[k]);
+        if (in > in_cap)
+            in_cap = (size_t)in;
+        if (RUP(tasks[i].max_cs) > out_cap)
+            out_cap = (size_t)RUP(tasks[i].max_cs);
+    }
+    int nbatches = 0;
+    {
+        uint64_t in_used = 0, out_used = 0;
+        for (size_t i = 0; i < nt; i++) {
+            task *t = &tasks[i];
+            uint64_t in = 0;
+            for (int k = 0; k < t->n; k++)
+                in += RUP(t->size[k]);
+            if (i == 0 || in_used + in > in_cap || out_used + RUP(t->max_cs) > out_cap) {
+                nbatches++;
+                in_used = out_used = 0;
+            }
+            t->batch = nbatches - 1;
+            for (int k = 0; k < t->n; k++) {
+                t->in_off[k] = in_used;
+                in_used += RUP(t->size[k]);
+            }
+            t->out_off = out_used;
+            out_used += RUP(t->max_cs);
+        }
+    }
+
+    slots = calloc((size_t)o.nslots, sizeof(slot));
+    if (!slots) {
+        rc = -ENOMEM;
+        goto out;
+    }
+    for (int s = 0; s < o.nslots; s++)
+        if ((rc = slot_alloc(eng, &slots[s], in_cap, out_cap)))
+            goto out;
+
+    /* 3. stream the batches */
+    size_t first = 0;
+    bcp_stripe *st = malloc((nt ? nt : 1) * sizeof(bcp_stripe));
+    bcp_source *so = malloc((nt ? nt : 1) * MAX_STORAGE_TARGETS * sizeof(bcp_source));
+    if (!st || !so) {
+        free(st);
+        free(so);
+        rc = -ENOMEM;
+        goto out;
+    }
+    for (int b = 0; b < nbatches && !rc; b++) {
+        slot *S = &slots[b % o.nslots];
+        if (S->busy) { /* writes of batch b - nslots still running */
+            latch_wait(&S->writes);
+            latch_destroy(&S->writes);
+            S->busy = 0;
+        }
+        size_t last = first;
+        while (last < nt && tasks[last].batch == b)
+            last++;
+        /* read */
+        long nreads = 0;
+        for (size_t i = first; i < last; i++)
+            nreads += tasks[i].n;
+        latch_init(&S->reads, nreads);
+        uint64_t in_used = 0;
+        for (size_t i = first; i < last; i++)
+            for (int k = 0; k < tasks[i].n; k++) {
+                read_arg *a = malloc(sizeof(*a));
+                *a = (read_arg){store_root, &tasks[i], k, S->h_in + tasks[i].in_off[k], &bytes_read, &S->reads};
+                pool_push(&readers, do_read, a);
+                uint64_t end = tasks[i].in_off[k] + RUP(tasks[i].size[k]);
+                if (end > in_used)
+                    in_used = end;
+            }
+        latch_wait(&S->reads);
+        latch_destroy(&S->reads);
+        /* descriptors */
+        uint32_t ns = 0, nsrc = 0;
+        uint64_t out_used = 0;
+        for (size_t i = first; i < last; i++) {
+            task *t = &tasks[i];
+            st[ns] = (bcp_stripe){(uint64_t)S->d_out + t->out_off, t->max_cs, nsrc, (uint32_t)t->n,
+                                  t->max_cs > WINDOW ? WINDOW : 0};
+            for (int k = 0; k < t->n; k++)
+                so[nsrc++] = (bcp_source){(uint64_t)S->d_in + t->in_off[k], t->size[k]};
+            ns++;
+            if (t->out_off + RUP(t->max_cs) > out_used)
+                out_used = t->out_off + RUP(t->max_cs);
+        }
+        /* device: H2D (side queue) -> kernel -> D2H (side queue) */
+        if ((rc = bcp_h2d_async(qh, S->d_in, S->h_in, (size_t)in_used)) || (rc = bcp_event_record(S->ev_h, qh)) ||
+            (rc = bcp_queue_wait_event(qk, S->ev_h)) || (rc = bcp_xor_stripes_async(qk, st, ns, so, nsrc)) ||
+            (rc = bcp_event_record(S->ev_k, qk)) || (rc = bcp_queue_wait_event(qd, S->ev_k)) ||
+            (rc = bcp_d2h_async(qd, S->h_out, S->d_out, (size_t)out_used)) || (rc = bcp_event_record(S->ev_d, qd)))
+            break;
+        /* writers for this batch start once its D2H is done (completion
+         * thread); the host moves on to reading batch b+1 meanwhile */
+        latch_init(&S->writes, (long)(last - first));
+        S->busy = 1;
+        complete_arg *ca = malloc(sizeof(*ca));
+        *ca = (complete_arg){S, store_root, tasks, first, last, &writers, log, &errors, &dev_rc};
+        pool_push(&completer, do_complete, ca);
+        for (size_t i = first; i < last; i++)
+            bytes_written += 8u * (uint64_t)tasks[i].n + tasks[i].max_cs;
+        ntasks += last - first;
+        first = last;
+    }
+    free(st);
+    free(so);
+    for (int s = 0; s < o.nslots; s++)
+        if (slots[s].busy) {
+            latch_wait(&slots[s].writes);
+            latch_destroy(&slots[s].writes);
+            slots[s].busy = 0;
+        }
+
+    if (!rc && dev_rc)
+        rc = dev_rc;
+
+out:
+    if (pools) {
+        pool_stop(&readers);
+        pool_stop(&completer);
+        pool_stop(&writers);
+    }
+    if (slots) {
+        for (int s = 0; s < o.nslots; s++)
+            slot_free(eng, &slots[s]);
+        free(slots);
+    }
+    if (qh)
+        bcp_queue_destroy(qh);
+    if (qk)
+        bcp_queue_destroy(qk);
+    if (qd)
+        bcp_queue_destroy(qd);
+    if (eng)
+        bcp_engine_destroy(eng);
+    free(tasks);
+    if (stats) {
+        memset(stats, 0, sizeof(*stats));
+        stats->seconds = now_s() - t0;
+        stats->tasks = ntasks;
+        stats->bytes_read = bytes_read;
+        stats->bytes_written = bytes_written;
+        stats->errors = errors;
+    }
+    return rc;
+}

@@ -165,6 +165,50 @@ int bcp_gen_run(const char *store_root, int ntargets, const bcp_work_item *items
 int bcp_rebuild_run(const char *store_root, int ntargets, int rebuild_target, const bcp_work_item *items,
                     size_t nitems, const char *corrupt_list_path, FILE *log, bcp_run_stats *stats);
 
+/* ---- chunk-event records and worklist planning ------------------------- */
+/* Record stream per storage target (bp-find-all-chunks/main.c:25-33,
+ * gen-chunkmod-filelist.py:35-41): {i64 ts, u64 size, u64 event 'm'|'d',
+ * u64 len, char path[len]}, native-endian.  Events aggregate per path as
+ * fih_add_info does (gen/file_info_hash.c:24-31). */
+typedef struct bcp_eventset bcp_eventset;
+int bcp_eventset_create(bcp_eventset **out);
+void bcp_eventset_destroy(bcp_eventset *s);
+/* Feed bytes of target st's stream; a partial trailing record is carried. */
+int bcp_eventset_feed(bcp_eventset *s, int st, const void *buf, size_t len);
+int bcp_eventset_feed_file(bcp_eventset *s, int st, const char *path);
+size_t bcp_eventset_count(const bcp_eventset *s);
+int bcp_eventset_get(const bcp_eventset *s, size_t i, const char **path, int64_t *timestamp, uint64_t *modified,
+                     uint64_t *deleted, uint64_t *size);
+/* simple_hash of gen/main.c:67-74 (djb2 over signed chars). */
+uint32_t bcp_path_hash(const char *p, size_t len);
+/* get_store_weight of gen/main.c:403-427 for a store directory fd. */
+int bcp_store_weight(int dirfd);
+/* The worklist of one gen round (gen/main.c:703-715, 768-791): events in
+ * shuffled-then-size order; each merged with the previous state `prev`
+ * (sorted by path), deleted holders dropped, P chosen by select_P with the
+ * cumulative weights cum_weight[0..ntargets-1], NO_P when unchanged.
+ * out[i].path points into the event set.  *nout = number of events. */
+int bcp_plan_worklist(const bcp_eventset *s, int ntargets, const int *cum_weight, const bcp_work_item *prev,
+                      size_t nprev, bcp_work_item *out, size_t out_cap, size_t *nout);
+
+/* ---- batched end-to-end pipeline (loopback stores) ---------------------- */
+typedef struct {
+    int device;          /* HIP device */
+    size_t slab_bytes;   /* pinned / device slab per slot (grown to the largest stripe) */
+    int io_threads;      /* reader and writer threads (each) */
+    int nslots;          /* slabs in flight (2..8) */
+} bcp_pipeline_opts;
+
+/* Parity generation for local stores without per-task messaging: chunk
+ * files are read by io threads into pinned slabs, copied H2D on a side
+ * queue, folded by one descriptor-kernel launch per batch, copied D2H on
+ * another side queue and written as parity chunk files -- byte-identical
+ * to bcp_gen_run's (same header, padding and window replay).  NO_P items are
+ * skipped; items without holders unlink their parity chunk.  opts may be
+ * NULL ({0, 256 MiB, 8, 3}). */
+int bcp_pipeline_gen(const char *store_root, int ntargets, const bcp_work_item *items, size_t nitems,
+                     const bcp_pipeline_opts *opts, FILE *log, bcp_run_stats *stats);
+
 #ifdef __cplusplus
 }
 #endif

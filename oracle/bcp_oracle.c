@@ -53,6 +53,31 @@ void oracle_xor_parity(uint8_t *restrict dst, size_t nbytes,
 }
 
 /*
+ * xor_parity over rows `pitch` bytes apart, with the signature of libbcp's
+ * bcp_xor_hook_fn: lets tools time the protocol with the reference's CPU
+ * fold in place of the GPU (the "reference CPU path" of config 1).
+ */
+int oracle_xor_rows(uint8_t *dst, size_t nbytes, const uint8_t *data, size_t pitch, int nsrc, void *ctx)
+{
+    (void)ctx;
+    memcpy(dst, data, nbytes);
+    for (int s = 1; s < nsrc; s++) {
+        const uint8_t *src = data + (size_t)s * pitch;
+        size_t i = 0;
+        for (; i + 8 < nbytes; i += 8) {
+            uint64_t a, b;
+            memcpy(&a, dst + i, 8);
+            memcpy(&b, src + i, 8);
+            a ^= b;
+            memcpy(dst + i, &a, 8);
+        }
+        for (; i < nbytes; i++)
+            dst[i] ^= src[i];
+    }
+    return 0;
+}
+
+/*
  * One source's sender state: mirrors chunk_sender's loop
  * (task_processing.c:282-308).  `data` persists across windows; a window is
  * refilled only while data_sent < fd_size, so once the file is exhausted the

@@ -88,3 +88,40 @@ def test_config1_shape_small(bcp, oracle, tmp_path):
     assert st.errors == 0 and st.tasks == 48 * 4
     for (path, holders, p, lens) in files:
         assert S.read_file(S.parity_path(root, p, path)) == oracle.gen_parity_file(contents[path])
+
+
+# --------------------------------------------------------------------------
+# batched pipeline (bcp_pipeline_gen): same files as the per-task protocol
+# --------------------------------------------------------------------------
+@pytest.mark.parametrize("slab", [1 << 20, 64 << 20])
+def test_pipeline_matches_oracle_mixed_sizes(bcp, oracle, tmp_path, slab):
+    rng = np.random.default_rng(77)
+    ntargets = 10
+    files = []
+    for i in range(80):
+        width = int(rng.integers(1, 9))
+        holders, p = S.random_layout(rng, ntargets, width)
+        lens = [int(x) for x in np.exp(rng.uniform(np.log(64 * KiB), np.log(4 * 1024 * KiB), size=width))]
+        lens[0] = lens[0] + int(rng.integers(0, 15))     # not 16-byte rounded
+        files.append((f"m/{i % 9}/c{i}", holders, p, lens))
+    root = str(tmp_path)
+    items, contents = S.populate(root, ntargets, files, seed=5)
+    os.remove(S.chunk_path(root, files[3][1][0], files[3][0]))   # a missing chunk: size 0 / zeros
+    contents[files[3][0]][0] = None
+    st = bcp.pipeline_gen(root, ntargets, items, slab_bytes=slab, io_threads=4, nslots=3)
+    assert st.errors == 0 and st.tasks == len(files)
+    for (path, holders, p, lens) in files:
+        assert S.read_file(S.parity_path(root, p, path)) == oracle.gen_parity_file(contents[path]), path
+
+
+def test_pipeline_multiwindow_and_delete(bcp, oracle, tmp_path):
+    root = str(tmp_path)
+    files = [("big/a", [0, 1], 4, [10485760, 26214405]),
+             ("big/b", [1, 2, 3], 0, [21 * 1024 * KiB, 0, 10 * 1024 * KiB + 17]),
+             ("small", [0, 2], 3, [100, 5])]
+    items, contents = S.populate(root, 5, files, seed=6)
+    bcp.pipeline_gen(root, 5, items, slab_bytes=8 << 20)
+    for (path, holders, p, lens) in files:
+        assert S.read_file(S.parity_path(root, p, path)) == oracle.gen_parity_file(contents[path]), path
+    bcp.pipeline_gen(root, 5, [("small", 0, S.with_p(0, 3))])
+    assert not os.path.exists(S.parity_path(root, 3, "small"))

@@ -1,0 +1,219 @@
+#!/usr/bin/env python3
+"""End-to-end measurements (chunk files in host storage -> parity files).
+
+config 1 (BASELINE.json configs[0] shape): 4 storage targets as loopback
+  ranks, 3-wide stripes with P rotating over the target left out, 1333 files
+  -> ~1000 x 512 KiB chunk files per target.  Timed three ways over the same
+  files: the per-rank protocol with the GPU fold (bcp_gen_run), the same
+  protocol with the reference's CPU fold (oracle_xor_rows as the fold hook:
+  the "reference CPU XOR path"), and the batched pipeline (bcp_pipeline_gen).
+  Then target 2 is lost and rebuilt through bcp_rebuild_run.
+config 5: 9 targets, 8-wide stripes, chunk sizes log-uniform in
+  [64 KiB, 4 MiB] (not 16-byte rounded); full parity gen (pipeline), then a
+  seeded 10 % of stripes is rewritten, their chunk events are emitted as the
+  binary record streams of bp-find-all-chunks (one per target), parsed and
+  planned by bcp_eventset / bcp_plan_worklist, and only that subset is
+  recomputed by the pipeline (pinned H2D/D2H on side queues).
+
+Rates are (sum of chunk bytes read + parity bytes written) / wall time.  The
+stores are freshly written, so reads come from the page cache: these are
+host-memory + PCIe rates, not disk rates.  Prints one JSON line per
+measurement.
+"""
+import argparse
+import ctypes
+import json
+import os
+import shutil
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "beegfs-chunk-parity_amd"))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+import numpy as np  # noqa: E402
+
+import bcp_ctypes as bcp  # noqa: E402
+import bcp_store as S  # noqa: E402
+import oracle  # noqa: E402  (checker + CPU fold for the reference path)
+
+KiB, MiB, GiB = 1024, 1024 ** 2, 1024 ** 3
+
+
+def emit(**kw):
+    print(json.dumps(kw), flush=True)
+
+
+def total_bytes(root, files):
+    rd = sum(sum(lens) for _, _, _, lens in files)
+    wr = sum(8 * len(lens) + max(lens) for _, _, _, lens in files)
+    return rd, wr
+
+
+def verify(root, files, contents, sample, rng):
+    idx = rng.choice(len(files), size=min(sample, len(files)), replace=False)
+    for i in idx:
+        path, holders, p, lens = files[i]
+        got = S.read_file(S.parity_path(root, p, path))
+        if got != oracle.gen_parity_file(contents[path]):
+            return False, path
+    return True, None
+
+
+def write_store(root, files, seed):
+    """Chunk contents from a fast generator (one random block, rotated per chunk)."""
+    S.make_store(root, max(max(h) for _, h, _, _ in files) + 1 if files else 1)
+    rng = np.random.default_rng(seed)
+    block = rng.integers(0, 256, size=8 * MiB + 4096, dtype=np.uint8)
+    contents = {}
+    for i, (path, holders, p, lens) in enumerate(files):
+        arrs = []
+        for h, L in zip(holders, lens):
+            off = int(rng.integers(0, 4096))
+            data = block[off:off + L] if L <= 8 * MiB else rng.integers(0, 256, size=L, dtype=np.uint8)
+            S.write_chunk(root, h, path, data)
+            arrs.append(data)
+        contents[path] = arrs
+    return contents
+
+
+def config1(a):
+    root = os.path.join(a.root, "c1")
+    shutil.rmtree(root, ignore_errors=True)
+    files = []
+    for i in range(a.c1_files):
+        p = i % 4
+        holders = [t for t in range(4) if t != p]
+        files.append((f"u0/{i % 64:02X}/chunk{i}", holders, p, [512 * KiB] * 3))
+    t = time.time()
+    contents = write_store(root, files, 1)
+    emit(stage="config1_store_written", files=len(files), seconds=round(time.time() - t, 2))
+    items = [(path, 2 ** 40, S.with_p(sum(1 << h for h in holders), p)) for path, holders, p, _ in files]
+    rd, wr = total_bytes(root, files)
+    rng = np.random.default_rng(0)
+
+    def run(label, fn):
+        for p in range(4):
+            shutil.rmtree(os.path.join(root, f"st{p}", "parity"), ignore_errors=True)
+            os.makedirs(os.path.join(root, f"st{p}", "parity"))
+        t0 = time.perf_counter()
+        st = fn()
+        dt = time.perf_counter() - t0
+        ok, bad = verify(root, files, contents, a.verify, rng)
+        emit(config=1, path=label, seconds=round(dt, 3), GiBps=round((rd + wr) / dt / GiB, 3),
+             bytes_read=rd, bytes_written=wr, tasks=int(st.tasks), errors=int(st.errors), verified=ok, bad=bad)
+        return ok
+
+    ok = run("protocol_gpu_fold(bcp_gen_run,12 lanes)", lambda: bcp.gen_run(root, 4, items, nlanes=12))
+    ol = oracle.lib()
+    bcp.set_xor_hook(ctypes.cast(ol.oracle_xor_rows, ctypes.c_void_p).value)
+    try:
+        ok &= run("protocol_cpu_fold_reference(oracle_xor_rows,12 lanes)", lambda: bcp.gen_run(root, 4, items, nlanes=12))
+    finally:
+        bcp.set_xor_hook(None)
+    ok &= run("pipeline(bcp_pipeline_gen)", lambda: bcp.pipeline_gen(root, 4, items, io_threads=a.io_threads))
+    # rebuild target 2 through the protocol
+    lost = {}
+    for path, holders, p, _ in files:
+        if 2 in holders:
+            lost[path] = S.chunk_path(root, 2, path)
+            os.remove(lost[path])
+    t0 = time.perf_counter()
+    st = bcp.rebuild_run(root, 4, 2, items)
+    dt = time.perf_counter() - t0
+    good = 0
+    for k, (path, fn) in enumerate(lost.items()):
+        if k % max(1, len(lost) // a.verify) == 0:
+            holders = next(h for pth, h, _, _ in files if pth == path)
+            good += S.read_file(fn) == contents[path][holders.index(2)].tobytes()
+    rb_bytes = len(lost) * 3 * (512 * KiB) + len(lost) * 512 * KiB
+    emit(config=1, path="rebuild_protocol_gpu_fold(bcp_rebuild_run)", seconds=round(dt, 3),
+         GiBps=round(rb_bytes / dt / GiB, 3), rebuilt=len(lost), errors=int(st.errors), sampled_ok=good)
+    bcp.task_shutdown()
+    if not a.keep:
+        shutil.rmtree(root, ignore_errors=True)
+    return ok
+
+
+def config5(a):
+    root = os.path.join(a.root, "c5")
+    shutil.rmtree(root, ignore_errors=True)
+    rng = np.random.default_rng(5)
+    ntargets = 9
+    files = []
+    for i in range(a.c5_stripes):
+        holders, p = S.random_layout(rng, ntargets, 8)
+        lens = [int(x) for x in np.exp(rng.uniform(np.log(64 * KiB), np.log(4 * MiB), size=8))]
+        files.append((f"u{i % 8}/{(i * 2654435761) % 65536:04X}/chunk{i}", holders, p, lens))
+    t = time.time()
+    contents = write_store(root, files, 2)
+    emit(stage="config5_store_written", stripes=len(files), GiB=round(sum(sum(f[3]) for f in files) / GiB, 2),
+         seconds=round(time.time() - t, 2))
+    ts0 = 1_700_000_000
+    items = [(path, ts0, S.with_p(sum(1 << h for h in holders), p)) for path, holders, p, _ in files]
+    rd, wr = total_bytes(root, files)
+    t0 = time.perf_counter()
+    st = bcp.pipeline_gen(root, ntargets, items, io_threads=a.io_threads)
+    dt = time.perf_counter() - t0
+    ok, bad = verify(root, files, contents, a.verify, rng)
+    emit(config=5, path="pipeline_full_gen", seconds=round(dt, 3), GiBps=round((rd + wr) / dt / GiB, 3),
+         bytes_read=rd, bytes_written=wr, tasks=int(st.tasks), verified=ok, bad=bad)
+    # changelog: a seeded 10 % of stripes rewritten -> record streams per target
+    sub = sorted(int(x) for x in rng.choice(len(files), size=max(1, len(files) // 10), replace=False))
+    streams = {t: [] for t in range(ntargets)}
+    ts1 = ts0 + 3600
+    for i in sub:
+        path, holders, p, lens = files[i]
+        new = []
+        for h, L in zip(holders, lens):
+            data = rng.integers(0, 256, size=L, dtype=np.uint8)
+            S.write_chunk(root, h, path, data)
+            new.append(data)
+            streams[h].append((ts1, L, "m", path))
+        contents[path] = new
+    t0 = time.perf_counter()
+    es = bcp.EventSet()
+    for t, recs in streams.items():
+        es.feed(t, bcp.pack_records(recs))
+    cum = list(np.cumsum([1000] * ntargets))
+    planned = es.plan(ntargets, cum, prev=items)
+    dt_plan = time.perf_counter() - t0
+    # the planner keeps each stripe's P (fill_in_missing_fields) -> same targets
+    want = {files[i][0]: items[i][2] for i in sub}
+    plan_ok = len(planned) == len(sub) and all(loc == want[p] and ts == ts1 for p, ts, loc in planned)
+    sub_files = [files[i] for i in sub]
+    srd, swr = total_bytes(root, sub_files)
+    t0 = time.perf_counter()
+    st = bcp.pipeline_gen(root, ntargets, planned, io_threads=a.io_threads)
+    dt = time.perf_counter() - t0
+    ok2, bad2 = verify(root, sub_files, contents, a.verify, rng)
+    emit(config=5, path="changelog_subset_pipeline", stripes=len(sub), plan_seconds=round(dt_plan, 4),
+         plan_matches=plan_ok, seconds=round(dt, 3), GiBps=round((srd + swr) / dt / GiB, 3), bytes_read=srd,
+         bytes_written=swr, tasks=int(st.tasks), verified=ok2, bad=bad2)
+    es.close()
+    if not a.keep:
+        shutil.rmtree(root, ignore_errors=True)
+    return ok and ok2 and plan_ok
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--root", default=os.environ.get("TMPDIR", "/tmp") + "/bcp_e2e")
+    ap.add_argument("--configs", default="1,5")
+    ap.add_argument("--c1-files", type=int, default=1333)
+    ap.add_argument("--c5-stripes", type=int, default=1000)
+    ap.add_argument("--io-threads", type=int, default=8)
+    ap.add_argument("--verify", type=int, default=20)
+    ap.add_argument("--keep", action="store_true")
+    a = ap.parse_args()
+    ok = True
+    cfgs = a.configs.split(",")
+    if "1" in cfgs:
+        ok &= config1(a)
+    if "5" in cfgs:
+        ok &= config5(a)
+    sys.exit(0 if ok else 3)
+
+
+if __name__ == "__main__":
+    main()
