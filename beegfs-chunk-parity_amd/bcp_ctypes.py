@@ -119,6 +119,10 @@ _SIGS = {
                          ctypes.c_char_p, _V, ctypes.POINTER(RunStats)], ctypes.c_int),
     "bcp_pipeline_gen": ([ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(WorkItem), ctypes.c_size_t,
                           ctypes.POINTER(PipelineOpts), _V, ctypes.POINTER(RunStats)], ctypes.c_int),
+    "bcp_pipeline_create": ([ctypes.POINTER(PipelineOpts), ctypes.POINTER(_V)], ctypes.c_int),
+    "bcp_pipeline_run": ([_V, ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(WorkItem), ctypes.c_size_t, _V,
+                          ctypes.POINTER(RunStats)], ctypes.c_int),
+    "bcp_pipeline_destroy": ([_V], ctypes.c_int),
     "bcp_lb_init": ([ctypes.c_int], ctypes.c_int),
     "bcp_eventset_create": ([ctypes.POINTER(_V)], ctypes.c_int),
     "bcp_eventset_destroy": ([_V], None),
@@ -379,6 +383,28 @@ def pipeline_gen(store_root: str, ntargets: int, items, device: int = 0, slab_by
     check("bcp_pipeline_gen", rc)
     del keep
     return st
+
+
+class Pipeline:
+    """Long-lived batched pipeline (bcp_pipeline_create / run / destroy)."""
+
+    def __init__(self, device: int = 0, slab_bytes: int = 256 << 20, io_threads: int = 8, nslots: int = 3):
+        h = _V()
+        opts = PipelineOpts(device, slab_bytes, io_threads, nslots)
+        call("bcp_pipeline_create", ctypes.byref(opts), ctypes.byref(h))
+        self.h = h
+
+    def run(self, store_root: str, ntargets: int, items, log=None) -> RunStats:
+        arr, keep = _items(items)
+        st = RunStats()
+        call("bcp_pipeline_run", self.h, store_root.encode(), ntargets, arr, len(items), log, ctypes.byref(st))
+        del keep
+        return st
+
+    def close(self):
+        if self.h:
+            call("bcp_pipeline_destroy", self.h)
+            self.h = None
 
 
 def set_xor_hook(fn_addr: int | None, ctx: int | None = None):

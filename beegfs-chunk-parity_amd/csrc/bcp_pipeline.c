@@ -384,11 +384,77 @@ static void slot_free(bcp_engine *e, slot *s)
         bcp_event_destroy(s->ev_d);
 }
 
-int bcp_pipeline_gen(const char *store_root, int ntargets, const bcp_work_item *items, size_t nitems,
-                     const bcp_pipeline_opts *opts_in, FILE *log, bcp_run_stats *stats)
+struct bcp_pipeline {
+    bcp_pipeline_opts o;
+    bcp_engine *eng;
+    bcp_queue *qh, *qk, *qd;
+    pool readers, writers, completer;
+    int pools;
+    slot *slots;
+    size_t in_cap, out_cap;
+    bcp_stripe *st;
+    bcp_source *so;
+    size_t desc_cap;    /* stripes the descriptor arrays hold */
+};
+
+int bcp_pipeline_destroy(bcp_pipeline *pl)
 {
-    if (!store_root || ntargets < 1 || ntargets > MAX_STORAGE_TARGETS || (nitems && !items))
+    if (!pl)
         return -EINVAL;
+    if (pl->pools) {
+        pool_stop(&pl->readers);
+        pool_stop(&pl->completer);
+        pool_stop(&pl->writers);
+    }
+    if (pl->slots) {
+        for (int s = 0; s < pl->o.nslots; s++)
+            slot_free(pl->eng, &pl->slots[s]);
+        free(pl->slots);
+    }
+    if (pl->qh)
+        bcp_queue_destroy(pl->qh);
+    if (pl->qk)
+        bcp_queue_destroy(pl->qk);
+    if (pl->qd)
+        bcp_queue_destroy(pl->qd);
+    if (pl->eng)
+        bcp_engine_destroy(pl->eng);
+    free(pl->st);
+    free(pl->so);
+    free(pl);
+    return 0;
+}
+
+static int ensure_slots(bcp_pipeline *pl, size_t in_cap, size_t out_cap)
+{
+    if (pl->slots && in_cap <= pl->in_cap && out_cap <= pl->out_cap)
+        return 0;
+    if (pl->slots) {
+        for (int s = 0; s < pl->o.nslots; s++)
+            slot_free(pl->eng, &pl->slots[s]);
+        free(pl->slots);
+        pl->slots = NULL;
+    }
+    in_cap = in_cap > pl->in_cap ? in_cap : pl->in_cap;
+    out_cap = out_cap > pl->out_cap ? out_cap : pl->out_cap;
+    pl->slots = calloc((size_t)pl->o.nslots, sizeof(slot));
+    if (!pl->slots)
+        return -ENOMEM;
+    for (int s = 0; s < pl->o.nslots; s++) {
+        int rc = slot_alloc(pl->eng, &pl->slots[s], in_cap, out_cap);
+        if (rc)
+            return rc;
+    }
+    pl->in_cap = in_cap;
+    pl->out_cap = out_cap;
+    return 0;
+}
+
+int bcp_pipeline_create(const bcp_pipeline_opts *opts_in, bcp_pipeline **out)
+{
+    if (!out)
+        return -EINVAL;
+    *out = NULL;
     bcp_pipeline_opts o = {0, 256u << 20, 8, 3};
     if (opts_in)
         o = *opts_in;
@@ -396,15 +462,52 @@ int bcp_pipeline_gen(const char *store_root, int ntargets, const bcp_work_item *
         o.slab_bytes = 1u << 20;
     if (o.io_threads < 1)
         o.io_threads = 1;
+    if (o.io_threads > 64)
+        o.io_threads = 64;
     if (o.nslots < 2)
         o.nslots = 2;
     if (o.nslots > 8)
         o.nslots = 8;
+    bcp_pipeline *pl = calloc(1, sizeof(*pl));
+    if (!pl)
+        return -ENOMEM;
+    pl->o = o;
+    int rc;
+    if ((rc = bcp_engine_create(o.device, &pl->eng)) || (rc = bcp_queue_create(pl->eng, &pl->qh)) ||
+        (rc = bcp_queue_create(pl->eng, &pl->qk)) || (rc = bcp_queue_create(pl->eng, &pl->qd)))
+        goto fail;
+    if ((rc = pool_start(&pl->readers, o.io_threads)) || (rc = pool_start(&pl->writers, o.io_threads)) ||
+        (rc = pool_start(&pl->completer, 1)))
+        goto fail;
+    pl->pools = 1;
+    if ((rc = ensure_slots(pl, o.slab_bytes, o.slab_bytes)))
+        goto fail;
+    *out = pl;
+    return 0;
+fail:
+    bcp_pipeline_destroy(pl);
+    return rc;
+}
 
+int bcp_pipeline_run(bcp_pipeline *pl, const char *store_root, int ntargets, const bcp_work_item *items,
+                     size_t nitems, FILE *log, bcp_run_stats *stats)
+{
+    if (!pl || !store_root || ntargets < 1 || ntargets > MAX_STORAGE_TARGETS || (nitems && !items))
+        return -EINVAL;
+    const int nslots = pl->o.nslots;
     double t0 = now_s();
-    int rc = 0, errors = 0;
+    int rc = 0, errors = 0, dev_rc = 0;
     uint64_t bytes_read = 0, bytes_written = 0, ntasks = 0;
 
+    /* validate everything before touching any file */
+    for (size_t i = 0; i < nitems; i++) {
+        uint64_t loc = items[i].fi.locations;
+        int P = GET_P(loc);
+        if ((uint64_t)P == NO_P)
+            continue;
+        if (!items[i].path || P >= ntargets || TEST_BIT(loc, P) || ((loc & L_MASK) >> ntargets))
+            return -EINVAL;
+    }
     /* tasks: skip NO_P, unlink deletes now (no data moves for them) */
     task *tasks = calloc(nitems ? nitems : 1, sizeof(task));
     if (!tasks)
@@ -415,10 +518,6 @@ int bcp_pipeline_gen(const char *store_root, int ntargets, const bcp_work_item *
         int P = GET_P(loc);
         if ((uint64_t)P == NO_P)
             continue;
-        if (P >= ntargets || TEST_BIT(loc, P) || ((loc & L_MASK) >> ntargets)) {
-            free(tasks);
-            return -EINVAL;
-        }
         if ((loc & L_MASK) == 0) {
             char fn[4352];
             chunk_file(fn, sizeof(fn), store_root, P, "parity", items[i].path);
@@ -433,32 +532,19 @@ int bcp_pipeline_gen(const char *store_root, int ntargets, const bcp_work_item *
                 t->holders[t->n++] = k;
     }
 
-    bcp_engine *eng = NULL;
-    bcp_queue *qh = NULL, *qk = NULL, *qd = NULL;
-    slot *slots = NULL;
-    pool readers, writers, completer;
-    int pools = 0, dev_rc = 0;
-    if ((rc = bcp_engine_create(o.device, &eng)))
-        goto out;
-    if ((rc = bcp_queue_create(eng, &qh)) || (rc = bcp_queue_create(eng, &qk)) || (rc = bcp_queue_create(eng, &qd)))
-        goto out;
-    if ((rc = pool_start(&readers, o.io_threads)) || (rc = pool_start(&writers, o.io_threads)) ||
-        (rc = pool_start(&completer, 1)))
-        goto out;
-    pools = 1;
-
     /* 1. stat every chunk (parallel) */
     {
         latch l;
         latch_init(&l, (long)nt);
         stat_arg *args = calloc(nt ? nt : 1, sizeof(stat_arg));
         if (!args) {
-            rc = -ENOMEM;
-            goto out;
+            latch_destroy(&l);
+            free(tasks);
+            return -ENOMEM;
         }
         for (size_t i = 0; i < nt; i++) {
             args[i] = (stat_arg){store_root, &tasks[i], &l};
-            pool_push(&readers, do_stat, &args[i]);
+            pool_push(&pl->readers, do_stat, &args[i]);
         }
         latch_wait(&l);
         latch_destroy(&l);
@@ -466,7 +552,7 @@ int bcp_pipeline_gen(const char *store_root, int ntargets, const bcp_work_item *
     }
 
     /* 2. plan batches: inputs at 256-byte pitch, outputs likewise */
-    size_t in_cap = o.slab_bytes, out_cap = o.slab_bytes;
+    size_t in_cap = pl->in_cap, out_cap = pl->out_cap;
     for (size_t i = 0; i < nt; i++) {
         uint64_t in = 0;
         for (int k = 0; k < tasks[i].n; k++)
@@ -476,6 +562,12 @@ int bcp_pipeline_gen(const char *store_root, int ntargets, const bcp_work_item *
         if (RUP(tasks[i].max_cs) > out_cap)
             out_cap = (size_t)RUP(tasks[i].max_cs);
     }
+    if ((rc = ensure_slots(pl, in_cap, out_cap))) {
+        free(tasks);
+        return rc;
+    }
+    in_cap = pl->in_cap;
+    out_cap = pl->out_cap;
     int nbatches = 0;
     {
         uint64_t in_used = 0, out_used = 0;
@@ -497,28 +589,24 @@ int bcp_pipeline_gen(const char *store_root, int ntargets, const bcp_work_item *
             out_used += RUP(t->max_cs);
         }
     }
-
-    slots = calloc((size_t)o.nslots, sizeof(slot));
-    if (!slots) {
-        rc = -ENOMEM;
-        goto out;
+    if (pl->desc_cap < nt) {
+        free(pl->st);
+        free(pl->so);
+        pl->st = malloc((nt ? nt : 1) * sizeof(bcp_stripe));
+        pl->so = malloc((nt ? nt : 1) * MAX_STORAGE_TARGETS * sizeof(bcp_source));
+        pl->desc_cap = (pl->st && pl->so) ? nt : 0;
+        if (!pl->desc_cap) {
+            free(tasks);
+            return -ENOMEM;
+        }
     }
-    for (int s = 0; s < o.nslots; s++)
-        if ((rc = slot_alloc(eng, &slots[s], in_cap, out_cap)))
-            goto out;
+    bcp_stripe *st = pl->st;
+    bcp_source *so = pl->so;
 
-    /* 3. stream the batches */
+    /* 3. stream the batches through the slots */
     size_t first = 0;
-    bcp_stripe *st = malloc((nt ? nt : 1) * sizeof(bcp_stripe));
-    bcp_source *so = malloc((nt ? nt : 1) * MAX_STORAGE_TARGETS * sizeof(bcp_source));
-    if (!st || !so) {
-        free(st);
-        free(so);
-        rc = -ENOMEM;
-        goto out;
-    }
     for (int b = 0; b < nbatches && !rc; b++) {
-        slot *S = &slots[b % o.nslots];
+        slot *S = &pl->slots[b % nslots];
         if (S->busy) { /* writes of batch b - nslots still running */
             latch_wait(&S->writes);
             latch_destroy(&S->writes);
@@ -527,7 +615,6 @@ int bcp_pipeline_gen(const char *store_root, int ntargets, const bcp_work_item *
         size_t last = first;
         while (last < nt && tasks[last].batch == b)
             last++;
-        /* read */
         long nreads = 0;
         for (size_t i = first; i < last; i++)
             nreads += tasks[i].n;
@@ -537,14 +624,13 @@ int bcp_pipeline_gen(const char *store_root, int ntargets, const bcp_work_item *
             for (int k = 0; k < tasks[i].n; k++) {
                 read_arg *a = malloc(sizeof(*a));
                 *a = (read_arg){store_root, &tasks[i], k, S->h_in + tasks[i].in_off[k], &bytes_read, &S->reads};
-                pool_push(&readers, do_read, a);
+                pool_push(&pl->readers, do_read, a);
                 uint64_t end = tasks[i].in_off[k] + RUP(tasks[i].size[k]);
                 if (end > in_used)
                     in_used = end;
             }
         latch_wait(&S->reads);
         latch_destroy(&S->reads);
-        /* descriptors */
         uint32_t ns = 0, nsrc = 0;
         uint64_t out_used = 0;
         for (size_t i = first; i < last; i++) {
@@ -558,54 +644,33 @@ int bcp_pipeline_gen(const char *store_root, int ntargets, const bcp_work_item *
                 out_used = t->out_off + RUP(t->max_cs);
         }
         /* device: H2D (side queue) -> kernel -> D2H (side queue) */
-        if ((rc = bcp_h2d_async(qh, S->d_in, S->h_in, (size_t)in_used)) || (rc = bcp_event_record(S->ev_h, qh)) ||
-            (rc = bcp_queue_wait_event(qk, S->ev_h)) || (rc = bcp_xor_stripes_async(qk, st, ns, so, nsrc)) ||
-            (rc = bcp_event_record(S->ev_k, qk)) || (rc = bcp_queue_wait_event(qd, S->ev_k)) ||
-            (rc = bcp_d2h_async(qd, S->h_out, S->d_out, (size_t)out_used)) || (rc = bcp_event_record(S->ev_d, qd)))
+        if ((rc = bcp_h2d_async(pl->qh, S->d_in, S->h_in, (size_t)in_used)) ||
+            (rc = bcp_event_record(S->ev_h, pl->qh)) || (rc = bcp_queue_wait_event(pl->qk, S->ev_h)) ||
+            (rc = bcp_xor_stripes_async(pl->qk, st, ns, so, nsrc)) || (rc = bcp_event_record(S->ev_k, pl->qk)) ||
+            (rc = bcp_queue_wait_event(pl->qd, S->ev_k)) ||
+            (rc = bcp_d2h_async(pl->qd, S->h_out, S->d_out, (size_t)out_used)) ||
+            (rc = bcp_event_record(S->ev_d, pl->qd)))
             break;
-        /* writers for this batch start once its D2H is done (completion
-         * thread); the host moves on to reading batch b+1 meanwhile */
+        /* writers start once the batch's D2H is done (completion thread);
+         * the host moves on to reading batch b+1 meanwhile */
         latch_init(&S->writes, (long)(last - first));
         S->busy = 1;
         complete_arg *ca = malloc(sizeof(*ca));
-        *ca = (complete_arg){S, store_root, tasks, first, last, &writers, log, &errors, &dev_rc};
-        pool_push(&completer, do_complete, ca);
+        *ca = (complete_arg){S, store_root, tasks, first, last, &pl->writers, log, &errors, &dev_rc};
+        pool_push(&pl->completer, do_complete, ca);
         for (size_t i = first; i < last; i++)
             bytes_written += 8u * (uint64_t)tasks[i].n + tasks[i].max_cs;
         ntasks += last - first;
         first = last;
     }
-    free(st);
-    free(so);
-    for (int s = 0; s < o.nslots; s++)
-        if (slots[s].busy) {
-            latch_wait(&slots[s].writes);
-            latch_destroy(&slots[s].writes);
-            slots[s].busy = 0;
+    for (int s = 0; s < nslots; s++)
+        if (pl->slots[s].busy) {
+            latch_wait(&pl->slots[s].writes);
+            latch_destroy(&pl->slots[s].writes);
+            pl->slots[s].busy = 0;
         }
-
     if (!rc && dev_rc)
         rc = dev_rc;
-
-out:
-    if (pools) {
-        pool_stop(&readers);
-        pool_stop(&completer);
-        pool_stop(&writers);
-    }
-    if (slots) {
-        for (int s = 0; s < o.nslots; s++)
-            slot_free(eng, &slots[s]);
-        free(slots);
-    }
-    if (qh)
-        bcp_queue_destroy(qh);
-    if (qk)
-        bcp_queue_destroy(qk);
-    if (qd)
-        bcp_queue_destroy(qd);
-    if (eng)
-        bcp_engine_destroy(eng);
     free(tasks);
     if (stats) {
         memset(stats, 0, sizeof(*stats));
@@ -615,5 +680,17 @@ out:
         stats->bytes_written = bytes_written;
         stats->errors = errors;
     }
+    return rc;
+}
+
+int bcp_pipeline_gen(const char *store_root, int ntargets, const bcp_work_item *items, size_t nitems,
+                     const bcp_pipeline_opts *opts, FILE *log, bcp_run_stats *stats)
+{
+    bcp_pipeline *pl = NULL;
+    int rc = bcp_pipeline_create(opts, &pl);
+    if (rc)
+        return rc;
+    rc = bcp_pipeline_run(pl, store_root, ntargets, items, nitems, log, stats);
+    bcp_pipeline_destroy(pl);
     return rc;
 }

@@ -96,55 +96,77 @@ static int engine_for_target(int st, bcp_engine **out, int *device)
     return rc;
 }
 
-/* ---- per-lane resources (thread-local, reused across tasks) ------------- */
-typedef struct {
-    int device;
+/* ---- fold resources: a shared pool, reused across tasks, lanes and runs --
+ * One resource = one HIP queue + pinned window rows + device buffers.  The P
+ * role takes one for the duration of a task and gives it back, so a
+ * long-running rank pays queue creation and page pinning once, not per task
+ * or per lane thread.  Host-only resources (test hook) use plain memory. */
+typedef struct fold_res {
+    struct fold_res *next;
+    int device;         /* -1: host-only (hook) */
     bcp_engine *eng;
     bcp_queue *q;
-    uint8_t *h_win[2];  /* pinned window rows [n][pitch] */
-    uint8_t *h_par;     /* pinned fold output */
-    size_t h_cap, hp_cap;
-    int h_pinned;
+    uint8_t *h_win[2];  /* window rows [n][pitch] (pinned when device >= 0) */
+    uint8_t *h_par;     /* fold output */
+    size_t h_cap, h_cap1, hp_cap;
     void *d_src, *d_out;
     size_t d_cap, dout_cap;
+} fold_res;
+
+static fold_res *g_pool = NULL; /* free list, under g_lock */
+
+typedef struct {
     uint8_t *send_buf;  /* chunk_sender window buffer */
     size_t send_cap;
 } lane_res;
 
-static __thread lane_res t_res = {.device = -1};
+static __thread lane_res t_res;
 
-static void free_host(lane_res *L, void *p)
+static void host_free(fold_res *R, void *p)
 {
     if (!p)
         return;
-    if (L->h_pinned)
-        bcp_host_free(L->eng, p);
+    if (R->device >= 0)
+        bcp_host_free(R->eng, p);
     else
         free(p);
 }
 
+static void res_destroy(fold_res *R)
+{
+    host_free(R, R->h_win[0]);
+    host_free(R, R->h_win[1]);
+    host_free(R, R->h_par);
+    if (R->device >= 0) {
+        if (R->d_src)
+            bcp_dev_free(R->eng, R->d_src);
+        if (R->d_out)
+            bcp_dev_free(R->eng, R->d_out);
+        if (R->q)
+            bcp_queue_destroy(R->q);
+    }
+    free(R);
+}
+
 void bcp_task_thread_release(void)
 {
-    lane_res *L = &t_res;
-    free_host(L, L->h_win[0]);
-    free_host(L, L->h_win[1]);
-    free_host(L, L->h_par);
-    if (L->eng) {
-        if (L->d_src)
-            bcp_dev_free(L->eng, L->d_src);
-        if (L->d_out)
-            bcp_dev_free(L->eng, L->d_out);
-    }
-    if (L->q)
-        bcp_queue_destroy(L->q);
-    free(L->send_buf);
-    memset(L, 0, sizeof(*L));
-    L->device = -1;
+    free(t_res.send_buf);
+    t_res.send_buf = NULL;
+    t_res.send_cap = 0;
 }
 
 int bcp_task_shutdown(void)
 {
     bcp_task_thread_release();
+    pthread_mutex_lock(&g_lock);
+    fold_res *R = g_pool;
+    g_pool = NULL;
+    pthread_mutex_unlock(&g_lock);
+    while (R) {
+        fold_res *nx = R->next;
+        res_destroy(R);
+        R = nx;
+    }
     pthread_mutex_lock(&g_lock);
     for (int d = 0; d < MAX_DEVICES; d++) {
         if (g_engines[d])
@@ -156,86 +178,105 @@ int bcp_task_shutdown(void)
     return 0;
 }
 
-/* Window buffers for n rows of `pitch` plus a fold output of `nbytes`.
- * Pinned through the engine when the GPU folds, plain memory under the hook. */
-static int lane_windows(lane_res *L, HostState *hs, int use_gpu, size_t rows_bytes, size_t nbytes)
+static void res_release(fold_res *R)
 {
+    if (!R)
+        return;
+    pthread_mutex_lock(&g_lock);
+    R->next = g_pool;
+    g_pool = R;
+    pthread_mutex_unlock(&g_lock);
+}
+
+static int grow(fold_res *R, uint8_t **p, size_t *cap, size_t need)
+{
+    if (*cap >= need && *p)
+        return 0;
+    host_free(R, *p);
+    *p = NULL;
+    *cap = 0;
+    size_t c = MAX_(need, (size_t)1 << 20);
     int rc = 0;
-    if (use_gpu && (!L->eng || L->device < 0)) {
-        int dev = -1;
-        bcp_engine *e = NULL;
-        if ((rc = engine_for_target(hs->storage_target, &e, &dev)))
-            return rc;
-        if (L->eng && L->device != dev)
-            bcp_task_thread_release();
-        L->eng = e;
-        L->device = dev;
-    }
-    if (use_gpu && !L->q && (rc = bcp_queue_create(L->eng, &L->q)))
+    if (R->device >= 0)
+        rc = bcp_host_alloc(R->eng, c, (void **)p);
+    else if (!(*p = malloc(c)))
+        rc = -ENOMEM;
+    if (!rc)
+        *cap = c;
+    return rc;
+}
+
+static int grow_dev(fold_res *R, void **p, size_t *cap, size_t need)
+{
+    if (*cap >= need && *p)
+        return 0;
+    if (*p)
+        bcp_dev_free(R->eng, *p);
+    *p = NULL;
+    *cap = 0;
+    size_t c = MAX_(need, (size_t)1 << 20);
+    int rc = bcp_dev_alloc(R->eng, c, p);
+    if (!rc)
+        *cap = c;
+    return rc;
+}
+
+/* Take a resource for storage target st with room for rows_bytes of window
+ * rows and an nbytes fold output.  use_gpu = 0 under the test hook. */
+static int res_acquire(HostState *hs, int use_gpu, size_t rows_bytes, size_t nbytes, fold_res **out)
+{
+    int rc = 0, dev = -1;
+    bcp_engine *e = NULL;
+    *out = NULL;
+    if (use_gpu && (rc = engine_for_target(hs->storage_target, &e, &dev)))
         return rc;
-    int want_pinned = use_gpu;
-    if (L->h_cap && L->h_pinned != want_pinned) {
-        free_host(L, L->h_win[0]);
-        free_host(L, L->h_win[1]);
-        free_host(L, L->h_par);
-        L->h_win[0] = L->h_win[1] = L->h_par = NULL;
-        L->h_cap = L->hp_cap = 0;
-    }
-    L->h_pinned = want_pinned;
-    if (L->h_cap < rows_bytes) {
-        free_host(L, L->h_win[0]);
-        free_host(L, L->h_win[1]);
-        L->h_win[0] = L->h_win[1] = NULL;
-        L->h_cap = 0;
-        size_t cap = MAX_(rows_bytes, (size_t)1 << 20);
-        for (int i = 0; i < 2; i++) {
-            if (want_pinned)
-                rc = bcp_host_alloc(L->eng, cap, (void **)&L->h_win[i]);
-            else
-                L->h_win[i] = malloc(cap), rc = L->h_win[i] ? 0 : -ENOMEM;
-            if (rc)
-                return rc;
+    /* prefer a free resource of the same device that is already big enough */
+    pthread_mutex_lock(&g_lock);
+    fold_res **best = NULL;
+    for (fold_res **pp = &g_pool; *pp; pp = &(*pp)->next) {
+        if ((*pp)->device != dev)
+            continue;
+        if (!best)
+            best = pp;
+        if ((*pp)->h_cap >= rows_bytes && (*pp)->h_cap1 >= rows_bytes && (*pp)->hp_cap >= nbytes) {
+            best = pp;
+            break;
         }
-        L->h_cap = cap;
     }
-    if (L->hp_cap < nbytes || !L->h_par) {
-        free_host(L, L->h_par);
-        L->h_par = NULL;
-        size_t cap = MAX_(nbytes, (size_t)1 << 20);
-        if (want_pinned)
-            rc = bcp_host_alloc(L->eng, cap, (void **)&L->h_par);
-        else
-            L->h_par = malloc(cap), rc = L->h_par ? 0 : -ENOMEM;
-        if (rc)
+    fold_res *R = NULL;
+    if (best) {
+        R = *best;
+        *best = R->next;
+        R->next = NULL;
+    }
+    pthread_mutex_unlock(&g_lock);
+    if (!R) {
+        R = calloc(1, sizeof(*R));
+        if (!R)
+            return -ENOMEM;
+        R->device = dev;
+        R->eng = e;
+        if (use_gpu && (rc = bcp_queue_create(e, &R->q))) {
+            free(R);
             return rc;
-        L->hp_cap = cap;
-    }
-    if (use_gpu) {
-        if (L->d_cap < rows_bytes) {
-            if (L->d_src)
-                bcp_dev_free(L->eng, L->d_src);
-            L->d_src = NULL;
-            L->d_cap = 0;
-            if ((rc = bcp_dev_alloc(L->eng, MAX_(rows_bytes, (size_t)1 << 20), &L->d_src)))
-                return rc;
-            L->d_cap = MAX_(rows_bytes, (size_t)1 << 20);
-        }
-        if (L->dout_cap < nbytes || !L->d_out) {
-            if (L->d_out)
-                bcp_dev_free(L->eng, L->d_out);
-            L->d_out = NULL;
-            L->dout_cap = 0;
-            if ((rc = bcp_dev_alloc(L->eng, MAX_(nbytes, (size_t)1 << 20), &L->d_out)))
-                return rc;
-            L->dout_cap = MAX_(nbytes, (size_t)1 << 20);
         }
     }
+    if ((rc = grow(R, &R->h_win[0], &R->h_cap, rows_bytes)) || (rc = grow(R, &R->h_win[1], &R->h_cap1, rows_bytes)) ||
+        (rc = grow(R, &R->h_par, &R->hp_cap, nbytes)))
+        goto fail;
+    if (use_gpu && ((rc = grow_dev(R, &R->d_src, &R->d_cap, rows_bytes)) ||
+                    (rc = grow_dev(R, &R->d_out, &R->dout_cap, nbytes))))
+        goto fail;
+    *out = R;
     return 0;
+fail:
+    res_destroy(R);
+    return rc;
 }
 
 /* The fold of one window (replaces xor_parity at task_processing.c:211):
  * out = XOR of n rows of `pitch` bytes, nbytes each. */
-static int fold_window(lane_res *L, HostState *hs, bcp_xor_hook_fn hook, void *ctx, const uint8_t *rows,
+static int fold_window(fold_res *R, HostState *hs, bcp_xor_hook_fn hook, void *ctx, const uint8_t *rows,
                        size_t pitch, size_t nbytes, int n, uint8_t *out)
 {
     if (hook) {
@@ -247,14 +288,14 @@ static int fold_window(lane_res *L, HostState *hs, bcp_xor_hook_fn hook, void *c
         return hook(out, nbytes, rows, pitch, n, ctx);
     }
     int rc;
-    if ((rc = bcp_h2d_async(L->q, L->d_src, rows, pitch * (size_t)n)))
+    if ((rc = bcp_h2d_async(R->q, R->d_src, rows, pitch * (size_t)n)))
         return rc;
-    if ((rc = bcp_xor_strided_async(L->q, L->d_out, pitch, L->d_src, pitch * (size_t)n, pitch, 1, (uint32_t)n,
+    if ((rc = bcp_xor_strided_async(R->q, R->d_out, pitch, R->d_src, pitch * (size_t)n, pitch, 1, (uint32_t)n,
                                     nbytes)))
         return rc;
-    if ((rc = bcp_d2h_async(L->q, out, L->d_out, nbytes)))
+    if ((rc = bcp_d2h_async(R->q, out, R->d_out, nbytes)))
         return rc;
-    return bcp_queue_sync(L->q);
+    return bcp_queue_sync(R->q);
 }
 
 /* ---- file helpers (task_processing.c:29-79) ----------------------------- */
@@ -362,9 +403,9 @@ static void parity_generator(const char *path, const FileInfo *task, TaskInfo ti
     void *hook_ctx = g_hook_ctx;
     pthread_mutex_unlock(&g_lock);
 
-    lane_res *L = &t_res;
+    fold_res *L = NULL;
     int have_had_error = hs->error;
-    int res_rc = expected_messages ? lane_windows(L, hs, hook == NULL, pitch * (size_t)n, buffer_size) : 0;
+    int res_rc = expected_messages ? res_acquire(hs, hook == NULL, pitch * (size_t)n, buffer_size, &L) : 0;
     uint8_t *scratch = NULL; /* receive space if staging could not be set up */
     uint8_t *win_a, *win_b, *pblk;
     if (res_rc) {
@@ -445,6 +486,7 @@ static void parity_generator(const char *path, const FileInfo *task, TaskInfo ti
         hs->error_path = strdup(path);
     }
     free(scratch);
+    res_release(L);
     if (P_fd != hs->fd_null)
         close(P_fd);
 }

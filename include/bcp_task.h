@@ -208,6 +208,14 @@ typedef struct {
  * NULL ({0, 256 MiB, 8, 3}). */
 int bcp_pipeline_gen(const char *store_root, int ntargets, const bcp_work_item *items, size_t nitems,
                      const bcp_pipeline_opts *opts, FILE *log, bcp_run_stats *stats);
+/* The same as a long-lived object: engine, queues, io threads and pinned /
+ * device slabs are set up once and reused by every run (a resident service
+ * pays page pinning and stream creation once). */
+typedef struct bcp_pipeline bcp_pipeline;
+int bcp_pipeline_create(const bcp_pipeline_opts *opts, bcp_pipeline **out);
+int bcp_pipeline_run(bcp_pipeline *pl, const char *store_root, int ntargets, const bcp_work_item *items,
+                     size_t nitems, FILE *log, bcp_run_stats *stats);
+int bcp_pipeline_destroy(bcp_pipeline *pl);
 
 #ifdef __cplusplus
 }

@@ -125,3 +125,32 @@ def test_pipeline_multiwindow_and_delete(bcp, oracle, tmp_path):
         assert S.read_file(S.parity_path(root, p, path)) == oracle.gen_parity_file(contents[path]), path
     bcp.pipeline_gen(root, 5, [("small", 0, S.with_p(0, 3))])
     assert not os.path.exists(S.parity_path(root, 3, "small"))
+
+
+def test_pipeline_object_reuse_and_growth(bcp, oracle, tmp_path):
+    """One long-lived pipeline, several runs; the second needs bigger slabs."""
+    root = str(tmp_path)
+    small = [("s/a", [0, 1], 2, [5000, 7000]), ("s/b", [1, 2], 0, [64 * KiB, 3])]
+    big = [("b/a", [0, 1, 2], 3, [3 * 1024 * KiB, 2 * 1024 * KiB + 5, 1])]
+    it1, c1 = S.populate(root, 4, small, seed=1)
+    it2, c2 = S.populate(root, 4, big, seed=2)
+    pl = bcp.Pipeline(slab_bytes=1 << 20, io_threads=2, nslots=2)
+    try:
+        for items, files, contents in ((it1, small, c1), (it2, big, c2), (it1, small, c1)):
+            st = pl.run(root, 4, items)
+            assert st.errors == 0
+            for (path, holders, p, lens) in files:
+                assert S.read_file(S.parity_path(root, p, path)) == oracle.gen_parity_file(contents[path]), path
+    finally:
+        pl.close()
+
+
+def test_protocol_repeated_runs_reuse_pool(bcp, oracle, tmp_path):
+    root = str(tmp_path)
+    files = [(f"r/{i}", [0, 1, 2], 3, [100000 + i, 90000, 5]) for i in range(20)]
+    items, contents = S.populate(root, 4, files, seed=3)
+    for _ in range(3):
+        st = bcp.gen_run(root, 4, items, nlanes=4)
+        assert st.errors == 0
+    for (path, holders, p, lens) in files:
+        assert S.read_file(S.parity_path(root, p, path)) == oracle.gen_parity_file(contents[path])
