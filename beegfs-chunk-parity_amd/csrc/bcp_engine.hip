@@ -7,7 +7,9 @@
 //    queue, so twelve lanes overlap their copies and kernels on the device;
 //  * descriptor batches are staged through a per-queue ring of pinned slots
 //    so submission never synchronises with earlier work of the same queue;
-//  * grids are persistent: CUs x blocks_per_cu workgroups of 256 threads.
+//  * grids are persistent: CUs x blocks_per_cu workgroups of 256 threads;
+//    the streaming kernel takes tiles from a per-queue device work queue
+//    (monotone counter, base advanced on the host per launch).
 #include <errno.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -48,6 +50,8 @@ struct bcp_queue {
   hipStream_t stream = nullptr;
   DescSlot ring[kRingSlots];
   int next_slot = 0;
+  unsigned long long *qctr = nullptr;  // work-queue counter of xor_stream (device)
+  unsigned long long qbase = 0;        // its value when the next launch starts
   hipEvent_t timer[kTimerSlots] = {};
 };
 
@@ -162,7 +166,7 @@ extern "C" int bcp_engine_create(int device, bcp_engine **out) {
   if (e->tuning.blocks_per_cu < 1 || e->tuning.blocks_per_cu > 32) e->tuning.blocks_per_cu = defaults.blocks_per_cu;
   if (e->tuning.vecs_per_thread != 1 && e->tuning.vecs_per_thread != 2 && e->tuning.vecs_per_thread != 4)
     e->tuning.vecs_per_thread = defaults.vecs_per_thread;
-  if (const char *v = getenv("BCP_POLICY")) e->tuning.policy = atoi(v) & 7;
+  if (const char *v = getenv("BCP_SCHEDULE")) e->tuning.schedule = atoi(v) == kSchedStatic ? kSchedStatic : kSchedQueue;
   *out = e;
   return 0;
 }
@@ -186,7 +190,7 @@ extern "C" int bcp_set_option(bcp_engine *eng, const char *key, int value) {
   pthread_mutex_lock(&eng->lock);
   if (!strcmp(key, "blocks_per_cu") && value >= 1 && value <= 32) eng->tuning.blocks_per_cu = value;
   else if (!strcmp(key, "vecs_per_thread") && (value == 1 || value == 2 || value == 4)) eng->tuning.vecs_per_thread = value;
-  else if (!strcmp(key, "policy") && value >= 0 && value <= 7) eng->tuning.policy = value;
+  else if (!strcmp(key, "schedule") && (value == kSchedQueue || value == kSchedStatic)) eng->tuning.schedule = value;
   else rc = -EINVAL;
   pthread_mutex_unlock(&eng->lock);
   return rc;
@@ -216,7 +220,12 @@ extern "C" int bcp_queue_create(bcp_engine *eng, bcp_queue **out) {
   if (!q) return -ENOMEM;
   q->eng = eng;
   hipError_t e = hipStreamCreateWithFlags(&q->stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipMalloc(&q->qctr, 256);
+  if (e == hipSuccess) e = hipMemsetAsync(q->qctr, 0, 256, q->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(q->stream);
   if (e != hipSuccess) {
+    if (q->qctr) (void)hipFree(q->qctr);
+    if (q->stream) (void)hipStreamDestroy(q->stream);
     delete q;
     return hip_to_errno(e);
   }
@@ -235,6 +244,7 @@ extern "C" int bcp_queue_destroy(bcp_queue *q) {
   }
   for (auto &t : q->timer)
     if (t) (void)hipEventDestroy(t);
+  if (q->qctr) (void)hipFree(q->qctr);
   (void)hipStreamDestroy(q->stream);
   delete q;
   return 0;
@@ -393,6 +403,40 @@ extern "C" int bcp_memset_async(bcp_queue *q, void *dst, int value, size_t bytes
 // XOR submission
 // ---------------------------------------------------------------------------
 
+// Launch the streaming kernel on q (work-queue or static schedule).
+static int launch_stream(bcp_queue *q, bool gather, StreamArgs a, uint64_t ntiles) {
+  bcp_engine *e = q->eng;
+  if (ntiles == 0) return 0;
+  if (ntiles > 0xFFFFFFF0ull) return -EINVAL;
+  a.ntiles = (uint32_t)ntiles;
+  a.sched = e->tuning.schedule;
+  a.ctr = q->qctr;
+  a.base = q->qbase;
+  int grid = grid_for(e);
+  if ((uint64_t)grid > ntiles) grid = (int)ntiles;
+  HIP_RC(launch_xor_stream(q->stream, grid, e->tuning.vecs_per_thread, gather, a));
+  if (a.sched == kSchedQueue) q->qbase += ntiles + (uint64_t)grid;
+  return 0;
+}
+
+// A batch is uniform when every stripe has the same nsrc and out_len, every
+// source is at least out_len long (so neither zero padding nor window replay
+// can apply) and all addresses and the length are 16-byte multiples: then the
+// streaming kernel's pointer-table form computes it (rebuild's shape).
+static bool uniform_batch(const bcp_stripe *st, uint32_t nstripes, const bcp_source *so) {
+  const uint32_t n = st[0].nsrc;
+  const uint64_t len = st[0].out_len;
+  if (n == 0 || len == 0 || !aligned16(len) || len / 16 > 0xFFFFFFFFull) return false;
+  for (uint32_t i = 0; i < nstripes; i++) {
+    if (st[i].nsrc != n || st[i].out_len != len || !aligned16(st[i].dst)) return false;
+    for (uint32_t k = 0; k < n; k++) {
+      const bcp_source &x = so[st[i].first_src + k];
+      if (x.len < len || !aligned16(x.ptr)) return false;
+    }
+  }
+  return true;
+}
+
 // Submit a descriptor batch (host arrays) on q.
 static int submit_desc(bcp_queue *q, const bcp_stripe *stripes, uint32_t nstripes, const bcp_source *sources,
                        uint32_t nsources) {
@@ -413,6 +457,30 @@ static int submit_desc(bcp_queue *q, const bcp_stripe *stripes, uint32_t nstripe
   }
   if (ntiles == 0) return 0;
   if (ntiles > 0xFFFFFFF0ull) return -EINVAL;
+  if (uniform_batch(stripes, nstripes, sources)) {
+    const int sv = e->tuning.vecs_per_thread;
+    const uint64_t len = stripes[0].out_len;
+    const uint32_t tps = stream_tiles_per_stripe(len, sv);
+    const size_t off_src = ((size_t)nstripes * sizeof(bcp_stripe) + 15) & ~(size_t)15;
+    const size_t bytes = off_src + (size_t)nsources * sizeof(bcp_source);
+    DescSlot *slot = nullptr;
+    int rc = ring_acquire(q, bytes, &slot);
+    if (rc) return rc;
+    memcpy(slot->host, stripes, (size_t)nstripes * sizeof(bcp_stripe));
+    memcpy((char *)slot->host + off_src, sources, (size_t)nsources * sizeof(bcp_source));
+    HIP_RC(hipMemcpyAsync(slot->dev, slot->host, bytes, hipMemcpyHostToDevice, q->stream));
+    StreamArgs a{};
+    a.stripes = (const bcp_stripe *)slot->dev;
+    a.sources = (const bcp_source *)((char *)slot->dev + off_src);
+    a.vps = (uint32_t)(len / 16);
+    a.tps = tps;
+    a.nsrc = stripes[0].nsrc;
+    rc = launch_stream(q, true, a, (uint64_t)nstripes * tps);
+    if (rc) return rc;
+    HIP_RC(hipEventRecord(slot->done, q->stream));
+    slot->used = true;
+    return 0;
+  }
   const size_t off_src = (size_t)nstripes * sizeof(bcp_stripe);
   const size_t off_tiles = (off_src + (size_t)nsources * sizeof(bcp_source) + 15) & ~(size_t)15;
   const size_t bytes = off_tiles + ((size_t)nstripes + 1) * sizeof(uint32_t);
@@ -466,9 +534,16 @@ extern "C" int bcp_xor_strided_async(bcp_queue *q, void *dst, uint64_t dst_strid
                     aligned16(stripe_stride) && aligned16(src_stride) && aligned16(chunk_bytes) &&
                     chunk_bytes / 16 <= 0xFFFFFFFFull;
   if (fast) {
-    HIP_RC(launch_xor_strided_fast(q->stream, grid_for(e), e->tuning.vecs_per_thread, e->tuning.policy, (char *)dst, dst_stride,
-                                   (const char *)src, stripe_stride, src_stride, nstripes, nsrc, chunk_bytes));
-    return 0;
+    StreamArgs a{};
+    a.dst = (char *)dst;
+    a.dst_stride = dst_stride;
+    a.src = (const char *)src;
+    a.stripe_stride = stripe_stride;
+    a.src_stride = src_stride;
+    a.vps = (uint32_t)(chunk_bytes / 16);
+    a.tps = stream_tiles_per_stripe(chunk_bytes, e->tuning.vecs_per_thread);
+    a.nsrc = nsrc;
+    return launch_stream(q, false, a, nstripes * a.tps);
   }
   // General geometry: express as descriptors (any alignment / tail).
   if (nstripes * nsrc > 0xFFFFFFFFull || nstripes > 0xFFFFFFFFull) return -EINVAL;

@@ -13,18 +13,35 @@ namespace bcp {
 constexpr int kBlock = 256;        // threads per workgroup (4 waves of 64)
 constexpr int kMaxVecsPerThread = 4;
 
-// Fast-path policy bits (8-wide stripes only; other widths use 0).
-constexpr int kPolPlainLoad = 1;   // default-policy loads instead of non-temporal
-constexpr int kPolPlainStore = 2;  // default-policy stores instead of non-temporal
-constexpr int kPolContig = 4;      // contiguous tile range per workgroup instead of grid-stride
+// Tile schedules of the streaming kernel.
+constexpr int kSchedQueue = 0;   // device-wide work queue (default)
+constexpr int kSchedStatic = 1;  // contiguous tile range per workgroup (r01 design; A/B only)
 
-// Defaults from the r01 interleaved sweep on MI355X (profiles/r01/sweep_fast.jsonl):
-// 16 x 256-thread workgroups per CU (8 resident, the rest queue behind them),
-// 4 vectors per lane, contiguous tile runs, non-temporal loads and stores.
+// Defaults from the r01 interleaved sweeps on MI355X (profiles/r01/):
+// 8 x 256-thread workgroups per CU (7 resident at 68 VGPRs), 4 vectors per
+// lane, work-queue schedule, non-temporal loads and stores.
 struct Tuning {
-    int blocks_per_cu = 16;     // 256-thread workgroups launched per CU
+    int blocks_per_cu = 8;      // 256-thread workgroups launched per CU
     int vecs_per_thread = 4;    // 16-byte vectors per lane per tile
-    int policy = kPolContig;    // kPol* bits for the 8-wide fast path
+    int schedule = kSchedQueue; // kSched*
+};
+
+// Arguments of the streaming kernel (xor_stream).
+struct StreamArgs {
+    char *dst;                  // GATHER = 0: output of stripe s at dst + s*dst_stride
+    uint64_t dst_stride;
+    const char *src;            // GATHER = 0: source k of stripe s at src + s*stripe_stride + k*src_stride
+    uint64_t stripe_stride;
+    uint64_t src_stride;
+    const bcp_stripe *stripes;  // GATHER = 1: uniform descriptor batch (device copy)
+    const bcp_source *sources;
+    uint32_t vps;               // 16-byte vectors per stripe output
+    uint32_t tps;               // tiles per stripe
+    uint32_t ntiles;
+    uint32_t nsrc;
+    unsigned long long *ctr;    // work-queue counter (per queue)
+    unsigned long long base;    // counter value at the start of this launch
+    int sched;                  // kSched*
 };
 
 // Device-side form of one stripe descriptor batch.
@@ -38,11 +55,11 @@ struct DescBatch {
 };
 
 // Kernel launchers (bcp_kernels.hip).  All return hipError_t.
-hipError_t launch_xor_strided_fast(hipStream_t st, int grid, int vecs, int pol,
-                                   char *dst, uint64_t dst_stride,
-                                   const char *src, uint64_t stripe_stride,
-                                   uint64_t src_stride, uint64_t nstripes,
-                                   uint32_t nsrc, uint64_t chunk_bytes);
+// Streaming fold.  Consumes ntiles + grid counts of a.ctr when a.sched is
+// kSchedQueue; the caller clamps grid to [1, ntiles].
+hipError_t launch_xor_stream(hipStream_t st, int grid, int vecs, bool gather,
+                             const StreamArgs &a);
+uint32_t stream_tiles_per_stripe(uint64_t chunk_bytes, int vecs);
 hipError_t launch_xor_desc(hipStream_t st, int grid, int vecs,
                            const DescBatch &b);
 hipError_t launch_fill_synthetic(hipStream_t st, int grid, char *dst,

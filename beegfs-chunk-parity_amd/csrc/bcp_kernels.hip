@@ -6,10 +6,12 @@
 // (N loads + 1 store per output byte, no reuse), so the design rules are the
 // HBM ones: 16-byte lanes (global_load_dwordx4), every source load of a lane
 // issued before the XORs, non-temporal hints so the 8:1 read stream does not
-// churn L2/MALL, and a persistent grid sized to the CU count.
+// churn L2/MALL, and a device-wide tile queue that keeps the chip's loads in
+// one narrow ascending address window.
 //
 // Kernels:
-//   xor_strided_fast<NSRC,U>  uniform stripes, 16-B aligned geometry (hot path)
+//   xor_stream<NSRC,U,GATHER>  uniform stripes, 16-B aligned geometry (hot path;
+//                              strided or pointer-table addressing)
 //   xor_desc<U>               descriptor batches: variable lengths, zero pad,
 //                             rebuild truncation, window replay, any alignment
 //   fill_synthetic / xor_fold / compare   synthetic inputs and verification
@@ -24,86 +26,117 @@ __device__ __forceinline__ v4u ld_nt(const v4u *p) { return __builtin_nontempora
 __device__ __forceinline__ v4u zero4() { return v4u{0u, 0u, 0u, 0u}; }
 
 // ---------------------------------------------------------------------------
-// Fast path.  Stripe s, source k starts at src + s*stripe_stride + k*src_stride
-// and holds vps 16-byte vectors; output s at dst + s*dst_stride.  A tile is
-// kBlock*U vectors of one stripe.  Lane l of a tile owns vectors l, l+256, ...
-// so each wave-instruction moves 1 KiB contiguous per source, and all
-// NSRC*U loads of a lane are issued before its XORs.  NSRC == 0 means
-// "runtime nsrc".  POL selects the cache policy and the tile schedule
-// (kPolPlainLoad / kPolPlainStore / kPolContig bits, see bcp_internal.h).
+// Streaming fold (hot path).  A tile is kBlock*U 16-byte vectors of one
+// stripe's output (16 KiB at U = 4); wave w of the workgroup owns the
+// contiguous run [w*64*U, (w+1)*64*U) of the tile, lane l vectors l, l+64, ...
+// so each wave streams 4 KiB contiguous per source and every NSRC*U load of a
+// lane is independent of the others.
+//
+// Tile schedule (r01 sweeps, profiles/r01/exp*.jsonl): a device-wide work
+// queue.  Thread 0 of a workgroup takes the next tile index with one atomic
+// per tile, so the tiles in flight on the whole chip are always a narrow,
+// ascending address window (~56 stripes at config 2).  In the interleaved r01
+// sweeps that schedule (with wave-contiguous lanes) beat per-workgroup
+// contiguous tile runs by 12-14 % on the same box.
+// The counter is monotone: launch k starts at `base`, every tile index
+// handed out is atomicAdd(ctr, 1) - base, and each workgroup makes exactly one
+// failing grab, so a launch consumes ntiles + grid counts and the host
+// advances base by that (no reset between launches).
+//
+// Addressing: GATHER = 0 -> source k of stripe s at src + s*stripe_stride +
+// k*src_stride, output at dst + s*dst_stride.  GATHER = 1 -> pointers from a
+// descriptor batch whose stripes are uniform (same nsrc, out_len, every
+// source at least out_len long, all 16-byte aligned) -- the rebuild shape.
+// NSRC == 0 means "runtime nsrc".
 // ---------------------------------------------------------------------------
-template <int POL>
-__device__ __forceinline__ v4u ld_pol(const v4u *p) {
-  if constexpr (POL & kPolPlainLoad) return *p;
-  else return __builtin_nontemporal_load(p);
-}
-template <int POL>
-__device__ __forceinline__ void st_pol(v4u *p, v4u v) {
-  if constexpr (POL & kPolPlainStore) *p = v;
-  else __builtin_nontemporal_store(v, p);
+template <int U>
+__device__ __forceinline__ uint32_t tile_vec(uint32_t tin, int u) {
+  return tin * (uint32_t)(kBlock * U) + (threadIdx.x >> 6) * (64u * U) + (uint32_t)u * 64u + (threadIdx.x & 63u);
 }
 
-template <int NSRC, int U, int POL>
-__device__ __forceinline__ void fast_tile(char *__restrict__ dst, uint64_t dst_stride, const char *__restrict__ src,
-                                          uint64_t stripe_stride, uint64_t src_stride, uint32_t vps, uint32_t tps,
-                                          uint32_t nsrc, uint32_t t) {
-  constexpr uint32_t tile_v = kBlock * U;
-  const uint32_t s = t / tps;
-  const uint32_t tin = t - s * tps;
-  const char *sb = src + (uint64_t)s * stripe_stride;
-  v4u *db = reinterpret_cast<v4u *>(dst + (uint64_t)s * dst_stride);
-  const uint32_t v0 = tin * tile_v + threadIdx.x;
+template <int NSRC, int U, int GATHER>
+__device__ __forceinline__ void stream_tile(const StreamArgs &a, uint32_t t) {
+  const uint32_t nsrc = NSRC > 0 ? (uint32_t)NSRC : a.nsrc;
+  const uint32_t s = t / a.tps;
+  const uint32_t tin = t - s * a.tps;
+  const char *sb = nullptr;
+  const bcp_source *sl = nullptr;
+  v4u *db;
+  if constexpr (GATHER) {
+    const bcp_stripe d = a.stripes[s];
+    sl = a.sources + d.first_src;
+    db = reinterpret_cast<v4u *>(d.dst);
+  } else {
+    sb = a.src + (uint64_t)s * a.stripe_stride;
+    db = reinterpret_cast<v4u *>(a.dst + (uint64_t)s * a.dst_stride);
+  }
+  auto src_k = [&](uint32_t k) -> const v4u * {
+    if constexpr (GATHER) return reinterpret_cast<const v4u *>(sl[k].ptr);
+    else return reinterpret_cast<const v4u *>(sb + (uint64_t)k * a.src_stride);
+  };
   v4u acc[U];
-  if (tin * tile_v + tile_v <= vps) {
-    const v4u *p0 = reinterpret_cast<const v4u *>(sb) + v0;
+  if ((tin + 1) * (uint32_t)(kBlock * U) <= a.vps) {
+    const v4u *p0 = src_k(0);
 #pragma unroll
-    for (int u = 0; u < U; u++) acc[u] = ld_pol<POL>(p0 + u * kBlock);
+    for (int u = 0; u < U; u++) acc[u] = ld_nt(p0 + tile_vec<U>(tin, u));
     if constexpr (NSRC > 0) {
 #pragma unroll
       for (int k = 1; k < NSRC; k++) {
-        const v4u *pk = reinterpret_cast<const v4u *>(sb + k * src_stride) + v0;
+        const v4u *pk = src_k(k);
 #pragma unroll
-        for (int u = 0; u < U; u++) acc[u] ^= ld_pol<POL>(pk + u * kBlock);
+        for (int u = 0; u < U; u++) acc[u] ^= ld_nt(pk + tile_vec<U>(tin, u));
       }
     } else {
 #pragma unroll 4
       for (uint32_t k = 1; k < nsrc; k++) {
-        const v4u *pk = reinterpret_cast<const v4u *>(sb + k * src_stride) + v0;
+        const v4u *pk = src_k(k);
 #pragma unroll
-        for (int u = 0; u < U; u++) acc[u] ^= ld_pol<POL>(pk + u * kBlock);
+        for (int u = 0; u < U; u++) acc[u] ^= ld_nt(pk + tile_vec<U>(tin, u));
       }
     }
 #pragma unroll
-    for (int u = 0; u < U; u++) st_pol<POL>(db + v0 + u * kBlock, acc[u]);
+    for (int u = 0; u < U; u++) __builtin_nontemporal_store(acc[u], db + tile_vec<U>(tin, u));
   } else {
     // Last, partial tile of a stripe: per-vector bounds.
 #pragma unroll
     for (int u = 0; u < U; u++) {
-      const uint32_t v = v0 + u * kBlock;
-      if (v < vps) {
-        v4u a = ld_pol<POL>(reinterpret_cast<const v4u *>(sb) + v);
-        for (uint32_t k = 1; k < nsrc; k++) a ^= ld_pol<POL>(reinterpret_cast<const v4u *>(sb + k * src_stride) + v);
-        st_pol<POL>(db + v, a);
+      const uint32_t v = tile_vec<U>(tin, u);
+      if (v < a.vps) {
+        v4u x = ld_nt(src_k(0) + v);
+        for (uint32_t k = 1; k < nsrc; k++) x ^= ld_nt(src_k(k) + v);
+        __builtin_nontemporal_store(x, db + v);
       }
     }
   }
 }
 
-template <int NSRC, int U, int POL>
-__global__ __launch_bounds__(kBlock) void xor_strided_fast(
-    char *__restrict__ dst, uint64_t dst_stride, const char *__restrict__ src,
-    uint64_t stripe_stride, uint64_t src_stride, uint32_t vps, uint32_t tps,
-    uint32_t ntiles, uint32_t nsrc_rt) {
-  const uint32_t nsrc = NSRC > 0 ? (uint32_t)NSRC : nsrc_rt;
-  if constexpr (POL & kPolContig) {
-    // Workgroup b owns tiles [b*T/G, (b+1)*T/G): one contiguous run each.
-    const uint32_t t0 = (uint32_t)(((uint64_t)blockIdx.x * ntiles) / gridDim.x);
-    const uint32_t t1 = (uint32_t)(((uint64_t)(blockIdx.x + 1) * ntiles) / gridDim.x);
-    for (uint32_t t = t0; t < t1; t++)
-      fast_tile<NSRC, U, POL>(dst, dst_stride, src, stripe_stride, src_stride, vps, tps, nsrc, t);
-  } else {
-    for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x)
-      fast_tile<NSRC, U, POL>(dst, dst_stride, src, stripe_stride, src_stride, vps, tps, nsrc, t);
+__device__ __forceinline__ uint32_t queue_grab(unsigned long long *ctr, unsigned long long base) {
+  const unsigned long long v = atomicAdd(ctr, 1ull) - base;
+  return v > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)v;
+}
+
+template <int NSRC, int U, int GATHER>
+__global__ __launch_bounds__(kBlock) void xor_stream(StreamArgs a) {
+  if (a.sched == kSchedStatic) {
+    // Workgroup b owns tiles [b*T/G, (b+1)*T/G) (the r01 schedule; A/B only).
+    const uint32_t t0 = (uint32_t)(((uint64_t)blockIdx.x * a.ntiles) / gridDim.x);
+    const uint32_t t1 = (uint32_t)(((uint64_t)(blockIdx.x + 1) * a.ntiles) / gridDim.x);
+    for (uint32_t t = t0; t < t1; t++) stream_tile<NSRC, U, GATHER>(a, t);
+    return;
+  }
+  // Two LDS slots: thread 0 writes slot i+1 only after the barrier that
+  // every wave reaches after reading slot i, so one barrier per tile is enough.
+  __shared__ uint32_t next[2];
+  if (threadIdx.x == 0) next[0] = queue_grab(a.ctr, a.base);
+  __syncthreads();
+  uint32_t t = __builtin_amdgcn_readfirstlane(next[0]);
+  int slot = 0;
+  while (t < a.ntiles) {
+    stream_tile<NSRC, U, GATHER>(a, t);
+    slot ^= 1;
+    if (threadIdx.x == 0) next[slot] = queue_grab(a.ctr, a.base);
+    __syncthreads();
+    t = __builtin_amdgcn_readfirstlane(next[slot]);
   }
 }
 
@@ -336,61 +369,45 @@ __global__ __launch_bounds__(kBlock) void compare_bytes(const unsigned char *a, 
 // ---------------------------------------------------------------------------
 // Launchers.
 // ---------------------------------------------------------------------------
-template <int NSRC, int U, int POL>
-static hipError_t launch_fast_nu(hipStream_t st, int grid, char *dst, uint64_t dst_stride, const char *src,
-                                 uint64_t stripe_stride, uint64_t src_stride, uint32_t vps, uint32_t tps,
-                                 uint32_t ntiles, uint32_t nsrc) {
-  hipLaunchKernelGGL((xor_strided_fast<NSRC, U, POL>), dim3(grid), dim3(kBlock), 0, st, dst, dst_stride, src,
-                     stripe_stride, src_stride, vps, tps, ntiles, nsrc);
+template <int NSRC, int U, int GATHER>
+static hipError_t launch_stream_nu(hipStream_t st, int grid, const StreamArgs &a) {
+  hipLaunchKernelGGL((xor_stream<NSRC, U, GATHER>), dim3(grid), dim3(kBlock), 0, st, a);
   return hipGetLastError();
 }
 
-// The hot 8-wide stripe gets every policy variant; other widths use the
-// default policy (non-temporal loads and stores, grid-stride tiles).
-template <int U>
-static hipError_t launch_fast_u(hipStream_t st, int grid, int pol, char *dst, uint64_t dst_stride, const char *src,
-                                uint64_t stripe_stride, uint64_t src_stride, uint32_t vps, uint32_t tps,
-                                uint32_t ntiles, uint32_t nsrc) {
-#define BCP_ARGS st, grid, dst, dst_stride, src, stripe_stride, src_stride, vps, tps, ntiles, nsrc
+template <int U, int GATHER>
+static hipError_t launch_stream_u(hipStream_t st, int grid, const StreamArgs &a) {
 #define BCP_NSRC_CASE(n) \
-  case n: return launch_fast_nu<n, U, 0>(BCP_ARGS);
-  if (nsrc == 8) {
-    switch (pol & 7) {
-      case 1: return launch_fast_nu<8, U, 1>(BCP_ARGS);
-      case 2: return launch_fast_nu<8, U, 2>(BCP_ARGS);
-      case 3: return launch_fast_nu<8, U, 3>(BCP_ARGS);
-      case 4: return launch_fast_nu<8, U, 4>(BCP_ARGS);
-      case 5: return launch_fast_nu<8, U, 5>(BCP_ARGS);
-      case 6: return launch_fast_nu<8, U, 6>(BCP_ARGS);
-      case 7: return launch_fast_nu<8, U, 7>(BCP_ARGS);
-      default: return launch_fast_nu<8, U, 0>(BCP_ARGS);
-    }
-  }
-  switch (nsrc) {
+  case n: return launch_stream_nu<n, U, GATHER>(st, grid, a);
+  switch (a.nsrc) {
     BCP_NSRC_CASE(1) BCP_NSRC_CASE(2) BCP_NSRC_CASE(3) BCP_NSRC_CASE(4) BCP_NSRC_CASE(5)
-    BCP_NSRC_CASE(6) BCP_NSRC_CASE(7) BCP_NSRC_CASE(9) BCP_NSRC_CASE(10)
+    BCP_NSRC_CASE(6) BCP_NSRC_CASE(7) BCP_NSRC_CASE(8) BCP_NSRC_CASE(9) BCP_NSRC_CASE(10)
     BCP_NSRC_CASE(11) BCP_NSRC_CASE(12) BCP_NSRC_CASE(16)
     default:
-      return launch_fast_nu<0, U, 0>(BCP_ARGS);
+      return launch_stream_nu<0, U, GATHER>(st, grid, a);
   }
 #undef BCP_NSRC_CASE
-#undef BCP_ARGS
 }
 
-hipError_t launch_xor_strided_fast(hipStream_t st, int grid, int vecs, int pol, char *dst, uint64_t dst_stride,
-                                   const char *src, uint64_t stripe_stride, uint64_t src_stride,
-                                   uint64_t nstripes, uint32_t nsrc, uint64_t chunk_bytes) {
-  const uint32_t vps = (uint32_t)(chunk_bytes / 16);
-  const uint32_t tile_v = (uint32_t)kBlock * vecs;
-  const uint32_t tps = (vps + tile_v - 1) / tile_v;
-  const uint64_t ntiles = nstripes * tps;
-  if (ntiles == 0) return hipSuccess;
-  if (ntiles > 0x7FFFFFFFull) return hipErrorInvalidValue;
-  if ((uint64_t)grid > ntiles) grid = (int)ntiles;
+uint32_t stream_tiles_per_stripe(uint64_t chunk_bytes, int vecs) {
+  const uint64_t vps = chunk_bytes / 16;
+  const uint64_t tile_v = (uint64_t)kBlock * vecs;
+  return (uint32_t)((vps + tile_v - 1) / tile_v);
+}
+
+hipError_t launch_xor_stream(hipStream_t st, int grid, int vecs, bool gather, const StreamArgs &a) {
+  if (a.ntiles == 0) return hipSuccess;
+  if (gather) {
+    switch (vecs) {
+      case 1: return launch_stream_u<1, 1>(st, grid, a);
+      case 4: return launch_stream_u<4, 1>(st, grid, a);
+      default: return launch_stream_u<2, 1>(st, grid, a);
+    }
+  }
   switch (vecs) {
-    case 1: return launch_fast_u<1>(st, grid, pol, dst, dst_stride, src, stripe_stride, src_stride, vps, tps, (uint32_t)ntiles, nsrc);
-    case 4: return launch_fast_u<4>(st, grid, pol, dst, dst_stride, src, stripe_stride, src_stride, vps, tps, (uint32_t)ntiles, nsrc);
-    default: return launch_fast_u<2>(st, grid, pol, dst, dst_stride, src, stripe_stride, src_stride, vps, tps, (uint32_t)ntiles, nsrc);
+    case 1: return launch_stream_u<1, 0>(st, grid, a);
+    case 4: return launch_stream_u<4, 0>(st, grid, a);
+    default: return launch_stream_u<2, 0>(st, grid, a);
   }
 }
 

@@ -3,10 +3,11 @@
 
 Workload (BASELINE.json configs[1], "config 2"): 12,500 stripes x 8 sources
 x 512 KiB (100,000 data chunks = 48.8 GiB) resident in HBM per GPU; one step
-= one pass of the parity kernel over all stripes (xor_strided_fast<8,U>,
+= one pass of the parity kernel over all stripes (xor_stream<8,4>,
 the reference's xor_parity, task_processing.c:96-109, batched).
 `--mode rebuild` times config 3 instead (7 survivors + parity body ->
-rebuilt chunk, descriptor kernel).
+rebuilt chunk; a uniform descriptor batch, so the same streaming kernel in
+its pointer-table form).
 
 value = algorithmic bytes of all ranks / max-over-ranks wall time, with
 algorithmic bytes = sum of source lengths + output length per stripe
@@ -93,8 +94,8 @@ def main():
         def step():
             q.xor_uniform(out, src, S, N, C)
         bytes_per_step = S * (N + 1) * C
-        kernel = f"xor_strided_fast<{N},U,POL>"
-        kernel_tag = "xor_strided_fast<"
+        kernel = f"xor_stream<{N},U,strided>"
+        kernel_tag = f"xor_stream<{N}, "
         workload = f"config2: parity gen, {S} stripes x {N} x {C // KiB} KiB device-resident"
     else:
         # config 3: parity first, then rebuild source index 3 from the other
@@ -118,8 +119,8 @@ def main():
         def step():
             bcp.check("bcp_xor_stripes_async", L.bcp_xor_stripes_async(q.h, st, len(stripes), so, len(sources)))
         bytes_per_step = S * (N + 1) * C
-        kernel = "xor_desc<U>"
-        kernel_tag = "xor_desc<"
+        kernel = f"xor_stream<{N},U,gather>"
+        kernel_tag = f"xor_stream<{N}, "
         workload = f"config3: rebuild, {S} stripes x ({N - 1} survivors + parity) x {C // KiB} KiB device-resident"
 
     for _ in range(a.warmup):

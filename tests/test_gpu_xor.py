@@ -155,14 +155,16 @@ def test_strided_layout(oracle, dev, queue):
         assert np.array_equal(out[s * pitch:s * pitch + chunk], ref)
 
 
+@pytest.mark.parametrize("sched", [0, 1])
 @pytest.mark.parametrize("bpc,vecs", [(1, 1), (2, 4), (4, 2), (8, 1), (16, 4)])
-def test_tuning_variants_agree(oracle, engine, dev, queue, bpc, vecs):
+def test_tuning_variants_agree(oracle, engine, dev, queue, bpc, vecs, sched):
     nstripes, nsrc, chunk = 7, 8, 524288 + 4096
-    rng = np.random.default_rng(bpc * 10 + vecs)
+    rng = np.random.default_rng(bpc * 10 + vecs + 100 * sched)
     data = rng.integers(0, 256, size=nstripes * nsrc * chunk, dtype=np.uint8)
     src = dev.put(data)
     dst = dev.alloc(nstripes * chunk)
     engine.tune(bpc, vecs)
+    engine.option("schedule", sched)
     try:
         queue.xor_uniform(dst, src, nstripes, nsrc, chunk)
         out = dev.get(dst, nstripes * chunk)
@@ -170,9 +172,57 @@ def test_tuning_variants_agree(oracle, engine, dev, queue, bpc, vecs):
         res = gpu_stripes(dev, queue, [dict(chunks=[data[:1000], data[5:70000], None], out_len=70000 - 5)])
     finally:
         engine.tune(0, 0)
+        engine.option("schedule", 0)
     ref = np.bitwise_xor.reduce(data.reshape(nstripes, nsrc, chunk), axis=1).reshape(-1)
     assert np.array_equal(out, ref)
     assert np.array_equal(res[0], oracle.xor_padded_np([data[:1000], data[5:70000]]))
+
+
+def test_work_queue_back_to_back_and_two_queues(oracle, engine, dev, queue):
+    """The work-queue counter is monotone per queue: many launches in a row on
+    one queue, a second queue interleaved, and a switch to the static schedule
+    and back must all cover every tile exactly once."""
+    rng = np.random.default_rng(77)
+    q2 = engine.queue()
+    try:
+        jobs = []
+        for i in range(24):
+            n, chunk, ns = int(rng.integers(1, 10)), 16 * int(rng.integers(1, 40000)), int(rng.integers(1, 6))
+            data = rng.integers(0, 256, size=ns * n * chunk, dtype=np.uint8)
+            src, dst = dev.put(data), dev.alloc(ns * chunk)
+            q = queue if i % 3 else q2
+            if i == 10:
+                engine.option("schedule", 1)
+            if i == 14:
+                engine.option("schedule", 0)
+            q.xor_uniform(dst, src, ns, n, chunk)
+            jobs.append((data, dst, ns, n, chunk))
+        q2.sync()
+        for data, dst, ns, n, chunk in jobs:
+            out = dev.get(dst, ns * chunk)
+            ref = np.bitwise_xor.reduce(data.reshape(ns, n, chunk), axis=1).reshape(-1)
+            assert np.array_equal(out, ref)
+    finally:
+        engine.option("schedule", 0)
+        q2.close()
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_uniform_descriptor_batch_takes_pointer_table_path(oracle, dev, queue, seed):
+    """Rebuild shape: every stripe has the same nsrc and out_len and every
+    source is at least out_len long (longer sources are truncated) -> the
+    streaming kernel's pointer-table form; results identical to the oracle."""
+    rng = np.random.default_rng(300 + seed)
+    n = int(rng.integers(1, 10))
+    out_len = 16 * int(rng.integers(1, 50000))
+    stripes, refs = [], []
+    for _ in range(int(rng.integers(1, 9))):
+        lens = [out_len + 16 * int(rng.integers(0, 3)) for _ in range(n)]
+        chunks = [rng.integers(0, 256, size=L, dtype=np.uint8) for L in lens]
+        stripes.append(dict(chunks=chunks, out_len=out_len))
+        refs.append(oracle.xor_padded_np([c[:out_len] for c in chunks]))
+    for o, r in zip(gpu_stripes(dev, queue, stripes), refs):
+        assert np.array_equal(o, r)
 
 
 # --------------------------------------------------------------------------
