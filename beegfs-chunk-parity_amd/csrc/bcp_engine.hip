@@ -191,6 +191,8 @@ extern "C" int bcp_set_option(bcp_engine *eng, const char *key, int value) {
   if (!strcmp(key, "blocks_per_cu") && value >= 1 && value <= 32) eng->tuning.blocks_per_cu = value;
   else if (!strcmp(key, "vecs_per_thread") && (value == 1 || value == 2 || value == 4)) eng->tuning.vecs_per_thread = value;
   else if (!strcmp(key, "schedule") && (value == kSchedQueue || value == kSchedStatic)) eng->tuning.schedule = value;
+  else if (!strcmp(key, "desc_schedule") && (value == kSchedQueue || value == kSchedStatic)) eng->tuning.desc_schedule = value;
+  else if (!strcmp(key, "desc_grab") && value >= 1 && value <= 64) eng->tuning.desc_grab = value;
   else rc = -EINVAL;
   pthread_mutex_unlock(&eng->lock);
   return rc;
@@ -475,6 +477,8 @@ static int submit_desc(bcp_queue *q, const bcp_stripe *stripes, uint32_t nstripe
     a.vps = (uint32_t)(len / 16);
     a.tps = tps;
     a.nsrc = stripes[0].nsrc;
+    a.dense = 1;
+    for (uint32_t i = 0; i < nstripes && a.dense; i++) a.dense = stripes[i].first_src == i * a.nsrc;
     rc = launch_stream(q, true, a, (uint64_t)nstripes * tps);
     if (rc) return rc;
     HIP_RC(hipEventRecord(slot->done, q->stream));
@@ -506,7 +510,15 @@ static int submit_desc(bcp_queue *q, const bcp_stripe *stripes, uint32_t nstripe
   b.nstripes = nstripes;
   b.ntiles = acc;
   b.tile_bytes = tile_bytes;
-  HIP_RC(launch_xor_desc(q->stream, grid_for(e), vecs, b));
+  b.sched = e->tuning.desc_schedule;
+  b.grab = (uint32_t)e->tuning.desc_grab;
+  b.ctr = q->qctr;
+  b.base = q->qbase;
+  const uint32_t nunits = b.sched == kSchedQueue ? (acc + b.grab - 1) / b.grab : acc;
+  int grid = grid_for(e);
+  if ((uint32_t)grid > nunits) grid = (int)nunits;
+  HIP_RC(launch_xor_desc(q->stream, grid, vecs, b));
+  if (b.sched == kSchedQueue) q->qbase += (uint64_t)nunits + (uint64_t)grid;
   HIP_RC(hipEventRecord(slot->done, q->stream));
   slot->used = true;
   return 0;

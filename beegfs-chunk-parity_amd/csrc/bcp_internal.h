@@ -23,7 +23,11 @@ constexpr int kSchedStatic = 1;  // contiguous tile range per workgroup (r01 des
 struct Tuning {
     int blocks_per_cu = 8;      // 256-thread workgroups launched per CU
     int vecs_per_thread = 4;    // 16-byte vectors per lane per tile
-    int schedule = kSchedQueue; // kSched*
+    int schedule = kSchedQueue; // kSched* of xor_stream
+    int desc_grab = 4;          // tiles per work-queue grab of xor_desc
+    int desc_schedule = kSchedStatic;  // kSched* of xor_desc (r01: the queue's one atomic per
+                                       // 16 KiB tile saturates on mixed sizes, whose tiles
+                                       // read ~3x fewer bytes; profiles/r01/bench_mixed.jsonl)
 };
 
 // Arguments of the streaming kernel (xor_stream).
@@ -39,6 +43,7 @@ struct StreamArgs {
     uint32_t tps;               // tiles per stripe
     uint32_t ntiles;
     uint32_t nsrc;
+    uint32_t dense;             // GATHER = 1: stripes[s].first_src == s * nsrc for every s
     unsigned long long *ctr;    // work-queue counter (per queue)
     unsigned long long base;    // counter value at the start of this launch
     int sched;                  // kSched*
@@ -52,6 +57,10 @@ struct DescBatch {
     uint32_t nstripes;
     uint32_t ntiles;
     uint32_t tile_bytes;        // bytes of output per tile
+    unsigned long long *ctr;    // work-queue counter (per queue), as StreamArgs
+    unsigned long long base;
+    int sched;                  // kSched*
+    uint32_t grab;              // kSchedQueue: tiles per grab
 };
 
 // Kernel launchers (bcp_kernels.hip).  All return hipError_t.
@@ -60,6 +69,7 @@ struct DescBatch {
 hipError_t launch_xor_stream(hipStream_t st, int grid, int vecs, bool gather,
                              const StreamArgs &a);
 uint32_t stream_tiles_per_stripe(uint64_t chunk_bytes, int vecs);
+// Descriptor kernel; same work-queue accounting as launch_xor_stream.
 hipError_t launch_xor_desc(hipStream_t st, int grid, int vecs,
                            const DescBatch &b);
 hipError_t launch_fill_synthetic(hipStream_t st, int grid, char *dst,

@@ -22,7 +22,31 @@ namespace bcp {
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 typedef v4u v4u_u __attribute__((aligned(1)));  // unaligned 16-byte view
 
-__device__ __forceinline__ v4u ld_nt(const v4u *p) { return __builtin_nontemporal_load(p); }
+template <typename T>
+__device__ __forceinline__ v4u ld_nt(const T *p) { return __builtin_nontemporal_load(p); }
+
+// Descriptor tables (stripes, sources, tile prefixes) are never written while
+// a kernel runs.  Reading them through the constant address space lets the
+// compiler use scalar loads (s_load, own lgkm counter) for the uniform
+// indices; through a generic pointer they become vector loads whose
+// s_waitcnt vmcnt(0) drains the data loads in flight on every tile.
+template <typename T>
+using const_as = const __attribute__((address_space(4))) T;
+template <typename T>
+__device__ __forceinline__ const_as<T> *cst(const T *p) {
+  return (const_as<T> *)(uintptr_t)p;
+}
+
+// Data pointers taken from descriptor tables are plain integers; without an
+// address space the compiler emits flat loads, which also count on lgkmcnt,
+// so every scalar-load wait would drain the whole data stream.  Cast them to
+// the global address space.
+template <typename T>
+using glob = __attribute__((address_space(1))) T;
+template <typename T>
+__device__ __forceinline__ glob<T> *gp(uint64_t p) {
+  return (glob<T> *)(uintptr_t)p;
+}
 __device__ __forceinline__ v4u zero4() { return v4u{0u, 0u, 0u, 0u}; }
 
 // ---------------------------------------------------------------------------
@@ -59,37 +83,39 @@ __device__ __forceinline__ void stream_tile(const StreamArgs &a, uint32_t t) {
   const uint32_t nsrc = NSRC > 0 ? (uint32_t)NSRC : a.nsrc;
   const uint32_t s = t / a.tps;
   const uint32_t tin = t - s * a.tps;
-  const char *sb = nullptr;
-  const bcp_source *sl = nullptr;
-  v4u *db;
+  uint64_t sb = 0;
+  const_as<bcp_source> *sl = nullptr;
+  glob<v4u> *db;
   if constexpr (GATHER) {
-    const bcp_stripe d = a.stripes[s];
-    sl = a.sources + d.first_src;
-    db = reinterpret_cast<v4u *>(d.dst);
+    // Dense batches (first_src == s * nsrc, the usual layout) need no
+    // dependent load of first_src: both table reads go out together.
+    const_as<bcp_stripe> *ds = cst(a.stripes) + s;
+    sl = cst(a.sources) + (a.dense ? s * nsrc : ds->first_src);
+    db = gp<v4u>(ds->dst);
   } else {
-    sb = a.src + (uint64_t)s * a.stripe_stride;
-    db = reinterpret_cast<v4u *>(a.dst + (uint64_t)s * a.dst_stride);
+    sb = (uint64_t)(uintptr_t)a.src + (uint64_t)s * a.stripe_stride;
+    db = gp<v4u>((uint64_t)(uintptr_t)a.dst + (uint64_t)s * a.dst_stride);
   }
-  auto src_k = [&](uint32_t k) -> const v4u * {
-    if constexpr (GATHER) return reinterpret_cast<const v4u *>(sl[k].ptr);
-    else return reinterpret_cast<const v4u *>(sb + (uint64_t)k * a.src_stride);
+  auto src_k = [&](uint32_t k) -> const glob<v4u> * {
+    if constexpr (GATHER) return gp<v4u>(sl[k].ptr);
+    else return gp<v4u>(sb + (uint64_t)k * a.src_stride);
   };
   v4u acc[U];
   if ((tin + 1) * (uint32_t)(kBlock * U) <= a.vps) {
-    const v4u *p0 = src_k(0);
+    const glob<v4u> *p0 = src_k(0);
 #pragma unroll
     for (int u = 0; u < U; u++) acc[u] = ld_nt(p0 + tile_vec<U>(tin, u));
     if constexpr (NSRC > 0) {
 #pragma unroll
       for (int k = 1; k < NSRC; k++) {
-        const v4u *pk = src_k(k);
+        const glob<v4u> *pk = src_k(k);
 #pragma unroll
         for (int u = 0; u < U; u++) acc[u] ^= ld_nt(pk + tile_vec<U>(tin, u));
       }
     } else {
 #pragma unroll 4
       for (uint32_t k = 1; k < nsrc; k++) {
-        const v4u *pk = src_k(k);
+        const glob<v4u> *pk = src_k(k);
 #pragma unroll
         for (int u = 0; u < U; u++) acc[u] ^= ld_nt(pk + tile_vec<U>(tin, u));
       }
@@ -145,8 +171,11 @@ __global__ __launch_bounds__(kBlock) void xor_stream(StreamArgs a) {
 // ---------------------------------------------------------------------------
 
 // 16 bytes of source `p` (readable length len) at offset off, zero past len.
-__device__ __forceinline__ v4u load_src_tail(const unsigned char *p, uint64_t len, uint64_t off) {
-  if (off + 16 <= len) return *reinterpret_cast<const v4u_u *>(p + off);
+typedef glob<const unsigned char> gbyte;
+__device__ __forceinline__ v4u ld16(gbyte *p) { return __builtin_nontemporal_load((const glob<v4u_u> *)p); }
+
+__device__ __forceinline__ v4u load_src_tail(gbyte *p, uint64_t len, uint64_t off) {
+  if (off + 16 <= len) return ld16(p + off);
   if (off >= len) return zero4();
   unsigned int w[4] = {0u, 0u, 0u, 0u};
   const uint32_t n = (uint32_t)(len - off);
@@ -165,9 +194,9 @@ __device__ __forceinline__ uint64_t replay_offset(uint64_t j, uint64_t len, uint
   return w > lw ? j - (w - lw) * window : j;
 }
 
-__device__ __forceinline__ void store_tail(unsigned char *d, uint64_t out_len, uint64_t off, v4u v) {
+__device__ __forceinline__ void store_tail(glob<unsigned char> *d, uint64_t out_len, uint64_t off, v4u v) {
   if (off + 16 <= out_len) {
-    *reinterpret_cast<v4u_u *>(d + off) = v;
+    *(glob<v4u_u> *)(d + off) = v;
     return;
   }
   if (off >= out_len) return;
@@ -177,99 +206,157 @@ __device__ __forceinline__ void store_tail(unsigned char *d, uint64_t out_len, u
 
 // ---------------------------------------------------------------------------
 // Descriptor kernel.  Tiles of tile_bytes output bytes are numbered across the
-// batch (tile_start prefix); workgroup b owns the contiguous tile range
-// [b*T/G, (b+1)*T/G), so it finds its first stripe by one binary search and
-// then walks forward.  Per tile and per source the coverage test is uniform:
-// a source either covers the whole tile (unconditional 16-B loads, four
+// batch (tile_start prefix) and handed out by the same work queue as
+// xor_stream (kSchedQueue) or as a contiguous range per workgroup
+// (kSchedStatic).  Tiles arrive in ascending order per workgroup, so the
+// stripe of a tile is found by a galloping search forward from the previous
+// one (scalar loads of tile_start, L2-resident).  Lanes are wave-contiguous as
+// in xor_stream.  Per tile and per source the coverage test is uniform: a
+// source either covers the whole tile (unconditional 16-B loads, eight or four
 // sources in flight together), misses it (skipped: zero padding), or ends
 // inside it (per-lane tail path).  Window-replay stripes take the per-lane
 // path for every source.
 // ---------------------------------------------------------------------------
-template <int U>
-__global__ __launch_bounds__(kBlock) void xor_desc(DescBatch b) {
-  const uint32_t g = gridDim.x;
-  const uint32_t t_begin = (uint32_t)(((uint64_t)blockIdx.x * b.ntiles) / g);
-  const uint32_t t_end = (uint32_t)(((uint64_t)(blockIdx.x + 1) * b.ntiles) / g);
-  if (t_begin >= t_end) return;
-  uint32_t lo = 0, hi = b.nstripes;
+__device__ __forceinline__ uint32_t find_stripe(const uint32_t *tsg, uint32_t nstripes, uint32_t s, uint32_t t) {
+  const_as<uint32_t> *ts = cst(tsg);
+  // Precondition: ts[s] <= t < ts[nstripes].  Returns the s' >= s with ts[s'] <= t < ts[s'+1].
+  if (ts[s + 1] > t) return s;
+  uint32_t lo = s + 1, step = 1;  // ts[lo] <= t
+  while (lo + step < nstripes && ts[lo + step] <= t) {
+    lo += step;
+    step <<= 1;
+  }
+  uint32_t hi = lo + step < nstripes ? lo + step : nstripes;  // ts[hi] > t
   while (hi - lo > 1) {
     const uint32_t mid = (lo + hi) >> 1;
-    if (b.tile_start[mid] <= t_begin) lo = mid; else hi = mid;
+    if (ts[mid] <= t) lo = mid; else hi = mid;
   }
-  uint32_t s = lo;
+  return lo;
+}
+
+template <int U>
+__device__ __forceinline__ void desc_tile(const DescBatch &b, uint32_t s, uint32_t t) {
   const uint64_t tile_bytes = b.tile_bytes;
-  for (uint32_t t = t_begin; t < t_end; t++) {
-    while (b.tile_start[s + 1] <= t) s++;
-    const bcp_stripe d = b.stripes[s];
-    const uint64_t tile_off = (uint64_t)(t - b.tile_start[s]) * tile_bytes;
-    const uint64_t tile_end = tile_off + tile_bytes;
-    uint64_t j[U];
+  const_as<bcp_stripe> *dp_ = cst(b.stripes) + s;
+  const bcp_stripe d = {dp_->dst, dp_->out_len, dp_->first_src, dp_->nsrc, dp_->window};
+  const uint64_t tile_off = (uint64_t)(t - cst(b.tile_start)[s]) * tile_bytes;
+  const uint64_t tile_end = tile_off + tile_bytes;
+  uint64_t j[U];
 #pragma unroll
-    for (int u = 0; u < U; u++) j[u] = tile_off + ((uint64_t)u * kBlock + threadIdx.x) * 16u;
-    v4u acc[U];
+  for (int u = 0; u < U; u++)
+    j[u] = tile_off + ((uint64_t)(threadIdx.x >> 6) * (64u * U) + (uint64_t)u * 64u + (threadIdx.x & 63u)) * 16u;
+  v4u acc[U];
 #pragma unroll
-    for (int u = 0; u < U; u++) acc[u] = zero4();
-    const bcp_source *srcs = b.sources + d.first_src;
-    uint32_t k = 0;
-    if (d.window == 0) {
-      // Groups of four sources that all cover the tile: 4*U loads in flight.
-      for (; k + 4 <= d.nsrc; k += 4) {
-        const bcp_source s0 = srcs[k], s1 = srcs[k + 1], s2 = srcs[k + 2], s3 = srcs[k + 3];
-        if (s0.len >= tile_end && s1.len >= tile_end && s2.len >= tile_end && s3.len >= tile_end) {
-          const unsigned char *p0 = (const unsigned char *)s0.ptr, *p1 = (const unsigned char *)s1.ptr;
-          const unsigned char *p2 = (const unsigned char *)s2.ptr, *p3 = (const unsigned char *)s3.ptr;
-          v4u x0[U], x1[U], x2[U], x3[U];
+  for (int u = 0; u < U; u++) acc[u] = zero4();
+  const_as<bcp_source> *srcs = cst(b.sources) + d.first_src;
+  uint32_t k = 0;
+  if (d.window == 0) {
+    // Groups of eight sources that all cover the tile: 8*U loads in flight.
+    for (; k + 8 <= d.nsrc; k += 8) {
+      bool all = true;
 #pragma unroll
-          for (int u = 0; u < U; u++) {
-            x0[u] = *reinterpret_cast<const v4u_u *>(p0 + j[u]);
-            x1[u] = *reinterpret_cast<const v4u_u *>(p1 + j[u]);
-            x2[u] = *reinterpret_cast<const v4u_u *>(p2 + j[u]);
-            x3[u] = *reinterpret_cast<const v4u_u *>(p3 + j[u]);
-          }
+      for (int i = 0; i < 8; i++) all = all && srcs[k + i].len >= tile_end;
+      if (!all) break;
+      // Sequential XOR chain: the compiler hoists the independent loads as far
+      // ahead as registers allow (as in xor_stream) instead of holding 8*U.
 #pragma unroll
-          for (int u = 0; u < U; u++) acc[u] ^= (x0[u] ^ x1[u]) ^ (x2[u] ^ x3[u]);
-        } else {
-          const bcp_source ss[4] = {s0, s1, s2, s3};
+      for (int i = 0; i < 8; i++) {
+        gbyte *p = gp<const unsigned char>(srcs[k + i].ptr);
 #pragma unroll
-          for (int i = 0; i < 4; i++) {
-            if (ss[i].len <= tile_off) continue;  // zero padding
-            const unsigned char *p = (const unsigned char *)ss[i].ptr;
-#pragma unroll
-            for (int u = 0; u < U; u++) acc[u] ^= load_src_tail(p, ss[i].len, j[u]);
-          }
-        }
+        for (int u = 0; u < U; u++) acc[u] ^= ld16(p + j[u]);
       }
-      for (; k < d.nsrc; k++) {
-        const bcp_source sk = srcs[k];
-        if (sk.len <= tile_off) continue;
-        const unsigned char *p = (const unsigned char *)sk.ptr;
-        if (sk.len >= tile_end) {
+    }
+    // Groups of four.
+    for (; k + 4 <= d.nsrc; k += 4) {
+      const bcp_source s0 = {srcs[k].ptr, srcs[k].len}, s1 = {srcs[k + 1].ptr, srcs[k + 1].len};
+      const bcp_source s2 = {srcs[k + 2].ptr, srcs[k + 2].len}, s3 = {srcs[k + 3].ptr, srcs[k + 3].len};
+      if (s0.len >= tile_end && s1.len >= tile_end && s2.len >= tile_end && s3.len >= tile_end) {
+        gbyte *p0 = gp<const unsigned char>(s0.ptr), *p1 = gp<const unsigned char>(s1.ptr);
+        gbyte *p2 = gp<const unsigned char>(s2.ptr), *p3 = gp<const unsigned char>(s3.ptr);
 #pragma unroll
-          for (int u = 0; u < U; u++) acc[u] ^= *reinterpret_cast<const v4u_u *>(p + j[u]);
-        } else {
+        for (int u = 0; u < U; u++) acc[u] ^= ld16(p0 + j[u]);
 #pragma unroll
-          for (int u = 0; u < U; u++) acc[u] ^= load_src_tail(p, sk.len, j[u]);
-        }
-      }
-    } else {
-      for (; k < d.nsrc; k++) {
-        const bcp_source sk = srcs[k];
-        const unsigned char *p = (const unsigned char *)sk.ptr;
+        for (int u = 0; u < U; u++) acc[u] ^= ld16(p1 + j[u]);
 #pragma unroll
-        for (int u = 0; u < U; u++) {
-          if (j[u] < d.out_len)
-            acc[u] ^= load_src_tail(p, sk.len, replay_offset(j[u], sk.len, d.window));
+        for (int u = 0; u < U; u++) acc[u] ^= ld16(p2 + j[u]);
+#pragma unroll
+        for (int u = 0; u < U; u++) acc[u] ^= ld16(p3 + j[u]);
+      } else {
+        const bcp_source ss[4] = {s0, s1, s2, s3};
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+          if (ss[i].len <= tile_off) continue;  // zero padding
+          gbyte *p = gp<const unsigned char>(ss[i].ptr);
+#pragma unroll
+          for (int u = 0; u < U; u++) acc[u] ^= load_src_tail(p, ss[i].len, j[u]);
         }
       }
     }
-    unsigned char *dp = (unsigned char *)d.dst;
-    if (tile_end <= d.out_len) {
+    for (; k < d.nsrc; k++) {
+      const bcp_source sk = {srcs[k].ptr, srcs[k].len};
+      if (sk.len <= tile_off) continue;
+      gbyte *p = gp<const unsigned char>(sk.ptr);
+      if (sk.len >= tile_end) {
 #pragma unroll
-      for (int u = 0; u < U; u++) *reinterpret_cast<v4u_u *>(dp + j[u]) = acc[u];
-    } else {
+        for (int u = 0; u < U; u++) acc[u] ^= ld16(p + j[u]);
+      } else {
 #pragma unroll
-      for (int u = 0; u < U; u++) store_tail(dp, d.out_len, j[u], acc[u]);
+        for (int u = 0; u < U; u++) acc[u] ^= load_src_tail(p, sk.len, j[u]);
+      }
     }
+  } else {
+    for (; k < d.nsrc; k++) {
+      const bcp_source sk = {srcs[k].ptr, srcs[k].len};
+      gbyte *p = gp<const unsigned char>(sk.ptr);
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        if (j[u] < d.out_len)
+          acc[u] ^= load_src_tail(p, sk.len, replay_offset(j[u], sk.len, d.window));
+      }
+    }
+  }
+  glob<unsigned char> *dp = gp<unsigned char>(d.dst);
+  if (tile_end <= d.out_len) {
+#pragma unroll
+    for (int u = 0; u < U; u++) __builtin_nontemporal_store(acc[u], (glob<v4u_u> *)(dp + j[u]));
+  } else {
+#pragma unroll
+    for (int u = 0; u < U; u++) store_tail(dp, d.out_len, j[u], acc[u]);
+  }
+}
+
+template <int U>
+__global__ __launch_bounds__(kBlock) void xor_desc(DescBatch b) {
+  uint32_t s = 0;
+  if (b.sched == kSchedStatic) {
+    const uint32_t g = gridDim.x;
+    const uint32_t t_begin = (uint32_t)(((uint64_t)blockIdx.x * b.ntiles) / g);
+    const uint32_t t_end = (uint32_t)(((uint64_t)(blockIdx.x + 1) * b.ntiles) / g);
+    for (uint32_t t = t_begin; t < t_end; t++) {
+      s = find_stripe(b.tile_start, b.nstripes, s, t);
+      desc_tile<U>(b, s, t);
+    }
+    return;
+  }
+  // Work queue in grabs of b.grab consecutive tiles (mixed-size tiles read
+  // fewer bytes, so one atomic per tile would saturate the counter).
+  __shared__ uint32_t next[2];
+  if (threadIdx.x == 0) next[0] = queue_grab(b.ctr, b.base);
+  __syncthreads();
+  uint32_t c = __builtin_amdgcn_readfirstlane(next[0]);
+  int slot = 0;
+  const uint32_t nchunks = (b.ntiles + b.grab - 1) / b.grab;
+  while (c < nchunks) {
+    const uint32_t t0 = c * b.grab;
+    const uint32_t t1 = min(t0 + b.grab, b.ntiles);
+    for (uint32_t t = t0; t < t1; t++) {
+      s = find_stripe(b.tile_start, b.nstripes, s, t);
+      desc_tile<U>(b, s, t);
+    }
+    slot ^= 1;
+    if (threadIdx.x == 0) next[slot] = queue_grab(b.ctr, b.base);
+    __syncthreads();
+    c = __builtin_amdgcn_readfirstlane(next[slot]);
   }
 }
 

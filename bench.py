@@ -7,7 +7,11 @@ x 512 KiB (100,000 data chunks = 48.8 GiB) resident in HBM per GPU; one step
 the reference's xor_parity, task_processing.c:96-109, batched).
 `--mode rebuild` times config 3 instead (7 survivors + parity body ->
 rebuilt chunk; a uniform descriptor batch, so the same streaming kernel in
-its pointer-table form).
+its pointer-table form).  `--mode mixed` times the config-5 chunk shapes
+device-resident: 8-wide stripes with seeded log-uniform chunk lengths in
+[64 KiB, 4 MiB] (not 16-byte multiples) at 256-byte-aligned offsets, zero
+padding to the stripe maximum (descriptor kernel xor_desc); algorithmic bytes
+per stripe = sum of lengths + max length (padding is not read).
 
 value = algorithmic bytes of all ranks / max-over-ranks wall time, with
 algorithmic bytes = sum of source lengths + output length per stripe
@@ -48,12 +52,15 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--mode", choices=["gen", "rebuild"], default="gen")
+    ap.add_argument("--mode", choices=["gen", "rebuild", "mixed"], default="gen")
     ap.add_argument("--stripes", type=int, default=12500, help="stripes per GPU")
     ap.add_argument("--nsrc", type=int, default=8)
     ap.add_argument("--chunk", type=int, default=512 * KiB)
     ap.add_argument("--blocks-per-cu", type=int, default=0)
     ap.add_argument("--vecs", type=int, default=0)
+    ap.add_argument("--schedule", type=int, default=-1,
+                    help="tile schedule of the timed kernel: 0 work queue, 1 static ranges (default: engine's)")
+    ap.add_argument("--grab", type=int, default=0, help="tiles per work-queue grab of the descriptor kernel")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-stripes", type=int, default=256, help="stripes in the CPU sample pool")
     ap.add_argument("--no-cpu", action="store_true")
@@ -82,15 +89,58 @@ def main():
     eng = bcp.Engine(d.local_rank % ndev)
     if a.blocks_per_cu or a.vecs:
         eng.tune(a.blocks_per_cu, a.vecs)
+    if a.grab:
+        eng.option("desc_grab", a.grab)
+    if a.schedule >= 0:
+        eng.option("schedule" if a.mode != "mixed" else "desc_schedule", a.schedule)
     cus, devname = eng.info()
     q = eng.queue()
     S, N, C = a.stripes, a.nsrc, a.chunk
-    src = eng.alloc(S * N * C)
-    out = eng.alloc(S * C)
     chk = eng.alloc(64)
-    q.fill_synthetic(src, S * N * C, seed=1 + d.rank)
+    if a.mode == "mixed":
+        import numpy as np
+        rng = np.random.default_rng(3 + d.rank)
+        # log-uniform lengths; as many stripes as fit the config-2 input volume
+        budget = S * N * C
+        lens_all, tot = [], 0
+        while tot < budget:
+            ls = np.exp(rng.uniform(np.log(64 * KiB), np.log(4 * 1024 * KiB), size=N)).astype(np.int64)
+            lens_all.append(ls)
+            tot += int(ls.sum())
+        align = lambda x: (x + 255) & ~255
+        src_bytes = sum(int(sum(align(int(x)) for x in ls)) for ls in lens_all)
+        out_bytes = sum(align(int(ls.max())) for ls in lens_all)
+        src = eng.alloc(src_bytes)
+        out = eng.alloc(out_bytes)
+    else:
+        src = eng.alloc(S * N * C)
+        out = eng.alloc(S * C)
+        src_bytes = S * N * C
+    q.fill_synthetic(src, src_bytes, seed=1 + d.rank)
 
-    if a.mode == "gen":
+    if a.mode == "mixed":
+        stripes, sources, so_off, do_off = [], [], 0, 0
+        for ls in lens_all:
+            first = len(sources)
+            for x in ls:
+                sources.append((src + so_off, int(x)))
+                so_off += align(int(x))
+            m = int(ls.max())
+            stripes.append((out + do_off, m, first, N, 0))
+            do_off += align(m)
+        st = (bcp.Stripe * len(stripes))(*[bcp.Stripe(*x) for x in stripes])
+        so = (bcp.Source * len(sources))(*[bcp.Source(*x) for x in sources])
+        L = bcp.lib()
+
+        def step():
+            bcp.check("bcp_xor_stripes_async", L.bcp_xor_stripes_async(q.h, st, len(stripes), so, len(sources)))
+        bytes_per_step = sum(int(ls.sum()) + int(ls.max()) for ls in lens_all)
+        S = len(stripes)
+        kernel = "xor_desc<U>"
+        kernel_tag = "xor_desc<"
+        workload = (f"config5 shapes: {S} stripes x {N} chunks, log-uniform 64 KiB-4 MiB, "
+                    f"zero-padded to the stripe max, device-resident")
+    elif a.mode == "gen":
         def step():
             q.xor_uniform(out, src, S, N, C)
         bytes_per_step = S * (N + 1) * C
@@ -142,7 +192,24 @@ def main():
 
     # device-side property check (no oracle here): fold(output) == fold(inputs)
     verified = None
-    if a.mode == "gen":
+    if a.mode == "mixed":
+        import numpy as np
+        ok = True
+        for i in sorted({0, len(stripes) - 1, len(stripes) // 2}):
+            dptr, m, first, n, _ = stripes[i]
+            acc = np.zeros(m, dtype=np.uint8)
+            for k in range(n):
+                p, ln = sources[first + k]
+                buf = np.empty(ln, dtype=np.uint8)
+                q.d2h(buf, p, ln)
+                q.sync()
+                acc[:ln] ^= buf
+            got = np.empty(m, dtype=np.uint8)
+            q.d2h(got, dptr, m)
+            q.sync()
+            ok = ok and bool(np.array_equal(got, acc))
+        verified = ok
+    elif a.mode == "gen":
         q.xor_fold(out, S * C, chk)
         q.xor_fold(src, S * N * C, chk + 16)
         import numpy as np
@@ -167,7 +234,7 @@ def main():
     kern_ms_max = d.max(kern_ms)
 
     cpu = None
-    if d.rank == 0 and d.world == 1 and not a.no_cpu:
+    if d.rank == 0 and d.world == 1 and not a.no_cpu and a.mode != "mixed":
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle  # cpu_baseline leg only
         bps = oracle.bench_xor(1, a.cpu_stripes, N, C, a.cpu_seconds)
@@ -201,7 +268,7 @@ def main():
                 "nsrc": N,
                 "chunk_bytes": C,
                 "bytes_per_step_per_gpu": bytes_per_step,
-                "data_rate_GiBps": round(value * N / (N + 1), 2),
+                "data_rate_GiBps": round(value * N / (N + 1), 2) if a.mode != "mixed" else None,
                 "pct_hbm_peak": round(100.0 * achieved / HBM_PEAK_GBS, 2),
                 "parallelism": f"shard{d.world} (stripes per GPU, no collective)",
                 "device": devname,
