@@ -137,6 +137,22 @@ _SIGS = {
     "bcp_plan_worklist": ([_V, ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(WorkItem), ctypes.c_size_t,
                            ctypes.POINTER(WorkItem), ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
     "bcp_lb_finalize": ([], ctypes.c_int),
+    "bcp_pdb_open": ([ctypes.c_char_p, ctypes.c_uint64, ctypes.POINTER(_V)], ctypes.c_int),
+    "bcp_pdb_close": ([_V], ctypes.c_int),
+    "bcp_pdb_set": ([_V, ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(FileInfo)], ctypes.c_int),
+    "bcp_pdb_del": ([_V, ctypes.c_char_p, ctypes.c_size_t], ctypes.c_int),
+    "bcp_pdb_get": ([_V, ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(FileInfo)], ctypes.c_int),
+    "bcp_pdb_count": ([_V], ctypes.c_size_t),
+    "bcp_pdb_sync": ([_V], ctypes.c_int),
+    "bcp_pdb_items": ([_V, ctypes.POINTER(ctypes.POINTER(WorkItem)), ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
+    "bcp_pdb_items_free": ([ctypes.POINTER(WorkItem)], None),
+    "bcp_gen_run_db": ([ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(WorkItem), ctypes.c_size_t, ctypes.c_int,
+                        ctypes.POINTER(ctypes.c_int), _V, ctypes.POINTER(RunStats)], ctypes.c_int),
+    "bcp_rebuild_run_db": ([ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_char_p, ctypes.c_char_p, _V,
+                            ctypes.POINTER(RunStats)], ctypes.c_int),
+    "bcp_store_cum_weights": ([ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
+    "bcp_gen_round": ([ctypes.c_char_p, ctypes.c_int, _V, ctypes.POINTER(ctypes.c_int), ctypes.c_int, _V,
+                       ctypes.POINTER(RunStats), ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
 }
 
 
@@ -370,6 +386,94 @@ def rebuild_run(store_root: str, ntargets: int, rebuild_target: int, items, corr
     check("bcp_rebuild_run", rc)
     del keep
     return st
+
+
+def gen_run_db(store_root: str, ntargets: int, items, nlanes: int = 12, lanes=None, log=None) -> RunStats:
+    """bcp_gen_run + per-target DB replicas <root>/st<k>/db (gen/main.c:146-149)."""
+    arr, keep = _items(items)
+    st = RunStats()
+    ln = (ctypes.c_int * max(len(lanes), 1))(*lanes) if lanes is not None else None
+    call("bcp_gen_run_db", store_root.encode(), ntargets, arr, len(items), nlanes, ln, log, ctypes.byref(st))
+    del keep
+    return st
+
+
+def rebuild_run_db(store_root: str, ntargets: int, rebuild_target: int, db_folder: str | None = None,
+                   corrupt_list: str | None = None, log=None) -> RunStats:
+    """Rebuild walking a DB in key order (rebuild/main.c:223-225)."""
+    st = RunStats()
+    call("bcp_rebuild_run_db", store_root.encode(), ntargets, rebuild_target,
+         db_folder.encode() if db_folder else None, corrupt_list.encode() if corrupt_list else None, log,
+         ctypes.byref(st))
+    return st
+
+
+def store_cum_weights(store_root: str, ntargets: int) -> list:
+    out = (ctypes.c_int * ntargets)()
+    call("bcp_store_cum_weights", store_root.encode(), ntargets, out)
+    return list(out)
+
+
+def gen_round(store_root: str, ntargets: int, events: "EventSet", cum_weight=None, nlanes: int = 12, log=None):
+    """One phase-2 round: plan from events + DB, run, update the DB.  Returns (RunStats, nplanned)."""
+    st = RunStats()
+    n = ctypes.c_size_t(0)
+    cw = (ctypes.c_int * ntargets)(*cum_weight) if cum_weight is not None else None
+    call("bcp_gen_round", store_root.encode(), ntargets, events.h, cw, nlanes, log, ctypes.byref(st), ctypes.byref(n))
+    return st, n.value
+
+
+DB_VERSION = 1  # common.h:31
+
+
+class PDB:
+    """Persistent chunk state (bcp_pdb_*, persistent_db.{c,h})."""
+
+    def __init__(self, folder: str, version: int = DB_VERSION):
+        h = _V()
+        call("bcp_pdb_open", folder.encode(), version, ctypes.byref(h))
+        self.h = h
+
+    @staticmethod
+    def _k(key):
+        return key.encode() if isinstance(key, str) else bytes(key)
+
+    def set(self, key, timestamp: int, locations: int):
+        k = self._k(key)
+        fi = FileInfo(timestamp, locations)
+        call("bcp_pdb_set", self.h, k, len(k), ctypes.byref(fi))
+
+    def delete(self, key):
+        k = self._k(key)
+        call("bcp_pdb_del", self.h, k, len(k))
+
+    def get(self, key):
+        k = self._k(key)
+        fi = FileInfo()
+        rc = lib().bcp_pdb_get(self.h, k, len(k), ctypes.byref(fi))
+        if rc < 0:
+            raise BcpError("bcp_pdb_get", rc)
+        return (fi.timestamp, fi.locations) if rc == 1 else None
+
+    def __len__(self):
+        return lib().bcp_pdb_count(self.h)
+
+    def items(self):
+        """[(key bytes, timestamp, locations)] in key order."""
+        p = ctypes.POINTER(WorkItem)()
+        n = ctypes.c_size_t(0)
+        call("bcp_pdb_items", self.h, ctypes.byref(p), ctypes.byref(n))
+        out = [(p[i].path, p[i].fi.timestamp, p[i].fi.locations) for i in range(n.value)]
+        lib().bcp_pdb_items_free(p)
+        return out
+
+    def sync(self):
+        call("bcp_pdb_sync", self.h)
+
+    def close(self):
+        if self.h:
+            call("bcp_pdb_close", self.h)
+            self.h = None
 
 
 def pipeline_gen(store_root: str, ntargets: int, items, device: int = 0, slab_bytes: int = 256 << 20,

@@ -24,10 +24,12 @@ struct Tuning {
     int blocks_per_cu = 8;      // 256-thread workgroups launched per CU
     int vecs_per_thread = 4;    // 16-byte vectors per lane per tile
     int schedule = kSchedQueue; // kSched* of xor_stream
-    int desc_grab = 4;          // tiles per work-queue grab of xor_desc
-    int desc_schedule = kSchedStatic;  // kSched* of xor_desc (r01: the queue's one atomic per
-                                       // 16 KiB tile saturates on mixed sizes, whose tiles
-                                       // read ~3x fewer bytes; profiles/r01/bench_mixed.jsonl)
+    // xor_desc: work queue in grabs of 2 tiles.  Mixed-size tiles read ~2.4x
+    // fewer bytes than config-2 tiles, so one atomic per tile saturates the
+    // counter (r01 config-5 sweep, profiles/r01/mixed/: static 61-64 %,
+    // grab 1 56 %, grab 2 71.5 %, grab 3 70 %, grab 4 67.5 %, grab 8 69 %).
+    int desc_grab = 2;
+    int desc_schedule = kSchedQueue;
 };
 
 // Arguments of the streaming kernel (xor_stream).

@@ -5,6 +5,12 @@
  *   bcp_gen_run       gen/main.c:116-164 (process_list) + the lane launch at
  *                     :821-889 and the per-rank HostState setup at :723-743
  *   bcp_rebuild_run   rebuild/main.c:40-89 (do_file) + setup at :200-225
+ *   bcp_gen_run_db / bcp_rebuild_run_db / bcp_gen_round
+ *                     the same with the persistent state: per-target DB
+ *                     replicas updated after every task (gen/main.c:146-149),
+ *                     rebuild walking a DB in key order (rebuild/main.c:
+ *                     223-225), and a whole phase-2 round from chunk events
+ *                     (gen/main.c:716-797: load DB, plan, run)
  *
  * Every storage target k is loopback rank k+1 (rank 0 is the coordinator,
  * idle here as in the reference's phase 2), with its store at
@@ -147,8 +153,10 @@ typedef struct {
     const int *lanes;
     int lane;
     int rank;
+    bcp_pdb *db;         /* this rank's replica, or NULL */
     ProgressSample sample;
     uint64_t tasks;
+    int db_rc;
 } lane_arg;
 
 /* process_list (gen/main.c:116-164) for one lane of one rank. */
@@ -164,6 +172,14 @@ static void *gen_lane(void *p)
             continue;
         double t0 = now_s();
         int report = process_task(a->hs, a->items[i].path, &a->items[i].fi, ti);
+        if (a->db) {
+            /* gen/main.c:146-149: keep the entry while it has holders */
+            const char *key = a->items[i].path;
+            int rc = (a->items[i].fi.locations & L_MASK) ? bcp_pdb_set(a->db, key, strlen(key), &a->items[i].fi)
+                                                          : bcp_pdb_del(a->db, key, strlen(key));
+            if (rc && !a->db_rc)
+                a->db_rc = rc;
+        }
         if (report) {
             a->sample.dt += now_s() - t0;
             a->sample.nfiles += 1;
@@ -172,6 +188,13 @@ static void *gen_lane(void *p)
     }
     bcp_task_thread_release();
     return NULL;
+}
+
+/* <root>/st<k>/db, the replica of storage target k. */
+static int db_path(const char *root, int k, char *out, size_t cap)
+{
+    int n = snprintf(out, cap, "%s/st%d/db", root, k);
+    return (n < 0 || (size_t)n >= cap) ? -ENAMETOOLONG : 0;
 }
 
 static int check_items(int ntargets, const bcp_work_item *items, size_t nitems)
@@ -189,8 +212,23 @@ static int check_items(int ntargets, const bcp_work_item *items, size_t nitems)
     return 0;
 }
 
+static int gen_run_impl(const char *store_root, int ntargets, const bcp_work_item *items, size_t nitems,
+                        int nlanes, const int *lanes_in, int use_db, FILE *log, bcp_run_stats *stats);
+
 int bcp_gen_run(const char *store_root, int ntargets, const bcp_work_item *items, size_t nitems, int nlanes,
                 const int *lanes_in, FILE *log, bcp_run_stats *stats)
+{
+    return gen_run_impl(store_root, ntargets, items, nitems, nlanes, lanes_in, 0, log, stats);
+}
+
+int bcp_gen_run_db(const char *store_root, int ntargets, const bcp_work_item *items, size_t nitems, int nlanes,
+                   const int *lanes_in, FILE *log, bcp_run_stats *stats)
+{
+    return gen_run_impl(store_root, ntargets, items, nitems, nlanes, lanes_in, 1, log, stats);
+}
+
+static int gen_run_impl(const char *store_root, int ntargets, const bcp_work_item *items, size_t nitems,
+                        int nlanes, const int *lanes_in, int use_db, FILE *log, bcp_run_stats *stats)
 {
     if (!store_root || ntargets < 1 || ntargets > MAX_STORAGE_TARGETS || nlanes < 1 || nlanes > 64 ||
         (nitems && !items))
@@ -222,13 +260,19 @@ int bcp_gen_run(const char *store_root, int ntargets, const bcp_work_item *items
     HostState *hs = calloc((size_t)ntargets, sizeof(HostState));
     lane_arg *args = calloc((size_t)ntargets * nlanes, sizeof(lane_arg));
     pthread_t *th = calloc((size_t)ntargets * nlanes, sizeof(pthread_t));
-    if (!hs || !args || !th) {
+    bcp_pdb **dbs = calloc((size_t)ntargets, sizeof(bcp_pdb *));
+    if (!hs || !args || !th || !dbs) {
         rc = -ENOMEM;
         goto out;
     }
     for (int k = 0; k < ntargets; k++)
         if ((rc = open_store(store_root, k, 0, -1, log, &hs[k])))
             goto out;
+    for (int k = 0; use_db && k < ntargets; k++) {
+        char dp[4096];
+        if ((rc = db_path(store_root, k, dp, sizeof(dp))) || (rc = bcp_pdb_open(dp, DB_VERSION, &dbs[k])))
+            goto out;
+    }
     double t0 = now_s();
     int started = 0;
     for (int k = 0; k < ntargets; k++)
@@ -240,6 +284,7 @@ int bcp_gen_run(const char *store_root, int ntargets, const bcp_work_item *items
             a->lanes = use_lanes;
             a->lane = l;
             a->rank = k + 1;
+            a->db = dbs[k];
             if (pthread_create(&th[started], NULL, gen_lane, a) != 0) {
                 /* cannot leave partner lanes blocked: give up loudly */
                 fprintf(stderr, "bcp_gen_run: thread create failed\n");
@@ -260,10 +305,20 @@ int bcp_gen_run(const char *store_root, int ntargets, const bcp_work_item *items
         for (int k = 0; k < ntargets; k++)
             stats->errors += hs[k].error != 0;
     }
+    for (int i = 0; i < started && !rc; i++)
+        rc = args[i].db_rc;
 out:
     if (hs)
         for (int k = 0; k < ntargets; k++)
             close_store(&hs[k], 0);
+    if (dbs)
+        for (int k = 0; k < ntargets; k++)
+            if (dbs[k]) {
+                int crc = bcp_pdb_close(dbs[k]);
+                if (!rc && crc)
+                    rc = crc;
+            }
+    free(dbs);
     {
         int frc = bcp_lb_finalize();
         if (!rc && frc)
@@ -384,5 +439,100 @@ out:
     free(th);
     free(args);
     free(hs);
+    return rc;
+}
+
+/* ---- with the persistent state ------------------------------------------ */
+
+int bcp_rebuild_run_db(const char *store_root, int ntargets, int rebuild_target, const char *db_folder,
+                       const char *corrupt_list_path, FILE *log, bcp_run_stats *stats)
+{
+    if (!store_root || ntargets < 2 || rebuild_target < 0 || rebuild_target >= ntargets)
+        return -EINVAL;
+    char dp[4096];
+    if (!db_folder) {
+        /* the replica of the first surviving target (the reference's
+         * orchestration copies a surviving DB before a rebuild) */
+        int rc = db_path(store_root, rebuild_target == 0 ? 1 : 0, dp, sizeof(dp));
+        if (rc)
+            return rc;
+        db_folder = dp;
+    }
+    struct stat sb;
+    if (stat(db_folder, &sb) != 0)
+        return -errno; /* never create an empty DB for a rebuild */
+    bcp_pdb *db = NULL;
+    int rc = bcp_pdb_open(db_folder, DB_VERSION, &db);
+    if (rc)
+        return rc;
+    bcp_work_item *items = NULL;
+    size_t n = 0;
+    rc = bcp_pdb_items(db, &items, &n); /* key order, as pdb_iterate */
+    bcp_pdb_close(db);
+    if (rc)
+        return rc;
+    rc = bcp_rebuild_run(store_root, ntargets, rebuild_target, items, n, corrupt_list_path, log, stats);
+    bcp_pdb_items_free(items);
+    return rc;
+}
+
+int bcp_store_cum_weights(const char *store_root, int ntargets, int *cum_weight)
+{
+    if (!store_root || !cum_weight || ntargets < 1 || ntargets > MAX_STORAGE_TARGETS)
+        return -EINVAL;
+    int total = 0;
+    for (int k = 0; k < ntargets; k++) {
+        char p[4096];
+        int n = snprintf(p, sizeof(p), "%s/st%d", store_root, k);
+        if (n < 0 || (size_t)n >= sizeof(p))
+            return -ENAMETOOLONG;
+        int fd = open(p, O_DIRECTORY | O_RDONLY | O_CLOEXEC);
+        if (fd < 0)
+            return -errno;
+        total += bcp_store_weight(fd); /* get_store_weight, gen/main.c:403-427, 485 */
+        close(fd);
+        cum_weight[k] = total; /* st_weight (gen/main.c:528-536) */
+    }
+    return total > 0 ? 0 : -ENOSPC;
+}
+
+int bcp_gen_round(const char *store_root, int ntargets, const bcp_eventset *events, const int *cum_weight_in,
+                  int nlanes, FILE *log, bcp_run_stats *stats, size_t *nplanned)
+{
+    if (!store_root || !events || ntargets < 1 || ntargets > MAX_STORAGE_TARGETS)
+        return -EINVAL;
+    int cw[MAX_STORAGE_TARGETS];
+    int rc = 0;
+    if (cum_weight_in)
+        memcpy(cw, cum_weight_in, (size_t)ntargets * sizeof(int));
+    else if ((rc = bcp_store_cum_weights(store_root, ntargets, cw)))
+        return rc;
+    /* previous state: the replica of target 0 (all replicas receive the same
+     * updates; the reference's eaters read their own, gen/main.c:777) */
+    char dp[4096];
+    if ((rc = db_path(store_root, 0, dp, sizeof(dp))))
+        return rc;
+    bcp_pdb *db = NULL;
+    if ((rc = bcp_pdb_open(dp, DB_VERSION, &db)))
+        return rc;
+    bcp_work_item *prev = NULL;
+    size_t nprev = 0;
+    rc = bcp_pdb_items(db, &prev, &nprev);
+    bcp_pdb_close(db);
+    if (rc)
+        return rc;
+    size_t n = 0;
+    bcp_work_item *work = NULL;
+    rc = bcp_plan_worklist(events, ntargets, cw, prev, nprev, NULL, 0, &n);
+    if (!rc) {
+        work = malloc((n ? n : 1) * sizeof(bcp_work_item));
+        rc = work ? bcp_plan_worklist(events, ntargets, cw, prev, nprev, work, n, &n) : -ENOMEM;
+    }
+    if (!rc)
+        rc = bcp_gen_run_db(store_root, ntargets, work, n, nlanes, NULL, log, stats);
+    if (nplanned)
+        *nplanned = n;
+    free(work);
+    bcp_pdb_items_free(prev);
     return rc;
 }

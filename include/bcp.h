@@ -168,7 +168,8 @@ int bcp_set_tuning(bcp_engine *eng, int blocks_per_cu, int vecs_per_thread);
 /* Named knob: "blocks_per_cu" (1..32), "vecs_per_thread" (1,2,4),
  * "schedule" (0 = device-wide tile work queue, the default; 1 = a static
  * contiguous tile range per workgroup, kept for A/B measurements) for the
- * uniform streaming kernel; "desc_schedule" (same values, default 1) for the
+ * uniform streaming kernel; "desc_schedule" (same values, default 0) and
+ * "desc_grab" (tiles per work-queue grab, 1..64, default 2) for the
  * descriptor kernel (mixed sizes, windows, unaligned). */
 int bcp_set_option(bcp_engine *eng, const char *key, int value);
 /* Timer slots for bcp_queue_mark / bcp_queue_elapsed_ms. */

@@ -144,6 +144,31 @@ typedef struct {
     int errors;                /* ranks that ended with a sticky error */
 } bcp_run_stats;
 
+/* ---- persistent chunk state (persistent_db.{c,h}) ---------------------- */
+/* path -> FileInfo, iterated in bytewise key order -- the reference's
+ * LevelDB store (persistent_db.c:23-145) as a self-contained append-log +
+ * hash table (LevelDB is absent here).  Every call returns 0 / -errno;
+ * bcp_pdb_get returns 1 found, 0 absent.  Thread-safe.  The key
+ * "?db_version" is reserved (persistent_db.c:13): the version lives in the
+ * log header and a mismatch makes bcp_pdb_open return -EPROTO
+ * (the reference's errx "Incompatible DB", :72-75). */
+#define BCP_PDB_MAX_KEY 255  /* mkdir_for_file's char[256], task_processing.c:31-32 */
+typedef struct bcp_pdb bcp_pdb;
+int bcp_pdb_open(const char *folder, uint64_t expected_version, bcp_pdb **out);  /* pdb_init */
+int bcp_pdb_close(bcp_pdb *db);                                                  /* pdb_term */
+int bcp_pdb_set(bcp_pdb *db, const char *key, size_t keylen, const FileInfo *val);
+int bcp_pdb_del(bcp_pdb *db, const char *key, size_t keylen);
+int bcp_pdb_get(bcp_pdb *db, const char *key, size_t keylen, FileInfo *val);
+size_t bcp_pdb_count(bcp_pdb *db);
+int bcp_pdb_sync(bcp_pdb *db);  /* fsync the log (LevelDB sync = 1 equivalent) */
+/* pdb_iterate: fn(key, keylen, value, ctx) over a snapshot in key order until
+ * it returns non-zero. */
+typedef int (*bcp_pdb_visit_fn)(const char *key, size_t keylen, const FileInfo *val, void *ctx);
+int bcp_pdb_iterate(bcp_pdb *db, bcp_pdb_visit_fn fn, void *ctx);
+/* Snapshot as work items sorted by path (one allocation; paths inside). */
+int bcp_pdb_items(bcp_pdb *db, bcp_work_item **items, size_t *nitems);
+void bcp_pdb_items_free(bcp_work_item *items);
+
 /* Greedy lane assignment of gen/assign_lanes.c:12-46 (16-deep history per
  * lane, tasks sharing targets kept apart).  Identical output to the
  * reference on x86-64, including its int-shift of P. */
@@ -164,6 +189,17 @@ int bcp_gen_run(const char *store_root, int ntargets, const bcp_work_item *items
  * line) to corrupt_list_path. */
 int bcp_rebuild_run(const char *store_root, int ntargets, int rebuild_target, const bcp_work_item *items,
                     size_t nitems, const char *corrupt_list_path, FILE *log, bcp_run_stats *stats);
+
+/* With the persistent state: bcp_gen_run plus, after every task of a lane
+ * of rank k, the process_list DB update (gen/main.c:146-149: set when the
+ * item still has holders, else delete) on target k's replica
+ * <root>/st<k>/db. */
+int bcp_gen_run_db(const char *store_root, int ntargets, const bcp_work_item *items, size_t nitems, int nlanes,
+                   const int *lanes, FILE *log, bcp_run_stats *stats);
+/* Rebuild walking the DB at db_folder in key order (rebuild/main.c:223-225);
+ * NULL = the replica of the first surviving target.  -ENOENT if absent. */
+int bcp_rebuild_run_db(const char *store_root, int ntargets, int rebuild_target, const char *db_folder,
+                       const char *corrupt_list_path, FILE *log, bcp_run_stats *stats);
 
 /* ---- chunk-event records and worklist planning ------------------------- */
 /* Record stream per storage target (bp-find-all-chunks/main.c:25-33,
@@ -190,6 +226,15 @@ int bcp_store_weight(int dirfd);
  * out[i].path points into the event set.  *nout = number of events. */
 int bcp_plan_worklist(const bcp_eventset *s, int ntargets, const int *cum_weight, const bcp_work_item *prev,
                       size_t nprev, bcp_work_item *out, size_t out_cap, size_t *nout);
+
+/* Cumulative store weights st_weight (gen/main.c:485, 528-536) of
+ * <root>/st<k>, k < ntargets. */
+int bcp_store_cum_weights(const char *store_root, int ntargets, int *cum_weight);
+/* One phase-2 gen round (gen/main.c:716-797): previous state from target
+ * 0's replica, worklist planned from `events` (cum_weight NULL = the stores'
+ * own weights), then bcp_gen_run_db.  *nplanned = worklist length. */
+int bcp_gen_round(const char *store_root, int ntargets, const bcp_eventset *events, const int *cum_weight,
+                  int nlanes, FILE *log, bcp_run_stats *stats, size_t *nplanned);
 
 /* ---- batched end-to-end pipeline (loopback stores) ---------------------- */
 typedef struct {

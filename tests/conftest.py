@@ -1,4 +1,6 @@
+import ctypes
 import os
+import subprocess
 import sys
 
 import pytest
@@ -45,3 +47,21 @@ def queue(engine):
     q = engine.queue()
     yield q
     q.close()
+
+
+@pytest.fixture(scope="session")
+def cpu_hook_lib(bcp, tmp_path_factory):
+    """Test double for the P role's fold (tests/native/cpu_xor_hook.c)."""
+    out = tmp_path_factory.mktemp("hook") / "libcpuxor.so"
+    subprocess.run(["gcc", "-O2", "-shared", "-fPIC", "-o", str(out),
+                    os.path.join(os.path.dirname(__file__), "native", "cpu_xor_hook.c")], check=True)
+    return ctypes.CDLL(str(out))
+
+
+@pytest.fixture
+def cpu_hook(bcp, cpu_hook_lib):
+    """Route the P role's fold to the CPU test double for one test (host-logic
+    tests on machines without a GPU; the product never sets the hook)."""
+    bcp.set_xor_hook(ctypes.cast(cpu_hook_lib.test_cpu_xor, ctypes.c_void_p).value)
+    yield cpu_hook_lib
+    bcp.set_xor_hook(None)

@@ -19,22 +19,6 @@ GOLD = json.load(open(os.path.join(HERE, "golden", "kats.json")))
 MiB = 1024 * 1024
 
 
-@pytest.fixture(scope="module")
-def cpu_hook_lib(bcp, tmp_path_factory):
-    out = tmp_path_factory.mktemp("hook") / "libcpuxor.so"
-    subprocess.run(["gcc", "-O2", "-shared", "-fPIC", "-o", str(out), os.path.join(HERE, "native", "cpu_xor_hook.c")],
-                   check=True)
-    return ctypes.CDLL(str(out))
-
-
-@pytest.fixture
-def cpu_hook(bcp, cpu_hook_lib):
-    """Route the P role's fold to the CPU test double for one test."""
-    bcp.set_xor_hook(ctypes.cast(cpu_hook_lib.test_cpu_xor, ctypes.c_void_p).value)
-    yield cpu_hook_lib
-    bcp.set_xor_hook(None)
-
-
 def parity_of(root, p_st, path):
     return S.read_file(S.parity_path(root, p_st, path))
 
