@@ -151,6 +151,8 @@ _SIGS = {
     "bcp_rebuild_run_db": ([ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_char_p, ctypes.c_char_p, _V,
                             ctypes.POINTER(RunStats)], ctypes.c_int),
     "bcp_store_cum_weights": ([ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
+    "bcp_gen_round_pipeline": ([_V, ctypes.c_char_p, ctypes.c_int, _V, ctypes.POINTER(ctypes.c_int), _V,
+                                ctypes.POINTER(RunStats), ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
     "bcp_gen_round": ([ctypes.c_char_p, ctypes.c_int, _V, ctypes.POINTER(ctypes.c_int), ctypes.c_int, _V,
                        ctypes.POINTER(RunStats), ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
 }
@@ -504,6 +506,15 @@ class Pipeline:
         call("bcp_pipeline_run", self.h, store_root.encode(), ntargets, arr, len(items), log, ctypes.byref(st))
         del keep
         return st
+
+    def round(self, store_root: str, ntargets: int, events: "EventSet", cum_weight=None, log=None):
+        """bcp_gen_round_pipeline: plan from events + DB, run batched, update the DB."""
+        st = RunStats()
+        n = ctypes.c_size_t(0)
+        cw = (ctypes.c_int * ntargets)(*cum_weight) if cum_weight is not None else None
+        call("bcp_gen_round_pipeline", self.h, store_root.encode(), ntargets, events.h, cw, log, ctypes.byref(st),
+             ctypes.byref(n))
+        return st, n.value
 
     def close(self):
         if self.h:

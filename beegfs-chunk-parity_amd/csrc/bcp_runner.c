@@ -496,8 +496,32 @@ int bcp_store_cum_weights(const char *store_root, int ntargets, int *cum_weight)
     return total > 0 ? 0 : -ENOSPC;
 }
 
-int bcp_gen_round(const char *store_root, int ntargets, const bcp_eventset *events, const int *cum_weight_in,
-                  int nlanes, FILE *log, bcp_run_stats *stats, size_t *nplanned)
+/* Apply the process_list DB update (gen/main.c:146-149) for every processed
+ * item to every replica (the batched pipeline has no per-rank lanes). */
+static int update_replicas(const char *root, int ntargets, const bcp_work_item *items, size_t n)
+{
+    int rc = 0;
+    for (int k = 0; k < ntargets && !rc; k++) {
+        char dp[4096];
+        bcp_pdb *db = NULL;
+        if ((rc = db_path(root, k, dp, sizeof(dp))) || (rc = bcp_pdb_open(dp, DB_VERSION, &db)))
+            break;
+        for (size_t i = 0; i < n && !rc; i++) {
+            if ((uint64_t)GET_P(items[i].fi.locations) == NO_P)
+                continue;
+            const char *key = items[i].path;
+            rc = (items[i].fi.locations & L_MASK) ? bcp_pdb_set(db, key, strlen(key), &items[i].fi)
+                                                  : bcp_pdb_del(db, key, strlen(key));
+        }
+        int crc = bcp_pdb_close(db);
+        if (!rc)
+            rc = crc;
+    }
+    return rc;
+}
+
+static int round_impl(bcp_pipeline *pl, const char *store_root, int ntargets, const bcp_eventset *events,
+                      const int *cum_weight_in, int nlanes, FILE *log, bcp_run_stats *stats, size_t *nplanned)
 {
     if (!store_root || !events || ntargets < 1 || ntargets > MAX_STORAGE_TARGETS)
         return -EINVAL;
@@ -528,11 +552,34 @@ int bcp_gen_round(const char *store_root, int ntargets, const bcp_eventset *even
         work = malloc((n ? n : 1) * sizeof(bcp_work_item));
         rc = work ? bcp_plan_worklist(events, ntargets, cw, prev, nprev, work, n, &n) : -ENOMEM;
     }
-    if (!rc)
+    if (!rc && !pl)
         rc = bcp_gen_run_db(store_root, ntargets, work, n, nlanes, NULL, log, stats);
+    if (!rc && pl) {
+        bcp_run_stats st;
+        memset(&st, 0, sizeof(st));
+        rc = bcp_pipeline_run(pl, store_root, ntargets, work, n, log, &st);
+        if (!rc && st.errors == 0)
+            rc = update_replicas(store_root, ntargets, work, n); /* only after the parity is on disk */
+        if (stats)
+            *stats = st;
+    }
     if (nplanned)
         *nplanned = n;
     free(work);
     bcp_pdb_items_free(prev);
     return rc;
+}
+
+int bcp_gen_round(const char *store_root, int ntargets, const bcp_eventset *events, const int *cum_weight,
+                  int nlanes, FILE *log, bcp_run_stats *stats, size_t *nplanned)
+{
+    return round_impl(NULL, store_root, ntargets, events, cum_weight, nlanes, log, stats, nplanned);
+}
+
+int bcp_gen_round_pipeline(bcp_pipeline *pl, const char *store_root, int ntargets, const bcp_eventset *events,
+                           const int *cum_weight, FILE *log, bcp_run_stats *stats, size_t *nplanned)
+{
+    if (!pl)
+        return -EINVAL;
+    return round_impl(pl, store_root, ntargets, events, cum_weight, 0, log, stats, nplanned);
 }

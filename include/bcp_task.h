@@ -261,6 +261,10 @@ int bcp_pipeline_create(const bcp_pipeline_opts *opts, bcp_pipeline **out);
 int bcp_pipeline_run(bcp_pipeline *pl, const char *store_root, int ntargets, const bcp_work_item *items,
                      size_t nitems, FILE *log, bcp_run_stats *stats);
 int bcp_pipeline_destroy(bcp_pipeline *pl);
+/* bcp_gen_round with the batched pipeline as the engine; the replicas are
+ * updated after the run, only when it finished without errors. */
+int bcp_gen_round_pipeline(bcp_pipeline *pl, const char *store_root, int ntargets, const bcp_eventset *events,
+                           const int *cum_weight, FILE *log, bcp_run_stats *stats, size_t *nplanned);
 
 #ifdef __cplusplus
 }

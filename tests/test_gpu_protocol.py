@@ -154,3 +154,68 @@ def test_protocol_repeated_runs_reuse_pool(bcp, oracle, tmp_path):
         assert st.errors == 0
     for (path, holders, p, lens) in files:
         assert S.read_file(S.parity_path(root, p, path)) == oracle.gen_parity_file(contents[path])
+
+
+@pytest.mark.parametrize("engine_kind", ["protocol", "pipeline"])
+def test_db_round_then_partial_round_then_rebuild(bcp, oracle, tmp_path, engine_kind):
+    """A full gen round from chunk events (plan + DB replicas), a changelog
+    round that recomputes only the modified stripe, then a rebuild walking
+    the DB -- on the device, with both engines."""
+    import planner as PL
+    rng = np.random.default_rng(11)
+    root, nt = str(tmp_path), 9
+    S.make_store(root, nt)
+    cw = [1000 * (k + 1) for k in range(nt)]
+    streams, contents, files = {k: [] for k in range(nt)}, {}, {}
+    for i in range(24):
+        path = f"d{i % 4}/c{i}"
+        holders = sorted(int(x) for x in rng.choice(nt, size=8, replace=False))
+        lens = [int(x) for x in np.exp(rng.uniform(np.log(1024), np.log(3 << 20), size=8))]
+        arrs = []
+        for h, L in zip(holders, lens):
+            d = S.synthetic_chunk(i * 97 + h, L)
+            S.write_chunk(root, h, path, d)
+            streams[h].append((1000 + i, L, "m", path))
+            arrs.append(d)
+        files[path], contents[path] = holders, arrs
+    pl = bcp.Pipeline() if engine_kind == "pipeline" else None
+
+    def round_(streams):
+        es = bcp.EventSet()
+        for k, recs in streams.items():
+            es.feed(k, bcp.pack_records(recs))
+        r = pl.round(root, nt, es, cum_weight=cw) if pl else bcp.gen_round(root, nt, es, cum_weight=cw, nlanes=4)
+        es.close()
+        return r
+
+    try:
+        st, n = round_(streams)
+        assert st.errors == 0 and n == 24
+        db = bcp.PDB(os.path.join(root, "st3", "db"))
+        placed = {k.decode(): loc for k, _, loc in db.items()}
+        db.close()
+        for path, holders in files.items():
+            p = PL.get_p(placed[path])
+            assert S.read_file(S.parity_path(root, p, path)) == oracle.gen_parity_file(contents[path]), path
+        # partial round: one chunk modified
+        path = "d1/c5"
+        h = files[path][2]
+        new = S.synthetic_chunk(4242, 777_777)
+        S.write_chunk(root, h, path, new)
+        contents[path][2] = new
+        st, n = round_({h: [(5000, 777_777, "m", path)]})
+        assert n == 1 and st.errors == 0
+        assert S.read_file(S.parity_path(root, PL.get_p(placed[path]), path)) == oracle.gen_parity_file(contents[path])
+    finally:
+        if pl:
+            pl.close()
+    victim = 5
+    lost = {}
+    for path, holders in files.items():
+        if victim in holders:
+            lost[path] = S.read_file(S.chunk_path(root, victim, path))
+            os.remove(S.chunk_path(root, victim, path))
+    st = bcp.rebuild_run_db(root, nt, victim)
+    assert st.errors == 0
+    for path, data in lost.items():
+        assert S.read_file(S.chunk_path(root, victim, path)) == data, path

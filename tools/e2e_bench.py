@@ -11,9 +11,10 @@ config 1 (BASELINE.json configs[0] shape): 4 storage targets as loopback
 config 5: 9 targets, 8-wide stripes, chunk sizes log-uniform in
   [64 KiB, 4 MiB] (not 16-byte rounded); full parity gen (pipeline), then a
   seeded 10 % of stripes is rewritten, their chunk events are emitted as the
-  binary record streams of bp-find-all-chunks (one per target), parsed and
-  planned by bcp_eventset / bcp_plan_worklist, and only that subset is
-  recomputed by the pipeline (pinned H2D/D2H on side queues).
+  binary record streams of bp-find-all-chunks (one per target), and one
+  changelog round (bcp_gen_round_pipeline) parses them, plans them against
+  the persistent state (per-target DB replicas), recomputes only that subset
+  through the pipeline (pinned H2D/D2H on side queues) and updates the DB.
 
 Rates are (sum of chunk bytes read + parity bytes written) / wall time.  The
 stores are freshly written, so reads come from the page cache: these are
@@ -183,24 +184,34 @@ def config5(a):
             new.append(data)
             streams[h].append((ts1, L, "m", path))
         contents[path] = new
+    # persistent state: seed every target's DB replica with the state of the
+    # full generation above (what that round's process_list updates leave)
+    t0 = time.perf_counter()
+    for k in range(ntargets):
+        db = bcp.PDB(os.path.join(root, f"st{k}", "db"))
+        for path, ts, loc in items:
+            db.set(path, ts, loc)
+        db.close()
+    emit(config=5, stage="db_seeded", replicas=ntargets, entries=len(items), seconds=round(time.perf_counter() - t0, 3))
+    # changelog round: events -> plan against the DB -> pipeline -> DB update
+    cum = list(np.cumsum([1000] * ntargets))
     t0 = time.perf_counter()
     es = bcp.EventSet()
     for t, recs in streams.items():
         es.feed(t, bcp.pack_records(recs))
-    cum = list(np.cumsum([1000] * ntargets))
-    planned = es.plan(ntargets, cum, prev=items)
-    dt_plan = time.perf_counter() - t0
+    st, nplanned = pl.round(root, ntargets, es, cum_weight=cum)
+    dt = time.perf_counter() - t0
     # the planner keeps each stripe's P (fill_in_missing_fields) -> same targets
+    db = bcp.PDB(os.path.join(root, "st0", "db"))
+    state = {k.decode(): (ts, loc) for k, ts, loc in db.items()}
+    db.close()
     want = {files[i][0]: items[i][2] for i in sub}
-    plan_ok = len(planned) == len(sub) and all(loc == want[p] and ts == ts1 for p, ts, loc in planned)
+    plan_ok = nplanned == len(sub) and all(state[p] == (ts1, loc) for p, loc in want.items())
     sub_files = [files[i] for i in sub]
     srd, swr = total_bytes(root, sub_files)
-    t0 = time.perf_counter()
-    st = pl.run(root, ntargets, planned)
-    dt = time.perf_counter() - t0
     pl.close()
     ok2, bad2 = verify(root, sub_files, contents, a.verify, rng)
-    emit(config=5, path="changelog_subset_pipeline", stripes=len(sub), plan_seconds=round(dt_plan, 4),
+    emit(config=5, path="changelog_round_pipeline(events->plan vs DB->pipeline->DB)", stripes=len(sub),
          plan_matches=plan_ok, seconds=round(dt, 3), GiBps=round((srd + swr) / dt / GiB, 3), bytes_read=srd,
          bytes_written=swr, tasks=int(st.tasks), verified=ok2, bad=bad2)
     es.close()
