@@ -151,6 +151,9 @@ _SIGS = {
     "bcp_rebuild_run_db": ([ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_char_p, ctypes.c_char_p, _V,
                             ctypes.POINTER(RunStats)], ctypes.c_int),
     "bcp_store_cum_weights": ([ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
+    "bcp_scan_chunks": ([ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64)], ctypes.c_int),
+    "bcp_eventset_scan": ([_V, ctypes.c_int, ctypes.c_char_p, ctypes.POINTER(ctypes.c_uint64)], ctypes.c_int),
+    "bcp_check_targets": ([ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, _V], ctypes.c_int),
     "bcp_gen_round_pipeline": ([_V, ctypes.c_char_p, ctypes.c_int, _V, ctypes.POINTER(ctypes.c_int), _V,
                                 ctypes.POINTER(RunStats), ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
     "bcp_gen_round": ([ctypes.c_char_p, ctypes.c_int, _V, ctypes.POINTER(ctypes.c_int), ctypes.c_int, _V,
@@ -558,6 +561,12 @@ class EventSet:
     def feed_file(self, st: int, path: str):
         call("bcp_eventset_feed_file", self.h, st, path.encode())
 
+    def scan(self, st: int, chunks_dir: str) -> int:
+        """Feed a bp-find-all-chunks walk of chunks_dir as target st's stream."""
+        n = ctypes.c_uint64(0)
+        call("bcp_eventset_scan", self.h, st, chunks_dir.encode(), ctypes.byref(n))
+        return n.value
+
     def __len__(self):
         return lib().bcp_eventset_count(self.h)
 
@@ -586,6 +595,13 @@ class EventSet:
         if self.h:
             lib().bcp_eventset_destroy(self.h)
             self.h = None
+
+
+BIN_PATH = os.path.join(PKG_DIR, "bin", "bcp")
+
+
+def check_targets(store_root: str, ntargets: int, run_data: str):
+    call("bcp_check_targets", store_root.encode(), ntargets, run_data.encode(), None)
 
 
 def path_hash(path: str) -> int:

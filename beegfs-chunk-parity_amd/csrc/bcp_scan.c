@@ -1,0 +1,238 @@
+/*
+ * bcp_scan.c -- the producers around a generation round on one node:
+ *
+ *   bcp_scan_chunks / bcp_eventset_scan
+ *       bp-find-all-chunks (src/bp-find-all-chunks/main.c:17-45): walk a
+ *       store's chunks directory and emit one 'm' record per regular file,
+ *       {i64 mtime, u64 size, u64 'm', u64 len, path relative to the chunks
+ *       dir}; the --complete input of phase 1 (gen/main.c:622-624).
+ *   bcp_check_targets
+ *       the storage-target bookkeeping of gen/main.c:472-551 (RunData
+ *       "last run" file, targetNumID per store, GIT_VERSION stamp): targets
+ *       may be added, never lost, duplicated or moved.
+ *
+ * The reference's phase-1 scatter (feeders -> eaters by simple_hash(path) %
+ * ntargets, gen/main.c:238-336, 576-699) exists to spread aggregation over
+ * MPI ranks; with loopback ranks every target's stream is fed into one event
+ * set, which aggregates identically (fih_add_info is per path).
+ */
+#define _GNU_SOURCE
+#include <errno.h>
+#include <fcntl.h>
+#include <ftw.h>
+#include <pthread.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include "bcp_task.h"
+
+#define SCAN_BUF (64 * 1024) /* bp-find-all-chunks/main.c:14 */
+
+typedef struct {
+    unsigned char buf[SCAN_BUF];
+    size_t used;
+    int fd;              /* >= 0: write the stream here */
+    bcp_eventset *set;   /* else: feed it here */
+    int st;
+    size_t prefix;       /* strlen(chunks_dir) + 1 */
+    int rc;
+    uint64_t nrec;
+} scan_ctx;
+
+/* nftw has no user pointer; scans are serialised by this lock. */
+static pthread_mutex_t g_scan_lock = PTHREAD_MUTEX_INITIALIZER;
+static scan_ctx *g_scan;
+
+static int flush_scan(scan_ctx *c)
+{
+    if (!c->used)
+        return 0;
+    if (c->fd >= 0) {
+        size_t off = 0;
+        while (off < c->used) {
+            ssize_t w = write(c->fd, c->buf + off, c->used - off);
+            if (w < 0 && errno == EINTR)
+                continue;
+            if (w < 0)
+                return -errno;
+            off += (size_t)w;
+        }
+    } else {
+        int rc = bcp_eventset_feed(c->set, c->st, c->buf, c->used);
+        if (rc)
+            return rc;
+    }
+    c->used = 0;
+    return 0;
+}
+
+static int visit(const char *fpath, const struct stat *sb, int typeflag, struct FTW *ftw)
+{
+    (void)ftw;
+    scan_ctx *c = g_scan;
+    if (typeflag != FTW_F)
+        return 0;
+    const char *rel = fpath + c->prefix;
+    const size_t len = strlen(rel);
+    if (len == 0 || len > BCP_PDB_MAX_KEY)
+        return 0;
+    const uint64_t f[4] = {(uint64_t)(int64_t)sb->st_mtime, (uint64_t)sb->st_size, 'm', len};
+    if (sizeof(f) + len + c->used >= sizeof(c->buf) && (c->rc = flush_scan(c)))
+        return 1;
+    memcpy(c->buf + c->used, f, sizeof(f));
+    memcpy(c->buf + c->used + sizeof(f), rel, len);
+    c->used += sizeof(f) + len;
+    c->nrec++;
+    return 0;
+}
+
+static int scan(const char *chunks_dir, int fd, bcp_eventset *set, int st, uint64_t *nrec)
+{
+    if (!chunks_dir || (fd < 0 && !set))
+        return -EINVAL;
+    struct stat sb;
+    if (stat(chunks_dir, &sb) != 0)
+        return -errno;
+    if (!S_ISDIR(sb.st_mode))
+        return -ENOTDIR;
+    scan_ctx *c = calloc(1, sizeof(*c));
+    if (!c)
+        return -ENOMEM;
+    c->fd = fd;
+    c->set = set;
+    c->st = st;
+    size_t dl = strlen(chunks_dir);
+    while (dl > 1 && chunks_dir[dl - 1] == '/')
+        dl--;
+    c->prefix = dl + 1;
+    char *root = strndup(chunks_dir, dl);
+    if (!root) {
+        free(c);
+        return -ENOMEM;
+    }
+    pthread_mutex_lock(&g_scan_lock);
+    g_scan = c;
+    int r = nftw(root, visit, 100, FTW_PHYS); /* ftw(".", visitor, 100) in the reference */
+    g_scan = NULL;
+    pthread_mutex_unlock(&g_scan_lock);
+    int rc = c->rc;
+    if (!rc && r < 0)
+        rc = -errno;
+    if (!rc)
+        rc = flush_scan(c);
+    if (nrec)
+        *nrec = c->nrec;
+    free(root);
+    free(c);
+    return rc;
+}
+
+int bcp_scan_chunks(const char *chunks_dir, int out_fd, uint64_t *nrecords)
+{
+    if (out_fd < 0)
+        return -EINVAL;
+    return scan(chunks_dir, out_fd, NULL, 0, nrecords);
+}
+
+int bcp_eventset_scan(bcp_eventset *s, int st, const char *chunks_dir, uint64_t *nrecords)
+{
+    if (!s || st < 0 || st >= MAX_STORAGE_TARGETS)
+        return -EINVAL;
+    return scan(chunks_dir, -1, s, st, nrecords);
+}
+
+/* ---- storage-target bookkeeping (gen/main.c:472-551) ------------------- */
+
+#define RUN_MAGIC "BCPRUN01"
+
+typedef struct {
+    char magic[8];
+    uint32_t version;    /* GIT_VERSION stamp of the writer: BCP_ABI_VERSION here */
+    uint32_t ntargets;
+    int32_t ids[MAX_STORAGE_TARGETS];
+} run_data;
+
+static int read_target_id(const char *root, int k, int32_t *id)
+{
+    char p[4096];
+    int n = snprintf(p, sizeof(p), "%s/st%d/targetNumID", root, k);
+    if (n < 0 || (size_t)n >= sizeof(p))
+        return -ENAMETOOLONG;
+    FILE *f = fopen(p, "r");
+    if (!f) {
+        if (errno != ENOENT)
+            return -errno;
+        *id = k + 1; /* a store without the file: its position is its identity */
+        return 0;
+    }
+    char s[20] = {0};
+    size_t got = fread(s, 1, sizeof(s) - 1, f); /* read(target_ID_fd, targetID_s, 20) */
+    fclose(f);
+    if (!got)
+        return -EPROTO;
+    *id = atoi(s);
+    return 0;
+}
+
+int bcp_check_targets(const char *store_root, int ntargets, const char *run_data_path, FILE *log)
+{
+    if (!store_root || !run_data_path || ntargets < 1 || ntargets > MAX_STORAGE_TARGETS)
+        return -EINVAL;
+    run_data cur;
+    memset(&cur, 0, sizeof(cur));
+    memcpy(cur.magic, RUN_MAGIC, 8);
+    cur.version = BCP_TASK_ABI_VERSION;
+    cur.ntargets = (uint32_t)ntargets;
+    for (int k = 0; k < ntargets; k++) {
+        int rc = read_target_id(store_root, k, &cur.ids[k]);
+        if (rc)
+            return rc;
+        for (int j = 0; j < k; j++)
+            if (cur.ids[j] == cur.ids[k]) {
+                if (log)
+                    fprintf(log, "Duplicate targetNumID = %d\n", cur.ids[k]);
+                return -EEXIST;
+            }
+    }
+    run_data last;
+    memset(&last, 0, sizeof(last));
+    int fd = open(run_data_path, O_RDWR | O_CREAT | O_CLOEXEC, 0600);
+    if (fd < 0)
+        return -errno;
+    ssize_t got = read(fd, &last, sizeof(last));
+    if (got == (ssize_t)sizeof(last) && !memcmp(last.magic, RUN_MAGIC, 8)) {
+        if (last.version != cur.version) {
+            if (log)
+                fprintf(log, "Version mismatch\n");
+            close(fd);
+            return -EPROTO;
+        }
+        if (cur.ntargets < last.ntargets) {
+            if (log)
+                fprintf(log, "Fewer targets than last run, something is wrong!\n");
+            close(fd);
+            return -ENODEV;
+        }
+        /* targets keep their storage-target index across runs; new ones are
+         * appended (gen/main.c:508-526) -- with fixed <root>/st<k> stores an
+         * index whose id changed is a lost target */
+        for (uint32_t k = 0; k < last.ntargets; k++)
+            if (last.ids[k] != cur.ids[k]) {
+                if (log)
+                    fprintf(log, "Storage target missing! targetNumID = %d\n", last.ids[k]);
+                close(fd);
+                return -ENODEV;
+            }
+    } else if (got != 0) {
+        close(fd);
+        return -EPROTO;
+    }
+    int rc = 0;
+    if (pwrite(fd, &cur, sizeof(cur), 0) != (ssize_t)sizeof(cur))
+        rc = -EIO;
+    close(fd);
+    return rc;
+}

@@ -1,0 +1,220 @@
+/*
+ * bcp_tool.c -- command-line front end (bin/bcp) over libbcp.so for
+ * loopback stores <root>/st<k>/{chunks,parity,db}: the single-node
+ * counterpart of the reference's programs.
+ *
+ *   bcp find-all-chunks <chunks_dir>
+ *       bp-find-all-chunks: the record stream on stdout.
+ *   bcp parity-gen --complete|--partial [--pipeline] [--lanes N] [--force]
+ *                  [--changelog DIR] <store_root> <ntargets>
+ *       beegfs-parity-gen + bp-parity-gen (src/beegfs-parity-gen:1-135,
+ *       gen/main.c): target bookkeeping, phase 1 from a scan of every
+ *       target (--complete) or from record files DIR/st<k> (--partial,
+ *       default DIR = <root>/changelog), then one round against the
+ *       persistent state, through the per-rank protocol (default, 12 lanes)
+ *       or the batched pipeline.  A --complete over an existing state needs
+ *       --force and first deletes the old parity data and DBs (the script's
+ *       clean_old, :94-108, :120-126).  On success <root>/last-gen-timestamp.
+ *   bcp parity-rebuild [--db DIR] [--corrupt FILE] <store_root> <ntargets> <target>
+ *       beegfs-parity-rebuild + bp-parity-rebuild (rebuild/main.c).
+ *
+ * Exit status 0 on success, 1 on any error (message on stderr).
+ */
+#define _GNU_SOURCE
+#include <errno.h>
+#include <ftw.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/stat.h>
+#include <time.h>
+#include <unistd.h>
+
+#include "bcp_task.h"
+
+static int usage(void)
+{
+    fputs("usage: bcp find-all-chunks <chunks_dir>\n"
+          "       bcp parity-gen --complete|--partial [--pipeline] [--lanes N] [--force]\n"
+          "                      [--changelog DIR] <store_root> <ntargets>\n"
+          "       bcp parity-rebuild [--db DIR] [--corrupt FILE] <store_root> <ntargets> <target>\n",
+          stderr);
+    return 1;
+}
+
+static int fail(const char *what, int rc)
+{
+    fprintf(stderr, "bcp: %s: %s\n", what, strerror(rc < 0 ? -rc : rc));
+    return 1;
+}
+
+static int rm_visit(const char *p, const struct stat *sb, int flag, struct FTW *ftw)
+{
+    (void)sb;
+    (void)flag;
+    if (ftw->level == 0)
+        return 0; /* keep the directory itself */
+    return remove(p) != 0 && errno != ENOENT;
+}
+
+static int clear_dir(const char *dir)
+{
+    struct stat sb;
+    if (stat(dir, &sb) != 0)
+        return errno == ENOENT ? 0 : -errno;
+    return nftw(dir, rm_visit, 64, FTW_DEPTH | FTW_PHYS) == 0 ? 0 : -EIO;
+}
+
+static int cmd_find(int argc, char **argv)
+{
+    if (argc != 1)
+        return usage();
+    int rc = bcp_scan_chunks(argv[0], STDOUT_FILENO, NULL);
+    return rc ? fail("find-all-chunks", rc) : 0;
+}
+
+static int cmd_gen(int argc, char **argv)
+{
+    int complete = -1, use_pipeline = 0, lanes = 12, force = 0;
+    const char *changelog = NULL;
+    int i = 0;
+    for (; i < argc && argv[i][0] == '-'; i++) {
+        if (!strcmp(argv[i], "--complete"))
+            complete = 1;
+        else if (!strcmp(argv[i], "--partial"))
+            complete = 0;
+        else if (!strcmp(argv[i], "--pipeline"))
+            use_pipeline = 1;
+        else if (!strcmp(argv[i], "--force"))
+            force = 1;
+        else if (!strcmp(argv[i], "--lanes") && i + 1 < argc)
+            lanes = atoi(argv[++i]);
+        else if (!strcmp(argv[i], "--changelog") && i + 1 < argc)
+            changelog = argv[++i];
+        else
+            return usage();
+    }
+    if (complete < 0 || argc - i != 2)
+        return usage();
+    const char *root = argv[i];
+    const int ntargets = atoi(argv[i + 1]);
+    if (ntargets < 1 || ntargets > MAX_STORAGE_TARGETS || lanes < 1 || lanes > 64)
+        return usage();
+    char p[4096];
+    snprintf(p, sizeof(p), "%s/run_data", root);
+    int rc = bcp_check_targets(root, ntargets, p, stderr);
+    if (rc)
+        return fail("storage targets", rc);
+    char ts_path[4096];
+    snprintf(ts_path, sizeof(ts_path), "%s/last-gen-timestamp", root);
+    struct stat sb;
+    if (complete && stat(ts_path, &sb) == 0) {
+        if (!force) {
+            fputs("bcp: a complete run has already been done; --force deletes all existing parity data\n", stderr);
+            return 1;
+        }
+        for (int k = 0; k < ntargets; k++) {
+            snprintf(p, sizeof(p), "%s/st%d/parity", root, k);
+            if ((rc = clear_dir(p)))
+                return fail("removing old parity data", rc);
+            snprintf(p, sizeof(p), "%s/st%d/db", root, k);
+            if ((rc = clear_dir(p)))
+                return fail("removing old parity databases", rc);
+        }
+    }
+    const time_t started = time(NULL);
+    bcp_eventset *es = NULL;
+    if ((rc = bcp_eventset_create(&es)))
+        return fail("event set", rc);
+    uint64_t nrec = 0;
+    for (int k = 0; k < ntargets && !rc; k++) {
+        if (complete) {
+            uint64_t n = 0;
+            snprintf(p, sizeof(p), "%s/st%d/chunks", root, k);
+            rc = bcp_eventset_scan(es, k, p, &n);
+            nrec += n;
+        } else {
+            if (changelog)
+                snprintf(p, sizeof(p), "%s/st%d", changelog, k);
+            else
+                snprintf(p, sizeof(p), "%s/changelog/st%d", root, k);
+            if (stat(p, &sb) == 0)
+                rc = bcp_eventset_feed_file(es, k, p);
+        }
+    }
+    if (rc) {
+        bcp_eventset_destroy(es);
+        return fail(complete ? "scanning chunks" : "reading changelog", rc);
+    }
+    printf("Total number of events found: %8zu\n", bcp_eventset_count(es));
+    bcp_run_stats st;
+    memset(&st, 0, sizeof(st));
+    size_t planned = 0;
+    if (use_pipeline) {
+        bcp_pipeline *pl = NULL;
+        rc = bcp_pipeline_create(NULL, &pl);
+        if (!rc)
+            rc = bcp_gen_round_pipeline(pl, root, ntargets, es, NULL, stderr, &st, &planned);
+        if (pl)
+            bcp_pipeline_destroy(pl);
+    } else {
+        rc = bcp_gen_round(root, ntargets, es, NULL, lanes, stderr, &st, &planned);
+        bcp_task_shutdown();
+    }
+    bcp_eventset_destroy(es);
+    if (rc)
+        return fail("parity generation", rc);
+    printf("worklist %zu items, %llu tasks, %.3f s, %.1f MiB read, %.1f MiB written, %d rank errors\n", planned,
+           (unsigned long long)st.tasks, st.seconds, st.bytes_read / 1048576.0, st.bytes_written / 1048576.0,
+           st.errors);
+    if (st.errors)
+        return 1;
+    FILE *f = fopen(ts_path, "w");
+    if (!f)
+        return fail("last-gen-timestamp", errno);
+    fprintf(f, "%lld\n", (long long)started);
+    fclose(f);
+    (void)nrec;
+    return 0;
+}
+
+static int cmd_rebuild(int argc, char **argv)
+{
+    const char *db = NULL, *corrupt = NULL;
+    int i = 0;
+    for (; i < argc && argv[i][0] == '-'; i++) {
+        if (!strcmp(argv[i], "--db") && i + 1 < argc)
+            db = argv[++i];
+        else if (!strcmp(argv[i], "--corrupt") && i + 1 < argc)
+            corrupt = argv[++i];
+        else
+            return usage();
+    }
+    if (argc - i != 3)
+        return usage();
+    const char *root = argv[i];
+    const int ntargets = atoi(argv[i + 1]), target = atoi(argv[i + 2]);
+    bcp_run_stats st;
+    memset(&st, 0, sizeof(st));
+    int rc = bcp_rebuild_run_db(root, ntargets, target, db, corrupt, stderr, &st);
+    bcp_task_shutdown();
+    if (rc)
+        return fail("rebuild", rc);
+    printf("rebuilt target %d: %llu tasks, %.3f s, %.1f MiB read, %.1f MiB written, %d rank errors\n", target,
+           (unsigned long long)st.tasks, st.seconds, st.bytes_read / 1048576.0, st.bytes_written / 1048576.0,
+           st.errors);
+    return st.errors ? 1 : 0;
+}
+
+int main(int argc, char **argv)
+{
+    if (argc < 2)
+        return usage();
+    if (!strcmp(argv[1], "find-all-chunks"))
+        return cmd_find(argc - 2, argv + 2);
+    if (!strcmp(argv[1], "parity-gen"))
+        return cmd_gen(argc - 2, argv + 2);
+    if (!strcmp(argv[1], "parity-rebuild"))
+        return cmd_rebuild(argc - 2, argv + 2);
+    return usage();
+}

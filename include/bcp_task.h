@@ -227,6 +227,19 @@ int bcp_store_weight(int dirfd);
 int bcp_plan_worklist(const bcp_eventset *s, int ntargets, const int *cum_weight, const bcp_work_item *prev,
                       size_t nprev, bcp_work_item *out, size_t out_cap, size_t *nout);
 
+/* bp-find-all-chunks (src/bp-find-all-chunks/main.c:17-45): one 'm' record
+ * per regular file under chunks_dir, path relative to it, written to out_fd
+ * in the record format above -- or fed straight into an event set as target
+ * st's stream (the --complete input of phase 1, gen/main.c:622-624). */
+int bcp_scan_chunks(const char *chunks_dir, int out_fd, uint64_t *nrecords);
+int bcp_eventset_scan(bcp_eventset *s, int st, const char *chunks_dir, uint64_t *nrecords);
+/* Storage-target bookkeeping of gen/main.c:472-551 over <root>/st<k>: ids
+ * from st<k>/targetNumID (k+1 when absent), checked against and saved to
+ * run_data_path.  -EEXIST duplicate id, -ENODEV fewer targets or a target
+ * whose id changed ("Storage target missing!"), -EPROTO version stamp. */
+#define BCP_TASK_ABI_VERSION 1
+int bcp_check_targets(const char *store_root, int ntargets, const char *run_data_path, FILE *log);
+
 /* Cumulative store weights st_weight (gen/main.c:485, 528-536) of
  * <root>/st<k>, k < ntargets. */
 int bcp_store_cum_weights(const char *store_root, int ntargets, int *cum_weight);

@@ -219,3 +219,60 @@ def test_db_round_then_partial_round_then_rebuild(bcp, oracle, tmp_path, engine_
     assert st.errors == 0
     for path, data in lost.items():
         assert S.read_file(S.chunk_path(root, victim, path)) == data, path
+
+
+@pytest.mark.parametrize("pipeline", [False, True])
+def test_cli_complete_partial_rebuild(bcp, oracle, tmp_path, pipeline):
+    """bin/bcp end to end on the device: --complete (scan of every target),
+    --partial from changelog record files, then parity-rebuild from the DB."""
+    import subprocess
+    import planner as PL
+    rng = np.random.default_rng(21)
+    root, nt = str(tmp_path / "store"), 6
+    S.make_store(root, nt)
+    files, contents = {}, {}
+    for i in range(20):
+        path = f"u{i % 2}/{i:02X}/c{i}"
+        holders = sorted(int(x) for x in rng.choice(nt, size=int(rng.integers(1, nt)), replace=False))
+        arrs = []
+        for h in holders:
+            d = S.synthetic_chunk(i * 13 + h, int(rng.integers(1, 300_000)))
+            S.write_chunk(root, h, path, d)
+            arrs.append(d)
+        files[path], contents[path] = holders, arrs
+    flags = ["--pipeline"] if pipeline else []
+    r = subprocess.run([bcp.BIN_PATH, "parity-gen", "--complete", *flags, root, str(nt)], capture_output=True)
+    assert r.returncode == 0, r.stderr
+    db = bcp.PDB(os.path.join(root, "st0", "db"))
+    placed = {k.decode(): loc for k, _, loc in db.items()}
+    db.close()
+    for path, holders in files.items():
+        assert placed[path] & PL.L_MASK == sum(1 << h for h in holders)
+        assert S.read_file(S.parity_path(root, PL.get_p(placed[path]), path)) == \
+            oracle.gen_parity_file(contents[path]), path
+    # a second --complete needs --force
+    r = subprocess.run([bcp.BIN_PATH, "parity-gen", "--complete", *flags, root, str(nt)], capture_output=True)
+    assert r.returncode == 1
+    # --partial: one chunk rewritten, its record in the changelog of its target
+    path = "u1/03/c3"
+    h = files[path][0]
+    new = S.synthetic_chunk(999, 123_457)
+    S.write_chunk(root, h, path, new)
+    contents[path][0] = new
+    os.makedirs(os.path.join(root, "changelog"))
+    with open(os.path.join(root, "changelog", f"st{h}"), "wb") as f:
+        f.write(bcp.pack_records([(2_000_000_000, len(new), "m", path)]))
+    r = subprocess.run([bcp.BIN_PATH, "parity-gen", "--partial", *flags, root, str(nt)], capture_output=True)
+    assert r.returncode == 0, r.stderr
+    assert S.read_file(S.parity_path(root, PL.get_p(placed[path]), path)) == oracle.gen_parity_file(contents[path])
+    # lose a target, rebuild it from the DB
+    victim = 2
+    lost = {}
+    for p_, holders in files.items():
+        if victim in holders:
+            lost[p_] = S.read_file(S.chunk_path(root, victim, p_))
+            os.remove(S.chunk_path(root, victim, p_))
+    r = subprocess.run([bcp.BIN_PATH, "parity-rebuild", root, str(nt), str(victim)], capture_output=True)
+    assert r.returncode == 0, r.stderr
+    for p_, data in lost.items():
+        assert S.read_file(S.chunk_path(root, victim, p_)) == data, p_
