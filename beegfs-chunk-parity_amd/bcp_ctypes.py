@@ -47,7 +47,7 @@ class RunStats(ctypes.Structure):
 
 class PipelineOpts(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int), ("slab_bytes", ctypes.c_size_t), ("io_threads", ctypes.c_int),
-                ("nslots", ctypes.c_int)]
+                ("nslots", ctypes.c_int), ("ndevices", ctypes.c_int)]
 
 
 XOR_HOOK = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t,
@@ -482,11 +482,11 @@ class PDB:
 
 
 def pipeline_gen(store_root: str, ntargets: int, items, device: int = 0, slab_bytes: int = 256 << 20,
-                 io_threads: int = 8, nslots: int = 3, log=None) -> RunStats:
+                 io_threads: int = 8, nslots: int = 3, log=None, ndevices: int = 1) -> RunStats:
     """Batched end-to-end parity generation (bcp_pipeline_gen)."""
     arr, keep = _items(items)
     st = RunStats()
-    opts = PipelineOpts(device, slab_bytes, io_threads, nslots)
+    opts = PipelineOpts(device, slab_bytes, io_threads, nslots, ndevices)
     rc = lib().bcp_pipeline_gen(store_root.encode(), ntargets, arr, len(items), ctypes.byref(opts), log,
                                 ctypes.byref(st))
     check("bcp_pipeline_gen", rc)
@@ -497,9 +497,10 @@ def pipeline_gen(store_root: str, ntargets: int, items, device: int = 0, slab_by
 class Pipeline:
     """Long-lived batched pipeline (bcp_pipeline_create / run / destroy)."""
 
-    def __init__(self, device: int = 0, slab_bytes: int = 256 << 20, io_threads: int = 8, nslots: int = 3):
+    def __init__(self, device: int = 0, slab_bytes: int = 256 << 20, io_threads: int = 8, nslots: int = 3,
+                 ndevices: int = 1):
         h = _V()
-        opts = PipelineOpts(device, slab_bytes, io_threads, nslots)
+        opts = PipelineOpts(device, slab_bytes, io_threads, nslots, ndevices)
         call("bcp_pipeline_create", ctypes.byref(opts), ctypes.byref(h))
         self.h = h
 

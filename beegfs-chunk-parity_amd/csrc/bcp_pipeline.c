@@ -15,7 +15,10 @@
  *
  * Slots are recycled round-robin, so batch b+1 is read while batch b is on
  * the device and batch b-1 is being written; H2D and D2H run on their own
- * queues beside the kernel (PCIe is full duplex).
+ * queues beside the kernel (PCIe is full duplex).  With ndevices > 1 the
+ * batches go round-robin to the node's GPUs (each with its own engine, queues
+ * and slots; stripes are independent, so nothing crosses GPUs): PCIe, not the
+ * kernel, bounds this path, and every GPU brings its own link.
  *
  * Output files are byte-identical to parity_generator's
  * (task_processing.c:146-226): header in ascending storage-target order, then
@@ -384,18 +387,37 @@ static void slot_free(bcp_engine *e, slot *s)
         bcp_event_destroy(s->ev_d);
 }
 
-struct bcp_pipeline {
-    bcp_pipeline_opts o;
+/* One GPU of the pipeline: engine, h2d / compute / d2h queues, slots. */
+typedef struct {
     bcp_engine *eng;
     bcp_queue *qh, *qk, *qd;
+    slot *slots;
+} dev_lane;
+
+struct bcp_pipeline {
+    bcp_pipeline_opts o;
+    int ndev;
+    dev_lane *dev;
     pool readers, writers, completer;
     int pools;
-    slot *slots;
     size_t in_cap, out_cap;
     bcp_stripe *st;
     bcp_source *so;
     size_t desc_cap;    /* stripes the descriptor arrays hold */
 };
+
+static void free_slots(bcp_pipeline *pl)
+{
+    for (int d = 0; d < pl->ndev; d++) {
+        dev_lane *L = &pl->dev[d];
+        if (!L->slots)
+            continue;
+        for (int s = 0; s < pl->o.nslots; s++)
+            slot_free(L->eng, &L->slots[s]);
+        free(L->slots);
+        L->slots = NULL;
+    }
+}
 
 int bcp_pipeline_destroy(bcp_pipeline *pl)
 {
@@ -406,19 +428,21 @@ int bcp_pipeline_destroy(bcp_pipeline *pl)
         pool_stop(&pl->completer);
         pool_stop(&pl->writers);
     }
-    if (pl->slots) {
-        for (int s = 0; s < pl->o.nslots; s++)
-            slot_free(pl->eng, &pl->slots[s]);
-        free(pl->slots);
+    if (pl->dev) {
+        free_slots(pl);
+        for (int d = 0; d < pl->ndev; d++) {
+            dev_lane *L = &pl->dev[d];
+            if (L->qh)
+                bcp_queue_destroy(L->qh);
+            if (L->qk)
+                bcp_queue_destroy(L->qk);
+            if (L->qd)
+                bcp_queue_destroy(L->qd);
+            if (L->eng)
+                bcp_engine_destroy(L->eng);
+        }
+        free(pl->dev);
     }
-    if (pl->qh)
-        bcp_queue_destroy(pl->qh);
-    if (pl->qk)
-        bcp_queue_destroy(pl->qk);
-    if (pl->qd)
-        bcp_queue_destroy(pl->qd);
-    if (pl->eng)
-        bcp_engine_destroy(pl->eng);
     free(pl->st);
     free(pl->so);
     free(pl);
@@ -427,23 +451,21 @@ int bcp_pipeline_destroy(bcp_pipeline *pl)
 
 static int ensure_slots(bcp_pipeline *pl, size_t in_cap, size_t out_cap)
 {
-    if (pl->slots && in_cap <= pl->in_cap && out_cap <= pl->out_cap)
+    if (pl->dev[0].slots && in_cap <= pl->in_cap && out_cap <= pl->out_cap)
         return 0;
-    if (pl->slots) {
-        for (int s = 0; s < pl->o.nslots; s++)
-            slot_free(pl->eng, &pl->slots[s]);
-        free(pl->slots);
-        pl->slots = NULL;
-    }
+    free_slots(pl);
     in_cap = in_cap > pl->in_cap ? in_cap : pl->in_cap;
     out_cap = out_cap > pl->out_cap ? out_cap : pl->out_cap;
-    pl->slots = calloc((size_t)pl->o.nslots, sizeof(slot));
-    if (!pl->slots)
-        return -ENOMEM;
-    for (int s = 0; s < pl->o.nslots; s++) {
-        int rc = slot_alloc(pl->eng, &pl->slots[s], in_cap, out_cap);
-        if (rc)
-            return rc;
+    for (int d = 0; d < pl->ndev; d++) {
+        dev_lane *L = &pl->dev[d];
+        L->slots = calloc((size_t)pl->o.nslots, sizeof(slot));
+        if (!L->slots)
+            return -ENOMEM;
+        for (int s = 0; s < pl->o.nslots; s++) {
+            int rc = slot_alloc(L->eng, &L->slots[s], in_cap, out_cap);
+            if (rc)
+                return rc;
+        }
     }
     pl->in_cap = in_cap;
     pl->out_cap = out_cap;
@@ -455,9 +477,15 @@ int bcp_pipeline_create(const bcp_pipeline_opts *opts_in, bcp_pipeline **out)
     if (!out)
         return -EINVAL;
     *out = NULL;
-    bcp_pipeline_opts o = {0, 256u << 20, 8, 3};
+    bcp_pipeline_opts o = {0, 256u << 20, 8, 3, 1};
     if (opts_in)
         o = *opts_in;
+    if (o.ndevices < 1)
+        o.ndevices = 1;
+    int ndev_vis = 0;
+    bcp_device_count(&ndev_vis);
+    if (o.device < 0 || o.ndevices > 64)
+        return -EINVAL;
     if (o.slab_bytes < (1u << 20))
         o.slab_bytes = 1u << 20;
     if (o.io_threads < 1)
@@ -472,10 +500,22 @@ int bcp_pipeline_create(const bcp_pipeline_opts *opts_in, bcp_pipeline **out)
     if (!pl)
         return -ENOMEM;
     pl->o = o;
-    int rc;
-    if ((rc = bcp_engine_create(o.device, &pl->eng)) || (rc = bcp_queue_create(pl->eng, &pl->qh)) ||
-        (rc = bcp_queue_create(pl->eng, &pl->qk)) || (rc = bcp_queue_create(pl->eng, &pl->qd)))
-        goto fail;
+    int rc = 0;
+    pl->dev = calloc((size_t)o.ndevices, sizeof(dev_lane));
+    if (!pl->dev) {
+        free(pl);
+        return -ENOMEM;
+    }
+    pl->ndev = o.ndevices;
+    for (int d = 0; d < pl->ndev; d++) {
+        dev_lane *L = &pl->dev[d];
+        /* devices wrap modulo the visible count: more lanes than GPUs runs
+         * several lanes per GPU (how the multi-device path is tested on one) */
+        const int dev = ndev_vis > 0 ? (o.device + d) % ndev_vis : o.device + d;
+        if ((rc = bcp_engine_create(dev, &L->eng)) || (rc = bcp_queue_create(L->eng, &L->qh)) ||
+            (rc = bcp_queue_create(L->eng, &L->qk)) || (rc = bcp_queue_create(L->eng, &L->qd)))
+            goto fail;
+    }
     if ((rc = pool_start(&pl->readers, o.io_threads)) || (rc = pool_start(&pl->writers, o.io_threads)) ||
         (rc = pool_start(&pl->completer, 1)))
         goto fail;
@@ -606,7 +646,8 @@ int bcp_pipeline_run(bcp_pipeline *pl, const char *store_root, int ntargets, con
     /* 3. stream the batches through the slots */
     size_t first = 0;
     for (int b = 0; b < nbatches && !rc; b++) {
-        slot *S = &pl->slots[b % nslots];
+        dev_lane *L = &pl->dev[b % pl->ndev];
+        slot *S = &L->slots[(b / pl->ndev) % nslots];
         if (S->busy) { /* writes of batch b - nslots still running */
             latch_wait(&S->writes);
             latch_destroy(&S->writes);
@@ -644,12 +685,12 @@ int bcp_pipeline_run(bcp_pipeline *pl, const char *store_root, int ntargets, con
                 out_used = t->out_off + RUP(t->max_cs);
         }
         /* device: H2D (side queue) -> kernel -> D2H (side queue) */
-        if ((rc = bcp_h2d_async(pl->qh, S->d_in, S->h_in, (size_t)in_used)) ||
-            (rc = bcp_event_record(S->ev_h, pl->qh)) || (rc = bcp_queue_wait_event(pl->qk, S->ev_h)) ||
-            (rc = bcp_xor_stripes_async(pl->qk, st, ns, so, nsrc)) || (rc = bcp_event_record(S->ev_k, pl->qk)) ||
-            (rc = bcp_queue_wait_event(pl->qd, S->ev_k)) ||
-            (rc = bcp_d2h_async(pl->qd, S->h_out, S->d_out, (size_t)out_used)) ||
-            (rc = bcp_event_record(S->ev_d, pl->qd)))
+        if ((rc = bcp_h2d_async(L->qh, S->d_in, S->h_in, (size_t)in_used)) ||
+            (rc = bcp_event_record(S->ev_h, L->qh)) || (rc = bcp_queue_wait_event(L->qk, S->ev_h)) ||
+            (rc = bcp_xor_stripes_async(L->qk, st, ns, so, nsrc)) || (rc = bcp_event_record(S->ev_k, L->qk)) ||
+            (rc = bcp_queue_wait_event(L->qd, S->ev_k)) ||
+            (rc = bcp_d2h_async(L->qd, S->h_out, S->d_out, (size_t)out_used)) ||
+            (rc = bcp_event_record(S->ev_d, L->qd)))
             break;
         /* writers start once the batch's D2H is done (completion thread);
          * the host moves on to reading batch b+1 meanwhile */
@@ -663,11 +704,14 @@ int bcp_pipeline_run(bcp_pipeline *pl, const char *store_root, int ntargets, con
         ntasks += last - first;
         first = last;
     }
-    for (int s = 0; s < nslots; s++)
-        if (pl->slots[s].busy) {
-            latch_wait(&pl->slots[s].writes);
-            latch_destroy(&pl->slots[s].writes);
-            pl->slots[s].busy = 0;
+    for (int d = 0; d < pl->ndev; d++)
+        for (int s = 0; s < nslots; s++) {
+            slot *S = &pl->dev[d].slots[s];
+            if (S->busy) {
+                latch_wait(&S->writes);
+                latch_destroy(&S->writes);
+                S->busy = 0;
+            }
         }
     if (!rc && dev_rc)
         rc = dev_rc;

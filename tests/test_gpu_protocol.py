@@ -276,3 +276,26 @@ def test_cli_complete_partial_rebuild(bcp, oracle, tmp_path, pipeline):
     assert r.returncode == 0, r.stderr
     for p_, data in lost.items():
         assert S.read_file(S.chunk_path(root, victim, p_)) == data, p_
+
+
+@pytest.mark.parametrize("ndevices", [2, 3])
+def test_pipeline_multi_device_lanes(bcp, oracle, tmp_path, ndevices):
+    """Batches round-robin over several device lanes (on a one-GPU box the
+    lanes wrap onto the same GPU, each with its own engine, queues and
+    slots); small slabs force many batches so every lane and slot recycles."""
+    rng = np.random.default_rng(ndevices)
+    files = []
+    for i in range(60):
+        holders, p = S.random_layout(rng, 9, int(rng.integers(1, 9)))
+        files.append((f"m/{i}", holders, p, [int(x) for x in rng.integers(0, 400_000, size=len(holders))]))
+    root = str(tmp_path)
+    items, contents = S.populate(root, 9, files, seed=ndevices)
+    pl = bcp.Pipeline(slab_bytes=1 << 20, io_threads=4, nslots=2, ndevices=ndevices)
+    try:
+        for _ in range(2):
+            st = pl.run(root, 9, items)
+            assert st.errors == 0 and st.tasks == len(files)
+            for (path, holders, p, lens) in files:
+                assert S.read_file(S.parity_path(root, p, path)) == oracle.gen_parity_file(contents[path]), path
+    finally:
+        pl.close()

@@ -117,8 +117,8 @@ def config1(a):
         ok &= run("protocol_cpu_fold_reference(oracle_xor_rows,12 lanes)", lambda: bcp.gen_run(root, 4, items, nlanes=12))
     finally:
         bcp.set_xor_hook(None)
-    pl = bcp.Pipeline(io_threads=a.io_threads)
-    ok &= run("pipeline(bcp_pipeline_run)", lambda: pl.run(root, 4, items))
+    pl = bcp.Pipeline(io_threads=a.io_threads, ndevices=a.ndevices)
+    ok &= run(f"pipeline(bcp_pipeline_run,{a.ndevices} GPU)", lambda: pl.run(root, 4, items))
     pl.close()
     # rebuild target 2 through the protocol
     lost = {}
@@ -160,7 +160,7 @@ def config5(a):
     ts0 = 1_700_000_000
     items = [(path, ts0, S.with_p(sum(1 << h for h in holders), p)) for path, holders, p, _ in files]
     rd, wr = total_bytes(root, files)
-    pl = bcp.Pipeline(io_threads=a.io_threads)
+    pl = bcp.Pipeline(io_threads=a.io_threads, ndevices=a.ndevices)
     times = []
     for r in range(1 + a.reps):
         t0 = time.perf_counter()
@@ -168,7 +168,7 @@ def config5(a):
         times.append(time.perf_counter() - t0)
     dt = float(np.median(times[1:])) if a.reps else times[0]
     ok, bad = verify(root, files, contents, a.verify, rng)
-    emit(config=5, path="pipeline_full_gen", cold_seconds=round(times[0], 3), warm_seconds=round(dt, 3),
+    emit(config=5, path=f"pipeline_full_gen({a.ndevices} GPU)", cold_seconds=round(times[0], 3), warm_seconds=round(dt, 3),
          GiBps=round((rd + wr) / dt / GiB, 3), bytes_read=rd, bytes_written=wr, tasks=int(st.tasks), verified=ok,
          bad=bad)
     # changelog: a seeded 10 % of stripes rewritten -> record streams per target
@@ -227,10 +227,13 @@ def main():
     ap.add_argument("--c1-files", type=int, default=1333)
     ap.add_argument("--c5-stripes", type=int, default=1000)
     ap.add_argument("--io-threads", type=int, default=16)
+    ap.add_argument("--ndevices", type=int, default=0, help="GPUs for the pipeline (0 = all visible)")
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--verify", type=int, default=20)
     ap.add_argument("--keep", action="store_true")
     a = ap.parse_args()
+    if a.ndevices <= 0:
+        a.ndevices = max(1, bcp.device_count())
     ok = True
     cfgs = a.configs.split(",")
     if "1" in cfgs:

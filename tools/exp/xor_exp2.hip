@@ -46,6 +46,7 @@ enum { MODE_XOR = 0, MODE_READ = 1, MODE_WRITE = 2 };
 struct Args {
   char *dst;
   const char *src;
+  uint64_t pitch;  // source row pitch (bytes); stripe pitch = NSRC * pitch
   uint32_t vps, tps, ntiles;
   unsigned long long *ctr;
   unsigned long long base;
@@ -59,7 +60,8 @@ __device__ __forceinline__ uint32_t grab(unsigned long long *ctr, unsigned long 
 template <int KB, int U, int LD, int ST, int DEFER, int MODE>
 __global__ __launch_bounds__(KB) void xe2(Args a) {
   constexpr uint32_t tile_v = KB * U;
-  const uint64_t S = (uint64_t)a.vps * 16;
+  const uint64_t S = a.pitch;
+  const uint64_t SO = (uint64_t)a.vps * 16;
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   __shared__ uint32_t next[2];
   if (threadIdx.x == 0) next[0] = grab(a.ctr, a.base);
@@ -75,7 +77,7 @@ __global__ __launch_bounds__(KB) void xe2(Args a) {
     const uint32_t s = t / a.tps;
     const uint32_t tin = t - s * a.tps;
     const char *sb = a.src + (uint64_t)s * NSRC * S;
-    v4u *db = reinterpret_cast<v4u *>(a.dst + (uint64_t)s * S);
+    v4u *db = reinterpret_cast<v4u *>(a.dst + (uint64_t)s * SO);
     const uint32_t vb = tin * tile_v + wave * 64 * U + lane;
     v4u acc[U];
     if constexpr (MODE == MODE_WRITE) {
@@ -131,7 +133,7 @@ __global__ __launch_bounds__(KB) void xe2(Args a) {
         if constexpr (ST == ST_NT) __builtin_nontemporal_store(acc[u], p);
         else if constexpr (ST == ST_PLAIN) *p = acc[u];
         else {
-          __amdgpu_buffer_rsrc_t w = __builtin_amdgcn_make_buffer_rsrc((void *)db, (short)0, (int)S, 0x00020000);
+          __amdgpu_buffer_rsrc_t w = __builtin_amdgcn_make_buffer_rsrc((void *)db, (short)0, (int)SO, 0x00020000);
           __builtin_amdgcn_raw_buffer_store_b128(acc[u], w, (int)((vb + u * 64) * 16), 0, ST == ST_BSC1 ? 16 : 17);
         }
       }
@@ -218,10 +220,25 @@ struct Entry {
   const char *name;
   KFn fn;
   int kb, u, mode, bpc;  // bpc: workgroups per CU launched
+  int pad;               // source row pitch = 512 KiB + pad (output unchanged)
 };
 
-#define X(name, KB, U, LD, ST, DEF, MODE, BPC) {name, xe2<KB, U, LD, ST, DEF, MODE>, KB, U, MODE, BPC}
+#define X(name, KB, U, LD, ST, DEF, MODE, BPC) {name, xe2<KB, U, LD, ST, DEF, MODE>, KB, U, MODE, BPC, 0}
+#define P(name, PAD) {name, xe2<256, 4, LD_GNT, ST_NT, 0, MODE_XOR>, 256, 4, MODE_XOR, 8, PAD}
 static const Entry kV[] = {
+#ifdef XE2_PITCH
+    X("base", 256, 4, LD_GNT, ST_NT, 0, MODE_XOR, 8),
+    P("pad256", 256),
+    P("pad1k", 1024),
+    P("pad4k", 4096),
+    P("pad8k", 8192),
+    P("pad16k", 16384),
+    P("pad64k", 65536),
+    P("pad3968", 3968),
+    P("pad12k", 12288),
+    {"read_only", xe2<256, 4, LD_GNT, ST_NONE, 0, MODE_READ>, 256, 4, MODE_READ, 8, 0},
+    {"read_only_pad4k", xe2<256, 4, LD_GNT, ST_NONE, 0, MODE_READ>, 256, 4, MODE_READ, 8, 4096},
+#else
     X("base", 256, 4, LD_GNT, ST_NT, 0, MODE_XOR, 8),
     X("read_only", 256, 4, LD_GNT, ST_NONE, 0, MODE_READ, 8),
     X("write_only", 256, 4, LD_GNT, ST_NT, 0, MODE_WRITE, 8),
@@ -237,8 +254,9 @@ static const Entry kV[] = {
     X("wg1024_u2", 1024, 2, LD_GNT, ST_NT, 0, MODE_XOR, 2),
     X("base_bpc4", 256, 4, LD_GNT, ST_NT, 0, MODE_XOR, 4),
     X("base_bpc6", 256, 4, LD_GNT, ST_NT, 0, MODE_XOR, 6),
-    {"lds_dma_u1", xe2_lds<1>, 256, 1, MODE_XOR, 8},
-    {"lds_dma_u2", xe2_lds<2>, 256, 2, MODE_XOR, 8},
+    {"lds_dma_u1", xe2_lds<1>, 256, 1, MODE_XOR, 8, 0},
+    {"lds_dma_u2", xe2_lds<2>, 256, 2, MODE_XOR, 8, 0},
+#endif
 };
 #undef X
 
@@ -247,12 +265,14 @@ int main(int argc, char **argv) {
   const int reps = argc > 2 ? atoi(argv[2]) : 5;
   const uint64_t S = 512 * 1024;
   const uint64_t in_bytes = stripes * NSRC * S, out_bytes = stripes * S;
+  const uint64_t max_pad = 65536;
+  const uint64_t alloc_in = stripes * NSRC * (S + max_pad);
   hipDeviceProp_t prop;
   CK(hipGetDeviceProperties(&prop, 0));
   const int cus = prop.multiProcessorCount;
   char *src, *dst, *ref;
   unsigned long long *ctr, *dcount;
-  CK(hipMalloc(&src, in_bytes));
+  CK(hipMalloc(&src, alloc_in));
   CK(hipMalloc(&dst, out_bytes));
   CK(hipMalloc(&ref, out_bytes));
   CK(hipMalloc(&ctr, 256));
@@ -260,7 +280,7 @@ int main(int argc, char **argv) {
   CK(hipMemset(ctr, 0, 256));
   hipStream_t st;
   CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-  hipLaunchKernelGGL(fill, dim3(cus * 8), dim3(256), 0, st, (uint64_t *)src, in_bytes / 8, 1ull);
+  hipLaunchKernelGGL(fill, dim3(cus * 8), dim3(256), 0, st, (uint64_t *)src, alloc_in / 8, 1ull);
   const uint32_t vps = S / 16;
   unsigned long long base = 0;
   const int nv = sizeof(kV) / sizeof(kV[0]);
@@ -268,6 +288,7 @@ int main(int argc, char **argv) {
     Args a;
     a.dst = out;
     a.src = src;
+    a.pitch = S + kV[v].pad;
     a.vps = vps;
     a.tps = vps / (kV[v].kb * kV[v].u);
     a.ntiles = (uint32_t)(stripes * a.tps);
@@ -289,7 +310,7 @@ int main(int argc, char **argv) {
     for (int v = 0; v < nv; v++) {
       if (r == 0) CK(hipMemsetAsync(dst, 0, out_bytes, st));
       launch(v, dst);
-      if (r == 0 && kV[v].mode == MODE_XOR) {
+      if (r == 0 && kV[v].mode == MODE_XOR && kV[v].pad == 0) {
         CK(hipMemsetAsync(dcount, 0, 8, st));
         hipLaunchKernelGGL(diff, dim3(cus * 4), dim3(256), 0, st, (const uint64_t *)dst, (const uint64_t *)ref,
                            out_bytes / 8, dcount);
@@ -315,9 +336,9 @@ int main(int argc, char **argv) {
     const double bytes = kV[v].mode == MODE_XOR ? (double)(in_bytes + out_bytes)
                          : kV[v].mode == MODE_READ ? (double)in_bytes : (double)out_bytes;
     printf("{\"variant\": \"%s\", \"wg\": %d, \"vecs\": %d, \"blocks_per_cu\": %d, \"median_ms\": %.4f, "
-           "\"min_ms\": %.4f, \"GBps\": %.1f, \"frac_8TBs\": %.4f, \"mismatch_words\": %lld}\n",
+           "\"min_ms\": %.4f, \"GBps\": %.1f, \"frac_8TBs\": %.4f, \"mismatch_words\": %lld, \"pad\": %d}\n",
            kV[v].name, kV[v].kb, kV[v].u, kV[v].bpc, med, ts[0], bytes / (med * 1e-3) / 1e9,
-           bytes / (med * 1e-3) / 8e12, bad[v]);
+           bytes / (med * 1e-3) / 8e12, bad[v], kV[v].pad);
   }
   return 0;
 }
