@@ -2,7 +2,8 @@
 """bench.py -- device-resident chunk-XOR parity throughput on MI355X.
 
 Workload (BASELINE.json configs[1], "config 2"): 12,500 stripes x 8 sources
-x 512 KiB (100,000 data chunks = 48.8 GiB) resident in HBM per GPU; one step
+x 512 KiB (100,000 data chunks = 48.8 GiB) resident in HBM per GPU (at 8
+GPUs config 4: 1,000,000 chunks = 15,625 stripes per GPU); one step
 = one pass of the parity kernel over all stripes (xor_stream<8,4>,
 the reference's xor_parity, task_processing.c:96-109, batched).
 `--mode rebuild` times config 3 instead (7 survivors + parity body ->
@@ -40,7 +41,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "beegfs-chunk-parity_amd"))
 
 import bcp_ctypes as bcp  # noqa: E402
-from bcp_dist import Dist  # noqa: E402
+from bcp_dist import Dist, shard_range  # noqa: E402
 
 KiB = 1024
 GiB = 1024 ** 3
@@ -54,7 +55,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--mode", choices=["gen", "rebuild", "mixed"], default="gen")
-    ap.add_argument("--stripes", type=int, default=12500, help="stripes per GPU")
+    ap.add_argument("--stripes", type=int, default=0,
+                    help="stripes per GPU (default: 12,500 = config 2; at 8 GPUs 15,625 = config 4's 1M chunks)")
     ap.add_argument("--nsrc", type=int, default=8)
     ap.add_argument("--chunk", type=int, default=512 * KiB)
     ap.add_argument("--blocks-per-cu", type=int, default=0)
@@ -96,6 +98,11 @@ def main():
         eng.option("schedule" if a.mode != "mixed" else "desc_schedule", a.schedule)
     cus, devname = eng.info()
     q = eng.queue()
+    # config 2 (100k chunks per GPU) up to 4 GPUs; at 8 GPUs config 4: 1,000,000
+    # chunks = 125,000 stripes sharded 15,625 per GPU (bcp_dist.shard_range)
+    if not a.stripes:
+        lo, hi = shard_range(125_000, d.world, d.rank)
+        a.stripes = hi - lo if d.world == 8 else 12_500
     S, N, C = a.stripes, a.nsrc, a.chunk
     chk = eng.alloc(64)
     if a.mode == "mixed":
@@ -147,7 +154,8 @@ def main():
         bytes_per_step = S * (N + 1) * C
         kernel = f"xor_stream<{N},U,strided>"
         kernel_tag = f"xor_stream<{N}, "
-        workload = f"config2: parity gen, {S} stripes x {N} x {C // KiB} KiB device-resident"
+        cfg = "config4" if d.world == 8 and S == 15_625 else "config2"
+        workload = f"{cfg}: parity gen, {S} stripes x {N} x {C // KiB} KiB device-resident per GPU"
     else:
         # config 3: parity first, then rebuild source index 3 from the other
         # N-1 chunks + parity body (descriptor kernel; truncation to 512 KiB).
