@@ -96,6 +96,14 @@ static int grid_for(const bcp_engine *e) {
   return g > 0 ? g : 256;
 }
 
+static int desc_grid_for(const bcp_engine *e) {
+  int g = e->num_cus * e->tuning.desc_blocks_per_cu;
+  return g > 0 ? g : 256;
+}
+
+static bool stream_vecs_ok(int v) { return v == 1 || v == 2 || v == 4 || v == 8; }
+static bool desc_vecs_ok(int v) { return v == 1 || v == 2 || v == 4; }
+
 static bool aligned16(uint64_t x) { return (x & 15u) == 0; }
 
 // Reserve a ring slot of at least `bytes`; waits only if that slot's
@@ -164,8 +172,7 @@ extern "C" int bcp_engine_create(int device, bcp_engine **out) {
   if (const char *v = getenv("BCP_VECS_PER_THREAD")) e->tuning.vecs_per_thread = atoi(v);
   const Tuning defaults;
   if (e->tuning.blocks_per_cu < 1 || e->tuning.blocks_per_cu > 32) e->tuning.blocks_per_cu = defaults.blocks_per_cu;
-  if (e->tuning.vecs_per_thread != 1 && e->tuning.vecs_per_thread != 2 && e->tuning.vecs_per_thread != 4)
-    e->tuning.vecs_per_thread = defaults.vecs_per_thread;
+  if (!stream_vecs_ok(e->tuning.vecs_per_thread)) e->tuning.vecs_per_thread = defaults.vecs_per_thread;
   if (const char *v = getenv("BCP_SCHEDULE")) e->tuning.schedule = atoi(v) == kSchedStatic ? kSchedStatic : kSchedQueue;
   *out = e;
   return 0;
@@ -189,7 +196,9 @@ extern "C" int bcp_set_option(bcp_engine *eng, const char *key, int value) {
   int rc = 0;
   pthread_mutex_lock(&eng->lock);
   if (!strcmp(key, "blocks_per_cu") && value >= 1 && value <= 32) eng->tuning.blocks_per_cu = value;
-  else if (!strcmp(key, "vecs_per_thread") && (value == 1 || value == 2 || value == 4)) eng->tuning.vecs_per_thread = value;
+  else if (!strcmp(key, "vecs_per_thread") && stream_vecs_ok(value)) eng->tuning.vecs_per_thread = value;
+  else if (!strcmp(key, "desc_blocks_per_cu") && value >= 1 && value <= 32) eng->tuning.desc_blocks_per_cu = value;
+  else if (!strcmp(key, "desc_vecs_per_thread") && desc_vecs_ok(value)) eng->tuning.desc_vecs = value;
   else if (!strcmp(key, "schedule") && (value == kSchedQueue || value == kSchedStatic)) eng->tuning.schedule = value;
   else if (!strcmp(key, "desc_schedule") && (value == kSchedQueue || value == kSchedStatic)) eng->tuning.desc_schedule = value;
   else if (!strcmp(key, "desc_grab") && value >= 1 && value <= 64) eng->tuning.desc_grab = value;
@@ -201,7 +210,7 @@ extern "C" int bcp_set_option(bcp_engine *eng, const char *key, int value) {
 extern "C" int bcp_set_tuning(bcp_engine *eng, int blocks_per_cu, int vecs_per_thread) {
   if (!eng) return -EINVAL;
   if (blocks_per_cu < 0 || blocks_per_cu > 32) return -EINVAL;
-  if (vecs_per_thread != 0 && vecs_per_thread != 1 && vecs_per_thread != 2 && vecs_per_thread != 4) return -EINVAL;
+  if (vecs_per_thread != 0 && !stream_vecs_ok(vecs_per_thread)) return -EINVAL;
   const Tuning defaults;
   pthread_mutex_lock(&eng->lock);
   eng->tuning.blocks_per_cu = blocks_per_cu ? blocks_per_cu : defaults.blocks_per_cu;
@@ -443,7 +452,7 @@ static bool uniform_batch(const bcp_stripe *st, uint32_t nstripes, const bcp_sou
 static int submit_desc(bcp_queue *q, const bcp_stripe *stripes, uint32_t nstripes, const bcp_source *sources,
                        uint32_t nsources) {
   bcp_engine *e = q->eng;
-  const int vecs = e->tuning.vecs_per_thread;
+  const int vecs = e->tuning.desc_vecs;
   const uint32_t tile_bytes = desc_tile_bytes(vecs);
   // Validate and count tiles.
   uint64_t ntiles = 0;
@@ -515,7 +524,7 @@ static int submit_desc(bcp_queue *q, const bcp_stripe *stripes, uint32_t nstripe
   b.ctr = q->qctr;
   b.base = q->qbase;
   const uint32_t nunits = b.sched == kSchedQueue ? (acc + b.grab - 1) / b.grab : acc;
-  int grid = grid_for(e);
+  int grid = desc_grid_for(e);
   if ((uint32_t)grid > nunits) grid = (int)nunits;
   HIP_RC(launch_xor_desc(q->stream, grid, vecs, b));
   if (b.sched == kSchedQueue) q->qbase += (uint64_t)nunits + (uint64_t)grid;

@@ -11,18 +11,21 @@
 namespace bcp {
 
 constexpr int kBlock = 256;        // threads per workgroup (4 waves of 64)
-constexpr int kMaxVecsPerThread = 4;
+constexpr int kMaxVecsPerThread = 8;     // xor_stream; xor_desc takes at most 4
 
 // Tile schedules of the streaming kernel.
 constexpr int kSchedQueue = 0;   // device-wide work queue (default)
 constexpr int kSchedStatic = 1;  // contiguous tile range per workgroup (r01 design; A/B only)
 
 // Defaults from the r01 interleaved sweeps on MI355X (profiles/r01/):
-// 8 x 256-thread workgroups per CU (7 resident at 68 VGPRs), 4 vectors per
-// lane, work-queue schedule, non-temporal loads and stores.
+// xor_stream: one 256-thread workgroup per CU with 8 vectors per lane (the
+// fewer tiles in flight, the narrower the queue's address window:
+// kernel_exp_6/7), work-queue schedule, non-temporal loads and stores.
 struct Tuning {
-    int blocks_per_cu = 8;      // 256-thread workgroups launched per CU
-    int vecs_per_thread = 4;    // 16-byte vectors per lane per tile
+    int blocks_per_cu = 1;      // xor_stream: 256-thread workgroups launched per CU
+    int vecs_per_thread = 8;    // xor_stream: 16-byte vectors per lane per tile (1, 2, 4, 8)
+    int desc_blocks_per_cu = 8; // xor_desc
+    int desc_vecs = 4;          // xor_desc (1, 2, 4)
     int schedule = kSchedQueue; // kSched* of xor_stream
     // xor_desc: work queue in grabs of 2 tiles.  Mixed-size tiles read ~2.4x
     // fewer bytes than config-2 tiles, so one atomic per tile saturates the

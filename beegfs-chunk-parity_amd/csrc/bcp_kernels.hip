@@ -488,12 +488,14 @@ hipError_t launch_xor_stream(hipStream_t st, int grid, int vecs, bool gather, co
     switch (vecs) {
       case 1: return launch_stream_u<1, 1>(st, grid, a);
       case 4: return launch_stream_u<4, 1>(st, grid, a);
+      case 8: return launch_stream_u<8, 1>(st, grid, a);
       default: return launch_stream_u<2, 1>(st, grid, a);
     }
   }
   switch (vecs) {
     case 1: return launch_stream_u<1, 0>(st, grid, a);
     case 4: return launch_stream_u<4, 0>(st, grid, a);
+    case 8: return launch_stream_u<8, 0>(st, grid, a);
     default: return launch_stream_u<2, 0>(st, grid, a);
   }
 }

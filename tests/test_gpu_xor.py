@@ -156,7 +156,7 @@ def test_strided_layout(oracle, dev, queue):
 
 
 @pytest.mark.parametrize("sched", [0, 1])
-@pytest.mark.parametrize("bpc,vecs", [(1, 1), (2, 4), (4, 2), (8, 1), (16, 4)])
+@pytest.mark.parametrize("bpc,vecs", [(1, 1), (2, 4), (4, 2), (8, 1), (16, 4), (1, 8), (3, 8)])
 def test_tuning_variants_agree(oracle, engine, dev, queue, bpc, vecs, sched):
     nstripes, nsrc, chunk = 7, 8, 524288 + 4096
     rng = np.random.default_rng(bpc * 10 + vecs + 100 * sched)
@@ -165,6 +165,9 @@ def test_tuning_variants_agree(oracle, engine, dev, queue, bpc, vecs, sched):
     dst = dev.alloc(nstripes * chunk)
     engine.tune(bpc, vecs)
     engine.option("schedule", sched)
+    engine.option("desc_schedule", sched)
+    engine.option("desc_blocks_per_cu", bpc)
+    engine.option("desc_vecs_per_thread", min(vecs, 4))
     try:
         queue.xor_uniform(dst, src, nstripes, nsrc, chunk)
         out = dev.get(dst, nstripes * chunk)
@@ -173,6 +176,9 @@ def test_tuning_variants_agree(oracle, engine, dev, queue, bpc, vecs, sched):
     finally:
         engine.tune(0, 0)
         engine.option("schedule", 0)
+        engine.option("desc_schedule", 0)
+        engine.option("desc_blocks_per_cu", 8)
+        engine.option("desc_vecs_per_thread", 4)
     ref = np.bitwise_xor.reduce(data.reshape(nstripes, nsrc, chunk), axis=1).reshape(-1)
     assert np.array_equal(out, ref)
     assert np.array_equal(res[0], oracle.xor_padded_np([data[:1000], data[5:70000]]))

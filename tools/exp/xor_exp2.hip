@@ -226,7 +226,36 @@ struct Entry {
 #define X(name, KB, U, LD, ST, DEF, MODE, BPC) {name, xe2<KB, U, LD, ST, DEF, MODE>, KB, U, MODE, BPC, 0}
 #define P(name, PAD) {name, xe2<256, 4, LD_GNT, ST_NT, 0, MODE_XOR>, 256, 4, MODE_XOR, 8, PAD}
 static const Entry kV[] = {
-#ifdef XE2_PITCH
+#if defined(XE2_OCC2)
+    X("base", 256, 4, LD_GNT, ST_NT, 0, MODE_XOR, 8),
+    X("u4_bpc1", 256, 4, LD_GNT, ST_NT, 0, MODE_XOR, 1),
+    X("u8_bpc1", 256, 8, LD_GNT, ST_NT, 0, MODE_XOR, 1),
+    X("u16_bpc1", 256, 16, LD_GNT, ST_NT, 0, MODE_XOR, 1),
+    X("u8_bpc1_defer", 256, 8, LD_GNT, ST_NT, 1, MODE_XOR, 1),
+    X("u4_bpc1_defer", 256, 4, LD_GNT, ST_NT, 1, MODE_XOR, 1),
+    X("wg512_u8_bpc1", 512, 8, LD_GNT, ST_NT, 0, MODE_XOR, 1),
+    X("wg128_u8_bpc2", 128, 8, LD_GNT, ST_NT, 0, MODE_XOR, 2),
+    X("wg128_u16_bpc1", 128, 16, LD_GNT, ST_NT, 0, MODE_XOR, 1),
+    X("wg128_u8_bpc1", 128, 8, LD_GNT, ST_NT, 0, MODE_XOR, 1),
+    X("wg64_u16_bpc2", 64, 16, LD_GNT, ST_NT, 0, MODE_XOR, 2),
+    X("u8_bpc1_bnt", 256, 8, LD_BNT, ST_NT, 0, MODE_XOR, 1),
+    X("read_u8_bpc1", 256, 8, LD_GNT, ST_NONE, 0, MODE_READ, 1),
+#elif defined(XE2_OCC)
+    X("base", 256, 4, LD_GNT, ST_NT, 0, MODE_XOR, 8),
+    X("bpc1", 256, 4, LD_GNT, ST_NT, 0, MODE_XOR, 1),
+    X("bpc2", 256, 4, LD_GNT, ST_NT, 0, MODE_XOR, 2),
+    X("bpc3", 256, 4, LD_GNT, ST_NT, 0, MODE_XOR, 3),
+    X("bpc4", 256, 4, LD_GNT, ST_NT, 0, MODE_XOR, 4),
+    X("u8_bpc1", 256, 8, LD_GNT, ST_NT, 0, MODE_XOR, 1),
+    X("u8_bpc2", 256, 8, LD_GNT, ST_NT, 0, MODE_XOR, 2),
+    X("u8_bpc4", 256, 8, LD_GNT, ST_NT, 0, MODE_XOR, 4),
+    X("wg512_u4_bpc1", 512, 4, LD_GNT, ST_NT, 0, MODE_XOR, 1),
+    X("wg512_u4_bpc2", 512, 4, LD_GNT, ST_NT, 0, MODE_XOR, 2),
+    X("wg1024_u4_bpc1", 1024, 4, LD_GNT, ST_NT, 0, MODE_XOR, 1),
+    X("wg1024_u2_bpc1", 1024, 2, LD_GNT, ST_NT, 0, MODE_XOR, 1),
+    X("defer_bpc2", 256, 4, LD_GNT, ST_NT, 1, MODE_XOR, 2),
+    X("defer_bpc4", 256, 4, LD_GNT, ST_NT, 1, MODE_XOR, 4),
+#elif defined(XE2_PITCH)
     X("base", 256, 4, LD_GNT, ST_NT, 0, MODE_XOR, 8),
     P("pad256", 256),
     P("pad1k", 1024),
