@@ -24,7 +24,7 @@ constexpr int kSchedStatic = 1;  // contiguous tile range per workgroup (r01 des
 struct Tuning {
     int blocks_per_cu = 1;      // xor_stream: 256-thread workgroups launched per CU
     int vecs_per_thread = 8;    // xor_stream: 16-byte vectors per lane per tile (1, 2, 4, 8)
-    int desc_blocks_per_cu = 8; // xor_desc
+    int desc_blocks_per_cu = 2; // xor_desc (config-5 shapes: 1/2/4/8 per CU = 53/75/72/69 %)
     int desc_vecs = 4;          // xor_desc (1, 2, 4)
     int schedule = kSchedQueue; // kSched* of xor_stream
     // xor_desc: work queue in grabs of 2 tiles.  Mixed-size tiles read ~2.4x

@@ -102,26 +102,36 @@ __device__ __forceinline__ void stream_tile(const StreamArgs &a, uint32_t t) {
   };
   v4u acc[U];
   if ((tin + 1) * (uint32_t)(kBlock * U) <= a.vps) {
-    const glob<v4u> *p0 = src_k(0);
-#pragma unroll
-    for (int u = 0; u < U; u++) acc[u] = ld_nt(p0 + tile_vec<U>(tin, u));
+    const uint32_t vb = tile_vec<U>(tin, 0);
     if constexpr (NSRC > 0) {
+      // Every load of the tile first, then the XOR tree: the compiler keeps
+      // the scheduling freedom (fewer VGPRs than an interleaved chain).
+      v4u x[NSRC][U];
 #pragma unroll
-      for (int k = 1; k < NSRC; k++) {
-        const glob<v4u> *pk = src_k(k);
+      for (int k = 0; k < NSRC; k++) {
+        const glob<v4u> *pk = src_k(k) + vb;
 #pragma unroll
-        for (int u = 0; u < U; u++) acc[u] ^= ld_nt(pk + tile_vec<U>(tin, u));
+        for (int u = 0; u < U; u++) x[k][u] = ld_nt(pk + u * 64);
+      }
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        acc[u] = x[0][u];
+#pragma unroll
+        for (int k = 1; k < NSRC; k++) acc[u] ^= x[k][u];
       }
     } else {
+      const glob<v4u> *p0 = src_k(0) + vb;
+#pragma unroll
+      for (int u = 0; u < U; u++) acc[u] = ld_nt(p0 + u * 64);
 #pragma unroll 4
       for (uint32_t k = 1; k < nsrc; k++) {
-        const glob<v4u> *pk = src_k(k);
+        const glob<v4u> *pk = src_k(k) + vb;
 #pragma unroll
-        for (int u = 0; u < U; u++) acc[u] ^= ld_nt(pk + tile_vec<U>(tin, u));
+        for (int u = 0; u < U; u++) acc[u] ^= ld_nt(pk + u * 64);
       }
     }
 #pragma unroll
-    for (int u = 0; u < U; u++) __builtin_nontemporal_store(acc[u], db + tile_vec<U>(tin, u));
+    for (int u = 0; u < U; u++) __builtin_nontemporal_store(acc[u], db + vb + u * 64);
   } else {
     // Last, partial tile of a stripe: per-vector bounds.
 #pragma unroll

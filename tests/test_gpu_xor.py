@@ -177,7 +177,7 @@ def test_tuning_variants_agree(oracle, engine, dev, queue, bpc, vecs, sched):
         engine.tune(0, 0)
         engine.option("schedule", 0)
         engine.option("desc_schedule", 0)
-        engine.option("desc_blocks_per_cu", 8)
+        engine.option("desc_blocks_per_cu", 2)
         engine.option("desc_vecs_per_thread", 4)
     ref = np.bitwise_xor.reduce(data.reshape(nstripes, nsrc, chunk), axis=1).reshape(-1)
     assert np.array_equal(out, ref)
