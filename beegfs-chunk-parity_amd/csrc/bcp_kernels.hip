@@ -78,7 +78,7 @@ __device__ __forceinline__ uint32_t tile_vec(uint32_t tin, int u) {
   return tin * (uint32_t)(kBlock * U) + (threadIdx.x >> 6) * (64u * U) + (uint32_t)u * 64u + (threadIdx.x & 63u);
 }
 
-template <int NSRC, int U, int GATHER>
+template <int NSRC, int U, int GATHER, bool PARTIAL>
 __device__ __forceinline__ void stream_tile(const StreamArgs &a, uint32_t t) {
   const uint32_t nsrc = NSRC > 0 ? (uint32_t)NSRC : a.nsrc;
   const uint32_t s = t / a.tps;
@@ -101,7 +101,7 @@ __device__ __forceinline__ void stream_tile(const StreamArgs &a, uint32_t t) {
     else return gp<v4u>(sb + (uint64_t)k * a.src_stride);
   };
   v4u acc[U];
-  if ((tin + 1) * (uint32_t)(kBlock * U) <= a.vps) {
+  if (!PARTIAL || (tin + 1) * (uint32_t)(kBlock * U) <= a.vps) {
     const uint32_t vb = tile_vec<U>(tin, 0);
     if constexpr (NSRC > 0) {
       // Every load of the tile first, then the XOR tree: the compiler keeps
@@ -132,7 +132,7 @@ __device__ __forceinline__ void stream_tile(const StreamArgs &a, uint32_t t) {
     }
 #pragma unroll
     for (int u = 0; u < U; u++) __builtin_nontemporal_store(acc[u], db + vb + u * 64);
-  } else {
+  } else if constexpr (PARTIAL) {
     // Last, partial tile of a stripe: per-vector bounds.
 #pragma unroll
     for (int u = 0; u < U; u++) {
@@ -151,28 +151,36 @@ __device__ __forceinline__ uint32_t queue_grab(unsigned long long *ctr, unsigned
   return v > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)v;
 }
 
-template <int NSRC, int U, int GATHER>
+// KIND: kQueueFull (work queue, every tile full: the config-2 shapes),
+// kQueuePartial (work queue, stripes end in a partial tile), kStatic
+// (contiguous tile range per workgroup; A/B only).  Separate instantiations
+// because the partial-tile and static code paths cost ~15-25 VGPRs at U = 8
+// even when never taken.
+constexpr int kQueueFull = 0, kQueuePartial = 1, kStatic = 2;
+
+template <int NSRC, int U, int GATHER, int KIND>
 __global__ __launch_bounds__(kBlock) void xor_stream(StreamArgs a) {
-  if (a.sched == kSchedStatic) {
+  constexpr bool PARTIAL = KIND != kQueueFull;
+  if constexpr (KIND == kStatic) {
     // Workgroup b owns tiles [b*T/G, (b+1)*T/G) (the r01 schedule; A/B only).
     const uint32_t t0 = (uint32_t)(((uint64_t)blockIdx.x * a.ntiles) / gridDim.x);
     const uint32_t t1 = (uint32_t)(((uint64_t)(blockIdx.x + 1) * a.ntiles) / gridDim.x);
-    for (uint32_t t = t0; t < t1; t++) stream_tile<NSRC, U, GATHER>(a, t);
-    return;
-  }
-  // Two LDS slots: thread 0 writes slot i+1 only after the barrier that
-  // every wave reaches after reading slot i, so one barrier per tile is enough.
-  __shared__ uint32_t next[2];
-  if (threadIdx.x == 0) next[0] = queue_grab(a.ctr, a.base);
-  __syncthreads();
-  uint32_t t = __builtin_amdgcn_readfirstlane(next[0]);
-  int slot = 0;
-  while (t < a.ntiles) {
-    stream_tile<NSRC, U, GATHER>(a, t);
-    slot ^= 1;
-    if (threadIdx.x == 0) next[slot] = queue_grab(a.ctr, a.base);
+    for (uint32_t t = t0; t < t1; t++) stream_tile<NSRC, U, GATHER, true>(a, t);
+  } else {
+    // Two LDS slots: thread 0 writes slot i+1 only after the barrier that
+    // every wave reaches after reading slot i, so one barrier per tile is enough.
+    __shared__ uint32_t next[2];
+    if (threadIdx.x == 0) next[0] = queue_grab(a.ctr, a.base);
     __syncthreads();
-    t = __builtin_amdgcn_readfirstlane(next[slot]);
+    uint32_t t = __builtin_amdgcn_readfirstlane(next[0]);
+    int slot = 0;
+    while (t < a.ntiles) {
+      stream_tile<NSRC, U, GATHER, PARTIAL>(a, t);
+      slot ^= 1;
+      if (threadIdx.x == 0) next[slot] = queue_grab(a.ctr, a.base);
+      __syncthreads();
+      t = __builtin_amdgcn_readfirstlane(next[slot]);
+    }
   }
 }
 
@@ -468,12 +476,25 @@ __global__ __launch_bounds__(kBlock) void compare_bytes(const unsigned char *a, 
 // ---------------------------------------------------------------------------
 template <int NSRC, int U, int GATHER>
 static hipError_t launch_stream_nu(hipStream_t st, int grid, const StreamArgs &a) {
-  hipLaunchKernelGGL((xor_stream<NSRC, U, GATHER>), dim3(grid), dim3(kBlock), 0, st, a);
+  if (a.vps % (uint32_t)(kBlock * U) != 0)
+    hipLaunchKernelGGL((xor_stream<NSRC, U, GATHER, kQueuePartial>), dim3(grid), dim3(kBlock), 0, st, a);
+  else
+    hipLaunchKernelGGL((xor_stream<NSRC, U, GATHER, kQueueFull>), dim3(grid), dim3(kBlock), 0, st, a);
+  return hipGetLastError();
+}
+
+template <int NSRC, int U, int GATHER>
+static hipError_t launch_static_nu(hipStream_t st, int grid, const StreamArgs &a) {
+  hipLaunchKernelGGL((xor_stream<NSRC, U, GATHER, kStatic>), dim3(grid), dim3(kBlock), 0, st, a);
   return hipGetLastError();
 }
 
 template <int U, int GATHER>
 static hipError_t launch_stream_u(hipStream_t st, int grid, const StreamArgs &a) {
+  // The static schedule (A/B only) is instantiated for the hot width and the
+  // runtime-width kernel only.
+  if (a.sched == kSchedStatic)
+    return a.nsrc == 8 ? launch_static_nu<8, U, GATHER>(st, grid, a) : launch_static_nu<0, U, GATHER>(st, grid, a);
 #define BCP_NSRC_CASE(n) \
   case n: return launch_stream_nu<n, U, GATHER>(st, grid, a);
   switch (a.nsrc) {
