@@ -109,6 +109,7 @@ _SIGS = {
     "bcp_queue_elapsed_ms": ([_V, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_float)], ctypes.c_int),
     "bcp_set_tuning": ([_V, ctypes.c_int, ctypes.c_int], ctypes.c_int),
     "bcp_set_option": ([_V, ctypes.c_char_p, ctypes.c_int], ctypes.c_int),
+    "bcp_get_option": ([_V, ctypes.c_char_p, ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
     "bcp_task_set_device_map": ([ctypes.POINTER(ctypes.c_int), ctypes.c_int], ctypes.c_int),
     "bcp_task_shutdown": ([], ctypes.c_int),
     "bcp_task_set_xor_hook": ([_V, _V], None),
@@ -216,8 +217,13 @@ class Engine:
     def tune(self, blocks_per_cu: int = 0, vecs_per_thread: int = 0):
         call("bcp_set_tuning", self.h, blocks_per_cu, vecs_per_thread)
 
-    def option(self, key: str, value: int):
-        call("bcp_set_option", self.h, key.encode(), value)
+    def option(self, key: str, value: int | None = None) -> int:
+        """Set a named knob (value given) or read it back."""
+        if value is not None:
+            call("bcp_set_option", self.h, key.encode(), value)
+        v = ctypes.c_int(0)
+        call("bcp_get_option", self.h, key.encode(), ctypes.byref(v))
+        return v.value
 
     def queue(self) -> "Queue":
         return Queue(self)

@@ -207,6 +207,23 @@ extern "C" int bcp_set_option(bcp_engine *eng, const char *key, int value) {
   return rc;
 }
 
+extern "C" int bcp_get_option(bcp_engine *eng, const char *key, int *value) {
+  if (!eng || !key || !value) return -EINVAL;
+  int rc = 0;
+  pthread_mutex_lock(&eng->lock);
+  const Tuning &t = eng->tuning;
+  if (!strcmp(key, "blocks_per_cu")) *value = t.blocks_per_cu;
+  else if (!strcmp(key, "vecs_per_thread")) *value = t.vecs_per_thread;
+  else if (!strcmp(key, "schedule")) *value = t.schedule;
+  else if (!strcmp(key, "desc_blocks_per_cu")) *value = t.desc_blocks_per_cu;
+  else if (!strcmp(key, "desc_vecs_per_thread")) *value = t.desc_vecs;
+  else if (!strcmp(key, "desc_schedule")) *value = t.desc_schedule;
+  else if (!strcmp(key, "desc_grab")) *value = t.desc_grab;
+  else rc = -EINVAL;
+  pthread_mutex_unlock(&eng->lock);
+  return rc;
+}
+
 extern "C" int bcp_set_tuning(bcp_engine *eng, int blocks_per_cu, int vecs_per_thread) {
   if (!eng) return -EINVAL;
   if (blocks_per_cu < 0 || blocks_per_cu > 32) return -EINVAL;

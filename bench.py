@@ -149,16 +149,18 @@ def main():
             bcp.check("bcp_xor_stripes_async", L.bcp_xor_stripes_async(q.h, st, len(stripes), so, len(sources)))
         bytes_per_step = sum(int(ls.sum()) + int(ls.max()) for ls in lens_all)
         S = len(stripes)
-        kernel = "xor_desc<U>"
-        kernel_tag = "xor_desc<"
+        U = eng.option("desc_vecs_per_thread")
+        kernel = f"xor_desc<{U}>"
+        kernel_tag = f"xor_desc<{U}>"
         workload = (f"config5 shapes: {S} stripes x {N} chunks, log-uniform 64 KiB-4 MiB, "
                     f"zero-padded to the stripe max, device-resident")
     elif a.mode == "gen":
         def step():
             q.xor_uniform(out, src, S, N, C)
         bytes_per_step = S * (N + 1) * C
-        kernel = f"xor_stream<{N},U,strided>"
-        kernel_tag = f"xor_stream<{N}, "
+        U = eng.option("vecs_per_thread")
+        kernel = f"xor_stream<{N},{U},strided>"
+        kernel_tag = f"xor_stream<{N}, {U}, 0, "
         cfg = "config4" if d.world == 8 and S == 15_625 else "config2"
         workload = f"{cfg}: parity gen, {S} stripes x {N} x {C // KiB} KiB device-resident per GPU"
     else:
@@ -183,8 +185,9 @@ def main():
         def step():
             bcp.check("bcp_xor_stripes_async", L.bcp_xor_stripes_async(q.h, st, len(stripes), so, len(sources)))
         bytes_per_step = S * (N + 1) * C
-        kernel = f"xor_stream<{N},U,gather>"
-        kernel_tag = f"xor_stream<{N}, "
+        U = eng.option("vecs_per_thread")
+        kernel = f"xor_stream<{N},{U},gather>"
+        kernel_tag = f"xor_stream<{N}, {U}, 1, "
         workload = f"config3: rebuild, {S} stripes x ({N - 1} survivors + parity) x {C // KiB} KiB device-resident"
 
     for _ in range(a.warmup):

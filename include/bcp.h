@@ -174,6 +174,8 @@ int bcp_set_tuning(bcp_engine *eng, int blocks_per_cu, int vecs_per_thread);
  * "desc_grab" (tiles per work-queue grab, 1..64, default 2) for the
  * descriptor kernel (mixed sizes, windows, unaligned). */
 int bcp_set_option(bcp_engine *eng, const char *key, int value);
+/* Current value of a named knob (same keys). */
+int bcp_get_option(bcp_engine *eng, const char *key, int *value);
 /* Timer slots for bcp_queue_mark / bcp_queue_elapsed_ms. */
 #define BCP_TIMER_SLOTS 64
 
