@@ -102,7 +102,7 @@ static int desc_grid_for(const bcp_engine *e) {
 }
 
 static bool stream_vecs_ok(int v) { return v == 1 || v == 2 || v == 4 || v == 8; }
-static bool desc_vecs_ok(int v) { return v == 1 || v == 2 || v == 4; }
+static bool desc_vecs_ok(int v) { return v == 1 || v == 2 || v == 4 || v == 8; }
 
 static bool aligned16(uint64_t x) { return (x & 15u) == 0; }
 

@@ -11,7 +11,7 @@
 namespace bcp {
 
 constexpr int kBlock = 256;        // threads per workgroup (4 waves of 64)
-constexpr int kMaxVecsPerThread = 8;     // xor_stream; xor_desc takes at most 4
+constexpr int kMaxVecsPerThread = 8;     // xor_stream and xor_desc
 
 // Tile schedules of the streaming kernel.
 constexpr int kSchedQueue = 0;   // device-wide work queue (default)
@@ -24,14 +24,14 @@ constexpr int kSchedStatic = 1;  // contiguous tile range per workgroup (r01 des
 struct Tuning {
     int blocks_per_cu = 1;      // xor_stream: 256-thread workgroups launched per CU
     int vecs_per_thread = 8;    // xor_stream: 16-byte vectors per lane per tile (1, 2, 4, 8)
-    int desc_blocks_per_cu = 2; // xor_desc (config-5 shapes: 1/2/4/8 per CU = 53/75/72/69 %)
-    int desc_vecs = 4;          // xor_desc (1, 2, 4)
-    int schedule = kSchedQueue; // kSched* of xor_stream
-    // xor_desc: work queue in grabs of 2 tiles.  Mixed-size tiles read ~2.4x
-    // fewer bytes than config-2 tiles, so one atomic per tile saturates the
-    // counter (r01 config-5 sweep, profiles/r01/mixed/: static 61-64 %,
-    // grab 1 56 %, grab 2 71.5 %, grab 3 70 %, grab 4 67.5 %, grab 8 69 %).
-    int desc_grab = 2;
+    int schedule = kSchedQueue; // xor_stream: kSched*
+    // xor_desc, config-5 shapes (profiles/r01/mixed/): 2 workgroups per CU,
+    // 8 vectors per lane, one 32 KiB tile per queue grab = 77.3 % (U = 4 needed
+    // 2-tile grabs: 72.9 %; 1 WG/CU 71.9-75.4 %).  Mixed-size tiles read ~2.4x
+    // fewer bytes than config-2 tiles, so the grab size is per kernel.
+    int desc_blocks_per_cu = 2;
+    int desc_vecs = 8;          // 1, 2, 4, 8
+    int desc_grab = 1;          // tiles per work-queue grab
     int desc_schedule = kSchedQueue;
 };
 

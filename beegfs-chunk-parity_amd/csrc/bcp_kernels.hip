@@ -537,6 +537,7 @@ hipError_t launch_xor_desc(hipStream_t st, int grid, int vecs, const DescBatch &
   switch (vecs) {
     case 1: hipLaunchKernelGGL((xor_desc<1>), dim3(grid), dim3(kBlock), 0, st, b); break;
     case 4: hipLaunchKernelGGL((xor_desc<4>), dim3(grid), dim3(kBlock), 0, st, b); break;
+    case 8: hipLaunchKernelGGL((xor_desc<8>), dim3(grid), dim3(kBlock), 0, st, b); break;
     default: hipLaunchKernelGGL((xor_desc<2>), dim3(grid), dim3(kBlock), 0, st, b); break;
   }
   return hipGetLastError();

@@ -4,7 +4,7 @@
 Workload (BASELINE.json configs[1], "config 2"): 12,500 stripes x 8 sources
 x 512 KiB (100,000 data chunks = 48.8 GiB) resident in HBM per GPU (at 8
 GPUs config 4: 1,000,000 chunks = 15,625 stripes per GPU); one step
-= one pass of the parity kernel over all stripes (xor_stream<8,4>,
+= one pass of the parity kernel over all stripes (xor_stream<8,U>,
 the reference's xor_parity, task_processing.c:96-109, batched).
 `--mode rebuild` times config 3 instead (7 survivors + parity body ->
 rebuilt chunk; a uniform descriptor batch, so the same streaming kernel in

@@ -167,7 +167,7 @@ def test_tuning_variants_agree(oracle, engine, dev, queue, bpc, vecs, sched):
     engine.option("schedule", sched)
     engine.option("desc_schedule", sched)
     engine.option("desc_blocks_per_cu", bpc)
-    engine.option("desc_vecs_per_thread", min(vecs, 4))
+    engine.option("desc_vecs_per_thread", vecs)
     try:
         queue.xor_uniform(dst, src, nstripes, nsrc, chunk)
         out = dev.get(dst, nstripes * chunk)
@@ -178,7 +178,7 @@ def test_tuning_variants_agree(oracle, engine, dev, queue, bpc, vecs, sched):
         engine.option("schedule", 0)
         engine.option("desc_schedule", 0)
         engine.option("desc_blocks_per_cu", 2)
-        engine.option("desc_vecs_per_thread", 4)
+        engine.option("desc_vecs_per_thread", 8)
     ref = np.bitwise_xor.reduce(data.reshape(nstripes, nsrc, chunk), axis=1).reshape(-1)
     assert np.array_equal(out, ref)
     assert np.array_equal(res[0], oracle.xor_padded_np([data[:1000], data[5:70000]]))
