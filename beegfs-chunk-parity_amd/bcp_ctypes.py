@@ -124,6 +124,8 @@ _SIGS = {
     "bcp_pipeline_run": ([_V, ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(WorkItem), ctypes.c_size_t, _V,
                           ctypes.POINTER(RunStats)], ctypes.c_int),
     "bcp_pipeline_destroy": ([_V], ctypes.c_int),
+    "bcp_pipeline_rebuild": ([_V, ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.POINTER(WorkItem),
+                              ctypes.c_size_t, ctypes.c_char_p, _V, ctypes.POINTER(RunStats)], ctypes.c_int),
     "bcp_lb_init": ([ctypes.c_int], ctypes.c_int),
     "bcp_eventset_create": ([ctypes.POINTER(_V)], ctypes.c_int),
     "bcp_eventset_destroy": ([_V], None),
@@ -514,6 +516,16 @@ class Pipeline:
         arr, keep = _items(items)
         st = RunStats()
         call("bcp_pipeline_run", self.h, store_root.encode(), ntargets, arr, len(items), log, ctypes.byref(st))
+        del keep
+        return st
+
+    def rebuild(self, store_root: str, ntargets: int, rebuild_target: int, items, corrupt_list: str | None = None,
+                log=None) -> RunStats:
+        """bcp_pipeline_rebuild: items in DB key order, as bcp_rebuild_run takes them."""
+        arr, keep = _items(items)
+        st = RunStats()
+        call("bcp_pipeline_rebuild", self.h, store_root.encode(), ntargets, rebuild_target, arr, len(items),
+             corrupt_list.encode() if corrupt_list else None, log, ctypes.byref(st))
         del keep
         return st
 

@@ -24,6 +24,13 @@
  * (task_processing.c:146-226): header in ascending storage-target order, then
  * the windowed XOR (replay semantics past one 10 MiB window); a missing chunk
  * counts as size 0 / zeros; an item with no holders unlinks its parity chunk.
+ *
+ * Rebuild mode (bcp_pipeline_rebuild) is the same machinery with do_file's
+ * roles (rebuild/main.c:40-89, task_processing.c:146-174,228-230,263-280):
+ * the sources are the surviving chunks plus the parity body (read after the
+ * u64 header), max_cs = max(header), and the lost chunk is written to the
+ * victim's chunks directory truncated to header[index of the victim];
+ * survivors newer than FileInfo.timestamp go to the corrupt list.
  */
 #define _GNU_SOURCE
 #include <errno.h>
@@ -171,11 +178,17 @@ static void latch_destroy(latch *l)
 /* ---- plan --------------------------------------------------------------- */
 typedef struct {
     const char *path;
-    int p;                               /* parity target */
-    int n;                               /* holders */
-    int holders[MAX_STORAGE_TARGETS];
-    uint64_t size[MAX_STORAGE_TARGETS];  /* chunk sizes at stat time (0 = missing) */
+    int p;                               /* output target: P (gen) or the victim (rebuild) */
+    int n;                               /* sources */
+    int holders[MAX_STORAGE_TARGETS];    /* source targets, ascending */
+    int rebuild;                         /* 1: rebuild task */
+    int parity_src;                      /* rebuild: index of the parity body among the sources */
+    int64_t timestamp;                   /* rebuild: FileInfo.timestamp (corrupt check) */
+    uint64_t size[MAX_STORAGE_TARGETS];  /* source lengths at stat time (0 = missing);
+                                            gen: also the parity header */
+    uint64_t src_off[MAX_STORAGE_TARGETS];/* file offset of the source data (parity body: 8n) */
     uint64_t max_cs;
+    uint64_t out_len;                    /* gen: max_cs; rebuild: header[victim index] */
     uint64_t in_off[MAX_STORAGE_TARGETS];/* offsets in the input slab */
     uint64_t out_off;                    /* offset in the output slab */
     int batch;
@@ -185,6 +198,7 @@ typedef struct {
     const char *root;
     task *t;
     latch *done;
+    int corrupt_fd;                      /* rebuild: corrupt list (or -1) */
 } stat_arg;
 
 typedef struct {
@@ -232,19 +246,85 @@ static void chunk_file(char *buf, size_t cap, const char *root, int st, const ch
     snprintf(buf, cap, "%s/st%d/%s/%s", root, st, dir, path);
 }
 
+/* Corrupt list line (task_processing.c:54-60, 268-271), written whole. */
+static void push_corrupt(int fd, const char *path)
+{
+    if (fd < 0)
+        return;
+    size_t len = strlen(path);
+    char *line = malloc(len + 2);
+    if (!line)
+        return;
+    memcpy(line, path, len);
+    line[len] = '\n';
+    ssize_t w = write(fd, line, len + 1);
+    (void)w;
+    free(line);
+}
+
 static void do_stat(void *p)
 {
     stat_arg *a = p;
     task *t = a->t;
     char fn[4352];
     t->max_cs = 0;
-    for (int k = 0; k < t->n; k++) {
-        chunk_file(fn, sizeof(fn), a->root, t->holders[k], "chunks", t->path);
-        struct stat st;
-        t->size[k] = stat(fn, &st) == 0 ? (uint64_t)st.st_size : 0;
-        if (t->size[k] > t->max_cs)
-            t->max_cs = t->size[k];
+    if (!t->rebuild) {
+        for (int k = 0; k < t->n; k++) {
+            chunk_file(fn, sizeof(fn), a->root, t->holders[k], "chunks", t->path);
+            struct stat st;
+            t->size[k] = stat(fn, &st) == 0 ? (uint64_t)st.st_size : 0;
+            t->src_off[k] = 0;
+            if (t->size[k] > t->max_cs)
+                t->max_cs = t->size[k];
+        }
+        t->out_len = t->max_cs;
+        latch_down(a->done);
+        return;
     }
+    /* rebuild: survivors as they are now; the parity holder contributes its
+     * stored header (sizes at generation) and the body after it */
+    uint64_t header[MAX_STORAGE_TARGETS] = {0};
+    const int n = t->n;
+    for (int k = 0; k < n; k++) {
+        struct stat st;
+        if (k == t->parity_src) {
+            chunk_file(fn, sizeof(fn), a->root, t->holders[k], "parity", t->path);
+            int fd = open(fn, O_RDONLY);
+            uint64_t fsize = 0;
+            if (fd >= 0) {
+                if (fstat(fd, &st) == 0)
+                    fsize = (uint64_t)st.st_size;
+                ssize_t r = pread(fd, header, (size_t)n * 8u, 0); /* a short header reads as zeros */
+                (void)r;
+                close(fd);
+            }
+            t->src_off[k] = (uint64_t)n * 8u;
+            t->size[k] = fsize > t->src_off[k] ? fsize - t->src_off[k] : 0;
+        } else {
+            chunk_file(fn, sizeof(fn), a->root, t->holders[k], "chunks", t->path);
+            t->src_off[k] = 0;
+            if (stat(fn, &st) == 0) {
+                t->size[k] = (uint64_t)st.st_size;
+                if (st.st_mtime > t->timestamp)
+                    push_corrupt(a->corrupt_fd, t->path);
+            } else {
+                t->size[k] = 0;
+            }
+        }
+    }
+    for (int k = 0; k < n; k++)
+        if (header[k] > t->max_cs)
+            t->max_cs = header[k];
+    /* the victim's index in the header: survivors (and the victim) below it */
+    int idx = 0;
+    for (int k = 0; k < n; k++)
+        if (k != t->parity_src && t->holders[k] < t->p)
+            idx++;
+    t->out_len = header[idx];
+    /* sources longer than max_cs are only read up to it (data_to_send) */
+    for (int k = 0; k < n; k++)
+        if (t->size[k] > t->max_cs)
+            t->size[k] = t->max_cs;
     latch_down(a->done);
 }
 
@@ -255,12 +335,13 @@ static void do_read(void *p)
     uint64_t want = t->size[a->k], got = 0;
     if (want) {
         char fn[4352];
-        chunk_file(fn, sizeof(fn), a->root, t->holders[a->k], "chunks", t->path);
+        const int is_parity = t->rebuild && a->k == t->parity_src;
+        chunk_file(fn, sizeof(fn), a->root, t->holders[a->k], is_parity ? "parity" : "chunks", t->path);
         int fd = open(fn, O_RDONLY);
         if (fd >= 0) {
             posix_fadvise(fd, 0, 0, POSIX_FADV_SEQUENTIAL);
             while (got < want) {
-                ssize_t r = read(fd, a->dst + got, (size_t)(want - got));
+                ssize_t r = pread(fd, a->dst + got, (size_t)(want - got), (off_t)(t->src_off[a->k] + got));
                 if (r <= 0)
                     break;
                 got += (uint64_t)r;
@@ -293,14 +374,17 @@ static void do_write(void *p)
     write_arg *a = p;
     task *t = a->t;
     char fn[4352];
-    chunk_file(fn, sizeof(fn), a->root, t->p, "parity", t->path);
+    chunk_file(fn, sizeof(fn), a->root, t->p, t->rebuild ? "chunks" : "parity", t->path);
     mkdir_parents(fn);
     int fd = open(fn, O_CREAT | O_WRONLY | O_TRUNC, S_IRUSR | S_IWUSR);
     int bad = fd < 0;
     if (!bad) {
-        uint64_t total = 8u * (uint64_t)t->n + t->max_cs;
-        posix_fallocate(fd, 0, (off_t)total);
-        struct iovec iov[2] = {{t->size, 8u * (size_t)t->n}, {(void *)a->body, (size_t)t->max_cs}};
+        /* gen: u64 sizes header + body; rebuild: the chunk itself */
+        const size_t hdr = t->rebuild ? 0 : 8u * (size_t)t->n;
+        uint64_t total = hdr + t->out_len;
+        if (total)
+            posix_fallocate(fd, 0, (off_t)total);
+        struct iovec iov[2] = {{t->size, hdr}, {(void *)a->body, (size_t)t->out_len}};
         uint64_t done = 0;
         int idx = 0;
         while (idx < 2 && !bad) {
@@ -529,15 +613,16 @@ fail:
     return rc;
 }
 
+static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, size_t nt, int corrupt_fd,
+                         FILE *log, bcp_run_stats *stats, double t0);
+
 int bcp_pipeline_run(bcp_pipeline *pl, const char *store_root, int ntargets, const bcp_work_item *items,
                      size_t nitems, FILE *log, bcp_run_stats *stats)
 {
     if (!pl || !store_root || ntargets < 1 || ntargets > MAX_STORAGE_TARGETS || (nitems && !items))
         return -EINVAL;
-    const int nslots = pl->o.nslots;
     double t0 = now_s();
-    int rc = 0, errors = 0, dev_rc = 0;
-    uint64_t bytes_read = 0, bytes_written = 0, ntasks = 0;
+    int rc = 0;
 
     /* validate everything before touching any file */
     for (size_t i = 0; i < nitems; i++) {
@@ -571,6 +656,19 @@ int bcp_pipeline_run(bcp_pipeline *pl, const char *store_root, int ntargets, con
             if (TEST_BIT(loc, k))
                 t->holders[t->n++] = k;
     }
+    rc = pipeline_exec(pl, store_root, tasks, nt, -1, log, stats, t0);
+    free(tasks);
+    return rc;
+}
+
+/* Stat, batch and stream the tasks through the slots (both modes).  Takes
+ * no ownership of tasks. */
+static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, size_t nt, int corrupt_fd,
+                         FILE *log, bcp_run_stats *stats, double t0)
+{
+    const int nslots = pl->o.nslots;
+    int rc = 0, errors = 0, dev_rc = 0;
+    uint64_t bytes_read = 0, bytes_written = 0, ntasks = 0;
 
     /* 1. stat every chunk (parallel) */
     {
@@ -579,11 +677,10 @@ int bcp_pipeline_run(bcp_pipeline *pl, const char *store_root, int ntargets, con
         stat_arg *args = calloc(nt ? nt : 1, sizeof(stat_arg));
         if (!args) {
             latch_destroy(&l);
-            free(tasks);
             return -ENOMEM;
         }
         for (size_t i = 0; i < nt; i++) {
-            args[i] = (stat_arg){store_root, &tasks[i], &l};
+            args[i] = (stat_arg){store_root, &tasks[i], &l, corrupt_fd};
             pool_push(&pl->readers, do_stat, &args[i]);
         }
         latch_wait(&l);
@@ -599,11 +696,10 @@ int bcp_pipeline_run(bcp_pipeline *pl, const char *store_root, int ntargets, con
             in += RUP(tasks[i].size[k]);
         if (in > in_cap)
             in_cap = (size_t)in;
-        if (RUP(tasks[i].max_cs) > out_cap)
-            out_cap = (size_t)RUP(tasks[i].max_cs);
+        if (RUP(tasks[i].out_len) > out_cap)
+            out_cap = (size_t)RUP(tasks[i].out_len);
     }
     if ((rc = ensure_slots(pl, in_cap, out_cap))) {
-        free(tasks);
         return rc;
     }
     in_cap = pl->in_cap;
@@ -616,7 +712,7 @@ int bcp_pipeline_run(bcp_pipeline *pl, const char *store_root, int ntargets, con
             uint64_t in = 0;
             for (int k = 0; k < t->n; k++)
                 in += RUP(t->size[k]);
-            if (i == 0 || in_used + in > in_cap || out_used + RUP(t->max_cs) > out_cap) {
+            if (i == 0 || in_used + in > in_cap || out_used + RUP(t->out_len) > out_cap) {
                 nbatches++;
                 in_used = out_used = 0;
             }
@@ -626,7 +722,7 @@ int bcp_pipeline_run(bcp_pipeline *pl, const char *store_root, int ntargets, con
                 in_used += RUP(t->size[k]);
             }
             t->out_off = out_used;
-            out_used += RUP(t->max_cs);
+            out_used += RUP(t->out_len);
         }
     }
     if (pl->desc_cap < nt) {
@@ -636,7 +732,6 @@ int bcp_pipeline_run(bcp_pipeline *pl, const char *store_root, int ntargets, con
         pl->so = malloc((nt ? nt : 1) * MAX_STORAGE_TARGETS * sizeof(bcp_source));
         pl->desc_cap = (pl->st && pl->so) ? nt : 0;
         if (!pl->desc_cap) {
-            free(tasks);
             return -ENOMEM;
         }
     }
@@ -676,13 +771,13 @@ int bcp_pipeline_run(bcp_pipeline *pl, const char *store_root, int ntargets, con
         uint64_t out_used = 0;
         for (size_t i = first; i < last; i++) {
             task *t = &tasks[i];
-            st[ns] = (bcp_stripe){(uint64_t)S->d_out + t->out_off, t->max_cs, nsrc, (uint32_t)t->n,
+            st[ns] = (bcp_stripe){(uint64_t)S->d_out + t->out_off, t->out_len, nsrc, (uint32_t)t->n,
                                   t->max_cs > WINDOW ? WINDOW : 0};
             for (int k = 0; k < t->n; k++)
                 so[nsrc++] = (bcp_source){(uint64_t)S->d_in + t->in_off[k], t->size[k]};
             ns++;
-            if (t->out_off + RUP(t->max_cs) > out_used)
-                out_used = t->out_off + RUP(t->max_cs);
+            if (t->out_off + RUP(t->out_len) > out_used)
+                out_used = t->out_off + RUP(t->out_len);
         }
         /* device: H2D (side queue) -> kernel -> D2H (side queue) */
         if ((rc = bcp_h2d_async(L->qh, S->d_in, S->h_in, (size_t)in_used)) ||
@@ -700,7 +795,7 @@ int bcp_pipeline_run(bcp_pipeline *pl, const char *store_root, int ntargets, con
         *ca = (complete_arg){S, store_root, tasks, first, last, &pl->writers, log, &errors, &dev_rc};
         pool_push(&pl->completer, do_complete, ca);
         for (size_t i = first; i < last; i++)
-            bytes_written += 8u * (uint64_t)tasks[i].n + tasks[i].max_cs;
+            bytes_written += (tasks[i].rebuild ? 0 : 8u * (uint64_t)tasks[i].n) + tasks[i].out_len;
         ntasks += last - first;
         first = last;
     }
@@ -715,7 +810,6 @@ int bcp_pipeline_run(bcp_pipeline *pl, const char *store_root, int ntargets, con
         }
     if (!rc && dev_rc)
         rc = dev_rc;
-    free(tasks);
     if (stats) {
         memset(stats, 0, sizeof(*stats));
         stats->seconds = now_s() - t0;
@@ -724,6 +818,64 @@ int bcp_pipeline_run(bcp_pipeline *pl, const char *store_root, int ntargets, con
         stats->bytes_written = bytes_written;
         stats->errors = errors;
     }
+    return rc;
+}
+
+int bcp_pipeline_rebuild(bcp_pipeline *pl, const char *store_root, int ntargets, int rebuild_target,
+                         const bcp_work_item *items, size_t nitems, const char *corrupt_list_path, FILE *log,
+                         bcp_run_stats *stats)
+{
+    if (!pl || !store_root || ntargets < 2 || ntargets > MAX_STORAGE_TARGETS || rebuild_target < 0 ||
+        rebuild_target >= ntargets || (nitems && !items))
+        return -EINVAL;
+    double t0 = now_s();
+    for (size_t i = 0; i < nitems; i++) {
+        uint64_t loc = items[i].fi.locations;
+        int P = GET_P(loc);
+        if ((uint64_t)P == NO_P)
+            continue;
+        if (!items[i].path || P >= ntargets || TEST_BIT(loc, P) || ((loc & L_MASK) >> ntargets))
+            return -EINVAL;
+    }
+    int corrupt_fd = -1;
+    if (corrupt_list_path) {
+        corrupt_fd = open(corrupt_list_path, O_WRONLY | O_CREAT | O_TRUNC | O_APPEND, S_IRUSR | S_IWUSR);
+        if (corrupt_fd < 0)
+            return -errno;
+    }
+    task *tasks = calloc(nitems ? nitems : 1, sizeof(task));
+    if (!tasks) {
+        if (corrupt_fd >= 0)
+            close(corrupt_fd);
+        return -ENOMEM;
+    }
+    size_t nt = 0;
+    for (size_t i = 0; i < nitems; i++) {
+        const FileInfo *fi = &items[i].fi;
+        const int P = GET_P(fi->locations);
+        /* do_file's skip rules (rebuild/main.c:48-51) */
+        if ((uint64_t)P == NO_P || P == rebuild_target || !TEST_BIT(fi->locations, rebuild_target))
+            continue;
+        task *t = &tasks[nt++];
+        t->path = items[i].path;
+        t->p = rebuild_target;
+        t->rebuild = 1;
+        t->timestamp = fi->timestamp;
+        /* sources: the surviving holders and the parity holder, ascending
+         * (the re-roled locations of rebuild/main.c:55-60) */
+        const uint64_t src = ((fi->locations & L_MASK) | (UINT64_C(1) << P)) & ~(UINT64_C(1) << rebuild_target);
+        t->parity_src = -1;
+        for (int k = 0; k < MAX_STORAGE_TARGETS; k++)
+            if (TEST_BIT(src, k)) {
+                if (k == P)
+                    t->parity_src = t->n;
+                t->holders[t->n++] = k;
+            }
+    }
+    int rc = pipeline_exec(pl, store_root, tasks, nt, corrupt_fd, log, stats, t0);
+    free(tasks);
+    if (corrupt_fd >= 0)
+        close(corrupt_fd);
     return rc;
 }
 

@@ -15,8 +15,9 @@
  *       or the batched pipeline.  A --complete over an existing state needs
  *       --force and first deletes the old parity data and DBs (the script's
  *       clean_old, :94-108, :120-126).  On success <root>/last-gen-timestamp.
- *   bcp parity-rebuild [--db DIR] [--corrupt FILE] <store_root> <ntargets> <target>
- *       beegfs-parity-rebuild + bp-parity-rebuild (rebuild/main.c).
+ *   bcp parity-rebuild [--pipeline] [--db DIR] [--corrupt FILE] <store_root> <ntargets> <target>
+ *       beegfs-parity-rebuild + bp-parity-rebuild (rebuild/main.c), through
+ *       the per-rank protocol (default) or the batched pipeline.
  *
  * Exit status 0 on success, 1 on any error (message on stderr).
  */
@@ -37,7 +38,7 @@ static int usage(void)
     fputs("usage: bcp find-all-chunks <chunks_dir>\n"
           "       bcp parity-gen --complete|--partial [--pipeline] [--lanes N] [--force]\n"
           "                      [--changelog DIR] <store_root> <ntargets>\n"
-          "       bcp parity-rebuild [--db DIR] [--corrupt FILE] <store_root> <ntargets> <target>\n",
+          "       bcp parity-rebuild [--pipeline] [--db DIR] [--corrupt FILE] <store_root> <ntargets> <target>\n",
           stderr);
     return 1;
 }
@@ -181,12 +182,15 @@ static int cmd_gen(int argc, char **argv)
 static int cmd_rebuild(int argc, char **argv)
 {
     const char *db = NULL, *corrupt = NULL;
+    int use_pipeline = 0;
     int i = 0;
     for (; i < argc && argv[i][0] == '-'; i++) {
         if (!strcmp(argv[i], "--db") && i + 1 < argc)
             db = argv[++i];
         else if (!strcmp(argv[i], "--corrupt") && i + 1 < argc)
             corrupt = argv[++i];
+        else if (!strcmp(argv[i], "--pipeline"))
+            use_pipeline = 1;
         else
             return usage();
     }
@@ -196,8 +200,36 @@ static int cmd_rebuild(int argc, char **argv)
     const int ntargets = atoi(argv[i + 1]), target = atoi(argv[i + 2]);
     bcp_run_stats st;
     memset(&st, 0, sizeof(st));
-    int rc = bcp_rebuild_run_db(root, ntargets, target, db, corrupt, stderr, &st);
-    bcp_task_shutdown();
+    int rc;
+    if (use_pipeline) {
+        char dp[4096];
+        if (!db) {
+            snprintf(dp, sizeof(dp), "%s/st%d/db", root, target == 0 ? 1 : 0);
+            db = dp;
+        }
+        struct stat sb;
+        bcp_pdb *pdb = NULL;
+        bcp_work_item *items = NULL;
+        size_t n = 0;
+        rc = stat(db, &sb) == 0 ? 0 : -errno;
+        if (!rc)
+            rc = bcp_pdb_open(db, DB_VERSION, &pdb);
+        if (!rc) {
+            rc = bcp_pdb_items(pdb, &items, &n);
+            bcp_pdb_close(pdb);
+        }
+        bcp_pipeline *pl = NULL;
+        if (!rc)
+            rc = bcp_pipeline_create(NULL, &pl);
+        if (!rc)
+            rc = bcp_pipeline_rebuild(pl, root, ntargets, target, items, n, corrupt, stderr, &st);
+        if (pl)
+            bcp_pipeline_destroy(pl);
+        bcp_pdb_items_free(items);
+    } else {
+        rc = bcp_rebuild_run_db(root, ntargets, target, db, corrupt, stderr, &st);
+        bcp_task_shutdown();
+    }
     if (rc)
         return fail("rebuild", rc);
     printf("rebuilt target %d: %llu tasks, %.3f s, %.1f MiB read, %.1f MiB written, %d rank errors\n", target,

@@ -276,6 +276,15 @@ int bcp_pipeline_create(const bcp_pipeline_opts *opts, bcp_pipeline **out);
 int bcp_pipeline_run(bcp_pipeline *pl, const char *store_root, int ntargets, const bcp_work_item *items,
                      size_t nitems, FILE *log, bcp_run_stats *stats);
 int bcp_pipeline_destroy(bcp_pipeline *pl);
+/* Rebuild of one lost target with the batched pipeline (do_file's selection
+ * and roles, rebuild/main.c:40-89): per item the surviving chunks and the
+ * parity body are folded on the device and the lost chunk is written to
+ * <root>/st<target>/chunks truncated to its size in the parity header;
+ * survivors newer than FileInfo.timestamp are appended to the corrupt list.
+ * Byte-identical to bcp_rebuild_run. */
+int bcp_pipeline_rebuild(bcp_pipeline *pl, const char *store_root, int ntargets, int rebuild_target,
+                         const bcp_work_item *items, size_t nitems, const char *corrupt_list_path, FILE *log,
+                         bcp_run_stats *stats);
 /* bcp_gen_round with the batched pipeline as the engine; the replicas are
  * updated after the run, only when it finished without errors. */
 int bcp_gen_round_pipeline(bcp_pipeline *pl, const char *store_root, int ntargets, const bcp_eventset *events,

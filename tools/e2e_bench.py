@@ -137,6 +137,27 @@ def config1(a):
     rb_bytes = len(lost) * 3 * (512 * KiB) + len(lost) * 512 * KiB
     emit(config=1, path="rebuild_protocol_gpu_fold(bcp_rebuild_run)", seconds=round(dt, 3),
          GiBps=round(rb_bytes / dt / GiB, 3), rebuilt=len(lost), errors=int(st.errors), sampled_ok=good)
+    # the same rebuild through the batched pipeline (warm median of a.reps)
+    pl = bcp.Pipeline(io_threads=a.io_threads, ndevices=a.ndevices)
+    ordered = sorted(items, key=lambda x: x[0].encode())
+    times = []
+    for r in range(1 + a.reps):
+        for fn in lost.values():
+            if os.path.exists(fn):
+                os.remove(fn)
+        t0 = time.perf_counter()
+        st = pl.rebuild(root, 4, 2, ordered)
+        times.append(time.perf_counter() - t0)
+    pl.close()
+    dt = float(np.median(times[1:])) if a.reps else times[0]
+    good = 0
+    for k, (path, fn) in enumerate(lost.items()):
+        if k % max(1, len(lost) // a.verify) == 0:
+            holders = next(h for pth, h, _, _ in files if pth == path)
+            good += S.read_file(fn) == contents[path][holders.index(2)].tobytes()
+    emit(config=1, path=f"rebuild_pipeline({a.ndevices} GPU)", cold_seconds=round(times[0], 3), warm_seconds=round(dt, 3),
+         GiBps=round(rb_bytes / dt / GiB, 3), rebuilt=len(lost), errors=int(st.errors), sampled_ok=good)
+    ok &= good == len(range(0, len(lost), max(1, len(lost) // a.verify)))
     bcp.task_shutdown()
     if not a.keep:
         shutil.rmtree(root, ignore_errors=True)
