@@ -386,7 +386,7 @@ static void do_write(void *p)
             posix_fallocate(fd, 0, (off_t)total);
         struct iovec iov[2] = {{t->size, hdr}, {(void *)a->body, (size_t)t->out_len}};
         uint64_t done = 0;
-        int idx = 0;
+        int idx = total ? 0 : 2; /* an empty rebuilt chunk: nothing to write */
         while (idx < 2 && !bad) {
             ssize_t w = writev(fd, iov + idx, 2 - idx);
             if (w <= 0) {
