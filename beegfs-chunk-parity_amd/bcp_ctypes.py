@@ -89,6 +89,7 @@ _SIGS = {
     "bcp_dev_alloc": ([_V, ctypes.c_size_t, ctypes.POINTER(_V)], ctypes.c_int),
     "bcp_dev_free": ([_V, _V], ctypes.c_int),
     "bcp_host_alloc": ([_V, ctypes.c_size_t, ctypes.POINTER(_V)], ctypes.c_int),
+    "bcp_host_alloc_mapped": ([_V, ctypes.c_size_t, ctypes.POINTER(_V)], ctypes.c_int),
     "bcp_host_free": ([_V, _V], ctypes.c_int),
     "bcp_h2d_async": ([_V, _V, _V, ctypes.c_size_t], ctypes.c_int),
     "bcp_d2h_async": ([_V, _V, _V, ctypes.c_size_t], ctypes.c_int),
@@ -113,6 +114,7 @@ _SIGS = {
     "bcp_task_set_device_map": ([ctypes.POINTER(ctypes.c_int), ctypes.c_int], ctypes.c_int),
     "bcp_task_shutdown": ([], ctypes.c_int),
     "bcp_task_set_xor_hook": ([_V, _V], None),
+    "bcp_task_set_fold_mode": ([ctypes.c_int], ctypes.c_int),
     "bcp_assign_lanes": ([ctypes.c_int, ctypes.c_uint64, ctypes.POINTER(FileInfo), ctypes.POINTER(ctypes.c_int)], None),
     "bcp_gen_run": ([ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(WorkItem), ctypes.c_size_t, ctypes.c_int,
                      ctypes.POINTER(ctypes.c_int), _V, ctypes.POINTER(RunStats)], ctypes.c_int),
@@ -241,9 +243,10 @@ class Engine:
     def free(self, ptr: int):
         call("bcp_dev_free", self.h, _V(ptr))
 
-    def host_alloc(self, nbytes: int) -> int:
+    def host_alloc(self, nbytes: int, mapped: bool = False) -> int:
+        """Pinned host memory; mapped=True: coherent, read/written by kernels in place."""
         p = _V()
-        call("bcp_host_alloc", self.h, nbytes, ctypes.byref(p))
+        call("bcp_host_alloc_mapped" if mapped else "bcp_host_alloc", self.h, nbytes, ctypes.byref(p))
         return p.value
 
     def host_free(self, ptr: int):
@@ -547,6 +550,17 @@ class Pipeline:
 def set_xor_hook(fn_addr: int | None, ctx: int | None = None):
     """Test injection point: route the P role's fold to a C function (address)."""
     lib().bcp_task_set_xor_hook(_V(fn_addr) if fn_addr else None, _V(ctx) if ctx else None)
+
+
+FOLD_ZERO_COPY, FOLD_STAGED = 0, 1
+
+
+def set_fold_mode(mode: int) -> int:
+    """P-role fold: FOLD_ZERO_COPY (default) or FOLD_STAGED; returns the previous mode."""
+    rc = lib().bcp_task_set_fold_mode(mode)
+    if rc < 0:
+        raise BcpError("bcp_task_set_fold_mode", rc)
+    return rc
 
 
 def task_shutdown():

@@ -383,6 +383,15 @@ extern "C" int bcp_host_alloc(bcp_engine *eng, size_t bytes, void **hptr) {
   return 0;
 }
 
+extern "C" int bcp_host_alloc_mapped(bcp_engine *eng, size_t bytes, void **hptr) {
+  if (!eng || !hptr) return -EINVAL;
+  *hptr = nullptr;
+  int rc = set_device(eng);
+  if (rc) return rc;
+  HIP_RC(hipHostMalloc(hptr, bytes ? bytes : 16, hipHostMallocMapped | hipHostMallocCoherent));
+  return 0;
+}
+
 extern "C" int bcp_host_free(bcp_engine *eng, void *hptr) {
   if (!eng) return -EINVAL;
   if (!hptr) return 0;

@@ -8,10 +8,12 @@
  *   parity_generator  :117-245  P role: sizes -> max_cs -> windows -> parity
  *   chunk_sender      :247-322  source role: size -> windows (zero padded)
  * over the loopback transport (bcp_loopback.c) instead of MPI.  The window
- * fold (xor_parity at :211) becomes: pinned window rows (256-byte pitch, so
- * every row is 16-byte aligned for the fast kernel) -> H2D -> XOR kernel ->
- * D2H on the calling lane's own HIP queue.  Twelve lanes per rank therefore
- * keep twelve queues of copies and kernels in flight on the device.
+ * fold (xor_parity at :211) becomes one XOR kernel on the lane's own HIP
+ * queue that reads the pinned window rows (256-byte pitch, so every row is
+ * 16-byte aligned for the fast kernel) and writes the pinned parity block in
+ * place over PCIe (zero copy; the staged H2D -> kernel -> D2H form is kept as
+ * bcp_task_set_fold_mode(BCP_FOLD_STAGED)).  Twelve lanes per rank keep
+ * twelve queues of folds in flight on the device.
  */
 #define _GNU_SOURCE
 #include <assert.h>
@@ -52,6 +54,7 @@ static int g_devmap[MAX_STORAGE_TARGETS];
 static int g_devmap_n = 0;
 static bcp_xor_hook_fn g_hook = NULL;
 static void *g_hook_ctx = NULL;
+static int g_fold_mode = BCP_FOLD_ZERO_COPY;
 
 int bcp_task_set_device_map(const int *devices, int ntargets)
 {
@@ -63,6 +66,17 @@ int bcp_task_set_device_map(const int *devices, int ntargets)
     g_devmap_n = ntargets;
     pthread_mutex_unlock(&g_lock);
     return 0;
+}
+
+int bcp_task_set_fold_mode(int mode)
+{
+    if (mode != BCP_FOLD_ZERO_COPY && mode != BCP_FOLD_STAGED)
+        return -EINVAL;
+    pthread_mutex_lock(&g_lock);
+    int prev = g_fold_mode;
+    g_fold_mode = mode;
+    pthread_mutex_unlock(&g_lock);
+    return prev;
 }
 
 void bcp_task_set_xor_hook(bcp_xor_hook_fn fn, void *ctx)
@@ -198,7 +212,7 @@ static int grow(fold_res *R, uint8_t **p, size_t *cap, size_t need)
     size_t c = MAX_(need, (size_t)1 << 20);
     int rc = 0;
     if (R->device >= 0)
-        rc = bcp_host_alloc(R->eng, c, (void **)p);
+        rc = bcp_host_alloc_mapped(R->eng, c, (void **)p);
     else if (!(*p = malloc(c)))
         rc = -ENOMEM;
     if (!rc)
@@ -264,9 +278,6 @@ static int res_acquire(HostState *hs, int use_gpu, size_t rows_bytes, size_t nby
     if ((rc = grow(R, &R->h_win[0], &R->h_cap, rows_bytes)) || (rc = grow(R, &R->h_win[1], &R->h_cap1, rows_bytes)) ||
         (rc = grow(R, &R->h_par, &R->hp_cap, nbytes)))
         goto fail;
-    if (use_gpu && ((rc = grow_dev(R, &R->d_src, &R->d_cap, rows_bytes)) ||
-                    (rc = grow_dev(R, &R->d_out, &R->dout_cap, nbytes))))
-        goto fail;
     *out = R;
     return 0;
 fail:
@@ -288,6 +299,18 @@ static int fold_window(fold_res *R, HostState *hs, bcp_xor_hook_fn hook, void *c
         return hook(out, nbytes, rows, pitch, n, ctx);
     }
     int rc;
+    pthread_mutex_lock(&g_lock);
+    const int mode = g_fold_mode;
+    pthread_mutex_unlock(&g_lock);
+    if (mode == BCP_FOLD_ZERO_COPY) {
+        /* rows and out are mapped pinned memory (grow): the kernel streams
+         * them over PCIe, no copy commands */
+        if ((rc = bcp_xor_strided_async(R->q, out, pitch, rows, pitch * (size_t)n, pitch, 1, (uint32_t)n, nbytes)))
+            return rc;
+        return bcp_queue_sync(R->q);
+    }
+    if ((rc = grow_dev(R, &R->d_src, &R->d_cap, pitch * (size_t)n)) || (rc = grow_dev(R, &R->d_out, &R->dout_cap, nbytes)))
+        return rc;
     if ((rc = bcp_h2d_async(R->q, R->d_src, rows, pitch * (size_t)n)))
         return rc;
     if ((rc = bcp_xor_strided_async(R->q, R->d_out, pitch, R->d_src, pitch * (size_t)n, pitch, 1, (uint32_t)n,

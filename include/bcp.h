@@ -108,6 +108,11 @@ int bcp_dev_alloc(bcp_engine *eng, size_t bytes, void **dptr);
 int bcp_dev_free(bcp_engine *eng, void *dptr);
 /* Pinned (page-locked) host memory for staging. */
 int bcp_host_alloc(bcp_engine *eng, size_t bytes, void **hptr);
+/* Pinned host memory that kernels read and write in place over PCIe
+ * (coherent, mapped at the same address on the device): zero-copy folds of
+ * single windows, where a copy command per direction costs more than the
+ * data.  Free with bcp_host_free. */
+int bcp_host_alloc_mapped(bcp_engine *eng, size_t bytes, void **hptr);
 int bcp_host_free(bcp_engine *eng, void *hptr);
 /* Async copies, in order on q. */
 int bcp_h2d_async(bcp_queue *q, void *dst, const void *src, size_t bytes);

@@ -98,6 +98,14 @@ int process_task(HostState *hs, const char *path, const FileInfo *fi, TaskInfo t
 /* Device used by the P role of storage target st: devices[st] if a map was
  * given, else st % device_count.  Engines are created lazily, one per device. */
 int bcp_task_set_device_map(const int *devices, int ntargets);
+/* How the P role folds a window on the GPU.  ZERO_COPY (default): the kernel
+ * reads the pinned window rows and writes the pinned parity block in place
+ * over PCIe (one launch + one sync per window).  STAGED: H2D of the rows,
+ * kernel on device buffers, D2H (three commands per window).  Returns the
+ * previous mode, or -EINVAL. */
+#define BCP_FOLD_ZERO_COPY 0
+#define BCP_FOLD_STAGED 1
+int bcp_task_set_fold_mode(int mode);
 /* Release the engines and every lane's queues / staging (call after all
  * lanes have joined). */
 int bcp_task_shutdown(void);

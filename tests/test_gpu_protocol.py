@@ -23,8 +23,17 @@ def gpu_fold(bcp, engine):
     bcp.task_shutdown()
 
 
+@pytest.fixture(params=["zero_copy", "staged"])
+def fold_mode(request, bcp):
+    """Both forms of the P role's GPU fold (bcp_task_set_fold_mode)."""
+    mode = bcp.FOLD_ZERO_COPY if request.param == "zero_copy" else bcp.FOLD_STAGED
+    prev = bcp.set_fold_mode(mode)
+    yield request.param
+    bcp.set_fold_mode(prev)
+
+
 @pytest.mark.parametrize("name", ["KAT-2", "KAT-3", "KAT-4"])
-def test_survey_kats_end_to_end(bcp, oracle, tmp_path, name):
+def test_survey_kats_end_to_end(bcp, oracle, tmp_path, name, fold_mode):
     k = GOLD["survey_kats"][name]
     n = len(k["lens"])
     p = 8 if n == 8 else 4
@@ -47,7 +56,7 @@ def test_survey_kats_end_to_end(bcp, oracle, tmp_path, name):
 
 
 @pytest.mark.parametrize("seed", range(3))
-def test_random_worklists_end_to_end(bcp, oracle, tmp_path, seed):
+def test_random_worklists_end_to_end(bcp, oracle, tmp_path, seed, fold_mode):
     rng = np.random.default_rng(50 + seed)
     ntargets = int(rng.integers(5, 14))
     files = []
@@ -154,6 +163,29 @@ def test_protocol_repeated_runs_reuse_pool(bcp, oracle, tmp_path):
         assert st.errors == 0
     for (path, holders, p, lens) in files:
         assert S.read_file(S.parity_path(root, p, path)) == oracle.gen_parity_file(contents[path])
+
+
+def test_zero_copy_pool_reuse_with_changing_data(bcp, oracle, tmp_path):
+    """The pooled mapped window rows are rewritten between runs and between
+    modes: no fold may see a previous task's bytes."""
+    root = str(tmp_path)
+    rng = np.random.default_rng(77)
+    for rnd in range(4):
+        files = [(f"z/{i}", [0, 1, 2], 3, [int(x) for x in rng.integers(1, 600_000, size=3)]) for i in range(24)]
+        items, contents = S.populate(root, 4, files, seed=100 + rnd)
+        prev = bcp.set_fold_mode(bcp.FOLD_STAGED if rnd % 2 else bcp.FOLD_ZERO_COPY)
+        try:
+            st = bcp.gen_run(root, 4, items, nlanes=6)
+        finally:
+            bcp.set_fold_mode(prev)
+        assert st.errors == 0
+        for (path, holders, p, lens) in files:
+            assert S.read_file(S.parity_path(root, p, path)) == oracle.gen_parity_file(contents[path]), (rnd, path)
+
+
+def test_fold_mode_rejects_unknown(bcp):
+    with pytest.raises(bcp.BcpError):
+        bcp.set_fold_mode(7)
 
 
 @pytest.mark.parametrize("engine_kind", ["protocol", "pipeline"])

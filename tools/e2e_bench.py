@@ -111,6 +111,11 @@ def config1(a):
         return ok
 
     ok = run("protocol_gpu_fold(bcp_gen_run,12 lanes)", lambda: bcp.gen_run(root, 4, items, nlanes=12))
+    bcp.set_fold_mode(bcp.FOLD_STAGED)
+    try:
+        ok &= run("protocol_gpu_fold_staged(H2D,kernel,D2H; 12 lanes)", lambda: bcp.gen_run(root, 4, items, nlanes=12))
+    finally:
+        bcp.set_fold_mode(bcp.FOLD_ZERO_COPY)
     ol = oracle.lib()
     bcp.set_xor_hook(ctypes.cast(ol.oracle_xor_rows, ctypes.c_void_p).value)
     try:
@@ -126,17 +131,39 @@ def config1(a):
         if 2 in holders:
             lost[path] = S.chunk_path(root, 2, path)
             os.remove(lost[path])
-    t0 = time.perf_counter()
-    st = bcp.rebuild_run(root, 4, 2, items)
-    dt = time.perf_counter() - t0
-    good = 0
-    for k, (path, fn) in enumerate(lost.items()):
-        if k % max(1, len(lost) // a.verify) == 0:
-            holders = next(h for pth, h, _, _ in files if pth == path)
-            good += S.read_file(fn) == contents[path][holders.index(2)].tobytes()
     rb_bytes = len(lost) * 3 * (512 * KiB) + len(lost) * 512 * KiB
-    emit(config=1, path="rebuild_protocol_gpu_fold(bcp_rebuild_run)", seconds=round(dt, 3),
-         GiBps=round(rb_bytes / dt / GiB, 3), rebuilt=len(lost), errors=int(st.errors), sampled_ok=good)
+
+    def rebuild_protocol(label):
+        """single lane, as rebuild/main.c; cold run then a.reps warm runs"""
+        times = []
+        for r in range(1 + a.reps):
+            for fn in lost.values():
+                if os.path.exists(fn):
+                    os.remove(fn)
+            t0 = time.perf_counter()
+            st = bcp.rebuild_run(root, 4, 2, items)
+            times.append(time.perf_counter() - t0)
+        dt = float(np.median(times[1:])) if a.reps else times[0]
+        good = 0
+        for k, (path, fn) in enumerate(lost.items()):
+            if k % max(1, len(lost) // a.verify) == 0:
+                holders = next(h for pth, h, _, _ in files if pth == path)
+                good += S.read_file(fn) == contents[path][holders.index(2)].tobytes()
+        emit(config=1, path=label, cold_seconds=round(times[0], 3), warm_seconds=round(dt, 3),
+             GiBps=round(rb_bytes / dt / GiB, 3), rebuilt=len(lost), errors=int(st.errors), sampled_ok=good)
+        return good == len(range(0, len(lost), max(1, len(lost) // a.verify)))
+
+    ok &= rebuild_protocol("rebuild_protocol_gpu_fold(bcp_rebuild_run)")
+    bcp.set_fold_mode(bcp.FOLD_STAGED)
+    try:
+        ok &= rebuild_protocol("rebuild_protocol_gpu_fold_staged(bcp_rebuild_run)")
+    finally:
+        bcp.set_fold_mode(bcp.FOLD_ZERO_COPY)
+    bcp.set_xor_hook(ctypes.cast(ol.oracle_xor_rows, ctypes.c_void_p).value)
+    try:
+        ok &= rebuild_protocol("rebuild_protocol_cpu_fold_reference(oracle_xor_rows)")
+    finally:
+        bcp.set_xor_hook(None)
     # the same rebuild through the batched pipeline (warm median of a.reps)
     pl = bcp.Pipeline(io_threads=a.io_threads, ndevices=a.ndevices)
     ordered = sorted(items, key=lambda x: x[0].encode())
