@@ -10,7 +10,7 @@ import os
 import subprocess
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG_DIR, "lib", "libbcp.so")
+LIB_PATH = os.environ.get("BCP_LIB") or os.path.join(PKG_DIR, "lib", "libbcp.so")  # BCP_LIB: A/B of another build
 HEADER_DIR = os.path.join(os.path.dirname(PKG_DIR), "include")
 
 MAX_SOURCES = 56

@@ -15,6 +15,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <new>
 #include <vector>
 
@@ -53,6 +54,8 @@ struct bcp_queue {
   unsigned long long *qctr = nullptr;  // work-queue counter of xor_stream (device)
   unsigned long long qbase = 0;        // its value when the next launch starts
   hipEvent_t timer[kTimerSlots] = {};
+  DescTile *tiles = nullptr;           // tile records of the descriptor kernel (device)
+  size_t tiles_cap = 0;                // in records
 };
 
 struct bcp_event {
@@ -96,8 +99,15 @@ static int grid_for(const bcp_engine *e) {
   return g > 0 ? g : 256;
 }
 
-static int desc_grid_for(const bcp_engine *e) {
-  int g = e->num_cus * e->tuning.desc_blocks_per_cu;
+// Workgroups per CU of the descriptor kernel.  Auto (0): tiles that move
+// close to a full 8-source tile's bytes run best at one workgroup per CU (the
+// narrowest queue window, as xor_stream); sparsely covered tiles (config-5
+// shapes: ~0.43 of a full tile on average) need a second workgroup per CU to
+// keep enough loads in flight (tools/exp/desc_probe.py, profiles/r01/mixed/).
+static int desc_grid_for(const bcp_engine *e, double bytes_per_tile, uint32_t tile_bytes) {
+  int bpc = e->tuning.desc_blocks_per_cu;
+  if (bpc <= 0) bpc = bytes_per_tile >= 0.6 * (double)(kTileSrcs + 1) * tile_bytes ? 1 : 2;
+  int g = e->num_cus * bpc;
   return g > 0 ? g : 256;
 }
 
@@ -197,11 +207,12 @@ extern "C" int bcp_set_option(bcp_engine *eng, const char *key, int value) {
   pthread_mutex_lock(&eng->lock);
   if (!strcmp(key, "blocks_per_cu") && value >= 1 && value <= 32) eng->tuning.blocks_per_cu = value;
   else if (!strcmp(key, "vecs_per_thread") && stream_vecs_ok(value)) eng->tuning.vecs_per_thread = value;
-  else if (!strcmp(key, "desc_blocks_per_cu") && value >= 1 && value <= 32) eng->tuning.desc_blocks_per_cu = value;
+  else if (!strcmp(key, "desc_blocks_per_cu") && value >= 0 && value <= 32) eng->tuning.desc_blocks_per_cu = value;
   else if (!strcmp(key, "desc_vecs_per_thread") && desc_vecs_ok(value)) eng->tuning.desc_vecs = value;
   else if (!strcmp(key, "schedule") && (value == kSchedQueue || value == kSchedStatic)) eng->tuning.schedule = value;
   else if (!strcmp(key, "desc_schedule") && (value == kSchedQueue || value == kSchedStatic)) eng->tuning.desc_schedule = value;
   else if (!strcmp(key, "desc_grab") && value >= 1 && value <= 64) eng->tuning.desc_grab = value;
+  else if (!strcmp(key, "desc_force") && (value == 0 || value == 1)) eng->tuning.desc_force = value;
   else rc = -EINVAL;
   pthread_mutex_unlock(&eng->lock);
   return rc;
@@ -219,6 +230,7 @@ extern "C" int bcp_get_option(bcp_engine *eng, const char *key, int *value) {
   else if (!strcmp(key, "desc_vecs_per_thread")) *value = t.desc_vecs;
   else if (!strcmp(key, "desc_schedule")) *value = t.desc_schedule;
   else if (!strcmp(key, "desc_grab")) *value = t.desc_grab;
+  else if (!strcmp(key, "desc_force")) *value = t.desc_force;
   else rc = -EINVAL;
   pthread_mutex_unlock(&eng->lock);
   return rc;
@@ -273,6 +285,7 @@ extern "C" int bcp_queue_destroy(bcp_queue *q) {
   for (auto &t : q->timer)
     if (t) (void)hipEventDestroy(t);
   if (q->qctr) (void)hipFree(q->qctr);
+  if (q->tiles) (void)hipFree(q->tiles);
   (void)hipStreamDestroy(q->stream);
   delete q;
   return 0;
@@ -480,21 +493,26 @@ static int submit_desc(bcp_queue *q, const bcp_stripe *stripes, uint32_t nstripe
   bcp_engine *e = q->eng;
   const int vecs = e->tuning.desc_vecs;
   const uint32_t tile_bytes = desc_tile_bytes(vecs);
-  // Validate and count tiles.
+  // Validate, count tiles and the bytes they move (padding is not read).
   uint64_t ntiles = 0;
+  double moved = 0;
   for (uint32_t i = 0; i < nstripes; i++) {
     const bcp_stripe &s = stripes[i];
     if ((uint64_t)s.first_src + s.nsrc > nsources) return -EINVAL;
     if (s.nsrc > BCP_MAX_SOURCES) return -EINVAL;
     if (s.out_len && !s.dst) return -EINVAL;
     if (s.window && (s.window & 15u)) return -EINVAL;
-    for (uint32_t k = 0; k < s.nsrc; k++)
-      if (sources[s.first_src + k].len && !sources[s.first_src + k].ptr) return -EINVAL;
+    for (uint32_t k = 0; k < s.nsrc; k++) {
+      const bcp_source &x = sources[s.first_src + k];
+      if (x.len && !x.ptr) return -EINVAL;
+      moved += (double)(x.len < s.out_len ? x.len : s.out_len);
+    }
+    moved += (double)s.out_len;
     ntiles += (s.out_len + tile_bytes - 1) / tile_bytes;
   }
   if (ntiles == 0) return 0;
   if (ntiles > 0xFFFFFFF0ull) return -EINVAL;
-  if (uniform_batch(stripes, nstripes, sources)) {
+  if (!e->tuning.desc_force && uniform_batch(stripes, nstripes, sources)) {
     const int sv = e->tuning.vecs_per_thread;
     const uint64_t len = stripes[0].out_len;
     const uint32_t tps = stream_tiles_per_stripe(len, sv);
@@ -520,15 +538,39 @@ static int submit_desc(bcp_queue *q, const bcp_stripe *stripes, uint32_t nstripe
     slot->used = true;
     return 0;
   }
+  // Staged copy: every stripe gets its own run of sources sorted by length,
+  // longest first (XOR is commutative), so the sources that cover a tile are
+  // always a prefix of the run (desc_tile).  Runs are laid out afresh, so
+  // stripes whose caller ranges overlap stay independent.
+  uint64_t nstaged = 0;
+  for (uint32_t i = 0; i < nstripes; i++) nstaged += stripes[i].nsrc;
+  if (nstaged > 0xFFFFFFFFull) return -EINVAL;
   const size_t off_src = (size_t)nstripes * sizeof(bcp_stripe);
-  const size_t off_tiles = (off_src + (size_t)nsources * sizeof(bcp_source) + 15) & ~(size_t)15;
+  const size_t off_tiles = (off_src + (size_t)nstaged * sizeof(bcp_source) + 15) & ~(size_t)15;
   const size_t bytes = off_tiles + ((size_t)nstripes + 1) * sizeof(uint32_t);
   DescSlot *slot = nullptr;
   int rc = ring_acquire(q, bytes, &slot);
   if (rc) return rc;
   char *h = (char *)slot->host;
-  memcpy(h, stripes, off_src);
-  if (nsources) memcpy(h + off_src, sources, (size_t)nsources * sizeof(bcp_source));
+  bcp_stripe *hs = (bcp_stripe *)h;
+  bcp_source *hso = (bcp_source *)(h + off_src);
+  uint32_t next_src = 0;
+  for (uint32_t i = 0; i < nstripes; i++) {
+    hs[i] = stripes[i];
+    hs[i].first_src = next_src;
+    bcp_source *run = hso + next_src;
+    for (uint32_t k = 0; k < stripes[i].nsrc; k++) {
+      // insertion sort, descending len (runs are short: <= BCP_MAX_SOURCES)
+      const bcp_source x = sources[stripes[i].first_src + k];
+      uint32_t m = k;
+      while (m > 0 && run[m - 1].len < x.len) {
+        run[m] = run[m - 1];
+        m--;
+      }
+      run[m] = x;
+    }
+    next_src += stripes[i].nsrc;
+  }
   uint32_t *ts = (uint32_t *)(h + off_tiles);
   uint32_t acc = 0;
   for (uint32_t i = 0; i < nstripes; i++) {
@@ -536,12 +578,23 @@ static int submit_desc(bcp_queue *q, const bcp_stripe *stripes, uint32_t nstripe
     acc += (uint32_t)((stripes[i].out_len + tile_bytes - 1) / tile_bytes);
   }
   ts[nstripes] = acc;
+  if (q->tiles_cap < acc) {
+    // launches on q are in order; the old records may still be in use
+    HIP_RC(hipStreamSynchronize(q->stream));
+    if (q->tiles) HIP_RC(hipFree(q->tiles));
+    q->tiles = nullptr;
+    q->tiles_cap = 0;
+    const size_t cap = std::max<size_t>(acc + acc / 4, 1u << 16);
+    HIP_RC(hipMalloc((void **)&q->tiles, cap * sizeof(DescTile)));
+    q->tiles_cap = cap;
+  }
   HIP_RC(hipMemcpyAsync(slot->dev, slot->host, bytes, hipMemcpyHostToDevice, q->stream));
   DescBatch b;
   char *d = (char *)slot->dev;
   b.stripes = (const bcp_stripe *)d;
   b.sources = (const bcp_source *)(d + off_src);
   b.tile_start = (const uint32_t *)(d + off_tiles);
+  b.tiles = q->tiles;
   b.nstripes = nstripes;
   b.ntiles = acc;
   b.tile_bytes = tile_bytes;
@@ -550,8 +603,9 @@ static int submit_desc(bcp_queue *q, const bcp_stripe *stripes, uint32_t nstripe
   b.ctr = q->qctr;
   b.base = q->qbase;
   const uint32_t nunits = b.sched == kSchedQueue ? (acc + b.grab - 1) / b.grab : acc;
-  int grid = desc_grid_for(e);
+  int grid = desc_grid_for(e, moved / (double)acc, tile_bytes);
   if ((uint32_t)grid > nunits) grid = (int)nunits;
+  HIP_RC(launch_desc_tiles(q->stream, b));
   HIP_RC(launch_xor_desc(q->stream, grid, vecs, b));
   if (b.sched == kSchedQueue) q->qbase += (uint64_t)nunits + (uint64_t)grid;
   HIP_RC(hipEventRecord(slot->done, q->stream));

@@ -25,14 +25,14 @@ struct Tuning {
     int blocks_per_cu = 1;      // xor_stream: 256-thread workgroups launched per CU
     int vecs_per_thread = 8;    // xor_stream: 16-byte vectors per lane per tile (1, 2, 4, 8)
     int schedule = kSchedQueue; // xor_stream: kSched*
-    // xor_desc, config-5 shapes (profiles/r01/mixed/): 2 workgroups per CU,
-    // 8 vectors per lane, one 32 KiB tile per queue grab = 77.3 % (U = 4 needed
-    // 2-tile grabs: 72.9 %; 1 WG/CU 71.9-75.4 %).  Mixed-size tiles read ~2.4x
-    // fewer bytes than config-2 tiles, so the grab size is per kernel.
-    int desc_blocks_per_cu = 2;
+    // xor_desc (tools/exp/desc_probe.py, profiles/r01/mixed/): 8 vectors per
+    // lane, one 32 KiB tile per queue grab; workgroups per CU 0 = auto by the
+    // batch's bytes per tile (desc_grid_for).
+    int desc_blocks_per_cu = 0;
     int desc_vecs = 8;          // 1, 2, 4, 8
     int desc_grab = 1;          // tiles per work-queue grab
     int desc_schedule = kSchedQueue;
+    int desc_force = 0;         // 1: uniform batches take xor_desc too (A/B only)
 };
 
 // Arguments of the streaming kernel (xor_stream).
@@ -54,11 +54,32 @@ struct StreamArgs {
     int sched;                  // kSched*
 };
 
+// One tile of a descriptor batch, written on the device by desc_tiles.  The
+// record is self-contained so that the fold needs ONE dependent scalar load
+// per tile before its data loads (in r01 every extra dependent round trip
+// in the per-tile chain cost 5-15 % of HBM rate at 1-2 workgroups per CU).
+// Plain tiles list the sources reaching into the tile, sorted longest first:
+// [0, nfull) cover it, [nfull, nany) end inside it (src_bytes readable
+// bytes); zero padding is not listed.  General tiles (window replay, or more
+// than kTileSrcs sources reaching in) take the table path: stripe / tile /
+// first_src in src_bytes[0..2].
+constexpr int kTileSrcs = 8;
+struct alignas(64) DescTile {
+    uint64_t dst;                   // output address of this tile (stripe dst + tile offset)
+    uint32_t out_bytes;             // output bytes in this tile (< tile_bytes on a stripe's last tile)
+    uint32_t meta;                  // nfull | nany << 8 | kTileGeneral
+    uint64_t src[kTileSrcs];        // source address + tile offset
+    uint32_t src_bytes[kTileSrcs];  // readable bytes from src[k]
+};
+constexpr uint32_t kTileGeneral = 0x80000000u;
+static_assert(sizeof(DescTile) == 128, "tile record is two s_load_dwordx16");
+
 // Device-side form of one stripe descriptor batch.
 struct DescBatch {
     const bcp_stripe *stripes;  // [nstripes]
-    const bcp_source *sources;  // [nsources]
+    const bcp_source *sources;  // staged runs, each sorted by len, longest first
     const uint32_t *tile_start; // [nstripes + 1] prefix of tiles per stripe
+    DescTile *tiles;            // [ntiles] (device; written by desc_tiles)
     uint32_t nstripes;
     uint32_t ntiles;
     uint32_t tile_bytes;        // bytes of output per tile
@@ -74,7 +95,10 @@ struct DescBatch {
 hipError_t launch_xor_stream(hipStream_t st, int grid, int vecs, bool gather,
                              const StreamArgs &a);
 uint32_t stream_tiles_per_stripe(uint64_t chunk_bytes, int vecs);
-// Descriptor kernel; same work-queue accounting as launch_xor_stream.
+// Descriptor batch: desc_tiles (one wave per stripe writes its tile records
+// into b.tiles), then the fold; same work-queue accounting as
+// launch_xor_stream.
+hipError_t launch_desc_tiles(hipStream_t st, const DescBatch &b);
 hipError_t launch_xor_desc(hipStream_t st, int grid, int vecs,
                            const DescBatch &b);
 hipError_t launch_fill_synthetic(hipStream_t st, int grid, char *dst,

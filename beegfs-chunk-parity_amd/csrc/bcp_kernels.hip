@@ -192,13 +192,20 @@ __global__ __launch_bounds__(kBlock) void xor_stream(StreamArgs a) {
 typedef glob<const unsigned char> gbyte;
 __device__ __forceinline__ v4u ld16(gbyte *p) { return __builtin_nontemporal_load((const glob<v4u_u> *)p); }
 
+// The one vector of a source that straddles its end: n (1..15) readable bytes
+// at p, zeros after.  Static byte indices keep w[] in registers.
+__device__ __forceinline__ v4u load_straddle(gbyte *p, uint32_t n) {
+  unsigned int w[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+  for (uint32_t i = 0; i < 16; i++)
+    if (i < n) w[i >> 2] |= (unsigned int)p[i] << (8 * (i & 3));
+  return v4u{w[0], w[1], w[2], w[3]};
+}
+
 __device__ __forceinline__ v4u load_src_tail(gbyte *p, uint64_t len, uint64_t off) {
   if (off + 16 <= len) return ld16(p + off);
   if (off >= len) return zero4();
-  unsigned int w[4] = {0u, 0u, 0u, 0u};
-  const uint32_t n = (uint32_t)(len - off);
-  for (uint32_t i = 0; i < n; i++) w[i >> 2] |= (unsigned int)p[off + i] << (8 * (i & 3));
-  return v4u{w[0], w[1], w[2], w[3]};
+  return load_straddle(p + off, (uint32_t)(len - off));
 }
 
 // Offset inside a source after the reference's window replay (quirk A3-q1):
@@ -214,150 +221,129 @@ __device__ __forceinline__ uint64_t replay_offset(uint64_t j, uint64_t len, uint
 
 __device__ __forceinline__ void store_tail(glob<unsigned char> *d, uint64_t out_len, uint64_t off, v4u v) {
   if (off + 16 <= out_len) {
-    *(glob<v4u_u> *)(d + off) = v;
+    __builtin_nontemporal_store(v, (glob<v4u_u> *)(d + off));
     return;
   }
   if (off >= out_len) return;
   const uint32_t n = (uint32_t)(out_len - off);
-  for (uint32_t i = 0; i < n; i++) d[off + i] = (unsigned char)(v[i >> 2] >> (8 * (i & 3)));
+#pragma unroll
+  for (uint32_t i = 0; i < 16; i++)
+    if (i < n) d[off + i] = (unsigned char)(v[i >> 2] >> (8 * (i & 3)));
 }
 
 // ---------------------------------------------------------------------------
 // Descriptor kernel.  Tiles of tile_bytes output bytes are numbered across the
 // batch (tile_start prefix) and handed out by the same work queue as
 // xor_stream (kSchedQueue) or as a contiguous range per workgroup
-// (kSchedStatic).  Tiles arrive in ascending order per workgroup, so the
-// stripe of a tile is found by a galloping search forward from the previous
-// one (scalar loads of tile_start, L2-resident).  Lanes are wave-contiguous as
-// in xor_stream.  Per tile and per source the coverage test is uniform: a
-// source either covers the whole tile (unconditional 16-B loads, eight or four
-// sources in flight together), misses it (skipped: zero padding), or ends
-// inside it (per-lane tail path).  Window-replay stripes take the per-lane
-// path for every source.
+// (kSchedStatic).  A small setup kernel (desc_tiles) first writes one 16-byte
+// record per tile (stripe, tile index, coverage counts, source run), so a
+// tile costs one scalar load before its stripe and source loads, instead of a
+// search over tile_start.  Lanes are wave-contiguous as in xor_stream.  Per
+// tile and per source the coverage test is uniform: a source either covers
+// the whole tile, misses it (skipped: zero padding), or ends inside it
+// (per-lane tail path).  The staged source runs are sorted longest first, so
+// the covering sources are a prefix of the run and are folded by one fully
+// unrolled fold_cover<G> (G = how many cover, up to 8 at a time).
+// Window-replay stripes take the per-lane path for every source.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t find_stripe(const uint32_t *tsg, uint32_t nstripes, uint32_t s, uint32_t t) {
-  const_as<uint32_t> *ts = cst(tsg);
-  // Precondition: ts[s] <= t < ts[nstripes].  Returns the s' >= s with ts[s'] <= t < ts[s'+1].
-  if (ts[s + 1] > t) return s;
-  uint32_t lo = s + 1, step = 1;  // ts[lo] <= t
-  while (lo + step < nstripes && ts[lo + step] <= t) {
-    lo += step;
-    step <<= 1;
+// G sources that all cover the tile: every load first, then the XOR tree
+// (the xor_stream pattern).  One base address per source and immediate
+// offsets per vector: a 64-bit address per load would cost 2 VGPRs each.
+template <int G, int U, typename P>
+__device__ __forceinline__ void fold_cover(v4u (&acc)[U], P src, uint32_t lane_off) {
+  v4u x[G][U];
+#pragma unroll
+  for (int i = 0; i < G; i++) {
+    const glob<v4u_u> *p = gp<const v4u_u>(src[i] + lane_off);
+#pragma unroll
+    for (int u = 0; u < U; u++) x[i][u] = __builtin_nontemporal_load(p + u * 64);
   }
-  uint32_t hi = lo + step < nstripes ? lo + step : nstripes;  // ts[hi] > t
-  while (hi - lo > 1) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if (ts[mid] <= t) lo = mid; else hi = mid;
+#pragma unroll
+  for (int u = 0; u < U; u++)
+#pragma unroll
+    for (int i = 0; i < G; i++) acc[u] ^= x[i][u];
+}
+
+// General tile: window replay (quirk A3-q1; only when max_cs exceeds the
+// transfer window) or more than kTileSrcs sources reaching in.  Each output
+// vector on its own through the stripe/source tables; rare, so compact.
+template <int U>
+__device__ __noinline__ void desc_tile_general(const DescBatch &b, uint32_t stripe, uint32_t tile,
+                                               uint32_t first_src) {
+  const_as<bcp_stripe> *dp_ = cst(b.stripes) + stripe;
+  const_as<bcp_source> *srcs = cst(b.sources) + first_src;
+  const uint32_t nsrc = dp_->nsrc;
+  const uint64_t out_len = dp_->out_len, window = dp_->window;
+  glob<unsigned char> *dp = gp<unsigned char>(dp_->dst);
+  const uint64_t lane_off = (uint64_t)tile * b.tile_bytes +
+                            (uint64_t)((threadIdx.x >> 6) * (64u * U) + (threadIdx.x & 63u)) * 16u;
+#pragma unroll 1
+  for (int u = 0; u < U; u++) {
+    const uint64_t off = lane_off + (uint64_t)u * 1024u;
+    if (off >= out_len) break;
+    v4u x = zero4();
+    for (uint32_t k = 0; k < nsrc; k++) {
+      const uint64_t len = srcs[k].len;
+      const uint64_t o = window ? replay_offset(off, len, window) : off;
+      x ^= load_src_tail(gp<const unsigned char>(srcs[k].ptr), len, o);
+    }
+    store_tail(dp, out_len, off, x);
   }
-  return lo;
 }
 
 template <int U>
-__device__ __forceinline__ void desc_tile(const DescBatch &b, uint32_t s, uint32_t t) {
-  const uint64_t tile_bytes = b.tile_bytes;
-  const_as<bcp_stripe> *dp_ = cst(b.stripes) + s;
-  const bcp_stripe d = {dp_->dst, dp_->out_len, dp_->first_src, dp_->nsrc, dp_->window};
-  const uint64_t tile_off = (uint64_t)(t - cst(b.tile_start)[s]) * tile_bytes;
-  const uint64_t tile_end = tile_off + tile_bytes;
-  uint64_t j[U];
-#pragma unroll
-  for (int u = 0; u < U; u++)
-    j[u] = tile_off + ((uint64_t)(threadIdx.x >> 6) * (64u * U) + (uint64_t)u * 64u + (threadIdx.x & 63u)) * 16u;
+__device__ __forceinline__ void desc_tile(const DescBatch &b, uint32_t t) {
+  const_as<DescTile> *r = cst(b.tiles) + t;
+  const uint32_t meta = r->meta;
+  if (meta & kTileGeneral) {
+    desc_tile_general<U>(b, r->src_bytes[0], r->src_bytes[1], r->src_bytes[2]);
+    return;
+  }
+  // this lane's vector u = 0 inside the tile; vector u is at + u * 1024
+  const uint32_t lane_off = ((threadIdx.x >> 6) * (64u * U) + (threadIdx.x & 63u)) * 16u;
+  const uint32_t nfull = meta & 0xFFu, nany = (meta >> 8) & 0xFFu;
   v4u acc[U];
 #pragma unroll
   for (int u = 0; u < U; u++) acc[u] = zero4();
-  const_as<bcp_source> *srcs = cst(b.sources) + d.first_src;
-  uint32_t k = 0;
-  if (d.window == 0) {
-    // Groups of eight sources that all cover the tile: 8*U loads in flight.
-    for (; k + 8 <= d.nsrc; k += 8) {
-      bool all = true;
-#pragma unroll
-      for (int i = 0; i < 8; i++) all = all && srcs[k + i].len >= tile_end;
-      if (!all) break;
-      // Sequential XOR chain: the compiler hoists the independent loads as far
-      // ahead as registers allow (as in xor_stream) instead of holding 8*U.
-#pragma unroll
-      for (int i = 0; i < 8; i++) {
-        gbyte *p = gp<const unsigned char>(srcs[k + i].ptr);
-#pragma unroll
-        for (int u = 0; u < U; u++) acc[u] ^= ld16(p + j[u]);
-      }
-    }
-    // Groups of four.
-    for (; k + 4 <= d.nsrc; k += 4) {
-      const bcp_source s0 = {srcs[k].ptr, srcs[k].len}, s1 = {srcs[k + 1].ptr, srcs[k + 1].len};
-      const bcp_source s2 = {srcs[k + 2].ptr, srcs[k + 2].len}, s3 = {srcs[k + 3].ptr, srcs[k + 3].len};
-      if (s0.len >= tile_end && s1.len >= tile_end && s2.len >= tile_end && s3.len >= tile_end) {
-        gbyte *p0 = gp<const unsigned char>(s0.ptr), *p1 = gp<const unsigned char>(s1.ptr);
-        gbyte *p2 = gp<const unsigned char>(s2.ptr), *p3 = gp<const unsigned char>(s3.ptr);
-#pragma unroll
-        for (int u = 0; u < U; u++) acc[u] ^= ld16(p0 + j[u]);
-#pragma unroll
-        for (int u = 0; u < U; u++) acc[u] ^= ld16(p1 + j[u]);
-#pragma unroll
-        for (int u = 0; u < U; u++) acc[u] ^= ld16(p2 + j[u]);
-#pragma unroll
-        for (int u = 0; u < U; u++) acc[u] ^= ld16(p3 + j[u]);
-      } else {
-        const bcp_source ss[4] = {s0, s1, s2, s3};
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-          if (ss[i].len <= tile_off) continue;  // zero padding
-          gbyte *p = gp<const unsigned char>(ss[i].ptr);
-#pragma unroll
-          for (int u = 0; u < U; u++) acc[u] ^= load_src_tail(p, ss[i].len, j[u]);
-        }
-      }
-    }
-    for (; k < d.nsrc; k++) {
-      const bcp_source sk = {srcs[k].ptr, srcs[k].len};
-      if (sk.len <= tile_off) continue;
-      gbyte *p = gp<const unsigned char>(sk.ptr);
-      if (sk.len >= tile_end) {
-#pragma unroll
-        for (int u = 0; u < U; u++) acc[u] ^= ld16(p + j[u]);
-      } else {
-#pragma unroll
-        for (int u = 0; u < U; u++) acc[u] ^= load_src_tail(p, sk.len, j[u]);
-      }
-    }
-  } else {
-    for (; k < d.nsrc; k++) {
-      const bcp_source sk = {srcs[k].ptr, srcs[k].len};
-      gbyte *p = gp<const unsigned char>(sk.ptr);
-#pragma unroll
-      for (int u = 0; u < U; u++) {
-        if (j[u] < d.out_len)
-          acc[u] ^= load_src_tail(p, sk.len, replay_offset(j[u], sk.len, d.window));
-      }
-    }
+  switch (nfull) {
+    case 8: fold_cover<8, U>(acc, r->src, lane_off); break;
+    case 7: fold_cover<7, U>(acc, r->src, lane_off); break;
+    case 6: fold_cover<6, U>(acc, r->src, lane_off); break;
+    case 5: fold_cover<5, U>(acc, r->src, lane_off); break;
+    case 4: fold_cover<4, U>(acc, r->src, lane_off); break;
+    case 3: fold_cover<3, U>(acc, r->src, lane_off); break;
+    case 2: fold_cover<2, U>(acc, r->src, lane_off); break;
+    case 1: fold_cover<1, U>(acc, r->src, lane_off); break;
+    default: break;
   }
-  glob<unsigned char> *dp = gp<unsigned char>(d.dst);
-  if (tile_end <= d.out_len) {
+  for (uint32_t k = nfull; k < nany; k++) {
+    gbyte *p = gp<const unsigned char>(r->src[k]);
+    const uint32_t len = r->src_bytes[k];
 #pragma unroll
-    for (int u = 0; u < U; u++) __builtin_nontemporal_store(acc[u], (glob<v4u_u> *)(dp + j[u]));
+    for (int u = 0; u < U; u++) acc[u] ^= load_src_tail(p, len, lane_off + u * 1024u);
+  }
+  glob<unsigned char> *dp = gp<unsigned char>(r->dst);
+  const uint32_t out_bytes = r->out_bytes;
+  if (out_bytes == b.tile_bytes) {
+    glob<v4u_u> *q = (glob<v4u_u> *)(dp + lane_off);
+#pragma unroll
+    for (int u = 0; u < U; u++) __builtin_nontemporal_store(acc[u], q + u * 64);
   } else {
 #pragma unroll
-    for (int u = 0; u < U; u++) store_tail(dp, d.out_len, j[u], acc[u]);
+    for (int u = 0; u < U; u++) store_tail(dp, out_bytes, lane_off + u * 1024u, acc[u]);
   }
 }
 
 template <int U>
 __global__ __launch_bounds__(kBlock) void xor_desc(DescBatch b) {
-  uint32_t s = 0;
   if (b.sched == kSchedStatic) {
     const uint32_t g = gridDim.x;
     const uint32_t t_begin = (uint32_t)(((uint64_t)blockIdx.x * b.ntiles) / g);
     const uint32_t t_end = (uint32_t)(((uint64_t)(blockIdx.x + 1) * b.ntiles) / g);
-    for (uint32_t t = t_begin; t < t_end; t++) {
-      s = find_stripe(b.tile_start, b.nstripes, s, t);
-      desc_tile<U>(b, s, t);
-    }
+    for (uint32_t t = t_begin; t < t_end; t++) desc_tile<U>(b, t);
     return;
   }
-  // Work queue in grabs of b.grab consecutive tiles (mixed-size tiles read
-  // fewer bytes, so one atomic per tile would saturate the counter).
+  // Work queue in grabs of b.grab consecutive tiles.
   __shared__ uint32_t next[2];
   if (threadIdx.x == 0) next[0] = queue_grab(b.ctr, b.base);
   __syncthreads();
@@ -367,14 +353,57 @@ __global__ __launch_bounds__(kBlock) void xor_desc(DescBatch b) {
   while (c < nchunks) {
     const uint32_t t0 = c * b.grab;
     const uint32_t t1 = min(t0 + b.grab, b.ntiles);
-    for (uint32_t t = t0; t < t1; t++) {
-      s = find_stripe(b.tile_start, b.nstripes, s, t);
-      desc_tile<U>(b, s, t);
-    }
+    for (uint32_t t = t0; t < t1; t++) desc_tile<U>(b, t);
     slot ^= 1;
     if (threadIdx.x == 0) next[slot] = queue_grab(b.ctr, b.base);
     __syncthreads();
     c = __builtin_amdgcn_readfirstlane(next[slot]);
+  }
+}
+
+// Tile records of a descriptor batch: one wave per stripe, lanes over its
+// tiles.  The stripe's staged run is sorted longest first, so the sources
+// reaching into a tile (len > tile offset) are a prefix of it.
+__global__ __launch_bounds__(kBlock) void desc_tiles(DescBatch b) {
+  const uint32_t s = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+  if (s >= b.nstripes) return;
+  const uint32_t lane = threadIdx.x & 63u;
+  const bcp_stripe d = b.stripes[s];
+  const uint32_t t0 = b.tile_start[s], nt = b.tile_start[s + 1] - t0;
+  const bcp_source *run = b.sources + d.first_src;
+  for (uint32_t i = lane; i < nt; i += 64) {
+    const uint64_t off = (uint64_t)i * b.tile_bytes, end = off + b.tile_bytes;
+    DescTile rec;
+    rec.dst = d.dst + off;
+    rec.out_bytes = (uint32_t)(d.out_len - off < b.tile_bytes ? d.out_len - off : b.tile_bytes);
+    uint32_t nfull = 0, nany = 0;
+    if (d.window == 0) {
+      for (uint32_t k = 0; k < d.nsrc; k++) {
+        const uint64_t len = run[k].len;
+        nfull += len >= end;
+        nany += len > off;
+      }
+    }
+    if (d.window != 0 || nany > (uint32_t)kTileSrcs) {
+      rec.meta = kTileGeneral;
+      rec.src_bytes[0] = s;
+      rec.src_bytes[1] = i;
+      rec.src_bytes[2] = d.first_src;
+#pragma unroll
+      for (int k = 3; k < kTileSrcs; k++) rec.src_bytes[k] = 0;
+#pragma unroll
+      for (int k = 0; k < kTileSrcs; k++) rec.src[k] = 0;
+    } else {
+      rec.meta = nfull | nany << 8;
+#pragma unroll
+      for (int k = 0; k < kTileSrcs; k++) {
+        const bool in = (uint32_t)k < nany;
+        const uint64_t len = in ? run[k].len : 0;
+        rec.src[k] = in ? run[k].ptr + off : 0;
+        rec.src_bytes[k] = in ? (uint32_t)(len - off < b.tile_bytes ? len - off : b.tile_bytes) : 0;
+      }
+    }
+    b.tiles[t0 + i] = rec;
   }
 }
 
@@ -529,6 +558,13 @@ hipError_t launch_xor_stream(hipStream_t st, int grid, int vecs, bool gather, co
     case 8: return launch_stream_u<8, 0>(st, grid, a);
     default: return launch_stream_u<2, 0>(st, grid, a);
   }
+}
+
+hipError_t launch_desc_tiles(hipStream_t st, const DescBatch &b) {
+  if (b.nstripes == 0) return hipSuccess;
+  const uint32_t waves = kBlock / 64;  // one wave per stripe
+  hipLaunchKernelGGL(desc_tiles, dim3((b.nstripes + waves - 1) / waves), dim3(kBlock), 0, st, b);
+  return hipGetLastError();
 }
 
 hipError_t launch_xor_desc(hipStream_t st, int grid, int vecs, const DescBatch &b) {

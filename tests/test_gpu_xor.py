@@ -177,7 +177,7 @@ def test_tuning_variants_agree(oracle, engine, dev, queue, bpc, vecs, sched):
         engine.tune(0, 0)
         engine.option("schedule", 0)
         engine.option("desc_schedule", 0)
-        engine.option("desc_blocks_per_cu", 2)
+        engine.option("desc_blocks_per_cu", 0)
         engine.option("desc_vecs_per_thread", 8)
     ref = np.bitwise_xor.reduce(data.reshape(nstripes, nsrc, chunk), axis=1).reshape(-1)
     assert np.array_equal(out, ref)
@@ -196,6 +196,7 @@ def test_work_queue_back_to_back_and_two_queues(oracle, engine, dev, queue):
             n, chunk, ns = int(rng.integers(1, 10)), 16 * int(rng.integers(1, 40000)), int(rng.integers(1, 6))
             data = rng.integers(0, 256, size=ns * n * chunk, dtype=np.uint8)
             src, dst = dev.put(data), dev.alloc(ns * chunk)
+            queue.sync()  # the upload ran on `queue`; q2's kernel must see it
             q = queue if i % 3 else q2
             if i == 10:
                 engine.option("schedule", 1)
