@@ -571,12 +571,17 @@ static int submit_desc(bcp_queue *q, const bcp_stripe *stripes, uint32_t nstripe
     }
     next_src += stripes[i].nsrc;
   }
+  // tiles per stripe (sub_class / tile_starts; desc_tiles repeats the cut)
   uint32_t *ts = (uint32_t *)(h + off_tiles);
-  uint32_t acc = 0;
+  uint64_t acc64 = 0;
   for (uint32_t i = 0; i < nstripes; i++) {
-    ts[i] = acc;
-    acc += (uint32_t)((stripes[i].out_len + tile_bytes - 1) / tile_bytes);
+    ts[i] = (uint32_t)acc64;
+    const bcp_stripe &st = hs[i];
+    const bcp_source *run = hso + st.first_src;
+    acc64 += count_tiles([run](uint32_t k) { return run[k].len; }, st.nsrc, st.out_len, tile_bytes, st.window != 0);
+    if (acc64 > 0xFFFFFFF0ull) return -EINVAL;
   }
+  const uint32_t acc = (uint32_t)acc64;
   ts[nstripes] = acc;
   if (q->tiles_cap < acc) {
     // launches on q are in order; the old records may still be in use

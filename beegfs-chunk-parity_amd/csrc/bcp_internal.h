@@ -58,21 +58,100 @@ struct StreamArgs {
 // record is self-contained so that the fold needs ONE dependent scalar load
 // per tile before its data loads (in r01 every extra dependent round trip
 // in the per-tile chain cost 5-15 % of HBM rate at 1-2 workgroups per CU).
-// Plain tiles list the sources reaching into the tile, sorted longest first:
-// [0, nfull) cover it, [nfull, nany) end inside it (src_bytes readable
-// bytes); zero padding is not listed.  General tiles (window replay, or more
-// than kTileSrcs sources reaching in) take the table path: stripe / tile /
-// first_src in src_bytes[0..2].
+// Plain tiles are one subtile of tile_bytes and list the sources reaching
+// into it, sorted longest first: [0, nfull) cover it, [nfull, nany) end
+// inside it (src_bytes readable bytes); zero padding is not listed.  Grouped
+// tiles are m > 1 consecutive full subtiles covered by the same nfull <= 4
+// sources and no others (nfull * m <= 8 rows, so a grouped tile moves about
+// as many bytes as an 8-source one -- group_rows: on config-5 shapes a
+// third of the subtiles are covered by a single source).  General tiles (window replay, or
+// more than kTileSrcs sources reaching in) take the table path: stripe /
+// subtile / first_src in src_bytes[0..2].
 constexpr int kTileSrcs = 8;
 struct alignas(64) DescTile {
-    uint64_t dst;                   // output address of this tile (stripe dst + tile offset)
-    uint32_t out_bytes;             // output bytes in this tile (< tile_bytes on a stripe's last tile)
-    uint32_t meta;                  // nfull | nany << 8 | kTileGeneral
-    uint64_t src[kTileSrcs];        // source address + tile offset
-    uint32_t src_bytes[kTileSrcs];  // readable bytes from src[k]
+    uint64_t dst;                   // output address of this tile's first subtile
+    uint32_t out_bytes;             // output bytes of the tile
+    uint32_t meta;                  // nfull | nany << 8 | (m - 1) << 16 | kTileGeneral
+    uint64_t src[kTileSrcs];        // source address + offset of the tile's first subtile
+    uint32_t src_bytes[kTileSrcs];  // readable bytes from src[k] (plain tiles)
 };
 constexpr uint32_t kTileGeneral = 0x80000000u;
 static_assert(sizeof(DescTile) == 128, "tile record is two s_load_dwordx16");
+
+// Rows (source x subtile pairs) of a grouped tile for U vectors per lane:
+// every load of the tile is in flight at once, so C*M*U <= 32 keeps the
+// fold within the register budget of the 8-source plain fold.
+__host__ __device__ constexpr int group_rows(int U) { return U >= 8 ? 4 : 8; }
+
+// How one stripe is cut into tiles.  Shared by the host (tile counts per
+// stripe) and desc_tiles (records, one lane per subtile), so both cut
+// identically.  A subtile i is groupable when the same nf sources cover it
+// completely, nobody else reaches into it, its output is full and 2*nf <=
+// group_rows.  A tile starts at every non-groupable subtile and, inside a run
+// of groupable subtiles with the same nf, at the run start and at every
+// subtile index that is a multiple of group_rows / nf (local rule: a lane
+// decides from subtiles i-1 and i alone).
+struct SubClass {
+    uint32_t nf, na;  // sources covering the subtile / reaching into it
+    bool g;           // groupable
+};
+
+// len_at(k): length of source k of the stripe's run, sorted longest first.
+template <typename LenAt>
+__host__ __device__ inline SubClass sub_class(LenAt len_at, uint32_t nsrc, uint64_t out_len, uint64_t sub_bytes,
+                                              uint64_t i) {
+    const uint64_t off = i * sub_bytes, end = off + sub_bytes;
+    uint32_t nf = 0, na = 0;
+    for (uint32_t k = 0; k < nsrc; k++) {
+        const uint64_t len = len_at(k);
+        nf += len >= end;
+        na += len > off;
+    }
+    const uint32_t rows = (uint32_t)group_rows((int)(sub_bytes / 4096u));
+    return SubClass{nf, na, nf == na && nf >= 1 && 2 * nf <= rows && end <= out_len};
+}
+
+__host__ __device__ inline bool tile_starts(const SubClass &prev, const SubClass &cur, uint64_t i, uint64_t sub_bytes) {
+    if (!cur.g || i == 0 || !prev.g || prev.nf != cur.nf) return true;
+    const uint32_t mmax = (uint32_t)group_rows((int)(sub_bytes / 4096u)) / cur.nf;
+    return i % mmax == 0;
+}
+
+// Tiles of one stripe, by the rule above, in O(nsrc): between breakpoints
+// (a source stops covering, a source stops reaching in, the output turns
+// partial) every subtile has the same class.  Equal to counting tile_starts
+// over every subtile (tests/native/tile_cut_test.cpp checks both).
+template <typename LenAt>
+__host__ __device__ inline uint64_t count_tiles(LenAt len_at, uint32_t nsrc, uint64_t out_len, uint64_t sub_bytes,
+                                                bool window) {
+    const uint64_t nsub = (out_len + sub_bytes - 1) / sub_bytes;
+    if (window) return nsub;
+    const uint32_t rows = (uint32_t)group_rows((int)(sub_bytes / 4096u));
+    uint32_t nf = nsrc, na = nsrc;
+    SubClass prev{0, 0, false};
+    uint64_t count = 0, j = 0;
+    while (j < nsub) {
+        const uint64_t off = j * sub_bytes, end = off + sub_bytes;
+        while (na > 0 && len_at(na - 1) <= off) na--;
+        while (nf > 0 && len_at(nf - 1) < end) nf--;
+        const SubClass cur{nf, na, nf == na && nf >= 1 && 2 * nf <= rows && end <= out_len};
+        uint64_t jn = nsub;
+        if (nf > 0 && len_at(nf - 1) / sub_bytes < jn) jn = len_at(nf - 1) / sub_bytes;
+        if (na > 0 && (len_at(na - 1) + sub_bytes - 1) / sub_bytes < jn) jn = (len_at(na - 1) + sub_bytes - 1) / sub_bytes;
+        if (end <= out_len && out_len / sub_bytes < jn) jn = out_len / sub_bytes;
+        if (jn <= j) jn = j + 1;  // cannot happen (see the breakpoints); keeps progress
+        if (!cur.g) {
+            count += jn - j;
+        } else {
+            const uint64_t mmax = rows / cur.nf;
+            count += tile_starts(prev, cur, j, sub_bytes);
+            if (jn - 1 >= j + 1) count += (jn - 1) / mmax - j / mmax;  // multiples of mmax in [j+1, jn-1]
+        }
+        prev = cur;
+        j = jn;
+    }
+    return count;
+}
 
 // Device-side form of one stripe descriptor batch.
 struct DescBatch {

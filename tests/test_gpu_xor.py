@@ -252,6 +252,34 @@ def test_descriptor_mixed_lengths_and_alignment(oracle, dev, queue, seed):
         assert np.array_equal(o, r)
 
 
+@pytest.mark.parametrize("vecs", [8, 4, 2, 1])
+def test_descriptor_grouped_tiles(oracle, engine, dev, queue, vecs):
+    """Staircase lengths whose covering sets hold for many consecutive
+    subtiles: every grouped-tile shape (1 source x 2..8 subtiles, 2 x 2..4,
+    3 x 2, 4 x 2), their boundaries with plain and partial tiles, the last
+    partial output tile, misaligned sources and outputs."""
+    T = 256 * vecs * 16
+    rng = np.random.default_rng(900 + vecs)
+    stripes, refs = [], []
+    shapes = [[9 * T], [9 * T, 1 * T], [5 * T, 4 * T + 3], [6 * T, 6 * T, 2 * T + 17],
+              [3 * T, 3 * T, 3 * T, 1 * T], [4 * T, 4 * T, 4 * T, 4 * T, 1 * T + 5],
+              [17 * T + 9, 12 * T, 7 * T, 3 * T, T // 2, 0], [2 * T, 2 * T, 2 * T, 2 * T, 2 * T]]
+    for lens in shapes:
+        for jitter in (0, 1):
+            ls = [L + (int(rng.integers(0, 40)) if jitter and L else 0) for L in lens]
+            chunks = [rng.integers(0, 256, size=L, dtype=np.uint8) for L in ls]
+            pads = [int(x) for x in rng.integers(0, 16, size=len(ls))] if jitter else None
+            stripes.append(dict(chunks=chunks, out_len=max(ls), pads=pads, dst_pad=3 * jitter))
+            refs.append(oracle.xor_padded_np(chunks))
+    engine.option("desc_vecs_per_thread", vecs)
+    try:
+        outs = gpu_stripes(dev, queue, stripes)
+    finally:
+        engine.option("desc_vecs_per_thread", 8)
+    for i, (o, r) in enumerate(zip(outs, refs)):
+        assert np.array_equal(o, r), i
+
+
 def test_golden_gen_files_on_gpu(oracle, dev, queue):
     for fx in GOLD["edge"]:
         if fx["kind"] != "gen_file":

@@ -31,6 +31,7 @@ KiB, MiB = 1024, 1024 ** 2
 ap = argparse.ArgumentParser()
 ap.add_argument("--reps", type=int, default=5)
 ap.add_argument("--tunings", default="8:2,8:1,8:3,4:2")
+ap.add_argument("--workloads", default="uniform_forced,uniform_desc,mixed,mixed_equal,mixed_big")
 a = ap.parse_args()
 
 eng = bcp.Engine(0)
@@ -83,7 +84,7 @@ def out_bytes(lens_all):
 
 
 L = bcp.lib()
-for kind in ["uniform_forced", "uniform_desc", "mixed", "mixed_equal", "mixed_big"]:
+for kind in a.workloads.split(","):
     eng.option("desc_force", 1 if kind == "uniform_forced" else 0)
     lens_all = shapes(kind, np.random.default_rng(3))
     out = eng.alloc(out_bytes(lens_all))
@@ -95,14 +96,16 @@ for kind in ["uniform_forced", "uniform_desc", "mixed", "mixed_equal", "mixed_bi
         for _ in range(2):
             bcp.check("x", L.bcp_xor_stripes_async(q.h, st, len(st), so, len(so)))
         q.sync()
-        ts = []
+        # steady state as bench.py runs it: launches back to back, the host
+        # stages launch k+1 while the device runs launch k (one launch is
+        # queued ahead of the first mark so the device is busy from the start)
+        bcp.check("x", L.bcp_xor_stripes_async(q.h, st, len(st), so, len(so)))
+        q.mark(0)
         for _ in range(a.reps):
-            q.mark(0)
             bcp.check("x", L.bcp_xor_stripes_async(q.h, st, len(st), so, len(so)))
-            q.mark(1)
-            q.sync()
-            ts.append(q.elapsed_ms(0, 1))
-        ms = sorted(ts)[len(ts) // 2]
+        q.mark(1)
+        q.sync()
+        ms = q.elapsed_ms(0, 1) / a.reps
         tiles = sum((int(ls.max()) + 4096 * u - 1) // (4096 * u) for ls in lens_all)
         print(json.dumps({"workload": kind, "vecs": u, "blocks_per_cu": bpc, "stripes": len(st),
                           "subtiles": tiles, "bytes_per_subtile": round(nbytes / tiles), "kernel_ms": round(ms, 4),
