@@ -15,7 +15,10 @@
  * Copies: blocking sends are rendezvous -- the receiver copies straight from
  * the sender's buffer (one memcpy, outside the lock) and then releases the
  * sender; non-blocking sends are eager (copied at post time; the protocol only
- * uses them for the 8-byte max_cs broadcast).
+ * uses them for the 8-byte max_cs broadcast).  Fill sends (bcp_lb_send_fill)
+ * copy nothing: once matched, the receiver's buffer is handed to the sending
+ * thread, whose callback writes the payload into it (the chunk sender reads
+ * its file straight into the P role's window row).
  */
 #define _GNU_SOURCE
 #include <errno.h>
@@ -25,6 +28,8 @@
 
 #include "bcp_task.h"
 
+struct bcp_lb_req;
+
 typedef struct lb_msg {
     struct lb_msg *next;
     int src, tag;
@@ -32,6 +37,8 @@ typedef struct lb_msg {
     size_t n;
     int eager;           /* payload is owned by this record */
     int done;            /* rendezvous: receiver finished copying */
+    int fill;            /* fill send: payload produced by the sender into `target` */
+    struct bcp_lb_req *target; /* fill send: the matched receive */
     pthread_cond_t cv;   /* rendezvous sender waits here */
 } lb_msg;
 
@@ -206,6 +213,63 @@ int bcp_lb_send(const void *buf, size_t n, int dst, int tag)
     return 0;
 }
 
+/* Run the sender's fill into a matched receive and complete it. */
+static int fill_into(bcp_lb_req *r, bcp_lb_fill_fn fill, void *ctx, size_t n)
+{
+    int frc;
+    if (n <= r->cap) {
+        frc = fill(ctx, r->buf, n);
+        r->received = n;
+        r->status = 0;
+    } else {
+        /* truncated receive (MPI_ERR_TRUNCATE): produce all, keep cap */
+        void *tmp = malloc(n ? n : 1);
+        if (!tmp) {
+            frc = -ENOMEM;
+            r->received = 0;
+        } else {
+            frc = fill(ctx, tmp, n);
+            if (r->cap)
+                memcpy(r->buf, tmp, r->cap);
+            free(tmp);
+            r->received = r->cap;
+        }
+        r->status = -EMSGSIZE;
+    }
+    const int st = frc ? frc : r->status;
+    complete_req(r);
+    return st;
+}
+
+int bcp_lb_send_fill(bcp_lb_fill_fn fill, void *ctx, size_t n, int dst, int tag)
+{
+    int rc = check_peer(dst);
+    if (rc)
+        return rc;
+    if (!fill)
+        return -EINVAL;
+    pthread_mutex_lock(&g_lock);
+    lb_rank *d = &g_ranks[dst];
+    bcp_lb_req *r = take_posted(d, t_rank, tag);
+    if (!r) {
+        lb_msg m = {0};
+        m.src = t_rank;
+        m.tag = tag;
+        m.n = n;
+        m.fill = 1;
+        pthread_cond_init(&m.cv, NULL);
+        push_inbox(d, &m);
+        while (!m.target)
+            pthread_cond_wait(&m.cv, &g_lock);
+        r = m.target;
+        pthread_mutex_unlock(&g_lock);
+        pthread_cond_destroy(&m.cv);
+    } else {
+        pthread_mutex_unlock(&g_lock);
+    }
+    return fill_into(r, fill, ctx, n);
+}
+
 int bcp_lb_isend(const void *buf, size_t n, int dst, int tag, bcp_lb_req **req)
 {
     int rc = check_peer(dst);
@@ -273,7 +337,13 @@ int bcp_lb_irecv(void *buf, size_t n, int src, int tag, bcp_lb_req **req)
     pthread_mutex_lock(&g_lock);
     lb_rank *me = &g_ranks[t_rank];
     lb_msg *m = take_inbox(me, src, tag);
-    if (m) {
+    if (m && m->fill) {
+        /* hand the buffer to the sending thread; it completes r */
+        r->next = NULL;
+        m->target = r;
+        pthread_cond_signal(&m->cv);
+        pthread_mutex_unlock(&g_lock);
+    } else if (m) {
         pthread_mutex_unlock(&g_lock);
         deliver(r, m->buf, m->n);
         r->done = 1;

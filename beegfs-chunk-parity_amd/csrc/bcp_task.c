@@ -527,6 +527,40 @@ static uint8_t *sender_buffer(size_t need)
     return L->send_buf;
 }
 
+/* One window of the source role, produced straight into the receiver's
+ * buffer (bcp_lb_send_fill): the file's next bytes, zero padded after a short
+ * read; zeros after an open or read error or for an empty chunk (A3-q2). */
+typedef struct {
+    int fd;
+    uint64_t fd_size, data_to_send, data_sent;
+    int err;
+    HostState *hs;
+    const char *path;
+} window_fill;
+
+static int fill_window(void *ctx, void *dst, size_t n)
+{
+    window_fill *w = ctx;
+    HostState *hs = w->hs;
+    uint8_t *data = dst;
+    if (w->err != 0 || w->data_sent >= w->fd_size) {
+        memset(data, 0, n);
+        return 0;
+    }
+    const uint64_t left = w->data_to_send - w->data_sent;
+    ssize_t r = read(w->fd, data, (size_t)MIN_((uint64_t)n, left));
+    if (r < 0) {
+        w->err = errno;
+        memset(data, 0, n);
+        LOGERR("reading '%s' caused new error %d (%s) after %llu bytes\n", w->path, errno, strerror(errno),
+               (unsigned long long)w->data_sent);
+        return 0;
+    }
+    if ((size_t)r < n)
+        memset(data + r, 0, n - (size_t)r);
+    return 0;
+}
+
 static void chunk_sender(const char *path, const FileInfo *task, TaskInfo ti, HostState *hs)
 {
     const int my_st = hs->storage_target;
@@ -563,6 +597,20 @@ static void chunk_sender(const char *path, const FileInfo *task, TaskInfo ti, Ho
     bcp_lb_recv(&data_to_send, sizeof(data_to_send), coordinator, ti.tag, NULL);
 
     const size_t buffer_size = (size_t)MIN_(WINDOW, data_to_send);
+    /* Zero copy: every window is read straight into P's window row, unless a
+     * later window could replay this one (A3-q1: the file ends before max_cs
+     * and more than one window is sent), which needs the sender's own buffer. */
+    if (!(fd_size < data_to_send && data_to_send > buffer_size)) {
+        window_fill wf = {fd, fd_size, data_to_send, 0, have_had_error, hs, path};
+        while (wf.data_sent < data_to_send) {
+            if (ti.sample)
+                ti.sample->bytes_read += buffer_size;
+            bcp_lb_send_fill(fill_window, &wf, buffer_size, coordinator, ti.tag);
+            wf.data_sent += buffer_size;
+        }
+        have_had_error = wf.err;
+        goto done;
+    }
     uint8_t *data = sender_buffer(buffer_size);
     if (!data)
         abort();
@@ -592,6 +640,7 @@ static void chunk_sender(const char *path, const FileInfo *task, TaskInfo ti, Ho
         bcp_lb_send(data, buffer_size, coordinator, ti.tag);
     }
 
+done:
     /* ENOENT: the chunk vanished after planning; an unlink event follows. */
     if (hs->error == 0 && have_had_error != 0 && have_had_error != ENOENT) {
         LOGERR("local error on '%s' elevated to global error\n", path);

@@ -137,6 +137,13 @@ int bcp_lb_isend(const void *buf, size_t n, int dst, int tag, bcp_lb_req **req);
 int bcp_lb_irecv(void *buf, size_t n, int src, int tag, bcp_lb_req **req);
 int bcp_lb_wait(bcp_lb_req *req, size_t *received);
 int bcp_lb_waitall(int n, bcp_lb_req **reqs);
+/* Zero-copy blocking send: instead of copying a buffer, the sender's
+ * fill(ctx, dst, n) writes the n-byte payload straight into the matched
+ * receive buffer (e.g. read() from the chunk file), on the sending thread,
+ * once a receiver is matched.  Same matching and ordering as bcp_lb_send;
+ * fill returns 0 or a negative errno, which bcp_lb_send_fill returns. */
+typedef int (*bcp_lb_fill_fn)(void *ctx, void *dst, size_t n);
+int bcp_lb_send_fill(bcp_lb_fill_fn fill, void *ctx, size_t n, int dst, int tag);
 
 /* ---- callers: generation lanes and rebuild (loopback drivers) ---------- */
 typedef struct {

@@ -9,6 +9,7 @@ import shutil
 import subprocess
 import sys
 import tempfile
+import argparse
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -23,6 +24,11 @@ import oracle  # noqa: E402
 from e2e_bench import write_store, total_bytes  # noqa: E402
 
 KiB, GiB = 1024, 1024 ** 3
+ap = argparse.ArgumentParser()
+ap.add_argument("--reps", type=int, default=4)
+ap.add_argument("--lanes", default="12,24")
+ap.add_argument("--folds", default="gpu_zero_copy,cpu_reference,noop")
+a = ap.parse_args()
 tmp = tempfile.mkdtemp(dir="/tmp")  # /dev/shm is noexec
 src = os.path.join(tmp, "noop.c")
 open(src, "w").write("#include <stddef.h>\n#include <stdint.h>\nint noop_fold(uint8_t *d, size_t n, const uint8_t *s,"
@@ -47,7 +53,7 @@ def timed(label, lanes, hook=None):
         bcp.set_xor_hook(hook)
     try:
         ts = []
-        for r in range(4):
+        for r in range(a.reps):
             for p in range(4):
                 shutil.rmtree(os.path.join(root, f"st{p}", "parity"), ignore_errors=True)
                 os.makedirs(os.path.join(root, f"st{p}", "parity"))
@@ -61,9 +67,10 @@ def timed(label, lanes, hook=None):
 
 
 ol = oracle.lib()
-for lanes in (12, 24):
-    timed("gpu_zero_copy", lanes)
-    timed("cpu_reference", lanes, ctypes.cast(ol.oracle_xor_rows, ctypes.c_void_p).value)
-    timed("noop", lanes, ctypes.cast(noop.noop_fold, ctypes.c_void_p).value)
+hooks = {"gpu_zero_copy": None, "cpu_reference": ctypes.cast(ol.oracle_xor_rows, ctypes.c_void_p).value,
+         "noop": ctypes.cast(noop.noop_fold, ctypes.c_void_p).value}
+for lanes in (int(x) for x in a.lanes.split(",")):
+    for f in a.folds.split(","):
+        timed(f, lanes, hooks[f])
 bcp.task_shutdown()
 shutil.rmtree(root, ignore_errors=True)
