@@ -337,13 +337,34 @@ __device__ __forceinline__ void desc_tile(const DescBatch &b, uint32_t t) {
     switch (nfull << 4 | m) {
 #define BCP_GROUP(c, mm) \
   case (c << 4 | mm):                                                 \
-    if constexpr (c * mm <= group_rows(U)) fold_group<c, mm, U>(r, lane_off); \
-    return;
+    if constexpr (c * mm <= group_rows(U)) {                           \
+      fold_group<c, mm, U>(r, lane_off);                               \
+      return;                                                          \
+    }                                                                  \
+    break;
       BCP_GROUP(1, 2) BCP_GROUP(1, 3) BCP_GROUP(1, 4) BCP_GROUP(1, 5) BCP_GROUP(1, 6) BCP_GROUP(1, 7)
       BCP_GROUP(1, 8) BCP_GROUP(2, 2) BCP_GROUP(2, 3) BCP_GROUP(2, 4) BCP_GROUP(3, 2) BCP_GROUP(4, 2)
 #undef BCP_GROUP
-      default: __builtin_trap();  // desc_tiles never writes another shape
+      default: break;
     }
+    // Shapes desc_tiles does not write for this U (C*M > group_rows(U));
+    // correct anyway: one subtile at a time.
+    for (uint32_t j = 0; j < m; j++) {
+      v4u acc[U];
+#pragma unroll
+      for (int u = 0; u < U; u++) acc[u] = zero4();
+      const uint32_t off = lane_off + j * b.tile_bytes;
+      switch (nfull) {
+        case 4: fold_cover<4, U>(acc, r->src, off); break;
+        case 3: fold_cover<3, U>(acc, r->src, off); break;
+        case 2: fold_cover<2, U>(acc, r->src, off); break;
+        default: fold_cover<1, U>(acc, r->src, off); break;
+      }
+      glob<v4u_u> *q = gp<v4u_u>(r->dst + off);
+#pragma unroll
+      for (int u = 0; u < U; u++) __builtin_nontemporal_store(acc[u], q + u * 64);
+    }
+    return;
   }
   v4u acc[U];
 #pragma unroll
