@@ -40,7 +40,8 @@ struct DescSlot {
   void *host = nullptr;   // pinned staging
   void *dev = nullptr;    // device copy
   size_t cap = 0;
-  hipEvent_t done = nullptr;  // recorded after the kernel that read `dev`
+  hipEvent_t done = nullptr;    // recorded after the kernel that read `dev`
+  hipEvent_t copied = nullptr;  // recorded on the copy stream after host -> dev
   bool used = false;
 };
 
@@ -56,6 +57,7 @@ struct bcp_queue {
   hipEvent_t timer[kTimerSlots] = {};
   DescTile *tiles = nullptr;           // tile records of the descriptor kernel (device)
   size_t tiles_cap = 0;                // in records
+  hipStream_t copy_stream = nullptr;   // descriptor-table uploads (created on first use)
 };
 
 struct bcp_event {
@@ -133,7 +135,20 @@ static int ring_acquire(bcp_queue *q, size_t bytes, DescSlot **out) {
     s->cap = cap;
   }
   if (!s->done) HIP_RC(hipEventCreateWithFlags(&s->done, hipEventDisableTiming));
+  if (!s->copied) HIP_RC(hipEventCreateWithFlags(&s->copied, hipEventDisableTiming));
   *out = s;
+  return 0;
+}
+
+// Upload a slot's tables on the queue's copy stream and make the compute
+// stream wait for them: the upload for launch k+1 overlaps kernel k instead
+// of sitting between them in stream order.  (The slot's previous kernel has
+// finished: ring_acquire waited for it.)
+static int stage_tables(bcp_queue *q, DescSlot *slot, size_t bytes) {
+  if (!q->copy_stream) HIP_RC(hipStreamCreateWithFlags(&q->copy_stream, hipStreamNonBlocking));
+  HIP_RC(hipMemcpyAsync(slot->dev, slot->host, bytes, hipMemcpyHostToDevice, q->copy_stream));
+  HIP_RC(hipEventRecord(slot->copied, q->copy_stream));
+  HIP_RC(hipStreamWaitEvent(q->stream, slot->copied, 0));
   return 0;
 }
 
@@ -277,11 +292,14 @@ extern "C" int bcp_queue_destroy(bcp_queue *q) {
   if (!q) return -EINVAL;
   set_device(q->eng);
   (void)hipStreamSynchronize(q->stream);
+  if (q->copy_stream) (void)hipStreamSynchronize(q->copy_stream);
   for (auto &s : q->ring) {
     if (s.host) (void)hipHostFree(s.host);
     if (s.dev) (void)hipFree(s.dev);
     if (s.done) (void)hipEventDestroy(s.done);
+    if (s.copied) (void)hipEventDestroy(s.copied);
   }
+  if (q->copy_stream) (void)hipStreamDestroy(q->copy_stream);
   for (auto &t : q->timer)
     if (t) (void)hipEventDestroy(t);
   if (q->qctr) (void)hipFree(q->qctr);
@@ -523,7 +541,7 @@ static int submit_desc(bcp_queue *q, const bcp_stripe *stripes, uint32_t nstripe
     if (rc) return rc;
     memcpy(slot->host, stripes, (size_t)nstripes * sizeof(bcp_stripe));
     memcpy((char *)slot->host + off_src, sources, (size_t)nsources * sizeof(bcp_source));
-    HIP_RC(hipMemcpyAsync(slot->dev, slot->host, bytes, hipMemcpyHostToDevice, q->stream));
+    if ((rc = stage_tables(q, slot, bytes))) return rc;
     StreamArgs a{};
     a.stripes = (const bcp_stripe *)slot->dev;
     a.sources = (const bcp_source *)((char *)slot->dev + off_src);
@@ -593,7 +611,7 @@ static int submit_desc(bcp_queue *q, const bcp_stripe *stripes, uint32_t nstripe
     HIP_RC(hipMalloc((void **)&q->tiles, cap * sizeof(DescTile)));
     q->tiles_cap = cap;
   }
-  HIP_RC(hipMemcpyAsync(slot->dev, slot->host, bytes, hipMemcpyHostToDevice, q->stream));
+  if ((rc = stage_tables(q, slot, bytes))) return rc;
   DescBatch b;
   char *d = (char *)slot->dev;
   b.stripes = (const bcp_stripe *)d;
