@@ -291,11 +291,9 @@ static int fold_window(fold_res *R, HostState *hs, bcp_xor_hook_fn hook, void *c
                        size_t pitch, size_t nbytes, int n, uint8_t *out)
 {
     if (hook) {
-        static int warned = 0;
-        if (!warned) {
-            warned = 1;
+        static int warned = 0; /* lanes race here: atomic exchange */
+        if (!__atomic_exchange_n(&warned, 1, __ATOMIC_RELAXED))
             LOGERR("XOR test hook active on st %d (no GPU fold)\n", hs->storage_target);
-        }
         return hook(out, nbytes, rows, pitch, n, ctx);
     }
     int rc;
@@ -374,6 +372,20 @@ static void push_corrupt_path(HostState *hs, const char *path)
 
 static int active_ranks(uint64_t locations) { return __builtin_popcountll(locations & L_MASK); }
 
+/* The sticky per-rank error (task_processing.c:232-236,313-317).  The lanes
+ * of a rank share hs; the reference writes hs->error / error_path from them
+ * without a lock (a data race).  Here the first error wins by
+ * compare-and-swap and only the winner sets error_path.  Returns 1 if this
+ * call raised it. */
+static int raise_sticky_error(HostState *hs, int err, const char *path)
+{
+    int expected = 0;
+    if (!__atomic_compare_exchange_n(&hs->error, &expected, err, 0, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE))
+        return 0;
+    hs->error_path = strdup(path);
+    return 1;
+}
+
 /* ---- roles ------------------------------------------------------------- */
 
 static void parity_generator(const char *path, const FileInfo *task, TaskInfo ti, HostState *hs)
@@ -427,7 +439,7 @@ static void parity_generator(const char *path, const FileInfo *task, TaskInfo ti
     pthread_mutex_unlock(&g_lock);
 
     fold_res *L = NULL;
-    int have_had_error = hs->error;
+    int have_had_error = __atomic_load_n(&hs->error, __ATOMIC_ACQUIRE);
     int res_rc = expected_messages ? res_acquire(hs, hook == NULL, pitch * (size_t)n, buffer_size, &L) : 0;
     uint8_t *scratch = NULL; /* receive space if staging could not be set up */
     uint8_t *win_a, *win_b, *pblk;
@@ -503,11 +515,8 @@ static void parity_generator(const char *path, const FileInfo *task, TaskInfo ti
         if (ftruncate(P_fd, (off_t)final_parity_chunk_size) != 0 && !have_had_error)
             have_had_error = errno;
 
-    if (hs->error == 0 && have_had_error != 0) {
+    if (have_had_error != 0 && raise_sticky_error(hs, have_had_error, path))
         LOGERR("local error on '%s' elevated to global error\n", path);
-        hs->error = have_had_error;
-        hs->error_path = strdup(path);
-    }
     free(scratch);
     res_release(L);
     if (P_fd != hs->fd_null)
@@ -642,11 +651,8 @@ static void chunk_sender(const char *path, const FileInfo *task, TaskInfo ti, Ho
 
 done:
     /* ENOENT: the chunk vanished after planning; an unlink event follows. */
-    if (hs->error == 0 && have_had_error != 0 && have_had_error != ENOENT) {
+    if (have_had_error != 0 && have_had_error != ENOENT && raise_sticky_error(hs, have_had_error, path))
         LOGERR("local error on '%s' elevated to global error\n", path);
-        hs->error = have_had_error;
-        hs->error_path = strdup(path);
-    }
     if (fd != hs->fd_zero)
         close(fd);
 }

@@ -1,0 +1,17 @@
+"""ThreadSanitizer run of the host C layer on the CPU (tools/tsan_host.sh):
+parity gen over 6 loopback ranks x 12 lanes and a rebuild (CPU test-double
+fold), plus a run where one rank's parity writes fail from many lanes at
+once (the sticky error is raised once, race-free; the reference writes it
+unlocked).  Fails on any TSan report."""
+import os
+import subprocess
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_protocol_under_threadsanitizer(bcp):
+    r = subprocess.run([os.path.join(ROOT, "tools", "tsan_host.sh")], capture_output=True, text=True, timeout=900)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, out[-4000:]
+    assert "ThreadSanitizer" not in out, out[-4000:]
+    assert "OK: 0 problems" in out
