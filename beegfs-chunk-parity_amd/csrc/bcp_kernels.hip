@@ -51,17 +51,18 @@ __device__ __forceinline__ v4u zero4() { return v4u{0u, 0u, 0u, 0u}; }
 
 // ---------------------------------------------------------------------------
 // Streaming fold (hot path).  A tile is kBlock*U 16-byte vectors of one
-// stripe's output (16 KiB at U = 4); wave w of the workgroup owns the
-// contiguous run [w*64*U, (w+1)*64*U) of the tile, lane l vectors l, l+64, ...
-// so each wave streams 4 KiB contiguous per source and every NSRC*U load of a
-// lane is independent of the others.
+// stripe's output (32 KiB at the default U = 8, one 256-thread workgroup per
+// CU); wave w of the workgroup owns the contiguous run [w*64*U, (w+1)*64*U)
+// of the tile, lane l vectors l, l+64, ... so each wave streams 8 KiB
+// contiguous per source and every NSRC*U load of a lane is independent of the
+// others.
 //
-// Tile schedule (r01 sweeps, profiles/r01/exp*.jsonl): a device-wide work
-// queue.  Thread 0 of a workgroup takes the next tile index with one atomic
-// per tile, so the tiles in flight on the whole chip are always a narrow,
-// ascending address window (~56 stripes at config 2).  In the interleaved r01
-// sweeps that schedule (with wave-contiguous lanes) beat per-workgroup
-// contiguous tile runs by 12-14 % on the same box.
+// Tile schedule (r01 sweeps, profiles/r01/kernel_exp_*.jsonl): a device-wide
+// work queue.  Thread 0 of a workgroup takes the next tile index with one
+// atomic per tile, so the tiles in flight on the whole chip are always a
+// narrow, ascending address window (~16 stripes at config 2).  It beat
+// per-workgroup contiguous tile runs by 12-14 % and a grid-stride schedule by
+// 10 points on the same box (exp 1-3, 9).
 // The counter is monotone: launch k starts at `base`, every tile index
 // handed out is atomicAdd(ctr, 1) - base, and each workgroup makes exactly one
 // failing grab, so a launch consumes ntiles + grid counts and the host
