@@ -6,10 +6,12 @@
 //  * one in-order HIP stream per queue; lanes (gen/main.c:821-845) each own a
 //    queue, so twelve lanes overlap their copies and kernels on the device;
 //  * descriptor batches are staged through a per-queue ring of pinned slots
-//    so submission never synchronises with earlier work of the same queue;
+//    and uploaded on the queue's copy stream (the kernel's stream waits by
+//    event), so submission never synchronises with earlier work of the same
+//    queue and the upload for launch k+1 overlaps kernel k;
 //  * grids are persistent: CUs x blocks_per_cu workgroups of 256 threads;
-//    the streaming kernel takes tiles from a per-queue device work queue
-//    (monotone counter, base advanced on the host per launch).
+//    both kernels take tiles from a per-queue device work queue (monotone
+//    counter, base advanced on the host per launch).
 #include <errno.h>
 #include <stdio.h>
 #include <stdlib.h>

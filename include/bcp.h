@@ -171,13 +171,14 @@ int bcp_queue_elapsed_ms(bcp_queue *q, int slot_from, int slot_to,
 /* Tuning knobs for the fast path (bench / autotune only; 0 = default). */
 int bcp_set_tuning(bcp_engine *eng, int blocks_per_cu, int vecs_per_thread);
 /* Named knob: "blocks_per_cu" (1..32), "vecs_per_thread" (1,2,4,8) of the
- * uniform streaming kernel; "desc_blocks_per_cu" (1..32),
- * "desc_vecs_per_thread" (1,2,4,8) of the descriptor kernel;
- * "schedule" (0 = device-wide tile work queue, the default; 1 = a static
- * contiguous tile range per workgroup, kept for A/B measurements) for the
- * uniform streaming kernel; "desc_schedule" (same values, default 0) and
- * "desc_grab" (tiles per work-queue grab, 1..64, default 1) for the
- * descriptor kernel (mixed sizes, windows, unaligned). */
+ * uniform streaming kernel; "desc_blocks_per_cu" (0 = chosen per batch from
+ * its bytes per tile, the default; 1..32), "desc_vecs_per_thread" (1,2,4,8)
+ * of the descriptor kernel; "schedule" (0 = device-wide tile work queue, the
+ * default; 1 = a static contiguous tile range per workgroup, kept for A/B
+ * measurements) for the uniform streaming kernel; "desc_schedule" (same
+ * values, default 0), "desc_grab" (tiles per work-queue grab, 1..64, default
+ * 1) and "desc_force" (1 = uniform batches take the descriptor kernel too;
+ * A/B only) for the descriptor kernel (mixed sizes, windows, unaligned). */
 int bcp_set_option(bcp_engine *eng, const char *key, int value);
 /* Current value of a named knob (same keys). */
 int bcp_get_option(bcp_engine *eng, const char *key, int *value);
