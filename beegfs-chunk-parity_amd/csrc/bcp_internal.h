@@ -64,9 +64,10 @@ struct StreamArgs {
 // tiles are m > 1 consecutive full subtiles covered by the same nfull <= 4
 // sources and no others (nfull * m <= 8 rows, so a grouped tile moves about
 // as many bytes as an 8-source one -- group_rows: on config-5 shapes a
-// third of the subtiles are covered by a single source).  General tiles (window replay, or
-// more than kTileSrcs sources reaching in) take the table path: stripe /
-// subtile / first_src in src_bytes[0..2].
+// third of the subtiles are covered by a single source).  General tiles take
+// the table path, stripe / subtile / first_src in src_bytes[0..2]: window
+// replay (per-lane path), or more than kTileSrcs sources reaching in
+// (kTileWide, counts in meta: eight-at-a-time folds from the staged run).
 constexpr int kTileSrcs = 8;
 struct alignas(64) DescTile {
     uint64_t dst;                   // output address of this tile's first subtile
@@ -76,6 +77,7 @@ struct alignas(64) DescTile {
     uint32_t src_bytes[kTileSrcs];  // readable bytes from src[k] (plain tiles)
 };
 constexpr uint32_t kTileGeneral = 0x80000000u;
+constexpr uint32_t kTileWide = 0x40000000u;  // with kTileGeneral: > kTileSrcs sources, no window
 static_assert(sizeof(DescTile) == 128, "tile record is two s_load_dwordx16");
 
 // Rows (source x subtile pairs) of a grouped tile for U vectors per lane:

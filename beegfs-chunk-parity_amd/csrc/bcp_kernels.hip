@@ -322,12 +322,68 @@ __device__ __noinline__ void desc_tile_general(const DescBatch &b, uint32_t stri
   }
 }
 
+// Source addresses of a staged run, offset to a tile (fold_cover's src[i]).
+struct RunAt {
+  const_as<bcp_source> *s;
+  uint64_t off;
+  __device__ __forceinline__ uint64_t operator[](int i) const { return s[i].ptr + off; }
+};
+
+// Wide tile: more than kTileSrcs sources reach into it (stripes wider than 8,
+// up to BCP_MAX_SOURCES).  The record cannot list them, so they come from the
+// staged run (sorted longest first: [0, nfull) cover, [nfull, nany) end
+// inside): covering sources eight at a time through fold_cover, then the
+// partial ones, as in the plain path.
+template <int U>
+__device__ __noinline__ void desc_tile_wide(const DescBatch &b, uint32_t stripe, uint32_t sub, uint32_t first_src,
+                                            uint32_t nfull, uint32_t nany) {
+  const_as<bcp_stripe> *dp_ = cst(b.stripes) + stripe;
+  const_as<bcp_source> *srcs = cst(b.sources) + first_src;
+  const uint64_t tile_off = (uint64_t)sub * b.tile_bytes;
+  const uint32_t lane_off = ((threadIdx.x >> 6) * (64u * U) + (threadIdx.x & 63u)) * 16u;
+  v4u acc[U];
+#pragma unroll
+  for (int u = 0; u < U; u++) acc[u] = zero4();
+  uint32_t k = 0;
+  for (; k + 8 <= nfull; k += 8) fold_cover<8, U>(acc, RunAt{srcs + k, tile_off}, lane_off);
+  const RunAt rest{srcs + k, tile_off};
+  switch (nfull - k) {
+    case 7: fold_cover<7, U>(acc, rest, lane_off); break;
+    case 6: fold_cover<6, U>(acc, rest, lane_off); break;
+    case 5: fold_cover<5, U>(acc, rest, lane_off); break;
+    case 4: fold_cover<4, U>(acc, rest, lane_off); break;
+    case 3: fold_cover<3, U>(acc, rest, lane_off); break;
+    case 2: fold_cover<2, U>(acc, rest, lane_off); break;
+    case 1: fold_cover<1, U>(acc, rest, lane_off); break;
+    default: break;
+  }
+  for (k = nfull; k < nany; k++) {
+    gbyte *p = gp<const unsigned char>(srcs[k].ptr + tile_off);
+    const uint64_t len = srcs[k].len - tile_off;  // < tile_bytes: ends inside the tile
+#pragma unroll
+    for (int u = 0; u < U; u++) acc[u] ^= load_src_tail(p, len, lane_off + u * 1024u);
+  }
+  const uint64_t out_len = dp_->out_len;
+  glob<unsigned char> *dp = gp<unsigned char>(dp_->dst + tile_off);
+  if (tile_off + b.tile_bytes <= out_len) {
+    glob<v4u_u> *q = (glob<v4u_u> *)(dp + lane_off);
+#pragma unroll
+    for (int u = 0; u < U; u++) __builtin_nontemporal_store(acc[u], q + u * 64);
+  } else {
+#pragma unroll
+    for (int u = 0; u < U; u++) store_tail(dp, out_len - tile_off, lane_off + u * 1024u, acc[u]);
+  }
+}
+
 template <int U>
 __device__ __forceinline__ void desc_tile(const DescBatch &b, uint32_t t) {
   const_as<DescTile> *r = cst(b.tiles) + t;
   const uint32_t meta = r->meta;
   if (meta & kTileGeneral) {
-    desc_tile_general<U>(b, r->src_bytes[0], r->src_bytes[1], r->src_bytes[2]);
+    if (meta & kTileWide)
+      desc_tile_wide<U>(b, r->src_bytes[0], r->src_bytes[1], r->src_bytes[2], meta & 0xFFu, (meta >> 8) & 0xFFu);
+    else
+      desc_tile_general<U>(b, r->src_bytes[0], r->src_bytes[1], r->src_bytes[2]);
     return;
   }
   // this lane's vector u = 0 inside the tile; vector u is at + u * 1024
@@ -451,7 +507,7 @@ __device__ __forceinline__ void write_tile(const DescBatch &b, uint32_t s, const
   rec.dst = d.dst + off;
   rec.out_bytes = (uint32_t)(d.out_len - off < want ? d.out_len - off : want);
   if (d.window != 0 || nany > (uint32_t)kTileSrcs) {
-    rec.meta = kTileGeneral;
+    rec.meta = d.window != 0 ? kTileGeneral : (kTileGeneral | kTileWide | nfull | nany << 8);
     rec.src_bytes[0] = s;
     rec.src_bytes[1] = (uint32_t)sub0;
     rec.src_bytes[2] = d.first_src;

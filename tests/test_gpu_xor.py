@@ -280,6 +280,33 @@ def test_descriptor_grouped_tiles(oracle, engine, dev, queue, vecs):
         assert np.array_equal(o, r), i
 
 
+@pytest.mark.parametrize("n", [9, 12, 20, 56])
+def test_descriptor_wide_stripes(oracle, dev, queue, n):
+    """Stripes wider than a tile record holds (> 8 sources reaching into a
+    tile, up to MAX_STORAGE_TARGETS - 1 + parity): mixed lengths,
+    misaligned sources and output, zero-length and equal-length sources."""
+    rng = np.random.default_rng(700 + n)
+    stripes, refs = [], []
+    for _ in range(3):
+        lens = [int(x) for x in rng.integers(0, 200_000, size=n)]
+        lens[0] = lens[1] = max(lens)  # ties
+        lens[2] = 0
+        chunks = [rng.integers(0, 256, size=L, dtype=np.uint8) for L in lens]
+        pads = [int(x) for x in rng.integers(0, 16, size=n)]
+        stripes.append(dict(chunks=chunks, out_len=max(lens), pads=pads, dst_pad=int(rng.integers(0, 16))))
+        refs.append(oracle.xor_padded_np(chunks))
+    # uniform lengths too (a 16-multiple out_len with one short source keeps
+    # the batch off the pointer-table fast path)
+    lens = [65536] * n
+    lens[-1] = 65536 - 48
+    chunks = [rng.integers(0, 256, size=L, dtype=np.uint8) for L in lens]
+    stripes.append(dict(chunks=chunks, out_len=65536))
+    refs.append(oracle.xor_padded_np(chunks))
+    outs = gpu_stripes(dev, queue, stripes)
+    for i, (o, r) in enumerate(zip(outs, refs)):
+        assert np.array_equal(o, r), i
+
+
 def test_golden_gen_files_on_gpu(oracle, dev, queue):
     for fx in GOLD["edge"]:
         if fx["kind"] != "gen_file":

@@ -10,6 +10,7 @@
                  the maximum (no zero padding, fewer bytes per tile varies
                  only across stripes)
   mixed_big      like mixed, lengths log-uniform in [1 MiB, 4 MiB]
+  wide16         16-wide stripes with config-5 lengths (> 8 sources per tile)
 
 Each line: workload, tuning, kernel ms (HIP events on the queue), algorithmic
 GB/s and fraction of 8 TB/s.
@@ -50,6 +51,8 @@ def shapes(kind, rng):
             ls = np.full(8, 512 * KiB - 8, dtype=np.int64)
         elif kind == "uniform_forced":
             ls = np.full(8, 512 * KiB, dtype=np.int64)
+        elif kind == "wide16":
+            ls = np.exp(rng.uniform(np.log(64 * KiB), np.log(4 * MiB), size=16)).astype(np.int64)
         elif kind == "mixed_big":
             ls = np.exp(rng.uniform(np.log(1 * MiB), np.log(4 * MiB), size=8)).astype(np.int64)
         else:
