@@ -506,6 +506,41 @@ __device__ __forceinline__ void write_tile(const DescBatch &b, uint32_t s, const
   DescTile rec;
   rec.dst = d.dst + off;
   rec.out_bytes = (uint32_t)(d.out_len - off < want ? d.out_len - off : want);
+  if (d.window != 0 && d.window % T == 0 && m == 1) {
+    // Window replay (A3-q1) on a tile that lies inside one transfer window:
+    // the replay is uniform over the tile, so source k is read from
+    // ptr + mapped offset (its last readable window re-sent for every later
+    // window) -- a plain tile with per-source addresses.  Covering sources
+    // first, then the ones ending inside the tile; more than kTileSrcs
+    // reaching in falls back to the general path.
+    const uint64_t w = off / d.window;
+    uint32_t nf = 0, na = 0;
+    for (int pass = 0; pass < 2; pass++)
+      for (uint32_t k = 0; k < d.nsrc; k++) {
+        const uint64_t len = run[k].len;
+        if (len == 0) continue;
+        const uint64_t lw = (len - 1) / d.window;
+        const uint64_t mo = w > lw ? off - (w - lw) * d.window : off;
+        if (len <= mo) continue;
+        const uint64_t eff = len - mo;
+        if ((pass == 0) != (eff >= T)) continue;
+        if (na < (uint32_t)kTileSrcs) {
+          rec.src[na] = run[k].ptr + mo;
+          rec.src_bytes[na] = (uint32_t)(eff < T ? eff : T);
+        }
+        na++;
+        nf += pass == 0;
+      }
+    if (na <= (uint32_t)kTileSrcs) {
+      for (uint32_t k = na; k < (uint32_t)kTileSrcs; k++) {
+        rec.src[k] = 0;
+        rec.src_bytes[k] = 0;
+      }
+      rec.meta = nf | na << 8;
+      *out = rec;
+      return;
+    }
+  }
   if (d.window != 0 || nany > (uint32_t)kTileSrcs) {
     rec.meta = d.window != 0 ? kTileGeneral : (kTileGeneral | kTileWide | nfull | nany << 8);
     rec.src_bytes[0] = s;

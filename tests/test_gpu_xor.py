@@ -340,6 +340,39 @@ def test_window_replay_random_data(oracle, dev, queue, lens):
     assert out.tobytes() == ref
 
 
+@pytest.mark.parametrize("vecs", [8, 4, 1])
+@pytest.mark.parametrize("window", [64 * 1024, 64 * 1024 + 16, 4 * 1024 * 1024])
+def test_window_replay_tiles(oracle, engine, dev, queue, vecs, window):
+    """Replay stripes (max_cs > window) folded as plain tiles with remapped
+    source addresses when the window is a multiple of the tile size, through
+    the general path when it is not (64 KiB + 16): eight sources around window
+    boundaries, misaligned sources and output, a wide (10-source) stripe,
+    rebuild-style truncation (out_len shorter than the longest source)."""
+    rng = np.random.default_rng(window + vecs)
+    W = window
+    stripes, refs = [], []
+    shapes = [[3 * W + 5, W, W - 1, 2 * W + 16, 17, 0, W + W // 2, 3 * W],
+              [4 * W - 3, 4 * W - 3, W // 3, 2 * W, 2 * W + 1, 3 * W + 100, 5, 4 * W - 16, 7, 2 * W - 9],
+              [2 * W + 1, 1]]
+    for ls in shapes:
+        chunks = [rng.integers(0, 256, size=L, dtype=np.uint8) for L in ls]
+        pads = [int(x) for x in rng.integers(0, 16, size=len(ls))]
+        ref = np.frombuffer(oracle.gen_parity_file(chunks, window=W)[8 * len(ls):], np.uint8)
+        out_len = max(ls)
+        stripes.append(dict(chunks=chunks, out_len=out_len, window=W, pads=pads, dst_pad=5))
+        refs.append(ref)
+        cut = out_len - W // 2 - 3  # truncated output (rebuild of a shorter victim)
+        stripes.append(dict(chunks=chunks, out_len=cut, window=W, pads=pads))
+        refs.append(ref[:cut])
+    engine.option("desc_vecs_per_thread", vecs)
+    try:
+        outs = gpu_stripes(dev, queue, stripes)
+    finally:
+        engine.option("desc_vecs_per_thread", 8)
+    for i, (o, r) in enumerate(zip(outs, refs)):
+        assert np.array_equal(o, r), i
+
+
 @pytest.mark.parametrize("seed", range(6))
 def test_rebuild_truncates_to_victim(oracle, dev, queue, seed):
     """Rebuild (task_processing.c:146-174,228-230): survivors + parity body,
