@@ -491,12 +491,13 @@ static int launch_stream(bcp_queue *q, bool gather, StreamArgs a, uint64_t ntile
 
 // A batch is uniform when every stripe has the same nsrc and out_len, every
 // source is at least out_len long (so neither zero padding nor window replay
-// can apply) and all addresses and the length are 16-byte multiples: then the
-// streaming kernel's pointer-table form computes it (rebuild's shape).
+// can apply) and all addresses are 16-byte multiples: then the streaming
+// kernel's pointer-table form computes it (rebuild's shape; a length that is
+// not a multiple of 16 ends in a byte tail).
 static bool uniform_batch(const bcp_stripe *st, uint32_t nstripes, const bcp_source *so) {
   const uint32_t n = st[0].nsrc;
   const uint64_t len = st[0].out_len;
-  if (n == 0 || len == 0 || !aligned16(len) || len / 16 > 0xFFFFFFFFull) return false;
+  if (n == 0 || len == 0 || len / 16 >= 0xFFFFFFFFull) return false;
   for (uint32_t i = 0; i < nstripes; i++) {
     if (st[i].nsrc != n || st[i].out_len != len || !aligned16(st[i].dst)) return false;
     for (uint32_t k = 0; k < n; k++) {
@@ -548,6 +549,7 @@ static int submit_desc(bcp_queue *q, const bcp_stripe *stripes, uint32_t nstripe
     a.stripes = (const bcp_stripe *)slot->dev;
     a.sources = (const bcp_source *)((char *)slot->dev + off_src);
     a.vps = (uint32_t)(len / 16);
+    a.tail = (uint32_t)(len % 16);
     a.tps = tps;
     a.nsrc = stripes[0].nsrc;
     a.dense = 1;
@@ -657,8 +659,7 @@ extern "C" int bcp_xor_strided_async(bcp_queue *q, void *dst, uint64_t dst_strid
   int rc = set_device(e);
   if (rc) return rc;
   const bool fast = aligned16((uint64_t)dst) && aligned16((uint64_t)src) && aligned16(dst_stride) &&
-                    aligned16(stripe_stride) && aligned16(src_stride) && aligned16(chunk_bytes) &&
-                    chunk_bytes / 16 <= 0xFFFFFFFFull;
+                    aligned16(stripe_stride) && aligned16(src_stride) && chunk_bytes / 16 < 0xFFFFFFFFull;
   if (fast) {
     StreamArgs a{};
     a.dst = (char *)dst;
@@ -667,6 +668,7 @@ extern "C" int bcp_xor_strided_async(bcp_queue *q, void *dst, uint64_t dst_strid
     a.stripe_stride = stripe_stride;
     a.src_stride = src_stride;
     a.vps = (uint32_t)(chunk_bytes / 16);
+    a.tail = (uint32_t)(chunk_bytes % 16);
     a.tps = stream_tiles_per_stripe(chunk_bytes, e->tuning.vecs_per_thread);
     a.nsrc = nsrc;
     return launch_stream(q, false, a, nstripes * a.tps);

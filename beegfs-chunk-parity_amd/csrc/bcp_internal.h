@@ -44,7 +44,8 @@ struct StreamArgs {
     uint64_t src_stride;
     const bcp_stripe *stripes;  // GATHER = 1: uniform descriptor batch (device copy)
     const bcp_source *sources;
-    uint32_t vps;               // 16-byte vectors per stripe output
+    uint32_t vps;               // whole 16-byte vectors per stripe output
+    uint32_t tail;              // bytes after them (0..15): the last, partial vector
     uint32_t tps;               // tiles per stripe
     uint32_t ntiles;
     uint32_t nsrc;

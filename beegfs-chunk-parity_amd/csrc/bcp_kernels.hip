@@ -49,6 +49,21 @@ __device__ __forceinline__ glob<T> *gp(uint64_t p) {
 }
 __device__ __forceinline__ v4u zero4() { return v4u{0u, 0u, 0u, 0u}; }
 
+// 16 bytes of source `p` (readable length len) at offset off, zero past len.
+typedef glob<const unsigned char> gbyte;
+__device__ __forceinline__ v4u ld16(gbyte *p) { return __builtin_nontemporal_load((const glob<v4u_u> *)p); }
+
+// The one vector of a source that straddles its end: n (1..15) readable bytes
+// at p, zeros after.  Static byte indices keep w[] in registers.
+__device__ __forceinline__ v4u load_straddle(gbyte *p, uint32_t n) {
+  unsigned int w[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+  for (uint32_t i = 0; i < 16; i++)
+    if (i < n) w[i >> 2] |= (unsigned int)p[i] << (8 * (i & 3));
+  return v4u{w[0], w[1], w[2], w[3]};
+}
+
+
 // ---------------------------------------------------------------------------
 // Streaming fold (hot path).  A tile is kBlock*U 16-byte vectors of one
 // stripe's output (32 KiB at the default U = 8, one 256-thread workgroup per
@@ -134,14 +149,40 @@ __device__ __forceinline__ void stream_tile(const StreamArgs &a, uint32_t t) {
 #pragma unroll
     for (int u = 0; u < U; u++) __builtin_nontemporal_store(acc[u], db + vb + u * 64);
   } else if constexpr (PARTIAL) {
-    // Last, partial tile of a stripe: per-vector bounds.
+    // Last, partial tile of a stripe: per-vector bounds (masked loads, all
+    // issued before the XORs when the width is known); the byte tail (a
+    // chunk length that is not a multiple of 16) in the lane that owns it.
+    if constexpr (NSRC > 0) {
+      v4u x[NSRC][U];
+#pragma unroll
+      for (int k = 0; k < NSRC; k++)
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+          const uint32_t v = tile_vec<U>(tin, u);
+          x[k][u] = v < a.vps ? ld_nt(src_k(k) + v) : zero4();
+        }
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const uint32_t v = tile_vec<U>(tin, u);
+        v4u acc = x[0][u];
+#pragma unroll
+        for (int k = 1; k < NSRC; k++) acc ^= x[k][u];
+        if (v < a.vps) __builtin_nontemporal_store(acc, db + v);
+      }
+    }
 #pragma unroll
     for (int u = 0; u < U; u++) {
       const uint32_t v = tile_vec<U>(tin, u);
-      if (v < a.vps) {
+      if (NSRC == 0 && v < a.vps) {
         v4u x = ld_nt(src_k(0) + v);
         for (uint32_t k = 1; k < nsrc; k++) x ^= ld_nt(src_k(k) + v);
         __builtin_nontemporal_store(x, db + v);
+      } else if (v == a.vps && a.tail) {
+        v4u x = zero4();
+        for (uint32_t k = 0; k < nsrc; k++)
+          x ^= load_straddle((gbyte *)(src_k(k) + v), a.tail);
+        glob<unsigned char> *d = (glob<unsigned char> *)(db + v);
+        for (uint32_t i = 0; i < a.tail; i++) d[i] = (unsigned char)(x[i >> 2] >> (8 * (i & 3)));
       }
     }
   }
@@ -188,20 +229,6 @@ __global__ __launch_bounds__(kBlock) void xor_stream(StreamArgs a) {
 // ---------------------------------------------------------------------------
 // Descriptor path helpers.
 // ---------------------------------------------------------------------------
-
-// 16 bytes of source `p` (readable length len) at offset off, zero past len.
-typedef glob<const unsigned char> gbyte;
-__device__ __forceinline__ v4u ld16(gbyte *p) { return __builtin_nontemporal_load((const glob<v4u_u> *)p); }
-
-// The one vector of a source that straddles its end: n (1..15) readable bytes
-// at p, zeros after.  Static byte indices keep w[] in registers.
-__device__ __forceinline__ v4u load_straddle(gbyte *p, uint32_t n) {
-  unsigned int w[4] = {0u, 0u, 0u, 0u};
-#pragma unroll
-  for (uint32_t i = 0; i < 16; i++)
-    if (i < n) w[i >> 2] |= (unsigned int)p[i] << (8 * (i & 3));
-  return v4u{w[0], w[1], w[2], w[3]};
-}
 
 __device__ __forceinline__ v4u load_src_tail(gbyte *p, uint64_t len, uint64_t off) {
   if (off + 16 <= len) return ld16(p + off);
@@ -713,7 +740,7 @@ __global__ __launch_bounds__(kBlock) void compare_bytes(const unsigned char *a, 
 // ---------------------------------------------------------------------------
 template <int NSRC, int U, int GATHER>
 static hipError_t launch_stream_nu(hipStream_t st, int grid, const StreamArgs &a) {
-  if (a.vps % (uint32_t)(kBlock * U) != 0)
+  if (a.vps % (uint32_t)(kBlock * U) != 0 || a.tail != 0)
     hipLaunchKernelGGL((xor_stream<NSRC, U, GATHER, kQueuePartial>), dim3(grid), dim3(kBlock), 0, st, a);
   else
     hipLaunchKernelGGL((xor_stream<NSRC, U, GATHER, kQueueFull>), dim3(grid), dim3(kBlock), 0, st, a);
@@ -745,7 +772,7 @@ static hipError_t launch_stream_u(hipStream_t st, int grid, const StreamArgs &a)
 }
 
 uint32_t stream_tiles_per_stripe(uint64_t chunk_bytes, int vecs) {
-  const uint64_t vps = chunk_bytes / 16;
+  const uint64_t vps = (chunk_bytes + 15) / 16;  // the byte tail is a (partial) vector too
   const uint64_t tile_v = (uint64_t)kBlock * vecs;
   return (uint32_t)((vps + tile_v - 1) / tile_v);
 }

@@ -184,6 +184,49 @@ def test_tuning_variants_agree(oracle, engine, dev, queue, bpc, vecs, sched):
     assert np.array_equal(res[0], oracle.xor_padded_np([data[:1000], data[5:70000]]))
 
 
+@pytest.mark.parametrize("vecs", [8, 4, 1])
+@pytest.mark.parametrize("chunk", [1, 15, 17, 1000, 4095, 524289, 3145745])
+@pytest.mark.parametrize("nsrc", [1, 3, 8, 13])
+def test_strided_byte_tail(oracle, engine, dev, queue, vecs, chunk, nsrc):
+    """Rows at a 256-byte pitch (the P role's window rows and the drop-in's
+    device layout) with a chunk length that is not a multiple of 16: the
+    streaming kernel's byte tail.  Bytes past each row's end stay untouched."""
+    nstripes = 3
+    pitch = (chunk + 255) // 256 * 256
+    rng = np.random.default_rng(chunk * 31 + nsrc * 7 + vecs)
+    rows = rng.integers(0, 256, size=(nstripes, nsrc, pitch), dtype=np.uint8)
+    src = dev.put(rows.reshape(-1))
+    out_pitch = pitch + 256
+    dst = dev.put(np.full(nstripes * out_pitch, 0xA5, dtype=np.uint8))
+    engine.tune(0, vecs)
+    try:
+        queue.xor_strided(dst, out_pitch, src, nsrc * pitch, pitch, nstripes, nsrc, chunk)
+        out = dev.get(dst, nstripes * out_pitch).reshape(nstripes, out_pitch)
+    finally:
+        engine.tune(0, 0)
+    for s in range(nstripes):
+        ref = np.bitwise_xor.reduce(rows[s, :, :chunk], axis=0)
+        assert np.array_equal(out[s, :chunk], ref), s
+        assert (out[s, chunk:] == 0xA5).all(), s
+
+
+@pytest.mark.parametrize("out_len", [1000, 524288 + 9, 65536 - 3])
+def test_uniform_batch_with_byte_tail(oracle, dev, queue, out_len):
+    """Rebuild shape with a length that is not a multiple of 16 (aligned
+    sources, some longer than out_len): pointer-table streaming kernel."""
+    rng = np.random.default_rng(out_len)
+    n = 8
+    stripes, refs = [], []
+    for _ in range(5):
+        lens = [out_len + int(rng.integers(0, 40)) for _ in range(n)]
+        chunks = [rng.integers(0, 256, size=L, dtype=np.uint8) for L in lens]
+        stripes.append(dict(chunks=chunks, out_len=out_len))
+        refs.append(np.bitwise_xor.reduce(np.stack([c[:out_len] for c in chunks]), axis=0))
+    outs = gpu_stripes(dev, queue, stripes)
+    for o, r in zip(outs, refs):
+        assert np.array_equal(o, r)
+
+
 def test_work_queue_back_to_back_and_two_queues(oracle, engine, dev, queue):
     """The work-queue counter is monotone per queue: many launches in a row on
     one queue, a second queue interleaved, and a switch to the static schedule
