@@ -144,7 +144,9 @@ int bcp_xor_stripes_async(bcp_queue *q, const bcp_stripe *stripes,
 
 /* ---- drop-in for xor_parity (task_processing.c:96-109) ----------------- */
 /* Host pointers, synchronous, same contract as the reference: dst gets
- * XOR of the nsources rows of `data` ([nsources][nbytes]).  Runs on a
+ * XOR of the nsources rows of `data` ([nsources][nbytes]).  nsources is
+ * 1..BCP_MAX_SOURCES (-EINVAL otherwise: the P role never folds zero rows,
+ * it unlinks the parity chunk instead, task_processing.c:141-144).  Runs on a
  * process-wide engine (device from $BCP_DEVICE, default 0) and a per-thread
  * queue with pinned staging; returns -ENODEV without a GPU. */
 int bcp_xor_parity(uint8_t *dst, size_t nbytes, const uint8_t *data,
