@@ -74,8 +74,16 @@ static int cmd_find(int argc, char **argv)
     return rc ? fail("find-all-chunks", rc) : 0;
 }
 
+static double now_s(void)
+{
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return (double)t.tv_sec + (double)t.tv_nsec * 1e-9;
+}
+
 static int cmd_gen(int argc, char **argv)
 {
+    const double t_start = now_s();
     int complete = -1, use_pipeline = 0, lanes = 12, force = 0;
     const char *changelog = NULL;
     int i = 0;
@@ -124,6 +132,7 @@ static int cmd_gen(int argc, char **argv)
         }
     }
     const time_t started = time(NULL);
+    const double t_phase1 = now_s();
     bcp_eventset *es = NULL;
     if ((rc = bcp_eventset_create(&es)))
         return fail("event set", rc);
@@ -148,12 +157,15 @@ static int cmd_gen(int argc, char **argv)
         return fail(complete ? "scanning chunks" : "reading changelog", rc);
     }
     printf("Total number of events found: %8zu\n", bcp_eventset_count(es));
+    const double t_round = now_s();
+    double t_setup = t_round;
     bcp_run_stats st;
     memset(&st, 0, sizeof(st));
     size_t planned = 0;
     if (use_pipeline) {
         bcp_pipeline *pl = NULL;
         rc = bcp_pipeline_create(NULL, &pl);
+        t_setup = now_s();
         if (!rc)
             rc = bcp_gen_round_pipeline(pl, root, ntargets, es, NULL, stderr, &st, &planned);
         if (pl)
@@ -165,9 +177,13 @@ static int cmd_gen(int argc, char **argv)
     bcp_eventset_destroy(es);
     if (rc)
         return fail("parity generation", rc);
+    const double t_end = now_s();
     printf("worklist %zu items, %llu tasks, %.3f s, %.1f MiB read, %.1f MiB written, %d rank errors\n", planned,
            (unsigned long long)st.tasks, st.seconds, st.bytes_read / 1048576.0, st.bytes_written / 1048576.0,
            st.errors);
+    /* stage timings, as the reference's rank 0 prints them (gen/main.c:920-928) */
+    printf("timings: init %.3f s, phase1 %.3f s, engine setup %.3f s, round %.3f s (run %.3f s), total %.3f s\n",
+           t_phase1 - t_start, t_round - t_phase1, t_setup - t_round, t_end - t_setup, st.seconds, t_end - t_start);
     if (st.errors)
         return 1;
     FILE *f = fopen(ts_path, "w");

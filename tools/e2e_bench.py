@@ -26,6 +26,7 @@ import ctypes
 import json
 import os
 import shutil
+import subprocess
 import sys
 import time
 
@@ -125,6 +126,25 @@ def config1(a):
     pl = bcp.Pipeline(io_threads=a.io_threads, ndevices=a.ndevices)
     ok &= run(f"pipeline(bcp_pipeline_run,{a.ndevices} GPU)", lambda: pl.run(root, 4, items))
     pl.close()
+    # the whole beegfs-parity-gen --complete flow through the CLI: scan every
+    # target, plan (P per select_P), run, fill the DB replicas (warm median)
+    tool = os.path.join(ROOT, "beegfs-chunk-parity_amd", "bin", "bcp")
+    for label, extra in (("cli_parity_gen_complete(protocol)", []), ("cli_parity_gen_complete(pipeline)", ["--pipeline"])):
+        times = []
+        for r in range(1 + a.reps):
+            t0 = time.perf_counter()
+            res = subprocess.run([tool, "parity-gen", "--complete", "--force"] + extra + [root, "4"],
+                                 capture_output=True, text=True)
+            times.append(time.perf_counter() - t0)
+            if res.returncode != 0:
+                emit(config=1, path=label, error=res.stderr[-500:])
+                break
+        else:
+            w = float(np.median(times[1:])) if a.reps else times[0]
+            stages = next((ln for ln in res.stdout.splitlines() if ln.startswith("timings:")), "")
+            emit(config=1, path=label, cold_seconds=round(times[0], 3), warm_seconds=round(w, 3),
+                 GiBps=round((rd + wr) / w / GiB, 3), note="process wall time: start-up, scan, planning, DB updates",
+                 last_run_stages=stages)
     # rebuild target 2 through the protocol
     lost = {}
     for path, holders, p, _ in files:
