@@ -15,6 +15,8 @@
 // (waves_per_eu(1)) 82-84 %, 2 WG/CU 80-83 %.  The read-only ceiling of the
 // same schedule is 91.9-92.0 % for both layouts.  The atomic round trip is not
 // the limiter; more data in flight per CU only widens the address window.
+// -DXE3_PRESTORE (profiles/r01/kernel_exp_8b_grab_before_stores.jsonl): the
+// grab between the XORs and the stores (AHEAD 4) 81.7 % vs 84.9 % shipped.
 //
 // Shipped schedule (bcp_kernels.hip xor_stream): thread 0 grabs tile t+1 with
 // one atomicAdd AFTER the stores of tile t, then one barrier; the atomic's
@@ -27,6 +29,7 @@
 //            loads and the pointer-table loads of t+1 are issued during t
 //            (pointer-table form only)
 //   AHEAD 3  grab issued right before tile t's loads
+//   AHEAD 4  grab issued after the XORs, before the stores
 // Workloads: GATHER 0 = config 2 gen (strided [stripes][8][S] -> [stripes][S]);
 // GATHER 1 = config 3 rebuild (dense pointer table: 7 survivors of the source
 // array + the parity array -> a third array).
@@ -144,6 +147,7 @@ __device__ __forceinline__ void xe3_body(const Args &a) {
 #pragma unroll
       for (int k = 1; k < NSRC; k++) acc[u] ^= x[k][u];
     }
+    if (AHEAD == 4 && threadIdx.x == 0) g = atomicAdd(a.ctr, 1ull);
     if constexpr (MODE == MODE_READ) {
 #pragma unroll
       for (int u = 0; u < U; u++) sink ^= acc[u];
@@ -205,6 +209,15 @@ struct Entry {
 #define X(name, U, G, A, M, BPC) {name, xe3<U, G, A, M>, U, G, A, M, BPC}
 #define W(name, U, G, A, M, BPC) {name, xe3w<U, G, A, M>, U, G, A, M, BPC}
 static const Entry kV[] = {
+#ifdef XE3_PRESTORE
+    X("gen_base_u8", 8, 0, 0, MODE_XOR, 1),
+    X("gen_prestore_u8", 8, 0, 4, MODE_XOR, 1),
+    X("gen_base_u4", 4, 0, 0, MODE_XOR, 1),
+    X("gen_prestore_u4", 4, 0, 4, MODE_XOR, 1),
+    X("gen_prestore_u4_bpc2", 4, 0, 4, MODE_XOR, 2),
+    X("reb_base_u8", 8, 1, 0, MODE_XOR, 1),
+    X("reb_prestore_u8", 8, 1, 4, MODE_XOR, 1),
+#else
     X("gen_base_u8", 8, 0, 0, MODE_XOR, 1),
     X("gen_ahead_u8", 8, 0, 1, MODE_XOR, 1),
     X("gen_base_u4", 4, 0, 0, MODE_XOR, 1),
@@ -230,6 +243,7 @@ static const Entry kV[] = {
     W("reb_w1_pre_u8", 8, 1, 3, MODE_XOR, 1),
     W("reb_w1_ahead2_u8", 8, 1, 2, MODE_XOR, 1),
     X("reb_read_base_u8", 8, 1, 0, MODE_READ, 1),
+#endif
 };
 #undef X
 #undef W
