@@ -33,6 +33,7 @@ struct Tuning {
     int desc_grab = 1;          // tiles per work-queue grab
     int desc_schedule = kSchedQueue;
     int desc_force = 0;         // 1: uniform batches take xor_desc too (A/B only)
+    int stream_grid = 0;        // xor_stream: explicit workgroup count (0: 15/16 of CUs x blocks_per_cu)
 };
 
 // Arguments of the streaming kernel (xor_stream).

@@ -64,6 +64,7 @@ def parse():
     ap.add_argument("--schedule", type=int, default=-1,
                     help="tile schedule of the timed kernel: 0 work queue, 1 static ranges (default: engine's)")
     ap.add_argument("--grab", type=int, default=0, help="tiles per work-queue grab of the descriptor kernel")
+    ap.add_argument("--grid", type=int, default=0, help="explicit workgroup count of the streaming kernel (A/B)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-stripes", type=int, default=256, help="stripes in the CPU sample pool")
     ap.add_argument("--no-cpu", action="store_true")
@@ -99,6 +100,8 @@ def main():
         eng.tune(a.blocks_per_cu, a.vecs)
     if a.grab:
         eng.option("desc_grab", a.grab)
+    if a.grid:
+        eng.option("stream_grid", a.grid)
     if a.schedule >= 0:
         eng.option("schedule" if a.mode != "mixed" else "desc_schedule", a.schedule)
     cus, devname = eng.info()

@@ -180,7 +180,9 @@ int bcp_set_tuning(bcp_engine *eng, int blocks_per_cu, int vecs_per_thread);
  * measurements) for the uniform streaming kernel; "desc_schedule" (same
  * values, default 0), "desc_grab" (tiles per work-queue grab, 1..64, default
  * 1) and "desc_force" (1 = uniform batches take the descriptor kernel too;
- * A/B only) for the descriptor kernel (mixed sizes, windows, unaligned). */
+ * A/B only) for the descriptor kernel (mixed sizes, windows, unaligned);
+ * "stream_grid" (explicit workgroup count of the streaming kernel; 0 = the
+ * default, blocks_per_cu on 15 of every 16 CUs). */
 int bcp_set_option(bcp_engine *eng, const char *key, int value);
 /* Current value of a named knob (same keys). */
 int bcp_get_option(bcp_engine *eng, const char *key, int *value);

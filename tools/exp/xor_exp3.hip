@@ -307,6 +307,7 @@ int main(int argc, char **argv) {
     a.ctr = ctr;
     a.base = base;
     int grid = std::min<int>(cus * kV[v].bpc, a.ntiles);
+    if (getenv("XE3_GRID")) grid = std::min<int>(atoi(getenv("XE3_GRID")), a.ntiles);  // A/B of the grid size
     hipLaunchKernelGGL(kV[v].fn, dim3(grid), dim3(KB), 0, st, a);
     CK(hipGetLastError());
     // every workgroup makes one failing grab (AHEAD 2: two)
