@@ -114,8 +114,15 @@ static int grid_for(const bcp_engine *e) {
 // shapes: ~0.43 of a full tile on average) need a second workgroup per CU to
 // keep enough loads in flight (tools/exp/desc_probe.py, profiles/r01/mixed/).
 static int desc_grid_for(const bcp_engine *e, double bytes_per_tile, uint32_t tile_bytes) {
+  if (e->tuning.desc_grid > 0) return e->tuning.desc_grid;
   int bpc = e->tuning.desc_blocks_per_cu;
-  if (bpc <= 0) bpc = bytes_per_tile >= 0.6 * (double)(kTileSrcs + 1) * tile_bytes ? 1 : 2;
+  if (bpc <= 0) {
+    // dense tiles: the streaming kernel's grid, one workgroup on 15 of
+    // every 16 CUs (+1 point here too); sparse tiles: a full 2 per CU
+    // (profiles/r01/mixed/desc_grid.jsonl)
+    if (bytes_per_tile >= 0.6 * (double)(kTileSrcs + 1) * tile_bytes) return std::max(1, e->num_cus * 15 / 16);
+    bpc = 2;
+  }
   int g = e->num_cus * bpc;
   return g > 0 ? g : 256;
 }
@@ -236,6 +243,7 @@ extern "C" int bcp_set_option(bcp_engine *eng, const char *key, int value) {
   else if (!strcmp(key, "desc_grab") && value >= 1 && value <= 64) eng->tuning.desc_grab = value;
   else if (!strcmp(key, "desc_force") && (value == 0 || value == 1)) eng->tuning.desc_force = value;
   else if (!strcmp(key, "stream_grid") && value >= 0 && value <= 65536) eng->tuning.stream_grid = value;
+  else if (!strcmp(key, "desc_grid") && value >= 0 && value <= 65536) eng->tuning.desc_grid = value;
   else rc = -EINVAL;
   pthread_mutex_unlock(&eng->lock);
   return rc;
@@ -255,6 +263,7 @@ extern "C" int bcp_get_option(bcp_engine *eng, const char *key, int *value) {
   else if (!strcmp(key, "desc_grab")) *value = t.desc_grab;
   else if (!strcmp(key, "desc_force")) *value = t.desc_force;
   else if (!strcmp(key, "stream_grid")) *value = t.stream_grid;
+  else if (!strcmp(key, "desc_grid")) *value = t.desc_grid;
   else rc = -EINVAL;
   pthread_mutex_unlock(&eng->lock);
   return rc;

@@ -34,6 +34,7 @@ struct Tuning {
     int desc_schedule = kSchedQueue;
     int desc_force = 0;         // 1: uniform batches take xor_desc too (A/B only)
     int stream_grid = 0;        // xor_stream: explicit workgroup count (0: 15/16 of CUs x blocks_per_cu)
+    int desc_grid = 0;          // xor_desc: explicit workgroup count (0: desc_grid_for)
 };
 
 // Arguments of the streaming kernel (xor_stream).

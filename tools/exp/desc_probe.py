@@ -98,9 +98,12 @@ for kind in a.workloads.split(","):
     out = eng.alloc(out_bytes(lens_all))
     st, so, nbytes = build(lens_all, out)
     for tun in a.tunings.split(","):
-        u, bpc = (int(x) for x in tun.split(":"))
+        parts = [int(x) for x in tun.split(":")]
+        u, bpc = parts[0], parts[1]
+        grid = parts[2] if len(parts) > 2 else 0
         eng.option("desc_vecs_per_thread", u)
         eng.option("desc_blocks_per_cu", bpc)
+        eng.option("desc_grid", grid)
         for _ in range(2):
             bcp.check("x", L.bcp_xor_stripes_async(q.h, st, len(st), so, len(so)))
         q.sync()
@@ -115,7 +118,7 @@ for kind in a.workloads.split(","):
         q.sync()
         ms = q.elapsed_ms(0, 1) / a.reps
         tiles = sum((int(ls.max()) + 4096 * u - 1) // (4096 * u) for ls in lens_all)
-        print(json.dumps({"workload": kind, "vecs": u, "blocks_per_cu": bpc, "stripes": len(st),
+        print(json.dumps({"workload": kind, "vecs": u, "blocks_per_cu": bpc, "grid": grid, "stripes": len(st),
                           "subtiles": tiles, "bytes_per_subtile": round(nbytes / tiles), "kernel_ms": round(ms, 4),
                           "GBps": round(nbytes / ms / 1e6, 1), "frac_8TBs": round(nbytes / ms / 8e9, 4)}),
               flush=True)
