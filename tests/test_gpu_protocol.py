@@ -123,6 +123,43 @@ def test_pipeline_matches_oracle_mixed_sizes(bcp, oracle, tmp_path, slab):
         assert S.read_file(S.parity_path(root, p, path)) == oracle.gen_parity_file(contents[path]), path
 
 
+def test_pipeline_wide_and_windowed_stripes(bcp, oracle, tmp_path):
+    """The batched pipeline on stripes wider than a tile record (up to 15
+    sources), chunks past the 10 MiB transfer window (replay) and grouped
+    sparse tiles; then a rebuild of one target through the pipeline."""
+    rng = np.random.default_rng(91)
+    ntargets = 16
+    files = []
+    for i in range(14):
+        width = int(rng.integers(9, 16)) if i % 2 else int(rng.integers(2, 9))
+        holders, p = S.random_layout(rng, ntargets, width)
+        hi = 24 * 1024 * KiB if i % 3 == 0 else 3 * 1024 * KiB
+        lens = [int(x) for x in np.exp(rng.uniform(np.log(16 * KiB), np.log(hi), size=width))]
+        lens[-1] += 7
+        files.append((f"w/{i % 4}/c{i}", holders, p, lens))
+    root = str(tmp_path)
+    items, contents = S.populate(root, ntargets, files, seed=12)
+    st = bcp.pipeline_gen(root, ntargets, items, slab_bytes=64 << 20, io_threads=4, nslots=3)
+    assert st.errors == 0 and st.tasks == len(files)
+    for (path, holders, p, lens) in files:
+        assert S.read_file(S.parity_path(root, p, path)) == oracle.gen_parity_file(contents[path]), path
+    victim = 5
+    lost = {}
+    for (path, holders, p, lens) in files:
+        if victim in holders:
+            lost[path] = S.read_file(S.chunk_path(root, victim, path))
+            os.remove(S.chunk_path(root, victim, path))
+    assert lost
+    pl = bcp.Pipeline(io_threads=4)
+    try:
+        st = pl.rebuild(root, ntargets, victim, sorted(items, key=lambda x: x[0].encode()))
+    finally:
+        pl.close()
+    assert st.errors == 0
+    for path, data in lost.items():
+        assert S.read_file(S.chunk_path(root, victim, path)) == data, path
+
+
 def test_pipeline_multiwindow_and_delete(bcp, oracle, tmp_path):
     root = str(tmp_path)
     files = [("big/a", [0, 1], 4, [10485760, 26214405]),
