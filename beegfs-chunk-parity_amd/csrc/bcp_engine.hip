@@ -244,6 +244,7 @@ extern "C" int bcp_set_option(bcp_engine *eng, const char *key, int value) {
   else if (!strcmp(key, "desc_force") && (value == 0 || value == 1)) eng->tuning.desc_force = value;
   else if (!strcmp(key, "stream_grid") && value >= 0 && value <= 65536) eng->tuning.stream_grid = value;
   else if (!strcmp(key, "desc_grid") && value >= 0 && value <= 65536) eng->tuning.desc_grid = value;
+  else if (!strcmp(key, "contiguous_alloc") && (value == 0 || value == 1)) eng->tuning.contiguous_alloc = value;
   else rc = -EINVAL;
   pthread_mutex_unlock(&eng->lock);
   return rc;
@@ -264,6 +265,7 @@ extern "C" int bcp_get_option(bcp_engine *eng, const char *key, int *value) {
   else if (!strcmp(key, "desc_force")) *value = t.desc_force;
   else if (!strcmp(key, "stream_grid")) *value = t.stream_grid;
   else if (!strcmp(key, "desc_grid")) *value = t.desc_grid;
+  else if (!strcmp(key, "contiguous_alloc")) *value = t.contiguous_alloc;
   else rc = -EINVAL;
   pthread_mutex_unlock(&eng->lock);
   return rc;
@@ -406,11 +408,23 @@ extern "C" int bcp_queue_elapsed_ms(bcp_queue *q, int a, int b, float *ms) {
 // ---------------------------------------------------------------------------
 // memory
 // ---------------------------------------------------------------------------
+// Option "contiguous_alloc" (off by default): large buffers requested
+// physically contiguous.  In interleaved A/B runs that helped the regular
+// 512 KiB-stride streams (gen +0.5-1.0, rebuild +0.8-1.3 points) but cost
+// the config-5 mixed shapes 2 points (profiles/r01/contig_alloc_ab*.jsonl),
+// so it stays a knob.  Falls back to a default allocation.
+constexpr size_t kContigMin = (size_t)64 << 20;
+
 extern "C" int bcp_dev_alloc(bcp_engine *eng, size_t bytes, void **dptr) {
   if (!eng || !dptr) return -EINVAL;
   *dptr = nullptr;
   int rc = set_device(eng);
   if (rc) return rc;
+  if (eng->tuning.contiguous_alloc && bytes >= kContigMin) {
+    if (hipExtMallocWithFlags(dptr, bytes, hipDeviceMallocContiguous) == hipSuccess) return 0;
+    (void)hipGetLastError();  // clear the sticky error of the failed attempt
+    *dptr = nullptr;
+  }
   HIP_RC(hipMalloc(dptr, bytes ? bytes : 16));
   return 0;
 }

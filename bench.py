@@ -65,6 +65,7 @@ def parse():
                     help="tile schedule of the timed kernel: 0 work queue, 1 static ranges (default: engine's)")
     ap.add_argument("--grab", type=int, default=0, help="tiles per work-queue grab of the descriptor kernel")
     ap.add_argument("--grid", type=int, default=0, help="explicit workgroup count of the streaming kernel (A/B)")
+    ap.add_argument("--contig", action="store_true", help="physically contiguous device allocations (A/B knob)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-stripes", type=int, default=256, help="stripes in the CPU sample pool")
     ap.add_argument("--no-cpu", action="store_true")
@@ -102,6 +103,8 @@ def main():
         eng.option("desc_grab", a.grab)
     if a.grid:
         eng.option("stream_grid", a.grid)
+    if a.contig:
+        eng.option("contiguous_alloc", 1)
     if a.schedule >= 0:
         eng.option("schedule" if a.mode != "mixed" else "desc_schedule", a.schedule)
     cus, devname = eng.info()

@@ -182,7 +182,9 @@ int bcp_set_tuning(bcp_engine *eng, int blocks_per_cu, int vecs_per_thread);
  * 1) and "desc_force" (1 = uniform batches take the descriptor kernel too;
  * A/B only) for the descriptor kernel (mixed sizes, windows, unaligned);
  * "stream_grid" (explicit workgroup count of the streaming kernel; 0 = the
- * default, blocks_per_cu on 15 of every 16 CUs). */
+ * default, blocks_per_cu on 15 of every 16 CUs), "desc_grid" (the same for
+ * the descriptor kernel), "contiguous_alloc" (1: bcp_dev_alloc requests
+ * physically contiguous memory for buffers of 64 MiB and more; default 0). */
 int bcp_set_option(bcp_engine *eng, const char *key, int value);
 /* Current value of a named knob (same keys). */
 int bcp_get_option(bcp_engine *eng, const char *key, int *value);

@@ -260,11 +260,17 @@ int main(int argc, char **argv) {
   Src *table;
   uint64_t *dsts;
   unsigned long long *ctr, *dcount;
-  CK(hipMalloc(&src, in_bytes));
-  CK(hipMalloc(&par, out_bytes));
-  CK(hipMalloc(&dst, out_bytes));
-  CK(hipMalloc(&ref_gen, out_bytes));
-  CK(hipMalloc(&ref_reb, out_bytes));
+  // XE3_CONTIG=1: physically contiguous allocations (hipDeviceMallocContiguous)
+  const bool contig = getenv("XE3_CONTIG") && atoi(getenv("XE3_CONTIG"));
+  auto dalloc = [&](char **p, size_t n) {
+    if (contig) CK(hipExtMallocWithFlags((void **)p, n, hipDeviceMallocContiguous));
+    else CK(hipMalloc(p, n));
+  };
+  dalloc(&src, in_bytes);
+  dalloc(&par, out_bytes);
+  dalloc(&dst, out_bytes);
+  dalloc(&ref_gen, out_bytes);
+  dalloc(&ref_reb, out_bytes);
   CK(hipMalloc(&table, stripes * NSRC * sizeof(Src)));
   CK(hipMalloc(&dsts, stripes * sizeof(uint64_t)));
   CK(hipMalloc(&ctr, 256));
