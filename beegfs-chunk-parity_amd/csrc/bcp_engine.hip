@@ -18,6 +18,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <new>
 #include <vector>
 
@@ -31,6 +32,7 @@ struct bcp_engine {
   char name[256] = {0};
   Tuning tuning;
   pthread_mutex_t lock = PTHREAD_MUTEX_INITIALIZER;
+  std::atomic<int> last_stream_vecs{0};  // U of the latest xor_stream launch (tools)
 };
 
 namespace {
@@ -128,6 +130,22 @@ static int desc_grid_for(const bcp_engine *e, double bytes_per_tile, uint32_t ti
 }
 
 static bool stream_vecs_ok(int v) { return v == 1 || v == 2 || v == 4 || v == 8; }
+
+// Vectors per lane (tile size) of one xor_stream launch.  Explicit tuning
+// wins; auto (0) keeps U = 8 (32 KiB per source per tile, the large-batch
+// optimum) unless the batch is small: with fewer than ~16 tiles per
+// workgroup the last tiles of the queue leave most CUs idle, and halving the
+// tile halves that tail.  Thresholds from tools/batch_curve.py
+// (profiles/r01/batch_tune.jsonl, 8 x 512 KiB stripes): U = 2 for 1-2
+// stripes (-38 %), U = 4 up to 128 stripes (-3..-25 %), U = 8 from 256.
+static int stream_vecs(const bcp_engine *e, uint64_t chunk_bytes, uint64_t nstripes) {
+  if (e->tuning.vecs_per_thread) return e->tuning.vecs_per_thread;
+  const uint64_t t8 = nstripes * stream_tiles_per_stripe(chunk_bytes, 8);
+  const uint64_t g = (uint64_t)grid_for(e);
+  if (t8 * 5 < g) return 2;
+  if (t8 < 16 * g) return 4;
+  return 8;
+}
 static bool desc_vecs_ok(int v) { return v == 1 || v == 2 || v == 4 || v == 8; }
 
 static bool aligned16(uint64_t x) { return (x & 15u) == 0; }
@@ -157,12 +175,21 @@ static int ring_acquire(bcp_queue *q, size_t bytes, DescSlot **out) {
 // Upload a slot's tables on the queue's copy stream and make the compute
 // stream wait for them: the upload for launch k+1 overlaps kernel k instead
 // of sitting between them in stream order.  (The slot's previous kernel has
-// finished: ring_acquire waited for it.)
-static int stage_tables(bcp_queue *q, DescSlot *slot, size_t bytes) {
+// finished: ring_acquire waited for it.)  Tables of at most host_max bytes
+// are not copied: the kernels read them from the pinned slot over PCIe,
+// which for small batches costs less than the copy and the cross-stream wait
+// (tools/batch_curve.py, profiles/r01/batch/).  Returns the tables' address
+// as the kernels see it.
+static int stage_tables(bcp_queue *q, DescSlot *slot, size_t bytes, size_t host_max, char **tables) {
+  if (bytes <= host_max) {
+    *tables = (char *)slot->host;
+    return 0;
+  }
   if (!q->copy_stream) HIP_RC(hipStreamCreateWithFlags(&q->copy_stream, hipStreamNonBlocking));
   HIP_RC(hipMemcpyAsync(slot->dev, slot->host, bytes, hipMemcpyHostToDevice, q->copy_stream));
   HIP_RC(hipEventRecord(slot->copied, q->copy_stream));
   HIP_RC(hipStreamWaitEvent(q->stream, slot->copied, 0));
+  *tables = (char *)slot->dev;
   return 0;
 }
 
@@ -211,7 +238,8 @@ extern "C" int bcp_engine_create(int device, bcp_engine **out) {
   if (const char *v = getenv("BCP_VECS_PER_THREAD")) e->tuning.vecs_per_thread = atoi(v);
   const Tuning defaults;
   if (e->tuning.blocks_per_cu < 1 || e->tuning.blocks_per_cu > 32) e->tuning.blocks_per_cu = defaults.blocks_per_cu;
-  if (!stream_vecs_ok(e->tuning.vecs_per_thread)) e->tuning.vecs_per_thread = defaults.vecs_per_thread;
+  if (e->tuning.vecs_per_thread && !stream_vecs_ok(e->tuning.vecs_per_thread))
+    e->tuning.vecs_per_thread = defaults.vecs_per_thread;
   if (const char *v = getenv("BCP_SCHEDULE")) e->tuning.schedule = atoi(v) == kSchedStatic ? kSchedStatic : kSchedQueue;
   *out = e;
   return 0;
@@ -235,7 +263,7 @@ extern "C" int bcp_set_option(bcp_engine *eng, const char *key, int value) {
   int rc = 0;
   pthread_mutex_lock(&eng->lock);
   if (!strcmp(key, "blocks_per_cu") && value >= 1 && value <= 32) eng->tuning.blocks_per_cu = value;
-  else if (!strcmp(key, "vecs_per_thread") && stream_vecs_ok(value)) eng->tuning.vecs_per_thread = value;
+  else if (!strcmp(key, "vecs_per_thread") && (value == 0 || stream_vecs_ok(value))) eng->tuning.vecs_per_thread = value;
   else if (!strcmp(key, "desc_blocks_per_cu") && value >= 0 && value <= 32) eng->tuning.desc_blocks_per_cu = value;
   else if (!strcmp(key, "desc_vecs_per_thread") && desc_vecs_ok(value)) eng->tuning.desc_vecs = value;
   else if (!strcmp(key, "schedule") && (value == kSchedQueue || value == kSchedStatic)) eng->tuning.schedule = value;
@@ -245,6 +273,9 @@ extern "C" int bcp_set_option(bcp_engine *eng, const char *key, int value) {
   else if (!strcmp(key, "stream_grid") && value >= 0 && value <= 65536) eng->tuning.stream_grid = value;
   else if (!strcmp(key, "desc_grid") && value >= 0 && value <= 65536) eng->tuning.desc_grid = value;
   else if (!strcmp(key, "contiguous_alloc") && (value == 0 || value == 1)) eng->tuning.contiguous_alloc = value;
+  else if (!strcmp(key, "table_host_max") && value >= 0 && value <= (1 << 24)) eng->tuning.table_host_max = value;
+  else if (!strcmp(key, "desc_table_host_max") && value >= 0 && value <= (1 << 24))
+    eng->tuning.desc_table_host_max = value;
   else rc = -EINVAL;
   pthread_mutex_unlock(&eng->lock);
   return rc;
@@ -266,6 +297,9 @@ extern "C" int bcp_get_option(bcp_engine *eng, const char *key, int *value) {
   else if (!strcmp(key, "stream_grid")) *value = t.stream_grid;
   else if (!strcmp(key, "desc_grid")) *value = t.desc_grid;
   else if (!strcmp(key, "contiguous_alloc")) *value = t.contiguous_alloc;
+  else if (!strcmp(key, "table_host_max")) *value = t.table_host_max;
+  else if (!strcmp(key, "desc_table_host_max")) *value = t.desc_table_host_max;
+  else if (!strcmp(key, "last_stream_vecs")) *value = eng->last_stream_vecs.load(std::memory_order_relaxed);
   else rc = -EINVAL;
   pthread_mutex_unlock(&eng->lock);
   return rc;
@@ -504,7 +538,7 @@ extern "C" int bcp_memset_async(bcp_queue *q, void *dst, int value, size_t bytes
 // ---------------------------------------------------------------------------
 
 // Launch the streaming kernel on q (work-queue or static schedule).
-static int launch_stream(bcp_queue *q, bool gather, StreamArgs a, uint64_t ntiles) {
+static int launch_stream(bcp_queue *q, bool gather, int vecs, StreamArgs a, uint64_t ntiles) {
   bcp_engine *e = q->eng;
   if (ntiles == 0) return 0;
   if (ntiles > 0xFFFFFFF0ull) return -EINVAL;
@@ -514,7 +548,8 @@ static int launch_stream(bcp_queue *q, bool gather, StreamArgs a, uint64_t ntile
   a.base = q->qbase;
   int grid = grid_for(e);
   if ((uint64_t)grid > ntiles) grid = (int)ntiles;
-  HIP_RC(launch_xor_stream(q->stream, grid, e->tuning.vecs_per_thread, gather, a));
+  HIP_RC(launch_xor_stream(q->stream, grid, vecs, gather, a));
+  e->last_stream_vecs.store(vecs, std::memory_order_relaxed);
   if (a.sched == kSchedQueue) q->qbase += ntiles + (uint64_t)grid;
   return 0;
 }
@@ -564,8 +599,8 @@ static int submit_desc(bcp_queue *q, const bcp_stripe *stripes, uint32_t nstripe
   if (ntiles == 0) return 0;
   if (ntiles > 0xFFFFFFF0ull) return -EINVAL;
   if (!e->tuning.desc_force && uniform_batch(stripes, nstripes, sources)) {
-    const int sv = e->tuning.vecs_per_thread;
     const uint64_t len = stripes[0].out_len;
+    const int sv = stream_vecs(e, len, nstripes);
     const uint32_t tps = stream_tiles_per_stripe(len, sv);
     const size_t off_src = ((size_t)nstripes * sizeof(bcp_stripe) + 15) & ~(size_t)15;
     const size_t bytes = off_src + (size_t)nsources * sizeof(bcp_source);
@@ -574,17 +609,18 @@ static int submit_desc(bcp_queue *q, const bcp_stripe *stripes, uint32_t nstripe
     if (rc) return rc;
     memcpy(slot->host, stripes, (size_t)nstripes * sizeof(bcp_stripe));
     memcpy((char *)slot->host + off_src, sources, (size_t)nsources * sizeof(bcp_source));
-    if ((rc = stage_tables(q, slot, bytes))) return rc;
+    char *d = nullptr;
+    if ((rc = stage_tables(q, slot, bytes, (size_t)e->tuning.table_host_max, &d))) return rc;
     StreamArgs a{};
-    a.stripes = (const bcp_stripe *)slot->dev;
-    a.sources = (const bcp_source *)((char *)slot->dev + off_src);
+    a.stripes = (const bcp_stripe *)d;
+    a.sources = (const bcp_source *)(d + off_src);
     a.vps = (uint32_t)(len / 16);
     a.tail = (uint32_t)(len % 16);
     a.tps = tps;
     a.nsrc = stripes[0].nsrc;
     a.dense = 1;
     for (uint32_t i = 0; i < nstripes && a.dense; i++) a.dense = stripes[i].first_src == i * a.nsrc;
-    rc = launch_stream(q, true, a, (uint64_t)nstripes * tps);
+    rc = launch_stream(q, true, sv, a, (uint64_t)nstripes * tps);
     if (rc) return rc;
     HIP_RC(hipEventRecord(slot->done, q->stream));
     slot->used = true;
@@ -645,9 +681,9 @@ static int submit_desc(bcp_queue *q, const bcp_stripe *stripes, uint32_t nstripe
     HIP_RC(hipMalloc((void **)&q->tiles, cap * sizeof(DescTile)));
     q->tiles_cap = cap;
   }
-  if ((rc = stage_tables(q, slot, bytes))) return rc;
+  char *d = nullptr;
+  if ((rc = stage_tables(q, slot, bytes, (size_t)e->tuning.desc_table_host_max, &d))) return rc;
   DescBatch b;
-  char *d = (char *)slot->dev;
   b.stripes = (const bcp_stripe *)d;
   b.sources = (const bcp_source *)(d + off_src);
   b.tile_start = (const uint32_t *)(d + off_tiles);
@@ -699,9 +735,10 @@ extern "C" int bcp_xor_strided_async(bcp_queue *q, void *dst, uint64_t dst_strid
     a.src_stride = src_stride;
     a.vps = (uint32_t)(chunk_bytes / 16);
     a.tail = (uint32_t)(chunk_bytes % 16);
-    a.tps = stream_tiles_per_stripe(chunk_bytes, e->tuning.vecs_per_thread);
+    const int sv = stream_vecs(e, chunk_bytes, nstripes);
+    a.tps = stream_tiles_per_stripe(chunk_bytes, sv);
     a.nsrc = nsrc;
-    return launch_stream(q, false, a, nstripes * a.tps);
+    return launch_stream(q, false, sv, a, nstripes * a.tps);
   }
   // General geometry: express as descriptors (any alignment / tail).
   if (nstripes * nsrc > 0xFFFFFFFFull || nstripes > 0xFFFFFFFFull) return -EINVAL;

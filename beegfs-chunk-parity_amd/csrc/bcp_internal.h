@@ -23,7 +23,7 @@ constexpr int kSchedStatic = 1;  // contiguous tile range per workgroup (r01 des
 // kernel_exp_6/7), work-queue schedule, non-temporal loads and stores.
 struct Tuning {
     int blocks_per_cu = 1;      // xor_stream: 256-thread workgroups launched per CU
-    int vecs_per_thread = 8;    // xor_stream: 16-byte vectors per lane per tile (1, 2, 4, 8)
+    int vecs_per_thread = 0;    // xor_stream: 16-byte vectors per lane per tile (1, 2, 4, 8; 0 = by batch size)
     int schedule = kSchedQueue; // xor_stream: kSched*
     // xor_desc (tools/exp/desc_probe.py, profiles/r01/mixed/): 8 vectors per
     // lane, one 32 KiB tile per queue grab; workgroups per CU 0 = auto by the
@@ -36,6 +36,12 @@ struct Tuning {
     int stream_grid = 0;        // xor_stream: explicit workgroup count (0: 15/16 of CUs x blocks_per_cu)
     int desc_grid = 0;          // xor_desc: explicit workgroup count (0: desc_grid_for)
     int contiguous_alloc = 0;   // 1: bcp_dev_alloc asks for physically contiguous buffers >= 64 MiB
+    // Descriptor tables up to this many bytes are read by the kernels from
+    // pinned host memory instead of being copied (tools/batch_curve.py):
+    // the pointer-table xor_stream reads its table once per tile (a win up
+    // to ~16 stripes of 8), desc_tiles once per batch (a win up to >= 512).
+    int table_host_max = 4096;
+    int desc_table_host_max = 128 * 1024;
 };
 
 // Arguments of the streaming kernel (xor_stream).

@@ -172,8 +172,9 @@ int bcp_queue_elapsed_ms(bcp_queue *q, int slot_from, int slot_to,
 
 /* Tuning knobs for the fast path (bench / autotune only; 0 = default). */
 int bcp_set_tuning(bcp_engine *eng, int blocks_per_cu, int vecs_per_thread);
-/* Named knob: "blocks_per_cu" (1..32), "vecs_per_thread" (1,2,4,8) of the
- * uniform streaming kernel; "desc_blocks_per_cu" (0 = chosen per batch from
+/* Named knob: "blocks_per_cu" (1..32), "vecs_per_thread" (1,2,4,8; 0 = the
+ * default: 8, or 4 / 2 for batches of few tiles) of the uniform streaming
+ * kernel; "desc_blocks_per_cu" (0 = chosen per batch from
  * its bytes per tile, the default; 1..32), "desc_vecs_per_thread" (1,2,4,8)
  * of the descriptor kernel; "schedule" (0 = device-wide tile work queue, the
  * default; 1 = a static contiguous tile range per workgroup, kept for A/B
@@ -184,9 +185,13 @@ int bcp_set_tuning(bcp_engine *eng, int blocks_per_cu, int vecs_per_thread);
  * "stream_grid" (explicit workgroup count of the streaming kernel; 0 = the
  * default, blocks_per_cu on 15 of every 16 CUs), "desc_grid" (the same for
  * the descriptor kernel), "contiguous_alloc" (1: bcp_dev_alloc requests
- * physically contiguous memory for buffers of 64 MiB and more; default 0). */
+ * physically contiguous memory for buffers of 64 MiB and more; default 0),
+ * "table_host_max" / "desc_table_host_max" (bytes: staged descriptor tables
+ * up to this size are read by the kernels from pinned host memory instead of
+ * being copied to the device first; defaults 4096 / 131072). */
 int bcp_set_option(bcp_engine *eng, const char *key, int value);
-/* Current value of a named knob (same keys). */
+/* Current value of a named knob (same keys; "last_stream_vecs": the
+ * vecs_per_thread of the engine's latest streaming-kernel launch). */
 int bcp_get_option(bcp_engine *eng, const char *key, int *value);
 /* Timer slots for bcp_queue_mark / bcp_queue_elapsed_ms. */
 #define BCP_TIMER_SLOTS 64

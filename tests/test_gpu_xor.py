@@ -210,6 +210,47 @@ def test_strided_byte_tail(oracle, engine, dev, queue, vecs, chunk, nsrc):
         assert (out[s, chunk:] == 0xA5).all(), s
 
 
+@pytest.mark.parametrize("nstripes,want_u", [(1, 2), (2, 2), (16, 4), (128, 4), (256, 8)])
+def test_auto_tile_size_by_batch(engine, dev, queue, nstripes, want_u):
+    """Default tuning (vecs_per_thread 0): the streaming kernel's tile size is
+    chosen per launch from the batch's tile count (U = 2 / 4 / 8 for 8 x
+    512 KiB stripes at 15/16 of 256 CUs), strided and pointer-table forms
+    alike, and every choice is bit-exact (checked on the device against a
+    per-stripe reference fold by U = 1 launches)."""
+    nsrc, chunk = 8, 512 * KiB
+    assert engine.option("vecs_per_thread") == 0
+    cus, _ = engine.info()
+    if cus != 256:
+        pytest.skip("thresholds checked for 256 CUs")
+    src = dev.alloc(nstripes * nsrc * chunk)
+    queue.fill_synthetic(src, nstripes * nsrc * chunk, seed=nstripes)
+    out = dev.alloc(nstripes * chunk)
+    out_t = dev.alloc(nstripes * chunk)
+    ref = dev.alloc(nstripes * chunk)
+    queue.xor_uniform(out, src, nstripes, nsrc, chunk)
+    queue.sync()
+    assert engine.option("last_stream_vecs") == want_u
+    queue.xor_stripes([(out_t + s * chunk, chunk, s * nsrc, nsrc, 0) for s in range(nstripes)],
+                      [(src + (s * nsrc + k) * chunk, chunk) for s in range(nstripes) for k in range(nsrc)])
+    queue.sync()
+    assert engine.option("last_stream_vecs") == want_u
+    engine.tune(0, 1)
+    try:
+        queue.xor_uniform(ref, src, nstripes, nsrc, chunk)
+        queue.sync()
+        assert engine.option("last_stream_vecs") == 1
+    finally:
+        engine.tune(0, 0)
+    flag = dev.alloc(16)
+    for got in (out, out_t):
+        queue.compare(got, ref, nstripes * chunk, flag)
+        assert int(dev.get(flag, 8).view("<u8")[0]) == 0
+    # sampled stripe against numpy
+    s = nstripes // 2
+    data = dev.get(src + s * nsrc * chunk, nsrc * chunk).reshape(nsrc, chunk)
+    assert np.array_equal(dev.get(out + s * chunk, chunk), np.bitwise_xor.reduce(data, axis=0))
+
+
 @pytest.mark.parametrize("out_len", [1000, 524288 + 9, 65536 - 3])
 def test_uniform_batch_with_byte_tail(oracle, dev, queue, out_len):
     """Rebuild shape with a length that is not a multiple of 16 (aligned
@@ -372,6 +413,44 @@ def test_survey_kats_on_gpu(oracle, dev, queue):
         out = gpu_stripes(dev, queue, [dict(chunks=chunks, out_len=m, window=window)])[0]
         hdr = np.array(k["lens"], dtype="<u8").tobytes()
         assert hashlib.sha256(hdr + out.tobytes()).hexdigest() == k["sha256"], name
+
+
+@pytest.mark.parametrize("host_max", [0, 1 << 24])
+def test_table_residency(oracle, engine, dev, queue, host_max):
+    """Descriptor tables read by the kernels from pinned host memory
+    (table_host_max / desc_table_host_max at 16 MiB) or copied to the device
+    first (0): same bytes for every tile kind -- plain, grouped, partial,
+    wide (12 sources), window replay through the general path (window not a
+    tile multiple) -- and for a uniform batch (pointer-table xor_stream)."""
+    rng = np.random.default_rng(host_max + 5)
+    W = 64 * KiB + 16
+    shapes = [[300000, 70000, 1, 0, 150001, 299999, 65536, 17],
+              [int(x) for x in rng.integers(1, 200000, size=12)],
+              [3 * W + 5, W, W - 1, 17],
+              [524288] * 8]
+    stripes, refs = [], []
+    for i, lens in enumerate(shapes):
+        chunks = [rng.integers(0, 256, size=L, dtype=np.uint8) for L in lens]
+        if i == 2:
+            stripes.append(dict(chunks=chunks, out_len=max(lens), window=W))
+            refs.append(np.frombuffer(oracle.gen_parity_file(chunks, window=W)[8 * len(lens):], dtype=np.uint8))
+        else:
+            stripes.append(dict(chunks=chunks, out_len=max(lens)))
+            refs.append(oracle.xor_padded_np(chunks))
+    uniform = [dict(chunks=[rng.integers(0, 256, size=4096, dtype=np.uint8) for _ in range(8)], out_len=4096)
+               for _ in range(3)]
+    engine.option("table_host_max", host_max)
+    engine.option("desc_table_host_max", host_max)
+    try:
+        outs = gpu_stripes(dev, queue, stripes)
+        outs_u = gpu_stripes(dev, queue, uniform)
+    finally:
+        engine.option("table_host_max", 4096)
+        engine.option("desc_table_host_max", 128 * 1024)
+    for i, (o, r) in enumerate(zip(outs, refs)):
+        assert np.array_equal(o, r), i
+    for o, st in zip(outs_u, uniform):
+        assert np.array_equal(o, oracle.xor_padded_np(st["chunks"]))
 
 
 @pytest.mark.parametrize("lens", [[10485760, 26214405], [26214405, 1, 15 * MiB + 3], [21 * MiB, 0, 10 * MiB + 17]])
