@@ -41,6 +41,12 @@ struct Tuning {
     // the pointer-table xor_stream reads its table once per tile (a win up
     // to ~16 stripes of 8), desc_tiles once per batch (a win up to >= 512).
     int table_host_max = 4096;
+    // Loads in flight per lane (profiles/r01/depth/): register budget of the
+    // strided xor_stream<8,8> in waves per SIMD (0: the compiler's own
+    // target; 5, 6, 7) and the rolling load window of xor_desc<8> (0: every
+    // load of the tile first; 2, 4: PipeShape in bcp_kernels.hip).
+    int stream_wpe = 6;
+    int desc_pipe = 4;
     int desc_table_host_max = 128 * 1024;
 };
 
@@ -184,14 +190,14 @@ struct DescBatch {
 // Streaming fold.  Consumes ntiles + grid counts of a.ctr when a.sched is
 // kSchedQueue; the caller clamps grid to [1, ntiles].
 hipError_t launch_xor_stream(hipStream_t st, int grid, int vecs, bool gather,
-                             const StreamArgs &a);
+                             const StreamArgs &a, int wpe = 0);
 uint32_t stream_tiles_per_stripe(uint64_t chunk_bytes, int vecs);
 // Descriptor batch: desc_tiles (one wave per stripe writes its tile records
 // into b.tiles), then the fold; same work-queue accounting as
 // launch_xor_stream.
 hipError_t launch_desc_tiles(hipStream_t st, const DescBatch &b);
 hipError_t launch_xor_desc(hipStream_t st, int grid, int vecs,
-                           const DescBatch &b);
+                           const DescBatch &b, int pipe = 0);
 hipError_t launch_fill_synthetic(hipStream_t st, int grid, char *dst,
                                  uint64_t bytes, uint64_t seed,
                                  uint64_t byte_offset);

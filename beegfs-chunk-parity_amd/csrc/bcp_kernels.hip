@@ -94,6 +94,52 @@ __device__ __forceinline__ uint32_t tile_vec(uint32_t tin, int u) {
   return tin * (uint32_t)(kBlock * U) + (threadIdx.x >> 6) * (64u * U) + (uint32_t)u * 64u + (threadIdx.x & 63u);
 }
 
+// Rolling load window of the descriptor kernel's covering-source fold
+// (PIPE > 0; engine option desc_pipe, default 4).  Folds G sources x U
+// vectors per lane into acc, issuing the loads as units of H vectors with D
+// units in flight: unit j + D - 1 goes out before unit j is XORed, and
+// sched_barrier keeps the compiler from hoisting every load of the tile
+// above the XORs (which it does when the kernel runs at one wave per SIMD
+// anyway), so (D - 1) * H .. D * H loads per lane are outstanding.  Every
+// load of a tile in flight at once widens the chip's address window and
+// costs HBM rate: PIPE 4 (H = 2, D = 5: 8-10 loads) +1.3 points on config-5
+// shapes, +1.8 on config-2 shapes through xor_desc (profiles/r01/depth/).
+// PIPE 1: H = U, D = 2; 2: H = U/2, D = 3; 3: H = U/2, D = 4; 4: H = U/4,
+// D = 5; 5: H = U/4, D = 7; 6: H = U/4, D = 6.  (The same window in
+// xor_stream measured 2 points below the compiler's own schedule.)
+template <int U, int PIPE>
+struct PipeShape {
+  static constexpr int H = PIPE == 1 ? U : PIPE <= 3 ? (U >= 2 ? U / 2 : 1) : (U >= 4 ? U / 4 : 1);
+  static constexpr int D = PIPE == 1 ? 2 : PIPE == 2 ? 3 : PIPE == 3 ? 4 : PIPE == 4 ? 5 : PIPE == 5 ? 7 : 6;
+};
+
+template <int G, int U, int PIPE, typename V, typename F>
+__device__ __forceinline__ void rolling_fold(v4u (&acc)[U], F base) {
+  constexpr int H = PipeShape<U, PIPE>::H, D = PipeShape<U, PIPE>::D;
+  constexpr int UPS = U / H;  // units per source
+  constexpr int NU = G * UPS;
+  v4u x[D][H];
+#pragma unroll
+  for (int j = 0; j < D - 1 && j < NU; j++) {
+    const glob<V> *p = base(j / UPS);
+#pragma unroll
+    for (int h = 0; h < H; h++) x[j % D][h] = __builtin_nontemporal_load(p + ((j % UPS) * H + h) * 64);
+  }
+#pragma unroll
+  for (int j = 0; j < NU; j++) {
+    if (j + D - 1 < NU) {
+      const int jn = j + D - 1;
+      const glob<V> *p = base(jn / UPS);
+#pragma unroll
+      for (int h = 0; h < H; h++) x[jn % D][h] = __builtin_nontemporal_load(p + ((jn % UPS) * H + h) * 64);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int h = 0; h < H; h++) acc[(j % UPS) * H + h] ^= x[j % D][h];
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
 template <int NSRC, int U, int GATHER, bool PARTIAL>
 __device__ __forceinline__ void stream_tile(const StreamArgs &a, uint32_t t) {
   const uint32_t nsrc = NSRC > 0 ? (uint32_t)NSRC : a.nsrc;
@@ -201,7 +247,7 @@ __device__ __forceinline__ uint32_t queue_grab(unsigned long long *ctr, unsigned
 constexpr int kQueueFull = 0, kQueuePartial = 1, kStatic = 2;
 
 template <int NSRC, int U, int GATHER, int KIND>
-__global__ __launch_bounds__(kBlock) void xor_stream(StreamArgs a) {
+__device__ __forceinline__ void stream_body(const StreamArgs &a) {
   constexpr bool PARTIAL = KIND != kQueueFull;
   if constexpr (KIND == kStatic) {
     // Workgroup b owns tiles [b*T/G, (b+1)*T/G) (the r01 schedule; A/B only).
@@ -224,6 +270,25 @@ __global__ __launch_bounds__(kBlock) void xor_stream(StreamArgs a) {
       t = __builtin_amdgcn_readfirstlane(next[slot]);
     }
   }
+}
+
+template <int NSRC, int U, int GATHER, int KIND>
+__global__ __launch_bounds__(kBlock) void xor_stream(StreamArgs a) {
+  stream_body<NSRC, U, GATHER, KIND>(a);
+}
+
+// The same kernel with a register budget of W waves per SIMD
+// (amdgpu_waves_per_eu; engine option stream_wpe).  The body says "every
+// load of the tile first"; the compiler software-pipelines it into the
+// budget it aims for, so W sets how many loads per lane stay in flight: no
+// budget (its own occupancy target) ~5-9, W = 6 ~14, W = 7 8, W = 1-2 ~43.
+// On config 2, W = 6 is +0.8..1.0 point over no budget in three separate
+// interleaved A/Bs, W = 7 -2.6, W = 5 -1.3, W <= 4 -1.5..-2.5
+// (tools/exp/xor_exp5.hip, profiles/r01/depth/); the pointer-table form
+// (rebuild) measured neutral, so only the strided form takes it.
+template <int NSRC, int U, int GATHER, int KIND, int W>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W, W))) void xor_stream_w(StreamArgs a) {
+  stream_body<NSRC, U, GATHER, KIND>(a);
 }
 
 // ---------------------------------------------------------------------------
@@ -277,8 +342,12 @@ __device__ __forceinline__ void store_tail(glob<unsigned char> *d, uint64_t out_
 // G sources that all cover the tile: every load first, then the XOR tree
 // (the xor_stream pattern).  One base address per source and immediate
 // offsets per vector: a 64-bit address per load would cost 2 VGPRs each.
-template <int G, int U, typename P>
+template <int G, int U, int PIPE = 0, typename P>
 __device__ __forceinline__ void fold_cover(v4u (&acc)[U], P src, uint32_t lane_off) {
+  if constexpr (PIPE > 0 && G > 1) {
+    rolling_fold<G, U, PIPE, v4u_u>(acc, [&](int i) { return gp<const v4u_u>(src[i] + lane_off); });
+    return;
+  }
   v4u x[G][U];
 #pragma unroll
   for (int i = 0; i < G; i++) {
@@ -402,7 +471,7 @@ __device__ __noinline__ void desc_tile_wide(const DescBatch &b, uint32_t stripe,
   }
 }
 
-template <int U>
+template <int U, int PIPE>
 __device__ __forceinline__ void desc_tile(const DescBatch &b, uint32_t t) {
   const_as<DescTile> *r = cst(b.tiles) + t;
   const uint32_t meta = r->meta;
@@ -454,14 +523,14 @@ __device__ __forceinline__ void desc_tile(const DescBatch &b, uint32_t t) {
 #pragma unroll
   for (int u = 0; u < U; u++) acc[u] = zero4();
   switch (nfull) {
-    case 8: fold_cover<8, U>(acc, r->src, lane_off); break;
-    case 7: fold_cover<7, U>(acc, r->src, lane_off); break;
-    case 6: fold_cover<6, U>(acc, r->src, lane_off); break;
-    case 5: fold_cover<5, U>(acc, r->src, lane_off); break;
-    case 4: fold_cover<4, U>(acc, r->src, lane_off); break;
-    case 3: fold_cover<3, U>(acc, r->src, lane_off); break;
-    case 2: fold_cover<2, U>(acc, r->src, lane_off); break;
-    case 1: fold_cover<1, U>(acc, r->src, lane_off); break;
+    case 8: fold_cover<8, U, PIPE>(acc, r->src, lane_off); break;
+    case 7: fold_cover<7, U, PIPE>(acc, r->src, lane_off); break;
+    case 6: fold_cover<6, U, PIPE>(acc, r->src, lane_off); break;
+    case 5: fold_cover<5, U, PIPE>(acc, r->src, lane_off); break;
+    case 4: fold_cover<4, U, PIPE>(acc, r->src, lane_off); break;
+    case 3: fold_cover<3, U, PIPE>(acc, r->src, lane_off); break;
+    case 2: fold_cover<2, U, PIPE>(acc, r->src, lane_off); break;
+    case 1: fold_cover<1, U, PIPE>(acc, r->src, lane_off); break;
     default: break;
   }
   // Sources ending inside the tile: whole vectors below the end as masked
@@ -495,13 +564,13 @@ __device__ __forceinline__ void desc_tile(const DescBatch &b, uint32_t t) {
   }
 }
 
-template <int U>
-__global__ __launch_bounds__(kBlock) void xor_desc(DescBatch b) {
+template <int U, int PIPE>
+__device__ __forceinline__ void desc_body(const DescBatch &b) {
   if (b.sched == kSchedStatic) {
     const uint32_t g = gridDim.x;
     const uint32_t t_begin = (uint32_t)(((uint64_t)blockIdx.x * b.ntiles) / g);
     const uint32_t t_end = (uint32_t)(((uint64_t)(blockIdx.x + 1) * b.ntiles) / g);
-    for (uint32_t t = t_begin; t < t_end; t++) desc_tile<U>(b, t);
+    for (uint32_t t = t_begin; t < t_end; t++) desc_tile<U, PIPE>(b, t);
     return;
   }
   // Work queue in grabs of b.grab consecutive tiles.
@@ -514,12 +583,23 @@ __global__ __launch_bounds__(kBlock) void xor_desc(DescBatch b) {
   while (c < nchunks) {
     const uint32_t t0 = c * b.grab;
     const uint32_t t1 = min(t0 + b.grab, b.ntiles);
-    for (uint32_t t = t0; t < t1; t++) desc_tile<U>(b, t);
+    for (uint32_t t = t0; t < t1; t++) desc_tile<U, PIPE>(b, t);
     slot ^= 1;
     if (threadIdx.x == 0) next[slot] = queue_grab(b.ctr, b.base);
     __syncthreads();
     c = __builtin_amdgcn_readfirstlane(next[slot]);
   }
+}
+
+template <int U>
+__global__ __launch_bounds__(kBlock) void xor_desc(DescBatch b) {
+  desc_body<U, 0>(b);
+}
+
+// Rolling-window load variants (A/B: engine option desc_pipe; fold_cover).
+template <int U, int PIPE>
+__global__ __launch_bounds__(kBlock) void xor_desc_p(DescBatch b) {
+  desc_body<U, PIPE>(b);
 }
 
 // Tile records of a descriptor batch: one wave per stripe, one lane per
@@ -738,6 +818,16 @@ __global__ __launch_bounds__(kBlock) void compare_bytes(const unsigned char *a, 
 // ---------------------------------------------------------------------------
 // Launchers.
 // ---------------------------------------------------------------------------
+template <int NSRC, int U, int GATHER, int W>
+static hipError_t launch_stream_w(hipStream_t st, int grid, const StreamArgs &a) {
+  if (a.vps % (uint32_t)(kBlock * U) != 0 || a.tail != 0)
+    hipLaunchKernelGGL((xor_stream_w<NSRC, U, GATHER, kQueuePartial, W>), dim3(grid), dim3(kBlock), 0, st, a);
+  else
+    hipLaunchKernelGGL((xor_stream_w<NSRC, U, GATHER, kQueueFull, W>), dim3(grid), dim3(kBlock), 0, st, a);
+  return hipGetLastError();
+}
+
+
 template <int NSRC, int U, int GATHER>
 static hipError_t launch_stream_nu(hipStream_t st, int grid, const StreamArgs &a) {
   if (a.vps % (uint32_t)(kBlock * U) != 0 || a.tail != 0)
@@ -777,8 +867,16 @@ uint32_t stream_tiles_per_stripe(uint64_t chunk_bytes, int vecs) {
   return (uint32_t)((vps + tile_v - 1) / tile_v);
 }
 
-hipError_t launch_xor_stream(hipStream_t st, int grid, int vecs, bool gather, const StreamArgs &a) {
+hipError_t launch_xor_stream(hipStream_t st, int grid, int vecs, bool gather, const StreamArgs &a, int wpe) {
   if (a.ntiles == 0) return hipSuccess;
+  if (wpe && !gather && a.nsrc == 8 && vecs == 8 && a.sched == kSchedQueue) {
+    switch (wpe) {
+      case 5: return launch_stream_w<8, 8, 0, 5>(st, grid, a);
+      case 6: return launch_stream_w<8, 8, 0, 6>(st, grid, a);
+      case 7: return launch_stream_w<8, 8, 0, 7>(st, grid, a);
+      default: break;
+    }
+  }
   if (gather) {
     switch (vecs) {
       case 1: return launch_stream_u<1, 1>(st, grid, a);
@@ -802,9 +900,16 @@ hipError_t launch_desc_tiles(hipStream_t st, const DescBatch &b) {
   return hipGetLastError();
 }
 
-hipError_t launch_xor_desc(hipStream_t st, int grid, int vecs, const DescBatch &b) {
+hipError_t launch_xor_desc(hipStream_t st, int grid, int vecs, const DescBatch &b, int pipe) {
   if (b.ntiles == 0) return hipSuccess;
   if ((uint32_t)grid > b.ntiles) grid = (int)b.ntiles;
+  if (pipe && vecs == 8) {
+    switch (pipe) {
+      case 2: hipLaunchKernelGGL((xor_desc_p<8, 2>), dim3(grid), dim3(kBlock), 0, st, b); return hipGetLastError();
+      case 4: hipLaunchKernelGGL((xor_desc_p<8, 4>), dim3(grid), dim3(kBlock), 0, st, b); return hipGetLastError();
+      default: break;
+    }
+  }
   switch (vecs) {
     case 1: hipLaunchKernelGGL((xor_desc<1>), dim3(grid), dim3(kBlock), 0, st, b); break;
     case 4: hipLaunchKernelGGL((xor_desc<4>), dim3(grid), dim3(kBlock), 0, st, b); break;

@@ -66,6 +66,8 @@ def parse():
     ap.add_argument("--grab", type=int, default=0, help="tiles per work-queue grab of the descriptor kernel")
     ap.add_argument("--grid", type=int, default=0, help="explicit workgroup count of the streaming kernel (A/B)")
     ap.add_argument("--contig", action="store_true", help="physically contiguous device allocations (A/B knob)")
+    ap.add_argument("--opt", action="append", default=[], metavar="KEY=VALUE",
+                    help="engine option (bcp_set_option) for A/B runs; repeatable")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-stripes", type=int, default=256, help="stripes in the CPU sample pool")
     ap.add_argument("--no-cpu", action="store_true")
@@ -105,6 +107,9 @@ def main():
         eng.option("stream_grid", a.grid)
     if a.contig:
         eng.option("contiguous_alloc", 1)
+    for kv in a.opt:
+        k, v = kv.split("=")
+        eng.option(k, int(v))
     if a.schedule >= 0:
         eng.option("schedule" if a.mode != "mixed" else "desc_schedule", a.schedule)
     cus, devname = eng.info()
@@ -156,8 +161,9 @@ def main():
         bytes_per_step = sum(int(ls.sum()) + int(ls.max()) for ls in lens_all)
         S = len(stripes)
         U = eng.option("desc_vecs_per_thread")
-        kernel = f"xor_desc<{U}>"
-        kernel_tag = f"xor_desc<{U}>"
+        pipe = eng.option("desc_pipe") if U == 8 else 0
+        kernel = f"xor_desc_p<{U},{pipe}>" if pipe else f"xor_desc<{U}>"
+        kernel_tag = f"xor_desc_p<{U}, {pipe}>" if pipe else f"xor_desc<{U}>"
         workload = (f"config5 shapes: {S} stripes x {N} chunks, log-uniform 64 KiB-4 MiB, "
                     f"zero-padded to the stripe max, device-resident")
     elif a.mode == "gen":
@@ -166,6 +172,10 @@ def main():
         bytes_per_step = S * (N + 1) * C
         kernel = "xor_stream<{N},{U},strided>"
         kernel_tag = "xor_stream<{N}, {U}, 0, "
+        wpe = eng.option("stream_wpe")
+        if wpe and N == 8 and a.schedule <= 0:  # register-budget variant (launch_xor_stream)
+            kernel = "xor_stream_w<{N},{U},strided,wpe%d>" % wpe
+            kernel_tag = "xor_stream_w<{N}, {U}, 0, 0, %d>" % wpe
         cfg = "config4" if d.world == 8 and S == 15_625 else "config2"
         workload = f"{cfg}: parity gen, {S} stripes x {N} x {C // KiB} KiB device-resident per GPU"
     else:
@@ -212,6 +222,8 @@ def main():
     kern_ms = q.elapsed_ms(0, 1) / a.steps  # avg launch duration on the kernel's stream
     if a.mode != "mixed":  # tile size the engine chose for the timed launches
         U = eng.option("last_stream_vecs")
+        if U != 8 and "_w<" in kernel:  # the budget variant exists for U = 8 only
+            kernel, kernel_tag = "xor_stream<{N},{U},strided>", "xor_stream<{N}, {U}, 0, "
         kernel, kernel_tag = kernel.format(N=N, U=U), kernel_tag.format(N=N, U=U)
 
     # device-side property check (no oracle here): fold(output) == fold(inputs)

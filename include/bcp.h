@@ -188,7 +188,10 @@ int bcp_set_tuning(bcp_engine *eng, int blocks_per_cu, int vecs_per_thread);
  * physically contiguous memory for buffers of 64 MiB and more; default 0),
  * "table_host_max" / "desc_table_host_max" (bytes: staged descriptor tables
  * up to this size are read by the kernels from pinned host memory instead of
- * being copied to the device first; defaults 4096 / 131072). */
+ * being copied to the device first; defaults 4096 / 131072), "stream_wpe"
+ * (register budget of the 8-source strided streaming kernel in waves per
+ * SIMD: 0 = the compiler's, 5, 6 = default, 7), "desc_pipe" (rolling load
+ * window of the descriptor kernel: 0 = every load first, 2, 4 = default). */
 int bcp_set_option(bcp_engine *eng, const char *key, int value);
 /* Current value of a named knob (same keys; "last_stream_vecs": the
  * vecs_per_thread of the engine's latest streaming-kernel launch). */

@@ -415,6 +415,44 @@ def test_survey_kats_on_gpu(oracle, dev, queue):
         assert hashlib.sha256(hdr + out.tobytes()).hexdigest() == k["sha256"], name
 
 
+@pytest.mark.parametrize("knob,value", [("stream_wpe", w) for w in (0, 5, 6, 7)] +
+                         [("desc_pipe", p) for p in (0, 2, 4)])
+def test_schedule_variants_agree(oracle, engine, dev, queue, knob, value):
+    """A/B kernel variants (register budget of xor_stream<8,8>, rolling load
+    window of xor_desc<8>): same bytes as the oracle on full and partial
+    streaming tiles (strided and pointer table) and on descriptor tiles with
+    1..8 covering sources."""
+    rng = np.random.default_rng(value * 7 + len(knob))
+    nstripes, nsrc = 5, 8
+    default = engine.option(knob)
+    engine.option(knob, value)
+    engine.tune(0, 8)
+    try:
+        res = {}
+        for chunk in (512 * KiB, 512 * KiB + 4096 + 16):
+            data = rng.integers(0, 256, size=nstripes * nsrc * chunk, dtype=np.uint8)
+            src = dev.put(data)
+            dst = dev.alloc(nstripes * chunk)
+            queue.xor_uniform(dst, src, nstripes, nsrc, chunk)
+            ref = np.bitwise_xor.reduce(data.reshape(nstripes, nsrc, chunk), axis=1).reshape(-1)
+            assert np.array_equal(dev.get(dst, nstripes * chunk), ref), chunk
+            # pointer-table form (uniform descriptor batch)
+            dst2 = dev.alloc(nstripes * chunk)
+            queue.xor_stripes([(dst2 + s * chunk, chunk, s * nsrc, nsrc, 0) for s in range(nstripes)],
+                              [(src + (s * nsrc + k) * chunk, chunk) for s in range(nstripes) for k in range(nsrc)])
+            assert np.array_equal(dev.get(dst2, nstripes * chunk), ref), chunk
+        shapes = [[300000] * 8, [300000] * 7 + [5], [200000, 150000, 140000, 70000, 66000, 65536, 1, 0],
+                  [int(x) for x in rng.integers(1, 300000, size=8)], [131072, 131072, 40000]]
+        stripes = [dict(chunks=[rng.integers(0, 256, size=L, dtype=np.uint8) for L in lens], out_len=max(lens))
+                   for lens in shapes]
+        outs = gpu_stripes(dev, queue, stripes)
+    finally:
+        engine.option(knob, default)
+        engine.tune(0, 0)
+    for o, st in zip(outs, stripes):
+        assert np.array_equal(o, oracle.xor_padded_np(st["chunks"]))
+
+
 @pytest.mark.parametrize("host_max", [0, 1 << 24])
 def test_table_residency(oracle, engine, dev, queue, host_max):
     """Descriptor tables read by the kernels from pinned host memory

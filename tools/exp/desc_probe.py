@@ -35,6 +35,8 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--reps", type=int, default=5)
 ap.add_argument("--tunings", default="8:2,8:1,8:3,4:2")
 ap.add_argument("--workloads", default="uniform_forced,uniform_desc,mixed,mixed_equal,mixed_big")
+ap.add_argument("--pipes", default="0", help="engine desc_pipe values to time (rolling load window)")
+ap.add_argument("--rounds", type=int, default=1, help="repeat the whole sweep (interleaved A/B)")
 a = ap.parse_args()
 
 eng = bcp.Engine(0)
@@ -92,12 +94,13 @@ def out_bytes(lens_all):
 
 
 L = bcp.lib()
-for kind in a.workloads.split(","):
+for rnd, kind in [(r, k) for r in range(a.rounds) for k in a.workloads.split(",")]:
     eng.option("desc_force", 1 if kind == "uniform_forced" else 0)
     lens_all = shapes(kind, np.random.default_rng(3))
     out = eng.alloc(out_bytes(lens_all))
     st, so, nbytes = build(lens_all, out)
-    for tun in a.tunings.split(","):
+    for tun, pipe in [(t, int(p)) for t in a.tunings.split(",") for p in a.pipes.split(",")]:
+        eng.option("desc_pipe", pipe)
         parts = [int(x) for x in tun.split(":")]
         u, bpc = parts[0], parts[1]
         grid = parts[2] if len(parts) > 2 else 0
@@ -118,7 +121,7 @@ for kind in a.workloads.split(","):
         q.sync()
         ms = q.elapsed_ms(0, 1) / a.reps
         tiles = sum((int(ls.max()) + 4096 * u - 1) // (4096 * u) for ls in lens_all)
-        print(json.dumps({"workload": kind, "vecs": u, "blocks_per_cu": bpc, "grid": grid, "stripes": len(st),
+        print(json.dumps({"workload": kind, "round": rnd, "pipe": pipe, "vecs": u, "blocks_per_cu": bpc, "grid": grid, "stripes": len(st),
                           "subtiles": tiles, "bytes_per_subtile": round(nbytes / tiles), "kernel_ms": round(ms, 4),
                           "GBps": round(nbytes / ms / 1e6, 1), "frac_8TBs": round(nbytes / ms / 8e9, 4)}),
               flush=True)
