@@ -275,7 +275,8 @@ extern "C" int bcp_set_option(bcp_engine *eng, const char *key, int value) {
   else if (!strcmp(key, "contiguous_alloc") && (value == 0 || value == 1)) eng->tuning.contiguous_alloc = value;
   else if (!strcmp(key, "table_host_max") && value >= 0 && value <= (1 << 24)) eng->tuning.table_host_max = value;
   else if (!strcmp(key, "stream_wpe") && (value == 0 || (value >= 5 && value <= 7))) eng->tuning.stream_wpe = value;
-  else if (!strcmp(key, "desc_pipe") && (value == 0 || value == 2 || value == 4)) eng->tuning.desc_pipe = value;
+  else if (!strcmp(key, "desc_pipe") && (value == 0 || value == 2 || value == 4 || value == 5))
+    eng->tuning.desc_pipe = value;
   else if (!strcmp(key, "desc_table_host_max") && value >= 0 && value <= (1 << 24))
     eng->tuning.desc_table_host_max = value;
   else rc = -EINVAL;

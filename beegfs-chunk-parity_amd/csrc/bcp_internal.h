@@ -44,9 +44,9 @@ struct Tuning {
     // Loads in flight per lane (profiles/r01/depth/): register budget of the
     // strided xor_stream<8,8> in waves per SIMD (0: the compiler's own
     // target; 5, 6, 7) and the rolling load window of xor_desc<8> (0: every
-    // load of the tile first; 2, 4: PipeShape in bcp_kernels.hip).
+    // load of the tile first; 2, 4, 5: PipeShape in bcp_kernels.hip).
     int stream_wpe = 6;
-    int desc_pipe = 4;
+    int desc_pipe = 5;
     int desc_table_host_max = 128 * 1024;
 };
 

@@ -103,14 +103,19 @@ __device__ __forceinline__ uint32_t tile_vec(uint32_t tin, int u) {
 // anyway), so (D - 1) * H .. D * H loads per lane are outstanding.  Every
 // load of a tile in flight at once widens the chip's address window and
 // costs HBM rate: PIPE 4 (H = 2, D = 5: 8-10 loads) +1.3 points on config-5
-// shapes, +1.8 on config-2 shapes through xor_desc (profiles/r01/depth/).
+// shapes, +1.8 on config-2 shapes through xor_desc; PIPE 5 (the default)
+// also windows tiles with more than 8 sources: 16-wide stripes 69 -> 81 %
+// (profiles/r01/depth/).
 // PIPE 1: H = U, D = 2; 2: H = U/2, D = 3; 3: H = U/2, D = 4; 4: H = U/4,
-// D = 5; 5: H = U/4, D = 7; 6: H = U/4, D = 6.  (The same window in
-// xor_stream measured 2 points below the compiler's own schedule.)
+// D = 5; 5: as 4, and tiles with more than 8 sources (desc_tile_wide)
+// through the window too.  (Grouped tiles keep all their <= 32 loads in
+// flight: a window there cost 1.4 points, depth/ab3_group_window_probe.jsonl;
+// the same window in xor_stream measured 2 points below the compiler's own
+// schedule.)
 template <int U, int PIPE>
 struct PipeShape {
   static constexpr int H = PIPE == 1 ? U : PIPE <= 3 ? (U >= 2 ? U / 2 : 1) : (U >= 4 ? U / 4 : 1);
-  static constexpr int D = PIPE == 1 ? 2 : PIPE == 2 ? 3 : PIPE == 3 ? 4 : PIPE == 4 ? 5 : PIPE == 5 ? 7 : 6;
+  static constexpr int D = PIPE == 1 ? 2 : PIPE == 2 ? 3 : PIPE == 3 ? 4 : 5;
 };
 
 template <int G, int U, int PIPE, typename V, typename F>
@@ -430,9 +435,10 @@ struct RunAt {
 // staged run (sorted longest first: [0, nfull) cover, [nfull, nany) end
 // inside): covering sources eight at a time through fold_cover, then the
 // partial ones, as in the plain path.
-template <int U>
+template <int U, int PIPE>
 __device__ __noinline__ void desc_tile_wide(const DescBatch &b, uint32_t stripe, uint32_t sub, uint32_t first_src,
                                             uint32_t nfull, uint32_t nany) {
+  constexpr int WP = PIPE >= 5 ? 4 : 0;
   const_as<bcp_stripe> *dp_ = cst(b.stripes) + stripe;
   const_as<bcp_source> *srcs = cst(b.sources) + first_src;
   const uint64_t tile_off = (uint64_t)sub * b.tile_bytes;
@@ -441,16 +447,16 @@ __device__ __noinline__ void desc_tile_wide(const DescBatch &b, uint32_t stripe,
 #pragma unroll
   for (int u = 0; u < U; u++) acc[u] = zero4();
   uint32_t k = 0;
-  for (; k + 8 <= nfull; k += 8) fold_cover<8, U>(acc, RunAt{srcs + k, tile_off}, lane_off);
+  for (; k + 8 <= nfull; k += 8) fold_cover<8, U, WP>(acc, RunAt{srcs + k, tile_off}, lane_off);
   const RunAt rest{srcs + k, tile_off};
   switch (nfull - k) {
-    case 7: fold_cover<7, U>(acc, rest, lane_off); break;
-    case 6: fold_cover<6, U>(acc, rest, lane_off); break;
-    case 5: fold_cover<5, U>(acc, rest, lane_off); break;
-    case 4: fold_cover<4, U>(acc, rest, lane_off); break;
-    case 3: fold_cover<3, U>(acc, rest, lane_off); break;
-    case 2: fold_cover<2, U>(acc, rest, lane_off); break;
-    case 1: fold_cover<1, U>(acc, rest, lane_off); break;
+    case 7: fold_cover<7, U, WP>(acc, rest, lane_off); break;
+    case 6: fold_cover<6, U, WP>(acc, rest, lane_off); break;
+    case 5: fold_cover<5, U, WP>(acc, rest, lane_off); break;
+    case 4: fold_cover<4, U, WP>(acc, rest, lane_off); break;
+    case 3: fold_cover<3, U, WP>(acc, rest, lane_off); break;
+    case 2: fold_cover<2, U, WP>(acc, rest, lane_off); break;
+    case 1: fold_cover<1, U, WP>(acc, rest, lane_off); break;
     default: break;
   }
   for (k = nfull; k < nany; k++) {
@@ -477,7 +483,7 @@ __device__ __forceinline__ void desc_tile(const DescBatch &b, uint32_t t) {
   const uint32_t meta = r->meta;
   if (meta & kTileGeneral) {
     if (meta & kTileWide)
-      desc_tile_wide<U>(b, r->src_bytes[0], r->src_bytes[1], r->src_bytes[2], meta & 0xFFu, (meta >> 8) & 0xFFu);
+      desc_tile_wide<U, PIPE>(b, r->src_bytes[0], r->src_bytes[1], r->src_bytes[2], meta & 0xFFu, (meta >> 8) & 0xFFu);
     else
       desc_tile_general<U>(b, r->src_bytes[0], r->src_bytes[1], r->src_bytes[2]);
     return;
@@ -907,6 +913,7 @@ hipError_t launch_xor_desc(hipStream_t st, int grid, int vecs, const DescBatch &
     switch (pipe) {
       case 2: hipLaunchKernelGGL((xor_desc_p<8, 2>), dim3(grid), dim3(kBlock), 0, st, b); return hipGetLastError();
       case 4: hipLaunchKernelGGL((xor_desc_p<8, 4>), dim3(grid), dim3(kBlock), 0, st, b); return hipGetLastError();
+      case 5: hipLaunchKernelGGL((xor_desc_p<8, 5>), dim3(grid), dim3(kBlock), 0, st, b); return hipGetLastError();
       default: break;
     }
   }

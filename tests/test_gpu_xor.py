@@ -416,7 +416,7 @@ def test_survey_kats_on_gpu(oracle, dev, queue):
 
 
 @pytest.mark.parametrize("knob,value", [("stream_wpe", w) for w in (0, 5, 6, 7)] +
-                         [("desc_pipe", p) for p in (0, 2, 4)])
+                         [("desc_pipe", p) for p in (0, 2, 4, 5)])
 def test_schedule_variants_agree(oracle, engine, dev, queue, knob, value):
     """A/B kernel variants (register budget of xor_stream<8,8>, rolling load
     window of xor_desc<8>): same bytes as the oracle on full and partial
