@@ -138,12 +138,15 @@ static bool stream_vecs_ok(int v) { return v == 1 || v == 2 || v == 4 || v == 8;
 // tile halves that tail.  Thresholds from tools/batch_curve.py
 // (profiles/r01/batch_tune.jsonl, 8 x 512 KiB stripes): U = 2 for 1-2
 // stripes (-38 %), U = 4 up to 128 stripes (-3..-25 %), U = 8 from 256.
-static int stream_vecs(const bcp_engine *e, uint64_t chunk_bytes, uint64_t nstripes) {
+// Stripes wider than 8 sources take U = 4 (the same ~256 KiB of loads per
+// tile): 16-wide 74-75 -> 87 % of HBM peak, 12-wide level
+// (profiles/r01/depth/ab5_wide_stream_tile_size.jsonl).
+static int stream_vecs(const bcp_engine *e, uint64_t chunk_bytes, uint64_t nstripes, uint32_t nsrc) {
   if (e->tuning.vecs_per_thread) return e->tuning.vecs_per_thread;
   const uint64_t t8 = nstripes * stream_tiles_per_stripe(chunk_bytes, 8);
   const uint64_t g = (uint64_t)grid_for(e);
   if (t8 * 5 < g) return 2;
-  if (t8 < 16 * g) return 4;
+  if (t8 < 16 * g || nsrc > 8) return 4;
   return 8;
 }
 static bool desc_vecs_ok(int v) { return v == 1 || v == 2 || v == 4 || v == 8; }
@@ -605,7 +608,7 @@ static int submit_desc(bcp_queue *q, const bcp_stripe *stripes, uint32_t nstripe
   if (ntiles > 0xFFFFFFF0ull) return -EINVAL;
   if (!e->tuning.desc_force && uniform_batch(stripes, nstripes, sources)) {
     const uint64_t len = stripes[0].out_len;
-    const int sv = stream_vecs(e, len, nstripes);
+    const int sv = stream_vecs(e, len, nstripes, stripes[0].nsrc);
     const uint32_t tps = stream_tiles_per_stripe(len, sv);
     const size_t off_src = ((size_t)nstripes * sizeof(bcp_stripe) + 15) & ~(size_t)15;
     const size_t bytes = off_src + (size_t)nsources * sizeof(bcp_source);
@@ -740,7 +743,7 @@ extern "C" int bcp_xor_strided_async(bcp_queue *q, void *dst, uint64_t dst_strid
     a.src_stride = src_stride;
     a.vps = (uint32_t)(chunk_bytes / 16);
     a.tail = (uint32_t)(chunk_bytes % 16);
-    const int sv = stream_vecs(e, chunk_bytes, nstripes);
+    const int sv = stream_vecs(e, chunk_bytes, nstripes, nsrc);
     a.tps = stream_tiles_per_stripe(chunk_bytes, sv);
     a.nsrc = nsrc;
     return launch_stream(q, false, sv, a, nstripes * a.tps);

@@ -210,14 +210,16 @@ def test_strided_byte_tail(oracle, engine, dev, queue, vecs, chunk, nsrc):
         assert (out[s, chunk:] == 0xA5).all(), s
 
 
-@pytest.mark.parametrize("nstripes,want_u", [(1, 2), (2, 2), (16, 4), (128, 4), (256, 8)])
-def test_auto_tile_size_by_batch(engine, dev, queue, nstripes, want_u):
+@pytest.mark.parametrize("nstripes,want_u,nsrc", [(1, 2, 8), (2, 2, 8), (16, 4, 8), (128, 4, 8), (256, 8, 8),
+                                                  (256, 4, 16), (300, 4, 12)])
+def test_auto_tile_size_by_batch(engine, dev, queue, nstripes, want_u, nsrc):
     """Default tuning (vecs_per_thread 0): the streaming kernel's tile size is
     chosen per launch from the batch's tile count (U = 2 / 4 / 8 for 8 x
     512 KiB stripes at 15/16 of 256 CUs), strided and pointer-table forms
     alike, and every choice is bit-exact (checked on the device against a
-    per-stripe reference fold by U = 1 launches)."""
-    nsrc, chunk = 8, 512 * KiB
+    per-stripe reference fold by U = 1 launches).  Stripes wider than 8
+    sources take U = 4."""
+    chunk = 512 * KiB
     assert engine.option("vecs_per_thread") == 0
     cus, _ = engine.info()
     if cus != 256:
