@@ -278,6 +278,7 @@ extern "C" int bcp_set_option(bcp_engine *eng, const char *key, int value) {
   else if (!strcmp(key, "contiguous_alloc") && (value == 0 || value == 1)) eng->tuning.contiguous_alloc = value;
   else if (!strcmp(key, "table_host_max") && value >= 0 && value <= (1 << 24)) eng->tuning.table_host_max = value;
   else if (!strcmp(key, "stream_wpe") && (value == 0 || (value >= 5 && value <= 7))) eng->tuning.stream_wpe = value;
+  else if (!strcmp(key, "table_wpe") && (value == 0 || (value >= 5 && value <= 7))) eng->tuning.table_wpe = value;
   else if (!strcmp(key, "desc_pipe") && (value == 0 || value == 2 || value == 4 || value == 5))
     eng->tuning.desc_pipe = value;
   else if (!strcmp(key, "desc_table_host_max") && value >= 0 && value <= (1 << 24))
@@ -305,6 +306,7 @@ extern "C" int bcp_get_option(bcp_engine *eng, const char *key, int *value) {
   else if (!strcmp(key, "contiguous_alloc")) *value = t.contiguous_alloc;
   else if (!strcmp(key, "table_host_max")) *value = t.table_host_max;
   else if (!strcmp(key, "stream_wpe")) *value = t.stream_wpe;
+  else if (!strcmp(key, "table_wpe")) *value = t.table_wpe;
   else if (!strcmp(key, "desc_pipe")) *value = t.desc_pipe;
   else if (!strcmp(key, "desc_table_host_max")) *value = t.desc_table_host_max;
   else if (!strcmp(key, "last_stream_vecs")) *value = eng->last_stream_vecs.load(std::memory_order_relaxed);
@@ -556,7 +558,7 @@ static int launch_stream(bcp_queue *q, bool gather, int vecs, StreamArgs a, uint
   a.base = q->qbase;
   int grid = grid_for(e);
   if ((uint64_t)grid > ntiles) grid = (int)ntiles;
-  HIP_RC(launch_xor_stream(q->stream, grid, vecs, gather, a, e->tuning.stream_wpe));
+  HIP_RC(launch_xor_stream(q->stream, grid, vecs, gather, a, gather ? e->tuning.table_wpe : e->tuning.stream_wpe));
   e->last_stream_vecs.store(vecs, std::memory_order_relaxed);
   if (a.sched == kSchedQueue) q->qbase += ntiles + (uint64_t)grid;
   return 0;

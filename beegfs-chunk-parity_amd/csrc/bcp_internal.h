@@ -41,11 +41,12 @@ struct Tuning {
     // the pointer-table xor_stream reads its table once per tile (a win up
     // to ~16 stripes of 8), desc_tiles once per batch (a win up to >= 512).
     int table_host_max = 4096;
-    // Loads in flight per lane (profiles/r01/depth/): register budget of the
-    // strided xor_stream<8,8> in waves per SIMD (0: the compiler's own
-    // target; 5, 6, 7) and the rolling load window of xor_desc<8> (0: every
+    // Loads in flight per lane (profiles/r01/depth/): register budget of
+    // xor_stream<8,8> in waves per SIMD (0: the compiler's own target; 5,
+    // 6, 7; same-allocation A/B: gen +0.8, rebuild +0.1 point at 6) and the rolling load window of xor_desc<8> (0: every
     // load of the tile first; 2, 4, 5: PipeShape in bcp_kernels.hip).
-    int stream_wpe = 6;
+    int stream_wpe = 6;         // strided form (config-2 gen)
+    int table_wpe = 6;          // pointer-table form (rebuild)
     int desc_pipe = 5;
     int desc_table_host_max = 128 * 1024;
 };

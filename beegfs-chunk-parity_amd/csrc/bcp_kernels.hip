@@ -875,11 +875,11 @@ uint32_t stream_tiles_per_stripe(uint64_t chunk_bytes, int vecs) {
 
 hipError_t launch_xor_stream(hipStream_t st, int grid, int vecs, bool gather, const StreamArgs &a, int wpe) {
   if (a.ntiles == 0) return hipSuccess;
-  if (wpe && !gather && a.nsrc == 8 && vecs == 8 && a.sched == kSchedQueue) {
+  if (wpe && a.nsrc == 8 && vecs == 8 && a.sched == kSchedQueue) {
     switch (wpe) {
-      case 5: return launch_stream_w<8, 8, 0, 5>(st, grid, a);
-      case 6: return launch_stream_w<8, 8, 0, 6>(st, grid, a);
-      case 7: return launch_stream_w<8, 8, 0, 7>(st, grid, a);
+      case 5: return gather ? launch_stream_w<8, 8, 1, 5>(st, grid, a) : launch_stream_w<8, 8, 0, 5>(st, grid, a);
+      case 6: return gather ? launch_stream_w<8, 8, 1, 6>(st, grid, a) : launch_stream_w<8, 8, 0, 6>(st, grid, a);
+      case 7: return gather ? launch_stream_w<8, 8, 1, 7>(st, grid, a) : launch_stream_w<8, 8, 0, 7>(st, grid, a);
       default: break;
     }
   }

@@ -417,7 +417,7 @@ def test_survey_kats_on_gpu(oracle, dev, queue):
         assert hashlib.sha256(hdr + out.tobytes()).hexdigest() == k["sha256"], name
 
 
-@pytest.mark.parametrize("knob,value", [("stream_wpe", w) for w in (0, 5, 6, 7)] +
+@pytest.mark.parametrize("knob,value", [("stream_wpe", w) for w in (0, 5, 6, 7)] + [("table_wpe", w) for w in (5, 6, 7)] +
                          [("desc_pipe", p) for p in (0, 2, 4, 5)])
 def test_schedule_variants_agree(oracle, engine, dev, queue, knob, value):
     """A/B kernel variants (register budget of xor_stream<8,8>, rolling load
