@@ -592,8 +592,10 @@ static int submit_desc(bcp_queue *q, const bcp_stripe *stripes, uint32_t nstripe
   // Validate, count tiles and the bytes they move (padding is not read).
   uint64_t ntiles = 0;
   double moved = 0;
+  bool plain = true;  // no tile takes the general / wide path (those read the tables per tile)
   for (uint32_t i = 0; i < nstripes; i++) {
     const bcp_stripe &s = stripes[i];
+    plain = plain && s.window == 0 && s.nsrc <= (uint32_t)kTileSrcs;
     if ((uint64_t)s.first_src + s.nsrc > nsources) return -EINVAL;
     if (s.nsrc > BCP_MAX_SOURCES) return -EINVAL;
     if (s.out_len && !s.dst) return -EINVAL;
@@ -692,7 +694,9 @@ static int submit_desc(bcp_queue *q, const bcp_stripe *stripes, uint32_t nstripe
     q->tiles_cap = cap;
   }
   char *d = nullptr;
-  if ((rc = stage_tables(q, slot, bytes, (size_t)e->tuning.desc_table_host_max, &d))) return rc;
+  // Host-resident tables only when desc_tiles alone reads them: the general
+  // and wide tile paths read them again per tile.
+  if ((rc = stage_tables(q, slot, bytes, plain ? (size_t)e->tuning.desc_table_host_max : 0, &d))) return rc;
   DescBatch b;
   b.stripes = (const bcp_stripe *)d;
   b.sources = (const bcp_source *)(d + off_src);
