@@ -110,22 +110,17 @@ static int grid_for(const bcp_engine *e) {
   return g > 0 ? g : 240;
 }
 
-// Workgroups per CU of the descriptor kernel.  Auto (0): tiles that move
-// close to a full 8-source tile's bytes run best at one workgroup per CU (the
-// narrowest queue window, as xor_stream); sparsely covered tiles (config-5
-// shapes: ~0.43 of a full tile on average) need a second workgroup per CU to
-// keep enough loads in flight (tools/exp/desc_probe.py, profiles/r01/mixed/).
-static int desc_grid_for(const bcp_engine *e, double bytes_per_tile, uint32_t tile_bytes) {
+// Workgroups of the descriptor kernel.  Auto (desc_blocks_per_cu 0): one
+// per CU on every CU.  With the rolling load window (desc_pipe) that is the
+// best grid for every non-uniform shape measured -- config-5 shapes +1.3
+// points over the earlier 2 per CU, 1-4 MiB mixed +0.4, equal-length mixed
+// +0.5 over 15/16 of the CUs, 16-wide +0.8 (tools/exp/desc_probe.py,
+// profiles/r01/depth/ab10_desc_grid.jsonl, ab11_desc_grid_fine.jsonl).
+// Uniform stripes would prefer 29/32 of the CUs, but they take xor_stream.
+static int desc_grid_for(const bcp_engine *e) {
   if (e->tuning.desc_grid > 0) return e->tuning.desc_grid;
-  int bpc = e->tuning.desc_blocks_per_cu;
-  if (bpc <= 0) {
-    // dense tiles: the streaming kernel's grid, one workgroup on 15 of
-    // every 16 CUs (+1 point here too); sparse tiles: a full 2 per CU
-    // (profiles/r01/mixed/desc_grid.jsonl)
-    if (bytes_per_tile >= 0.6 * (double)(kTileSrcs + 1) * tile_bytes) return std::max(1, e->num_cus * 15 / 16);
-    bpc = 2;
-  }
-  int g = e->num_cus * bpc;
+  const int bpc = e->tuning.desc_blocks_per_cu > 0 ? e->tuning.desc_blocks_per_cu : 1;
+  const int g = e->num_cus * bpc;
   return g > 0 ? g : 256;
 }
 
@@ -591,7 +586,6 @@ static int submit_desc(bcp_queue *q, const bcp_stripe *stripes, uint32_t nstripe
   const uint32_t tile_bytes = desc_tile_bytes(vecs);
   // Validate, count tiles and the bytes they move (padding is not read).
   uint64_t ntiles = 0;
-  double moved = 0;
   bool plain = true;  // no tile takes the general / wide path (those read the tables per tile)
   for (uint32_t i = 0; i < nstripes; i++) {
     const bcp_stripe &s = stripes[i];
@@ -603,9 +597,7 @@ static int submit_desc(bcp_queue *q, const bcp_stripe *stripes, uint32_t nstripe
     for (uint32_t k = 0; k < s.nsrc; k++) {
       const bcp_source &x = sources[s.first_src + k];
       if (x.len && !x.ptr) return -EINVAL;
-      moved += (double)(x.len < s.out_len ? x.len : s.out_len);
     }
-    moved += (double)s.out_len;
     ntiles += (s.out_len + tile_bytes - 1) / tile_bytes;
   }
   if (ntiles == 0) return 0;
@@ -710,7 +702,7 @@ static int submit_desc(bcp_queue *q, const bcp_stripe *stripes, uint32_t nstripe
   b.ctr = q->qctr;
   b.base = q->qbase;
   const uint32_t nunits = b.sched == kSchedQueue ? (acc + b.grab - 1) / b.grab : acc;
-  int grid = desc_grid_for(e, moved / (double)acc, tile_bytes);
+  int grid = desc_grid_for(e);
   if ((uint32_t)grid > nunits) grid = (int)nunits;
   HIP_RC(launch_desc_tiles(q->stream, b));
   HIP_RC(launch_xor_desc(q->stream, grid, vecs, b, e->tuning.desc_pipe));

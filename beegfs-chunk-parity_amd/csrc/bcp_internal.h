@@ -25,9 +25,9 @@ struct Tuning {
     int blocks_per_cu = 1;      // xor_stream: 256-thread workgroups launched per CU
     int vecs_per_thread = 0;    // xor_stream: 16-byte vectors per lane per tile (1, 2, 4, 8; 0 = by batch size)
     int schedule = kSchedQueue; // xor_stream: kSched*
-    // xor_desc (tools/exp/desc_probe.py, profiles/r01/mixed/): 8 vectors per
-    // lane, one 32 KiB tile per queue grab; workgroups per CU 0 = auto by the
-    // batch's bytes per tile (desc_grid_for).
+    // xor_desc (tools/exp/desc_probe.py, profiles/r01/mixed/, depth/): 8
+    // vectors per lane, one 32 KiB tile per queue grab; workgroups per CU
+    // 0 = auto (desc_grid_for: one per CU).
     int desc_blocks_per_cu = 0;
     int desc_vecs = 8;          // 1, 2, 4, 8
     int desc_grab = 1;          // tiles per work-queue grab

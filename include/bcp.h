@@ -174,8 +174,8 @@ int bcp_queue_elapsed_ms(bcp_queue *q, int slot_from, int slot_to,
 int bcp_set_tuning(bcp_engine *eng, int blocks_per_cu, int vecs_per_thread);
 /* Named knob: "blocks_per_cu" (1..32), "vecs_per_thread" (1,2,4,8; 0 = the
  * default: 8, or 4 / 2 for batches of few tiles) of the uniform streaming
- * kernel; "desc_blocks_per_cu" (0 = chosen per batch from
- * its bytes per tile, the default; 1..32), "desc_vecs_per_thread" (1,2,4,8)
+ * kernel; "desc_blocks_per_cu" (0 = the default, one per CU; 1..32),
+ * "desc_vecs_per_thread" (1,2,4,8)
  * of the descriptor kernel; "schedule" (0 = device-wide tile work queue, the
  * default; 1 = a static contiguous tile range per workgroup, kept for A/B
  * measurements) for the uniform streaming kernel; "desc_schedule" (same
