@@ -101,13 +101,16 @@ static int set_device(bcp_engine *e) {
 }
 
 // Workgroups of the streaming kernel: stream_grid if set, else blocks_per_cu
-// per CU on 15 of every 16 CUs (240 on MI355X): in interleaved A/B runs the
+// per CU on 29 of every 32 CUs (232 on MI355X): in interleaved A/B runs the
 // slightly narrower grid beat a full one by 0.6-0.9 points of HBM peak on
-// config-2 gen and tied on rebuild (profiles/r01/grid_*.jsonl).
+// config-2 gen and tied on rebuild (profiles/r01/grid_*.jsonl: 240 against
+// 256); with the waves_per_eu(6) budget, same-allocation sweeps put the
+// optimum at 228-236 (232: +0.3 / +0.4 over 240 on gen, +0.1 on rebuild;
+// profiles/r01/depth/ab9_grid_wpe6.jsonl, ab12_stream_grid_fine.jsonl).
 static int grid_for(const bcp_engine *e) {
   if (e->tuning.stream_grid > 0) return e->tuning.stream_grid;
-  int g = e->num_cus * e->tuning.blocks_per_cu * 15 / 16;
-  return g > 0 ? g : 240;
+  int g = e->num_cus * e->tuning.blocks_per_cu * 29 / 32;
+  return g > 0 ? g : 232;
 }
 
 // Workgroups of the descriptor kernel.  Auto (desc_blocks_per_cu 0): one

@@ -33,7 +33,7 @@ struct Tuning {
     int desc_grab = 1;          // tiles per work-queue grab
     int desc_schedule = kSchedQueue;
     int desc_force = 0;         // 1: uniform batches take xor_desc too (A/B only)
-    int stream_grid = 0;        // xor_stream: explicit workgroup count (0: 15/16 of CUs x blocks_per_cu)
+    int stream_grid = 0;        // xor_stream: explicit workgroup count (0: 29/32 of CUs x blocks_per_cu)
     int desc_grid = 0;          // xor_desc: explicit workgroup count (0: desc_grid_for)
     int contiguous_alloc = 0;   // 1: bcp_dev_alloc asks for physically contiguous buffers >= 64 MiB
     // Descriptor tables up to this many bytes are read by the kernels from

@@ -183,7 +183,7 @@ int bcp_set_tuning(bcp_engine *eng, int blocks_per_cu, int vecs_per_thread);
  * 1) and "desc_force" (1 = uniform batches take the descriptor kernel too;
  * A/B only) for the descriptor kernel (mixed sizes, windows, unaligned);
  * "stream_grid" (explicit workgroup count of the streaming kernel; 0 = the
- * default, blocks_per_cu on 15 of every 16 CUs), "desc_grid" (the same for
+ * default, blocks_per_cu on 29 of every 32 CUs), "desc_grid" (the same for
  * the descriptor kernel), "contiguous_alloc" (1: bcp_dev_alloc requests
  * physically contiguous memory for buffers of 64 MiB and more; default 0),
  * "table_host_max" / "desc_table_host_max" (bytes: staged descriptor tables
