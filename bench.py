@@ -202,6 +202,10 @@ def main():
         bytes_per_step = S * (N + 1) * C
         kernel = "xor_stream<{N},{U},gather>"
         kernel_tag = "xor_stream<{N}, {U}, 1, "
+        wpe = eng.option("table_wpe")
+        if wpe and N == 8 and a.schedule <= 0:  # register-budget variant (launch_xor_stream)
+            kernel = "xor_stream_w<{N},{U},gather,wpe%d>" % wpe
+            kernel_tag = "xor_stream_w<{N}, {U}, 1, 0, %d>" % wpe
         workload = f"config3: rebuild, {S} stripes x ({N - 1} survivors + parity) x {C // KiB} KiB device-resident"
 
     for _ in range(a.warmup):
@@ -223,7 +227,8 @@ def main():
     if a.mode != "mixed":  # tile size the engine chose for the timed launches
         U = eng.option("last_stream_vecs")
         if U != 8 and "_w<" in kernel:  # the budget variant exists for U = 8 only
-            kernel, kernel_tag = "xor_stream<{N},{U},strided>", "xor_stream<{N}, {U}, 0, "
+            form, g = ("gather", 1) if a.mode == "rebuild" else ("strided", 0)
+            kernel, kernel_tag = "xor_stream<{N},{U},%s>" % form, "xor_stream<{N}, {U}, %d, " % g
         kernel, kernel_tag = kernel.format(N=N, U=U), kernel_tag.format(N=N, U=U)
 
     # device-side property check (no oracle here): fold(output) == fold(inputs)

@@ -49,14 +49,13 @@ L = bcp.lib()
 victim = 3
 
 
-def rebuild_tables(par, out):
+def rebuild_tables(par, out, victim=3, par_first=False):
     stripes, sources = [], []
     for s in range(S):
         first = len(sources)
-        for k in range(N):
-            if k != victim:
-                sources.append(bcp.Source(src + (s * N + k) * C, C))
-        sources.append(bcp.Source(par + s * C, C))
+        run = [bcp.Source(src + (s * N + k) * C, C) for k in range(N) if k != victim]
+        p = bcp.Source(par + s * C, C)
+        sources += [p] + run if par_first else run + [p]
         stripes.append(bcp.Stripe(out + s * C, C, first, N, 0))
     return (bcp.Stripe * S)(*stripes), (bcp.Source * len(sources))(*sources)
 
@@ -80,6 +79,10 @@ for po, oo in offsets:
         continue
     if "gen" in a.modes:
         work["gen"] = lambda: q.xor_uniform(out0, src, S, N, C)
+    if "rebuild_orders" in a.modes:
+        for v, pf in ((7, False), (0, False), (3, True), (7, True)):
+            st_o, so_o = rebuild_tables(par, out0, victim=v, par_first=pf)
+            work[f"rebuild_victim{v}{'_par_first' if pf else ''}"] = (lambda st_o=st_o, so_o=so_o: submit(st_o, so_o))
     if "rebuild_one_alloc" in a.modes:  # parity array in the tail of the source allocation
         par_in = src + S * N * C
         q.xor_uniform(par_in, src, S, N, C)
