@@ -9,6 +9,7 @@
 // scheduler picks moves with it:
 //   amdgpu_waves_per_eu(W, W)  W = 8 (<= 64 VGPRs) ... 2 (<= 256)
 //   amdgpu_num_vgpr(R)
+// Second use: tile size U = 4 / 8 / 16 under the budget.
 //
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -Ibeegfs-chunk-parity_amd/csrc -Iinclude \
 //         tools/exp/xor_exp5.hip -o tools/exp/xor_exp5
@@ -32,6 +33,7 @@
 
 namespace bcp {
 
+template <int U>
 __device__ __forceinline__ void queue_loop(const StreamArgs &a) {
   __shared__ uint32_t next[2];
   if (threadIdx.x == 0) next[0] = queue_grab(a.ctr, a.base);
@@ -39,7 +41,7 @@ __device__ __forceinline__ void queue_loop(const StreamArgs &a) {
   uint32_t t = __builtin_amdgcn_readfirstlane(next[0]);
   int slot = 0;
   while (t < a.ntiles) {
-    stream_tile<8, 8, 0, false>(a, t);
+    stream_tile<8, U, 0, false>(a, t);
     slot ^= 1;
     if (threadIdx.x == 0) next[slot] = queue_grab(a.ctr, a.base);
     __syncthreads();
@@ -47,14 +49,14 @@ __device__ __forceinline__ void queue_loop(const StreamArgs &a) {
   }
 }
 
-#define WPE(w) \
-  __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(w, w))) void xs_w##w(StreamArgs a) { queue_loop(a); }
-WPE(1) WPE(2) WPE(3) WPE(4) WPE(5) WPE(6) WPE(8)
-#undef WPE
-#define NV(r) \
-  __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_vgpr(r))) void xs_v##r(StreamArgs a) { queue_loop(a); }
-NV(40) NV(48) NV(56) NV(96) NV(128) NV(160)
-#undef NV
+template <int U, int W>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W, W))) void xs_uw(StreamArgs a) {
+  queue_loop<U>(a);
+}
+template <int U>
+__global__ __launch_bounds__(kBlock) void xs_u(StreamArgs a) {
+  queue_loop<U>(a);
+}
 
 }  // namespace bcp
 
@@ -62,15 +64,23 @@ typedef void (*KFn)(bcp::StreamArgs);
 struct Entry {
   const char *name;
   KFn fn;
+  int u;
 };
 
+// (The r01 sweep of waves_per_eu 1..8 and amdgpu_num_vgpr at U = 8 is
+// profiles/r01/depth/exp5_wpe_sweep.jsonl; this is the tile-size sweep under
+// the shipped budget.)
 static const Entry kV[] = {
-    {"shipped xor_stream<8,8,0,full>", bcp::xor_stream<8, 8, 0, bcp::kQueueFull>},
-    {"waves_per_eu 8", bcp::xs_w8},   {"waves_per_eu 6", bcp::xs_w6},   {"waves_per_eu 5", bcp::xs_w5},
-    {"waves_per_eu 4", bcp::xs_w4},   {"waves_per_eu 3", bcp::xs_w3},   {"waves_per_eu 2", bcp::xs_w2},
-    {"waves_per_eu 1", bcp::xs_w1},   {"num_vgpr 40", bcp::xs_v40},     {"num_vgpr 48", bcp::xs_v48},
-    {"num_vgpr 56", bcp::xs_v56},     {"num_vgpr 96", bcp::xs_v96},     {"num_vgpr 128", bcp::xs_v128},
-    {"num_vgpr 160", bcp::xs_v160},
+    {"shipped xor_stream_w<8,8,0,full,6>", bcp::xor_stream_w<8, 8, 0, bcp::kQueueFull, 6>, 8},
+    {"U=8 no budget", bcp::xs_u<8>, 8},
+    {"U=16 wpe 6", bcp::xs_uw<16, 6>, 16},
+    {"U=16 wpe 5", bcp::xs_uw<16, 5>, 16},
+    {"U=16 wpe 7", bcp::xs_uw<16, 7>, 16},
+    {"U=16 no budget", bcp::xs_u<16>, 16},
+    {"U=4 wpe 6", bcp::xs_uw<4, 6>, 4},
+    {"U=4 wpe 7", bcp::xs_uw<4, 7>, 4},
+    {"U=4 wpe 5", bcp::xs_uw<4, 5>, 4},
+    {"U=4 no budget", bcp::xs_u<4>, 4},
 };
 
 int main(int argc, char **argv) {
@@ -80,7 +90,7 @@ int main(int argc, char **argv) {
   const uint64_t in_bytes = stripes * N * S, out_bytes = stripes * S;
   hipDeviceProp_t prop;
   CK(hipGetDeviceProperties(&prop, 0));
-  const int grid = prop.multiProcessorCount * 15 / 16;
+  const int grid = prop.multiProcessorCount * 29 / 32;
   char *src, *dst, *ref;
   unsigned long long *ctr, *dcount;
   CK(hipMalloc(&src, in_bytes));
@@ -102,7 +112,7 @@ int main(int argc, char **argv) {
     a.stripe_stride = N * S;
     a.src_stride = S;
     a.vps = (uint32_t)(S / 16);
-    a.tps = (uint32_t)(S / 16 / (256 * 8));
+    a.tps = (uint32_t)(S / 16 / (256 * kV[v].u));
     a.ntiles = (uint32_t)(stripes * a.tps);
     a.nsrc = N;
     a.ctr = ctr;
