@@ -25,6 +25,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--n", type=int, default=3)
 ap.add_argument("--chunk", type=int, default=512 * 1024)
 ap.add_argument("--iters", type=int, default=300)
+ap.add_argument("--vecs", default="", help="comma list: also time the zero-copy mapped fold at these tile sizes")
 a = ap.parse_args()
 
 eng = bcp.Engine(0)
@@ -117,6 +118,10 @@ for i in range(50):
     zero_copy_mapped()
     bad += not np.array_equal(mout, np.bitwise_xor.reduce(mrows.reshape(n, C), axis=0))
 print(json.dumps({"step": "zero_copy_mapped_reuse_50", "mismatching_folds": bad}))
+for v in filter(None, a.vecs.split(",")):
+    eng.tune(0, int(v))
+    timed(f"zero_copy_mapped vecs={v}", zero_copy_mapped)
+eng.tune(0, 0)
 pg_rows = rows.copy()
 pg_out = np.empty(C, dtype=np.uint8)
 timed("bcp_xor_parity(drop-in, pageable)", lambda: bcp.xor_parity(pg_out, C, pg_rows, n))
