@@ -647,3 +647,48 @@ def test_config2_and_config3_full_size(oracle, dev, queue):
     queue.compare(reb, gathered, nstripes * chunk, res)
     bad = int(dev.get(res, 8).view("<u8")[0])
     assert bad == 0
+
+
+# Documented engine knobs (include/bcp.h): defaults, valid values round-trip,
+# invalid values are refused with -EINVAL and leave the knob unchanged.
+KNOBS = {
+    "blocks_per_cu": (1, [1, 2, 32], [0, 33]),
+    "vecs_per_thread": (0, [0, 1, 2, 4, 8], [3, 16]),
+    "desc_blocks_per_cu": (0, [0, 1, 32], [-1, 33]),
+    "desc_vecs_per_thread": (8, [1, 2, 4, 8], [0, 3]),
+    "schedule": (0, [0, 1], [2]),
+    "desc_schedule": (0, [0, 1], [2]),
+    "desc_grab": (1, [1, 64], [0, 65]),
+    "desc_force": (0, [0, 1], [2]),
+    "stream_grid": (0, [0, 1, 65536], [-1, 65537]),
+    "desc_grid": (0, [0, 7], [-1]),
+    "contiguous_alloc": (0, [0, 1], [2]),
+    "table_host_max": (4096, [0, 1 << 24], [-1, (1 << 24) + 1]),
+    "desc_table_host_max": (128 * 1024, [0, 1 << 24], [-1]),
+    "stream_wpe": (6, [0, 5, 6, 7], [1, 4, 8]),
+    "table_wpe": (6, [0, 5, 6, 7], [4, 8]),
+    "desc_pipe": (5, [0, 2, 4, 5], [1, 3, 6]),
+}
+
+
+@pytest.mark.parametrize("key", sorted(KNOBS))
+def test_engine_knobs(bcp, engine, key):
+    default, good, bad = KNOBS[key]
+    assert engine.option(key) == default, key
+    try:
+        for v in good:
+            assert engine.option(key, v) == v
+        for v in bad:
+            with pytest.raises(bcp.BcpError):
+                engine.option(key, v)
+            assert engine.option(key) == good[-1]
+    finally:
+        engine.option(key, default)
+    assert engine.option(key) == default
+
+
+def test_unknown_knob_refused(bcp, engine):
+    with pytest.raises(bcp.BcpError):
+        engine.option("no_such_knob", 1)
+    with pytest.raises(bcp.BcpError):
+        engine.option("no_such_knob")
