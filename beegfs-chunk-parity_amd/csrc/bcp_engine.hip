@@ -129,6 +129,13 @@ static int desc_grid_for(const bcp_engine *e) {
 
 static bool stream_vecs_ok(int v) { return v == 1 || v == 2 || v == 4 || v == 8; }
 
+// Tiles per work-queue grab for stripes of 1-4 sources (auto): two.  One
+// tile per grab leaves N = 1 (a copy) at 62 % of HBM peak and N = 2 at 77 %,
+// bound by the single counter; two per grab 84 / 83 %, N = 3..4 level or
+// +0.5; three or more widen the address window and lose 2-6 points
+// (profiles/r01/depth/ab15_narrow_stripes.jsonl, ab16_narrow_grab.jsonl).
+static uint32_t stream_grab_auto(uint32_t nsrc) { return nsrc >= 1 && nsrc <= 4 ? 2u : 1u; }
+
 // Vectors per lane (tile size) of one xor_stream launch.  Explicit tuning
 // wins; auto (0) keeps U = 8 (32 KiB per source per tile, the large-batch
 // optimum) unless the batch is small: with fewer than ~16 tiles per
@@ -277,6 +284,7 @@ extern "C" int bcp_set_option(bcp_engine *eng, const char *key, int value) {
   else if (!strcmp(key, "table_host_max") && value >= 0 && value <= (1 << 24)) eng->tuning.table_host_max = value;
   else if (!strcmp(key, "stream_wpe") && (value == 0 || (value >= 5 && value <= 7))) eng->tuning.stream_wpe = value;
   else if (!strcmp(key, "table_wpe") && (value == 0 || (value >= 5 && value <= 7))) eng->tuning.table_wpe = value;
+  else if (!strcmp(key, "stream_grab") && value >= 0 && value <= 64) eng->tuning.stream_grab = value;
   else if (!strcmp(key, "desc_pipe") && (value == 0 || value == 2 || value == 4 || value == 5))
     eng->tuning.desc_pipe = value;
   else if (!strcmp(key, "desc_table_host_max") && value >= 0 && value <= (1 << 24))
@@ -306,6 +314,7 @@ extern "C" int bcp_get_option(bcp_engine *eng, const char *key, int *value) {
   else if (!strcmp(key, "stream_wpe")) *value = t.stream_wpe;
   else if (!strcmp(key, "table_wpe")) *value = t.table_wpe;
   else if (!strcmp(key, "desc_pipe")) *value = t.desc_pipe;
+  else if (!strcmp(key, "stream_grab")) *value = t.stream_grab;
   else if (!strcmp(key, "desc_table_host_max")) *value = t.desc_table_host_max;
   else if (!strcmp(key, "last_stream_vecs")) *value = eng->last_stream_vecs.load(std::memory_order_relaxed);
   else rc = -EINVAL;
@@ -554,11 +563,16 @@ static int launch_stream(bcp_queue *q, bool gather, int vecs, StreamArgs a, uint
   a.sched = e->tuning.schedule;
   a.ctr = q->qctr;
   a.base = q->qbase;
+  // Tiles per grab: the kernels for 1-4 sources take several (stream_body).
+  a.grab = 1;
+  if (a.nsrc >= 1 && a.nsrc <= 4 && a.sched == kSchedQueue)
+    a.grab = e->tuning.stream_grab > 0 ? (uint32_t)e->tuning.stream_grab : stream_grab_auto(a.nsrc);
+  const uint64_t nunits = (ntiles + a.grab - 1) / a.grab;
   int grid = grid_for(e);
-  if ((uint64_t)grid > ntiles) grid = (int)ntiles;
+  if ((uint64_t)grid > nunits) grid = (int)nunits;
   HIP_RC(launch_xor_stream(q->stream, grid, vecs, gather, a, gather ? e->tuning.table_wpe : e->tuning.stream_wpe));
   e->last_stream_vecs.store(vecs, std::memory_order_relaxed);
-  if (a.sched == kSchedQueue) q->qbase += ntiles + (uint64_t)grid;
+  if (a.sched == kSchedQueue) q->qbase += nunits + (uint64_t)grid;
   return 0;
 }
 

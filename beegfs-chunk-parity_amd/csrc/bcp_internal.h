@@ -48,6 +48,7 @@ struct Tuning {
     int stream_wpe = 6;         // strided form (config-2 gen)
     int table_wpe = 6;          // pointer-table form (rebuild)
     int desc_pipe = 5;
+    int stream_grab = 0;        // xor_stream, 1-4 sources: tiles per queue grab (0: auto)
     int desc_table_host_max = 128 * 1024;
 };
 
@@ -69,6 +70,7 @@ struct StreamArgs {
     unsigned long long *ctr;    // work-queue counter (per queue)
     unsigned long long base;    // counter value at the start of this launch
     int sched;                  // kSched*
+    uint32_t grab;              // tiles per queue grab (NSRC 1..4 instantiations; others take 1)
 };
 
 // One tile of a descriptor batch, written on the device by desc_tiles.  The

@@ -267,12 +267,29 @@ __device__ __forceinline__ void stream_body(const StreamArgs &a) {
     __syncthreads();
     uint32_t t = __builtin_amdgcn_readfirstlane(next[0]);
     int slot = 0;
-    while (t < a.ntiles) {
-      stream_tile<NSRC, U, GATHER, PARTIAL>(a, t);
-      slot ^= 1;
-      if (threadIdx.x == 0) next[slot] = queue_grab(a.ctr, a.base);
-      __syncthreads();
-      t = __builtin_amdgcn_readfirstlane(next[slot]);
+    if constexpr (NSRC >= 1 && NSRC <= 4) {
+      // Narrow stripes: a.grab consecutive tiles per queue grab (a tile moves
+      // only (NSRC + 1) x 32 KiB at U = 8, and one counter serves ~60-80
+      // grabs per microsecond: at one tile per grab, N = 1..2 are
+      // counter-bound).
+      const uint32_t g = a.grab;
+      const uint32_t nunits = (a.ntiles + g - 1) / g;
+      while (t < nunits) {
+        const uint32_t t0 = t * g, t1 = min(t0 + g, a.ntiles);
+        for (uint32_t x = t0; x < t1; x++) stream_tile<NSRC, U, GATHER, PARTIAL>(a, x);
+        slot ^= 1;
+        if (threadIdx.x == 0) next[slot] = queue_grab(a.ctr, a.base);
+        __syncthreads();
+        t = __builtin_amdgcn_readfirstlane(next[slot]);
+      }
+    } else {
+      while (t < a.ntiles) {
+        stream_tile<NSRC, U, GATHER, PARTIAL>(a, t);
+        slot ^= 1;
+        if (threadIdx.x == 0) next[slot] = queue_grab(a.ctr, a.base);
+        __syncthreads();
+        t = __builtin_amdgcn_readfirstlane(next[slot]);
+      }
     }
   }
 }

@@ -192,7 +192,9 @@ int bcp_set_tuning(bcp_engine *eng, int blocks_per_cu, int vecs_per_thread);
  * (register budget of the 8-source strided streaming kernel in waves per
  * SIMD: 0 = the compiler's, 5, 6 = default, 7), "desc_pipe" (rolling load
  * window of the descriptor kernel: 0 = every load first, 2, 4, 5 = default:
- * 4 and tiles wider than 8 sources windowed too). */
+ * 4 and tiles wider than 8 sources windowed too), "stream_grab" (tiles per
+ * work-queue grab of the streaming kernel for stripes of 1-4 sources, 1..64;
+ * 0 = the default, 2). */
 int bcp_set_option(bcp_engine *eng, const char *key, int value);
 /* Current value of a named knob (same keys; "last_stream_vecs": the
  * vecs_per_thread of the engine's latest streaming-kernel launch). */

@@ -668,6 +668,7 @@ KNOBS = {
     "stream_wpe": (6, [0, 5, 6, 7], [1, 4, 8]),
     "table_wpe": (6, [0, 5, 6, 7], [4, 8]),
     "desc_pipe": (5, [0, 2, 4, 5], [1, 3, 6]),
+    "stream_grab": (0, [0, 1, 64], [-1, 65]),
 }
 
 
@@ -692,3 +693,28 @@ def test_unknown_knob_refused(bcp, engine):
         engine.option("no_such_knob", 1)
     with pytest.raises(bcp.BcpError):
         engine.option("no_such_knob")
+
+
+@pytest.mark.parametrize("grab", [0, 1, 2, 3, 8])
+@pytest.mark.parametrize("nsrc", [1, 2, 3, 4])
+def test_narrow_stripes_multi_tile_grabs(engine, dev, queue, nsrc, grab):
+    """Stripes of 1-4 sources take several tiles per work-queue grab
+    (stream_grab; 0 = auto): every tile folded exactly once, full and
+    partial last tiles, strided and pointer-table forms."""
+    default = engine.option("stream_grab")
+    rng = np.random.default_rng(nsrc * 10 + grab)
+    engine.option("stream_grab", grab)
+    try:
+        for nstripes, chunk in ((37, 512 * KiB), (5, 3 * 32 * KiB + 48), (1, 16)):
+            data = rng.integers(0, 256, size=nstripes * nsrc * chunk, dtype=np.uint8)
+            src = dev.put(data)
+            dst = dev.alloc(nstripes * chunk)
+            queue.xor_uniform(dst, src, nstripes, nsrc, chunk)
+            ref = np.bitwise_xor.reduce(data.reshape(nstripes, nsrc, chunk), axis=1).reshape(-1)
+            assert np.array_equal(dev.get(dst, nstripes * chunk), ref), (nstripes, chunk)
+            dst2 = dev.alloc(nstripes * chunk)
+            queue.xor_stripes([(dst2 + s * chunk, chunk, s * nsrc, nsrc, 0) for s in range(nstripes)],
+                              [(src + (s * nsrc + k) * chunk, chunk) for s in range(nstripes) for k in range(nsrc)])
+            assert np.array_equal(dev.get(dst2, nstripes * chunk), ref), (nstripes, chunk)
+    finally:
+        engine.option("stream_grab", default)
