@@ -892,12 +892,34 @@ uint32_t stream_tiles_per_stripe(uint64_t chunk_bytes, int vecs) {
 
 hipError_t launch_xor_stream(hipStream_t st, int grid, int vecs, bool gather, const StreamArgs &a, int wpe) {
   if (a.ntiles == 0) return hipSuccess;
-  if (wpe && a.nsrc == 8 && vecs == 8 && a.sched == kSchedQueue) {
-    switch (wpe) {
-      case 5: return gather ? launch_stream_w<8, 8, 1, 5>(st, grid, a) : launch_stream_w<8, 8, 0, 5>(st, grid, a);
-      case 6: return gather ? launch_stream_w<8, 8, 1, 6>(st, grid, a) : launch_stream_w<8, 8, 0, 6>(st, grid, a);
-      case 7: return gather ? launch_stream_w<8, 8, 1, 7>(st, grid, a) : launch_stream_w<8, 8, 0, 7>(st, grid, a);
-      default: break;
+  // Register budget (stream_wpe / table_wpe; profiles/r01/depth/ab18_wpe_widths.jsonl):
+  // W = 6 is +0.8 (N = 8), +0.9..+6.6 (N = 5..7 at U = 8) and +1.2..+2.7
+  // (N = 12, 16 at U = 4) on the strided form, but -1.4 / -4.5 at N = 3 / 4,
+  // which keep the compiler's schedule; the pointer-table form has it for
+  // N = 8 (+0.1).  W = 5 / 7 exist for N = 8 as A/B points.
+  if (wpe && a.sched == kSchedQueue) {
+    if (vecs == 8 && a.nsrc == 8) {
+      switch (wpe) {
+        case 5: return gather ? launch_stream_w<8, 8, 1, 5>(st, grid, a) : launch_stream_w<8, 8, 0, 5>(st, grid, a);
+        case 6: return gather ? launch_stream_w<8, 8, 1, 6>(st, grid, a) : launch_stream_w<8, 8, 0, 6>(st, grid, a);
+        case 7: return gather ? launch_stream_w<8, 8, 1, 7>(st, grid, a) : launch_stream_w<8, 8, 0, 7>(st, grid, a);
+        default: break;
+      }
+    }
+    if (wpe == 6 && !gather && vecs == 8) {
+      switch (a.nsrc) {
+        case 5: return launch_stream_w<5, 8, 0, 6>(st, grid, a);
+        case 6: return launch_stream_w<6, 8, 0, 6>(st, grid, a);
+        case 7: return launch_stream_w<7, 8, 0, 6>(st, grid, a);
+        default: break;
+      }
+    }
+    if (wpe == 6 && !gather && vecs == 4) {
+      switch (a.nsrc) {
+        case 12: return launch_stream_w<12, 4, 0, 6>(st, grid, a);
+        case 16: return launch_stream_w<16, 4, 0, 6>(st, grid, a);
+        default: break;
+      }
     }
   }
   if (gather) {

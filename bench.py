@@ -173,9 +173,6 @@ def main():
         kernel = "xor_stream<{N},{U},strided>"
         kernel_tag = "xor_stream<{N}, {U}, 0, "
         wpe = eng.option("stream_wpe")
-        if wpe and N == 8 and a.schedule <= 0:  # register-budget variant (launch_xor_stream)
-            kernel = "xor_stream_w<{N},{U},strided,wpe%d>" % wpe
-            kernel_tag = "xor_stream_w<{N}, {U}, 0, 0, %d>" % wpe
         cfg = "config4" if d.world == 8 and S == 15_625 else "config2"
         workload = f"{cfg}: parity gen, {S} stripes x {N} x {C // KiB} KiB device-resident per GPU"
     else:
@@ -203,9 +200,6 @@ def main():
         kernel = "xor_stream<{N},{U},gather>"
         kernel_tag = "xor_stream<{N}, {U}, 1, "
         wpe = eng.option("table_wpe")
-        if wpe and N == 8 and a.schedule <= 0:  # register-budget variant (launch_xor_stream)
-            kernel = "xor_stream_w<{N},{U},gather,wpe%d>" % wpe
-            kernel_tag = "xor_stream_w<{N}, {U}, 1, 0, %d>" % wpe
         workload = f"config3: rebuild, {S} stripes x ({N - 1} survivors + parity) x {C // KiB} KiB device-resident"
 
     for _ in range(a.warmup):
@@ -226,9 +220,14 @@ def main():
     kern_ms = q.elapsed_ms(0, 1) / a.steps  # avg launch duration on the kernel's stream
     if a.mode != "mixed":  # tile size the engine chose for the timed launches
         U = eng.option("last_stream_vecs")
-        if U != 8 and "_w<" in kernel:  # the budget variant exists for U = 8 only
+        # register-budget instantiations (launch_xor_stream in bcp_kernels.hip)
+        budget = a.schedule <= 0 and wpe and (
+            (N == 8 and U == 8) or (a.mode == "gen" and wpe == 6 and ((5 <= N <= 7 and U == 8) or
+                                                                      (N in (12, 16) and U == 4))))
+        if budget:
             form, g = ("gather", 1) if a.mode == "rebuild" else ("strided", 0)
-            kernel, kernel_tag = "xor_stream<{N},{U},%s>" % form, "xor_stream<{N}, {U}, %d, " % g
+            kernel = "xor_stream_w<{N},{U},%s,wpe%d>" % (form, wpe)
+            kernel_tag = "xor_stream_w<{N}, {U}, %d, 0, %d>" % (g, wpe)
         kernel, kernel_tag = kernel.format(N=N, U=U), kernel_tag.format(N=N, U=U)
 
     # device-side property check (no oracle here): fold(output) == fold(inputs)

@@ -718,3 +718,20 @@ def test_narrow_stripes_multi_tile_grabs(engine, dev, queue, nsrc, grab):
             assert np.array_equal(dev.get(dst2, nstripes * chunk), ref), (nstripes, chunk)
     finally:
         engine.option("stream_grab", default)
+
+
+@pytest.mark.parametrize("nsrc", [5, 6, 7, 12, 16])
+def test_budget_widths_default_tuning(engine, dev, queue, nsrc):
+    """Widths that take the waves_per_eu(6) instantiations by default
+    (5-7 at U = 8, 12 and 16 at U = 4): full and partial tiles, bit-exact."""
+    rng = np.random.default_rng(nsrc)
+    for nstripes, chunk in ((300, 512 * KiB), (7, 5 * 16 * KiB + 32)):
+        data = rng.integers(0, 256, size=nstripes * nsrc * chunk, dtype=np.uint8)
+        src = dev.put(data)
+        dst = dev.alloc(nstripes * chunk)
+        queue.xor_uniform(dst, src, nstripes, nsrc, chunk)
+        queue.sync()
+        if nstripes == 300:
+            assert engine.option("last_stream_vecs") == (8 if nsrc <= 8 else 4)
+        ref = np.bitwise_xor.reduce(data.reshape(nstripes, nsrc, chunk), axis=1).reshape(-1)
+        assert np.array_equal(dev.get(dst, nstripes * chunk), ref), (nstripes, chunk)

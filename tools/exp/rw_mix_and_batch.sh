@@ -10,4 +10,4 @@ for n in 1 2 3 4 6 8 12 16; do
   s=$(( 100000 / n ))
   timeout -k 10 120 python3 bench.py --no-cpu --steps 10 --warmup 2 --nsrc $n --stripes $s >> $out || exit $?
 done
-timeout -k 10 300 python3 tools/batch_curve.py > gpurun_out/batch_curve.jsonl
+[ -n "$SKIP_BATCH" ] || timeout -k 10 300 python3 tools/batch_curve.py > gpurun_out/batch_curve.jsonl
