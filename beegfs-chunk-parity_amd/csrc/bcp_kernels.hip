@@ -893,8 +893,8 @@ uint32_t stream_tiles_per_stripe(uint64_t chunk_bytes, int vecs) {
 hipError_t launch_xor_stream(hipStream_t st, int grid, int vecs, bool gather, const StreamArgs &a, int wpe) {
   if (a.ntiles == 0) return hipSuccess;
   // Register budget (stream_wpe / table_wpe; profiles/r01/depth/ab18_wpe_widths.jsonl):
-  // W = 6 is +0.8 (N = 8), +0.9..+6.6 (N = 5..7 at U = 8) and +1.2..+2.7
-  // (N = 12, 16 at U = 4) on the strided form, but -1.4 / -4.5 at N = 3 / 4,
+  // W = 6 is +0.8 (N = 8), +0.9..+6.6 (N = 5..7 at U = 8) and +0.3..+3.8
+  // (N = 9..12, 16 at U = 4; ab19) on the strided form, but -1.4 / -4.5 at N = 3 / 4,
   // which keep the compiler's schedule; the pointer-table form has it for
   // N = 8 (+0.1).  W = 5 / 7 exist for N = 8 as A/B points.
   if (wpe && a.sched == kSchedQueue) {
@@ -916,6 +916,9 @@ hipError_t launch_xor_stream(hipStream_t st, int grid, int vecs, bool gather, co
     }
     if (wpe == 6 && !gather && vecs == 4) {
       switch (a.nsrc) {
+        case 9: return launch_stream_w<9, 4, 0, 6>(st, grid, a);
+        case 10: return launch_stream_w<10, 4, 0, 6>(st, grid, a);
+        case 11: return launch_stream_w<11, 4, 0, 6>(st, grid, a);
         case 12: return launch_stream_w<12, 4, 0, 6>(st, grid, a);
         case 16: return launch_stream_w<16, 4, 0, 6>(st, grid, a);
         default: break;

@@ -223,12 +223,13 @@ def main():
         # register-budget instantiations (launch_xor_stream in bcp_kernels.hip)
         budget = a.schedule <= 0 and wpe and (
             (N == 8 and U == 8) or (a.mode == "gen" and wpe == 6 and ((5 <= N <= 7 and U == 8) or
-                                                                      (N in (12, 16) and U == 4))))
+                                                                      (N in (9, 10, 11, 12, 16) and U == 4))))
         if budget:
             form, g = ("gather", 1) if a.mode == "rebuild" else ("strided", 0)
             kernel = "xor_stream_w<{N},{U},%s,wpe%d>" % (form, wpe)
             kernel_tag = "xor_stream_w<{N}, {U}, %d, 0, %d>" % (g, wpe)
-        kernel, kernel_tag = kernel.format(N=N, U=U), kernel_tag.format(N=N, U=U)
+        NS = N if (1 <= N <= 12 or N == 16) else 0  # widths without a specialisation run xor_stream<0, ...>
+        kernel, kernel_tag = kernel.format(N=NS, U=U), kernel_tag.format(N=NS, U=U)
 
     # device-side property check (no oracle here): fold(output) == fold(inputs)
     verified = None

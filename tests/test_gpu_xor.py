@@ -720,7 +720,7 @@ def test_narrow_stripes_multi_tile_grabs(engine, dev, queue, nsrc, grab):
         engine.option("stream_grab", default)
 
 
-@pytest.mark.parametrize("nsrc", [5, 6, 7, 12, 16])
+@pytest.mark.parametrize("nsrc", [5, 6, 7, 9, 10, 11, 12, 16])
 def test_budget_widths_default_tuning(engine, dev, queue, nsrc):
     """Widths that take the waves_per_eu(6) instantiations by default
     (5-7 at U = 8, 12 and 16 at U = 4): full and partial tiles, bit-exact."""
