@@ -300,6 +300,9 @@ class Queue:
         addr, n = _host_addr(host, nbytes)
         call("bcp_d2h_async", self.h, _V(addr), _V(dptr), n)
 
+    def d2d(self, dst: int, src: int, nbytes: int):
+        call("bcp_d2d_async", self.h, _V(dst), _V(src), nbytes)
+
     def memset(self, dptr: int, value: int, nbytes: int):
         call("bcp_memset_async", self.h, _V(dptr), value, nbytes)
 

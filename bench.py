@@ -58,6 +58,8 @@ def parse():
     ap.add_argument("--stripes", type=int, default=0,
                     help="stripes per GPU (default: 12,500 = config 2; at 8 GPUs 15,625 = config 4's 1M chunks)")
     ap.add_argument("--nsrc", type=int, default=8)
+    ap.add_argument("--rebuild-layout", choices=["packed", "split"], default="packed",
+                    help="rebuild inputs per stripe: packed as the pipeline stages them, or split over two arrays")
     ap.add_argument("--chunk", type=int, default=512 * KiB)
     ap.add_argument("--blocks-per-cu", type=int, default=0)
     ap.add_argument("--vecs", type=int, default=0)
@@ -177,18 +179,32 @@ def main():
         workload = f"{cfg}: parity gen, {S} stripes x {N} x {C // KiB} KiB device-resident per GPU"
     else:
         # config 3: parity first, then rebuild source index 3 from the other
-        # N-1 chunks + parity body (descriptor kernel; truncation to 512 KiB).
+        # N-1 chunks + parity body.  Layout "packed" (default): each stripe's
+        # inputs staged contiguously as bcp_pipeline_rebuild stages them in its
+        # slab (survivors and the parity body in ascending target order, here
+        # the parity body in the lost chunk's slot); "split": survivors read in
+        # place from the gen source array + parity bodies from a second array.
         par = eng.alloc(S * C)
         q.xor_uniform(par, src, S, N, C)
         victim = min(3, N - 1)
         stripes, sources = [], []
-        for s in range(S):
-            first = len(sources)
-            for k in range(N):
-                if k != victim:
-                    sources.append((src + (s * N + k) * C, C))
-            sources.append((par + s * C, C))
-            stripes.append((out + s * C, C, first, N, 0))
+        if a.rebuild_layout == "packed":
+            rin = eng.alloc(S * N * C)
+            q.d2d(rin, src, S * N * C)
+            q.xor_strided(rin + victim * C, N * C, par, C, C, S, 1, C)  # parity body -> the lost slot
+            for s in range(S):
+                first = len(sources)
+                for k in range(N):
+                    sources.append((rin + (s * N + k) * C, C))
+                stripes.append((out + s * C, C, first, N, 0))
+        else:
+            for s in range(S):
+                first = len(sources)
+                for k in range(N):
+                    if k != victim:
+                        sources.append((src + (s * N + k) * C, C))
+                sources.append((par + s * C, C))
+                stripes.append((out + s * C, C, first, N, 0))
         import ctypes
         st = (bcp.Stripe * len(stripes))(*[bcp.Stripe(*x) for x in stripes])
         so = (bcp.Source * len(sources))(*[bcp.Source(*x) for x in sources])
@@ -200,7 +216,8 @@ def main():
         kernel = "xor_stream<{N},{U},gather>"
         kernel_tag = "xor_stream<{N}, {U}, 1, "
         wpe = eng.option("table_wpe")
-        workload = f"config3: rebuild, {S} stripes x ({N - 1} survivors + parity) x {C // KiB} KiB device-resident"
+        workload = (f"config3: rebuild, {S} stripes x ({N - 1} survivors + parity) x {C // KiB} KiB device-resident, "
+                    f"{a.rebuild_layout} layout")
 
     for _ in range(a.warmup):
         step()
@@ -301,7 +318,8 @@ def main():
     if d.rank == 0:
         value = total_bytes / wall_max / GiB
         achieved = bytes_per_step / (kern_ms_max * 1e-3) / 1e9
-        wkey = f"{a.mode}:{S}x{N}x{C}"
+        mode_key = "rebuild_packed" if (a.mode == "rebuild" and a.rebuild_layout == "packed") else a.mode
+        wkey = f"{mode_key}:{S}x{N}x{C}"
         pmc = pmc_traffic(wkey, kernel_tag)
         line = {
             "metric": METRIC,
