@@ -95,7 +95,7 @@ __device__ __forceinline__ uint32_t tile_vec(uint32_t tin, int u) {
 }
 
 // Rolling load window of the descriptor kernel's covering-source fold
-// (PIPE > 0; engine option desc_pipe, default 4).  Folds G sources x U
+// (PIPE > 0; engine option desc_pipe, default 5).  Folds G sources x U
 // vectors per lane into acc, issuing the loads as units of H vectors with D
 // units in flight: unit j + D - 1 goes out before unit j is XORed, and
 // sched_barrier keeps the compiler from hoisting every load of the tile
@@ -106,6 +106,7 @@ __device__ __forceinline__ uint32_t tile_vec(uint32_t tin, int u) {
 // shapes, +1.8 on config-2 shapes through xor_desc; PIPE 5 (the default)
 // also windows tiles with more than 8 sources: 16-wide stripes 69 -> 81 %
 // (profiles/r01/depth/).
+// Shapes (the engine exposes 2, 4 and 5; 1 and 3 were r01 A/B points):
 // PIPE 1: H = U, D = 2; 2: H = U/2, D = 3; 3: H = U/2, D = 4; 4: H = U/4,
 // D = 5; 5: as 4, and tiles with more than 8 sources (desc_tile_wide)
 // through the window too.  (Grouped tiles keep all their <= 32 loads in
