@@ -895,7 +895,8 @@ hipError_t launch_xor_stream(hipStream_t st, int grid, int vecs, bool gather, co
   if (a.ntiles == 0) return hipSuccess;
   // Register budget (stream_wpe / table_wpe; profiles/r01/depth/ab18_wpe_widths.jsonl):
   // W = 6 is +0.8 (N = 8), +0.9..+6.6 (N = 5..7 at U = 8) and +0.3..+3.8
-  // (N = 9..12, 16 at U = 4; ab19) on the strided form, but -1.4 / -4.5 at N = 3 / 4,
+  // (N = 9..12, 16 at U = 4; ab19) on the strided form, but -1.4 / -4.5 at N = 3 / 4
+  // (W = 5 / 7 there: -1.1 / -1.6 at N = 3, -1.7 / +0.45 at N = 4; ab20),
   // which keep the compiler's schedule; the pointer-table form has it for
   // N = 8 (+0.1).  W = 5 / 7 exist for N = 8 as A/B points.
   if (wpe && a.sched == kSchedQueue) {
