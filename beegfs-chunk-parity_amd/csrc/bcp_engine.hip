@@ -62,6 +62,7 @@ struct bcp_queue {
   DescTile *tiles = nullptr;           // tile records of the descriptor kernel (device)
   size_t tiles_cap = 0;                // in records
   hipStream_t copy_stream = nullptr;   // descriptor-table uploads (created on first use)
+  hipEvent_t sync_ev = nullptr;        // blocking-sync event (sync_mode 1; created on first use)
 };
 
 struct bcp_event {
@@ -249,6 +250,7 @@ extern "C" int bcp_engine_create(int device, bcp_engine **out) {
   if (e->tuning.vecs_per_thread && !stream_vecs_ok(e->tuning.vecs_per_thread))
     e->tuning.vecs_per_thread = defaults.vecs_per_thread;
   if (const char *v = getenv("BCP_SCHEDULE")) e->tuning.schedule = atoi(v) == kSchedStatic ? kSchedStatic : kSchedQueue;
+  if (const char *v = getenv("BCP_SYNC_MODE")) e->tuning.sync_mode = atoi(v) == 1 ? 1 : 0;
   *out = e;
   return 0;
 }
@@ -285,6 +287,7 @@ extern "C" int bcp_set_option(bcp_engine *eng, const char *key, int value) {
   else if (!strcmp(key, "stream_wpe") && (value == 0 || (value >= 5 && value <= 7))) eng->tuning.stream_wpe = value;
   else if (!strcmp(key, "table_wpe") && (value == 0 || (value >= 5 && value <= 7))) eng->tuning.table_wpe = value;
   else if (!strcmp(key, "stream_grab") && value >= 0 && value <= 64) eng->tuning.stream_grab = value;
+  else if (!strcmp(key, "sync_mode") && (value == 0 || value == 1)) eng->tuning.sync_mode = value;
   else if (!strcmp(key, "desc_pipe") && (value == 0 || value == 2 || value == 4 || value == 5))
     eng->tuning.desc_pipe = value;
   else if (!strcmp(key, "desc_table_host_max") && value >= 0 && value <= (1 << 24))
@@ -315,6 +318,7 @@ extern "C" int bcp_get_option(bcp_engine *eng, const char *key, int *value) {
   else if (!strcmp(key, "table_wpe")) *value = t.table_wpe;
   else if (!strcmp(key, "desc_pipe")) *value = t.desc_pipe;
   else if (!strcmp(key, "stream_grab")) *value = t.stream_grab;
+  else if (!strcmp(key, "sync_mode")) *value = t.sync_mode;
   else if (!strcmp(key, "desc_table_host_max")) *value = t.desc_table_host_max;
   else if (!strcmp(key, "last_stream_vecs")) *value = eng->last_stream_vecs.load(std::memory_order_relaxed);
   else rc = -EINVAL;
@@ -375,13 +379,24 @@ extern "C" int bcp_queue_destroy(bcp_queue *q) {
     if (t) (void)hipEventDestroy(t);
   if (q->qctr) (void)hipFree(q->qctr);
   if (q->tiles) (void)hipFree(q->tiles);
+  if (q->sync_ev) (void)hipEventDestroy(q->sync_ev);
   (void)hipStreamDestroy(q->stream);
   delete q;
   return 0;
 }
 
+// sync_mode 0: hipStreamSynchronize (the runtime's spin-then-yield wait);
+// 1: a blocking-sync event, so a waiting host thread sleeps instead of
+// competing for cores with the threads that feed the GPU (the per-task
+// protocol's 12 lanes and their senders on a 16-core share).
 extern "C" int bcp_queue_sync(bcp_queue *q) {
   if (!q) return -EINVAL;
+  if (q->eng->tuning.sync_mode == 1) {
+    if (!q->sync_ev) HIP_RC(hipEventCreateWithFlags(&q->sync_ev, hipEventBlockingSync | hipEventDisableTiming));
+    HIP_RC(hipEventRecord(q->sync_ev, q->stream));
+    HIP_RC(hipEventSynchronize(q->sync_ev));
+    return 0;
+  }
   HIP_RC(hipStreamSynchronize(q->stream));
   return 0;
 }

@@ -49,6 +49,7 @@ struct Tuning {
     int table_wpe = 6;          // pointer-table form (rebuild)
     int desc_pipe = 5;
     int stream_grab = 0;        // xor_stream, 1-4 sources: tiles per queue grab (0: auto)
+    int sync_mode = 0;          // bcp_queue_sync: 0 hipStreamSynchronize, 1 blocking-sync event
     int desc_table_host_max = 128 * 1024;
 };
 

@@ -194,7 +194,8 @@ int bcp_set_tuning(bcp_engine *eng, int blocks_per_cu, int vecs_per_thread);
  * window of the descriptor kernel: 0 = every load first, 2, 4, 5 = default:
  * 4 and tiles wider than 8 sources windowed too), "stream_grab" (tiles per
  * work-queue grab of the streaming kernel for stripes of 1-4 sources, 1..64;
- * 0 = the default, 2). */
+ * 0 = the default, 2), "sync_mode" (bcp_queue_sync: 0 = hipStreamSynchronize,
+ * the default; 1 = wait on a blocking-sync event; env BCP_SYNC_MODE). */
 int bcp_set_option(bcp_engine *eng, const char *key, int value);
 /* Current value of a named knob (same keys; "last_stream_vecs": the
  * vecs_per_thread of the engine's latest streaming-kernel launch). */

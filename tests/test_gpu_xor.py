@@ -669,6 +669,7 @@ KNOBS = {
     "table_wpe": (6, [0, 5, 6, 7], [4, 8]),
     "desc_pipe": (5, [0, 2, 4, 5], [1, 3, 6]),
     "stream_grab": (0, [0, 1, 64], [-1, 65]),
+    "sync_mode": (0, [0, 1], [2]),
 }
 
 

@@ -239,6 +239,31 @@ def config5(a):
     emit(config=5, path=f"pipeline_full_gen({a.ndevices} GPU)", cold_seconds=round(times[0], 3), warm_seconds=round(dt, 3),
          GiBps=round((rd + wr) / dt / GiB, 3), bytes_read=rd, bytes_written=wr, tasks=int(st.tasks), verified=ok,
          bad=bad)
+    # the same full generation through the per-task protocol (12 lanes), GPU
+    # fold against the reference CPU fold: 8 rows of up to 4 MiB per window
+    ol = oracle.lib()
+    for label, hook in (("protocol_gpu_fold(bcp_gen_run,12 lanes)", None),
+                        ("protocol_cpu_fold_reference(oracle_xor_rows,12 lanes)",
+                         ctypes.cast(ol.oracle_xor_rows, ctypes.c_void_p).value)):
+        bcp.set_xor_hook(hook)
+        try:
+            times = []
+            for r in range(1 + a.reps):
+                for k in range(ntargets):
+                    shutil.rmtree(os.path.join(root, f"st{k}", "parity"), ignore_errors=True)
+                    os.makedirs(os.path.join(root, f"st{k}", "parity"))
+                t0 = time.perf_counter()
+                st = bcp.gen_run(root, ntargets, items, nlanes=12)
+                times.append(time.perf_counter() - t0)
+        finally:
+            bcp.set_xor_hook(None)
+        dtp = float(np.median(times[1:])) if a.reps else times[0]
+        okp, badp = verify(root, files, contents, a.verify, rng)
+        ok &= okp
+        emit(config=5, path=label, cold_seconds=round(times[0], 3), warm_seconds=round(dtp, 3),
+             GiBps=round((rd + wr) / dtp / GiB, 3), bytes_read=rd, bytes_written=wr, tasks=int(st.tasks),
+             errors=int(st.errors), verified=okp, bad=badp)
+    bcp.task_shutdown()
     # changelog: a seeded 10 % of stripes rewritten -> record streams per target
     sub = sorted(int(x) for x in rng.choice(len(files), size=max(1, len(files) // 10), replace=False))
     streams = {t: [] for t in range(ntargets)}
