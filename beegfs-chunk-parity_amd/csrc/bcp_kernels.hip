@@ -273,7 +273,7 @@ __device__ __forceinline__ void stream_body(const StreamArgs &a) {
       // only (NSRC + 1) x 32 KiB at U = 8, and one counter serves ~60-80
       // grabs per microsecond: at one tile per grab, N = 1..2 are
       // counter-bound).
-      const uint32_t g = a.grab;
+      const uint32_t g = a.grab ? a.grab : 1u;  // the host always sets >= 1; never divide by 0
       const uint32_t nunits = (a.ntiles + g - 1) / g;
       while (t < nunits) {
         const uint32_t t0 = t * g, t1 = min(t0 + g, a.ntiles);
