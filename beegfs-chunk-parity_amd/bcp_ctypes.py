@@ -76,6 +76,7 @@ _SIGS = {
     "bcp_engine_create": ([ctypes.c_int, ctypes.POINTER(_V)], ctypes.c_int),
     "bcp_engine_destroy": ([_V], ctypes.c_int),
     "bcp_engine_info": ([_V, ctypes.POINTER(ctypes.c_int), ctypes.c_char_p, ctypes.c_size_t], ctypes.c_int),
+    "bcp_engine_pci_bus_id": ([_V, ctypes.c_char_p, ctypes.c_size_t], ctypes.c_int),
     "bcp_queue_create": ([_V, ctypes.POINTER(_V)], ctypes.c_int),
     "bcp_queue_destroy": ([_V], ctypes.c_int),
     "bcp_queue_sync": ([_V], ctypes.c_int),
@@ -218,6 +219,12 @@ class Engine:
         call("bcp_engine_info", self.h, ctypes.byref(cus), name, 256)
         return cus.value, name.value.decode()
 
+    def pci_bus_id(self) -> str:
+        """PCI bus id of the device (distinct per physical GPU)."""
+        buf = ctypes.create_string_buffer(64)
+        call("bcp_engine_pci_bus_id", self.h, buf, 64)
+        return buf.value.decode()
+
     def tune(self, blocks_per_cu: int = 0, vecs_per_thread: int = 0):
         call("bcp_set_tuning", self.h, blocks_per_cu, vecs_per_thread)
 
@@ -297,7 +304,7 @@ class Queue:
         call("bcp_h2d_async", self.h, _V(dptr), _V(addr), n)
 
     def d2h(self, host, dptr: int, nbytes: int | None = None):
-        addr, n = _host_addr(host, nbytes)
+        addr, n = _host_addr(host, nbytes, writable=True)
         call("bcp_d2h_async", self.h, _V(addr), _V(dptr), n)
 
     def d2d(self, dst: int, src: int, nbytes: int):
@@ -343,20 +350,40 @@ class Queue:
             self.h = None
 
 
-def _host_addr(host, nbytes):
+def _host_addr(host, nbytes, writable: bool = False):
+    """(address, nbytes) of a host buffer: numpy array, bytes / bytearray, or an
+    int address (then nbytes is required and trusted).  nbytes may not exceed
+    the buffer; a copy destination (writable) must be a writable buffer."""
     import numpy as np
     if isinstance(host, int):
-        assert nbytes is not None
+        if nbytes is None:
+            raise ValueError("an int host address needs an explicit nbytes")
         return host, nbytes
-    if isinstance(host, (bytes, bytearray)):
+    if isinstance(host, (bytes, bytearray, memoryview)):
+        if writable and (isinstance(host, bytes) or (isinstance(host, memoryview) and host.readonly)):
+            raise ValueError("read-only host buffer as a copy destination")
         arr = np.frombuffer(host, dtype=np.uint8)
-        return arr.ctypes.data, len(host) if nbytes is None else nbytes
-    return host.ctypes.data, host.nbytes if nbytes is None else nbytes
+    elif isinstance(host, np.ndarray):
+        if writable and not host.flags.writeable:
+            raise ValueError("read-only numpy array as a copy destination")
+        if not host.flags.c_contiguous:
+            raise ValueError("host buffer must be C-contiguous")
+        arr = host
+    else:
+        raise TypeError(f"unsupported host buffer {type(host).__name__}")
+    size = arr.nbytes
+    if nbytes is None:
+        nbytes = size
+    if nbytes < 0 or nbytes > size:
+        raise ValueError(f"nbytes {nbytes} outside the {size}-byte host buffer")
+    return arr.ctypes.data, nbytes
 
 
 def xor_parity(dst, nbytes: int, data, nsources: int):
     """Drop-in for task_processing.c:96-109 on numpy buffers (GPU)."""
-    call("bcp_xor_parity", _V(dst.ctypes.data), nbytes, _V(data.ctypes.data), nsources)
+    d, _ = _host_addr(dst, nbytes, writable=True)
+    s, _ = _host_addr(data, nbytes * max(nsources, 0))
+    call("bcp_xor_parity", _V(d), nbytes, _V(s), nsources)
 
 
 # ---------------------------------------------------------------------------

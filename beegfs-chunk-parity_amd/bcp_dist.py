@@ -50,6 +50,14 @@ class Dist:
     def sum(self, x: float) -> float:
         return self._reduce(x, self.pg.ReduceOp.SUM) if self.pg else x
 
+    def gather(self, obj) -> list:
+        """Every rank's obj (picklable), in rank order, on every rank."""
+        if not self.pg:
+            return [obj]
+        out = [None] * self.world
+        self.pg.all_gather_object(out, obj)
+        return out
+
     def close(self):
         if self.pg and self.pg.is_initialized():
             self.pg.destroy_process_group()

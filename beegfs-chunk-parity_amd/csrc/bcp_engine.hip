@@ -63,6 +63,7 @@ struct bcp_queue {
   size_t tiles_cap = 0;                // in records
   hipStream_t copy_stream = nullptr;   // descriptor-table uploads (created on first use)
   hipEvent_t sync_ev = nullptr;        // blocking-sync event (sync_mode 1; created on first use)
+  bool broken = false;                 // work-queue counter could not be restarted after a failed launch
 };
 
 struct bcp_event {
@@ -99,6 +100,22 @@ static int hip_to_errno(hipError_t e) {
 static int set_device(bcp_engine *e) {
   HIP_RC(hipSetDevice(e->device));
   return 0;
+}
+
+// Work-queue accounting after a launch that takes tiles from q->qctr.  On
+// success the next launch starts `consumed` counts later.  On any error the
+// kernel may or may not have taken counts, so the counter is restarted
+// (memset on the stream, ordered after anything that did run) and the base
+// reset; if even that fails the queue refuses further XOR work (-EIO)
+// instead of starting a later launch partway through its tile range.
+static int queue_launched(bcp_queue *q, hipError_t e, uint64_t consumed) {
+  if (e == hipSuccess) {
+    q->qbase += consumed;
+    return 0;
+  }
+  if (hipMemsetAsync(q->qctr, 0, sizeof(unsigned long long), q->stream) == hipSuccess) q->qbase = 0;
+  else q->broken = true;
+  return hip_to_errno(e);
 }
 
 // Workgroups of the streaming kernel: stream_grid if set, else blocks_per_cu
@@ -268,6 +285,12 @@ extern "C" int bcp_engine_info(bcp_engine *eng, int *num_cus, char *name, size_t
   return 0;
 }
 
+extern "C" int bcp_engine_pci_bus_id(bcp_engine *eng, char *bus_id, size_t bus_id_cap) {
+  if (!eng || !bus_id || bus_id_cap < 13 || bus_id_cap > (1u << 20)) return -EINVAL;
+  HIP_RC(hipDeviceGetPCIBusId(bus_id, (int)bus_id_cap, eng->device));
+  return 0;
+}
+
 extern "C" int bcp_set_option(bcp_engine *eng, const char *key, int value) {
   if (!eng || !key) return -EINVAL;
   int rc = 0;
@@ -392,7 +415,11 @@ extern "C" int bcp_queue_destroy(bcp_queue *q) {
 extern "C" int bcp_queue_sync(bcp_queue *q) {
   if (!q) return -EINVAL;
   if (q->eng->tuning.sync_mode == 1) {
-    if (!q->sync_ev) HIP_RC(hipEventCreateWithFlags(&q->sync_ev, hipEventBlockingSync | hipEventDisableTiming));
+    if (!q->sync_ev) {
+      const int rc = set_device(q->eng);  // the event must belong to the queue's device
+      if (rc) return rc;
+      HIP_RC(hipEventCreateWithFlags(&q->sync_ev, hipEventBlockingSync | hipEventDisableTiming));
+    }
     HIP_RC(hipEventRecord(q->sync_ev, q->stream));
     HIP_RC(hipEventSynchronize(q->sync_ev));
     return 0;
@@ -585,9 +612,13 @@ static int launch_stream(bcp_queue *q, bool gather, int vecs, StreamArgs a, uint
   const uint64_t nunits = (ntiles + a.grab - 1) / a.grab;
   int grid = grid_for(e);
   if ((uint64_t)grid > nunits) grid = (int)nunits;
-  HIP_RC(launch_xor_stream(q->stream, grid, vecs, gather, a, gather ? e->tuning.table_wpe : e->tuning.stream_wpe));
-  e->last_stream_vecs.store(vecs, std::memory_order_relaxed);
-  if (a.sched == kSchedQueue) q->qbase += nunits + (uint64_t)grid;
+  if (q->broken) return -EIO;
+  (void)hipGetLastError();  // an error left by an earlier call must not read as this launch's
+  const hipError_t le =
+      launch_xor_stream(q->stream, grid, vecs, gather, a, gather ? e->tuning.table_wpe : e->tuning.stream_wpe);
+  if (le == hipSuccess) e->last_stream_vecs.store(vecs, std::memory_order_relaxed);
+  if (a.sched == kSchedQueue) return queue_launched(q, le, nunits + (uint64_t)grid);
+  HIP_RC(le);
   return 0;
 }
 
@@ -736,9 +767,13 @@ static int submit_desc(bcp_queue *q, const bcp_stripe *stripes, uint32_t nstripe
   const uint32_t nunits = b.sched == kSchedQueue ? (acc + b.grab - 1) / b.grab : acc;
   int grid = desc_grid_for(e);
   if ((uint32_t)grid > nunits) grid = (int)nunits;
+  if (q->broken) return -EIO;
+  (void)hipGetLastError();  // see launch_stream
   HIP_RC(launch_desc_tiles(q->stream, b));
-  HIP_RC(launch_xor_desc(q->stream, grid, vecs, b, e->tuning.desc_pipe));
-  if (b.sched == kSchedQueue) q->qbase += (uint64_t)nunits + (uint64_t)grid;
+  const hipError_t le = launch_xor_desc(q->stream, grid, vecs, b, e->tuning.desc_pipe);
+  if (b.sched == kSchedQueue) rc = queue_launched(q, le, (uint64_t)nunits + (uint64_t)grid);
+  else rc = hip_to_errno(le);
+  if (rc) return rc;
   HIP_RC(hipEventRecord(slot->done, q->stream));
   slot->used = true;
   return 0;
@@ -780,8 +815,14 @@ extern "C" int bcp_xor_strided_async(bcp_queue *q, void *dst, uint64_t dst_strid
   }
   // General geometry: express as descriptors (any alignment / tail).
   if (nstripes * nsrc > 0xFFFFFFFFull || nstripes > 0xFFFFFFFFull) return -EINVAL;
-  std::vector<bcp_stripe> st(nstripes);
-  std::vector<bcp_source> so(nstripes * nsrc);
+  std::vector<bcp_stripe> st;
+  std::vector<bcp_source> so;
+  try {  // nothing may throw across the C ABI
+    st.resize(nstripes);
+    so.resize(nstripes * nsrc);
+  } catch (const std::bad_alloc &) {
+    return -ENOMEM;
+  }
   for (uint64_t s = 0; s < nstripes; s++) {
     st[s].dst = (uint64_t)dst + s * dst_stride;
     st[s].out_len = chunk_bytes;

@@ -20,13 +20,21 @@ algorithmic bytes = sum of source lengths + output length per stripe
 its own stripe shard on its own GPU (no data-path collective; gloo only for
 the start barrier and the max-time reduction), scaling "weak".
 
-roofline.achieved uses the kernel's HIP-event time on the stream it runs on;
-roofline.traffic comes from the committed rocprofv3 PMC pass
-(profiles/*pmc*.json) when it matches this workload, else null.
-cpu_baseline: rank 0 at N=1 times the oracle's C restatement of xor_parity
-(-std=gnu99 -Os, the reference flags) on a bounded sample of the same
-stripes ("port"): 16 host threads (the box's CPU share) as the value, 1
-thread beside it.
+roofline.achieved / frac (= frac_event) use the kernel's HIP-event time on the
+stream it runs on; frac_rocprof, traffic and their provenance (profile files
+and the code commit they were measured at) come from the committed rocprofv3
+kernel-trace stats and PMC passes of the same command (profiles/**/*pmc*.json,
+tools/pmc_summary.py) when they match this workload, else null.
+n_gpus counts DISTINCT devices (PCI bus ids gathered over gloo): ranks that
+share a GPU are flagged shared_gpu instead of being reported as more GPUs.
+cpu_baseline: rank 0 at N=1 times the reference's OWN xor_parity
+(task_processing.c:96-109 compiled unchanged -std=gnu99 -Os into oracle/_ref,
+kind "reference"; the oracle's restatement, kind "port", where _ref was not
+built) on a bounded sample of the same stripe shape at 1 thread, 16 threads
+(the box's CPU share for one GPU) and len(sched_getaffinity) threads; value =
+the fastest of those legs, nproc and the affinity count stated.
+The output is verified after timing: cleared, one more step, then fold
+conservation plus sampled stripes compared byte for byte with numpy.
 """
 from __future__ import annotations
 
@@ -70,14 +78,16 @@ def parse():
     ap.add_argument("--contig", action="store_true", help="physically contiguous device allocations (A/B knob)")
     ap.add_argument("--opt", action="append", default=[], metavar="KEY=VALUE",
                     help="engine option (bcp_set_option) for A/B runs; repeatable")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--cpu-stripes", type=int, default=256, help="stripes in the CPU sample pool")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget over its three legs")
+    ap.add_argument("--cpu-stripes", type=int, default=256, help="stripes in the 1-thread CPU sample pool")
     ap.add_argument("--no-cpu", action="store_true")
     return ap.parse_args()
 
 
 def pmc_traffic(workload_key: str, kernel_tag: str):
-    """Per-launch HBM bytes from the committed PMC summary, if it matches."""
+    """Committed profile summary (tools/pmc_summary.py) of this workload and
+    kernel: per-launch HBM bytes (PMC), rocprofv3 kernel-trace average, the
+    files and the code commit they came from; the newest matching one."""
     best = None
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "**", "*pmc*.json"), recursive=True)):
         try:
@@ -86,6 +96,7 @@ def pmc_traffic(workload_key: str, kernel_tag: str):
             continue
         if (doc.get("workload_key") == workload_key and doc.get("hbm_bytes_per_launch")
                 and kernel_tag in doc.get("kernel", "")):
+            doc.setdefault("files", {})["pmc_summary"] = os.path.relpath(path, ROOT)
             best = doc
     return best
 
@@ -96,6 +107,10 @@ def main():
     ndev = bcp.device_count()
     assert ndev > 0, "bench.py needs a HIP device (there is no CPU path)"
     eng = bcp.Engine(d.local_rank % ndev)
+    # physical GPUs in the job: ranks that map to the same device share it
+    bus_ids = d.gather(eng.pci_bus_id())
+    n_devices = len(set(bus_ids))
+    shared_gpu = n_devices < d.world
     if a.mode == "mixed":  # the timed kernel is the descriptor kernel
         if a.blocks_per_cu:
             eng.option("desc_blocks_per_cu", a.blocks_per_cu)
@@ -248,43 +263,57 @@ def main():
         NS = N if (1 <= N <= 12 or N == 16) else 0  # widths without a specialisation run xor_stream<0, ...>
         kernel, kernel_tag = kernel.format(N=NS, U=U), kernel_tag.format(N=NS, U=U)
 
-    # device-side property check (no oracle here): fold(output) == fold(inputs)
+    # Verification after the timed region: clear the output, run ONE more
+    # step, then check it on the device (fold conservation / rebuild compare)
+    # and sampled stripes byte for byte against numpy (not the oracle).
+    import numpy as np
+    q.memset(out, 0xA5, out_bytes if a.mode == "mixed" else S * C)
+    step()
+    q.sync()
+    rng = np.random.default_rng(7 + d.rank)
+
+    def sampled(idx, fetch_inputs, out_ptr, out_len):
+        ok = True
+        for i in idx:
+            ins = fetch_inputs(i)
+            ref = np.zeros(out_len, dtype=np.uint8)
+            for buf in ins:
+                ref[:len(buf)] ^= buf[:out_len]
+            got = np.empty(out_len, dtype=np.uint8)
+            q.d2h(got, out_ptr(i), out_len)
+            q.sync()
+            ok = ok and bool(np.array_equal(got, ref))
+        return ok
+
+    def dget(ptr, n):
+        buf = np.empty(n, dtype=np.uint8)
+        q.d2h(buf, ptr, n)
+        q.sync()
+        return buf
+
     verified = None
     if a.mode == "mixed":
-        import numpy as np
         ok = True
-        for i in sorted({0, len(stripes) - 1, len(stripes) // 2}):
+        for i in sorted({0, len(stripes) - 1, len(stripes) // 2} | {int(x) for x in rng.integers(0, len(stripes), 3)}):
             dptr, m, first, n, _ = stripes[i]
-            acc = np.zeros(m, dtype=np.uint8)
-            for k in range(n):
-                p, ln = sources[first + k]
-                buf = np.empty(ln, dtype=np.uint8)
-                q.d2h(buf, p, ln)
-                q.sync()
-                acc[:ln] ^= buf
-            got = np.empty(m, dtype=np.uint8)
-            q.d2h(got, dptr, m)
-            q.sync()
-            ok = ok and bool(np.array_equal(got, acc))
+            ok = ok and sampled([i], lambda i: [dget(*sources[first + k]) for k in range(n)], lambda i: dptr, m)
         verified = ok
     elif a.mode == "gen":
         q.xor_fold(out, S * C, chk)
         q.xor_fold(src, S * N * C, chk + 16)
-        import numpy as np
-        f = np.empty(32, dtype=np.uint8)
-        q.d2h(f, chk, 32)
-        q.sync()
-        verified = bool(np.array_equal(f[:16], f[16:]))
+        f = dget(chk, 32)
+        idx = sorted({0, S - 1} | {int(x) for x in rng.integers(0, S, 4)})
+        verified = bool(np.array_equal(f[:16], f[16:])) and sampled(
+            idx, lambda i: [dget(src + (i * N + k) * C, C) for k in range(N)], lambda i: out + i * C, C)
     else:
-        import numpy as np
         victim = min(3, N - 1)
         gathered = eng.alloc(S * C)
         q.xor_strided(gathered, C, src + victim * C, N * C, C, S, 1, C)
         q.compare(out, gathered, S * C, chk)
-        f = np.empty(8, dtype=np.uint8)
-        q.d2h(f, chk, 8)
-        q.sync()
-        verified = int(f.view("<u8")[0]) == 0
+        f = dget(chk, 8)
+        idx = sorted({0, S - 1} | {int(x) for x in rng.integers(0, S, 4)})
+        verified = int(f.view("<u8")[0]) == 0 and sampled(
+            idx, lambda i: [dget(src + (i * N + victim) * C, C)], lambda i: out + i * C, C)
 
     wall_max = d.max(wall)
     total_bytes = d.sum(float(bytes_per_step * a.steps))
@@ -295,25 +324,35 @@ def main():
     if d.rank == 0 and d.world == 1 and not a.no_cpu and a.mode != "mixed":
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle  # cpu_baseline leg only
-        # the box's CPU share is 16 threads (one GPU); the reference runs 12
-        # lanes per rank, each folding with xor_parity (gen/main.c:821-845)
-        threads = max(1, min(16, os.cpu_count() or 1))
-        half = a.cpu_seconds / 2
-        bps1 = oracle.bench_xor(1, a.cpu_stripes, N, C, half)
-        per_thread = max(16, a.cpu_stripes * 2 // threads)  # private pool per thread, ~2 GiB in all
-        bpsn = oracle.bench_xor(threads, per_thread, N, C, half)
+        use_ref = oracle.ref_lib() is not None
+        nproc = os.cpu_count() or 1
+        try:
+            affinity = len(os.sched_getaffinity(0))
+        except (AttributeError, OSError):
+            affinity = nproc
+        legs_t = sorted({1, min(16, affinity), affinity})
+        leg_s = a.cpu_seconds / len(legs_t)
+        legs = []
+        for t in legs_t:
+            # private pool per thread: ~2 GiB in all at 16 threads (out of
+            # cache), at least 4 stripes each when the affinity set is large
+            per_thread = a.cpu_stripes if t == 1 else max(4, a.cpu_stripes * 2 // t)
+            bps = oracle.bench_xor(t, per_thread, N, C, leg_s, use_ref=use_ref)
+            legs.append({"threads": t, "value": round(bps / GiB, 3), "pool_stripes_per_thread": per_thread})
+        best = max(legs, key=lambda x: x["value"])
         model = ""
         try:
             model = next(l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name"))
         except (OSError, StopIteration):
             pass
-        cpu = {"value": round(bpsn / GiB, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
-               "sample": f"oracle_xor_parity (-std=gnu99 -Os, the reference's xor_parity restated) on "
-                         f"{threads} host threads, each over a private {per_thread}-stripe pool of {N} x "
-                         f"{C // KiB} KiB synthetic chunks, looped >= {half:g} s; (N+1)*S bytes per stripe",
-               "single_thread": {"value": round(bps1 / GiB, 3), "cores": 1,
-                                 "sample": f"same on 1 thread, {a.cpu_stripes}-stripe pool, >= {half:g} s"},
-               "cpu_model": model}
+        fn = ("the reference's own xor_parity (task_processing.c:96-109 compiled unchanged, -std=gnu99 -Os, "
+              "oracle/_ref)") if use_ref else "oracle_xor_parity (the reference's xor_parity restated, -std=gnu99 -Os)"
+        cpu = {"value": best["value"], "unit": "GiB/s", "cores": best["threads"],
+               "kind": "reference" if use_ref else "port",
+               "sample": f"{fn}: each thread folds a private pool of {N} x {C // KiB} KiB synthetic stripes "
+                         f"in a loop for >= {leg_s:g} s; (N+1)*S bytes per stripe; legs at 1, 16 and "
+                         f"sched_getaffinity threads, value = the fastest leg",
+               "legs": legs, "nproc": nproc, "affinity_cpus": affinity, "cpu_model": model}
 
     if d.rank == 0:
         value = total_bytes / wall_max / GiB
@@ -321,11 +360,14 @@ def main():
         mode_key = "rebuild_packed" if (a.mode == "rebuild" and a.rebuild_layout == "packed") else a.mode
         wkey = f"{mode_key}:{S}x{N}x{C}"
         pmc = pmc_traffic(wkey, kernel_tag)
+        frac_rocprof = None
+        if pmc and pmc.get("rocprof_avg_ns"):
+            frac_rocprof = round(bytes_per_step / (pmc["rocprof_avg_ns"] * 1e-9) / 1e9 / HBM_PEAK_GBS, 4)
         line = {
             "metric": METRIC,
             "value": round(value, 2),
             "unit": "GiB/s",
-            "n_gpus": d.world,
+            "n_gpus": n_devices,
             "steps": a.steps,
             "warmup": a.warmup,
             "ms_per_step": round(wall_max / a.steps * 1e3, 4),
@@ -343,9 +385,11 @@ def main():
                 "bytes_per_step_per_gpu": bytes_per_step,
                 "data_rate_GiBps": round(value * N / (N + 1), 2) if a.mode != "mixed" else None,
                 "pct_hbm_peak": round(100.0 * achieved / HBM_PEAK_GBS, 2),
-                # whole job (wall clock, all ranks) against N x 8 TB/s
-                "pct_aggregate_hbm_peak": round(100.0 * total_bytes / wall_max / 1e9 / (HBM_PEAK_GBS * d.world), 2),
-                "parallelism": f"shard{d.world} (stripes per GPU, no collective)",
+                # whole job (wall clock, all ranks) against (distinct GPUs) x 8 TB/s
+                "pct_aggregate_hbm_peak": round(100.0 * total_bytes / wall_max / 1e9 / (HBM_PEAK_GBS * n_devices), 2),
+                "parallelism": f"shard{d.world} (stripes per rank, no collective)",
+                "ranks": d.world,
+                "shared_gpu": shared_gpu,
                 "device": devname,
                 "cus": cus,
                 "verified_on_device": ok_all,
@@ -357,9 +401,15 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "frac_event": round(achieved / HBM_PEAK_GBS, 4),
+                "frac_rocprof": frac_rocprof,
                 "kernel_ms": round(kern_ms_max, 4),
                 "traffic": pmc["hbm_bytes_per_launch"] if pmc else None,
                 "traffic_source": pmc["source"] if pmc else None,
+                "profile_files": pmc.get("files") if pmc else None,
+                "profile_commit": pmc.get("code_commit") if pmc else None,
+                "frac_note": "frac = frac_event: algorithmic bytes / HIP-event kernel time in this run; "
+                             "frac_rocprof: the same bytes / the committed rocprofv3 kernel-trace average",
             },
             "cpu_baseline": cpu,
         }

@@ -79,6 +79,11 @@ int bcp_engine_create(int device, bcp_engine **out);
 int bcp_engine_destroy(bcp_engine *eng);
 /* Device properties the bench reports: CU count and the name string. */
 int bcp_engine_info(bcp_engine *eng, int *num_cus, char *name, size_t name_cap);
+/* PCI bus id of the engine's device ("dddd:bb:dd.f"): identifies the physical
+ * GPU across processes whatever HIP_VISIBLE_DEVICES renumbers (bench.py counts
+ * distinct devices with it, so ranks sharing a GPU are not reported as more
+ * GPUs).  -EINVAL if bus_id_cap is too small. */
+int bcp_engine_pci_bus_id(bcp_engine *eng, char *bus_id, size_t bus_id_cap);
 
 /* ---- queues (one in-order HIP stream each) ----------------------------- */
 /* Work on one queue runs in submission order.  Overlap (copy beside compute)

@@ -278,7 +278,10 @@ void oracle_fill_synthetic(uint8_t *buf, uint64_t len, uint64_t seed,
 
 /* --- CPU baseline timing (bench.py cpu_baseline leg) -------------------- */
 
+typedef void (*xor_fn)(uint8_t *, size_t, const uint8_t *, int);
+
 typedef struct {
+    xor_fn fn;         /* the fold timed: oracle_xor_parity or the reference's own */
     uint8_t *pool;     /* [nstripes][nsrc][chunk] */
     uint8_t *out;      /* [nstripes][chunk] */
     uint64_t nstripes, chunk;
@@ -302,8 +305,8 @@ static void *bench_thread(void *p)
     uint64_t done = 0;
     do {
         for (uint64_t s = 0; s < a->nstripes; s++) {
-            oracle_xor_parity(a->out + s * a->chunk, a->chunk,
-                              a->pool + s * a->chunk * a->nsrc, a->nsrc);
+            a->fn(a->out + s * a->chunk, a->chunk,
+                  a->pool + s * a->chunk * a->nsrc, a->nsrc);
             done++;
         }
         t = now_s();
@@ -314,12 +317,13 @@ static void *bench_thread(void *p)
 }
 
 /*
- * Times oracle_xor_parity over `nthreads` private pools of nstripes stripes
- * (nsrc x chunk bytes each, synthetic data), for at least `seconds`.
- * Returns aggregate algorithmic bytes/s ((nsrc+1)*chunk per stripe) or <0.
+ * Times fn (xor_parity's signature; NULL = oracle_xor_parity) over `nthreads`
+ * private pools of nstripes stripes (nsrc x chunk bytes each, synthetic
+ * data), for at least `seconds`.  Returns aggregate algorithmic bytes/s
+ * ((nsrc+1)*chunk per stripe) or <0.
  */
-double oracle_bench_xor(int nthreads, uint64_t nstripes, int nsrc,
-                        uint64_t chunk, double seconds)
+double oracle_bench_xor_fn(void *fn, int nthreads, uint64_t nstripes, int nsrc,
+                           uint64_t chunk, double seconds)
 {
     if (nthreads < 1 || nthreads > 256 || nsrc < 1)
         return -1.0;
@@ -327,10 +331,16 @@ double oracle_bench_xor(int nthreads, uint64_t nstripes, int nsrc,
     pthread_t th[256];
     for (int t = 0; t < nthreads; t++) {
         args[t] = (bench_arg){0};
+        args[t].fn = fn ? (xor_fn)fn : oracle_xor_parity;
         args[t].pool = malloc(nstripes * nsrc * chunk);
         args[t].out = malloc(nstripes * chunk);
-        if (!args[t].pool || !args[t].out)
+        if (!args[t].pool || !args[t].out) {
+            for (int u = 0; u <= t; u++) {
+                free(args[u].pool);
+                free(args[u].out);
+            }
             return -2.0;
+        }
         /* cheap non-constant fill; content does not affect integer XOR speed */
         uint64_t *w = (uint64_t *)args[t].pool;
         for (uint64_t i = 0; i < nstripes * nsrc * chunk / 8; i++)
@@ -353,4 +363,10 @@ double oracle_bench_xor(int nthreads, uint64_t nstripes, int nsrc,
         free(args[t].out);
     }
     return bytes / worst;
+}
+
+double oracle_bench_xor(int nthreads, uint64_t nstripes, int nsrc,
+                        uint64_t chunk, double seconds)
+{
+    return oracle_bench_xor_fn(NULL, nthreads, nstripes, nsrc, chunk, seconds);
 }

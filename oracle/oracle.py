@@ -12,7 +12,11 @@ Reference behaviour restated (paths relative to the reference repo):
   * windowed P role / senders    task_processing.c:117-245 / :247-322
   * parity chunk file format     task_processing.c:168,186,199-201,213-214
   * rebuild index / truncation   task_processing.c:169-174,228-230
-Pinned by SURVEY.md §8(c) KAT-1..4 (tests/golden/kats.json).
+Pinning: ``oracle_xor_parity`` reproduces the reference's OWN xor_parity
+(task_processing.c:96-109 compiled unchanged into oracle/_ref/libref_xor.so,
+container only) on every fixture of tests/golden/ref_xor.json; the MPI-role
+assembly (windows, padding, replay, file format) is pinned by SURVEY.md §8(c)
+KAT-1..4 (tests/golden/kats.json).
 """
 from __future__ import annotations
 
@@ -24,6 +28,7 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "build", "liboracle.so")
+REF_LIB_PATH = os.path.join(HERE, "_ref", "libref_xor.so")  # reference's own xor_parity (container-built)
 WINDOW = 10 * 1024 * 1024  # FILE_TRANSFER_BUFFER_SIZE, task_processing.c:20
 KAT_MUL = 2654435761
 
@@ -33,6 +38,39 @@ _lib = None
 def build() -> str:
     subprocess.run(["make", "-s", "-C", HERE], check=True)
     return LIB_PATH
+
+
+def build_ref() -> str | None:
+    """Build oracle/_ref (only where /root/reference exists); path or None."""
+    subprocess.run(["make", "-s", "-C", HERE, "ref"], check=True)
+    return REF_LIB_PATH if os.path.exists(REF_LIB_PATH) else None
+
+
+_ref = None
+
+
+def ref_lib():
+    """The reference's own xor_parity as ref_xor_parity(), or None when
+    oracle/_ref was not built (no /root/reference where it was built)."""
+    global _ref
+    if _ref is None and os.path.exists(REF_LIB_PATH):
+        L = ctypes.CDLL(REF_LIB_PATH)
+        L.ref_xor_parity.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_int]
+        L.ref_xor_parity.restype = None
+        _ref = L
+    return _ref
+
+
+def ref_xor_parity(data: np.ndarray, nbytes: int, nsources: int) -> np.ndarray:
+    """task_processing.c:96-109 itself (oracle/_ref); raises if not built."""
+    L = ref_lib()
+    if L is None:
+        raise FileNotFoundError(REF_LIB_PATH)
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    assert data.size >= nbytes * nsources
+    dst = np.empty(max(nbytes, 1), dtype=np.uint8)
+    L.ref_xor_parity(_ptr(dst), nbytes, _ptr(data), nsources)
+    return dst[:nbytes]
 
 
 def lib() -> ctypes.CDLL:
@@ -58,6 +96,9 @@ def lib() -> ctypes.CDLL:
         L.oracle_fill_synthetic.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64]
         L.oracle_bench_xor.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_int, ctypes.c_uint64, ctypes.c_double]
         L.oracle_bench_xor.restype = ctypes.c_double
+        L.oracle_bench_xor_fn.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_uint64, ctypes.c_int,
+                                          ctypes.c_uint64, ctypes.c_double]
+        L.oracle_bench_xor_fn.restype = ctypes.c_double
         del u8p
         _lib = L
     return _lib
@@ -158,6 +199,16 @@ def rebuild_index(locations: int, actual_p: int, victim: int) -> int:
     return lib().oracle_rebuild_index(locations, actual_p, victim)
 
 
-def bench_xor(nthreads: int, nstripes: int, nsrc: int, chunk: int, seconds: float) -> float:
-    """Algorithmic bytes/s of oracle_xor_parity ((nsrc+1)*chunk per stripe)."""
-    return lib().oracle_bench_xor(nthreads, nstripes, nsrc, chunk, seconds)
+def bench_xor(nthreads: int, nstripes: int, nsrc: int, chunk: int, seconds: float, use_ref: bool = False) -> float:
+    """Algorithmic bytes/s ((nsrc+1)*chunk per stripe) of oracle_xor_parity, or
+    of the reference's own xor_parity (oracle/_ref) when use_ref."""
+    fn = None
+    if use_ref:
+        L = ref_lib()
+        if L is None:
+            raise FileNotFoundError(REF_LIB_PATH)
+        fn = ctypes.cast(L.ref_xor_parity, ctypes.c_void_p).value
+    r = lib().oracle_bench_xor_fn(fn, nthreads, nstripes, nsrc, chunk, seconds)
+    if r < 0:
+        raise MemoryError(f"oracle_bench_xor_fn: {r}")
+    return r

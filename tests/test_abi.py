@@ -75,3 +75,25 @@ def test_argument_validation_without_device(bcp):
     assert L.bcp_engine_create(0, None) == -errno.EINVAL
     assert L.bcp_queue_sync(None) == -errno.EINVAL
     assert L.bcp_strerror(-errno.ENODEV) == b"no usable HIP device"
+
+
+def test_host_buffer_bounds_checked(bcp):
+    """The binding refuses an nbytes beyond the host buffer and a read-only
+    buffer as a copy destination, before any HIP call."""
+    import numpy as np
+    a = np.zeros(64, np.uint8)
+    assert bcp._host_addr(a, 64) == (a.ctypes.data, 64)
+    with pytest.raises(ValueError):
+        bcp._host_addr(a, 65)
+    with pytest.raises(ValueError):
+        bcp._host_addr(b"\0" * 16, 16, writable=True)
+    ro = np.zeros(16, np.uint8)
+    ro.flags.writeable = False
+    with pytest.raises(ValueError):
+        bcp._host_addr(ro, None, writable=True)
+    with pytest.raises(ValueError):
+        bcp._host_addr(a[::2], None)
+    with pytest.raises(ValueError):
+        bcp._host_addr(12345, None)
+    with pytest.raises(ValueError):
+        bcp.xor_parity(np.zeros(8, np.uint8), 8, np.zeros(15, np.uint8), 2)  # data shorter than 2 rows

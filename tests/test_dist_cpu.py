@@ -30,9 +30,10 @@ def _worker(rank, world, port, q):
     d.barrier()
     mx = d.max(float(rank + 1) * 1.5)
     sm = d.sum(float(rank + 1))
+    ids = d.gather(f"0000:{rank % 1:02x}:00.0")  # two ranks on one device, as bench.py sees them
     d.barrier()
     d.close()
-    q.put((rank, mx, sm))
+    q.put((rank, mx, sm, tuple(ids)))
 
 
 def _free_port():
@@ -55,4 +56,5 @@ def test_gloo_world2_reductions():
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    assert res == [(0, 3.0, 3.0), (1, 3.0, 3.0)]
+    assert [r[:3] for r in res] == [(0, 3.0, 3.0), (1, 3.0, 3.0)]
+    assert all(r[3] == ("0000:00:00.0", "0000:00:00.0") for r in res)

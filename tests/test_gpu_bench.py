@@ -1,0 +1,58 @@
+"""bench.py as the driver runs it, at a small size: one rank, and two ranks
+under torchrun (a child process, never an exec).  Checks the on-device
+verification and the GPU-count labels: ranks that share a device are
+reported as that many distinct GPUs with shared_gpu set, never as more."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _last_json(out: str) -> dict:
+    lines = [l for l in out.splitlines() if l.startswith("{")]
+    assert lines, out[-2000:]
+    return json.loads(lines[-1])
+
+
+def _run(cmd, timeout):
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)
+    assert r.returncode == 0, (r.returncode, r.stdout[-2000:], r.stderr[-4000:])
+    return _last_json(r.stdout)
+
+
+@pytest.mark.timeout(400)
+@pytest.mark.parametrize("mode", ["gen", "rebuild", "mixed"])
+def test_bench_one_rank_small(bcp, mode):
+    line = _run([sys.executable, "bench.py", "--stripes", "64", "--steps", "2", "--warmup", "1", "--no-cpu",
+                 "--mode", mode], 300)
+    assert line["config"]["verified_on_device"] is True
+    assert line["n_gpus"] == 1 and line["config"]["ranks"] == 1 and line["config"]["shared_gpu"] is False
+    assert line["roofline"]["frac"] == line["roofline"]["frac_event"] > 0
+
+
+@pytest.mark.timeout(500)
+def test_bench_torchrun_two_ranks_labels(bcp):
+    ndev = bcp.device_count()
+    line = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                 "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+                 "bench.py", "--gpus", "2", "--stripes", "64", "--steps", "2", "--warmup", "1", "--no-cpu"], 420)
+    assert line["config"]["verified_on_device"] is True
+    assert line["config"]["ranks"] == 2
+    distinct = min(ndev, 2)  # bench maps local rank r to device r % ndev
+    assert line["n_gpus"] == distinct
+    assert line["config"]["shared_gpu"] is (distinct < 2)

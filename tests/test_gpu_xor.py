@@ -607,16 +607,20 @@ def test_fold_and_compare(dev, queue):
 
 # --------------------------------------------------------------------------
 # BASELINE sizes: config 2 (gen) and config 3 (rebuild), 12,500 stripes of
-# 8 x 512 KiB device-resident -- size-independent properties
+# 8 x 512 KiB device-resident, and config 4's per-GPU shard (1,000,000 chunks
+# over 8 GPUs = 15,625 stripes, 61 GiB of chunks + parity + rebuild buffers
+# ~84 GiB on one GPU) -- size-independent properties
 # --------------------------------------------------------------------------
-def test_config2_and_config3_full_size(oracle, dev, queue):
-    nstripes, nsrc, chunk = 12500, 8, 512 * KiB
+@pytest.mark.parametrize("nstripes", [12500, 15625], ids=["config2-3", "config4-shard"])
+def test_config2_and_config3_full_size(oracle, dev, queue, nstripes):
+    nsrc, chunk = 8, 512 * KiB
     total = nstripes * nsrc * chunk
     src = dev.alloc(total)
     par = dev.alloc(nstripes * chunk)
     reb = dev.alloc(nstripes * chunk)
     res = dev.alloc(64)
     queue.fill_synthetic(src, total, 1)
+    queue.memset(par, 0xA5, nstripes * chunk)  # no stale parity from an earlier test can pass
     queue.xor_uniform(par, src, nstripes, nsrc, chunk)
     # (1) XOR-fold conservation: fold(parity) == fold(all sources)
     queue.xor_fold(par, nstripes * chunk, res)
@@ -736,3 +740,36 @@ def test_budget_widths_default_tuning(engine, dev, queue, nsrc):
             assert engine.option("last_stream_vecs") == (8 if nsrc <= 8 else 4)
         ref = np.bitwise_xor.reduce(data.reshape(nstripes, nsrc, chunk), axis=1).reshape(-1)
         assert np.array_equal(dev.get(dst, nstripes * chunk), ref), (nstripes, chunk)
+
+
+def test_launch_after_pending_query_keeps_the_work_queue(bcp, engine, dev, queue):
+    """A query that reports pending work (-EAGAIN, hipErrorNotReady left on the
+    thread) must not be read as a failed launch by the next submission: the
+    work-queue base stays in step and every later launch folds all its tiles
+    (qbase advancement after a launch error)."""
+    nstripes, nsrc, chunk = 2000, 8, 512 * KiB
+    src = dev.alloc(nstripes * nsrc * chunk)
+    out = dev.alloc(nstripes * chunk)
+    res = dev.alloc(64)
+    queue.fill_synthetic(src, nstripes * nsrc * chunk, 5)
+    L = bcp.lib()
+    pending = 0
+    for rep in range(4):
+        queue.memset(out, 0xA5, nstripes * chunk)
+        queue.xor_uniform(out, src, nstripes, nsrc, chunk)
+        pending += L.bcp_queue_query(queue.h) == -11  # -EAGAIN while the big launch runs
+        queue.xor_uniform(out, src, nstripes, nsrc, chunk)  # submitted right after the query
+        queue.xor_fold(out, nstripes * chunk, res)
+        queue.xor_fold(src, nstripes * nsrc * chunk, res + 16)
+        f = dev.get(res, 32)
+        assert np.array_equal(f[:16], f[16:]), rep
+    assert pending >= 1  # the scenario actually happened
+    # a small descriptor batch after another pending query
+    queue.xor_uniform(out, src, nstripes, nsrc, chunk)
+    L.bcp_queue_query(queue.h)
+    queue.xor_stripes([(out, 1000, 0, 2, 0)], [(src, 1000), (src + chunk, 999)])
+    got = dev.get(out, 1000)
+    a, b = dev.get(src, 1000), dev.get(src + chunk, 999)
+    ref = a.copy()
+    ref[:999] ^= b
+    assert np.array_equal(got, ref)

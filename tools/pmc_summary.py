@@ -35,14 +35,27 @@ def main():
     ap.add_argument("--workload-key", required=True)
     ap.add_argument("--algorithmic", type=float, required=True, help="algorithmic bytes per launch")
     ap.add_argument("--out", required=True)
+    ap.add_argument("--stats", help="rocprofv3 --kernel-trace --stats kernel_stats.csv of the same command")
+    ap.add_argument("--commit", help="code commit the profiled tree was built from")
+    ap.add_argument("--files", nargs="*", default=[], help="committed copies of the raw inputs (provenance)")
     a = ap.parse_args()
     fe = per_dispatch(a.fetch, "FETCH_SIZE", a.kernel)
     wr = per_dispatch(a.write, "WRITE_SIZE", a.kernel)
     assert fe and wr, "no matching dispatches"
     fetch_b = statistics.median(v[0] for v in fe.values()) * 1024 * 2
     write_b = statistics.median(v[0] for v in wr.values()) * 1024
+    avg_ns = None
+    if a.stats:
+        with open(a.stats) as f:
+            for row in csv.DictReader(f):
+                if a.kernel in row["Name"]:
+                    avg_ns = float(row["AverageNs"])
+                    break
     doc = {
         "workload_key": a.workload_key,
+        "code_commit": a.commit,
+        "rocprof_avg_ns": avg_ns,
+        "files": {"stats": a.stats, "raw": a.files},
         "kernel": next(iter(fe.values()))[1],
         "dispatches": {"fetch_pass": len(fe), "write_pass": len(wr)},
         "fetch_bytes_per_launch": round(fetch_b),
