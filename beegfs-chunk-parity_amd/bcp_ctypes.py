@@ -116,6 +116,14 @@ _SIGS = {
     "bcp_task_shutdown": ([], ctypes.c_int),
     "bcp_task_set_xor_hook": ([_V, _V], None),
     "bcp_task_set_fold_mode": ([ctypes.c_int], ctypes.c_int),
+    "bcp_task_fold_stats": ([ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)], ctypes.c_int),
+    "bcp_task_inject_failure": ([ctypes.c_int, ctypes.c_int, ctypes.c_int], ctypes.c_int),
+    "bcp_task_set_transport": ([_V], ctypes.c_int),
+    "bcp_lb_transport": ([], _V),
+    "bcp_gen_run_procs": ([ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(WorkItem), ctypes.c_size_t, ctypes.c_int,
+                           ctypes.POINTER(ctypes.c_int), _V, ctypes.POINTER(RunStats)], ctypes.c_int),
+    "bcp_rebuild_run_procs": ([ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.POINTER(WorkItem), ctypes.c_size_t,
+                               ctypes.c_char_p, _V, ctypes.POINTER(RunStats)], ctypes.c_int),
     "bcp_assign_lanes": ([ctypes.c_int, ctypes.c_uint64, ctypes.POINTER(FileInfo), ctypes.POINTER(ctypes.c_int)], None),
     "bcp_gen_run": ([ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(WorkItem), ctypes.c_size_t, ctypes.c_int,
                      ctypes.POINTER(ctypes.c_int), _V, ctypes.POINTER(RunStats)], ctypes.c_int),
@@ -434,6 +442,31 @@ def rebuild_run(store_root: str, ntargets: int, rebuild_target: int, items, corr
     return st
 
 
+def gen_run_procs(store_root: str, ntargets: int, items, nlanes: int = 12, lanes=None, log=None) -> RunStats:
+    """bcp_gen_run with every target's rank as its own forked process
+    (socketpair transport).  Only from a process that has not used the GPU."""
+    arr, keep = _items(items)
+    st = RunStats()
+    ln = None
+    if lanes is not None:
+        ln = (ctypes.c_int * max(len(lanes), 1))(*lanes)
+    rc = lib().bcp_gen_run_procs(store_root.encode(), ntargets, arr, len(items), nlanes, ln, log, ctypes.byref(st))
+    check("bcp_gen_run_procs", rc)
+    del keep
+    return st
+
+
+def rebuild_run_procs(store_root: str, ntargets: int, rebuild_target: int, items, corrupt_list: str | None = None,
+                      log=None) -> RunStats:
+    arr, keep = _items(items)
+    st = RunStats()
+    rc = lib().bcp_rebuild_run_procs(store_root.encode(), ntargets, rebuild_target, arr, len(items),
+                                     corrupt_list.encode() if corrupt_list else None, log, ctypes.byref(st))
+    check("bcp_rebuild_run_procs", rc)
+    del keep
+    return st
+
+
 def gen_run_db(store_root: str, ntargets: int, items, nlanes: int = 12, lanes=None, log=None) -> RunStats:
     """bcp_gen_run + per-target DB replicas <root>/st<k>/db (gen/main.c:146-149)."""
     arr, keep = _items(items)
@@ -582,11 +615,12 @@ def set_xor_hook(fn_addr: int | None, ctx: int | None = None):
     lib().bcp_task_set_xor_hook(_V(fn_addr) if fn_addr else None, _V(ctx) if ctx else None)
 
 
-FOLD_ZERO_COPY, FOLD_STAGED = 0, 1
+FOLD_ZERO_COPY, FOLD_STAGED, FOLD_BATCHED = 0, 1, 2
+INJECT_FOLD_RES, INJECT_DRAIN_ROW, INJECT_SEND_BUF, INJECT_THREAD = 1, 2, 4, 8
 
 
 def set_fold_mode(mode: int) -> int:
-    """P-role fold: FOLD_ZERO_COPY (default) or FOLD_STAGED; returns the previous mode."""
+    """P-role fold: FOLD_BATCHED (default), FOLD_ZERO_COPY or FOLD_STAGED; returns the previous mode."""
     rc = lib().bcp_task_set_fold_mode(mode)
     if rc < 0:
         raise BcpError("bcp_task_set_fold_mode", rc)
@@ -595,6 +629,23 @@ def set_fold_mode(mode: int) -> int:
 
 def task_shutdown():
     call("bcp_task_shutdown")
+
+
+def fold_stats() -> tuple[int, int]:
+    """(windows folded, launches) of the batched fold service."""
+    w, l = ctypes.c_uint64(0), ctypes.c_uint64(0)
+    call("bcp_task_fold_stats", ctypes.byref(w), ctypes.byref(l))
+    return w.value, l.value
+
+
+def inject_failure(site: int, after: int = 0, count: int = 1):
+    """Test hook: the next `count` passes through `site` fail after `after` succeed (0 clears)."""
+    call("bcp_task_inject_failure", site, after, count)
+
+
+def set_transport(ops_addr: int | None):
+    """Install a bcp_transport_ops table by address (None: the loopback default)."""
+    call("bcp_task_set_transport", ops_addr)
 
 
 # ---------------------------------------------------------------------------

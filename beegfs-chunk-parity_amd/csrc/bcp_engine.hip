@@ -224,10 +224,16 @@ static int stage_tables(bcp_queue *q, DescSlot *slot, size_t bytes, size_t host_
 // ---------------------------------------------------------------------------
 extern "C" int bcp_abi_version(void) { return BCP_ABI_VERSION; }
 
+// Set once a HIP runtime with a device was initialised by this library: a
+// forked child cannot use it (bcp_gen_run_procs refuses to fork then).
+static std::atomic<int> g_hip_touched{0};
+extern "C" int bcpi_hip_touched(void) { return g_hip_touched.load(std::memory_order_relaxed); }
+
 extern "C" int bcp_device_count(int *count) {
   if (!count) return -EINVAL;
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+  if (n > 0) g_hip_touched.store(1, std::memory_order_relaxed);
   *count = n;
   return 0;
 }
@@ -252,6 +258,7 @@ extern "C" int bcp_engine_create(int device, bcp_engine **out) {
   *out = nullptr;
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return -ENODEV;
+  g_hip_touched.store(1, std::memory_order_relaxed);
   if (device < 0 || device >= n) return -ENODEV;
   hipDeviceProp_t prop;
   HIP_RC(hipGetDeviceProperties(&prop, device));

@@ -406,3 +406,45 @@ int bcp_lb_recv(void *buf, size_t n, int src, int tag, size_t *received)
         return rc;
     return bcp_lb_wait(r, received);
 }
+
+/* ---- the loopback world as a transport table (process_task's default) ---- */
+static int lbt_send(void *ctx, const void *buf, size_t n, int dst, int tag)
+{
+    (void)ctx;
+    return bcp_lb_send(buf, n, dst, tag);
+}
+static int lbt_recv(void *ctx, void *buf, size_t n, int src, int tag)
+{
+    (void)ctx;
+    return bcp_lb_recv(buf, n, src, tag, NULL);
+}
+static int lbt_isend(void *ctx, const void *buf, size_t n, int dst, int tag, void **req)
+{
+    (void)ctx;
+    return bcp_lb_isend(buf, n, dst, tag, (bcp_lb_req **)req);
+}
+static int lbt_irecv(void *ctx, void *buf, size_t n, int src, int tag, void **req)
+{
+    (void)ctx;
+    return bcp_lb_irecv(buf, n, src, tag, (bcp_lb_req **)req);
+}
+static int lbt_wait(void *ctx, void *req)
+{
+    (void)ctx;
+    return bcp_lb_wait((bcp_lb_req *)req, NULL);
+}
+static int lbt_waitall(void *ctx, int n, void **reqs)
+{
+    (void)ctx;
+    return bcp_lb_waitall(n, (bcp_lb_req **)reqs);
+}
+static int lbt_send_fill(void *ctx, bcp_lb_fill_fn fill, void *fctx, size_t n, int dst, int tag)
+{
+    (void)ctx;
+    return bcp_lb_send_fill(fill, fctx, n, dst, tag);
+}
+
+static const bcp_transport_ops g_lb_ops = {NULL,     lbt_send, lbt_recv,    lbt_isend,    lbt_irecv,
+                                           lbt_wait, lbt_waitall, lbt_send_fill};
+
+const bcp_transport_ops *bcp_lb_transport(void) { return &g_lb_ops; }

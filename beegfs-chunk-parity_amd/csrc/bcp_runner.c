@@ -12,9 +12,14 @@
  *                     223-225), and a whole phase-2 round from chunk events
  *                     (gen/main.c:716-797: load DB, plan, run)
  *
- * Every storage target k is loopback rank k+1 (rank 0 is the coordinator,
- * idle here as in the reference's phase 2), with its store at
- * <root>/st<k>/{chunks,parity}.  The worklist is shared memory instead of an
+ * Every storage target k is rank k+1 (rank 0 is the coordinator, idle here
+ * as in the reference's phase 2), with its store at <root>/st<k>/{chunks,
+ * parity}: a set of threads of this process on the loopback transport, or
+ * (bcp_*_run_procs) a process of its own on the socketpair transport, as the
+ * reference's ranks are under mpirun.  Lane threads start behind a gate: if
+ * one cannot be created, none has begun a task, so the others are released
+ * without work and joined, and the run returns -EAGAIN (no partner lane is
+ * ever left waiting for a rank that does not exist).  The worklist is shared memory instead of an
  * MPI_Bcast (gen/main.c:794-797); every rank still walks it in the same order,
  * which is what keeps the per-(pair, tag) message order consistent.
  */
@@ -26,10 +31,11 @@
 #include <stdlib.h>
 #include <string.h>
 #include <sys/stat.h>
+#include <sys/wait.h>
 #include <time.h>
 #include <unistd.h>
 
-#include "bcp_task.h"
+#include "bcp_host.h"
 
 #define PER_LANE 16
 #define LANE_MASK 15
@@ -144,6 +150,42 @@ static void close_store(HostState *hs, int rebuilding)
                 hs->error_path ? hs->error_path : "?", hs->error, strerror(hs->error), hs->storage_target);
 }
 
+/* ---- start gate ----------------------------------------------------------- */
+typedef struct {
+    pthread_mutex_t mu;
+    pthread_cond_t cv;
+    int open, cancel;
+} start_gate;
+
+#define START_GATE_INIT {PTHREAD_MUTEX_INITIALIZER, PTHREAD_COND_INITIALIZER, 0, 0}
+
+/* Lane side: wait until the runner opens the gate; 1 = run, 0 = cancelled. */
+static int gate_pass(start_gate *g)
+{
+    pthread_mutex_lock(&g->mu);
+    while (!g->open)
+        pthread_cond_wait(&g->cv, &g->mu);
+    const int run = !g->cancel;
+    pthread_mutex_unlock(&g->mu);
+    return run;
+}
+
+static void gate_open(start_gate *g, int cancel)
+{
+    pthread_mutex_lock(&g->mu);
+    g->cancel = cancel;
+    g->open = 1;
+    pthread_cond_broadcast(&g->cv);
+    pthread_mutex_unlock(&g->mu);
+}
+
+static int spawn(pthread_t *th, void *(*fn)(void *), void *arg)
+{
+    if (bcpi_inject_hit(BCP_INJECT_THREAD))
+        return EAGAIN;
+    return pthread_create(th, NULL, fn, arg);
+}
+
 /* ---- generation lanes --------------------------------------------------- */
 
 typedef struct {
@@ -154,6 +196,7 @@ typedef struct {
     int lane;
     int rank;
     bcp_pdb *db;         /* this rank's replica, or NULL */
+    start_gate *gate;
     ProgressSample sample;
     uint64_t tasks;
     int db_rc;
@@ -163,6 +206,8 @@ typedef struct {
 static void *gen_lane(void *p)
 {
     lane_arg *a = p;
+    if (!gate_pass(a->gate))
+        return NULL;
     bcp_lb_set_rank(a->rank);
     TaskInfo ti = {a->hs->read_chunk_dir, 0, -1, a->lane, &a->sample};
     for (size_t i = 0; i < a->nitems; i++) {
@@ -274,9 +319,10 @@ static int gen_run_impl(const char *store_root, int ntargets, const bcp_work_ite
             goto out;
     }
     double t0 = now_s();
-    int started = 0;
-    for (int k = 0; k < ntargets; k++)
-        for (int l = 0; l < nlanes; l++) {
+    int started = 0, spawn_rc = 0;
+    start_gate gate = START_GATE_INIT;
+    for (int k = 0; k < ntargets && !spawn_rc; k++)
+        for (int l = 0; l < nlanes && !spawn_rc; l++) {
             lane_arg *a = &args[k * nlanes + l];
             a->hs = &hs[k];
             a->items = items;
@@ -285,15 +331,20 @@ static int gen_run_impl(const char *store_root, int ntargets, const bcp_work_ite
             a->lane = l;
             a->rank = k + 1;
             a->db = dbs[k];
-            if (pthread_create(&th[started], NULL, gen_lane, a) != 0) {
-                /* cannot leave partner lanes blocked: give up loudly */
-                fprintf(stderr, "bcp_gen_run: thread create failed\n");
-                abort();
-            }
-            started++;
+            a->gate = &gate;
+            if ((spawn_rc = spawn(&th[started], gen_lane, a)) == 0)
+                started++;
         }
+    gate_open(&gate, spawn_rc != 0);
     for (int i = 0; i < started; i++)
         pthread_join(th[i], NULL);
+    if (spawn_rc) {
+        if (log)
+            fprintf(log, "bcp_gen_run: lane thread %d of %d not created (%s); no task was started\n", started,
+                    ntargets * nlanes, strerror(spawn_rc));
+        rc = -EAGAIN;
+        goto out;
+    }
     if (stats) {
         memset(stats, 0, sizeof(*stats));
         stats->seconds = now_s() - t0;
@@ -339,6 +390,7 @@ typedef struct {
     size_t nitems;
     int rebuild_target;
     int rank;
+    start_gate *gate;
     ProgressSample sample;
     uint64_t tasks;
 } rebuild_arg;
@@ -347,6 +399,8 @@ typedef struct {
 static void *rebuild_rank(void *p)
 {
     rebuild_arg *a = p;
+    if (a->gate && !gate_pass(a->gate))
+        return NULL;
     bcp_lb_set_rank(a->rank);
     const int my_st = a->hs->storage_target;
     const int victim = a->rebuild_target;
@@ -407,15 +461,23 @@ int bcp_rebuild_run(const char *store_root, int ntargets, int rebuild_target, co
         if ((rc = open_store(store_root, k, 1, corrupt_fd, log, &hs[k])))
             goto out;
     double t0 = now_s();
-    for (int k = 0; k < ntargets; k++) {
-        args[k] = (rebuild_arg){&hs[k], items, nitems, rebuild_target, k + 1, PROGRESS_SAMPLE_INIT, 0};
-        if (pthread_create(&th[k], NULL, rebuild_rank, &args[k]) != 0) {
-            fprintf(stderr, "bcp_rebuild_run: thread create failed\n");
-            abort();
-        }
+    int started = 0, spawn_rc = 0;
+    start_gate gate = START_GATE_INIT;
+    for (int k = 0; k < ntargets && !spawn_rc; k++) {
+        args[k] = (rebuild_arg){&hs[k], items, nitems, rebuild_target, k + 1, &gate, PROGRESS_SAMPLE_INIT, 0};
+        if ((spawn_rc = spawn(&th[k], rebuild_rank, &args[k])) == 0)
+            started++;
     }
-    for (int k = 0; k < ntargets; k++)
+    gate_open(&gate, spawn_rc != 0);
+    for (int k = 0; k < started; k++)
         pthread_join(th[k], NULL);
+    if (spawn_rc) {
+        if (log)
+            fprintf(log, "bcp_rebuild_run: rank thread %d of %d not created (%s); no task was started\n", started,
+                    ntargets, strerror(spawn_rc));
+        rc = -EAGAIN;
+        goto out;
+    }
     if (stats) {
         memset(stats, 0, sizeof(*stats));
         stats->seconds = now_s() - t0;
@@ -582,4 +644,225 @@ int bcp_gen_round_pipeline(bcp_pipeline *pl, const char *store_root, int ntarget
     if (!pl)
         return -EINVAL;
     return round_impl(pl, store_root, ntargets, events, cum_weight, 0, log, stats, nplanned);
+}
+
+/* ---- ranks as processes (bcp_gen_run_procs / bcp_rebuild_run_procs) -------
+ * One forked process per storage target, connected by a bcp_sock_world --
+ * the shape of the reference's deployment (one MPI process per target,
+ * src/beegfs-parity-gen:114-127).  Children wait on a start pipe, so a failed
+ * fork cancels the run before any rank has begun a task; each child reports
+ * its counters through a result pipe (one record < PIPE_BUF: atomic). */
+typedef struct {
+    int rank;
+    int error;        /* the rank's sticky error at the end */
+    int rc;           /* setup failure inside the child, 0 = ran */
+    uint64_t tasks, bytes_read, bytes_written;
+} rank_report;
+
+typedef struct {
+    const char *root;
+    int ntargets, nlanes, rebuilding, rebuild_target, corrupt_fd;
+    const bcp_work_item *items;
+    size_t nitems;
+    const int *lanes;
+    FILE *log;
+} procs_job;
+
+/* The body of rank process k+1 (never returns). */
+static void rank_child(const procs_job *J, bcp_sock_world *w, int k, int go_fd, int res_fd)
+{
+    rank_report rep = {k + 1, 0, 0, 0, 0, 0};
+    char go = 0;
+    ssize_t g = read(go_fd, &go, 1); /* EOF: the run was cancelled */
+    close(go_fd);
+    if (g != 1)
+        _exit(0);
+    bcp_transport_ops ops;
+    HostState hs;
+    int rc = bcp_sock_world_attach(w, k + 1, &ops);
+    if (!rc)
+        rc = bcp_task_set_transport(&ops);
+    if (!rc)
+        rc = open_store(J->root, k, J->rebuilding, J->corrupt_fd, J->log, &hs);
+    if (!rc && !J->rebuilding) {
+        lane_arg *args = calloc((size_t)J->nlanes, sizeof(lane_arg));
+        pthread_t *th = calloc((size_t)J->nlanes, sizeof(pthread_t));
+        start_gate gate = START_GATE_INIT;
+        int started = 0, src = 0;
+        if (!args || !th)
+            src = ENOMEM;
+        for (int l = 0; l < J->nlanes && !src; l++) {
+            args[l] = (lane_arg){&hs, J->items, J->nitems, J->lanes, l, k + 1, NULL, &gate, PROGRESS_SAMPLE_INIT, 0, 0};
+            if ((src = spawn(&th[l], gen_lane, &args[l])) == 0)
+                started++;
+        }
+        /* A rank whose lanes cannot all start fails as a whole: its lanes
+         * are released without work, the process exits, and its partners see
+         * its sockets close and fail the tasks they share with it. */
+        gate_open(&gate, src != 0);
+        for (int l = 0; l < started; l++)
+            pthread_join(th[l], NULL);
+        for (int l = 0; l < started && !src; l++) {
+            rep.tasks += args[l].tasks;
+            rep.bytes_read += args[l].sample.bytes_read;
+            rep.bytes_written += args[l].sample.bytes_written;
+        }
+        rc = src ? -src : 0;
+        free(args);
+        free(th);
+    } else if (!rc) {
+        rebuild_arg a = {&hs, J->items, J->nitems, J->rebuild_target, k + 1, NULL, PROGRESS_SAMPLE_INIT, 0};
+        rebuild_rank(&a);
+        rep.tasks = a.tasks;
+        rep.bytes_read = a.sample.bytes_read;
+        rep.bytes_written = a.sample.bytes_written;
+    }
+    if (!rc) {
+        rep.error = hs.error;
+        close_store(&hs, J->rebuilding);
+    }
+    rep.rc = rc;
+    bcp_task_shutdown();
+    ssize_t wr = write(res_fd, &rep, sizeof(rep));
+    (void)wr;
+    close(res_fd);
+    bcp_sock_world_destroy(w);
+    _exit(rc ? 2 : 0);
+}
+
+static int run_procs(const procs_job *J, bcp_run_stats *stats)
+{
+    if (bcpi_hip_touched())
+        return -EBUSY; /* children could not use the HIP runtime of this process */
+    for (int k = 0; k < MAX_STORAGE_TARGETS; k++)
+        st2rank[k] = k < J->ntargets ? k + 1 : -1;
+    bcp_sock_world *w = NULL;
+    int rc = bcp_sock_world_create(J->ntargets + 1, &w);
+    if (rc)
+        return rc;
+    int go[2] = {-1, -1}, res[2] = {-1, -1};
+    pid_t *pids = calloc((size_t)J->ntargets, sizeof(pid_t));
+    if (!pids || pipe(go) != 0 || pipe(res) != 0) {
+        rc = pids ? -errno : -ENOMEM;
+        goto out;
+    }
+    if (J->log)
+        fflush(J->log);
+    fflush(stdout);
+    fflush(stderr);
+    int nforked = 0;
+    for (int k = 0; k < J->ntargets; k++) {
+        pid_t pid = fork();
+        if (pid == 0) {
+            close(go[1]);
+            close(res[0]);
+            rank_child(J, w, k, go[0], res[1]);
+        }
+        if (pid < 0) {
+            rc = -errno;
+            break;
+        }
+        pids[nforked++] = pid;
+    }
+    close(go[0]);
+    close(res[1]);
+    go[0] = res[1] = -1;
+    bcp_sock_world_destroy(w); /* the ranks hold their own ends now */
+    w = NULL;
+    double t0 = now_s();
+    if (!rc) {
+        char buf[MAX_STORAGE_TARGETS];
+        memset(buf, 1, sizeof(buf));
+        if (write(go[1], buf, (size_t)nforked) != (ssize_t)nforked)
+            rc = -EPIPE;
+    }
+    close(go[1]); /* cancels whoever has not read a go byte */
+    go[1] = -1;
+    int died = 0;
+    for (int i = 0; i < nforked; i++) {
+        int status = 0;
+        while (waitpid(pids[i], &status, 0) < 0 && errno == EINTR)
+            ;
+        if (!WIFEXITED(status) || WEXITSTATUS(status) != 0)
+            died++;
+    }
+    double secs = now_s() - t0;
+    bcp_run_stats st;
+    memset(&st, 0, sizeof(st));
+    st.seconds = secs;
+    rank_report rep;
+    int got = 0;
+    while (read(res[0], &rep, sizeof(rep)) == (ssize_t)sizeof(rep)) {
+        got++;
+        st.tasks += rep.tasks;
+        st.bytes_read += rep.bytes_read;
+        st.bytes_written += rep.bytes_written;
+        st.errors += rep.error != 0;
+        if (rep.rc && !rc)
+            rc = rep.rc;
+    }
+    if (!rc && (died || got != nforked))
+        rc = -ECHILD;
+    if (stats)
+        *stats = st;
+out:
+    for (int i = 0; i < 2; i++) {
+        if (go[i] >= 0)
+            close(go[i]);
+        if (res[i] >= 0)
+            close(res[i]);
+    }
+    if (w)
+        bcp_sock_world_destroy(w);
+    free(pids);
+    return rc;
+}
+
+int bcp_gen_run_procs(const char *store_root, int ntargets, const bcp_work_item *items, size_t nitems, int nlanes,
+                      const int *lanes_in, FILE *log, bcp_run_stats *stats)
+{
+    if (!store_root || ntargets < 1 || ntargets > MAX_STORAGE_TARGETS || nlanes < 1 || nlanes > 64 ||
+        (nitems && !items))
+        return -EINVAL;
+    int rc = check_items(ntargets, items, nitems);
+    if (rc)
+        return rc;
+    int *lanes = NULL;
+    if (!lanes_in) {
+        FileInfo *fis = malloc((nitems ? nitems : 1) * sizeof(FileInfo));
+        lanes = malloc((nitems ? nitems : 1) * sizeof(int));
+        if (!fis || !lanes) {
+            free(fis);
+            free(lanes);
+            return -ENOMEM;
+        }
+        for (size_t i = 0; i < nitems; i++)
+            fis[i] = items[i].fi;
+        bcp_assign_lanes(nlanes, nitems, fis, lanes);
+        free(fis);
+    }
+    procs_job J = {store_root, ntargets, nlanes, 0, -1, -1, items, nitems, lanes_in ? lanes_in : lanes, log};
+    rc = run_procs(&J, stats);
+    free(lanes);
+    return rc;
+}
+
+int bcp_rebuild_run_procs(const char *store_root, int ntargets, int rebuild_target, const bcp_work_item *items,
+                          size_t nitems, const char *corrupt_list_path, FILE *log, bcp_run_stats *stats)
+{
+    if (!store_root || ntargets < 2 || ntargets > MAX_STORAGE_TARGETS || rebuild_target < 0 ||
+        rebuild_target >= ntargets || (nitems && !items))
+        return -EINVAL;
+    int rc = check_items(ntargets, items, nitems);
+    if (rc)
+        return rc;
+    int corrupt_fd = corrupt_list_path
+                         ? open(corrupt_list_path, O_WRONLY | O_CREAT | O_TRUNC | O_APPEND, S_IRUSR | S_IWUSR)
+                         : open("/dev/null", O_WRONLY);
+    if (corrupt_fd < 0)
+        return -errno;
+    procs_job J = {store_root, ntargets, 1, 1, rebuild_target, corrupt_fd, items, nitems, NULL, log};
+    rc = run_procs(&J, stats);
+    close(corrupt_fd);
+    return rc;
 }

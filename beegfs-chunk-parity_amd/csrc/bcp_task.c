@@ -2,18 +2,24 @@
  * bcp_task.c -- the per-rank chunk-streaming protocol (process_task) with the
  * P role's fold on the GPU.
  *
- * Follows the reference's roles and message flow
+ * Behaviour follows the reference's roles and message flow
  * (src/beegfs-raid5/common/task_processing.c):
  *   process_task      :325-340  dispatch by role
  *   parity_generator  :117-245  P role: sizes -> max_cs -> windows -> parity
  *   chunk_sender      :247-322  source role: size -> windows (zero padded)
- * over the loopback transport (bcp_loopback.c) instead of MPI.  The window
- * fold (xor_parity at :211) becomes one XOR kernel on the lane's own HIP
- * queue that reads the pinned window rows (256-byte pitch, so every row is
- * 16-byte aligned for the fast kernel) and writes the pinned parity block in
- * place over PCIe (zero copy; the staged H2D -> kernel -> D2H form is kept as
- * bcp_task_set_fold_mode(BCP_FOLD_STAGED)).  Twelve lanes per rank keep
- * twelve queues of folds in flight on the device.
+ * What is underneath is this library's:
+ *   - the peers are reached through a transport table (bcp_task_set_transport:
+ *     in-process loopback ranks by default, socketpair-connected rank
+ *     processes, or an MPI binding), exactly the point-to-point subset the
+ *     reference uses;
+ *   - the window fold (xor_parity at :211) runs on the GPU over pinned,
+ *     device-mapped window rows (256-byte pitch, so every row is 16-byte
+ *     aligned for the streaming kernel): per lane on its own HIP queue
+ *     (ZERO_COPY, STAGED) or through a per-device fold service that batches
+ *     the pending windows of every lane and rank into one launch (BATCHED);
+ *   - nothing aborts: when the P role cannot get fold resources it still
+ *     drains its senders through one bounded row and raises the sticky error;
+ *     a source without a window buffer sends zeros and raises it.
  */
 #define _GNU_SOURCE
 #include <assert.h>
@@ -27,11 +33,12 @@
 #include <sys/types.h>
 #include <unistd.h>
 
-#include "bcp_task.h"
+#include "bcp_host.h"
 
 #define WINDOW ((uint64_t)BCP_WINDOW_BYTES)
 #define ROW_ALIGN 256u
 #define MAX_DEVICES 64
+#define DRAIN_SMALL 16384u
 
 __attribute__((weak)) int st2rank[MAX_STORAGE_TARGETS];
 
@@ -46,7 +53,7 @@ __attribute__((weak)) int st2rank[MAX_STORAGE_TARGETS];
 #define MIN_(a, b) ((a) < (b) ? (a) : (b))
 #define MAX_(a, b) ((a) > (b) ? (a) : (b))
 
-/* ---- engines / device map / test hook ---------------------------------- */
+/* ---- global state: engines, device map, test hook, transport ------------ */
 static pthread_mutex_t g_lock = PTHREAD_MUTEX_INITIALIZER;
 static bcp_engine *g_engines[MAX_DEVICES];
 static int g_engine_rc[MAX_DEVICES];
@@ -54,7 +61,13 @@ static int g_devmap[MAX_STORAGE_TARGETS];
 static int g_devmap_n = 0;
 static bcp_xor_hook_fn g_hook = NULL;
 static void *g_hook_ctx = NULL;
-static int g_fold_mode = BCP_FOLD_ZERO_COPY;
+static int g_fold_mode = BCP_FOLD_BATCHED;
+static bcp_transport_ops g_tp;
+static int g_tp_set = 0;
+
+/* Never written: the source role's windows when it has no buffer of its own
+ * (zero pages until read; .bss costs no file or resident memory). */
+static uint8_t g_zero_window[BCP_WINDOW_BYTES];
 
 int bcp_task_set_device_map(const int *devices, int ntargets)
 {
@@ -70,7 +83,7 @@ int bcp_task_set_device_map(const int *devices, int ntargets)
 
 int bcp_task_set_fold_mode(int mode)
 {
-    if (mode != BCP_FOLD_ZERO_COPY && mode != BCP_FOLD_STAGED)
+    if (mode != BCP_FOLD_ZERO_COPY && mode != BCP_FOLD_STAGED && mode != BCP_FOLD_BATCHED)
         return -EINVAL;
     pthread_mutex_lock(&g_lock);
     int prev = g_fold_mode;
@@ -85,6 +98,73 @@ void bcp_task_set_xor_hook(bcp_xor_hook_fn fn, void *ctx)
     g_hook = fn;
     g_hook_ctx = ctx;
     pthread_mutex_unlock(&g_lock);
+}
+
+int bcp_task_set_transport(const bcp_transport_ops *ops)
+{
+    if (ops && (!ops->send || !ops->recv || !ops->isend || !ops->irecv || !ops->wait || !ops->waitall))
+        return -EINVAL;
+    pthread_mutex_lock(&g_lock);
+    if (ops)
+        g_tp = *ops;
+    g_tp_set = ops != NULL;
+    pthread_mutex_unlock(&g_lock);
+    return 0;
+}
+
+/* The transport of one task (a snapshot: stable for the task's duration). */
+static bcp_transport_ops transport_now(void)
+{
+    pthread_mutex_lock(&g_lock);
+    bcp_transport_ops t = g_tp_set ? g_tp : *bcp_lb_transport();
+    pthread_mutex_unlock(&g_lock);
+    return t;
+}
+
+/* ---- failure injection (tests) ------------------------------------------ */
+#define NSITES 4
+static int g_inj_after[NSITES], g_inj_count[NSITES];
+
+static int site_index(int site)
+{
+    switch (site) {
+    case BCP_INJECT_FOLD_RES: return 0;
+    case BCP_INJECT_DRAIN_ROW: return 1;
+    case BCP_INJECT_SEND_BUF: return 2;
+    case BCP_INJECT_THREAD: return 3;
+    default: return -1;
+    }
+}
+
+int bcp_task_inject_failure(int site, int after, int count)
+{
+    const int i = site_index(site);
+    if (i < 0 || after < 0 || count < 0)
+        return -EINVAL;
+    pthread_mutex_lock(&g_lock);
+    g_inj_after[i] = after;
+    g_inj_count[i] = count;
+    pthread_mutex_unlock(&g_lock);
+    return 0;
+}
+
+int bcpi_inject_hit(int site)
+{
+    const int i = site_index(site);
+    if (i < 0)
+        return 0;
+    int hit = 0;
+    pthread_mutex_lock(&g_lock);
+    if (g_inj_count[i] > 0) {
+        if (g_inj_after[i] > 0)
+            g_inj_after[i]--;
+        else {
+            g_inj_count[i]--;
+            hit = 1;
+        }
+    }
+    pthread_mutex_unlock(&g_lock);
+    return hit;
 }
 
 static int engine_for_target(int st, bcp_engine **out, int *device)
@@ -110,17 +190,192 @@ static int engine_for_target(int st, bcp_engine **out, int *device)
     return rc;
 }
 
+/* ---- fold service (BCP_FOLD_BATCHED) --------------------------------------
+ * One per device.  P roles append their window (rows + output, mapped pinned
+ * memory) and sleep; the flusher takes EVERYTHING pending, folds it with one
+ * descriptor batch on its own queue, syncs once and wakes the lanes whose
+ * windows were in it.  While a batch is on the device the next one gathers,
+ * so the batch size follows the load: one window when a lane is alone, up to
+ * every concurrent P role when all twelve lanes of every rank fold at once. */
+typedef struct fold_job {
+    struct fold_job *next;
+    const uint8_t *rows;
+    size_t pitch, nbytes;
+    int n;
+    uint8_t *out;
+    int done, rc;
+} fold_job;
+
+typedef struct {
+    bcp_engine *eng;
+    bcp_queue *q;
+    pthread_t th;
+    int stop;
+    pthread_mutex_t mu;
+    pthread_cond_t cv_work, cv_done;
+    fold_job *head, *tail;
+    bcp_stripe *st;
+    bcp_source *so;
+    size_t st_cap, so_cap;
+    uint64_t windows, launches;
+} fold_svc;
+
+static fold_svc *g_svc[MAX_DEVICES];
+static uint64_t g_svc_windows, g_svc_launches; /* of services already shut down */
+
+static int svc_tables(fold_svc *S, size_t nst, size_t nso)
+{
+    if (nst > S->st_cap) {
+        bcp_stripe *p = realloc(S->st, nst * 2 * sizeof(*p));
+        if (!p)
+            return -ENOMEM;
+        S->st = p;
+        S->st_cap = nst * 2;
+    }
+    if (nso > S->so_cap) {
+        bcp_source *p = realloc(S->so, nso * 2 * sizeof(*p));
+        if (!p)
+            return -ENOMEM;
+        S->so = p;
+        S->so_cap = nso * 2;
+    }
+    return 0;
+}
+
+static void *svc_main(void *p)
+{
+    fold_svc *S = p;
+    pthread_mutex_lock(&S->mu);
+    for (;;) {
+        while (!S->head && !S->stop)
+            pthread_cond_wait(&S->cv_work, &S->mu);
+        if (!S->head)
+            break; /* stop, nothing pending */
+        fold_job *batch = S->head;
+        S->head = S->tail = NULL;
+        pthread_mutex_unlock(&S->mu);
+        size_t nst = 0, nso = 0;
+        for (fold_job *j = batch; j; j = j->next) {
+            nst++;
+            nso += (size_t)j->n;
+        }
+        int rc = nst > 0xFFFFFFFFu || nso > 0xFFFFFFFFu ? -EINVAL : svc_tables(S, nst, nso);
+        if (!rc) {
+            size_t i = 0, k = 0;
+            for (fold_job *j = batch; j; j = j->next, i++) {
+                S->st[i] = (bcp_stripe){(uint64_t)(uintptr_t)j->out, j->nbytes, (uint32_t)k, (uint32_t)j->n, 0};
+                for (int r = 0; r < j->n; r++, k++)
+                    S->so[k] = (bcp_source){(uint64_t)(uintptr_t)(j->rows + (size_t)r * j->pitch), j->nbytes};
+            }
+            rc = bcp_xor_stripes_async(S->q, S->st, (uint32_t)nst, S->so, (uint32_t)nso);
+            if (!rc)
+                rc = bcp_queue_sync(S->q);
+        }
+        pthread_mutex_lock(&S->mu);
+        for (fold_job *j = batch, *nx; j; j = nx) {
+            nx = j->next; /* j lives on its lane's stack: read next before done */
+            j->rc = rc;
+            j->done = 1;
+        }
+        S->windows += nst;
+        S->launches += 1;
+        pthread_cond_broadcast(&S->cv_done);
+    }
+    pthread_mutex_unlock(&S->mu);
+    return NULL;
+}
+
+static void svc_destroy(fold_svc *S)
+{
+    if (!S)
+        return;
+    if (S->q)
+        bcp_queue_destroy(S->q);
+    pthread_cond_destroy(&S->cv_work);
+    pthread_cond_destroy(&S->cv_done);
+    pthread_mutex_destroy(&S->mu);
+    free(S->st);
+    free(S->so);
+    free(S);
+}
+
+/* The service of device dev (started on first use; under g_lock). */
+static int svc_get(int dev, bcp_engine *e, fold_svc **out)
+{
+    pthread_mutex_lock(&g_lock);
+    fold_svc *S = g_svc[dev];
+    int rc = 0;
+    if (!S) {
+        S = calloc(1, sizeof(*S));
+        if (!S)
+            rc = -ENOMEM;
+        else {
+            S->eng = e;
+            pthread_mutex_init(&S->mu, NULL);
+            pthread_cond_init(&S->cv_work, NULL);
+            pthread_cond_init(&S->cv_done, NULL);
+            if ((rc = bcp_queue_create(e, &S->q)) || (rc = -pthread_create(&S->th, NULL, svc_main, S))) {
+                svc_destroy(S);
+                S = NULL;
+            } else {
+                g_svc[dev] = S;
+            }
+        }
+    }
+    pthread_mutex_unlock(&g_lock);
+    *out = S;
+    return rc;
+}
+
+static int fold_batched(fold_svc *S, const uint8_t *rows, size_t pitch, size_t nbytes, int n, uint8_t *out)
+{
+    fold_job j = {NULL, rows, pitch, nbytes, n, out, 0, 0};
+    pthread_mutex_lock(&S->mu);
+    if (S->tail)
+        S->tail->next = &j;
+    else
+        S->head = &j;
+    S->tail = &j;
+    pthread_cond_signal(&S->cv_work);
+    while (!j.done)
+        pthread_cond_wait(&S->cv_done, &S->mu);
+    pthread_mutex_unlock(&S->mu);
+    return j.rc;
+}
+
+int bcp_task_fold_stats(uint64_t *windows, uint64_t *launches)
+{
+    uint64_t w = 0, l = 0;
+    pthread_mutex_lock(&g_lock);
+    w = g_svc_windows;
+    l = g_svc_launches;
+    for (int d = 0; d < MAX_DEVICES; d++)
+        if (g_svc[d]) {
+            pthread_mutex_lock(&g_svc[d]->mu);
+            w += g_svc[d]->windows;
+            l += g_svc[d]->launches;
+            pthread_mutex_unlock(&g_svc[d]->mu);
+        }
+    pthread_mutex_unlock(&g_lock);
+    if (windows)
+        *windows = w;
+    if (launches)
+        *launches = l;
+    return 0;
+}
+
 /* ---- fold resources: a shared pool, reused across tasks, lanes and runs --
- * One resource = one HIP queue + pinned window rows + device buffers.  The P
- * role takes one for the duration of a task and gives it back, so a
- * long-running rank pays queue creation and page pinning once, not per task
- * or per lane thread.  Host-only resources (test hook) use plain memory. */
+ * One resource = pinned, device-mapped window rows + output block (+ a HIP
+ * queue and device buffers for the per-lane fold modes, made on first use).
+ * The P role takes one for the duration of a task and gives it back, so a
+ * long-running rank pays page pinning once, not per task or per lane thread.
+ * Host-only resources (test hook) use plain memory. */
 typedef struct fold_res {
     struct fold_res *next;
     int device;         /* -1: host-only (hook) */
     bcp_engine *eng;
-    bcp_queue *q;
-    uint8_t *h_win[2];  /* window rows [n][pitch] (pinned when device >= 0) */
+    bcp_queue *q;       /* ZERO_COPY / STAGED only */
+    uint8_t *h_win[2];  /* window rows [n][pitch] (pinned + mapped when device >= 0) */
     uint8_t *h_par;     /* fold output */
     size_t h_cap, h_cap1, hp_cap;
     void *d_src, *d_out;
@@ -172,6 +427,29 @@ void bcp_task_thread_release(void)
 int bcp_task_shutdown(void)
 {
     bcp_task_thread_release();
+    /* fold services first: they hold queues on the engines */
+    fold_svc *svc[MAX_DEVICES];
+    pthread_mutex_lock(&g_lock);
+    for (int d = 0; d < MAX_DEVICES; d++) {
+        svc[d] = g_svc[d];
+        g_svc[d] = NULL;
+    }
+    pthread_mutex_unlock(&g_lock);
+    for (int d = 0; d < MAX_DEVICES; d++) {
+        fold_svc *S = svc[d];
+        if (!S)
+            continue;
+        pthread_mutex_lock(&S->mu);
+        S->stop = 1;
+        pthread_cond_signal(&S->cv_work);
+        pthread_mutex_unlock(&S->mu);
+        pthread_join(S->th, NULL);
+        pthread_mutex_lock(&g_lock);
+        g_svc_windows += S->windows;
+        g_svc_launches += S->launches;
+        pthread_mutex_unlock(&g_lock);
+        svc_destroy(S);
+    }
     pthread_mutex_lock(&g_lock);
     fold_res *R = g_pool;
     g_pool = NULL;
@@ -242,6 +520,8 @@ static int res_acquire(HostState *hs, int use_gpu, size_t rows_bytes, size_t nby
     int rc = 0, dev = -1;
     bcp_engine *e = NULL;
     *out = NULL;
+    if (bcpi_inject_hit(BCP_INJECT_FOLD_RES))
+        return -ENOMEM;
     if (use_gpu && (rc = engine_for_target(hs->storage_target, &e, &dev)))
         return rc;
     /* prefer a free resource of the same device that is already big enough */
@@ -270,10 +550,6 @@ static int res_acquire(HostState *hs, int use_gpu, size_t rows_bytes, size_t nby
             return -ENOMEM;
         R->device = dev;
         R->eng = e;
-        if (use_gpu && (rc = bcp_queue_create(e, &R->q))) {
-            free(R);
-            return rc;
-        }
     }
     if ((rc = grow(R, &R->h_win[0], &R->h_cap, rows_bytes)) || (rc = grow(R, &R->h_win[1], &R->h_cap1, rows_bytes)) ||
         (rc = grow(R, &R->h_par, &R->hp_cap, nbytes)))
@@ -300,6 +576,14 @@ static int fold_window(fold_res *R, HostState *hs, bcp_xor_hook_fn hook, void *c
     pthread_mutex_lock(&g_lock);
     const int mode = g_fold_mode;
     pthread_mutex_unlock(&g_lock);
+    if (mode == BCP_FOLD_BATCHED) {
+        fold_svc *S = NULL;
+        if ((rc = svc_get(R->device, R->eng, &S)))
+            return rc;
+        return fold_batched(S, rows, pitch, nbytes, n, out);
+    }
+    if (!R->q && (rc = bcp_queue_create(R->eng, &R->q)))
+        return rc;
     if (mode == BCP_FOLD_ZERO_COPY) {
         /* rows and out are mapped pinned memory (grow): the kernel streams
          * them over PCIe, no copy commands */
@@ -386,9 +670,69 @@ static int raise_sticky_error(HostState *hs, int err, const char *path)
     return 1;
 }
 
+/* errno value for the sticky error from a negative library / transport code */
+static int as_errno(int rc) { return rc < 0 ? -rc : (rc ? rc : EIO); }
+
 /* ---- roles ------------------------------------------------------------- */
 
-static void parity_generator(const char *path, const FileInfo *task, TaskInfo ti, HostState *hs)
+/* Post one receive per source (window row j at base + j * pitch).  Every
+ * source gets its receive even if an earlier post failed (a live sender must
+ * never be left blocked); a failed post leaves its slot NULL.  Returns the
+ * first error. */
+static int post_recvs(const bcp_transport_ops *T, void **req, int n, uint8_t *base, size_t pitch, size_t len,
+                      const int *ranks, int tag)
+{
+    int first = 0;
+    for (int j = 0; j < n; j++) {
+        req[j] = NULL;
+        int rc = T->irecv(T->ctx, base + (size_t)j * pitch, len, ranks[j], tag, &req[j]);
+        if (rc) {
+            req[j] = NULL;
+            if (!first)
+                first = rc;
+        }
+    }
+    return first;
+}
+
+/* Wait for every request actually posted (never leave a receive pending on
+ * a buffer that goes away); returns the first error. */
+static int wait_posted(const bcp_transport_ops *T, void **req, int n)
+{
+    void *live[MAX_STORAGE_TARGETS];
+    int m = 0;
+    for (int j = 0; j < n; j++)
+        if (req[j])
+            live[m++] = req[j];
+    for (int j = 0; j < n; j++)
+        req[j] = NULL;
+    return m ? T->waitall(T->ctx, m, live) : 0;
+}
+
+/* The P role without fold resources: every window of every source is still
+ * received (the senders block until it is), source by source into ONE row
+ * reused for all of them; without even that row, into a 16 KiB stack row
+ * with truncating receives.  Nothing is folded or written. */
+static int drain_windows(const bcp_transport_ops *T, const int *ranks, int n, size_t buffer_size,
+                         uint64_t expected_messages, int tag)
+{
+    uint8_t small[DRAIN_SMALL];
+    uint8_t *row = bcpi_inject_hit(BCP_INJECT_DRAIN_ROW) ? NULL : malloc(buffer_size ? buffer_size : 1);
+    uint8_t *dst = row ? row : small;
+    const size_t cap = row ? buffer_size : MIN_(buffer_size, (size_t)DRAIN_SMALL);
+    int rc = 0;
+    for (uint64_t w = 0; w < expected_messages; w++)
+        for (int j = 0; j < n; j++) {
+            int e = T->recv(T->ctx, dst, cap, ranks[j], tag);
+            if (e && e != -EMSGSIZE && !rc)
+                rc = e;
+        }
+    free(row);
+    return rc;
+}
+
+static void parity_generator(const bcp_transport_ops *T, const char *path, const FileInfo *task, TaskInfo ti,
+                             HostState *hs)
 {
     const int n = active_ranks(task->locations);
     int ranks[MAX_STORAGE_TARGETS];
@@ -402,22 +746,40 @@ static void parity_generator(const char *path, const FileInfo *task, TaskInfo ti
         return;
     }
 
-    bcp_lb_req *req[MAX_STORAGE_TARGETS];
+    void *req[MAX_STORAGE_TARGETS];
     uint64_t chunk_sizes[MAX_STORAGE_TARGETS] = {0};
+    int have_had_error = 0, trc = 0;
     if (ti.is_rebuilding) {
-        bcp_lb_recv(chunk_sizes, (size_t)n * sizeof(uint64_t), st2rank[ti.actual_P_st], ti.tag, NULL);
+        /* the parity holder forwards the stored header (:149-156) */
+        trc = T->recv(T->ctx, chunk_sizes, (size_t)n * sizeof(uint64_t), st2rank[ti.actual_P_st], ti.tag);
     } else {
-        for (int j = 0; j < n; j++)
-            bcp_lb_irecv(&chunk_sizes[j], sizeof(uint64_t), ranks[j], ti.tag, &req[j]);
-        bcp_lb_waitall(n, req);
+        trc = post_recvs(T, req, n, (uint8_t *)chunk_sizes, sizeof(uint64_t), sizeof(uint64_t), ranks, ti.tag);
+        int w = wait_posted(T, req, n);
+        trc = trc ? trc : w;
+    }
+    if (trc) {
+        have_had_error = as_errno(trc);
+        LOGERR("chunk sizes for '%s' not received: %s\n", path, strerror(have_had_error));
     }
 
     uint64_t max_cs = 0;
     for (int j = 0; j < n; j++)
         max_cs = MAX_(max_cs, chunk_sizes[j]);
     for (int j = 0; j < n; j++)
-        bcp_lb_isend(&max_cs, sizeof(max_cs), ranks[j], ti.tag, &req[j]);
-    bcp_lb_waitall(n, req);
+        req[j] = NULL;
+    for (int j = 0; j < n; j++)
+        if ((trc = T->isend(T->ctx, &max_cs, sizeof(max_cs), ranks[j], ti.tag, &req[j]))) {
+            req[j] = NULL;
+            break;
+        }
+    {
+        int w = wait_posted(T, req, n);
+        trc = trc ? trc : w;
+    }
+    if (trc && !have_had_error) {
+        have_had_error = as_errno(trc);
+        LOGERR("window size for '%s' not sent: %s\n", path, strerror(have_had_error));
+    }
 
     uint64_t final_parity_chunk_size = max_cs + (uint64_t)n * sizeof(uint64_t);
     if (ti.is_rebuilding) {
@@ -438,27 +800,14 @@ static void parity_generator(const char *path, const FileInfo *task, TaskInfo ti
     void *hook_ctx = g_hook_ctx;
     pthread_mutex_unlock(&g_lock);
 
+    if (!have_had_error)
+        have_had_error = __atomic_load_n(&hs->error, __ATOMIC_ACQUIRE);
     fold_res *L = NULL;
-    int have_had_error = __atomic_load_n(&hs->error, __ATOMIC_ACQUIRE);
     int res_rc = expected_messages ? res_acquire(hs, hook == NULL, pitch * (size_t)n, buffer_size, &L) : 0;
-    uint8_t *scratch = NULL; /* receive space if staging could not be set up */
-    uint8_t *win_a, *win_b, *pblk;
     if (res_rc) {
-        LOGERR("no parity engine for '%s' on st %d: %s\n", path, hs->storage_target, bcp_strerror(res_rc));
+        LOGERR("no fold resources for '%s' on st %d: %s\n", path, hs->storage_target, bcp_strerror(res_rc));
         if (!have_had_error)
-            have_had_error = res_rc == -ENODEV ? ENODEV : (res_rc == -ENOMEM ? ENOMEM : EIO);
-        scratch = malloc(2 * pitch * (size_t)n + buffer_size + 1);
-        if (!scratch)
-            abort(); /* cannot even drain the senders */
-        win_a = scratch;
-        win_b = scratch + pitch * (size_t)n;
-        pblk = scratch + 2 * pitch * (size_t)n;
-    } else if (expected_messages) {
-        win_a = L->h_win[0];
-        win_b = L->h_win[1];
-        pblk = L->h_par;
-    } else {
-        win_a = win_b = pblk = NULL; /* header-only parity chunk */
+            have_had_error = as_errno(res_rc);
     }
 
     int P_fd = hs->fd_null;
@@ -466,11 +815,20 @@ static void parity_generator(const char *path, const FileInfo *task, TaskInfo ti
         P_fd = open_new_parity(hs->write_dir, path, (off_t)final_size);
         if (P_fd <= 0) {
             have_had_error = errno;
-            LOGERR("opened parity chunk '%s' with error = '%s'\n", path, strerror(errno));
+            LOGERR("cannot open parity chunk '%s': %s\n", path, strerror(errno));
             P_fd = hs->fd_null;
         }
     } else {
-        LOGERR("using null for '%s', we already have global errno %d\n", path, have_had_error);
+        LOGERR("'%s' goes to the null device: error %d is sticky on this rank\n", path, have_had_error);
+    }
+
+    if (res_rc) {
+        int drc = drain_windows(T, ranks, n, buffer_size, expected_messages, ti.tag);
+        if (drc)
+            LOGERR("draining the senders of '%s' failed: %s\n", path, strerror(as_errno(drc)));
+        if (ti.sample)
+            ti.sample->bytes_written += buffer_size * expected_messages;
+        goto done;
     }
 
     /* gen: the chunk sizes head the parity chunk (:199-201) */
@@ -478,14 +836,25 @@ static void parity_generator(const char *path, const FileInfo *task, TaskInfo ti
         if (write(P_fd, chunk_sizes, sizeof(uint64_t) * (size_t)n) <= 0)
             have_had_error = errno;
 
+    uint8_t *win_a = L ? L->h_win[0] : NULL, *win_b = L ? L->h_win[1] : NULL, *pblk = L ? L->h_par : NULL;
+    for (int j = 0; j < n; j++)
+        req[j] = NULL;
     for (uint64_t msg_i = 0; msg_i < expected_messages; msg_i++) {
+        /* After a transport error the loop keeps receiving every window from
+         * every source (failed peers fail fast): live senders finish their
+         * task instead of blocking; nothing more is folded or written. */
         if (msg_i == 0)
-            for (int j = 0; j < n; j++)
-                bcp_lb_irecv(win_a + (size_t)j * pitch, buffer_size, ranks[j], ti.tag, &req[j]);
-        bcp_lb_waitall(n, req);
-        if (msg_i + 1 != expected_messages)
-            for (int j = 0; j < n; j++)
-                bcp_lb_irecv(win_b + (size_t)j * pitch, buffer_size, ranks[j], ti.tag, &req[j]);
+            trc = post_recvs(T, req, n, win_a, pitch, buffer_size, ranks, ti.tag);
+        int w = wait_posted(T, req, n);
+        trc = trc ? trc : w;
+        if (msg_i + 1 != expected_messages) {
+            int p2 = post_recvs(T, req, n, win_b, pitch, buffer_size, ranks, ti.tag);
+            trc = trc ? trc : p2;
+        }
+        if (trc && !have_had_error) {
+            have_had_error = as_errno(trc);
+            LOGERR("windows of '%s' not received: %s\n", path, strerror(have_had_error));
+        }
         /* fold window msg_i on the GPU while the senders fill win_b */
         if (!have_had_error) {
             int frc = fold_window(L, hs, hook, hook_ctx, win_a, pitch, buffer_size, n, pblk);
@@ -496,10 +865,10 @@ static void parity_generator(const char *path, const FileInfo *task, TaskInfo ti
         }
         if (!have_had_error) {
             size_t wsize = (size_t)MIN_((uint64_t)buffer_size, data_left);
-            ssize_t w = write(P_fd, pblk, wsize);
-            if (w <= 0) {
+            ssize_t wr = write(P_fd, pblk, wsize);
+            if (wr <= 0) {
                 have_had_error = errno;
-                LOGERR("writing '%s' caused new error %d (%s) after %llu bytes\n", path, errno, strerror(errno),
+                LOGERR("write of '%s' failed with %d (%s) after %llu bytes\n", path, errno, strerror(errno),
                        (unsigned long long)(final_size - data_left));
             }
             data_left -= wsize;
@@ -515,9 +884,9 @@ static void parity_generator(const char *path, const FileInfo *task, TaskInfo ti
         if (ftruncate(P_fd, (off_t)final_parity_chunk_size) != 0 && !have_had_error)
             have_had_error = errno;
 
+done:
     if (have_had_error != 0 && raise_sticky_error(hs, have_had_error, path))
-        LOGERR("local error on '%s' elevated to global error\n", path);
-    free(scratch);
+        LOGERR("error on '%s' is now sticky for st %d\n", path, hs->storage_target);
     res_release(L);
     if (P_fd != hs->fd_null)
         close(P_fd);
@@ -528,17 +897,20 @@ static uint8_t *sender_buffer(size_t need)
     lane_res *L = &t_res;
     if (L->send_cap < need || !L->send_buf) {
         free(L->send_buf);
-        L->send_cap = MAX_(need, (size_t)1 << 20);
-        L->send_buf = malloc(L->send_cap);
-        if (!L->send_buf)
-            L->send_cap = 0;
+        L->send_buf = NULL;
+        L->send_cap = 0;
+        if (bcpi_inject_hit(BCP_INJECT_SEND_BUF))
+            return NULL;
+        size_t cap = MAX_(need, (size_t)1 << 20);
+        if ((L->send_buf = malloc(cap)))
+            L->send_cap = cap;
     }
     return L->send_buf;
 }
 
 /* One window of the source role, produced straight into the receiver's
- * buffer (bcp_lb_send_fill): the file's next bytes, zero padded after a short
- * read; zeros after an open or read error or for an empty chunk (A3-q2). */
+ * buffer (send_fill): the file's next bytes, zero padded after a short read;
+ * zeros after an open or read error or for an empty chunk (A3-q2). */
 typedef struct {
     int fd;
     uint64_t fd_size, data_to_send, data_sent;
@@ -561,7 +933,7 @@ static int fill_window(void *ctx, void *dst, size_t n)
     if (r < 0) {
         w->err = errno;
         memset(data, 0, n);
-        LOGERR("reading '%s' caused new error %d (%s) after %llu bytes\n", w->path, errno, strerror(errno),
+        LOGERR("read of '%s' failed with %d (%s) after %llu bytes\n", w->path, errno, strerror(errno),
                (unsigned long long)w->data_sent);
         return 0;
     }
@@ -570,18 +942,19 @@ static int fill_window(void *ctx, void *dst, size_t n)
     return 0;
 }
 
-static void chunk_sender(const char *path, const FileInfo *task, TaskInfo ti, HostState *hs)
+static void chunk_sender(const bcp_transport_ops *T, const char *path, const FileInfo *task, TaskInfo ti,
+                         HostState *hs)
 {
     const int my_st = hs->storage_target;
     const int coordinator = st2rank[GET_P(task->locations)];
     const int ntargets = active_ranks(task->locations);
     uint64_t fd_size = 0;
-    int have_had_error = 0;
+    int have_had_error = 0, trc = 0;
     int fd = open_chunk_readonly(ti.read_dir, path);
     if (fd <= 0) {
         have_had_error = errno;
         fd = hs->fd_zero;
-        LOGERR("opening '%s' caused new error %d (%s)\n", path, errno, strerror(errno));
+        LOGERR("cannot open '%s': %d (%s)\n", path, errno, strerror(errno));
     } else {
         struct stat st;
         fstat(fd, &st);
@@ -597,32 +970,61 @@ static void chunk_sender(const char *path, const FileInfo *task, TaskInfo ti, Ho
         uint64_t chunk_sizes[MAX_STORAGE_TARGETS] = {0};
         ssize_t r = read(fd, chunk_sizes, (size_t)ntargets * sizeof(uint64_t));
         (void)r;
-        bcp_lb_send(chunk_sizes, (size_t)ntargets * sizeof(uint64_t), coordinator, ti.tag);
+        trc = T->send(T->ctx, chunk_sizes, (size_t)ntargets * sizeof(uint64_t), coordinator, ti.tag);
     } else if (!ti.is_rebuilding) {
-        bcp_lb_send(&fd_size, sizeof(fd_size), coordinator, ti.tag);
+        trc = T->send(T->ctx, &fd_size, sizeof(fd_size), coordinator, ti.tag);
     }
 
     uint64_t data_to_send = 0;
-    bcp_lb_recv(&data_to_send, sizeof(data_to_send), coordinator, ti.tag, NULL);
+    if (!trc)
+        trc = T->recv(T->ctx, &data_to_send, sizeof(data_to_send), coordinator, ti.tag);
+    if (trc) {
+        /* no window size: nothing more can be exchanged for this task */
+        if (!have_had_error)
+            have_had_error = as_errno(trc);
+        LOGERR("size exchange for '%s' failed: %s\n", path, strerror(as_errno(trc)));
+        goto done;
+    }
 
     const size_t buffer_size = (size_t)MIN_(WINDOW, data_to_send);
-    /* Zero copy: every window is read straight into P's window row, unless a
-     * later window could replay this one (A3-q1: the file ends before max_cs
-     * and more than one window is sent), which needs the sender's own buffer. */
-    if (!(fd_size < data_to_send && data_to_send > buffer_size)) {
+    /* Zero copy (a transport with send_fill): every window is read straight
+     * into P's window row, unless a later window could replay this one
+     * (A3-q1: the file ends before max_cs and more than one window is sent),
+     * which needs the sender's own buffer. */
+    const int replay = fd_size < data_to_send && data_to_send > buffer_size;
+    uint8_t *data = NULL;
+    if (!(T->send_fill && !replay)) {
+        data = sender_buffer(buffer_size);
+        if (!data) {
+            if (!have_had_error)
+                have_had_error = ENOMEM;
+            LOGERR("no window buffer for '%s': sending zeros\n", path);
+        }
+    }
+    if (T->send_fill && (!replay || !data)) {
         window_fill wf = {fd, fd_size, data_to_send, 0, have_had_error, hs, path};
         while (wf.data_sent < data_to_send) {
             if (ti.sample)
                 ti.sample->bytes_read += buffer_size;
-            bcp_lb_send_fill(fill_window, &wf, buffer_size, coordinator, ti.tag);
+            int e = T->send_fill(T->ctx, fill_window, &wf, buffer_size, coordinator, ti.tag);
+            if (e && e != -EMSGSIZE && !trc)
+                trc = e;
             wf.data_sent += buffer_size;
         }
         have_had_error = wf.err;
-        goto done;
+        goto sent;
     }
-    uint8_t *data = sender_buffer(buffer_size);
-    if (!data)
-        abort();
+    if (!data) {
+        /* no buffer and no fill send: the windows go out as zeros */
+        for (uint64_t sent = 0; sent < data_to_send; sent += buffer_size) {
+            if (ti.sample)
+                ti.sample->bytes_read += buffer_size;
+            int e = T->send(T->ctx, g_zero_window, buffer_size, coordinator, ti.tag);
+            if (e && !trc)
+                trc = e;
+        }
+        goto sent;
+    }
     /* A buffer that is never filled is sent as zeros: the reference sends
      * uninitialised memory for a zero-length chunk (quirk A3-q2). */
     if (have_had_error != 0 || fd_size == 0)
@@ -637,7 +1039,7 @@ static void chunk_sender(const char *path, const FileInfo *task, TaskInfo ti, Ho
             if (r < 0) {
                 have_had_error = errno;
                 memset(data, 0, buffer_size);
-                LOGERR("reading '%s' caused new error %d (%s) after %llu bytes\n", path, errno, strerror(errno),
+                LOGERR("read of '%s' failed with %d (%s) after %llu bytes\n", path, errno, strerror(errno),
                        (unsigned long long)data_sent);
             }
             if (r >= 0 && (size_t)r < buffer_size)
@@ -646,13 +1048,20 @@ static void chunk_sender(const char *path, const FileInfo *task, TaskInfo ti, Ho
         if (ti.sample)
             ti.sample->bytes_read += buffer_size;
         data_sent += buffer_size;
-        bcp_lb_send(data, buffer_size, coordinator, ti.tag);
+        int e = T->send(T->ctx, data, buffer_size, coordinator, ti.tag);
+        if (e && !trc)
+            trc = e;
     }
 
+sent:
+    if (trc && !have_had_error) {
+        have_had_error = as_errno(trc);
+        LOGERR("windows of '%s' not sent: %s\n", path, strerror(have_had_error));
+    }
 done:
     /* ENOENT: the chunk vanished after planning; an unlink event follows. */
     if (have_had_error != 0 && have_had_error != ENOENT && raise_sticky_error(hs, have_had_error, path))
-        LOGERR("local error on '%s' elevated to global error\n", path);
+        LOGERR("error on '%s' is now sticky for st %d\n", path, hs->storage_target);
     if (fd != hs->fd_zero)
         close(fd);
 }
@@ -663,10 +1072,11 @@ int process_task(HostState *hs, const char *path, const FileInfo *fi, TaskInfo t
     assert(P_IS_INVALID(fi->locations) == 0);
     assert(hs->storage_target >= 0);
 
+    const bcp_transport_ops T = transport_now();
     if (GET_P(fi->locations) == hs->storage_target)
-        parity_generator(path, fi, ti, hs);
+        parity_generator(&T, path, fi, ti, hs);
     else if (TEST_BIT(fi->locations, hs->storage_target))
-        chunk_sender(path, fi, ti, hs);
+        chunk_sender(&T, path, fi, ti, hs);
     else
         return 0;
     return active_ranks(fi->locations) != 0;

@@ -98,14 +98,23 @@ int process_task(HostState *hs, const char *path, const FileInfo *fi, TaskInfo t
 /* Device used by the P role of storage target st: devices[st] if a map was
  * given, else st % device_count.  Engines are created lazily, one per device. */
 int bcp_task_set_device_map(const int *devices, int ntargets);
-/* How the P role folds a window on the GPU.  ZERO_COPY (default): the kernel
- * reads the pinned window rows and writes the pinned parity block in place
- * over PCIe (one launch + one sync per window).  STAGED: H2D of the rows,
- * kernel on device buffers, D2H (three commands per window).  Returns the
+/* How the P role folds a window on the GPU.  ZERO_COPY: the kernel reads the
+ * pinned window rows and writes the pinned parity block in place over PCIe,
+ * one launch + one sync per window on the lane's own queue.  STAGED: H2D of
+ * the rows, kernel on device buffers, D2H (three commands per window).
+ * BATCHED: the window is handed to the device's fold service -- one flusher
+ * thread per GPU gathers the windows every P role of every rank has pending
+ * into ONE descriptor batch (zero-copy rows), launches it and wakes each
+ * lane when its own window is done (process_task stays synchronous per task,
+ * as the reference's window loop is, task_processing.c:203-226).  Returns the
  * previous mode, or -EINVAL. */
 #define BCP_FOLD_ZERO_COPY 0
 #define BCP_FOLD_STAGED 1
+#define BCP_FOLD_BATCHED 2
 int bcp_task_set_fold_mode(int mode);
+/* Fold-service counters since the last shutdown (BATCHED mode): windows
+ * folded and launches issued (windows / launches = the batching achieved). */
+int bcp_task_fold_stats(uint64_t *windows, uint64_t *launches);
 /* Release the engines and every lane's queues / staging (call after all
  * lanes have joined). */
 int bcp_task_shutdown(void);
@@ -118,6 +127,62 @@ void bcp_task_thread_release(void);
 typedef int (*bcp_xor_hook_fn)(uint8_t *dst, size_t nbytes, const uint8_t *data, size_t pitch, int nsrc,
                                void *ctx);
 void bcp_task_set_xor_hook(bcp_xor_hook_fn fn, void *ctx);
+
+/* Failure injection for tests (the product never sets it): the next `count`
+ * passes through `site` fail as if the allocation / thread creation had,
+ * after `after` passes succeed.  Sites: the P role's fold resources (as
+ * -ENOMEM), its single drain row (then a bounded 64 KiB per-thread drain
+ * with truncated receives is used), the source role's window buffer, and the
+ * runners' lane-thread creation.  count 0 clears the site. */
+#define BCP_INJECT_FOLD_RES 1
+#define BCP_INJECT_DRAIN_ROW 2
+#define BCP_INJECT_SEND_BUF 4
+#define BCP_INJECT_THREAD 8
+int bcp_task_inject_failure(int site, int after, int count);
+
+/* ---- transport seam (the MPI subset process_task speaks) ---------------- */
+/* process_task talks to its peers through exactly the point-to-point subset
+ * the reference uses (task_processing.c:43-52,120-130,151-166,203-209,
+ * 274-307): blocking send / recv, non-blocking isend / irecv, wait, waitall,
+ * matched by (source rank, tag), non-overtaking per (source, destination,
+ * tag), ranks numbered as st2rank numbers them.  A transport is this table;
+ * every entry returns 0 or a negative errno (a receive shorter than the
+ * message may return -EMSGSIZE and must still consume it).  send_fill is
+ * optional (NULL: the source role reads each window into its own buffer and
+ * sends that, as the reference does); when present it is the zero-copy send
+ * of bcp_lb_send_fill.  An MPI binding maps each entry onto
+ * MPI_Send / MPI_Recv / MPI_Isend / MPI_Irecv / MPI_Wait / MPI_Waitall on
+ * MPI_COMM_WORLD with MPI_BYTE. */
+typedef int (*bcp_lb_fill_fn)(void *ctx, void *dst, size_t n);
+typedef struct bcp_transport_ops {
+    void *ctx;
+    int (*send)(void *ctx, const void *buf, size_t n, int dst, int tag);
+    int (*recv)(void *ctx, void *buf, size_t n, int src, int tag);
+    int (*isend)(void *ctx, const void *buf, size_t n, int dst, int tag, void **req);
+    int (*irecv)(void *ctx, void *buf, size_t n, int src, int tag, void **req);
+    int (*wait)(void *ctx, void *req);
+    int (*waitall)(void *ctx, int n, void **reqs);
+    int (*send_fill)(void *ctx, bcp_lb_fill_fn fill, void *fill_ctx, size_t n, int dst, int tag);
+} bcp_transport_ops;
+/* Install the transport process_task uses from now on (copied); NULL
+ * restores the default, the in-process loopback below.  -EINVAL if a
+ * mandatory entry is missing.  Not to be changed while tasks run. */
+int bcp_task_set_transport(const bcp_transport_ops *ops);
+/* The loopback transport as an ops table (the default). */
+const bcp_transport_ops *bcp_lb_transport(void);
+
+/* Ranks as PROCESSES: a world of world_size ranks connected pairwise by
+ * Unix socketpairs (created before fork; each rank process attaches as its
+ * rank and gets a transport whose receives are progressed by the waiting
+ * threads themselves, unexpected messages buffered).  Any number of threads
+ * of a rank process may use it (the 12 lanes). */
+typedef struct bcp_sock_world bcp_sock_world;
+int bcp_sock_world_create(int world_size, bcp_sock_world **out);
+/* In the rank's process: keep rank's sockets, close the others, fill *ops
+ * (pass it to bcp_task_set_transport).  Once per process. */
+int bcp_sock_world_attach(bcp_sock_world *w, int rank, bcp_transport_ops *ops);
+/* Close whatever sockets this process still holds and free the world. */
+int bcp_sock_world_destroy(bcp_sock_world *w);
 
 /* ---- loopback rank transport (replaces the MPI subset of §2) ----------- */
 /* A world of `world_size` ranks inside this process.  Every thread acting
@@ -142,7 +207,6 @@ int bcp_lb_waitall(int n, bcp_lb_req **reqs);
  * receive buffer (e.g. read() from the chunk file), on the sending thread,
  * once a receiver is matched.  Same matching and ordering as bcp_lb_send;
  * fill returns 0 or a negative errno, which bcp_lb_send_fill returns. */
-typedef int (*bcp_lb_fill_fn)(void *ctx, void *dst, size_t n);
 int bcp_lb_send_fill(bcp_lb_fill_fn fill, void *ctx, size_t n, int dst, int tag);
 
 /* ---- callers: generation lanes and rebuild (loopback drivers) ---------- */
@@ -204,6 +268,18 @@ int bcp_gen_run(const char *store_root, int ntargets, const bcp_work_item *items
  * line) to corrupt_list_path. */
 int bcp_rebuild_run(const char *store_root, int ntargets, int rebuild_target, const bcp_work_item *items,
                     size_t nitems, const char *corrupt_list_path, FILE *log, bcp_run_stats *stats);
+
+/* The same two drivers with every storage target's rank as its own PROCESS
+ * (fork; socketpair transport, bcp_sock_world_*), the way the reference's
+ * ranks run under mpirun: rank k+1 = target k runs its lanes as threads and
+ * reports its counters to the caller through a pipe.  The calling process
+ * must not have used the GPU yet (a forked child cannot use a HIP runtime
+ * its parent initialised): -EBUSY if this library already did.  -ECHILD if a
+ * rank process died. */
+int bcp_gen_run_procs(const char *store_root, int ntargets, const bcp_work_item *items, size_t nitems,
+                      int nlanes, const int *lanes, FILE *log, bcp_run_stats *stats);
+int bcp_rebuild_run_procs(const char *store_root, int ntargets, int rebuild_target, const bcp_work_item *items,
+                          size_t nitems, const char *corrupt_list_path, FILE *log, bcp_run_stats *stats);
 
 /* With the persistent state: bcp_gen_run plus, after every task of a lane
  * of rank k, the process_list DB update (gen/main.c:146-149: set when the

@@ -20,6 +20,7 @@ def declared_functions():
         text = open(h).read()
         text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
         text = re.sub(r"#define[^\n]*(\\\n[^\n]*)*", "", text)
+        text = re.sub(r"typedef\s+struct[^{;]*\{.*?\}[^;]*;", "", text, flags=re.S)  # struct bodies
         text = re.sub(r"typedef[^;]*;", "", text)
         for m in DECL.finditer(text):
             name = m.group(1)

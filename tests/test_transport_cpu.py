@@ -1,0 +1,192 @@
+"""The transport seam under process_task, ranks as processes, and the
+failure paths that used to abort -- host logic on the CPU (the P role's fold
+is the test double of tests/native/cpu_xor_hook.c; no GPU).
+
+* bcp_gen_run_procs / bcp_rebuild_run_procs: one forked process per storage
+  target, socketpair transport (bcp_sock_world), parity files and rebuilds
+  compared with the oracle -- including multi-window stripes (replay quirk
+  A3-q1) and the corrupt list;
+* the transport table: loopback installed explicitly, incomplete tables
+  refused;
+* failure injection: the P role without fold resources still drains its
+  senders (one bounded row, or a 16 KiB truncating one) and raises the
+  sticky error; a source without a window buffer sends zeros and raises it;
+  a lane thread that cannot be created cancels the run before any task
+  (-EAGAIN) -- in both runners, no abort, no hang.
+"""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import bcp_store as S
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KiB, MiB = 1024, 1024 * 1024
+
+
+@pytest.fixture(autouse=True)
+def _clean(bcp):
+    yield
+    for site in (bcp.INJECT_FOLD_RES, bcp.INJECT_DRAIN_ROW, bcp.INJECT_SEND_BUF, bcp.INJECT_THREAD):
+        bcp.inject_failure(site, 0, 0)
+    bcp.set_transport(None)
+
+
+def _random_files(rng, ntargets, nfiles, maxlen):
+    files = []
+    for i in range(nfiles):
+        width = int(rng.integers(1, min(8, ntargets - 1) + 1))
+        holders, p = S.random_layout(rng, ntargets, width)
+        lens = [int(x) for x in rng.integers(0, maxlen, size=width)]
+        files.append((f"p{i % 5}/{i:04x}/chunk{i}", holders, p, lens))
+    return files
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("seed", range(2))
+def test_rank_processes_gen_and_rebuild(bcp, oracle, cpu_hook, tmp_path, seed):
+    rng = np.random.default_rng(700 + seed)
+    ntargets = int(rng.integers(5, 10))
+    files = _random_files(rng, ntargets, 40, 600_000)
+    root = str(tmp_path)
+    items, contents = S.populate(root, ntargets, files, seed=seed)
+    st = bcp.gen_run_procs(root, ntargets, items, nlanes=12)
+    assert st.errors == 0
+    assert st.tasks == sum(len(h) + 1 for (_, h, _, _) in files)
+    for (path, holders, p, lens) in files:
+        assert S.read_file(S.parity_path(root, p, path)) == oracle.gen_parity_file(contents[path]), path
+    victim = int(rng.integers(0, ntargets))
+    lost = {}
+    for (path, holders, p, lens) in files:
+        if victim in holders:
+            lost[path] = S.read_file(S.chunk_path(root, victim, path))
+            os.remove(S.chunk_path(root, victim, path))
+    corrupt = str(tmp_path / "corrupt.txt")
+    st = bcp.rebuild_run_procs(root, ntargets, victim, items, corrupt_list=corrupt)
+    assert st.errors == 0
+    for path, data in lost.items():
+        assert S.read_file(S.chunk_path(root, victim, path)) == data, path
+    assert open(corrupt).read() == ""  # every survivor is older than its FileInfo timestamp
+
+
+@pytest.mark.timeout(300)
+def test_rank_processes_multiwindow_replay(bcp, oracle, cpu_hook, tmp_path):
+    """Stripes above the 10 MiB window across processes: the socket transport
+    carries the replayed windows (A3-q1) exactly as the loopback does."""
+    root = str(tmp_path)
+    files = [("big/a", [0, 1], 2, [10 * MiB, 25 * MiB + 5]), ("big/b", [1, 2, 3], 0, [3, 21 * MiB, 0])]
+    items, contents = S.populate(root, 4, files, seed=3)
+    st = bcp.gen_run_procs(root, 4, items, nlanes=2)
+    assert st.errors == 0
+    for (path, holders, p, lens) in files:
+        assert S.read_file(S.parity_path(root, p, path)) == oracle.gen_parity_file(contents[path]), path
+
+
+def test_explicit_loopback_transport_and_validation(bcp, oracle, cpu_hook, tmp_path):
+    import ctypes
+    L = bcp.lib()
+    bcp.set_transport(L.bcp_lb_transport())
+    root = str(tmp_path)
+    files = [(f"x/{i}", [0, 1, 2], 3, [100_000 + i, 64 * KiB, 7]) for i in range(6)]
+    items, contents = S.populate(root, 4, files, seed=1)
+    st = bcp.gen_run(root, 4, items)
+    assert st.errors == 0
+    for (path, holders, p, lens) in files:
+        assert S.read_file(S.parity_path(root, p, path)) == oracle.gen_parity_file(contents[path])
+    # a table without its mandatory entries is refused
+    empty = (ctypes.c_void_p * 8)()
+    assert L.bcp_task_set_transport(ctypes.addressof(empty)) == -22
+
+
+def _config(tmp_path, seed=5, nfiles=24):
+    rng = np.random.default_rng(seed)
+    files = _random_files(rng, 6, nfiles, 300_000)
+    root = str(tmp_path)
+    items, contents = S.populate(root, 6, files, seed=seed)
+    return root, files, items, contents
+
+
+@pytest.mark.timeout(120)
+@pytest.mark.parametrize("drain_row", [True, False], ids=["one-row-drain", "16KiB-truncating-drain"])
+def test_p_role_without_resources_drains_and_raises(bcp, oracle, cpu_hook, tmp_path, drain_row):
+    root, files, items, contents = _config(tmp_path)
+    bcp.inject_failure(bcp.INJECT_FOLD_RES, 0, 1)
+    if not drain_row:
+        bcp.inject_failure(bcp.INJECT_DRAIN_ROW, 0, 1)
+    st = bcp.gen_run(root, 6, items, nlanes=4)  # returns: no hang, no abort
+    assert st.errors == 1  # exactly the rank whose P role had no resources
+    bad = 0
+    for (path, holders, p, lens) in files:
+        f = S.parity_path(root, p, path)
+        if os.path.exists(f) and S.read_file(f) == oracle.gen_parity_file(contents[path]):
+            continue
+        bad += 1
+    # the failing rank's parity files (that task and its later ones) are missing;
+    # every other rank's are exact
+    assert 1 <= bad < len(files)
+
+
+@pytest.mark.timeout(120)
+def test_source_without_buffer_sends_zeros_and_raises(bcp, oracle, cpu_hook, tmp_path):
+    """The buffered source path (a window that could be replayed) with its
+    buffer allocation failing: zeros go out, the rank's error is sticky."""
+    root = str(tmp_path)
+    files = [("w/a", [0, 1], 2, [10 * MiB + 1, 21 * MiB])]
+    items, contents = S.populate(root, 3, files, seed=2)
+    bcp.inject_failure(bcp.INJECT_SEND_BUF, 0, 1)
+    st = bcp.gen_run(root, 3, items, nlanes=1)
+    assert st.errors == 1
+    # the P role still wrote a parity file: chunk 0's stream was zeros
+    pf = S.read_file(S.parity_path(root, 2, "w/a"))
+    hdr = np.frombuffer(pf[:16], "<u8").tolist()
+    assert hdr == [10 * MiB + 1, 21 * MiB]
+    body = np.frombuffer(pf[16:], np.uint8)
+    assert body.tobytes() == oracle.gen_parity_file([contents["w/a"][1]])[8:]
+
+
+@pytest.mark.timeout(120)
+@pytest.mark.parametrize("after", [0, 5, 17])
+def test_lane_thread_failure_cancels_before_any_task(bcp, cpu_hook, tmp_path, after):
+    root, files, items, contents = _config(tmp_path, nfiles=10)
+    bcp.inject_failure(bcp.INJECT_THREAD, after, 1)
+    with pytest.raises(bcp.BcpError) as ei:
+        bcp.gen_run(root, 6, items, nlanes=4)
+    assert ei.value.rc == -11  # -EAGAIN
+    assert not any(os.path.exists(S.parity_path(root, p, path)) for (path, _, p, _) in files)
+    bcp.inject_failure(bcp.INJECT_THREAD, min(after, 3), 1)  # the rebuild starts one thread per rank
+    with pytest.raises(bcp.BcpError) as ei:
+        bcp.rebuild_run(root, 6, 0, items)
+    assert ei.value.rc == -11
+    # and the library is usable afterwards
+    bcp.inject_failure(bcp.INJECT_THREAD, 0, 0)
+    assert bcp.gen_run(root, 6, items, nlanes=4).errors == 0
+
+
+@pytest.mark.timeout(120)
+def test_rank_process_failure_is_reported_not_hung(bcp, cpu_hook, tmp_path):
+    """One rank process cannot start its lanes (injected before the fork, so
+    the first child to create lane 3 fails): it exits, its partners see its
+    sockets close and fail their shared tasks, the run returns an error."""
+    root, files, items, contents = _config(tmp_path, nfiles=10)
+    bcp.inject_failure(bcp.INJECT_THREAD, 2, 1)  # inherited by every child: each fails its 3rd lane
+    with pytest.raises(bcp.BcpError) as ei:
+        bcp.gen_run_procs(root, 6, items, nlanes=4)
+    assert ei.value.rc in (-11, -10)  # -EAGAIN from a rank, or -ECHILD
+
+
+@pytest.mark.timeout(200)
+def test_caller_defined_st2rank_and_hoststate(bcp, tmp_path):
+    """A C caller shaped like gen/main.c: its own int st2rank[56] and
+    HostState, sizeof/offsetof of FileInfo / TaskInfo / HostState checked
+    against the reference's layout, ranks as forked processes on the
+    socketpair transport calling process_task directly, parity checked."""
+    exe = tmp_path / "caller"
+    lib_dir = os.path.dirname(bcp.LIB_PATH)
+    subprocess.run(["gcc", "-std=gnu99", "-O1", "-Wall", "-Werror", "-pthread", "-I", os.path.join(ROOT, "include"),
+                    "-o", str(exe), os.path.join(ROOT, "tests", "native", "caller_test.c"), "-L", lib_dir, "-lbcp",
+                    f"-Wl,-rpath,{lib_dir}"], check=True)
+    r = subprocess.run([str(exe), str(tmp_path / "store")], capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "caller_test ok" in r.stdout
