@@ -23,10 +23,10 @@ def gpu_fold(bcp, engine):
     bcp.task_shutdown()
 
 
-@pytest.fixture(params=["zero_copy", "staged"])
+@pytest.fixture(params=["batched", "zero_copy", "staged"])
 def fold_mode(request, bcp):
-    """Both forms of the P role's GPU fold (bcp_task_set_fold_mode)."""
-    mode = bcp.FOLD_ZERO_COPY if request.param == "zero_copy" else bcp.FOLD_STAGED
+    """Every form of the P role's GPU fold (bcp_task_set_fold_mode)."""
+    mode = {"batched": bcp.FOLD_BATCHED, "zero_copy": bcp.FOLD_ZERO_COPY, "staged": bcp.FOLD_STAGED}[request.param]
     prev = bcp.set_fold_mode(mode)
     yield request.param
     bcp.set_fold_mode(prev)

@@ -78,7 +78,7 @@ def gpu_protocol(bcp, engine):
     bcp.task_shutdown()
 
 
-@pytest.mark.parametrize("mode", ["zero_copy", "staged", "pipeline"])
+@pytest.mark.parametrize("mode", ["batched", "zero_copy", "staged", "pipeline"])
 @pytest.mark.parametrize("fx", GEN, ids=lambda c: c["name"])
 def test_parity_files_match_reference_folds(bcp, oracle, tmp_path, gpu_protocol, fx, mode):
     lens = fx["lens"]
@@ -91,14 +91,17 @@ def test_parity_files_match_reference_folds(bcp, oracle, tmp_path, gpu_protocol,
     for k, c in enumerate(chunks):
         S.write_chunk(root, k, "r/e/f", c)
     items = [("r/e/f", 2**40, S.with_p((1 << n) - 1, p))]
-    if mode == "pipeline":
-        st = bcp.pipeline_gen(root, nt, items)
-    else:
-        prev = bcp.set_fold_mode(bcp.FOLD_ZERO_COPY if mode == "zero_copy" else bcp.FOLD_STAGED)
-        try:
-            st = bcp.gen_run(root, nt, items)
-        finally:
+    prev = None if mode == "pipeline" else bcp.set_fold_mode(
+        {"batched": bcp.FOLD_BATCHED, "zero_copy": bcp.FOLD_ZERO_COPY, "staged": bcp.FOLD_STAGED}[mode])
+    try:
+        _gen_and_rebuild(bcp, root, nt, p, items, fx, mode)
+    finally:
+        if prev is not None:
             bcp.set_fold_mode(prev)
+
+
+def _gen_and_rebuild(bcp, root, nt, p, items, fx, mode):
+    st = bcp.pipeline_gen(root, nt, items) if mode == "pipeline" else bcp.gen_run(root, nt, items)
     assert st.errors == 0
     pf = S.read_file(S.parity_path(root, p, "r/e/f"))
     assert len(pf) == fx["file_len"] and sha(pf) == fx["sha256"]

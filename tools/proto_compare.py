@@ -1,0 +1,204 @@
+#!/usr/bin/env python3
+"""Per-task protocol (process_task over loopback ranks) with every P-role fold,
+interleaved in ONE run on ONE box:
+
+  gpu_batched    BCP_FOLD_BATCHED: the device's fold service batches the
+                 pending windows of every lane into one launch (default)
+  gpu_zero_copy  one zero-copy launch + sync per window on the lane's queue
+  gpu_staged     H2D -> kernel -> D2H per window
+  cpu_reference  the reference's xor_parity restated (oracle_xor_rows) as the
+                 fold: the reference CPU path
+  noop           a fold that does nothing: the bound of the protocol itself
+                 (no parity is correct; not verified)
+
+Workloads: config 1 (4 targets, 1333 x 3-wide 512 KiB stripes, 12 lanes; gen,
+and rebuild of target 2 with the single rebuild lane) and config 5 (9
+targets, 8-wide stripes of log-uniform 64 KiB-4 MiB chunks, 12 lanes).
+Rate = (chunk bytes read + parity bytes written) / wall; each round runs
+every fold once in a rotating order, medians over rounds after a cold one.
+Parity of the GPU and CPU runs is checked against the oracle on a sample.
+One JSON line per (workload, fold); tools only.
+"""
+import argparse
+import ctypes
+import json
+import os
+import shutil
+import subprocess
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "beegfs-chunk-parity_amd"))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+import numpy as np  # noqa: E402
+
+import bcp_ctypes as bcp  # noqa: E402
+import bcp_store as S  # noqa: E402
+import oracle  # noqa: E402  (checker + the reference CPU fold)
+from e2e_bench import total_bytes, verify, write_store  # noqa: E402
+
+KiB, MiB, GiB = 1024, 1024 ** 2, 1024 ** 3
+
+
+def emit(**kw):
+    print(json.dumps(kw), flush=True)
+
+
+def noop_hook():
+    tmp = tempfile.mkdtemp(dir="/tmp")  # /dev/shm may be noexec
+    src = os.path.join(tmp, "noop.c")
+    open(src, "w").write("#include <stddef.h>\n#include <stdint.h>\nint noop_fold(uint8_t *d, size_t n, const uint8_t"
+                         " *s, size_t p, int k, void *c) { (void)d; (void)n; (void)s; (void)p; (void)k; (void)c;"
+                         " return 0; }\n")
+    so = os.path.join(tmp, "libnoop.so")
+    subprocess.run(["gcc", "-O2", "-shared", "-fPIC", "-o", so, src], check=True)
+    return ctypes.CDLL(so)
+
+
+def fold_setup(fold, hooks):
+    """Returns a context restore callable."""
+    if fold.startswith("gpu_"):
+        mode = {"gpu_batched": bcp.FOLD_BATCHED, "gpu_zero_copy": bcp.FOLD_ZERO_COPY,
+                "gpu_staged": bcp.FOLD_STAGED}[fold]
+        prev = bcp.set_fold_mode(mode)
+        return lambda: bcp.set_fold_mode(prev)
+    bcp.set_xor_hook(hooks[fold])
+    return lambda: bcp.set_xor_hook(None)
+
+
+def measure(name, folds, rounds, run_once, verify_fn, nbytes, hooks, extra=None):
+    times = {f: [] for f in folds}
+    batching = {}
+    for r in range(rounds + 1):
+        order = folds[r % len(folds):] + folds[:r % len(folds)]
+        for f in order:
+            restore = fold_setup(f, hooks)
+            try:
+                w0, l0 = bcp.fold_stats()
+                t0 = time.perf_counter()
+                st = run_once()
+                dt = time.perf_counter() - t0
+                w1, l1 = bcp.fold_stats()
+            finally:
+                restore()
+            if st.errors:
+                raise RuntimeError(f"{name}/{f}: {st.errors} rank errors")
+            times[f].append(dt)
+            if f == "gpu_batched" and r > 0:
+                batching.setdefault("windows", 0)
+                batching["windows"] = batching["windows"] + (w1 - w0)
+                batching["launches"] = batching.get("launches", 0) + (l1 - l0)
+            if r == rounds and f != "noop":
+                ok, bad = verify_fn()
+                if not ok:
+                    raise RuntimeError(f"{name}/{f}: parity mismatch on {bad}")
+    res = {}
+    for f in folds:
+        warm = float(np.median(times[f][1:]))
+        res[f] = nbytes / warm / GiB
+        line = dict(workload=name, fold=f, GiBps=round(res[f], 3), warm_median_s=round(warm, 4),
+                    runs_s=[round(x, 4) for x in times[f]], cold_s=round(times[f][0], 4))
+        if f == "gpu_batched" and batching.get("launches"):
+            line["windows_per_launch"] = round(batching["windows"] / batching["launches"], 2)
+        if extra:
+            line.update(extra)
+        emit(**line)
+    if "noop" in res:
+        emit(workload=name, summary={f: round(v, 3) for f, v in res.items()},
+             frac_of_noop_bound={f: round(v / res["noop"], 3) for f, v in res.items() if f != "noop"},
+             gpu_batched_vs_cpu=round(res.get("gpu_batched", 0) / res["cpu_reference"], 3)
+             if "cpu_reference" in res else None)
+    return res
+
+
+def reset_parity(root, ntargets):
+    for k in range(ntargets):
+        shutil.rmtree(os.path.join(root, f"st{k}", "parity"), ignore_errors=True)
+        os.makedirs(os.path.join(root, f"st{k}", "parity"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--root", default="/dev/shm/bcp_proto")
+    ap.add_argument("--rounds", type=int, default=4)
+    ap.add_argument("--folds", default="gpu_batched,gpu_zero_copy,cpu_reference,noop,gpu_staged")
+    ap.add_argument("--workloads", default="c1_gen,c1_rebuild,c5_gen")
+    ap.add_argument("--c1-files", type=int, default=1333)
+    ap.add_argument("--c5-stripes", type=int, default=600)
+    ap.add_argument("--lanes", type=int, default=12)
+    a = ap.parse_args()
+    folds = a.folds.split(",")
+    noop = noop_hook()
+    hooks = {"cpu_reference": ctypes.cast(oracle.lib().oracle_xor_rows, ctypes.c_void_p).value,
+             "noop": ctypes.cast(noop.noop_fold, ctypes.c_void_p).value}
+    rng = np.random.default_rng(0)
+    wl = a.workloads.split(",")
+    if "c1_gen" in wl or "c1_rebuild" in wl:
+        root = os.path.join(a.root, "c1")
+        shutil.rmtree(root, ignore_errors=True)
+        files = []
+        for i in range(a.c1_files):
+            p = i % 4
+            files.append((f"u0/{i % 64:02X}/chunk{i}", [t for t in range(4) if t != p], p, [512 * KiB] * 3))
+        contents = write_store(root, files, 1)
+        items = [(path, 2 ** 40, S.with_p(sum(1 << h for h in holders), p)) for path, holders, p, _ in files]
+        rd, wr = total_bytes(root, files)
+        if "c1_gen" in wl:
+            def run_gen():
+                reset_parity(root, 4)
+                return bcp.gen_run(root, 4, items, nlanes=a.lanes)
+            measure("config1_gen", folds, a.rounds, run_gen, lambda: verify(root, files, contents, 20, rng), rd + wr,
+                    hooks, {"lanes": a.lanes})
+        if "c1_rebuild" in wl:
+            # parity from a correct run, then rebuild target 2 again and again
+            bcp.set_xor_hook(hooks["cpu_reference"])
+            try:
+                reset_parity(root, 4)
+                bcp.gen_run(root, 4, items, nlanes=a.lanes)
+            finally:
+                bcp.set_xor_hook(None)
+            lost = {path: S.chunk_path(root, 2, path) for path, holders, _, _ in files if 2 in holders}
+            rb_bytes = len(lost) * 4 * 512 * KiB
+
+            def run_rb():
+                for fn in lost.values():
+                    if os.path.exists(fn):
+                        os.remove(fn)
+                return bcp.rebuild_run(root, 4, 2, items)
+
+            def check_rb():
+                for k, (path, fn) in enumerate(lost.items()):
+                    if k % 50 == 0:
+                        holders = next(h for pth, h, _, _ in files if pth == path)
+                        if S.read_file(fn) != contents[path][holders.index(2)].tobytes():
+                            return False, path
+                return True, None
+            measure("config1_rebuild", folds, a.rounds, run_rb, check_rb, rb_bytes, hooks, {"lanes": 1})
+        shutil.rmtree(root, ignore_errors=True)
+    if "c5_gen" in wl:
+        root = os.path.join(a.root, "c5")
+        shutil.rmtree(root, ignore_errors=True)
+        r5 = np.random.default_rng(5)
+        files = []
+        for i in range(a.c5_stripes):
+            holders, p = S.random_layout(r5, 9, 8)
+            lens = [int(x) for x in np.exp(r5.uniform(np.log(64 * KiB), np.log(4 * MiB), size=8))]
+            files.append((f"u{i % 8}/{(i * 2654435761) % 65536:04X}/chunk{i}", holders, p, lens))
+        contents = write_store(root, files, 2)
+        items = [(path, 1_700_000_000, S.with_p(sum(1 << h for h in holders), p)) for path, holders, p, _ in files]
+        rd, wr = total_bytes(root, files)
+
+        def run5():
+            reset_parity(root, 9)
+            return bcp.gen_run(root, 9, items, nlanes=a.lanes)
+        measure("config5_gen", folds, a.rounds, run5, lambda: verify(root, files, contents, 20, rng), rd + wr, hooks,
+                {"lanes": a.lanes, "stripes": len(files)})
+        shutil.rmtree(root, ignore_errors=True)
+    bcp.task_shutdown()
+
+
+if __name__ == "__main__":
+    main()
