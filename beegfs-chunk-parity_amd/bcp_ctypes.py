@@ -615,7 +615,7 @@ def set_xor_hook(fn_addr: int | None, ctx: int | None = None):
     lib().bcp_task_set_xor_hook(_V(fn_addr) if fn_addr else None, _V(ctx) if ctx else None)
 
 
-FOLD_ZERO_COPY, FOLD_STAGED, FOLD_BATCHED = 0, 1, 2
+FOLD_ZERO_COPY, FOLD_STAGED, FOLD_BATCHED, FOLD_STREAMED = 0, 1, 2, 3
 INJECT_FOLD_RES, INJECT_DRAIN_ROW, INJECT_SEND_BUF, INJECT_THREAD = 1, 2, 4, 8
 
 

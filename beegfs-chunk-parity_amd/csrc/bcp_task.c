@@ -14,9 +14,11 @@
  *     reference uses;
  *   - the window fold (xor_parity at :211) runs on the GPU over pinned,
  *     device-mapped window rows (256-byte pitch, so every row is 16-byte
- *     aligned for the streaming kernel): per lane on its own HIP queue
- *     (ZERO_COPY, STAGED) or through a per-device fold service that batches
- *     the pending windows of every lane and rank into one launch (BATCHED);
+ *     aligned for the streaming kernel): per lane on its own HIP queue --
+ *     rows DMA'd to HBM one by one as they arrive, data bytes only (STREAMED),
+ *     read in place over PCIe (ZERO_COPY), or copied after the last one
+ *     (STAGED) -- or through a per-device fold service that batches the
+ *     pending windows of every lane and rank into one launch (BATCHED);
  *   - nothing aborts: when the P role cannot get fold resources it still
  *     drains its senders through one bounded row and raises the sticky error;
  *     a source without a window buffer sends zeros and raises it.
@@ -83,7 +85,8 @@ int bcp_task_set_device_map(const int *devices, int ntargets)
 
 int bcp_task_set_fold_mode(int mode)
 {
-    if (mode != BCP_FOLD_ZERO_COPY && mode != BCP_FOLD_STAGED && mode != BCP_FOLD_BATCHED)
+    if (mode != BCP_FOLD_ZERO_COPY && mode != BCP_FOLD_STAGED && mode != BCP_FOLD_BATCHED &&
+        mode != BCP_FOLD_STREAMED)
         return -EINVAL;
     pthread_mutex_lock(&g_lock);
     int prev = g_fold_mode;
@@ -603,6 +606,39 @@ static int fold_window(fold_res *R, HostState *hs, bcp_xor_hook_fn hook, void *c
     return bcp_queue_sync(R->q);
 }
 
+/* STREAMED mode, per window: wait for the rows in source order and, as each
+ * arrives, copy its data bytes (valid[j]) to device row j on the lane's
+ * queue -- the DMA of row j overlaps the senders still filling rows j+1...
+ * Every posted request is waited for, whatever fails.  Returns the first
+ * transport error in *trc and the first copy error as the result. */
+static int stream_rows_in(const bcp_transport_ops *T, fold_res *R, void **req, int n, const uint8_t *rows,
+                          size_t pitch, const size_t *valid, int *trc)
+{
+    int crc = 0;
+    *trc = 0;
+    for (int j = 0; j < n; j++) {
+        int e = req[j] ? T->wait(T->ctx, req[j]) : 0;
+        req[j] = NULL;
+        if (e && !*trc)
+            *trc = e;
+        if (!e && !crc && valid[j])
+            crc = bcp_h2d_async(R->q, (uint8_t *)R->d_src + (size_t)j * pitch, rows + (size_t)j * pitch, valid[j]);
+    }
+    return crc;
+}
+
+/* STREAMED mode: fold the device rows (row j = valid[j] data bytes, zero
+ * padded to nbytes) into the pinned output block, then sync. */
+static int stream_fold(fold_res *R, int n, size_t pitch, const size_t *valid, size_t nbytes, uint8_t *out)
+{
+    bcp_stripe st = {(uint64_t)(uintptr_t)out, nbytes, 0, (uint32_t)n, 0};
+    bcp_source so[MAX_STORAGE_TARGETS];
+    for (int j = 0; j < n; j++)
+        so[j] = (bcp_source){(uint64_t)(uintptr_t)((uint8_t *)R->d_src + (size_t)j * pitch), valid[j]};
+    int rc = bcp_xor_stripes_async(R->q, &st, 1, so, (uint32_t)n);
+    return rc ? rc : bcp_queue_sync(R->q);
+}
+
 /* ---- file helpers (task_processing.c:29-79) ----------------------------- */
 
 /* mkdir -p for the directories of `filename` under wdir. */
@@ -822,6 +858,30 @@ static void parity_generator(const bcp_transport_ops *T, const char *path, const
         LOGERR("'%s' goes to the null device: error %d is sticky on this rank\n", path, have_had_error);
     }
 
+    /* STREAMED: the lane's queue and device rows; row j's data bytes.  A
+     * gen-mode single-window row holds chunk_sizes[j] bytes then the
+     * sender's zero padding (chunk_sender reads a chunk up to the size it
+     * reported); anything else (rebuild: the survivors' current sizes are
+     * not sent; windows past the first: replay) is taken whole. */
+    pthread_mutex_lock(&g_lock);
+    int streamed = g_fold_mode == BCP_FOLD_STREAMED && !hook && !res_rc && expected_messages > 0;
+    pthread_mutex_unlock(&g_lock);
+    size_t valid[MAX_STORAGE_TARGETS];
+    for (int j = 0; j < n; j++)
+        valid[j] = (!ti.is_rebuilding && expected_messages == 1) ? (size_t)MIN_(chunk_sizes[j], (uint64_t)buffer_size)
+                                                                 : buffer_size;
+    if (streamed) {
+        int src = L->q ? 0 : bcp_queue_create(L->eng, &L->q);
+        if (!src)
+            src = grow_dev(L, &L->d_src, &L->d_cap, pitch * (size_t)n);
+        if (src) {
+            LOGERR("no device rows for '%s' on st %d: %s\n", path, hs->storage_target, bcp_strerror(src));
+            if (!have_had_error)
+                have_had_error = as_errno(src);
+            streamed = 0;
+        }
+    }
+
     if (res_rc) {
         int drc = drain_windows(T, ranks, n, buffer_size, expected_messages, ti.tag);
         if (drc)
@@ -845,8 +905,16 @@ static void parity_generator(const bcp_transport_ops *T, const char *path, const
          * task instead of blocking; nothing more is folded or written. */
         if (msg_i == 0)
             trc = post_recvs(T, req, n, win_a, pitch, buffer_size, ranks, ti.tag);
-        int w = wait_posted(T, req, n);
+        int w = 0, crc = 0;
+        if (streamed && !have_had_error && !trc)
+            crc = stream_rows_in(T, L, req, n, win_a, pitch, valid, &w);
+        else
+            w = wait_posted(T, req, n);
         trc = trc ? trc : w;
+        if (crc && !have_had_error) {
+            have_had_error = EIO;
+            LOGERR("row copy of '%s' failed: %s\n", path, bcp_strerror(crc));
+        }
         if (msg_i + 1 != expected_messages) {
             int p2 = post_recvs(T, req, n, win_b, pitch, buffer_size, ranks, ti.tag);
             trc = trc ? trc : p2;
@@ -857,7 +925,8 @@ static void parity_generator(const bcp_transport_ops *T, const char *path, const
         }
         /* fold window msg_i on the GPU while the senders fill win_b */
         if (!have_had_error) {
-            int frc = fold_window(L, hs, hook, hook_ctx, win_a, pitch, buffer_size, n, pblk);
+            int frc = streamed ? stream_fold(L, n, pitch, valid, buffer_size, pblk)
+                               : fold_window(L, hs, hook, hook_ctx, win_a, pitch, buffer_size, n, pblk);
             if (frc) {
                 have_had_error = EIO;
                 LOGERR("GPU fold of '%s' failed: %s\n", path, bcp_strerror(frc));
@@ -928,7 +997,9 @@ static int fill_window(void *ctx, void *dst, size_t n)
         memset(data, 0, n);
         return 0;
     }
-    const uint64_t left = w->data_to_send - w->data_sent;
+    /* up to the size the chunk reported (not past it should the file have
+     * grown since fstat: the parity body then agrees with its header) */
+    const uint64_t left = MIN_(w->data_to_send, w->fd_size) - w->data_sent;
     ssize_t r = read(w->fd, data, (size_t)MIN_((uint64_t)n, left));
     if (r < 0) {
         w->err = errno;
@@ -1032,7 +1103,7 @@ static void chunk_sender(const bcp_transport_ops *T, const char *path, const Fil
 
     uint64_t data_sent = 0;
     while (data_sent < data_to_send) {
-        uint64_t left = data_to_send - data_sent;
+        uint64_t left = MIN_(data_to_send, fd_size) - data_sent; /* up to the reported size (fill_window) */
         /* once the file is exhausted the previous window is re-sent (A3-q1) */
         if (have_had_error == 0 && data_sent < fd_size) {
             ssize_t r = read(fd, data, (size_t)MIN_((uint64_t)buffer_size, left));

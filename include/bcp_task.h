@@ -111,6 +111,13 @@ int bcp_task_set_device_map(const int *devices, int ntargets);
 #define BCP_FOLD_ZERO_COPY 0
 #define BCP_FOLD_STAGED 1
 #define BCP_FOLD_BATCHED 2
+/* STREAMED: as each source's window row arrives, its DATA bytes (a gen-mode
+ * single-window row holds chunk_size bytes, the rest is the sender's zero
+ * padding) are DMA'd to device memory on the lane's queue, overlapping the
+ * rows still being read; after the last row one kernel folds the rows from
+ * HBM (padding implicit, never transferred) straight into the pinned output
+ * block, then one sync.  PCIe carries the chunk bytes once, not the padding. */
+#define BCP_FOLD_STREAMED 3
 int bcp_task_set_fold_mode(int mode);
 /* Fold-service counters since the last shutdown (BATCHED mode): windows
  * folded and launches issued (windows / launches = the batching achieved). */

@@ -23,10 +23,11 @@ def gpu_fold(bcp, engine):
     bcp.task_shutdown()
 
 
-@pytest.fixture(params=["batched", "zero_copy", "staged"])
+@pytest.fixture(params=["streamed", "batched", "zero_copy", "staged"])
 def fold_mode(request, bcp):
     """Every form of the P role's GPU fold (bcp_task_set_fold_mode)."""
-    mode = {"batched": bcp.FOLD_BATCHED, "zero_copy": bcp.FOLD_ZERO_COPY, "staged": bcp.FOLD_STAGED}[request.param]
+    mode = {"batched": bcp.FOLD_BATCHED, "zero_copy": bcp.FOLD_ZERO_COPY, "staged": bcp.FOLD_STAGED,
+            "streamed": bcp.FOLD_STREAMED}[request.param]
     prev = bcp.set_fold_mode(mode)
     yield request.param
     bcp.set_fold_mode(prev)
