@@ -118,6 +118,7 @@ _SIGS = {
     "bcp_task_set_fold_mode": ([ctypes.c_int], ctypes.c_int),
     "bcp_task_fold_stats": ([ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)], ctypes.c_int),
     "bcp_task_inject_failure": ([ctypes.c_int, ctypes.c_int, ctypes.c_int], ctypes.c_int),
+    "bcp_task_phase_stats": ([ctypes.POINTER(ctypes.c_double), ctypes.c_int, ctypes.c_int], ctypes.c_int),
     "bcp_task_set_transport": ([_V], ctypes.c_int),
     "bcp_lb_transport": ([], _V),
     "bcp_gen_run_procs": ([ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(WorkItem), ctypes.c_size_t, ctypes.c_int,
@@ -636,6 +637,22 @@ def fold_stats() -> tuple[int, int]:
     w, l = ctypes.c_uint64(0), ctypes.c_uint64(0)
     call("bcp_task_fold_stats", ctypes.byref(w), ctypes.byref(l))
     return w.value, l.value
+
+
+PHASES = ("p_sizes", "p_open", "p_rows", "p_fold", "p_write", "p_close", "s_sizes", "s_send", "p_tasks", "s_tasks")
+
+
+def phase_stats(reset: bool = False) -> dict:
+    """Per-phase protocol wall time summed over tasks (bcp_task_phase_stats);
+    p_tasks / s_tasks are counts."""
+    buf = (ctypes.c_double * len(PHASES))()
+    rc = lib().bcp_task_phase_stats(buf, len(PHASES), 1 if reset else 0)
+    if rc < 0:
+        raise BcpError("bcp_task_phase_stats", rc)
+    out = {k: buf[i] for i, k in enumerate(PHASES)}
+    out["p_tasks"] = int(out["p_tasks"])
+    out["s_tasks"] = int(out["s_tasks"])
+    return out
 
 
 def inject_failure(site: int, after: int = 0, count: int = 1):

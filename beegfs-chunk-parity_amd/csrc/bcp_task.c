@@ -33,6 +33,7 @@
 #include <string.h>
 #include <sys/stat.h>
 #include <sys/types.h>
+#include <time.h>
 #include <unistd.h>
 
 #include "bcp_host.h"
@@ -709,6 +710,38 @@ static int raise_sticky_error(HostState *hs, int err, const char *path)
 /* errno value for the sticky error from a negative library / transport code */
 static int as_errno(int rc) { return rc < 0 ? -rc : (rc ? rc : EIO); }
 
+/* ---- phase accounting (bcp_task_phase_stats) -----------------------------
+ * Wall time per P-role phase summed over tasks (relaxed atomics: a few ns
+ * per task), to see where a task's latency goes on a given box. */
+static uint64_t g_phase_ns[BCP_PHASES];
+
+static uint64_t mono_ns(void)
+{
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return (uint64_t)t.tv_sec * 1000000000u + (uint64_t)t.tv_nsec;
+}
+
+static void phase_add(int ph, uint64_t *t)
+{
+    const uint64_t now = mono_ns();
+    __atomic_fetch_add(&g_phase_ns[ph], now - *t, __ATOMIC_RELAXED);
+    *t = now;
+}
+
+int bcp_task_phase_stats(double *seconds, int nphases, int reset)
+{
+    if (nphases < 0 || (nphases && !seconds))
+        return -EINVAL;
+    for (int i = 0; i < BCP_PHASES; i++) {
+        const uint64_t v = reset ? __atomic_exchange_n(&g_phase_ns[i], 0, __ATOMIC_RELAXED)
+                                 : __atomic_load_n(&g_phase_ns[i], __ATOMIC_RELAXED);
+        if (i < nphases)
+            seconds[i] = i >= BCP_PHASE_P_TASKS ? (double)v : (double)v * 1e-9; /* counts, else ns -> s */
+    }
+    return BCP_PHASES;
+}
+
 /* ---- roles ------------------------------------------------------------- */
 
 /* Post one receive per source (window row j at base + j * pitch).  Every
@@ -785,6 +818,7 @@ static void parity_generator(const bcp_transport_ops *T, const char *path, const
     void *req[MAX_STORAGE_TARGETS];
     uint64_t chunk_sizes[MAX_STORAGE_TARGETS] = {0};
     int have_had_error = 0, trc = 0;
+    uint64_t tph = mono_ns();
     if (ti.is_rebuilding) {
         /* the parity holder forwards the stored header (:149-156) */
         trc = T->recv(T->ctx, chunk_sizes, (size_t)n * sizeof(uint64_t), st2rank[ti.actual_P_st], ti.tag);
@@ -817,6 +851,7 @@ static void parity_generator(const bcp_transport_ops *T, const char *path, const
         LOGERR("window size for '%s' not sent: %s\n", path, strerror(have_had_error));
     }
 
+    phase_add(BCP_PHASE_P_SIZES, &tph);
     uint64_t final_parity_chunk_size = max_cs + (uint64_t)n * sizeof(uint64_t);
     if (ti.is_rebuilding) {
         /* index of this (rebuilt) target in the stored header (:169-174) */
@@ -882,6 +917,7 @@ static void parity_generator(const bcp_transport_ops *T, const char *path, const
         }
     }
 
+    phase_add(BCP_PHASE_P_OPEN, &tph);
     if (res_rc) {
         int drc = drain_windows(T, ranks, n, buffer_size, expected_messages, ti.tag);
         if (drc)
@@ -919,6 +955,7 @@ static void parity_generator(const bcp_transport_ops *T, const char *path, const
             int p2 = post_recvs(T, req, n, win_b, pitch, buffer_size, ranks, ti.tag);
             trc = trc ? trc : p2;
         }
+        phase_add(BCP_PHASE_P_ROWS, &tph);
         if (trc && !have_had_error) {
             have_had_error = as_errno(trc);
             LOGERR("windows of '%s' not received: %s\n", path, strerror(have_had_error));
@@ -932,6 +969,7 @@ static void parity_generator(const bcp_transport_ops *T, const char *path, const
                 LOGERR("GPU fold of '%s' failed: %s\n", path, bcp_strerror(frc));
             }
         }
+        phase_add(BCP_PHASE_P_FOLD, &tph);
         if (!have_had_error) {
             size_t wsize = (size_t)MIN_((uint64_t)buffer_size, data_left);
             ssize_t wr = write(P_fd, pblk, wsize);
@@ -944,6 +982,7 @@ static void parity_generator(const bcp_transport_ops *T, const char *path, const
         }
         if (ti.sample)
             ti.sample->bytes_written += buffer_size;
+        phase_add(BCP_PHASE_P_WRITE, &tph);
         uint8_t *t = win_a;
         win_a = win_b;
         win_b = t;
@@ -959,6 +998,8 @@ done:
     res_release(L);
     if (P_fd != hs->fd_null)
         close(P_fd);
+    phase_add(BCP_PHASE_P_CLOSE, &tph);
+    __atomic_fetch_add(&g_phase_ns[BCP_PHASE_P_TASKS], 1, __ATOMIC_RELAXED);
 }
 
 static uint8_t *sender_buffer(size_t need)
@@ -1021,6 +1062,7 @@ static void chunk_sender(const bcp_transport_ops *T, const char *path, const Fil
     const int ntargets = active_ranks(task->locations);
     uint64_t fd_size = 0;
     int have_had_error = 0, trc = 0;
+    uint64_t tph = mono_ns();
     int fd = open_chunk_readonly(ti.read_dir, path);
     if (fd <= 0) {
         have_had_error = errno;
@@ -1057,6 +1099,7 @@ static void chunk_sender(const bcp_transport_ops *T, const char *path, const Fil
         goto done;
     }
 
+    phase_add(BCP_PHASE_S_SIZES, &tph);
     const size_t buffer_size = (size_t)MIN_(WINDOW, data_to_send);
     /* Zero copy (a transport with send_fill): every window is read straight
      * into P's window row, unless a later window could replay this one
@@ -1135,6 +1178,8 @@ done:
         LOGERR("error on '%s' is now sticky for st %d\n", path, hs->storage_target);
     if (fd != hs->fd_zero)
         close(fd);
+    phase_add(BCP_PHASE_S_SEND, &tph);
+    __atomic_fetch_add(&g_phase_ns[BCP_PHASE_S_TASKS], 1, __ATOMIC_RELAXED);
 }
 
 int process_task(HostState *hs, const char *path, const FileInfo *fi, TaskInfo ti)

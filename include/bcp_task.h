@@ -122,6 +122,24 @@ int bcp_task_set_fold_mode(int mode);
 /* Fold-service counters since the last shutdown (BATCHED mode): windows
  * folded and launches issued (windows / launches = the batching achieved). */
 int bcp_task_fold_stats(uint64_t *windows, uint64_t *launches);
+/* Wall time spent per protocol phase, summed over every task of every lane
+ * since the last reset (seconds[i] for i < nphases; the last two entries are
+ * task COUNTS, not seconds).  Returns BCP_PHASES.  P role: size exchange,
+ * resources + parity open + header, waiting for the window rows, the fold,
+ * the parity write, close; source role: open + size exchange, the window
+ * sends (from the P role's receive, i.e. the chunk reads). */
+#define BCP_PHASE_P_SIZES 0
+#define BCP_PHASE_P_OPEN 1
+#define BCP_PHASE_P_ROWS 2
+#define BCP_PHASE_P_FOLD 3
+#define BCP_PHASE_P_WRITE 4
+#define BCP_PHASE_P_CLOSE 5
+#define BCP_PHASE_S_SIZES 6
+#define BCP_PHASE_S_SEND 7
+#define BCP_PHASE_P_TASKS 8
+#define BCP_PHASE_S_TASKS 9
+#define BCP_PHASES 10
+int bcp_task_phase_stats(double *seconds, int nphases, int reset);
 /* Release the engines and every lane's queues / staging (call after all
  * lanes have joined). */
 int bcp_task_shutdown(void);

@@ -1,0 +1,8 @@
+# r02 call D: per-task protocol fold comparison with per-phase timings.
+set -o pipefail
+R=$GRAFT_REPO_ROOT; cd $R
+O=$R/gpurun_out/r2d; mkdir -p $O
+nproc > $O/host.txt; cat /sys/fs/cgroup/cpu.max >> $O/host.txt 2>/dev/null; python -c "import os; print(len(os.sched_getaffinity(0)))" >> $O/host.txt
+timeout -k 10 600 python -u tools/proto_compare.py --rounds 4 > $O/proto_compare.jsonl 2> $O/proto_compare.err || { echo PROTO_FAIL; tail -20 $O/proto_compare.err; exit 1; }
+cat $O/host.txt
+echo ALL_OK

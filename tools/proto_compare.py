@@ -74,16 +74,23 @@ def fold_setup(fold, hooks):
 def measure(name, folds, rounds, run_once, verify_fn, nbytes, hooks, extra=None):
     times = {f: [] for f in folds}
     batching = {}
+    phases = {}
     for r in range(rounds + 1):
         order = folds[r % len(folds):] + folds[:r % len(folds)]
         for f in order:
             restore = fold_setup(f, hooks)
             try:
                 w0, l0 = bcp.fold_stats()
+                bcp.phase_stats(reset=True)
                 t0 = time.perf_counter()
                 st = run_once()
                 dt = time.perf_counter() - t0
                 w1, l1 = bcp.fold_stats()
+                ph = bcp.phase_stats()
+                if r > 0:
+                    acc = phases.setdefault(f, {})
+                    for k, v in ph.items():
+                        acc[k] = acc.get(k, 0) + v
             finally:
                 restore()
             if st.errors:
@@ -105,6 +112,13 @@ def measure(name, folds, rounds, run_once, verify_fn, nbytes, hooks, extra=None)
                     runs_s=[round(x, 4) for x in times[f]], cold_s=round(times[f][0], 4))
         if f == "gpu_batched" and batching.get("launches"):
             line["windows_per_launch"] = round(batching["windows"] / batching["launches"], 2)
+        acc = phases.get(f)
+        if acc and acc.get("p_tasks"):
+            # mean wall microseconds per P task / per source task in each phase
+            line["p_phase_us"] = {k[2:]: round(acc[k] / acc["p_tasks"] * 1e6, 1) for k in acc
+                                  if k.startswith("p_") and k != "p_tasks"}
+            line["s_phase_us"] = {k[2:]: round(acc[k] / max(acc["s_tasks"], 1) * 1e6, 1) for k in acc
+                                  if k.startswith("s_") and k != "s_tasks"}
         if extra:
             line.update(extra)
         emit(**line)
