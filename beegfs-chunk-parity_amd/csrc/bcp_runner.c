@@ -582,7 +582,7 @@ static int update_replicas(const char *root, int ntargets, const bcp_work_item *
     return rc;
 }
 
-static int round_impl(bcp_pipeline *pl, const char *store_root, int ntargets, const bcp_eventset *events,
+static int round_impl(bcp_pipeline *pl, int procs, const char *store_root, int ntargets, const bcp_eventset *events,
                       const int *cum_weight_in, int nlanes, FILE *log, bcp_run_stats *stats, size_t *nplanned)
 {
     if (!store_root || !events || ntargets < 1 || ntargets > MAX_STORAGE_TARGETS)
@@ -614,12 +614,13 @@ static int round_impl(bcp_pipeline *pl, const char *store_root, int ntargets, co
         work = malloc((n ? n : 1) * sizeof(bcp_work_item));
         rc = work ? bcp_plan_worklist(events, ntargets, cw, prev, nprev, work, n, &n) : -ENOMEM;
     }
-    if (!rc && !pl)
+    if (!rc && !pl && !procs)
         rc = bcp_gen_run_db(store_root, ntargets, work, n, nlanes, NULL, log, stats);
-    if (!rc && pl) {
+    if (!rc && (pl || procs)) {
         bcp_run_stats st;
         memset(&st, 0, sizeof(st));
-        rc = bcp_pipeline_run(pl, store_root, ntargets, work, n, log, &st);
+        rc = pl ? bcp_pipeline_run(pl, store_root, ntargets, work, n, log, &st)
+                : bcp_gen_run_procs(store_root, ntargets, work, n, nlanes, NULL, log, &st);
         if (!rc && st.errors == 0)
             rc = update_replicas(store_root, ntargets, work, n); /* only after the parity is on disk */
         if (stats)
@@ -635,7 +636,13 @@ static int round_impl(bcp_pipeline *pl, const char *store_root, int ntargets, co
 int bcp_gen_round(const char *store_root, int ntargets, const bcp_eventset *events, const int *cum_weight,
                   int nlanes, FILE *log, bcp_run_stats *stats, size_t *nplanned)
 {
-    return round_impl(NULL, store_root, ntargets, events, cum_weight, nlanes, log, stats, nplanned);
+    return round_impl(NULL, 0, store_root, ntargets, events, cum_weight, nlanes, log, stats, nplanned);
+}
+
+int bcp_gen_round_procs(const char *store_root, int ntargets, const bcp_eventset *events, const int *cum_weight,
+                        int nlanes, FILE *log, bcp_run_stats *stats, size_t *nplanned)
+{
+    return round_impl(NULL, 1, store_root, ntargets, events, cum_weight, nlanes, log, stats, nplanned);
 }
 
 int bcp_gen_round_pipeline(bcp_pipeline *pl, const char *store_root, int ntargets, const bcp_eventset *events,
@@ -643,7 +650,7 @@ int bcp_gen_round_pipeline(bcp_pipeline *pl, const char *store_root, int ntarget
 {
     if (!pl)
         return -EINVAL;
-    return round_impl(pl, store_root, ntargets, events, cum_weight, 0, log, stats, nplanned);
+    return round_impl(pl, 0, store_root, ntargets, events, cum_weight, 0, log, stats, nplanned);
 }
 
 /* ---- ranks as processes (bcp_gen_run_procs / bcp_rebuild_run_procs) -------

@@ -5,19 +5,23 @@
  *
  *   bcp find-all-chunks <chunks_dir>
  *       bp-find-all-chunks: the record stream on stdout.
- *   bcp parity-gen --complete|--partial [--pipeline] [--lanes N] [--force]
- *                  [--changelog DIR] <store_root> <ntargets>
+ *   bcp parity-gen --complete|--partial [--pipeline|--procs] [--fold MODE] [--lanes N]
+ *                  [--force] [--changelog DIR] <store_root> <ntargets>
  *       beegfs-parity-gen + bp-parity-gen (src/beegfs-parity-gen:1-135,
  *       gen/main.c): target bookkeeping, phase 1 from a scan of every
  *       target (--complete) or from record files DIR/st<k> (--partial,
  *       default DIR = <root>/changelog), then one round against the
- *       persistent state, through the per-rank protocol (default, 12 lanes)
- *       or the batched pipeline.  A --complete over an existing state needs
+ *       persistent state, through the per-rank protocol (default, 12 lanes;
+ *       ranks as threads, or with --procs as one process per target, as
+ *       under mpirun) or the batched pipeline.  --fold picks the P role's GPU
+ *       fold: batched, streamed, zero-copy or staged.  A --complete over an existing state needs
  *       --force and first deletes the old parity data and DBs (the script's
  *       clean_old, :94-108, :120-126).  On success <root>/last-gen-timestamp.
- *   bcp parity-rebuild [--pipeline] [--db DIR] [--corrupt FILE] <store_root> <ntargets> <target>
+ *   bcp parity-rebuild [--pipeline|--procs] [--fold MODE] [--db DIR] [--corrupt FILE]
+ *                      <store_root> <ntargets> <target>
  *       beegfs-parity-rebuild + bp-parity-rebuild (rebuild/main.c), through
- *       the per-rank protocol (default) or the batched pipeline.
+ *       the per-rank protocol (default; --procs: rank processes) or the
+ *       batched pipeline.
  *
  * Exit status 0 on success, 1 on any error (message on stderr).
  */
@@ -36,11 +40,26 @@
 static int usage(void)
 {
     fputs("usage: bcp find-all-chunks <chunks_dir>\n"
-          "       bcp parity-gen --complete|--partial [--pipeline] [--lanes N] [--force]\n"
+          "       bcp parity-gen --complete|--partial [--pipeline|--procs] [--fold MODE] [--lanes N] [--force]\n"
           "                      [--changelog DIR] <store_root> <ntargets>\n"
-          "       bcp parity-rebuild [--pipeline] [--db DIR] [--corrupt FILE] <store_root> <ntargets> <target>\n",
+          "       bcp parity-rebuild [--pipeline|--procs] [--fold MODE] [--db DIR] [--corrupt FILE]\n"
+          "                          <store_root> <ntargets> <target>\n"
+          "       MODE: batched | streamed | zero-copy | staged\n",
           stderr);
     return 1;
+}
+
+static int fold_mode_arg(const char *s)
+{
+    if (!strcmp(s, "batched"))
+        return BCP_FOLD_BATCHED;
+    if (!strcmp(s, "streamed"))
+        return BCP_FOLD_STREAMED;
+    if (!strcmp(s, "zero-copy"))
+        return BCP_FOLD_ZERO_COPY;
+    if (!strcmp(s, "staged"))
+        return BCP_FOLD_STAGED;
+    return -1;
 }
 
 static int fail(const char *what, int rc)
@@ -84,7 +103,7 @@ static double now_s(void)
 static int cmd_gen(int argc, char **argv)
 {
     const double t_start = now_s();
-    int complete = -1, use_pipeline = 0, lanes = 12, force = 0;
+    int complete = -1, use_pipeline = 0, use_procs = 0, lanes = 12, force = 0;
     const char *changelog = NULL;
     int i = 0;
     for (; i < argc && argv[i][0] == '-'; i++) {
@@ -94,6 +113,12 @@ static int cmd_gen(int argc, char **argv)
             complete = 0;
         else if (!strcmp(argv[i], "--pipeline"))
             use_pipeline = 1;
+        else if (!strcmp(argv[i], "--procs"))
+            use_procs = 1;
+        else if (!strcmp(argv[i], "--fold") && i + 1 < argc) {
+            if (fold_mode_arg(argv[++i]) < 0 || bcp_task_set_fold_mode(fold_mode_arg(argv[i])) < 0)
+                return usage();
+        }
         else if (!strcmp(argv[i], "--force"))
             force = 1;
         else if (!strcmp(argv[i], "--lanes") && i + 1 < argc)
@@ -103,7 +128,7 @@ static int cmd_gen(int argc, char **argv)
         else
             return usage();
     }
-    if (complete < 0 || argc - i != 2)
+    if (complete < 0 || argc - i != 2 || (use_pipeline && use_procs))
         return usage();
     const char *root = argv[i];
     const int ntargets = atoi(argv[i + 1]);
@@ -170,6 +195,8 @@ static int cmd_gen(int argc, char **argv)
             rc = bcp_gen_round_pipeline(pl, root, ntargets, es, NULL, stderr, &st, &planned);
         if (pl)
             bcp_pipeline_destroy(pl);
+    } else if (use_procs) {
+        rc = bcp_gen_round_procs(root, ntargets, es, NULL, lanes, stderr, &st, &planned);
     } else {
         rc = bcp_gen_round(root, ntargets, es, NULL, lanes, stderr, &st, &planned);
         bcp_task_shutdown();
@@ -198,7 +225,7 @@ static int cmd_gen(int argc, char **argv)
 static int cmd_rebuild(int argc, char **argv)
 {
     const char *db = NULL, *corrupt = NULL;
-    int use_pipeline = 0;
+    int use_pipeline = 0, use_procs = 0;
     int i = 0;
     for (; i < argc && argv[i][0] == '-'; i++) {
         if (!strcmp(argv[i], "--db") && i + 1 < argc)
@@ -207,17 +234,22 @@ static int cmd_rebuild(int argc, char **argv)
             corrupt = argv[++i];
         else if (!strcmp(argv[i], "--pipeline"))
             use_pipeline = 1;
-        else
+        else if (!strcmp(argv[i], "--procs"))
+            use_procs = 1;
+        else if (!strcmp(argv[i], "--fold") && i + 1 < argc) {
+            if (fold_mode_arg(argv[++i]) < 0 || bcp_task_set_fold_mode(fold_mode_arg(argv[i])) < 0)
+                return usage();
+        } else
             return usage();
     }
-    if (argc - i != 3)
+    if (argc - i != 3 || (use_pipeline && use_procs))
         return usage();
     const char *root = argv[i];
     const int ntargets = atoi(argv[i + 1]), target = atoi(argv[i + 2]);
     bcp_run_stats st;
     memset(&st, 0, sizeof(st));
     int rc;
-    if (use_pipeline) {
+    if (use_pipeline || use_procs) {
         char dp[4096];
         if (!db) {
             snprintf(dp, sizeof(dp), "%s/st%d/db", root, target == 0 ? 1 : 0);
@@ -234,13 +266,16 @@ static int cmd_rebuild(int argc, char **argv)
             rc = bcp_pdb_items(pdb, &items, &n);
             bcp_pdb_close(pdb);
         }
-        bcp_pipeline *pl = NULL;
-        if (!rc)
+        if (!rc && use_procs) {
+            rc = bcp_rebuild_run_procs(root, ntargets, target, items, n, corrupt, stderr, &st);
+        } else if (!rc) {
+            bcp_pipeline *pl = NULL;
             rc = bcp_pipeline_create(NULL, &pl);
-        if (!rc)
-            rc = bcp_pipeline_rebuild(pl, root, ntargets, target, items, n, corrupt, stderr, &st);
-        if (pl)
-            bcp_pipeline_destroy(pl);
+            if (!rc)
+                rc = bcp_pipeline_rebuild(pl, root, ntargets, target, items, n, corrupt, stderr, &st);
+            if (pl)
+                bcp_pipeline_destroy(pl);
+        }
         bcp_pdb_items_free(items);
     } else {
         rc = bcp_rebuild_run_db(root, ntargets, target, db, corrupt, stderr, &st);

@@ -364,6 +364,10 @@ int bcp_store_cum_weights(const char *store_root, int ntargets, int *cum_weight)
  * own weights), then bcp_gen_run_db.  *nplanned = worklist length. */
 int bcp_gen_round(const char *store_root, int ntargets, const bcp_eventset *events, const int *cum_weight,
                   int nlanes, FILE *log, bcp_run_stats *stats, size_t *nplanned);
+/* The same round with rank processes (bcp_gen_run_procs); every replica is
+ * updated after the run, only when it finished without errors. */
+int bcp_gen_round_procs(const char *store_root, int ntargets, const bcp_eventset *events, const int *cum_weight,
+                        int nlanes, FILE *log, bcp_run_stats *stats, size_t *nplanned);
 
 /* ---- batched end-to-end pipeline (loopback stores) ---------------------- */
 typedef struct {

@@ -291,10 +291,13 @@ def test_db_round_then_partial_round_then_rebuild(bcp, oracle, tmp_path, engine_
         assert S.read_file(S.chunk_path(root, victim, path)) == data, path
 
 
-@pytest.mark.parametrize("pipeline", [False, True])
-def test_cli_complete_partial_rebuild(bcp, oracle, tmp_path, pipeline):
+@pytest.mark.parametrize("engine_kind", ["protocol", "pipeline", "procs"])
+def test_cli_complete_partial_rebuild(bcp, oracle, tmp_path, engine_kind):
     """bin/bcp end to end on the device: --complete (scan of every target),
-    --partial from changelog record files, then parity-rebuild from the DB."""
+    --partial from changelog record files, then parity-rebuild from the DB --
+    ranks as threads, the batched pipeline, or ranks as processes (--procs:
+    one forked process per target on the socketpair transport, each with its
+    own HIP context, P roles folding with the streamed GPU fold)."""
     import subprocess
     import planner as PL
     rng = np.random.default_rng(21)
@@ -310,7 +313,7 @@ def test_cli_complete_partial_rebuild(bcp, oracle, tmp_path, pipeline):
             S.write_chunk(root, h, path, d)
             arrs.append(d)
         files[path], contents[path] = holders, arrs
-    flags = ["--pipeline"] if pipeline else []
+    flags = {"protocol": [], "pipeline": ["--pipeline"], "procs": ["--procs", "--fold", "streamed"]}[engine_kind]
     r = subprocess.run([bcp.BIN_PATH, "parity-gen", "--complete", *flags, root, str(nt)], capture_output=True)
     assert r.returncode == 0, r.stderr
     db = bcp.PDB(os.path.join(root, "st0", "db"))
@@ -342,7 +345,7 @@ def test_cli_complete_partial_rebuild(bcp, oracle, tmp_path, pipeline):
         if victim in holders:
             lost[p_] = S.read_file(S.chunk_path(root, victim, p_))
             os.remove(S.chunk_path(root, victim, p_))
-    r = subprocess.run([bcp.BIN_PATH, "parity-rebuild", root, str(nt), str(victim)], capture_output=True)
+    r = subprocess.run([bcp.BIN_PATH, "parity-rebuild", *flags, root, str(nt), str(victim)], capture_output=True)
     assert r.returncode == 0, r.stderr
     for p_, data in lost.items():
         assert S.read_file(S.chunk_path(root, victim, p_)) == data, p_
