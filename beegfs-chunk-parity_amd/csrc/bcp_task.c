@@ -195,16 +195,22 @@ static int engine_for_target(int st, bcp_engine **out, int *device)
 }
 
 /* ---- fold service (BCP_FOLD_BATCHED) --------------------------------------
- * One per device.  P roles append their window (rows + output, mapped pinned
- * memory) and sleep; the flusher takes EVERYTHING pending, folds it with one
- * descriptor batch on its own queue, syncs once and wakes the lanes whose
- * windows were in it.  While a batch is on the device the next one gathers,
- * so the batch size follows the load: one window when a lane is alone, up to
- * every concurrent P role when all twelve lanes of every rank fold at once. */
+ * One per device, flat combining: a P role appends its window (rows +
+ * output, mapped pinned memory; row j's data bytes) and, if no batch is on
+ * the device, becomes the leader -- it takes EVERY pending window (its own
+ * included), folds them with one descriptor batch on the service's queue,
+ * syncs once and completes them all; otherwise it sleeps until a leader has
+ * completed its window, or leads the next batch itself.  The batch size
+ * follows the load with no thread of its own: a lone lane (the single rebuild
+ * lane) folds its window directly, twelve lanes of every rank share one
+ * launch.  Rows are read over PCIe for their data bytes only: a gen-mode
+ * window is padded to the stripe's largest chunk, and the padding is zeros
+ * the kernel supplies itself. */
 typedef struct fold_job {
     struct fold_job *next;
     const uint8_t *rows;
     size_t pitch, nbytes;
+    const size_t *valid;
     int n;
     uint8_t *out;
     int done, rc;
@@ -213,10 +219,9 @@ typedef struct fold_job {
 typedef struct {
     bcp_engine *eng;
     bcp_queue *q;
-    pthread_t th;
-    int stop;
+    int busy; /* a leader's batch is on the device */
     pthread_mutex_t mu;
-    pthread_cond_t cv_work, cv_done;
+    pthread_cond_t cv_done;
     fold_job *head, *tail;
     bcp_stripe *st;
     bcp_source *so;
@@ -246,47 +251,25 @@ static int svc_tables(fold_svc *S, size_t nst, size_t nso)
     return 0;
 }
 
-static void *svc_main(void *p)
+/* The leader's batch (called without S->mu; S->busy keeps it exclusive). */
+static int svc_fold(fold_svc *S, fold_job *batch)
 {
-    fold_svc *S = p;
-    pthread_mutex_lock(&S->mu);
-    for (;;) {
-        while (!S->head && !S->stop)
-            pthread_cond_wait(&S->cv_work, &S->mu);
-        if (!S->head)
-            break; /* stop, nothing pending */
-        fold_job *batch = S->head;
-        S->head = S->tail = NULL;
-        pthread_mutex_unlock(&S->mu);
-        size_t nst = 0, nso = 0;
-        for (fold_job *j = batch; j; j = j->next) {
-            nst++;
-            nso += (size_t)j->n;
-        }
-        int rc = nst > 0xFFFFFFFFu || nso > 0xFFFFFFFFu ? -EINVAL : svc_tables(S, nst, nso);
-        if (!rc) {
-            size_t i = 0, k = 0;
-            for (fold_job *j = batch; j; j = j->next, i++) {
-                S->st[i] = (bcp_stripe){(uint64_t)(uintptr_t)j->out, j->nbytes, (uint32_t)k, (uint32_t)j->n, 0};
-                for (int r = 0; r < j->n; r++, k++)
-                    S->so[k] = (bcp_source){(uint64_t)(uintptr_t)(j->rows + (size_t)r * j->pitch), j->nbytes};
-            }
-            rc = bcp_xor_stripes_async(S->q, S->st, (uint32_t)nst, S->so, (uint32_t)nso);
-            if (!rc)
-                rc = bcp_queue_sync(S->q);
-        }
-        pthread_mutex_lock(&S->mu);
-        for (fold_job *j = batch, *nx; j; j = nx) {
-            nx = j->next; /* j lives on its lane's stack: read next before done */
-            j->rc = rc;
-            j->done = 1;
-        }
-        S->windows += nst;
-        S->launches += 1;
-        pthread_cond_broadcast(&S->cv_done);
+    size_t nst = 0, nso = 0;
+    for (fold_job *j = batch; j; j = j->next) {
+        nst++;
+        nso += (size_t)j->n;
     }
-    pthread_mutex_unlock(&S->mu);
-    return NULL;
+    int rc = nst > 0xFFFFFFFFu || nso > 0xFFFFFFFFu ? -EINVAL : svc_tables(S, nst, nso);
+    if (rc)
+        return rc;
+    size_t i = 0, k = 0;
+    for (fold_job *j = batch; j; j = j->next, i++) {
+        S->st[i] = (bcp_stripe){(uint64_t)(uintptr_t)j->out, j->nbytes, (uint32_t)k, (uint32_t)j->n, 0};
+        for (int r = 0; r < j->n; r++, k++)
+            S->so[k] = (bcp_source){(uint64_t)(uintptr_t)(j->rows + (size_t)r * j->pitch), j->valid[r]};
+    }
+    rc = bcp_xor_stripes_async(S->q, S->st, (uint32_t)nst, S->so, (uint32_t)nso);
+    return rc ? rc : bcp_queue_sync(S->q);
 }
 
 static void svc_destroy(fold_svc *S)
@@ -295,7 +278,6 @@ static void svc_destroy(fold_svc *S)
         return;
     if (S->q)
         bcp_queue_destroy(S->q);
-    pthread_cond_destroy(&S->cv_work);
     pthread_cond_destroy(&S->cv_done);
     pthread_mutex_destroy(&S->mu);
     free(S->st);
@@ -303,7 +285,7 @@ static void svc_destroy(fold_svc *S)
     free(S);
 }
 
-/* The service of device dev (started on first use; under g_lock). */
+/* The service of device dev (made on first use). */
 static int svc_get(int dev, bcp_engine *e, fold_svc **out)
 {
     pthread_mutex_lock(&g_lock);
@@ -316,9 +298,8 @@ static int svc_get(int dev, bcp_engine *e, fold_svc **out)
         else {
             S->eng = e;
             pthread_mutex_init(&S->mu, NULL);
-            pthread_cond_init(&S->cv_work, NULL);
             pthread_cond_init(&S->cv_done, NULL);
-            if ((rc = bcp_queue_create(e, &S->q)) || (rc = -pthread_create(&S->th, NULL, svc_main, S))) {
+            if ((rc = bcp_queue_create(e, &S->q))) {
                 svc_destroy(S);
                 S = NULL;
             } else {
@@ -331,18 +312,39 @@ static int svc_get(int dev, bcp_engine *e, fold_svc **out)
     return rc;
 }
 
-static int fold_batched(fold_svc *S, const uint8_t *rows, size_t pitch, size_t nbytes, int n, uint8_t *out)
+static int fold_batched(fold_svc *S, const uint8_t *rows, size_t pitch, const size_t *valid, size_t nbytes, int n,
+                        uint8_t *out)
 {
-    fold_job j = {NULL, rows, pitch, nbytes, n, out, 0, 0};
+    fold_job j = {NULL, rows, pitch, nbytes, valid, n, out, 0, 0};
     pthread_mutex_lock(&S->mu);
     if (S->tail)
         S->tail->next = &j;
     else
         S->head = &j;
     S->tail = &j;
-    pthread_cond_signal(&S->cv_work);
-    while (!j.done)
-        pthread_cond_wait(&S->cv_done, &S->mu);
+    while (!j.done) {
+        if (S->busy) {
+            pthread_cond_wait(&S->cv_done, &S->mu);
+            continue;
+        }
+        /* lead: everything pending, this window included */
+        S->busy = 1;
+        fold_job *batch = S->head;
+        S->head = S->tail = NULL;
+        pthread_mutex_unlock(&S->mu);
+        const int rc = svc_fold(S, batch);
+        pthread_mutex_lock(&S->mu);
+        size_t nb = 0;
+        for (fold_job *x = batch, *nx; x; x = nx, nb++) {
+            nx = x->next; /* x lives on its lane's stack: read next before done */
+            x->rc = rc;
+            x->done = 1;
+        }
+        S->windows += nb;
+        S->launches += 1;
+        S->busy = 0;
+        pthread_cond_broadcast(&S->cv_done);
+    }
     pthread_mutex_unlock(&S->mu);
     return j.rc;
 }
@@ -431,29 +433,19 @@ void bcp_task_thread_release(void)
 int bcp_task_shutdown(void)
 {
     bcp_task_thread_release();
-    /* fold services first: they hold queues on the engines */
-    fold_svc *svc[MAX_DEVICES];
+    /* fold services first: they hold queues on the engines (all lanes have
+     * returned, so no batch is in flight) */
     pthread_mutex_lock(&g_lock);
     for (int d = 0; d < MAX_DEVICES; d++) {
-        svc[d] = g_svc[d];
+        fold_svc *S = g_svc[d];
         g_svc[d] = NULL;
-    }
-    pthread_mutex_unlock(&g_lock);
-    for (int d = 0; d < MAX_DEVICES; d++) {
-        fold_svc *S = svc[d];
         if (!S)
             continue;
-        pthread_mutex_lock(&S->mu);
-        S->stop = 1;
-        pthread_cond_signal(&S->cv_work);
-        pthread_mutex_unlock(&S->mu);
-        pthread_join(S->th, NULL);
-        pthread_mutex_lock(&g_lock);
         g_svc_windows += S->windows;
         g_svc_launches += S->launches;
-        pthread_mutex_unlock(&g_lock);
         svc_destroy(S);
     }
+    pthread_mutex_unlock(&g_lock);
     pthread_mutex_lock(&g_lock);
     fold_res *R = g_pool;
     g_pool = NULL;
@@ -568,7 +560,7 @@ fail:
 /* The fold of one window (replaces xor_parity at task_processing.c:211):
  * out = XOR of n rows of `pitch` bytes, nbytes each. */
 static int fold_window(fold_res *R, HostState *hs, bcp_xor_hook_fn hook, void *ctx, const uint8_t *rows,
-                       size_t pitch, size_t nbytes, int n, uint8_t *out)
+                       size_t pitch, const size_t *valid, size_t nbytes, int n, uint8_t *out)
 {
     if (hook) {
         static int warned = 0; /* lanes race here: atomic exchange */
@@ -584,7 +576,7 @@ static int fold_window(fold_res *R, HostState *hs, bcp_xor_hook_fn hook, void *c
         fold_svc *S = NULL;
         if ((rc = svc_get(R->device, R->eng, &S)))
             return rc;
-        return fold_batched(S, rows, pitch, nbytes, n, out);
+        return fold_batched(S, rows, pitch, valid, nbytes, n, out);
     }
     if (!R->q && (rc = bcp_queue_create(R->eng, &R->q)))
         return rc;
@@ -963,7 +955,7 @@ static void parity_generator(const bcp_transport_ops *T, const char *path, const
         /* fold window msg_i on the GPU while the senders fill win_b */
         if (!have_had_error) {
             int frc = streamed ? stream_fold(L, n, pitch, valid, buffer_size, pblk)
-                               : fold_window(L, hs, hook, hook_ctx, win_a, pitch, buffer_size, n, pblk);
+                               : fold_window(L, hs, hook, hook_ctx, win_a, pitch, valid, buffer_size, n, pblk);
             if (frc) {
                 have_had_error = EIO;
                 LOGERR("GPU fold of '%s' failed: %s\n", path, bcp_strerror(frc));
