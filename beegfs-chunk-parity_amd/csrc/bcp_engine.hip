@@ -546,12 +546,23 @@ extern "C" int bcp_host_alloc(bcp_engine *eng, size_t bytes, void **hptr) {
   return 0;
 }
 
+// Mapped pinned memory for the P role's rows and output.  Experiment knob
+// BCP_MAPPED_FLAGS (tools/exp: which host memory kind the protocol's CPU
+// copies and the zero-copy kernel prefer): 0 coherent (default), 1
+// non-coherent, 2 coherent + NUMA placement by the calling thread's policy,
+// 3 non-coherent + NUMA by policy.
 extern "C" int bcp_host_alloc_mapped(bcp_engine *eng, size_t bytes, void **hptr) {
   if (!eng || !hptr) return -EINVAL;
   *hptr = nullptr;
   int rc = set_device(eng);
   if (rc) return rc;
-  HIP_RC(hipHostMalloc(hptr, bytes ? bytes : 16, hipHostMallocMapped | hipHostMallocCoherent));
+  unsigned flags = hipHostMallocMapped | hipHostMallocCoherent;
+  if (const char *v = getenv("BCP_MAPPED_FLAGS")) {
+    const int k = atoi(v);
+    flags = hipHostMallocMapped | ((k & 1) ? hipHostMallocNonCoherent : hipHostMallocCoherent) |
+            ((k & 2) ? hipHostMallocNumaUser : 0u);
+  }
+  HIP_RC(hipHostMalloc(hptr, bytes ? bytes : 16, flags));
   return 0;
 }
 

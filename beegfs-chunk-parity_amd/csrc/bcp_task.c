@@ -866,7 +866,11 @@ static void parity_generator(const bcp_transport_ops *T, const char *path, const
     if (!have_had_error)
         have_had_error = __atomic_load_n(&hs->error, __ATOMIC_ACQUIRE);
     fold_res *L = NULL;
-    int res_rc = expected_messages ? res_acquire(hs, hook == NULL, pitch * (size_t)n, buffer_size, &L) : 0;
+    /* (experiment knob BCP_HOOK_PINNED_ROWS: the test-hook fold over the same
+     * pinned device-mapped rows the GPU folds use, to separate the memory
+     * kind from the fold in tools/exp measurements) */
+    const int pinned_rows = hook == NULL || getenv("BCP_HOOK_PINNED_ROWS") != NULL;
+    int res_rc = expected_messages ? res_acquire(hs, pinned_rows, pitch * (size_t)n, buffer_size, &L) : 0;
     if (res_rc) {
         LOGERR("no fold resources for '%s' on st %d: %s\n", path, hs->storage_target, bcp_strerror(res_rc));
         if (!have_had_error)
