@@ -14,6 +14,7 @@
 //    counter, base advanced on the host per launch).
 #include <errno.h>
 #include <stdio.h>
+#include <sys/mman.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -546,11 +547,70 @@ extern "C" int bcp_host_alloc(bcp_engine *eng, size_t bytes, void **hptr) {
   return 0;
 }
 
-// Mapped pinned memory for the P role's rows and output.  Experiment knob
-// BCP_MAPPED_FLAGS (tools/exp: which host memory kind the protocol's CPU
-// copies and the zero-copy kernel prefer): 0 coherent (default), 1
-// non-coherent, 2 coherent + NUMA placement by the calling thread's policy,
-// 3 non-coherent + NUMA by policy.
+// Ordinary (THP-backed) host memory registered with HIP: allocations made
+// by bcp_host_alloc_mapped in "registered" form, freed by bcp_host_free.
+namespace {
+struct RegAlloc {
+  RegAlloc *next;
+  void *p;
+};
+pthread_mutex_t g_reg_lock = PTHREAD_MUTEX_INITIALIZER;
+RegAlloc *g_reg = nullptr;
+
+// posix_memalign (2 MiB, MADV_HUGEPAGE) + first touch + hipHostRegister
+// (mapped): the CPU side stays normal write-back, huge-page-backed memory;
+// the device reads and writes it at the same address.
+int alloc_registered(size_t bytes, void **out) {
+  const size_t huge = (size_t)2 << 20;
+  const size_t n = (bytes + huge - 1) / huge * huge;
+  RegAlloc *r = (RegAlloc *)malloc(sizeof(RegAlloc));
+  void *p = nullptr;
+  if (!r || posix_memalign(&p, huge, n) != 0) {
+    free(r);
+    return -ENOMEM;
+  }
+  (void)madvise(p, n, MADV_HUGEPAGE);
+  memset(p, 0, n);  // fault the pages in here, not under the first copy
+  void *dev = nullptr;
+  if (hipHostRegister(p, n, hipHostRegisterMapped) != hipSuccess ||
+      hipHostGetDevicePointer(&dev, p, 0) != hipSuccess || dev != p) {
+    (void)hipGetLastError();
+    if (dev) (void)hipHostUnregister(p);
+    free(p);
+    free(r);
+    return -EIO;  // the kernels address host rows by their host address
+  }
+  r->p = p;
+  pthread_mutex_lock(&g_reg_lock);
+  r->next = g_reg;
+  g_reg = r;
+  pthread_mutex_unlock(&g_reg_lock);
+  *out = p;
+  return 0;
+}
+
+// 1 if p came from alloc_registered (then unregistered and freed here).
+int free_registered(void *p) {
+  pthread_mutex_lock(&g_reg_lock);
+  RegAlloc **pp = &g_reg;
+  while (*pp && (*pp)->p != p) pp = &(*pp)->next;
+  RegAlloc *r = *pp;
+  if (r) *pp = r->next;
+  pthread_mutex_unlock(&g_reg_lock);
+  if (!r) return 0;
+  (void)hipHostUnregister(p);
+  free(p);
+  free(r);
+  return 1;
+}
+}  // namespace
+
+// Mapped host memory for the P role's rows and output.  Experiment knob
+// BCP_MAPPED_FLAGS (tools/exp/host_kind_ab.py: which host memory kind the
+// protocol's CPU copies and the zero-copy kernel prefer): 0 hipHostMalloc
+// coherent (default), 1 non-coherent, 2 coherent + NUMA placement by the
+// calling thread's policy, 3 non-coherent + NUMA by policy, 4 ordinary
+// huge-page memory registered with hipHostRegister.
 extern "C" int bcp_host_alloc_mapped(bcp_engine *eng, size_t bytes, void **hptr) {
   if (!eng || !hptr) return -EINVAL;
   *hptr = nullptr;
@@ -559,6 +619,7 @@ extern "C" int bcp_host_alloc_mapped(bcp_engine *eng, size_t bytes, void **hptr)
   unsigned flags = hipHostMallocMapped | hipHostMallocCoherent;
   if (const char *v = getenv("BCP_MAPPED_FLAGS")) {
     const int k = atoi(v);
+    if (k == 4) return alloc_registered(bytes ? bytes : 16, hptr);
     flags = hipHostMallocMapped | ((k & 1) ? hipHostMallocNonCoherent : hipHostMallocCoherent) |
             ((k & 2) ? hipHostMallocNumaUser : 0u);
   }
@@ -569,6 +630,7 @@ extern "C" int bcp_host_alloc_mapped(bcp_engine *eng, size_t bytes, void **hptr)
 extern "C" int bcp_host_free(bcp_engine *eng, void *hptr) {
   if (!eng) return -EINVAL;
   if (!hptr) return 0;
+  if (free_registered(hptr)) return 0;
   HIP_RC(hipHostFree(hptr));
   return 0;
 }

@@ -3,7 +3,8 @@
 per-task protocol with the batched GPU fold and the reference CPU fold, the
 CPU fold once over malloc'd rows and once over the same pinned mapped rows
 the GPU uses (BCP_HOOK_PINNED_ROWS), for each BCP_MAPPED_FLAGS variant
-(0 coherent, 1 non-coherent, 2 coherent + NUMA by policy, 3 both).
+(0 coherent, 1 non-coherent, 2 coherent + NUMA by policy, 3 both, 4 THP
+malloc + hipHostRegister).  A warm-up run per variant (pinning) is dropped.
 Interleaved rounds; one JSON line per (variant, fold)."""
 import ctypes
 import json
@@ -48,10 +49,13 @@ def run():
 
 
 res = {}
+VARS = sys.argv[2].split(",") if len(sys.argv) > 2 else ["0", "1", "4"]
 for rnd in range(4):
-    for var in ("0", "1", "2", "3"):
+    for var in VARS:
         os.environ["BCP_MAPPED_FLAGS"] = var
         bcp.task_shutdown()  # drop pooled rows: the next allocations take the variant
+        bcp.set_fold_mode(bcp.FOLD_BATCHED)
+        run()  # warm-up: the variant's rows get allocated and pinned
         for fold in ("gpu_batched", "cpu_pinned_rows", "cpu_malloc_rows"):
             if fold == "gpu_batched":
                 bcp.set_fold_mode(bcp.FOLD_BATCHED)
@@ -64,7 +68,7 @@ for rnd in range(4):
             finally:
                 bcp.set_xor_hook(None)
                 os.environ.pop("BCP_HOOK_PINNED_ROWS", None)
-            if rnd:
+            if rnd >= 0:
                 res.setdefault((var, fold), []).append(dt)
 for (var, fold), ts in sorted(res.items()):
     print(json.dumps({"mapped_flags": int(var), "fold": fold, "GiBps": round((rd + wr) / float(np.median(ts)) / GiB, 3),
