@@ -276,6 +276,7 @@ extern "C" int bcp_engine_create(int device, bcp_engine **out) {
     e->tuning.vecs_per_thread = defaults.vecs_per_thread;
   if (const char *v = getenv("BCP_SCHEDULE")) e->tuning.schedule = atoi(v) == kSchedStatic ? kSchedStatic : kSchedQueue;
   if (const char *v = getenv("BCP_SYNC_MODE")) e->tuning.sync_mode = atoi(v) == 1 ? 1 : 0;
+  if (const char *v = getenv("BCP_HOST_REGISTERED")) e->tuning.host_registered = atoi(v) ? 1 : 0;
   *out = e;
   return 0;
 }
@@ -319,6 +320,7 @@ extern "C" int bcp_set_option(bcp_engine *eng, const char *key, int value) {
   else if (!strcmp(key, "table_wpe") && (value == 0 || (value >= 5 && value <= 7))) eng->tuning.table_wpe = value;
   else if (!strcmp(key, "stream_grab") && value >= 0 && value <= 64) eng->tuning.stream_grab = value;
   else if (!strcmp(key, "sync_mode") && (value == 0 || value == 1)) eng->tuning.sync_mode = value;
+  else if (!strcmp(key, "host_registered") && (value == 0 || value == 1)) eng->tuning.host_registered = value;
   else if (!strcmp(key, "desc_pipe") && (value == 0 || value == 2 || value == 4 || value == 5))
     eng->tuning.desc_pipe = value;
   else if (!strcmp(key, "desc_table_host_max") && value >= 0 && value <= (1 << 24))
@@ -350,6 +352,7 @@ extern "C" int bcp_get_option(bcp_engine *eng, const char *key, int *value) {
   else if (!strcmp(key, "desc_pipe")) *value = t.desc_pipe;
   else if (!strcmp(key, "stream_grab")) *value = t.stream_grab;
   else if (!strcmp(key, "sync_mode")) *value = t.sync_mode;
+  else if (!strcmp(key, "host_registered")) *value = t.host_registered;
   else if (!strcmp(key, "desc_table_host_max")) *value = t.desc_table_host_max;
   else if (!strcmp(key, "last_stream_vecs")) *value = eng->last_stream_vecs.load(std::memory_order_relaxed);
   else rc = -EINVAL;
@@ -538,11 +541,16 @@ extern "C" int bcp_dev_free(bcp_engine *eng, void *dptr) {
   return 0;
 }
 
+namespace {
+int alloc_registered(size_t bytes, void **out);
+}
+
 extern "C" int bcp_host_alloc(bcp_engine *eng, size_t bytes, void **hptr) {
   if (!eng || !hptr) return -EINVAL;
   *hptr = nullptr;
   int rc = set_device(eng);
   if (rc) return rc;
+  if (eng->tuning.host_registered && alloc_registered(bytes ? bytes : 16, hptr) == 0) return 0;
   HIP_RC(hipHostMalloc(hptr, bytes ? bytes : 16, hipHostMallocDefault));
   return 0;
 }
@@ -605,24 +613,30 @@ int free_registered(void *p) {
 }
 }  // namespace
 
-// Mapped host memory for the P role's rows and output.  Experiment knob
-// BCP_MAPPED_FLAGS (tools/exp/host_kind_ab.py: which host memory kind the
-// protocol's CPU copies and the zero-copy kernel prefer): 0 hipHostMalloc
-// coherent (default), 1 non-coherent, 2 coherent + NUMA placement by the
-// calling thread's policy, 3 non-coherent + NUMA by policy, 4 ordinary
-// huge-page memory registered with hipHostRegister.
+// Mapped host memory for the P role's rows and output.  Default (option
+// host_registered = 1): ordinary huge-page memory registered with HIP -- the
+// chunk reads into the rows and the parity write out of the output are plain
+// CPU copies, and over hipHostMalloc'd memory they ran so much slower that
+// the per-task protocol lost ~40 % with the CPU fold itself unchanged
+// (config 5, same box, same run: 14.8-18.2 against 24.8-29.7 GiB/s over
+// ordinary memory; profiles/r02/protocol/host_kind_ab*.jsonl).  Falls back to
+// hipHostMalloc.  Experiment knob BCP_MAPPED_FLAGS: 0 hipHostMalloc coherent,
+// 1 non-coherent, 2 coherent + NUMA placement by the calling thread's
+// policy, 3 non-coherent + NUMA by policy, 4 registered.
 extern "C" int bcp_host_alloc_mapped(bcp_engine *eng, size_t bytes, void **hptr) {
   if (!eng || !hptr) return -EINVAL;
   *hptr = nullptr;
   int rc = set_device(eng);
   if (rc) return rc;
   unsigned flags = hipHostMallocMapped | hipHostMallocCoherent;
+  int registered = eng->tuning.host_registered;
   if (const char *v = getenv("BCP_MAPPED_FLAGS")) {
     const int k = atoi(v);
-    if (k == 4) return alloc_registered(bytes ? bytes : 16, hptr);
+    registered = k == 4;
     flags = hipHostMallocMapped | ((k & 1) ? hipHostMallocNonCoherent : hipHostMallocCoherent) |
             ((k & 2) ? hipHostMallocNumaUser : 0u);
   }
+  if (registered && alloc_registered(bytes ? bytes : 16, hptr) == 0) return 0;
   HIP_RC(hipHostMalloc(hptr, bytes ? bytes : 16, flags));
   return 0;
 }

@@ -51,6 +51,10 @@ struct Tuning {
     int stream_grab = 0;        // xor_stream, 1-4 sources: tiles per queue grab (0: auto)
     int sync_mode = 0;          // bcp_queue_sync: 0 hipStreamSynchronize, 1 blocking-sync event
     int desc_table_host_max = 128 * 1024;
+    // bcp_host_alloc / bcp_host_alloc_mapped: 1 = ordinary huge-page memory
+    // registered with HIP (CPU copies into and out of it run at malloc speed),
+    // 0 = hipHostMalloc.
+    int host_registered = 1;
 };
 
 // Arguments of the streaming kernel (xor_stream).

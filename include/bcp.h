@@ -111,7 +111,8 @@ int bcp_event_query(bcp_event *ev);
 /* ---- memory ----------------------------------------------------------- */
 int bcp_dev_alloc(bcp_engine *eng, size_t bytes, void **dptr);
 int bcp_dev_free(bcp_engine *eng, void *dptr);
-/* Pinned (page-locked) host memory for staging. */
+/* Pinned (page-locked) host memory for staging (registered huge-page memory
+ * by default, option host_registered). */
 int bcp_host_alloc(bcp_engine *eng, size_t bytes, void **hptr);
 /* Pinned host memory that kernels read and write in place over PCIe
  * (coherent, mapped at the same address on the device): zero-copy folds of
@@ -200,7 +201,10 @@ int bcp_set_tuning(bcp_engine *eng, int blocks_per_cu, int vecs_per_thread);
  * 4 and tiles wider than 8 sources windowed too), "stream_grab" (tiles per
  * work-queue grab of the streaming kernel for stripes of 1-4 sources, 1..64;
  * 0 = the default, 2), "sync_mode" (bcp_queue_sync: 0 = hipStreamSynchronize,
- * the default; 1 = wait on a blocking-sync event; env BCP_SYNC_MODE). */
+ * the default; 1 = wait on a blocking-sync event; env BCP_SYNC_MODE),
+ * "host_registered" (bcp_host_alloc / bcp_host_alloc_mapped: 1 = ordinary
+ * huge-page memory registered with HIP, the default -- CPU copies into and
+ * out of it run at malloc speed; 0 = hipHostMalloc; env BCP_HOST_REGISTERED). */
 int bcp_set_option(bcp_engine *eng, const char *key, int value);
 /* Current value of a named knob (same keys; "last_stream_vecs": the
  * vecs_per_thread of the engine's latest streaming-kernel launch). */

@@ -674,6 +674,7 @@ KNOBS = {
     "desc_pipe": (5, [0, 2, 4, 5], [1, 3, 6]),
     "stream_grab": (0, [0, 1, 64], [-1, 65]),
     "sync_mode": (0, [0, 1], [2]),
+    "host_registered": (1, [0, 1], [2]),
 }
 
 
