@@ -71,13 +71,15 @@ def fold_setup(fold, hooks):
     return lambda: bcp.set_xor_hook(None)
 
 
-def measure(name, folds, rounds, run_once, verify_fn, nbytes, hooks, extra=None):
+def measure(name, folds, rounds, run_once, verify_fn, nbytes, hooks, extra=None, prepare=None):
     times = {f: [] for f in folds}
     batching = {}
     phases = {}
     for r in range(rounds + 1):
         order = folds[r % len(folds):] + folds[:r % len(folds)]
         for f in order:
+            if prepare:
+                prepare()  # outside the timed region (removing old parity files)
             restore = fold_setup(f, hooks)
             try:
                 w0, l0 = bcp.fold_stats()
@@ -139,11 +141,11 @@ def reset_parity(root, ntargets):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--root", default="/dev/shm/bcp_proto")
-    ap.add_argument("--rounds", type=int, default=4)
+    ap.add_argument("--rounds", type=int, default=6)
     ap.add_argument("--folds", default="gpu_streamed,gpu_batched,gpu_zero_copy,cpu_reference,noop")
     ap.add_argument("--workloads", default="c1_gen,c1_rebuild,c5_gen")
     ap.add_argument("--c1-files", type=int, default=1333)
-    ap.add_argument("--c5-stripes", type=int, default=600)
+    ap.add_argument("--c5-stripes", type=int, default=1000)
     ap.add_argument("--lanes", type=int, default=12)
     a = ap.parse_args()
     folds = a.folds.split(",")
@@ -164,10 +166,9 @@ def main():
         rd, wr = total_bytes(root, files)
         if "c1_gen" in wl:
             def run_gen():
-                reset_parity(root, 4)
                 return bcp.gen_run(root, 4, items, nlanes=a.lanes)
             measure("config1_gen", folds, a.rounds, run_gen, lambda: verify(root, files, contents, 20, rng), rd + wr,
-                    hooks, {"lanes": a.lanes})
+                    hooks, {"lanes": a.lanes}, prepare=lambda: reset_parity(root, 4))
         if "c1_rebuild" in wl:
             # parity from a correct run, then rebuild target 2 again and again
             bcp.set_xor_hook(hooks["cpu_reference"])
@@ -179,10 +180,12 @@ def main():
             lost = {path: S.chunk_path(root, 2, path) for path, holders, _, _ in files if 2 in holders}
             rb_bytes = len(lost) * 4 * 512 * KiB
 
-            def run_rb():
+            def drop_lost():
                 for fn in lost.values():
                     if os.path.exists(fn):
                         os.remove(fn)
+
+            def run_rb():
                 return bcp.rebuild_run(root, 4, 2, items)
 
             def check_rb():
@@ -192,7 +195,8 @@ def main():
                         if S.read_file(fn) != contents[path][holders.index(2)].tobytes():
                             return False, path
                 return True, None
-            measure("config1_rebuild", folds, a.rounds, run_rb, check_rb, rb_bytes, hooks, {"lanes": 1})
+            measure("config1_rebuild", folds, a.rounds, run_rb, check_rb, rb_bytes, hooks, {"lanes": 1},
+                    prepare=drop_lost)
         shutil.rmtree(root, ignore_errors=True)
     if "c5_gen" in wl:
         root = os.path.join(a.root, "c5")
@@ -208,10 +212,9 @@ def main():
         rd, wr = total_bytes(root, files)
 
         def run5():
-            reset_parity(root, 9)
             return bcp.gen_run(root, 9, items, nlanes=a.lanes)
         measure("config5_gen", folds, a.rounds, run5, lambda: verify(root, files, contents, 20, rng), rd + wr, hooks,
-                {"lanes": a.lanes, "stripes": len(files)})
+                {"lanes": a.lanes, "stripes": len(files)}, prepare=lambda: reset_parity(root, 9))
         shutil.rmtree(root, ignore_errors=True)
     bcp.task_shutdown()
 
