@@ -116,6 +116,7 @@ _SIGS = {
     "bcp_task_shutdown": ([], ctypes.c_int),
     "bcp_task_set_xor_hook": ([_V, _V], None),
     "bcp_task_set_fold_mode": ([ctypes.c_int], ctypes.c_int),
+    "bcp_task_set_fold_inflight": ([ctypes.c_int], ctypes.c_int),
     "bcp_task_fold_stats": ([ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)], ctypes.c_int),
     "bcp_task_inject_failure": ([ctypes.c_int, ctypes.c_int, ctypes.c_int], ctypes.c_int),
     "bcp_task_phase_stats": ([ctypes.POINTER(ctypes.c_double), ctypes.c_int, ctypes.c_int], ctypes.c_int),
@@ -630,6 +631,14 @@ def set_fold_mode(mode: int) -> int:
 
 def task_shutdown():
     call("bcp_task_shutdown")
+
+
+def set_fold_inflight(k: int) -> int:
+    """Concurrent batches of the batched fold service; returns the previous value."""
+    rc = lib().bcp_task_set_fold_inflight(k)
+    if rc < 0:
+        raise BcpError("bcp_task_set_fold_inflight", rc)
+    return rc
 
 
 def fold_stats() -> tuple[int, int]:

@@ -196,14 +196,14 @@ static int engine_for_target(int st, bcp_engine **out, int *device)
 
 /* ---- fold service (BCP_FOLD_BATCHED) --------------------------------------
  * One per device, flat combining: a P role appends its window (rows +
- * output, mapped pinned memory; row j's data bytes) and, if no batch is on
- * the device, becomes the leader -- it takes EVERY pending window (its own
- * included), folds them with one descriptor batch on the service's queue,
- * syncs once and completes them all; otherwise it sleeps until a leader has
- * completed its window, or leads the next batch itself.  The batch size
- * follows the load with no thread of its own: a lone lane (the single rebuild
- * lane) folds its window directly, twelve lanes of every rank share one
- * launch.  Rows are read over PCIe for their data bytes only: a gen-mode
+ * output, mapped host memory; row j's data bytes) and, if fewer than
+ * max_inflight batches are on the device, becomes a leader -- it takes EVERY
+ * pending window (its own included), folds them with one descriptor batch on
+ * a free slot's queue, syncs once and completes them all; otherwise it
+ * sleeps until a leader has completed its window, or leads a later batch
+ * itself.  The batch size follows the load with no thread of its own: a lone
+ * lane (the single rebuild lane) folds its window directly, and when every
+ * slot is busy the windows that arrive meanwhile share the next launch.  Rows are read over PCIe for their data bytes only: a gen-mode
  * window is padded to the stripe's largest chunk, and the padding is zeros
  * the kernel supplies itself. */
 typedef struct fold_job {
@@ -216,76 +216,107 @@ typedef struct fold_job {
     int done, rc;
 } fold_job;
 
+#define MAX_INFLIGHT 16
+
 typedef struct {
-    bcp_engine *eng;
     bcp_queue *q;
-    int busy; /* a leader's batch is on the device */
-    pthread_mutex_t mu;
-    pthread_cond_t cv_done;
-    fold_job *head, *tail;
     bcp_stripe *st;
     bcp_source *so;
     size_t st_cap, so_cap;
+    int busy;
+} fold_slot;
+
+typedef struct {
+    bcp_engine *eng;
+    int inflight;     /* batches on the device (leaders folding) */
+    int max_inflight; /* concurrent batches, each on its own slot's queue */
+    fold_slot slot[MAX_INFLIGHT];
+    pthread_mutex_t mu;
+    pthread_cond_t cv_done;
+    fold_job *head, *tail;
     uint64_t windows, launches;
 } fold_svc;
 
 static fold_svc *g_svc[MAX_DEVICES];
 static uint64_t g_svc_windows, g_svc_launches; /* of services already shut down */
+static int g_fold_inflight = 4;
 
-static int svc_tables(fold_svc *S, size_t nst, size_t nso)
+int bcp_task_set_fold_inflight(int k)
 {
-    if (nst > S->st_cap) {
-        bcp_stripe *p = realloc(S->st, nst * 2 * sizeof(*p));
+    if (k < 1 || k > MAX_INFLIGHT)
+        return -EINVAL;
+    pthread_mutex_lock(&g_lock);
+    const int prev = g_fold_inflight;
+    g_fold_inflight = k;
+    for (int d = 0; d < MAX_DEVICES; d++)
+        if (g_svc[d]) {
+            pthread_mutex_lock(&g_svc[d]->mu);
+            g_svc[d]->max_inflight = k;
+            pthread_mutex_unlock(&g_svc[d]->mu);
+        }
+    pthread_mutex_unlock(&g_lock);
+    return prev;
+}
+
+static int slot_tables(fold_slot *F, size_t nst, size_t nso)
+{
+    if (nst > F->st_cap) {
+        bcp_stripe *p = realloc(F->st, nst * 2 * sizeof(*p));
         if (!p)
             return -ENOMEM;
-        S->st = p;
-        S->st_cap = nst * 2;
+        F->st = p;
+        F->st_cap = nst * 2;
     }
-    if (nso > S->so_cap) {
-        bcp_source *p = realloc(S->so, nso * 2 * sizeof(*p));
+    if (nso > F->so_cap) {
+        bcp_source *p = realloc(F->so, nso * 2 * sizeof(*p));
         if (!p)
             return -ENOMEM;
-        S->so = p;
-        S->so_cap = nso * 2;
+        F->so = p;
+        F->so_cap = nso * 2;
     }
     return 0;
 }
 
-/* The leader's batch (called without S->mu; S->busy keeps it exclusive). */
-static int svc_fold(fold_svc *S, fold_job *batch)
+/* A leader's batch on its slot (called without S->mu; the slot is its own). */
+static int slot_fold(fold_svc *S, fold_slot *F, fold_job *batch)
 {
+    int rc = F->q ? 0 : bcp_queue_create(S->eng, &F->q);
+    if (rc)
+        return rc;
     size_t nst = 0, nso = 0;
     for (fold_job *j = batch; j; j = j->next) {
         nst++;
         nso += (size_t)j->n;
     }
-    int rc = nst > 0xFFFFFFFFu || nso > 0xFFFFFFFFu ? -EINVAL : svc_tables(S, nst, nso);
+    rc = nst > 0xFFFFFFFFu || nso > 0xFFFFFFFFu ? -EINVAL : slot_tables(F, nst, nso);
     if (rc)
         return rc;
     size_t i = 0, k = 0;
     for (fold_job *j = batch; j; j = j->next, i++) {
-        S->st[i] = (bcp_stripe){(uint64_t)(uintptr_t)j->out, j->nbytes, (uint32_t)k, (uint32_t)j->n, 0};
+        F->st[i] = (bcp_stripe){(uint64_t)(uintptr_t)j->out, j->nbytes, (uint32_t)k, (uint32_t)j->n, 0};
         for (int r = 0; r < j->n; r++, k++)
-            S->so[k] = (bcp_source){(uint64_t)(uintptr_t)(j->rows + (size_t)r * j->pitch), j->valid[r]};
+            F->so[k] = (bcp_source){(uint64_t)(uintptr_t)(j->rows + (size_t)r * j->pitch), j->valid[r]};
     }
-    rc = bcp_xor_stripes_async(S->q, S->st, (uint32_t)nst, S->so, (uint32_t)nso);
-    return rc ? rc : bcp_queue_sync(S->q);
+    rc = bcp_xor_stripes_async(F->q, F->st, (uint32_t)nst, F->so, (uint32_t)nso);
+    return rc ? rc : bcp_queue_sync(F->q);
 }
 
 static void svc_destroy(fold_svc *S)
 {
     if (!S)
         return;
-    if (S->q)
-        bcp_queue_destroy(S->q);
+    for (int i = 0; i < MAX_INFLIGHT; i++) {
+        if (S->slot[i].q)
+            bcp_queue_destroy(S->slot[i].q);
+        free(S->slot[i].st);
+        free(S->slot[i].so);
+    }
     pthread_cond_destroy(&S->cv_done);
     pthread_mutex_destroy(&S->mu);
-    free(S->st);
-    free(S->so);
     free(S);
 }
 
-/* The service of device dev (made on first use). */
+/* The service of device dev (made on first use; slot queues on first use). */
 static int svc_get(int dev, bcp_engine *e, fold_svc **out)
 {
     pthread_mutex_lock(&g_lock);
@@ -297,14 +328,10 @@ static int svc_get(int dev, bcp_engine *e, fold_svc **out)
             rc = -ENOMEM;
         else {
             S->eng = e;
+            S->max_inflight = g_fold_inflight;
             pthread_mutex_init(&S->mu, NULL);
             pthread_cond_init(&S->cv_done, NULL);
-            if ((rc = bcp_queue_create(e, &S->q))) {
-                svc_destroy(S);
-                S = NULL;
-            } else {
-                g_svc[dev] = S;
-            }
+            g_svc[dev] = S;
         }
     }
     pthread_mutex_unlock(&g_lock);
@@ -323,16 +350,22 @@ static int fold_batched(fold_svc *S, const uint8_t *rows, size_t pitch, const si
         S->head = &j;
     S->tail = &j;
     while (!j.done) {
-        if (S->busy) {
+        if (S->inflight >= S->max_inflight || !S->head) {
             pthread_cond_wait(&S->cv_done, &S->mu);
             continue;
         }
-        /* lead: everything pending, this window included */
-        S->busy = 1;
+        /* lead a batch: everything pending (this window, if no other leader
+         * took it yet) on a free slot */
+        fold_slot *F = NULL;
+        for (int i = 0; i < MAX_INFLIGHT && !F; i++)
+            if (!S->slot[i].busy)
+                F = &S->slot[i];
+        F->busy = 1;
+        S->inflight++;
         fold_job *batch = S->head;
         S->head = S->tail = NULL;
         pthread_mutex_unlock(&S->mu);
-        const int rc = svc_fold(S, batch);
+        const int rc = slot_fold(S, F, batch);
         pthread_mutex_lock(&S->mu);
         size_t nb = 0;
         for (fold_job *x = batch, *nx; x; x = nx, nb++) {
@@ -342,7 +375,8 @@ static int fold_batched(fold_svc *S, const uint8_t *rows, size_t pitch, const si
         }
         S->windows += nb;
         S->launches += 1;
-        S->busy = 0;
+        S->inflight--;
+        F->busy = 0;
         pthread_cond_broadcast(&S->cv_done);
     }
     pthread_mutex_unlock(&S->mu);

@@ -119,6 +119,10 @@ int bcp_task_set_device_map(const int *devices, int ntargets);
  * block, then one sync.  PCIe carries the chunk bytes once, not the padding. */
 #define BCP_FOLD_STREAMED 3
 int bcp_task_set_fold_mode(int mode);
+/* BATCHED mode: how many batches may be on a device at once (1..16, each
+ * led by one waiting lane on its own queue; default 4).  Returns the
+ * previous value or -EINVAL. */
+int bcp_task_set_fold_inflight(int k);
 /* Fold-service counters since the last shutdown (BATCHED mode): windows
  * folded and launches issued (windows / launches = the batching achieved). */
 int bcp_task_fold_stats(uint64_t *windows, uint64_t *launches);

@@ -62,6 +62,16 @@ def noop_hook():
 
 def fold_setup(fold, hooks):
     """Returns a context restore callable."""
+    if fold.startswith("gpu_batched"):
+        # gpu_batched[K]: K concurrent batches (bcp_task_set_fold_inflight)
+        k = int(fold[len("gpu_batched"):] or 4)
+        prev_k = bcp.set_fold_inflight(k)
+        prev = bcp.set_fold_mode(bcp.FOLD_BATCHED)
+
+        def restore():
+            bcp.set_fold_mode(prev)
+            bcp.set_fold_inflight(prev_k)
+        return restore
     if fold.startswith("gpu_"):
         mode = {"gpu_batched": bcp.FOLD_BATCHED, "gpu_zero_copy": bcp.FOLD_ZERO_COPY,
                 "gpu_staged": bcp.FOLD_STAGED, "gpu_streamed": bcp.FOLD_STREAMED}[fold]
@@ -98,10 +108,10 @@ def measure(name, folds, rounds, run_once, verify_fn, nbytes, hooks, extra=None,
             if st.errors:
                 raise RuntimeError(f"{name}/{f}: {st.errors} rank errors")
             times[f].append(dt)
-            if f == "gpu_batched" and r > 0:
-                batching.setdefault("windows", 0)
-                batching["windows"] = batching["windows"] + (w1 - w0)
-                batching["launches"] = batching.get("launches", 0) + (l1 - l0)
+            if f.startswith("gpu_batched") and r > 0:
+                b = batching.setdefault(f, {"windows": 0, "launches": 0})
+                b["windows"] += w1 - w0
+                b["launches"] += l1 - l0
             if r == rounds and f != "noop":
                 ok, bad = verify_fn()
                 if not ok:
@@ -112,8 +122,8 @@ def measure(name, folds, rounds, run_once, verify_fn, nbytes, hooks, extra=None,
         res[f] = nbytes / warm / GiB
         line = dict(workload=name, fold=f, GiBps=round(res[f], 3), warm_median_s=round(warm, 4),
                     runs_s=[round(x, 4) for x in times[f]], cold_s=round(times[f][0], 4))
-        if f == "gpu_batched" and batching.get("launches"):
-            line["windows_per_launch"] = round(batching["windows"] / batching["launches"], 2)
+        if batching.get(f, {}).get("launches"):
+            line["windows_per_launch"] = round(batching[f]["windows"] / batching[f]["launches"], 2)
         acc = phases.get(f)
         if acc and acc.get("p_tasks"):
             # mean wall microseconds per P task / per source task in each phase
