@@ -239,7 +239,7 @@ typedef struct {
 
 static fold_svc *g_svc[MAX_DEVICES];
 static uint64_t g_svc_windows, g_svc_launches; /* of services already shut down */
-static int g_fold_inflight = 4;
+static int g_fold_inflight = 1;
 
 int bcp_task_set_fold_inflight(int k)
 {

@@ -120,7 +120,8 @@ int bcp_task_set_device_map(const int *devices, int ntargets);
 #define BCP_FOLD_STREAMED 3
 int bcp_task_set_fold_mode(int mode);
 /* BATCHED mode: how many batches may be on a device at once (1..16, each
- * led by one waiting lane on its own queue; default 4).  Returns the
+ * led by one waiting lane on its own queue; default 1: pure flat
+ * combining).  Returns the
  * previous value or -EINVAL. */
 int bcp_task_set_fold_inflight(int k);
 /* Fold-service counters since the last shutdown (BATCHED mode): windows
