@@ -34,6 +34,8 @@ struct bcp_engine {
   Tuning tuning;
   pthread_mutex_t lock = PTHREAD_MUTEX_INITIALIZER;
   std::atomic<int> last_stream_vecs{0};  // U of the latest xor_stream launch (tools)
+  std::atomic<int> last_desc_vecs{0};    // U of the latest descriptor-kernel launch (tools)
+  std::atomic<int> last_desc_form{0};    // 1 xor_desc (desc_tiles), 2 xor_desc_args
 };
 
 namespace {
@@ -46,8 +48,10 @@ struct DescSlot {
   void *dev = nullptr;    // device copy
   size_t cap = 0;
   hipEvent_t done = nullptr;    // recorded after the kernel that read `dev`
-  hipEvent_t copied = nullptr;  // recorded on the copy stream after host -> dev
+  hipEvent_t copied = nullptr;  // recorded on the copy stream after host -> dev (or after desc_tiles there)
   bool used = false;
+  DescTile *tiles = nullptr;    // this slot's tile records (desc_tiles -> xor_desc)
+  size_t tiles_cap = 0;         // in records
 };
 
 }  // namespace
@@ -60,8 +64,6 @@ struct bcp_queue {
   unsigned long long *qctr = nullptr;  // work-queue counter of xor_stream (device)
   unsigned long long qbase = 0;        // its value when the next launch starts
   hipEvent_t timer[kTimerSlots] = {};
-  DescTile *tiles = nullptr;           // tile records of the descriptor kernel (device)
-  size_t tiles_cap = 0;                // in records
   hipStream_t copy_stream = nullptr;   // descriptor-table uploads (created on first use)
   hipEvent_t sync_ev = nullptr;        // blocking-sync event (sync_mode 1; created on first use)
   bool broken = false;                 // work-queue counter could not be restarted after a failed launch
@@ -175,6 +177,13 @@ static int stream_vecs(const bcp_engine *e, uint64_t chunk_bytes, uint64_t nstri
 }
 static bool desc_vecs_ok(int v) { return v == 1 || v == 2 || v == 4 || v == 8; }
 
+// Vectors per lane of the descriptor kernel.  Explicit tuning wins; auto (0,
+// the default): 32 KiB tiles (U = 8) once the batch has twice as many of them
+// as the grid has workgroups, 16 KiB from half the grid, 8 KiB below -- a
+// one-stripe batch of 512 KiB is 16 tiles at U = 8, i.e. 16 CUs busy; 64 at
+// U = 2 (the streaming kernel's small-batch rule, stream_vecs).
+static int desc_vecs_for(const bcp_engine *e, uint64_t tiles8);
+
 static bool aligned16(uint64_t x) { return (x & 15u) == 0; }
 
 // Reserve a ring slot of at least `bytes`; waits only if that slot's
@@ -207,15 +216,20 @@ static int ring_acquire(bcp_queue *q, size_t bytes, DescSlot **out) {
 // which for small batches costs less than the copy and the cross-stream wait
 // (tools/batch_curve.py, profiles/r01/batch/).  Returns the tables' address
 // as the kernels see it.
-static int stage_tables(bcp_queue *q, DescSlot *slot, size_t bytes, size_t host_max, char **tables) {
+// compute_waits = false: the caller enqueues more on the copy stream (the
+// descriptor batch's desc_tiles) and makes the compute stream wait after it.
+static int stage_tables(bcp_queue *q, DescSlot *slot, size_t bytes, size_t host_max, char **tables,
+                        bool compute_waits = true) {
   if (bytes <= host_max) {
     *tables = (char *)slot->host;
     return 0;
   }
   if (!q->copy_stream) HIP_RC(hipStreamCreateWithFlags(&q->copy_stream, hipStreamNonBlocking));
   HIP_RC(hipMemcpyAsync(slot->dev, slot->host, bytes, hipMemcpyHostToDevice, q->copy_stream));
-  HIP_RC(hipEventRecord(slot->copied, q->copy_stream));
-  HIP_RC(hipStreamWaitEvent(q->stream, slot->copied, 0));
+  if (compute_waits) {
+    HIP_RC(hipEventRecord(slot->copied, q->copy_stream));
+    HIP_RC(hipStreamWaitEvent(q->stream, slot->copied, 0));
+  }
   *tables = (char *)slot->dev;
   return 0;
 }
@@ -307,7 +321,9 @@ extern "C" int bcp_set_option(bcp_engine *eng, const char *key, int value) {
   if (!strcmp(key, "blocks_per_cu") && value >= 1 && value <= 32) eng->tuning.blocks_per_cu = value;
   else if (!strcmp(key, "vecs_per_thread") && (value == 0 || stream_vecs_ok(value))) eng->tuning.vecs_per_thread = value;
   else if (!strcmp(key, "desc_blocks_per_cu") && value >= 0 && value <= 32) eng->tuning.desc_blocks_per_cu = value;
-  else if (!strcmp(key, "desc_vecs_per_thread") && desc_vecs_ok(value)) eng->tuning.desc_vecs = value;
+  else if (!strcmp(key, "desc_vecs_per_thread") && (value == 0 || desc_vecs_ok(value))) eng->tuning.desc_vecs = value;
+  else if (!strcmp(key, "desc_args_max") && value >= 0 && value <= kArgStripes) eng->tuning.desc_args_max = value;
+  else if (!strcmp(key, "desc_side_tiles") && (value == 0 || value == 1)) eng->tuning.desc_side_tiles = value;
   else if (!strcmp(key, "schedule") && (value == kSchedQueue || value == kSchedStatic)) eng->tuning.schedule = value;
   else if (!strcmp(key, "desc_schedule") && (value == kSchedQueue || value == kSchedStatic)) eng->tuning.desc_schedule = value;
   else if (!strcmp(key, "desc_grab") && value >= 1 && value <= 64) eng->tuning.desc_grab = value;
@@ -340,6 +356,8 @@ extern "C" int bcp_get_option(bcp_engine *eng, const char *key, int *value) {
   else if (!strcmp(key, "schedule")) *value = t.schedule;
   else if (!strcmp(key, "desc_blocks_per_cu")) *value = t.desc_blocks_per_cu;
   else if (!strcmp(key, "desc_vecs_per_thread")) *value = t.desc_vecs;
+  else if (!strcmp(key, "desc_args_max")) *value = t.desc_args_max;
+  else if (!strcmp(key, "desc_side_tiles")) *value = t.desc_side_tiles;
   else if (!strcmp(key, "desc_schedule")) *value = t.desc_schedule;
   else if (!strcmp(key, "desc_grab")) *value = t.desc_grab;
   else if (!strcmp(key, "desc_force")) *value = t.desc_force;
@@ -355,6 +373,8 @@ extern "C" int bcp_get_option(bcp_engine *eng, const char *key, int *value) {
   else if (!strcmp(key, "host_registered")) *value = t.host_registered;
   else if (!strcmp(key, "desc_table_host_max")) *value = t.desc_table_host_max;
   else if (!strcmp(key, "last_stream_vecs")) *value = eng->last_stream_vecs.load(std::memory_order_relaxed);
+  else if (!strcmp(key, "last_desc_vecs")) *value = eng->last_desc_vecs.load(std::memory_order_relaxed);
+  else if (!strcmp(key, "last_desc_form")) *value = eng->last_desc_form.load(std::memory_order_relaxed);
   else rc = -EINVAL;
   pthread_mutex_unlock(&eng->lock);
   return rc;
@@ -407,12 +427,12 @@ extern "C" int bcp_queue_destroy(bcp_queue *q) {
     if (s.dev) (void)hipFree(s.dev);
     if (s.done) (void)hipEventDestroy(s.done);
     if (s.copied) (void)hipEventDestroy(s.copied);
+    if (s.tiles) (void)hipFree(s.tiles);
   }
   if (q->copy_stream) (void)hipStreamDestroy(q->copy_stream);
   for (auto &t : q->timer)
     if (t) (void)hipEventDestroy(t);
   if (q->qctr) (void)hipFree(q->qctr);
-  if (q->tiles) (void)hipFree(q->tiles);
   if (q->sync_ev) (void)hipEventDestroy(q->sync_ev);
   (void)hipStreamDestroy(q->stream);
   delete q;
@@ -736,13 +756,78 @@ static bool uniform_batch(const bcp_stripe *st, uint32_t nstripes, const bcp_sou
 }
 
 // Submit a descriptor batch (host arrays) on q.
+static int desc_vecs_for(const bcp_engine *e, uint64_t tiles8) {
+  if (e->tuning.desc_vecs) return e->tuning.desc_vecs;
+  const uint64_t g = (uint64_t)desc_grid_for(e);
+  if (tiles8 * 2 < g) return 2;
+  if (tiles8 < 2 * g) return 4;
+  return 8;
+}
+
+// Small batches (engine option desc_args_max, default kArgStripes stripes):
+// the whole descriptor in the kernel arguments, one launch (xor_desc_args).
+// Returns 1 if the batch does not qualify (caller takes the general path).
+static int submit_desc_args(bcp_queue *q, const bcp_stripe *stripes, uint32_t nstripes, const bcp_source *sources,
+                            int vecs) {
+  bcp_engine *e = q->eng;
+  if (nstripes > (uint32_t)e->tuning.desc_args_max || nstripes > (uint32_t)kArgStripes) return 1;
+  uint32_t nsrc_all = 0;
+  for (uint32_t i = 0; i < nstripes; i++) {
+    if (stripes[i].window || stripes[i].nsrc > (uint32_t)kTileSrcs) return 1;
+    nsrc_all += stripes[i].nsrc;
+  }
+  if (nsrc_all > (uint32_t)kArgSources) return 1;
+  const uint64_t T = desc_tile_bytes(vecs);
+  DescArgs a;
+  memset(&a, 0, sizeof(a));
+  uint64_t acc = 0;
+  uint32_t k = 0;
+  for (uint32_t i = 0; i < nstripes; i++) {
+    const bcp_stripe &st = stripes[i];
+    a.dst[i] = st.dst;
+    a.out_len[i] = st.out_len;
+    a.first[i] = k;
+    a.nsrc[i] = st.nsrc;
+    a.tile_start[i] = (uint32_t)acc;
+    acc += (st.out_len + T - 1) / T;
+    if (acc > 0xFFFFFFF0ull) return 1;
+    for (uint32_t j = 0; j < st.nsrc; j++) {  // insertion sort, longest first (submit_desc)
+      const bcp_source x = sources[st.first_src + j];
+      uint32_t m = k + j;
+      while (m > k && a.src_len[m - 1] < x.len) {
+        a.src_ptr[m] = a.src_ptr[m - 1];
+        a.src_len[m] = a.src_len[m - 1];
+        m--;
+      }
+      a.src_ptr[m] = x.ptr;
+      a.src_len[m] = x.len;
+    }
+    k += st.nsrc;
+  }
+  a.tile_start[nstripes] = (uint32_t)acc;
+  a.nstripes = nstripes;
+  a.ntiles = (uint32_t)acc;
+  if (!acc) return 0;
+  if (q->broken) return -EIO;
+  a.ctr = q->qctr;
+  a.base = q->qbase;
+  int grid = desc_grid_for(e);
+  if ((uint64_t)grid > acc) grid = (int)acc;
+  (void)hipGetLastError();  // see launch_stream
+  const hipError_t le = launch_xor_desc_args(q->stream, grid, vecs, a);
+  if (le == hipSuccess) {
+    e->last_desc_vecs.store(vecs, std::memory_order_relaxed);
+    e->last_desc_form.store(2, std::memory_order_relaxed);
+  }
+  return queue_launched(q, le, acc + (uint64_t)grid);
+}
+
+// Submit a descriptor batch (host arrays) on q.
 static int submit_desc(bcp_queue *q, const bcp_stripe *stripes, uint32_t nstripes, const bcp_source *sources,
                        uint32_t nsources) {
   bcp_engine *e = q->eng;
-  const int vecs = e->tuning.desc_vecs;
-  const uint32_t tile_bytes = desc_tile_bytes(vecs);
-  // Validate, count tiles and the bytes they move (padding is not read).
-  uint64_t ntiles = 0;
+  // Validate, count 32 KiB tiles (the tile size is chosen from them).
+  uint64_t tiles8 = 0;
   bool plain = true;  // no tile takes the general / wide path (those read the tables per tile)
   for (uint32_t i = 0; i < nstripes; i++) {
     const bcp_stripe &s = stripes[i];
@@ -755,10 +840,12 @@ static int submit_desc(bcp_queue *q, const bcp_stripe *stripes, uint32_t nstripe
       const bcp_source &x = sources[s.first_src + k];
       if (x.len && !x.ptr) return -EINVAL;
     }
-    ntiles += (s.out_len + tile_bytes - 1) / tile_bytes;
+    tiles8 += (s.out_len + desc_tile_bytes(8) - 1) / desc_tile_bytes(8);
   }
-  if (ntiles == 0) return 0;
-  if (ntiles > 0xFFFFFFF0ull) return -EINVAL;
+  if (tiles8 == 0) return 0;
+  if (tiles8 > 0xFFFFFFF0ull / 4) return -EINVAL;
+  const int vecs = desc_vecs_for(e, tiles8);
+  const uint32_t tile_bytes = desc_tile_bytes(vecs);
   if (!e->tuning.desc_force && uniform_batch(stripes, nstripes, sources)) {
     const uint64_t len = stripes[0].out_len;
     const int sv = stream_vecs(e, len, nstripes, stripes[0].nsrc);
@@ -786,6 +873,10 @@ static int submit_desc(bcp_queue *q, const bcp_stripe *stripes, uint32_t nstripe
     HIP_RC(hipEventRecord(slot->done, q->stream));
     slot->used = true;
     return 0;
+  }
+  {
+    const int rc = submit_desc_args(q, stripes, nstripes, sources, vecs);
+    if (rc <= 0) return rc;
   }
   // Staged copy: every stripe gets its own run of sources sorted by length,
   // longest first (XOR is commutative), so the sources that cover a tile are
@@ -832,25 +923,32 @@ static int submit_desc(bcp_queue *q, const bcp_stripe *stripes, uint32_t nstripe
   }
   const uint32_t acc = (uint32_t)acc64;
   ts[nstripes] = acc;
-  if (q->tiles_cap < acc) {
-    // launches on q are in order; the old records may still be in use
-    HIP_RC(hipStreamSynchronize(q->stream));
-    if (q->tiles) HIP_RC(hipFree(q->tiles));
-    q->tiles = nullptr;
-    q->tiles_cap = 0;
-    const size_t cap = std::max<size_t>(acc + acc / 4, 1u << 16);
-    HIP_RC(hipMalloc((void **)&q->tiles, cap * sizeof(DescTile)));
-    q->tiles_cap = cap;
+  if (slot->tiles_cap < acc) {
+    // the slot's previous kernels have finished (ring_acquire waited)
+    if (slot->tiles) HIP_RC(hipFree(slot->tiles));
+    slot->tiles = nullptr;
+    slot->tiles_cap = 0;
+    const size_t cap = std::max<size_t>(acc + acc / 4, 1u << 12);
+    HIP_RC(hipMalloc((void **)&slot->tiles, cap * sizeof(DescTile)));
+    slot->tiles_cap = cap;
   }
+  const uint32_t nunits = e->tuning.desc_schedule == kSchedQueue ? (acc + e->tuning.desc_grab - 1) / e->tuning.desc_grab : acc;
+  int grid = desc_grid_for(e);
+  if ((uint32_t)grid > nunits) grid = (int)nunits;
+  // Large batches: desc_tiles on the copy stream (after the table upload),
+  // so it overlaps the previous batch's fold on the compute stream instead of
+  // sitting between two folds; the fold waits for it by event.  Small batches
+  // keep it in line (a cross-stream wait costs more than it hides).
+  const bool side = e->tuning.desc_side_tiles && acc >= 2u * (uint32_t)grid;
   char *d = nullptr;
   // Host-resident tables only when desc_tiles alone reads them: the general
   // and wide tile paths read them again per tile.
-  if ((rc = stage_tables(q, slot, bytes, plain ? (size_t)e->tuning.desc_table_host_max : 0, &d))) return rc;
+  if ((rc = stage_tables(q, slot, bytes, plain ? (size_t)e->tuning.desc_table_host_max : 0, &d, !side))) return rc;
   DescBatch b;
   b.stripes = (const bcp_stripe *)d;
   b.sources = (const bcp_source *)(d + off_src);
   b.tile_start = (const uint32_t *)(d + off_tiles);
-  b.tiles = q->tiles;
+  b.tiles = slot->tiles;
   b.nstripes = nstripes;
   b.ntiles = acc;
   b.tile_bytes = tile_bytes;
@@ -858,13 +956,21 @@ static int submit_desc(bcp_queue *q, const bcp_stripe *stripes, uint32_t nstripe
   b.grab = (uint32_t)e->tuning.desc_grab;
   b.ctr = q->qctr;
   b.base = q->qbase;
-  const uint32_t nunits = b.sched == kSchedQueue ? (acc + b.grab - 1) / b.grab : acc;
-  int grid = desc_grid_for(e);
-  if ((uint32_t)grid > nunits) grid = (int)nunits;
   if (q->broken) return -EIO;
   (void)hipGetLastError();  // see launch_stream
-  HIP_RC(launch_desc_tiles(q->stream, b));
+  if (side) {
+    if (!q->copy_stream) HIP_RC(hipStreamCreateWithFlags(&q->copy_stream, hipStreamNonBlocking));
+    HIP_RC(launch_desc_tiles(q->copy_stream, b));
+    HIP_RC(hipEventRecord(slot->copied, q->copy_stream));
+    HIP_RC(hipStreamWaitEvent(q->stream, slot->copied, 0));
+  } else {
+    HIP_RC(launch_desc_tiles(q->stream, b));
+  }
   const hipError_t le = launch_xor_desc(q->stream, grid, vecs, b, e->tuning.desc_pipe);
+  if (le == hipSuccess) {
+    e->last_desc_vecs.store(vecs, std::memory_order_relaxed);
+    e->last_desc_form.store(1, std::memory_order_relaxed);
+  }
   if (b.sched == kSchedQueue) rc = queue_launched(q, le, (uint64_t)nunits + (uint64_t)grid);
   else rc = hip_to_errno(le);
   if (rc) return rc;

@@ -29,7 +29,9 @@ struct Tuning {
     // vectors per lane, one 32 KiB tile per queue grab; workgroups per CU
     // 0 = auto (desc_grid_for: one per CU).
     int desc_blocks_per_cu = 0;
-    int desc_vecs = 8;          // 1, 2, 4, 8
+    int desc_vecs = 0;          // 1, 2, 4, 8; 0 = by batch size (desc_vecs_for)
+    int desc_args_max = 4;      // batches of at most this many stripes go in the kernel arguments (0 = never)
+    int desc_side_tiles = 1;    // large batches: desc_tiles on the copy stream, overlapping the previous fold
     int desc_grab = 1;          // tiles per work-queue grab
     int desc_schedule = kSchedQueue;
     int desc_force = 0;         // 1: uniform batches take xor_desc too (A/B only)
@@ -194,6 +196,24 @@ struct DescBatch {
     uint32_t grab;              // kSchedQueue: tiles per grab
 };
 
+// A small descriptor batch passed whole in the kernel arguments
+// (xor_desc_args): <= kArgStripes stripes, <= kArgSources sources in all, each
+// stripe's run sorted longest first, <= kTileSrcs per stripe, no window.
+constexpr int kArgStripes = 4;
+constexpr int kArgSources = 32;
+struct DescArgs {
+    uint64_t dst[kArgStripes];
+    uint64_t out_len[kArgStripes];
+    uint32_t first[kArgStripes];
+    uint32_t nsrc[kArgStripes];
+    uint32_t tile_start[kArgStripes + 1];  // prefix of tiles (one per subtile)
+    uint32_t nstripes, ntiles;
+    uint64_t src_ptr[kArgSources];
+    uint64_t src_len[kArgSources];
+    unsigned long long *ctr;  // work-queue counter (per queue), as StreamArgs
+    unsigned long long base;
+};
+
 // Kernel launchers (bcp_kernels.hip).  All return hipError_t.
 // Streaming fold.  Consumes ntiles + grid counts of a.ctr when a.sched is
 // kSchedQueue; the caller clamps grid to [1, ntiles].
@@ -206,6 +226,8 @@ uint32_t stream_tiles_per_stripe(uint64_t chunk_bytes, int vecs);
 hipError_t launch_desc_tiles(hipStream_t st, const DescBatch &b);
 hipError_t launch_xor_desc(hipStream_t st, int grid, int vecs,
                            const DescBatch &b, int pipe = 0);
+// Small batch in the arguments; same work-queue accounting (ntiles + grid).
+hipError_t launch_xor_desc_args(hipStream_t st, int grid, int vecs, const DescArgs &a);
 hipError_t launch_fill_synthetic(hipStream_t st, int grid, char *dst,
                                  uint64_t bytes, uint64_t seed,
                                  uint64_t byte_offset);

@@ -390,19 +390,19 @@ __device__ __forceinline__ void fold_cover(v4u (&acc)[U], P src, uint32_t lane_o
 // subtile instead, the loads of subtile j+1 cannot move above the stores of
 // subtile j -- the compiler cannot rule out aliasing -- and each subtile
 // drains the pipe: config-5 shapes 78 -> 70 %.)
-template <int C, int M, int U>
-__device__ __forceinline__ void fold_group(const_as<DescTile> *r, uint32_t lane_off) {
+template <int C, int M, int U, typename RT>
+__device__ __forceinline__ void fold_group(const RT &r, uint32_t lane_off) {
   constexpr uint32_t T = (uint32_t)kBlock * U * 16u;  // == b.tile_bytes
   v4u x[C][M][U];
 #pragma unroll
   for (int i = 0; i < C; i++) {
-    const glob<v4u_u> *p = gp<const v4u_u>(r->src[i] + lane_off);
+    const glob<v4u_u> *p = gp<const v4u_u>(r.src[i] + lane_off);
 #pragma unroll
     for (int j = 0; j < M; j++)
 #pragma unroll
       for (int u = 0; u < U; u++) x[i][j][u] = __builtin_nontemporal_load(p + j * (T / 16) + u * 64);
   }
-  glob<v4u_u> *q = gp<v4u_u>(r->dst + lane_off);
+  glob<v4u_u> *q = gp<v4u_u>(r.dst + lane_off);
 #pragma unroll
   for (int j = 0; j < M; j++)
 #pragma unroll
@@ -495,17 +495,12 @@ __device__ __noinline__ void desc_tile_wide(const DescBatch &b, uint32_t stripe,
   }
 }
 
-template <int U, int PIPE>
-__device__ __forceinline__ void desc_tile(const DescBatch &b, uint32_t t) {
-  const_as<DescTile> *r = cst(b.tiles) + t;
-  const uint32_t meta = r->meta;
-  if (meta & kTileGeneral) {
-    if (meta & kTileWide)
-      desc_tile_wide<U, PIPE>(b, r->src_bytes[0], r->src_bytes[1], r->src_bytes[2], meta & 0xFFu, (meta >> 8) & 0xFFu);
-    else
-      desc_tile_general<U>(b, r->src_bytes[0], r->src_bytes[1], r->src_bytes[2]);
-    return;
-  }
+// One plain or grouped tile from its record r: any type with the DescTile
+// members (the device-written record read through the constant address
+// space, or the register view of xor_desc_args).  tile_bytes = kBlock*U*16.
+template <int U, int PIPE, typename RT>
+__device__ __forceinline__ void desc_plain(const RT &r, uint32_t tile_bytes) {
+  const uint32_t meta = r.meta;
   // this lane's vector u = 0 inside the tile; vector u is at + u * 1024
   const uint32_t lane_off = ((threadIdx.x >> 6) * (64u * U) + (threadIdx.x & 63u)) * 16u;
   const uint32_t nfull = meta & 0xFFu, nany = (meta >> 8) & 0xFFu;
@@ -530,14 +525,14 @@ __device__ __forceinline__ void desc_tile(const DescBatch &b, uint32_t t) {
       v4u acc[U];
 #pragma unroll
       for (int u = 0; u < U; u++) acc[u] = zero4();
-      const uint32_t off = lane_off + j * b.tile_bytes;
+      const uint32_t off = lane_off + j * tile_bytes;
       switch (nfull) {
-        case 4: fold_cover<4, U>(acc, r->src, off); break;
-        case 3: fold_cover<3, U>(acc, r->src, off); break;
-        case 2: fold_cover<2, U>(acc, r->src, off); break;
-        default: fold_cover<1, U>(acc, r->src, off); break;
+        case 4: fold_cover<4, U>(acc, r.src, off); break;
+        case 3: fold_cover<3, U>(acc, r.src, off); break;
+        case 2: fold_cover<2, U>(acc, r.src, off); break;
+        default: fold_cover<1, U>(acc, r.src, off); break;
       }
-      glob<v4u_u> *q = gp<v4u_u>(r->dst + off);
+      glob<v4u_u> *q = gp<v4u_u>(r.dst + off);
 #pragma unroll
       for (int u = 0; u < U; u++) __builtin_nontemporal_store(acc[u], q + u * 64);
     }
@@ -547,38 +542,38 @@ __device__ __forceinline__ void desc_tile(const DescBatch &b, uint32_t t) {
 #pragma unroll
   for (int u = 0; u < U; u++) acc[u] = zero4();
   switch (nfull) {
-    case 8: fold_cover<8, U, PIPE>(acc, r->src, lane_off); break;
-    case 7: fold_cover<7, U, PIPE>(acc, r->src, lane_off); break;
-    case 6: fold_cover<6, U, PIPE>(acc, r->src, lane_off); break;
-    case 5: fold_cover<5, U, PIPE>(acc, r->src, lane_off); break;
-    case 4: fold_cover<4, U, PIPE>(acc, r->src, lane_off); break;
-    case 3: fold_cover<3, U, PIPE>(acc, r->src, lane_off); break;
-    case 2: fold_cover<2, U, PIPE>(acc, r->src, lane_off); break;
-    case 1: fold_cover<1, U, PIPE>(acc, r->src, lane_off); break;
+    case 8: fold_cover<8, U, PIPE>(acc, r.src, lane_off); break;
+    case 7: fold_cover<7, U, PIPE>(acc, r.src, lane_off); break;
+    case 6: fold_cover<6, U, PIPE>(acc, r.src, lane_off); break;
+    case 5: fold_cover<5, U, PIPE>(acc, r.src, lane_off); break;
+    case 4: fold_cover<4, U, PIPE>(acc, r.src, lane_off); break;
+    case 3: fold_cover<3, U, PIPE>(acc, r.src, lane_off); break;
+    case 2: fold_cover<2, U, PIPE>(acc, r.src, lane_off); break;
+    case 1: fold_cover<1, U, PIPE>(acc, r.src, lane_off); break;
     default: break;
   }
   // Sources ending inside the tile: whole vectors below the end as masked
   // loads (no per-lane byte path in the way of the loads), then the one vector
   // that straddles the end, in the lane that owns it.
   for (uint32_t k = nfull; k < nany; k++) {
-    gbyte *p = gp<const unsigned char>(r->src[k]);
-    const uint32_t len = r->src_bytes[k];
+    gbyte *p = gp<const unsigned char>(r.src[k]);
+    const uint32_t len = r.src_bytes[k];
 #pragma unroll
     for (int u = 0; u < U; u++)
       if (lane_off + u * 1024u + 16u <= len) acc[u] ^= ld16(p + lane_off + u * 1024u);
   }
   for (uint32_t k = nfull; k < nany; k++) {
-    const uint32_t len = r->src_bytes[k];
+    const uint32_t len = r.src_bytes[k];
     if (len & 15u) {
       const uint32_t soff = len & ~15u;  // offset of the straddling vector inside the tile
 #pragma unroll
       for (int u = 0; u < U; u++)
-        if (lane_off + u * 1024u == soff) acc[u] ^= load_straddle(gp<const unsigned char>(r->src[k]) + soff, len & 15u);
+        if (lane_off + u * 1024u == soff) acc[u] ^= load_straddle(gp<const unsigned char>(r.src[k]) + soff, len & 15u);
     }
   }
-  glob<unsigned char> *dp = gp<unsigned char>(r->dst);
-  const uint32_t out_bytes = r->out_bytes;
-  if (out_bytes == b.tile_bytes) {
+  glob<unsigned char> *dp = gp<unsigned char>(r.dst);
+  const uint32_t out_bytes = r.out_bytes;
+  if (out_bytes == tile_bytes) {
     glob<v4u_u> *q = (glob<v4u_u> *)(dp + lane_off);
 #pragma unroll
     for (int u = 0; u < U; u++) __builtin_nontemporal_store(acc[u], q + u * 64);
@@ -586,6 +581,20 @@ __device__ __forceinline__ void desc_tile(const DescBatch &b, uint32_t t) {
 #pragma unroll
     for (int u = 0; u < U; u++) store_tail(dp, out_bytes, lane_off + u * 1024u, acc[u]);
   }
+}
+
+template <int U, int PIPE>
+__device__ __forceinline__ void desc_tile(const DescBatch &b, uint32_t t) {
+  const_as<DescTile> &r = cst(b.tiles)[t];
+  const uint32_t meta = r.meta;
+  if (meta & kTileGeneral) {
+    if (meta & kTileWide)
+      desc_tile_wide<U, PIPE>(b, r.src_bytes[0], r.src_bytes[1], r.src_bytes[2], meta & 0xFFu, (meta >> 8) & 0xFFu);
+    else
+      desc_tile_general<U>(b, r.src_bytes[0], r.src_bytes[1], r.src_bytes[2]);
+    return;
+  }
+  desc_plain<U, PIPE>(r, b.tile_bytes);
 }
 
 template <int U, int PIPE>
@@ -624,6 +633,70 @@ __global__ __launch_bounds__(kBlock) void xor_desc(DescBatch b) {
 template <int U, int PIPE>
 __global__ __launch_bounds__(kBlock) void xor_desc_p(DescBatch b) {
   desc_body<U, PIPE>(b);
+}
+
+// ---------------------------------------------------------------------------
+// Small descriptor batches (a few stripes, <= 8 sources each, no window):
+// the whole descriptor travels in the kernel arguments (DescArgs, runs
+// sorted longest first) and every tile derives its record in scalar
+// registers -- no desc_tiles launch, no staged tables, one launch.  Tiles are
+// single subtiles (no grouping: the batch is latency-bound, not byte-bound).
+// ---------------------------------------------------------------------------
+struct ArgSrc {  // r.src[i]: source i of the stripe's run, offset to the tile
+  const_as<uint64_t> *p;
+  uint64_t off;
+  __device__ __forceinline__ uint64_t operator[](uint32_t i) const { return p[i] + off; }
+};
+struct ArgLen {  // r.src_bytes[i]: readable bytes of source i inside the tile
+  const_as<uint64_t> *len;
+  uint64_t off, T;
+  __device__ __forceinline__ uint32_t operator[](uint32_t i) const {
+    const uint64_t l = len[i] - off;
+    return (uint32_t)(l < T ? l : T);
+  }
+};
+struct ArgRec {
+  uint64_t dst;
+  uint32_t out_bytes, meta;
+  ArgSrc src;
+  ArgLen src_bytes;
+};
+
+template <int U>
+__global__ __launch_bounds__(kBlock) void xor_desc_args(DescArgs a) {
+  // read in place from the kernarg segment (the only explicit argument, at
+  // offset 0): dynamic indices become scalar loads, nothing is copied
+  const_as<DescArgs> *A = (const_as<DescArgs> *)__builtin_amdgcn_kernarg_segment_ptr();
+  constexpr uint32_t T = (uint32_t)kBlock * U * 16u;
+  __shared__ uint32_t next[2];
+  if (threadIdx.x == 0) next[0] = queue_grab(a.ctr, a.base);
+  __syncthreads();
+  uint32_t t = __builtin_amdgcn_readfirstlane(next[0]);
+  int slot = 0;
+  while (t < a.ntiles) {
+    uint32_t s = 0;
+    while (s + 1 < a.nstripes && t >= A->tile_start[s + 1]) s++;
+    const uint64_t off = (uint64_t)(t - A->tile_start[s]) * T;
+    const uint32_t first = A->first[s], n = A->nsrc[s];
+    uint32_t nf = 0, na = 0;
+    for (uint32_t k = 0; k < n; k++) {
+      const uint64_t len = A->src_len[first + k];
+      nf += len >= off + T;
+      na += len > off;
+    }
+    const uint64_t out_left = A->out_len[s] - off;
+    ArgRec r;
+    r.dst = A->dst[s] + off;
+    r.out_bytes = (uint32_t)(out_left < T ? out_left : T);
+    r.meta = nf | na << 8;
+    r.src = ArgSrc{A->src_ptr + first, off};
+    r.src_bytes = ArgLen{A->src_len + first, off, T};
+    desc_plain<U, 0>(r, T);
+    slot ^= 1;
+    if (threadIdx.x == 0) next[slot] = queue_grab(a.ctr, a.base);
+    __syncthreads();
+    t = __builtin_amdgcn_readfirstlane(next[slot]);
+  }
 }
 
 // Tile records of a descriptor batch: one wave per stripe, one lane per
@@ -966,6 +1039,18 @@ hipError_t launch_xor_desc(hipStream_t st, int grid, int vecs, const DescBatch &
     case 4: hipLaunchKernelGGL((xor_desc<4>), dim3(grid), dim3(kBlock), 0, st, b); break;
     case 8: hipLaunchKernelGGL((xor_desc<8>), dim3(grid), dim3(kBlock), 0, st, b); break;
     default: hipLaunchKernelGGL((xor_desc<2>), dim3(grid), dim3(kBlock), 0, st, b); break;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_xor_desc_args(hipStream_t st, int grid, int vecs, const DescArgs &a) {
+  if (a.ntiles == 0) return hipSuccess;
+  if ((uint32_t)grid > a.ntiles) grid = (int)a.ntiles;
+  switch (vecs) {
+    case 1: hipLaunchKernelGGL((xor_desc_args<1>), dim3(grid), dim3(kBlock), 0, st, a); break;
+    case 4: hipLaunchKernelGGL((xor_desc_args<4>), dim3(grid), dim3(kBlock), 0, st, a); break;
+    case 8: hipLaunchKernelGGL((xor_desc_args<8>), dim3(grid), dim3(kBlock), 0, st, a); break;
+    default: hipLaunchKernelGGL((xor_desc_args<2>), dim3(grid), dim3(kBlock), 0, st, a); break;
   }
   return hipGetLastError();
 }

@@ -177,8 +177,8 @@ def main():
             bcp.check("bcp_xor_stripes_async", L.bcp_xor_stripes_async(q.h, st, len(stripes), so, len(sources)))
         bytes_per_step = sum(int(ls.sum()) + int(ls.max()) for ls in lens_all)
         S = len(stripes)
-        U = eng.option("desc_vecs_per_thread")
-        pipe = eng.option("desc_pipe") if U == 8 else 0
+        U = 0  # read back after the timed launches (auto tile size)
+        pipe = 0
         kernel = f"xor_desc_p<{U},{pipe}>" if pipe else f"xor_desc<{U}>"
         kernel_tag = f"xor_desc_p<{U}, {pipe}>" if pipe else f"xor_desc<{U}>"
         workload = (f"config5 shapes: {S} stripes x {N} chunks, log-uniform 64 KiB-4 MiB, "
@@ -250,6 +250,14 @@ def main():
     d.barrier()
     wall = t1 - t0
     kern_ms = q.elapsed_ms(0, 1) / a.steps  # avg launch duration on the kernel's stream
+    if a.mode == "mixed":  # the descriptor kernel's form and tile size of the timed launches
+        U = eng.option("last_desc_vecs")
+        pipe = eng.option("desc_pipe") if U == 8 else 0
+        if eng.option("last_desc_form") == 2:
+            kernel, kernel_tag = f"xor_desc_args<{U}>", f"xor_desc_args<{U}>"
+        else:
+            kernel = f"xor_desc_p<{U},{pipe}>" if pipe else f"xor_desc<{U}>"
+            kernel_tag = f"xor_desc_p<{U}, {pipe}>" if pipe else f"xor_desc<{U}>"
     if a.mode != "mixed":  # tile size the engine chose for the timed launches
         U = eng.option("last_stream_vecs")
         # register-budget instantiations (launch_xor_stream in bcp_kernels.hip)

@@ -178,7 +178,7 @@ def test_tuning_variants_agree(oracle, engine, dev, queue, bpc, vecs, sched):
         engine.option("schedule", 0)
         engine.option("desc_schedule", 0)
         engine.option("desc_blocks_per_cu", 0)
-        engine.option("desc_vecs_per_thread", 8)
+        engine.option("desc_vecs_per_thread", 0)
     ref = np.bitwise_xor.reduce(data.reshape(nstripes, nsrc, chunk), axis=1).reshape(-1)
     assert np.array_equal(out, ref)
     assert np.array_equal(res[0], oracle.xor_padded_np([data[:1000], data[5:70000]]))
@@ -321,8 +321,18 @@ def test_uniform_descriptor_batch_takes_pointer_table_path(oracle, dev, queue, s
 # --------------------------------------------------------------------------
 # descriptor path: variable lengths, padding, alignment, windows, rebuild
 # --------------------------------------------------------------------------
+@pytest.fixture(params=["args", "general"])
+def desc_path(request, engine):
+    """Small descriptor batches through the kernel-argument form
+    (xor_desc_args, desc_args_max 4) and through desc_tiles + xor_desc (0)."""
+    prev = engine.option("desc_args_max")
+    engine.option("desc_args_max", 4 if request.param == "args" else 0)
+    yield request.param
+    engine.option("desc_args_max", prev)
+
+
 @pytest.mark.parametrize("seed", range(8))
-def test_descriptor_mixed_lengths_and_alignment(oracle, dev, queue, seed):
+def test_descriptor_mixed_lengths_and_alignment(oracle, dev, queue, seed, desc_path):
     rng = np.random.default_rng(100 + seed)
     stripes, refs = [], []
     for _ in range(int(rng.integers(1, 12))):
@@ -339,7 +349,7 @@ def test_descriptor_mixed_lengths_and_alignment(oracle, dev, queue, seed):
 
 
 @pytest.mark.parametrize("vecs", [8, 4, 2, 1])
-def test_descriptor_grouped_tiles(oracle, engine, dev, queue, vecs):
+def test_descriptor_grouped_tiles(oracle, engine, dev, queue, vecs, desc_path):
     """Staircase lengths whose covering sets hold for many consecutive
     subtiles: every grouped-tile shape (1 source x 2..8 subtiles, 2 x 2..4,
     3 x 2, 4 x 2), their boundaries with plain and partial tiles, the last
@@ -360,10 +370,64 @@ def test_descriptor_grouped_tiles(oracle, engine, dev, queue, vecs):
     engine.option("desc_vecs_per_thread", vecs)
     try:
         outs = gpu_stripes(dev, queue, stripes)
+        # the same stripes a few at a time: small batches (the args form when on)
+        outs4 = []
+        for i in range(0, len(stripes), 3):
+            outs4 += gpu_stripes(dev, queue, stripes[i:i + 3])
     finally:
-        engine.option("desc_vecs_per_thread", 8)
-    for i, (o, r) in enumerate(zip(outs, refs)):
+        engine.option("desc_vecs_per_thread", 0)
+    for i, (o, o4, r) in enumerate(zip(outs, outs4, refs)):
         assert np.array_equal(o, r), i
+        assert np.array_equal(o4, r), i
+
+
+@pytest.mark.parametrize("nstripes,nsrc", [(1, 1), (1, 8), (2, 5), (4, 8), (5, 8), (3, 9), (4, 7)])
+def test_small_batches_in_kernel_arguments(oracle, engine, dev, queue, nstripes, nsrc, desc_path):
+    """Batches of at most 4 stripes and 32 sources (<= 8 per stripe) travel in
+    the kernel arguments; 5 stripes or 9 sources take the general path.
+    Mixed lengths (zero padding, byte tails, a zero-length source), unsorted
+    input order, misaligned sources and outputs, every auto tile size."""
+    rng = np.random.default_rng(31 * nstripes + nsrc)
+    for scale in (40_000, 600_000, 3_000_000):
+        stripes, refs = [], []
+        for _ in range(nstripes):
+            lens = [int(x) for x in rng.integers(0, scale, size=nsrc)]
+            if nsrc > 2:
+                lens[1] = 0
+            chunks = [rng.integers(0, 256, size=L, dtype=np.uint8) for L in lens]
+            pads = [int(x) for x in rng.integers(0, 16, size=nsrc)]
+            stripes.append(dict(chunks=chunks, out_len=max(lens) + int(rng.integers(0, 3)), pads=pads,
+                                dst_pad=int(rng.integers(0, 16))))
+            ref = np.zeros(stripes[-1]["out_len"], np.uint8)
+            for c in chunks:
+                ref[:len(c)] ^= c
+            refs.append(ref)
+        outs = gpu_stripes(dev, queue, stripes)
+        for i, (o, r) in enumerate(zip(outs, refs)):
+            assert np.array_equal(o, r), (scale, i)
+
+
+@pytest.mark.parametrize("side", [1, 0])
+def test_large_mixed_batch_side_stream_tiles(oracle, engine, dev, queue, side):
+    """A batch large enough for desc_tiles to run on the side stream (>= 2 x
+    grid tiles), submitted twice back to back (the second desc_tiles overlaps
+    the first fold, on another ring slot's records): both outputs exact."""
+    rng = np.random.default_rng(77 + side)
+    prev = engine.option("desc_side_tiles")
+    engine.option("desc_side_tiles", side)
+    try:
+        stripes, refs = [], []
+        for _ in range(60):
+            lens = [int(x) for x in np.exp(rng.uniform(np.log(64 * KiB), np.log(4 * MiB), size=8))]
+            chunks = [rng.integers(0, 256, size=L, dtype=np.uint8) for L in lens]
+            stripes.append(dict(chunks=chunks, out_len=max(lens)))
+            refs.append(oracle.xor_padded_np(chunks))
+        a = gpu_stripes(dev, queue, stripes)
+        b = gpu_stripes(dev, queue, stripes)
+    finally:
+        engine.option("desc_side_tiles", prev)
+    for i, (x, y, r) in enumerate(zip(a, b, refs)):
+        assert np.array_equal(x, r) and np.array_equal(y, r), i
 
 
 @pytest.mark.parametrize("n", [9, 12, 20, 56])
@@ -530,7 +594,7 @@ def test_window_replay_tiles(oracle, engine, dev, queue, vecs, window):
     try:
         outs = gpu_stripes(dev, queue, stripes)
     finally:
-        engine.option("desc_vecs_per_thread", 8)
+        engine.option("desc_vecs_per_thread", 0)
     for i, (o, r) in enumerate(zip(outs, refs)):
         assert np.array_equal(o, r), i
 
@@ -659,7 +723,9 @@ KNOBS = {
     "blocks_per_cu": (1, [1, 2, 32], [0, 33]),
     "vecs_per_thread": (0, [0, 1, 2, 4, 8], [3, 16]),
     "desc_blocks_per_cu": (0, [0, 1, 32], [-1, 33]),
-    "desc_vecs_per_thread": (8, [1, 2, 4, 8], [0, 3]),
+    "desc_vecs_per_thread": (0, [0, 1, 2, 4, 8], [3, 16]),
+    "desc_args_max": (4, [0, 1, 4], [-1, 5]),
+    "desc_side_tiles": (1, [0, 1], [2]),
     "schedule": (0, [0, 1], [2]),
     "desc_schedule": (0, [0, 1], [2]),
     "desc_grab": (1, [1, 64], [0, 65]),

@@ -5,8 +5,10 @@ stripes, device-resident.  For each batch size and each entry point:
   stream  bcp_xor_uniform_async (xor_stream<8,U>, the config-2 kernel)
   table   bcp_xor_stripes_async with a descriptor table of the same stripes
           (uniform: host staging + the pointer-table xor_stream, the rebuild form)
-  desc    the same call with engine option desc_force = 1 (host staging +
-          desc_tiles setup kernel + xor_desc, the config-5 kernel)
+  desc    the same call with engine option desc_force = 1: the descriptor
+          kernel (batches of <= 4 stripes in the kernel arguments, xor_desc_args;
+          larger ones host staging + desc_tiles + xor_desc, the config-5 kernel)
+  desc_tiles  desc_force = 1 and desc_args_max = 0: always desc_tiles + xor_desc
 
 two figures:
   pipelined_us  launches back to back, HIP-event time per launch on the queue
@@ -34,7 +36,7 @@ KiB = 1024
 ap = argparse.ArgumentParser()
 ap.add_argument("--reps", type=int, default=50)
 ap.add_argument("--batches", default="1,2,4,8,16,32,64,128,256,512,1024,2048,4096,12500")
-ap.add_argument("--entries", default="stream,table,desc")
+ap.add_argument("--entries", default="stream,table,desc,desc_tiles")
 ap.add_argument("--table-host-max", default="", help="comma list: time table/desc at each engine table_host_max")
 ap.add_argument("--tunings", default="",
                 help="U:bpc list: time the stream entry with each explicit tuning (A/B for small batches)")
@@ -66,6 +68,7 @@ for s in batches:
         "stream": lambda: q.xor_uniform(dst, src, s, N, C),
         "table": table,
         "desc": table,
+        "desc_tiles": table,
     }
     runs = [(n, entry[n], None) for n in a.entries.split(",") if n]
     for thm in filter(None, a.table_host_max.split(",")):
@@ -74,7 +77,8 @@ for s in batches:
         u, bpc = (int(x) for x in tun.split(":"))
         runs.append(("stream", entry["stream"], (u, bpc)))
     for name, fn, tun in runs:
-        eng.option("desc_force", 1 if name == "desc" else 0)
+        eng.option("desc_force", 1 if name.startswith("desc") else 0)
+        eng.option("desc_args_max", 0 if name == "desc_tiles" else 4)
         if tun and tun[0] == "thm":
             eng.option("table_host_max", tun[1])
         elif tun:
