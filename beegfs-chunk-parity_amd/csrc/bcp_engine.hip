@@ -324,6 +324,7 @@ extern "C" int bcp_set_option(bcp_engine *eng, const char *key, int value) {
   else if (!strcmp(key, "desc_vecs_per_thread") && (value == 0 || desc_vecs_ok(value))) eng->tuning.desc_vecs = value;
   else if (!strcmp(key, "desc_args_max") && value >= 0 && value <= kArgStripes) eng->tuning.desc_args_max = value;
   else if (!strcmp(key, "desc_side_tiles") && (value == 0 || value == 1)) eng->tuning.desc_side_tiles = value;
+  else if (!strcmp(key, "desc_ahead") && (value == 0 || value == 1)) eng->tuning.desc_ahead = value;
   else if (!strcmp(key, "schedule") && (value == kSchedQueue || value == kSchedStatic)) eng->tuning.schedule = value;
   else if (!strcmp(key, "desc_schedule") && (value == kSchedQueue || value == kSchedStatic)) eng->tuning.desc_schedule = value;
   else if (!strcmp(key, "desc_grab") && value >= 1 && value <= 64) eng->tuning.desc_grab = value;
@@ -358,6 +359,7 @@ extern "C" int bcp_get_option(bcp_engine *eng, const char *key, int *value) {
   else if (!strcmp(key, "desc_vecs_per_thread")) *value = t.desc_vecs;
   else if (!strcmp(key, "desc_args_max")) *value = t.desc_args_max;
   else if (!strcmp(key, "desc_side_tiles")) *value = t.desc_side_tiles;
+  else if (!strcmp(key, "desc_ahead")) *value = t.desc_ahead;
   else if (!strcmp(key, "desc_schedule")) *value = t.desc_schedule;
   else if (!strcmp(key, "desc_grab")) *value = t.desc_grab;
   else if (!strcmp(key, "desc_force")) *value = t.desc_force;
@@ -966,7 +968,7 @@ static int submit_desc(bcp_queue *q, const bcp_stripe *stripes, uint32_t nstripe
   } else {
     HIP_RC(launch_desc_tiles(q->stream, b));
   }
-  const hipError_t le = launch_xor_desc(q->stream, grid, vecs, b, e->tuning.desc_pipe);
+  const hipError_t le = launch_xor_desc(q->stream, grid, vecs, b, e->tuning.desc_pipe, e->tuning.desc_ahead);
   if (le == hipSuccess) {
     e->last_desc_vecs.store(vecs, std::memory_order_relaxed);
     e->last_desc_form.store(1, std::memory_order_relaxed);

@@ -30,7 +30,8 @@ struct Tuning {
     // 0 = auto (desc_grid_for: one per CU).
     int desc_blocks_per_cu = 0;
     int desc_vecs = 0;          // 1, 2, 4, 8; 0 = by batch size (desc_vecs_for)
-    int desc_args_max = 4;      // batches of at most this many stripes go in the kernel arguments (0 = never)
+    int desc_args_max = 16;     // batches of at most this many stripes go in the kernel arguments (0 = never)
+    int desc_ahead = 0;         // xor_desc: take the next tile and touch its record before folding the current one
     int desc_side_tiles = 1;    // large batches: desc_tiles on the copy stream, overlapping the previous fold
     int desc_grab = 1;          // tiles per work-queue grab
     int desc_schedule = kSchedQueue;
@@ -105,6 +106,7 @@ struct alignas(64) DescTile {
 constexpr uint32_t kTileGeneral = 0x80000000u;
 constexpr uint32_t kTileWide = 0x40000000u;  // with kTileGeneral: > kTileSrcs sources, no window
 static_assert(sizeof(DescTile) == 128, "tile record is two s_load_dwordx16");
+static_assert(kTileSrcs == 8, "xor_desc_args counts covering sources in scalar registers");
 
 // Rows (source x subtile pairs) of a grouped tile for U vectors per lane:
 // every load of the tile is in flight at once, so C*M*U <= 32 keeps the
@@ -199,8 +201,8 @@ struct DescBatch {
 // A small descriptor batch passed whole in the kernel arguments
 // (xor_desc_args): <= kArgStripes stripes, <= kArgSources sources in all, each
 // stripe's run sorted longest first, <= kTileSrcs per stripe, no window.
-constexpr int kArgStripes = 4;
-constexpr int kArgSources = 32;
+constexpr int kArgStripes = 16;
+constexpr int kArgSources = 128;  // DescArgs stays < 3 KiB of the 4 KiB kernarg space
 struct DescArgs {
     uint64_t dst[kArgStripes];
     uint64_t out_len[kArgStripes];
@@ -225,7 +227,7 @@ uint32_t stream_tiles_per_stripe(uint64_t chunk_bytes, int vecs);
 // launch_xor_stream.
 hipError_t launch_desc_tiles(hipStream_t st, const DescBatch &b);
 hipError_t launch_xor_desc(hipStream_t st, int grid, int vecs,
-                           const DescBatch &b, int pipe = 0);
+                           const DescBatch &b, int pipe = 0, int ahead = 0);
 // Small batch in the arguments; same work-queue accounting (ntiles + grid).
 hipError_t launch_xor_desc_args(hipStream_t st, int grid, int vecs, const DescArgs &a);
 hipError_t launch_fill_synthetic(hipStream_t st, int grid, char *dst,

@@ -597,7 +597,7 @@ __device__ __forceinline__ void desc_tile(const DescBatch &b, uint32_t t) {
   desc_plain<U, PIPE>(r, b.tile_bytes);
 }
 
-template <int U, int PIPE>
+template <int U, int PIPE, int AHEAD = 0>
 __device__ __forceinline__ void desc_body(const DescBatch &b) {
   if (b.sched == kSchedStatic) {
     const uint32_t g = gridDim.x;
@@ -606,13 +606,49 @@ __device__ __forceinline__ void desc_body(const DescBatch &b) {
     for (uint32_t t = t_begin; t < t_end; t++) desc_tile<U, PIPE>(b, t);
     return;
   }
+  const uint32_t nchunks = (b.ntiles + b.grab - 1) / b.grab;
+  if constexpr (AHEAD) {
+    // Grab-ahead (engine option desc_ahead): the next tile is taken before
+    // the current one is folded and the first line of its record touched, so
+    // the queue atomic and the dependent record load overlap the current
+    // tile's data loads instead of sitting between two tiles.  Exactly one
+    // failing grab per workgroup, as the host's counter accounting expects:
+    // no further grab once one has failed.
+    __shared__ uint32_t next[2];
+    if (threadIdx.x == 0) {
+      next[0] = queue_grab(b.ctr, b.base);
+      next[1] = next[0] < nchunks ? queue_grab(b.ctr, b.base) : 0xFFFFFFFFu;
+    }
+    __syncthreads();
+    uint32_t c = __builtin_amdgcn_readfirstlane(next[0]);
+    uint32_t n1 = __builtin_amdgcn_readfirstlane(next[1]);
+    __syncthreads();  // both slots read before thread 0 rewrites one
+    while (c < nchunks) {
+      uint32_t g = 0xFFFFFFFFu;
+      if (threadIdx.x == 0 && n1 < nchunks) g = queue_grab(b.ctr, b.base);
+      // the next record's first line into the scalar cache: issued here (a
+      // volatile load is neither dropped nor sunk), consumed after the tile
+      uint32_t touch = 0;
+      if (n1 < nchunks)
+        touch = ((const volatile __attribute__((address_space(4))) uint32_t *)&cst(b.tiles)[n1 * b.grab].meta)[0];
+      const uint32_t t0 = c * b.grab;
+      const uint32_t t1 = min(t0 + b.grab, b.ntiles);
+      for (uint32_t t = t0; t < t1; t++) desc_tile<U, PIPE>(b, t);
+      __asm__ volatile("" ::"s"(touch));
+      if (threadIdx.x == 0) next[0] = g;
+      __syncthreads();
+      c = n1;
+      n1 = __builtin_amdgcn_readfirstlane(next[0]);
+      __syncthreads();  // every wave has read next[0] before it is rewritten
+    }
+    return;
+  }
   // Work queue in grabs of b.grab consecutive tiles.
   __shared__ uint32_t next[2];
   if (threadIdx.x == 0) next[0] = queue_grab(b.ctr, b.base);
   __syncthreads();
   uint32_t c = __builtin_amdgcn_readfirstlane(next[0]);
   int slot = 0;
-  const uint32_t nchunks = (b.ntiles + b.grab - 1) / b.grab;
   while (c < nchunks) {
     const uint32_t t0 = c * b.grab;
     const uint32_t t1 = min(t0 + b.grab, b.ntiles);
@@ -629,10 +665,11 @@ __global__ __launch_bounds__(kBlock) void xor_desc(DescBatch b) {
   desc_body<U, 0>(b);
 }
 
-// Rolling-window load variants (A/B: engine option desc_pipe; fold_cover).
-template <int U, int PIPE>
+// Rolling-window load variants (A/B: engine option desc_pipe; fold_cover),
+// and the grab-ahead form (desc_ahead).
+template <int U, int PIPE, int AHEAD = 0>
 __global__ __launch_bounds__(kBlock) void xor_desc_p(DescBatch b) {
-  desc_body<U, PIPE>(b);
+  desc_body<U, PIPE, AHEAD>(b);
 }
 
 // ---------------------------------------------------------------------------
@@ -1023,9 +1060,13 @@ hipError_t launch_desc_tiles(hipStream_t st, const DescBatch &b) {
   return hipGetLastError();
 }
 
-hipError_t launch_xor_desc(hipStream_t st, int grid, int vecs, const DescBatch &b, int pipe) {
+hipError_t launch_xor_desc(hipStream_t st, int grid, int vecs, const DescBatch &b, int pipe, int ahead) {
   if (b.ntiles == 0) return hipSuccess;
   if ((uint32_t)grid > b.ntiles) grid = (int)b.ntiles;
+  if (ahead && pipe == 5 && vecs == 8 && b.sched == kSchedQueue) {
+    hipLaunchKernelGGL((xor_desc_p<8, 5, 1>), dim3(grid), dim3(kBlock), 0, st, b);
+    return hipGetLastError();
+  }
   if (pipe && vecs == 8) {
     switch (pipe) {
       case 2: hipLaunchKernelGGL((xor_desc_p<8, 2>), dim3(grid), dim3(kBlock), 0, st, b); return hipGetLastError();

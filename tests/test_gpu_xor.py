@@ -326,7 +326,7 @@ def desc_path(request, engine):
     """Small descriptor batches through the kernel-argument form
     (xor_desc_args, desc_args_max 4) and through desc_tiles + xor_desc (0)."""
     prev = engine.option("desc_args_max")
-    engine.option("desc_args_max", 4 if request.param == "args" else 0)
+    engine.option("desc_args_max", 16 if request.param == "args" else 0)
     yield request.param
     engine.option("desc_args_max", prev)
 
@@ -381,10 +381,10 @@ def test_descriptor_grouped_tiles(oracle, engine, dev, queue, vecs, desc_path):
         assert np.array_equal(o4, r), i
 
 
-@pytest.mark.parametrize("nstripes,nsrc", [(1, 1), (1, 8), (2, 5), (4, 8), (5, 8), (3, 9), (4, 7)])
+@pytest.mark.parametrize("nstripes,nsrc", [(1, 1), (1, 8), (2, 5), (4, 8), (16, 8), (17, 8), (3, 9), (12, 7)])
 def test_small_batches_in_kernel_arguments(oracle, engine, dev, queue, nstripes, nsrc, desc_path):
-    """Batches of at most 4 stripes and 32 sources (<= 8 per stripe) travel in
-    the kernel arguments; 5 stripes or 9 sources take the general path.
+    """Batches of at most 16 stripes and 128 sources (<= 8 per stripe) travel
+    in the kernel arguments; 17 stripes or 9 sources take the general path.
     Mixed lengths (zero padding, byte tails, a zero-length source), unsorted
     input order, misaligned sources and outputs, every auto tile size."""
     rng = np.random.default_rng(31 * nstripes + nsrc)
@@ -407,14 +407,16 @@ def test_small_batches_in_kernel_arguments(oracle, engine, dev, queue, nstripes,
             assert np.array_equal(o, r), (scale, i)
 
 
+@pytest.mark.parametrize("ahead", [0, 1])
 @pytest.mark.parametrize("side", [1, 0])
-def test_large_mixed_batch_side_stream_tiles(oracle, engine, dev, queue, side):
+def test_large_mixed_batch_side_stream_tiles(oracle, engine, dev, queue, side, ahead):
     """A batch large enough for desc_tiles to run on the side stream (>= 2 x
     grid tiles), submitted twice back to back (the second desc_tiles overlaps
     the first fold, on another ring slot's records): both outputs exact."""
     rng = np.random.default_rng(77 + side)
     prev = engine.option("desc_side_tiles")
     engine.option("desc_side_tiles", side)
+    engine.option("desc_ahead", ahead)
     try:
         stripes, refs = [], []
         for _ in range(60):
@@ -426,6 +428,7 @@ def test_large_mixed_batch_side_stream_tiles(oracle, engine, dev, queue, side):
         b = gpu_stripes(dev, queue, stripes)
     finally:
         engine.option("desc_side_tiles", prev)
+        engine.option("desc_ahead", 0)
     for i, (x, y, r) in enumerate(zip(a, b, refs)):
         assert np.array_equal(x, r) and np.array_equal(y, r), i
 
@@ -724,7 +727,8 @@ KNOBS = {
     "vecs_per_thread": (0, [0, 1, 2, 4, 8], [3, 16]),
     "desc_blocks_per_cu": (0, [0, 1, 32], [-1, 33]),
     "desc_vecs_per_thread": (0, [0, 1, 2, 4, 8], [3, 16]),
-    "desc_args_max": (4, [0, 1, 4], [-1, 5]),
+    "desc_args_max": (16, [0, 1, 16], [-1, 17]),
+    "desc_ahead": (0, [0, 1], [2]),
     "desc_side_tiles": (1, [0, 1], [2]),
     "schedule": (0, [0, 1], [2]),
     "desc_schedule": (0, [0, 1], [2]),

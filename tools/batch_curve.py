@@ -6,7 +6,7 @@ stripes, device-resident.  For each batch size and each entry point:
   table   bcp_xor_stripes_async with a descriptor table of the same stripes
           (uniform: host staging + the pointer-table xor_stream, the rebuild form)
   desc    the same call with engine option desc_force = 1: the descriptor
-          kernel (batches of <= 4 stripes in the kernel arguments, xor_desc_args;
+          kernel (batches of <= 16 stripes in the kernel arguments, xor_desc_args;
           larger ones host staging + desc_tiles + xor_desc, the config-5 kernel)
   desc_tiles  desc_force = 1 and desc_args_max = 0: always desc_tiles + xor_desc
 
@@ -78,7 +78,7 @@ for s in batches:
         runs.append(("stream", entry["stream"], (u, bpc)))
     for name, fn, tun in runs:
         eng.option("desc_force", 1 if name.startswith("desc") else 0)
-        eng.option("desc_args_max", 0 if name == "desc_tiles" else 4)
+        eng.option("desc_args_max", 0 if name == "desc_tiles" else 16)
         if tun and tun[0] == "thm":
             eng.option("table_host_max", tun[1])
         elif tun:
