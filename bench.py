@@ -256,8 +256,9 @@ def main():
         if eng.option("last_desc_form") == 2:
             kernel, kernel_tag = f"xor_desc_args<{U}>", f"xor_desc_args<{U}>"
         else:
+            ahead = eng.option("desc_ahead") if pipe == 5 else 0
             kernel = f"xor_desc_p<{U},{pipe}>" if pipe else f"xor_desc<{U}>"
-            kernel_tag = f"xor_desc_p<{U}, {pipe}>" if pipe else f"xor_desc<{U}>"
+            kernel_tag = f"xor_desc_p<{U}, {pipe}, {ahead}>" if pipe else f"xor_desc<{U}>"
     if a.mode != "mixed":  # tile size the engine chose for the timed launches
         U = eng.option("last_stream_vecs")
         # register-budget instantiations (launch_xor_stream in bcp_kernels.hip)
@@ -405,6 +406,7 @@ def main():
             "roofline": {
                 "bound": "hbm",
                 "kernel": kernel,
+                "kernel_tag": kernel_tag,  # as rocprofv3 names it
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",

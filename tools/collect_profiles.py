@@ -25,6 +25,19 @@ def one(pattern):
     return hits[-1]
 
 
+def derive_tag(kern: str) -> str:
+    """rocprofv3 name fragment of a bench.py display name (lines written
+    before bench.py reported kernel_tag)."""
+    import re
+    m = re.match(r"xor_stream_w<(\d+),(\d+),(strided|gather),wpe(\d+)>", kern)
+    if m:
+        return f"xor_stream_w<{m[1]}, {m[2]}, {1 if m[3] == 'gather' else 0}, 0, {m[4]}>"
+    m = re.match(r"xor_desc_p<(\d+),(\d+)>", kern)
+    if m:
+        return f"xor_desc_p<{m[1]}, {m[2]}, 0>"
+    return kern
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--src", required=True)
@@ -45,8 +58,7 @@ def main():
         write = os.path.join(a.dst, f"{m}_pmc_write.csv")
         shutil.copy(one(os.path.join(d, "pmc_fetch", "**", "*counter_collection.csv")), fetch)
         shutil.copy(one(os.path.join(d, "pmc_write", "**", "*counter_collection.csv")), write)
-        kern = line["roofline"]["kernel"]
-        tag = kern.split("<")[0]  # kernel base name for the CSV match; the full template below
+        tag = line["roofline"].get("kernel_tag") or derive_tag(line["roofline"]["kernel"])
         cfg = line["config"]
         mode_key = "rebuild_packed" if m == "rebuild" else ("gen" if m == "config4" else m)
         wkey = f"{mode_key}:{cfg['stripes_per_gpu']}x{cfg['nsrc']}x{cfg['chunk_bytes']}"
