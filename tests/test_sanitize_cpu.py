@@ -1,8 +1,10 @@
 """ThreadSanitizer run of the host C layer on the CPU (tools/tsan_host.sh):
 parity gen over 6 loopback ranks x 12 lanes and a rebuild (CPU test-double
-fold), plus a run where one rank's parity writes fail from many lanes at
+fold), a run where one rank's parity writes fail from many lanes at
 once (the sticky error is raised once, race-free; the reference writes it
-unlocked).  Fails on any TSan report."""
+unlocked), and the C caller test with one forked process per
+rank on the socketpair transport (3 lanes per rank share its sockets).  Fails
+on any TSan report."""
 import os
 import subprocess
 
@@ -15,3 +17,4 @@ def test_protocol_under_threadsanitizer(bcp):
     assert r.returncode == 0, out[-4000:]
     assert "ThreadSanitizer" not in out, out[-4000:]
     assert "OK: 0 problems" in out
+    assert "caller_test ok" in out

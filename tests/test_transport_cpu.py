@@ -183,10 +183,11 @@ def test_caller_defined_st2rank_and_hoststate(bcp, tmp_path):
     against the reference's layout, ranks as forked processes on the
     socketpair transport calling process_task directly, parity checked."""
     exe = tmp_path / "caller"
-    lib_dir = os.path.dirname(bcp.LIB_PATH)
-    subprocess.run(["gcc", "-std=gnu99", "-O1", "-Wall", "-Werror", "-pthread", "-I", os.path.join(ROOT, "include"),
-                    "-o", str(exe), os.path.join(ROOT, "tests", "native", "caller_test.c"), "-L", lib_dir, "-lbcp",
-                    f"-Wl,-rpath,{lib_dir}"], check=True)
+    lib = bcp.LIB_PATH  # the product library (or its sanitizer build under tools/asan_host.sh)
+    san = ["-fsanitize=address,undefined"] if "asan" in os.path.basename(lib) else []
+    subprocess.run(["gcc", "-std=gnu99", "-O1", "-Wall", "-Werror", "-pthread", *san, "-I",
+                    os.path.join(ROOT, "include"), "-o", str(exe), os.path.join(ROOT, "tests", "native", "caller_test.c"),
+                    lib, f"-Wl,-rpath,{os.path.dirname(lib)}"], check=True)
     r = subprocess.run([str(exe), str(tmp_path / "store")], capture_output=True, text=True, timeout=180)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "caller_test ok" in r.stdout

@@ -25,3 +25,12 @@ gcc -fsanitize=thread -o $B/protocol_driver $B/driver.o $B/hook.o $objs $P/build
 rm -rf /tmp/bcp_tsan_store
 TSAN_OPTIONS="halt_on_error=1 second_deadlock_stack=1" $B/protocol_driver /tmp/bcp_tsan_store
 rm -rf /tmp/bcp_tsan_store
+# ranks as processes: the C caller (its own st2rank / HostState) forks one
+# process per target on the socketpair transport; 3 lanes per rank share
+# that rank's sockets (progress by the waiting threads, unexpected messages)
+gcc $CF -c $R/tests/native/caller_test.c -o $B/caller.o
+gcc -fsanitize=thread -o $B/caller_test $B/caller.o $objs $P/build/bcp_kernels.o $P/build/bcp_engine.o \
+  -L/opt/rocm/lib -lamdhip64 -Wl,-rpath,/opt/rocm/lib -lstdc++ -lm -pthread
+rm -rf /tmp/bcp_tsan_caller
+TSAN_OPTIONS="halt_on_error=1 second_deadlock_stack=1" $B/caller_test /tmp/bcp_tsan_caller
+rm -rf /tmp/bcp_tsan_caller
