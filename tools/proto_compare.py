@@ -19,6 +19,10 @@ targets, 8-wide stripes of log-uniform 64 KiB-4 MiB chunks, 12 lanes).
 Rate = (chunk bytes read + parity bytes written) / wall; each round runs
 every fold once in a rotating order, medians over rounds after a cold one.
 Parity of the GPU and CPU runs is checked against the oracle on a sample.
+--procs: every storage target's rank is its own forked PROCESS (socketpair
+transport, bcp_gen_run_procs / bcp_rebuild_run_procs); this process never
+touches the GPU then (the ranks create their own HIP contexts), and the
+per-phase and fold-service counters live in the ranks (not reported).
 One JSON line per (workload, fold); tools only.
 """
 import argparse
@@ -157,13 +161,17 @@ def main():
     ap.add_argument("--c1-files", type=int, default=1333)
     ap.add_argument("--c5-stripes", type=int, default=1000)
     ap.add_argument("--lanes", type=int, default=12)
+    ap.add_argument("--procs", action="store_true", help="ranks as forked processes (socketpair transport)")
     a = ap.parse_args()
+    gen = bcp.gen_run_procs if a.procs else bcp.gen_run
+    rebuild = bcp.rebuild_run_procs if a.procs else bcp.rebuild_run
     folds = a.folds.split(",")
     noop = noop_hook()
     hooks = {"cpu_reference": ctypes.cast(oracle.lib().oracle_xor_rows, ctypes.c_void_p).value,
              "noop": ctypes.cast(noop.noop_fold, ctypes.c_void_p).value}
     rng = np.random.default_rng(0)
     wl = a.workloads.split(",")
+    tr = {"transport": "socketpair rank processes" if a.procs else "loopback threads"}
     if "c1_gen" in wl or "c1_rebuild" in wl:
         root = os.path.join(a.root, "c1")
         shutil.rmtree(root, ignore_errors=True)
@@ -176,15 +184,15 @@ def main():
         rd, wr = total_bytes(root, files)
         if "c1_gen" in wl:
             def run_gen():
-                return bcp.gen_run(root, 4, items, nlanes=a.lanes)
+                return gen(root, 4, items, nlanes=a.lanes)
             measure("config1_gen", folds, a.rounds, run_gen, lambda: verify(root, files, contents, 20, rng), rd + wr,
-                    hooks, {"lanes": a.lanes}, prepare=lambda: reset_parity(root, 4))
+                    hooks, {"lanes": a.lanes, **tr}, prepare=lambda: reset_parity(root, 4))
         if "c1_rebuild" in wl:
             # parity from a correct run, then rebuild target 2 again and again
             bcp.set_xor_hook(hooks["cpu_reference"])
             try:
                 reset_parity(root, 4)
-                bcp.gen_run(root, 4, items, nlanes=a.lanes)
+                gen(root, 4, items, nlanes=a.lanes)
             finally:
                 bcp.set_xor_hook(None)
             lost = {path: S.chunk_path(root, 2, path) for path, holders, _, _ in files if 2 in holders}
@@ -196,7 +204,7 @@ def main():
                         os.remove(fn)
 
             def run_rb():
-                return bcp.rebuild_run(root, 4, 2, items)
+                return rebuild(root, 4, 2, items)
 
             def check_rb():
                 for k, (path, fn) in enumerate(lost.items()):
@@ -205,7 +213,7 @@ def main():
                         if S.read_file(fn) != contents[path][holders.index(2)].tobytes():
                             return False, path
                 return True, None
-            measure("config1_rebuild", folds, a.rounds, run_rb, check_rb, rb_bytes, hooks, {"lanes": 1},
+            measure("config1_rebuild", folds, a.rounds, run_rb, check_rb, rb_bytes, hooks, {"lanes": 1, **tr},
                     prepare=drop_lost)
         shutil.rmtree(root, ignore_errors=True)
     if "c5_gen" in wl:
@@ -222,11 +230,12 @@ def main():
         rd, wr = total_bytes(root, files)
 
         def run5():
-            return bcp.gen_run(root, 9, items, nlanes=a.lanes)
+            return gen(root, 9, items, nlanes=a.lanes)
         measure("config5_gen", folds, a.rounds, run5, lambda: verify(root, files, contents, 20, rng), rd + wr, hooks,
-                {"lanes": a.lanes, "stripes": len(files)}, prepare=lambda: reset_parity(root, 9))
+                {"lanes": a.lanes, "stripes": len(files), **tr}, prepare=lambda: reset_parity(root, 9))
         shutil.rmtree(root, ignore_errors=True)
-    bcp.task_shutdown()
+    if not a.procs:
+        bcp.task_shutdown()
 
 
 if __name__ == "__main__":
