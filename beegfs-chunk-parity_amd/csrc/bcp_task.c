@@ -517,7 +517,11 @@ static int grow(fold_res *R, uint8_t **p, size_t *cap, size_t need)
     host_free(R, *p);
     *p = NULL;
     *cap = 0;
-    size_t c = MAX_(need, (size_t)1 << 20);
+    /* next power of two (>= 1 MiB): a worklist sorted by size (gen/main.c:
+     * 703-715) would otherwise re-pin rows at nearly every task */
+    size_t c = (size_t)1 << 20;
+    while (c < need)
+        c <<= 1;
     int rc = 0;
     if (R->device >= 0)
         rc = bcp_host_alloc_mapped(R->eng, c, (void **)p);
@@ -544,8 +548,11 @@ static int grow_dev(fold_res *R, void **p, size_t *cap, size_t need)
 }
 
 /* Take a resource for storage target st with room for rows_bytes of window
- * rows and an nbytes fold output.  use_gpu = 0 under the test hook. */
-static int res_acquire(HostState *hs, int use_gpu, size_t rows_bytes, size_t nbytes, fold_res **out)
+ * rows (twice when `windows` > 1: the next window is received while one is
+ * folded; a single-window task needs one set) and an nbytes fold output.
+ * use_gpu = 0 under the test hook. */
+static int res_acquire(HostState *hs, int use_gpu, size_t rows_bytes, size_t nbytes, uint64_t windows,
+                       fold_res **out)
 {
     int rc = 0, dev = -1;
     bcp_engine *e = NULL;
@@ -562,7 +569,7 @@ static int res_acquire(HostState *hs, int use_gpu, size_t rows_bytes, size_t nby
             continue;
         if (!best)
             best = pp;
-        if ((*pp)->h_cap >= rows_bytes && (*pp)->h_cap1 >= rows_bytes && (*pp)->hp_cap >= nbytes) {
+        if ((*pp)->h_cap >= rows_bytes && ((*pp)->h_cap1 >= rows_bytes || windows < 2) && (*pp)->hp_cap >= nbytes) {
             best = pp;
             break;
         }
@@ -581,7 +588,8 @@ static int res_acquire(HostState *hs, int use_gpu, size_t rows_bytes, size_t nby
         R->device = dev;
         R->eng = e;
     }
-    if ((rc = grow(R, &R->h_win[0], &R->h_cap, rows_bytes)) || (rc = grow(R, &R->h_win[1], &R->h_cap1, rows_bytes)) ||
+    if ((rc = grow(R, &R->h_win[0], &R->h_cap, rows_bytes)) ||
+        (windows > 1 && (rc = grow(R, &R->h_win[1], &R->h_cap1, rows_bytes))) ||
         (rc = grow(R, &R->h_par, &R->hp_cap, nbytes)))
         goto fail;
     *out = R;
@@ -904,7 +912,9 @@ static void parity_generator(const bcp_transport_ops *T, const char *path, const
      * pinned device-mapped rows the GPU folds use, to separate the memory
      * kind from the fold in tools/exp measurements) */
     const int pinned_rows = hook == NULL || getenv("BCP_HOOK_PINNED_ROWS") != NULL;
-    int res_rc = expected_messages ? res_acquire(hs, pinned_rows, pitch * (size_t)n, buffer_size, &L) : 0;
+    int res_rc = expected_messages
+                     ? res_acquire(hs, pinned_rows, pitch * (size_t)n, buffer_size, expected_messages, &L)
+                     : 0;
     if (res_rc) {
         LOGERR("no fold resources for '%s' on st %d: %s\n", path, hs->storage_target, bcp_strerror(res_rc));
         if (!have_had_error)
