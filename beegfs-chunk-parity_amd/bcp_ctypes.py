@@ -88,6 +88,7 @@ _SIGS = {
     "bcp_event_sync": ([_V], ctypes.c_int),
     "bcp_event_query": ([_V], ctypes.c_int),
     "bcp_dev_alloc": ([_V, ctypes.c_size_t, ctypes.POINTER(_V)], ctypes.c_int),
+    "bcp_dev_alloc_hostwrite": ([_V, ctypes.c_size_t, ctypes.POINTER(_V)], ctypes.c_int),
     "bcp_dev_free": ([_V, _V], ctypes.c_int),
     "bcp_host_alloc": ([_V, ctypes.c_size_t, ctypes.POINTER(_V)], ctypes.c_int),
     "bcp_host_alloc_mapped": ([_V, ctypes.c_size_t, ctypes.POINTER(_V)], ctypes.c_int),
@@ -255,6 +256,12 @@ class Engine:
     def alloc(self, nbytes: int) -> int:
         p = _V()
         call("bcp_dev_alloc", self.h, nbytes, ctypes.byref(p))
+        return p.value
+
+    def alloc_hostwrite(self, nbytes: int) -> int:
+        """Device memory host code may WRITE (never read back) at this address."""
+        p = _V()
+        call("bcp_dev_alloc_hostwrite", self.h, nbytes, ctypes.byref(p))
         return p.value
 
     def free(self, ptr: int):
@@ -617,7 +624,7 @@ def set_xor_hook(fn_addr: int | None, ctx: int | None = None):
     lib().bcp_task_set_xor_hook(_V(fn_addr) if fn_addr else None, _V(ctx) if ctx else None)
 
 
-FOLD_ZERO_COPY, FOLD_STAGED, FOLD_BATCHED, FOLD_STREAMED = 0, 1, 2, 3
+FOLD_ZERO_COPY, FOLD_STAGED, FOLD_BATCHED, FOLD_STREAMED, FOLD_DEVICE_ROWS = 0, 1, 2, 3, 4
 INJECT_FOLD_RES, INJECT_DRAIN_ROW, INJECT_SEND_BUF, INJECT_THREAD = 1, 2, 4, 8
 
 

@@ -87,7 +87,7 @@ int bcp_task_set_device_map(const int *devices, int ntargets)
 int bcp_task_set_fold_mode(int mode)
 {
     if (mode != BCP_FOLD_ZERO_COPY && mode != BCP_FOLD_STAGED && mode != BCP_FOLD_BATCHED &&
-        mode != BCP_FOLD_STREAMED)
+        mode != BCP_FOLD_STREAMED && mode != BCP_FOLD_DEVICE_ROWS)
         return -EINVAL;
     pthread_mutex_lock(&g_lock);
     int prev = g_fold_mode;
@@ -416,6 +416,7 @@ typedef struct fold_res {
     bcp_engine *eng;
     bcp_queue *q;       /* ZERO_COPY / STAGED only */
     uint8_t *h_win[2];  /* window rows [n][pitch] (pinned + mapped when device >= 0) */
+    int rows_dev;       /* h_win are device memory the host writes (DEVICE_ROWS) */
     uint8_t *h_par;     /* fold output */
     size_t h_cap, h_cap1, hp_cap;
     void *d_src, *d_out;
@@ -441,10 +442,18 @@ static void host_free(fold_res *R, void *p)
         free(p);
 }
 
+static void rows_free(fold_res *R, void *p)
+{
+    if (p && R->rows_dev)
+        bcp_dev_free(R->eng, p);
+    else
+        host_free(R, p);
+}
+
 static void res_destroy(fold_res *R)
 {
-    host_free(R, R->h_win[0]);
-    host_free(R, R->h_win[1]);
+    rows_free(R, R->h_win[0]);
+    rows_free(R, R->h_win[1]);
     host_free(R, R->h_par);
     if (R->device >= 0) {
         if (R->d_src)
@@ -510,11 +519,16 @@ static void res_release(fold_res *R)
     pthread_mutex_unlock(&g_lock);
 }
 
-static int grow(fold_res *R, uint8_t **p, size_t *cap, size_t need)
+/* kind: 0 host (pinned + mapped on a GPU resource), 1 device memory the
+ * host writes (window rows under DEVICE_ROWS) */
+static int grow(fold_res *R, uint8_t **p, size_t *cap, size_t need, int kind)
 {
     if (*cap >= need && *p)
         return 0;
-    host_free(R, *p);
+    if (kind)
+        bcp_dev_free(R->eng, *p);
+    else
+        host_free(R, *p);
     *p = NULL;
     *cap = 0;
     /* next power of two (>= 1 MiB): a worklist sorted by size (gen/main.c:
@@ -523,7 +537,9 @@ static int grow(fold_res *R, uint8_t **p, size_t *cap, size_t need)
     while (c < need)
         c <<= 1;
     int rc = 0;
-    if (R->device >= 0)
+    if (kind)
+        rc = bcp_dev_alloc_hostwrite(R->eng, c, (void **)p);
+    else if (R->device >= 0)
         rc = bcp_host_alloc_mapped(R->eng, c, (void **)p);
     else if (!(*p = malloc(c)))
         rc = -ENOMEM;
@@ -550,8 +566,9 @@ static int grow_dev(fold_res *R, void **p, size_t *cap, size_t need)
 /* Take a resource for storage target st with room for rows_bytes of window
  * rows (twice when `windows` > 1: the next window is received while one is
  * folded; a single-window task needs one set) and an nbytes fold output.
- * use_gpu = 0 under the test hook. */
-static int res_acquire(HostState *hs, int use_gpu, size_t rows_bytes, size_t nbytes, uint64_t windows,
+ * use_gpu = 0 under the test hook; dev_rows: rows in device memory the host
+ * writes (DEVICE_ROWS). */
+static int res_acquire(HostState *hs, int use_gpu, int dev_rows, size_t rows_bytes, size_t nbytes, uint64_t windows,
                        fold_res **out)
 {
     int rc = 0, dev = -1;
@@ -567,9 +584,9 @@ static int res_acquire(HostState *hs, int use_gpu, size_t rows_bytes, size_t nby
     for (fold_res **pp = &g_pool; *pp; pp = &(*pp)->next) {
         if ((*pp)->device != dev)
             continue;
-        if (!best)
+        if (!best || ((*best)->rows_dev != dev_rows && (*pp)->rows_dev == dev_rows))
             best = pp;
-        if ((*pp)->h_cap >= rows_bytes && ((*pp)->h_cap1 >= rows_bytes || windows < 2) && (*pp)->hp_cap >= nbytes) {
+        if ((*pp)->rows_dev == dev_rows && (*pp)->h_cap >= rows_bytes && ((*pp)->h_cap1 >= rows_bytes || windows < 2) && (*pp)->hp_cap >= nbytes) {
             best = pp;
             break;
         }
@@ -588,9 +605,16 @@ static int res_acquire(HostState *hs, int use_gpu, size_t rows_bytes, size_t nby
         R->device = dev;
         R->eng = e;
     }
-    if ((rc = grow(R, &R->h_win[0], &R->h_cap, rows_bytes)) ||
-        (windows > 1 && (rc = grow(R, &R->h_win[1], &R->h_cap1, rows_bytes))) ||
-        (rc = grow(R, &R->h_par, &R->hp_cap, nbytes)))
+    if (R->rows_dev != dev_rows) { /* rows of the other kind: drop them */
+        rows_free(R, R->h_win[0]);
+        rows_free(R, R->h_win[1]);
+        R->h_win[0] = R->h_win[1] = NULL;
+        R->h_cap = R->h_cap1 = 0;
+        R->rows_dev = dev_rows;
+    }
+    if ((rc = grow(R, &R->h_win[0], &R->h_cap, rows_bytes, dev_rows)) ||
+        (windows > 1 && (rc = grow(R, &R->h_win[1], &R->h_cap1, rows_bytes, dev_rows))) ||
+        (rc = grow(R, &R->h_par, &R->hp_cap, nbytes, 0)))
         goto fail;
     *out = R;
     return 0;
@@ -601,7 +625,7 @@ fail:
 
 /* The fold of one window (replaces xor_parity at task_processing.c:211):
  * out = XOR of n rows of `pitch` bytes, nbytes each. */
-static int fold_window(fold_res *R, HostState *hs, bcp_xor_hook_fn hook, void *ctx, const uint8_t *rows,
+static int fold_window(fold_res *R, HostState *hs, int mode, bcp_xor_hook_fn hook, void *ctx, const uint8_t *rows,
                        size_t pitch, const size_t *valid, size_t nbytes, int n, uint8_t *out)
 {
     if (hook) {
@@ -611,10 +635,12 @@ static int fold_window(fold_res *R, HostState *hs, bcp_xor_hook_fn hook, void *c
         return hook(out, nbytes, rows, pitch, n, ctx);
     }
     int rc;
-    pthread_mutex_lock(&g_lock);
-    const int mode = g_fold_mode;
-    pthread_mutex_unlock(&g_lock);
-    if (mode == BCP_FOLD_BATCHED) {
+    if (mode == BCP_FOLD_BATCHED || mode == BCP_FOLD_DEVICE_ROWS) {
+        /* DEVICE_ROWS: the rows were stored through the BAR by other threads
+         * (write-combined); their hand-over to this one passed locked
+         * instructions, and this fence drains this thread's own (a socket
+         * receive copies into the rows on this thread) before the launch */
+        __atomic_thread_fence(__ATOMIC_SEQ_CST);
         fold_svc *S = NULL;
         if ((rc = svc_get(R->device, R->eng, &S)))
             return rc;
@@ -903,6 +929,7 @@ static void parity_generator(const bcp_transport_ops *T, const char *path, const
     pthread_mutex_lock(&g_lock);
     bcp_xor_hook_fn hook = g_hook;
     void *hook_ctx = g_hook_ctx;
+    const int mode = g_fold_mode; /* one mode for the whole task */
     pthread_mutex_unlock(&g_lock);
 
     if (!have_had_error)
@@ -912,9 +939,10 @@ static void parity_generator(const bcp_transport_ops *T, const char *path, const
      * pinned device-mapped rows the GPU folds use, to separate the memory
      * kind from the fold in tools/exp measurements) */
     const int pinned_rows = hook == NULL || getenv("BCP_HOOK_PINNED_ROWS") != NULL;
-    int res_rc = expected_messages
-                     ? res_acquire(hs, pinned_rows, pitch * (size_t)n, buffer_size, expected_messages, &L)
-                     : 0;
+    const int dev_rows = hook == NULL && mode == BCP_FOLD_DEVICE_ROWS;
+    int res_rc = expected_messages ? res_acquire(hs, pinned_rows, dev_rows, pitch * (size_t)n, buffer_size,
+                                                 expected_messages, &L)
+                                   : 0;
     if (res_rc) {
         LOGERR("no fold resources for '%s' on st %d: %s\n", path, hs->storage_target, bcp_strerror(res_rc));
         if (!have_had_error)
@@ -938,13 +966,11 @@ static void parity_generator(const bcp_transport_ops *T, const char *path, const
      * sender's zero padding (chunk_sender reads a chunk up to the size it
      * reported); anything else (rebuild: the survivors' current sizes are
      * not sent; windows past the first: replay) is taken whole. */
-    pthread_mutex_lock(&g_lock);
-    int streamed = g_fold_mode == BCP_FOLD_STREAMED && !hook && !res_rc && expected_messages > 0;
-    pthread_mutex_unlock(&g_lock);
+    int streamed = mode == BCP_FOLD_STREAMED && !hook && !res_rc && expected_messages > 0;
     size_t valid[MAX_STORAGE_TARGETS];
+    const int implicit_pad = !ti.is_rebuilding && expected_messages == 1; /* as chunk_sender decides */
     for (int j = 0; j < n; j++)
-        valid[j] = (!ti.is_rebuilding && expected_messages == 1) ? (size_t)MIN_(chunk_sizes[j], (uint64_t)buffer_size)
-                                                                 : buffer_size;
+        valid[j] = implicit_pad ? (size_t)MIN_(chunk_sizes[j], (uint64_t)buffer_size) : buffer_size;
     if (streamed) {
         int src = L->q ? 0 : bcp_queue_create(L->eng, &L->q);
         if (!src)
@@ -957,6 +983,9 @@ static void parity_generator(const bcp_transport_ops *T, const char *path, const
         }
     }
 
+    /* folds that read whole rows (the test hook, ZERO_COPY, STAGED) */
+    const int pad_rows = implicit_pad && !res_rc &&
+                         (hook != NULL || (mode != BCP_FOLD_BATCHED && mode != BCP_FOLD_DEVICE_ROWS && !streamed));
     phase_add(BCP_PHASE_P_OPEN, &tph);
     if (res_rc) {
         int drc = drain_windows(T, ranks, n, buffer_size, expected_messages, ti.tag);
@@ -995,6 +1024,12 @@ static void parity_generator(const bcp_transport_ops *T, const char *path, const
             int p2 = post_recvs(T, req, n, win_b, pitch, buffer_size, ranks, ti.tag);
             trc = trc ? trc : p2;
         }
+        /* implicit padding (chunk_sender): a fold that reads whole rows gets
+         * the zeros past each chunk here; the others read valid[j] bytes */
+        if (pad_rows)
+            for (int j = 0; j < n; j++)
+                if (valid[j] < buffer_size)
+                    memset(win_a + (size_t)j * pitch + valid[j], 0, buffer_size - valid[j]);
         phase_add(BCP_PHASE_P_ROWS, &tph);
         if (trc && !have_had_error) {
             have_had_error = as_errno(trc);
@@ -1003,7 +1038,7 @@ static void parity_generator(const bcp_transport_ops *T, const char *path, const
         /* fold window msg_i on the GPU while the senders fill win_b */
         if (!have_had_error) {
             int frc = streamed ? stream_fold(L, n, pitch, valid, buffer_size, pblk)
-                               : fold_window(L, hs, hook, hook_ctx, win_a, pitch, valid, buffer_size, n, pblk);
+                               : fold_window(L, hs, mode, hook, hook_ctx, win_a, pitch, valid, buffer_size, n, pblk);
             if (frc) {
                 have_had_error = EIO;
                 LOGERR("GPU fold of '%s' failed: %s\n", path, bcp_strerror(frc));
@@ -1067,16 +1102,37 @@ typedef struct {
     int err;
     HostState *hs;
     const char *path;
+    int implicit_pad; /* produce the chunk's bytes only (chunk_sender) */
 } window_fill;
+
+/* Bytes of the window starting at data_sent that carry the chunk (up to the
+ * size it reported, and never past data_to_send). */
+static size_t window_data_bytes(uint64_t data_to_send, uint64_t fd_size, uint64_t data_sent, size_t n)
+{
+    const uint64_t lim = MIN_(data_to_send, fd_size);
+    return data_sent < lim ? (size_t)MIN_((uint64_t)n, lim - data_sent) : 0;
+}
+
+static void fill_bytes(window_fill *w, uint8_t *data, size_t n);
 
 static int fill_window(void *ctx, void *dst, size_t n)
 {
-    window_fill *w = ctx;
+    fill_bytes(ctx, dst, n);
+    /* dst may be device memory stored through the BAR (DEVICE_ROWS): drain
+     * this thread's write-combining buffers before the window is handed on */
+    __atomic_thread_fence(__ATOMIC_SEQ_CST);
+    return 0;
+}
+
+static void fill_bytes(window_fill *w, uint8_t *data, size_t n)
+{
     HostState *hs = w->hs;
-    uint8_t *data = dst;
+    /* the bytes this window must define: all n, or with implicit padding
+     * the chunk's own (the P role supplies the zeros past them) */
+    const size_t need = w->implicit_pad ? window_data_bytes(w->data_to_send, w->fd_size, w->data_sent, n) : n;
     if (w->err != 0 || w->data_sent >= w->fd_size) {
-        memset(data, 0, n);
-        return 0;
+        memset(data, 0, need);
+        return;
     }
     /* up to the size the chunk reported (not past it should the file have
      * grown since fstat: the parity body then agrees with its header) */
@@ -1084,14 +1140,13 @@ static int fill_window(void *ctx, void *dst, size_t n)
     ssize_t r = read(w->fd, data, (size_t)MIN_((uint64_t)n, left));
     if (r < 0) {
         w->err = errno;
-        memset(data, 0, n);
+        memset(data, 0, need);
         LOGERR("read of '%s' failed with %d (%s) after %llu bytes\n", w->path, errno, strerror(errno),
                (unsigned long long)w->data_sent);
-        return 0;
+        return;
     }
-    if ((size_t)r < n)
-        memset(data + r, 0, n - (size_t)r);
-    return 0;
+    if ((size_t)r < need)
+        memset(data + r, 0, need - (size_t)r);
 }
 
 static void chunk_sender(const bcp_transport_ops *T, const char *path, const FileInfo *task, TaskInfo ti,
@@ -1141,6 +1196,16 @@ static void chunk_sender(const bcp_transport_ops *T, const char *path, const Fil
 
     phase_add(BCP_PHASE_S_SIZES, &tph);
     const size_t buffer_size = (size_t)MIN_(WINDOW, data_to_send);
+    /* Implicit padding: in gen with ONE window (max_cs <= WINDOW) the P role
+     * takes row j's first chunk_sizes[j] bytes and supplies the zeros past
+     * them itself (parity_generator), so the window carries the chunk's
+     * bytes only -- a fill of that many bytes, or a shorter message (an MPI
+     * receive takes a message shorter than its buffer).  The reference pads
+     * every window to buffer_size with zeros (task_processing.c:302-303);
+     * the parity is the same, and the padding (up to 60x the data for a
+     * small chunk in a stripe of large ones) neither crosses PCIe into
+     * device rows nor a socket. */
+    const int implicit_pad = !ti.is_rebuilding && data_to_send <= WINDOW;
     /* Zero copy (a transport with send_fill): every window is read straight
      * into P's window row, unless a later window could replay this one
      * (A3-q1: the file ends before max_cs and more than one window is sent),
@@ -1156,7 +1221,7 @@ static void chunk_sender(const bcp_transport_ops *T, const char *path, const Fil
         }
     }
     if (T->send_fill && (!replay || !data)) {
-        window_fill wf = {fd, fd_size, data_to_send, 0, have_had_error, hs, path};
+        window_fill wf = {fd, fd_size, data_to_send, 0, have_had_error, hs, path, implicit_pad};
         while (wf.data_sent < data_to_send) {
             if (ti.sample)
                 ti.sample->bytes_read += buffer_size;
@@ -1187,22 +1252,24 @@ static void chunk_sender(const bcp_transport_ops *T, const char *path, const Fil
     uint64_t data_sent = 0;
     while (data_sent < data_to_send) {
         uint64_t left = MIN_(data_to_send, fd_size) - data_sent; /* up to the reported size (fill_window) */
+        const size_t msg = implicit_pad ? window_data_bytes(data_to_send, fd_size, data_sent, buffer_size)
+                                        : buffer_size;
         /* once the file is exhausted the previous window is re-sent (A3-q1) */
         if (have_had_error == 0 && data_sent < fd_size) {
             ssize_t r = read(fd, data, (size_t)MIN_((uint64_t)buffer_size, left));
             if (r < 0) {
                 have_had_error = errno;
-                memset(data, 0, buffer_size);
+                memset(data, 0, msg);
                 LOGERR("read of '%s' failed with %d (%s) after %llu bytes\n", path, errno, strerror(errno),
                        (unsigned long long)data_sent);
             }
-            if (r >= 0 && (size_t)r < buffer_size)
-                memset(data + r, 0, buffer_size - (size_t)r);
+            if (r >= 0 && (size_t)r < msg)
+                memset(data + r, 0, msg - (size_t)r);
         }
         if (ti.sample)
             ti.sample->bytes_read += buffer_size;
         data_sent += buffer_size;
-        int e = T->send(T->ctx, data, buffer_size, coordinator, ti.tag);
+        int e = T->send(T->ctx, data, msg, coordinator, ti.tag);
         if (e && !trc)
             trc = e;
     }

@@ -102,11 +102,12 @@ int bcp_task_set_device_map(const int *devices, int ntargets);
  * pinned window rows and writes the pinned parity block in place over PCIe,
  * one launch + one sync per window on the lane's own queue.  STAGED: H2D of
  * the rows, kernel on device buffers, D2H (three commands per window).
- * BATCHED: the window is handed to the device's fold service -- one flusher
- * thread per GPU gathers the windows every P role of every rank has pending
- * into ONE descriptor batch (zero-copy rows), launches it and wakes each
- * lane when its own window is done (process_task stays synchronous per task,
- * as the reference's window loop is, task_processing.c:203-226).  Returns the
+ * BATCHED: the window is handed to the device's fold service (flat
+ * combining, no thread of its own): a waiting lane leads a launch that folds
+ * EVERY window the P roles of this process have pending as ONE descriptor
+ * batch (zero-copy rows, data bytes only) and wakes each lane when its own
+ * window is done (process_task stays synchronous per task, as the
+ * reference's window loop is, task_processing.c:203-226).  Returns the
  * previous mode, or -EINVAL. */
 #define BCP_FOLD_ZERO_COPY 0
 #define BCP_FOLD_STAGED 1
@@ -118,6 +119,14 @@ int bcp_task_set_device_map(const int *devices, int ntargets);
  * HBM (padding implicit, never transferred) straight into the pinned output
  * block, then one sync.  PCIe carries the chunk bytes once, not the padding. */
 #define BCP_FOLD_STREAMED 3
+/* DEVICE_ROWS: the window rows themselves live in device memory the host
+ * writes through the GPU's BAR (bcp_dev_alloc_hostwrite): the senders' chunk
+ * reads (or the transport's receive copies) store straight into HBM, so the
+ * row bytes cross PCIe once, as CPU stores, while they arrive; the fold is
+ * then an HBM-rate kernel (the fold service's batch, data bytes only) whose
+ * output block goes to pinned host memory for the parity write.  No host
+ * code reads the rows. */
+#define BCP_FOLD_DEVICE_ROWS 4
 int bcp_task_set_fold_mode(int mode);
 /* BATCHED mode: how many batches may be on a device at once (1..16, each
  * led by one waiting lane on its own queue; default 1: pure flat

@@ -23,11 +23,11 @@ def gpu_fold(bcp, engine):
     bcp.task_shutdown()
 
 
-@pytest.fixture(params=["streamed", "batched", "zero_copy", "staged"])
+@pytest.fixture(params=["device_rows", "streamed", "batched", "zero_copy", "staged"])
 def fold_mode(request, bcp):
     """Every form of the P role's GPU fold (bcp_task_set_fold_mode)."""
     mode = {"batched": bcp.FOLD_BATCHED, "zero_copy": bcp.FOLD_ZERO_COPY, "staged": bcp.FOLD_STAGED,
-            "streamed": bcp.FOLD_STREAMED}[request.param]
+            "streamed": bcp.FOLD_STREAMED, "device_rows": bcp.FOLD_DEVICE_ROWS}[request.param]
     prev = bcp.set_fold_mode(mode)
     yield request.param
     bcp.set_fold_mode(prev)
@@ -204,14 +204,17 @@ def test_protocol_repeated_runs_reuse_pool(bcp, oracle, tmp_path):
 
 
 def test_zero_copy_pool_reuse_with_changing_data(bcp, oracle, tmp_path):
-    """The pooled mapped window rows are rewritten between runs and between
-    modes: no fold may see a previous task's bytes."""
+    """The pooled window rows (mapped host memory, or device memory the host
+    writes) are rewritten between runs and the pool switches row kinds
+    between modes: no fold may see a previous task's bytes."""
     root = str(tmp_path)
     rng = np.random.default_rng(77)
-    for rnd in range(4):
+    modes = [bcp.FOLD_ZERO_COPY, bcp.FOLD_DEVICE_ROWS, bcp.FOLD_STAGED, bcp.FOLD_DEVICE_ROWS, bcp.FOLD_DEVICE_ROWS,
+             bcp.FOLD_BATCHED]
+    for rnd, mode in enumerate(modes):
         files = [(f"z/{i}", [0, 1, 2], 3, [int(x) for x in rng.integers(1, 600_000, size=3)]) for i in range(24)]
         items, contents = S.populate(root, 4, files, seed=100 + rnd)
-        prev = bcp.set_fold_mode(bcp.FOLD_STAGED if rnd % 2 else bcp.FOLD_ZERO_COPY)
+        prev = bcp.set_fold_mode(mode)
         try:
             st = bcp.gen_run(root, 4, items, nlanes=6)
         finally:
@@ -291,13 +294,14 @@ def test_db_round_then_partial_round_then_rebuild(bcp, oracle, tmp_path, engine_
         assert S.read_file(S.chunk_path(root, victim, path)) == data, path
 
 
-@pytest.mark.parametrize("engine_kind", ["protocol", "pipeline", "procs"])
+@pytest.mark.parametrize("engine_kind", ["protocol", "pipeline", "procs", "procs_device_rows"])
 def test_cli_complete_partial_rebuild(bcp, oracle, tmp_path, engine_kind):
     """bin/bcp end to end on the device: --complete (scan of every target),
     --partial from changelog record files, then parity-rebuild from the DB --
     ranks as threads, the batched pipeline, or ranks as processes (--procs:
     one forked process per target on the socketpair transport, each with its
-    own HIP context, P roles folding with the streamed GPU fold)."""
+    own HIP context, P roles folding with the streamed GPU fold, or with rows
+    in device memory that the socket receives write)."""
     import subprocess
     import planner as PL
     rng = np.random.default_rng(21)
@@ -313,7 +317,8 @@ def test_cli_complete_partial_rebuild(bcp, oracle, tmp_path, engine_kind):
             S.write_chunk(root, h, path, d)
             arrs.append(d)
         files[path], contents[path] = holders, arrs
-    flags = {"protocol": [], "pipeline": ["--pipeline"], "procs": ["--procs", "--fold", "streamed"]}[engine_kind]
+    flags = {"protocol": [], "pipeline": ["--pipeline"], "procs": ["--procs", "--fold", "streamed"],
+             "procs_device_rows": ["--procs", "--fold", "device-rows"]}[engine_kind]
     r = subprocess.run([bcp.BIN_PATH, "parity-gen", "--complete", *flags, root, str(nt)], capture_output=True)
     assert r.returncode == 0, r.stderr
     db = bcp.PDB(os.path.join(root, "st0", "db"))

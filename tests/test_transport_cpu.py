@@ -84,6 +84,33 @@ def test_rank_processes_multiwindow_replay(bcp, oracle, cpu_hook, tmp_path):
         assert S.read_file(S.parity_path(root, p, path)) == oracle.gen_parity_file(contents[path]), path
 
 
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("procs", [False, True], ids=["threads", "rank-processes"])
+def test_implicit_padding_never_folds_stale_row_bytes(bcp, oracle, cpu_hook, tmp_path, procs):
+    """Gen with one window: sources send their chunk's bytes only (a shorter
+    message on the socket transport, a shorter fill on the loopback) and the
+    P role supplies the zeros past each chunk.  Large chunks first, then the
+    same stripes with small / empty chunks next to large ones, so the reused
+    window rows hold stale bytes exactly where the padding belongs."""
+    rng = np.random.default_rng(31)
+    root = str(tmp_path)
+    ntargets = 6
+    run = bcp.gen_run_procs if procs else bcp.gen_run
+    big = []
+    for i in range(30):
+        holders, p = S.random_layout(rng, ntargets, 4)
+        big.append((f"s/{i}", holders, p, [int(x) for x in rng.integers(700_000, 900_000, size=4)]))
+    items, contents = S.populate(root, ntargets, big, seed=1)
+    assert run(root, ntargets, items, nlanes=4).errors == 0
+    small = [(path, holders, p, [int(rng.choice([0, 1, 17, 4096, 333_333])), 850_000,
+                                 int(rng.integers(0, 5000)), 3])
+             for (path, holders, p, _) in big]
+    items, contents = S.populate(root, ntargets, small, seed=2)
+    assert run(root, ntargets, items, nlanes=4).errors == 0
+    for (path, holders, p, lens) in small:
+        assert S.read_file(S.parity_path(root, p, path)) == oracle.gen_parity_file(contents[path]), path
+
+
 def test_explicit_loopback_transport_and_validation(bcp, oracle, cpu_hook, tmp_path):
     import ctypes
     L = bcp.lib()

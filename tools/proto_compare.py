@@ -8,6 +8,9 @@ interleaved in ONE run on ONE box:
   gpu_staged     H2D -> kernel -> D2H per window
   gpu_streamed   each row's data bytes DMA'd to HBM as it arrives, one kernel
                  from HBM into the pinned output
+  gpu_device_rows  the rows themselves in device memory the host writes
+                 (BCP_FOLD_DEVICE_ROWS): chunk reads store into HBM through
+                 the BAR, the fold service's kernel reads HBM
   cpu_reference  the reference's xor_parity restated (oracle_xor_rows) as the
                  fold: the reference CPU path
   noop           a fold that does nothing: the bound of the protocol itself
@@ -78,7 +81,8 @@ def fold_setup(fold, hooks):
         return restore
     if fold.startswith("gpu_"):
         mode = {"gpu_batched": bcp.FOLD_BATCHED, "gpu_zero_copy": bcp.FOLD_ZERO_COPY,
-                "gpu_staged": bcp.FOLD_STAGED, "gpu_streamed": bcp.FOLD_STREAMED}[fold]
+                "gpu_staged": bcp.FOLD_STAGED, "gpu_streamed": bcp.FOLD_STREAMED,
+                "gpu_device_rows": bcp.FOLD_DEVICE_ROWS}[fold]
         prev = bcp.set_fold_mode(mode)
         return lambda: bcp.set_fold_mode(prev)
     bcp.set_xor_hook(hooks[fold])
@@ -156,7 +160,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--root", default="/dev/shm/bcp_proto")
     ap.add_argument("--rounds", type=int, default=6)
-    ap.add_argument("--folds", default="gpu_streamed,gpu_batched,gpu_zero_copy,cpu_reference,noop")
+    ap.add_argument("--folds", default="gpu_device_rows,gpu_streamed,gpu_batched,cpu_reference,noop")
     ap.add_argument("--workloads", default="c1_gen,c1_rebuild,c5_gen")
     ap.add_argument("--c1-files", type=int, default=1333)
     ap.add_argument("--c5-stripes", type=int, default=1000)
