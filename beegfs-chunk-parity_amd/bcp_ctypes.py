@@ -117,6 +117,7 @@ _SIGS = {
     "bcp_task_shutdown": ([], ctypes.c_int),
     "bcp_task_set_xor_hook": ([_V, _V], None),
     "bcp_task_set_fold_mode": ([ctypes.c_int], ctypes.c_int),
+    "bcp_task_set_explicit_padding": ([ctypes.c_int], ctypes.c_int),
     "bcp_task_set_fold_inflight": ([ctypes.c_int], ctypes.c_int),
     "bcp_task_fold_stats": ([ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)], ctypes.c_int),
     "bcp_task_inject_failure": ([ctypes.c_int, ctypes.c_int, ctypes.c_int], ctypes.c_int),
@@ -629,11 +630,21 @@ INJECT_FOLD_RES, INJECT_DRAIN_ROW, INJECT_SEND_BUF, INJECT_THREAD = 1, 2, 4, 8
 
 
 def set_fold_mode(mode: int) -> int:
-    """P-role fold: FOLD_BATCHED (default), FOLD_ZERO_COPY or FOLD_STAGED; returns the previous mode."""
+    """P-role fold: FOLD_BATCHED (default), FOLD_DEVICE_ROWS, FOLD_STREAMED, FOLD_ZERO_COPY or
+    FOLD_STAGED; returns the previous mode."""
     rc = lib().bcp_task_set_fold_mode(mode)
     if rc < 0:
         raise BcpError("bcp_task_set_fold_mode", rc)
     return rc
+
+
+def set_explicit_padding(on: bool) -> bool:
+    """Sources zero-pad every window as the reference does (True) or send a
+    one-window gen chunk's bytes only (False, default); returns the previous."""
+    rc = lib().bcp_task_set_explicit_padding(int(bool(on)))
+    if rc < 0:
+        raise BcpError("bcp_task_set_explicit_padding", rc)
+    return bool(rc)
 
 
 def task_shutdown():

@@ -65,6 +65,7 @@ static int g_devmap_n = 0;
 static bcp_xor_hook_fn g_hook = NULL;
 static void *g_hook_ctx = NULL;
 static int g_fold_mode = BCP_FOLD_BATCHED;
+static int g_explicit_pad = 0; /* 1: sources pad every window, as the reference does */
 static bcp_transport_ops g_tp;
 static int g_tp_set = 0;
 
@@ -94,6 +95,13 @@ int bcp_task_set_fold_mode(int mode)
     g_fold_mode = mode;
     pthread_mutex_unlock(&g_lock);
     return prev;
+}
+
+int bcp_task_set_explicit_padding(int on)
+{
+    if (on != 0 && on != 1)
+        return -EINVAL;
+    return __atomic_exchange_n(&g_explicit_pad, on, __ATOMIC_ACQ_REL);
 }
 
 void bcp_task_set_xor_hook(bcp_xor_hook_fn fn, void *ctx)
@@ -1205,7 +1213,8 @@ static void chunk_sender(const bcp_transport_ops *T, const char *path, const Fil
      * the parity is the same, and the padding (up to 60x the data for a
      * small chunk in a stripe of large ones) neither crosses PCIe into
      * device rows nor a socket. */
-    const int implicit_pad = !ti.is_rebuilding && data_to_send <= WINDOW;
+    const int implicit_pad =
+        !ti.is_rebuilding && data_to_send <= WINDOW && !__atomic_load_n(&g_explicit_pad, __ATOMIC_ACQUIRE);
     /* Zero copy (a transport with send_fill): every window is read straight
      * into P's window row, unless a later window could replay this one
      * (A3-q1: the file ends before max_cs and more than one window is sent),

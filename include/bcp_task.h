@@ -128,6 +128,13 @@ int bcp_task_set_device_map(const int *devices, int ntargets);
  * code reads the rows. */
 #define BCP_FOLD_DEVICE_ROWS 4
 int bcp_task_set_fold_mode(int mode);
+/* on = 0 (default): in a gen task with ONE window a source sends its
+ * chunk's bytes only and the P role supplies the zeros past them (implicit
+ * padding).  on = 1: the reference's wire exactly -- every window
+ * zero-padded to buffer_size (task_processing.c:302-303) -- for a job whose
+ * P roles run the reference's parity_generator.  The P role of this library
+ * takes either.  Returns the previous value or -EINVAL. */
+int bcp_task_set_explicit_padding(int on);
 /* BATCHED mode: how many batches may be on a device at once (1..16, each
  * led by one waiting lane on its own queue; default 1: pure flat
  * combining).  Returns the

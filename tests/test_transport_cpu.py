@@ -85,13 +85,23 @@ def test_rank_processes_multiwindow_replay(bcp, oracle, cpu_hook, tmp_path):
 
 
 @pytest.mark.timeout(300)
+@pytest.mark.parametrize("explicit", [False, True], ids=["implicit-pad", "reference-wire"])
 @pytest.mark.parametrize("procs", [False, True], ids=["threads", "rank-processes"])
-def test_implicit_padding_never_folds_stale_row_bytes(bcp, oracle, cpu_hook, tmp_path, procs):
+def test_implicit_padding_never_folds_stale_row_bytes(bcp, oracle, cpu_hook, tmp_path, procs, explicit):
     """Gen with one window: sources send their chunk's bytes only (a shorter
     message on the socket transport, a shorter fill on the loopback) and the
     P role supplies the zeros past each chunk.  Large chunks first, then the
     same stripes with small / empty chunks next to large ones, so the reused
-    window rows hold stale bytes exactly where the padding belongs."""
+    window rows hold stale bytes exactly where the padding belongs.  Also
+    with the reference's wire restored (bcp_task_set_explicit_padding)."""
+    prev = bcp.set_explicit_padding(explicit)
+    try:
+        _padding_rounds(bcp, oracle, tmp_path, procs)
+    finally:
+        bcp.set_explicit_padding(prev)
+
+
+def _padding_rounds(bcp, oracle, tmp_path, procs):
     rng = np.random.default_rng(31)
     root = str(tmp_path)
     ntargets = 6
