@@ -128,6 +128,12 @@ _SIGS = {
                            ctypes.POINTER(ctypes.c_int), _V, ctypes.POINTER(RunStats)], ctypes.c_int),
     "bcp_rebuild_run_procs": ([ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.POINTER(WorkItem), ctypes.c_size_t,
                                ctypes.c_char_p, _V, ctypes.POINTER(RunStats)], ctypes.c_int),
+    "bcp_rank_pool_create": ([ctypes.c_int, _V, ctypes.POINTER(_V)], ctypes.c_int),
+    "bcp_rank_pool_gen": ([_V, ctypes.c_char_p, ctypes.POINTER(WorkItem), ctypes.c_size_t, ctypes.c_int,
+                           ctypes.POINTER(ctypes.c_int), ctypes.POINTER(RunStats)], ctypes.c_int),
+    "bcp_rank_pool_rebuild": ([_V, ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(WorkItem), ctypes.c_size_t,
+                               ctypes.c_char_p, ctypes.POINTER(RunStats)], ctypes.c_int),
+    "bcp_rank_pool_destroy": ([_V], ctypes.c_int),
     "bcp_assign_lanes": ([ctypes.c_int, ctypes.c_uint64, ctypes.POINTER(FileInfo), ctypes.POINTER(ctypes.c_int)], None),
     "bcp_gen_run": ([ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(WorkItem), ctypes.c_size_t, ctypes.c_int,
                      ctypes.POINTER(ctypes.c_int), _V, ctypes.POINTER(RunStats)], ctypes.c_int),
@@ -475,6 +481,47 @@ def rebuild_run_procs(store_root: str, ntargets: int, rebuild_target: int, items
     check("bcp_rebuild_run_procs", rc)
     del keep
     return st
+
+
+class RankPool:
+    """Rank processes kept alive across runs (bcp_rank_pool_*): one forked
+    process per storage target; each run takes this process's P-role settings
+    at call time.  Create it before this process touches the GPU."""
+
+    def __init__(self, ntargets: int, log=None):
+        h = _V()
+        check("bcp_rank_pool_create", lib().bcp_rank_pool_create(ntargets, log, ctypes.byref(h)))
+        self.h = h
+        self.ntargets = ntargets
+
+    def gen(self, store_root: str, items, nlanes: int = 12, lanes=None) -> RunStats:
+        arr, keep = _items(items)
+        st = RunStats()
+        ln = (ctypes.c_int * max(len(lanes), 1))(*lanes) if lanes is not None else None
+        rc = lib().bcp_rank_pool_gen(self.h, store_root.encode(), arr, len(items), nlanes, ln, ctypes.byref(st))
+        check("bcp_rank_pool_gen", rc)
+        del keep
+        return st
+
+    def rebuild(self, store_root: str, rebuild_target: int, items, corrupt_list: str | None = None) -> RunStats:
+        arr, keep = _items(items)
+        st = RunStats()
+        rc = lib().bcp_rank_pool_rebuild(self.h, store_root.encode(), rebuild_target, arr, len(items),
+                                         corrupt_list.encode() if corrupt_list else None, ctypes.byref(st))
+        check("bcp_rank_pool_rebuild", rc)
+        del keep
+        return st
+
+    def close(self):
+        if self.h:
+            h, self.h = self.h, None
+            check("bcp_rank_pool_destroy", lib().bcp_rank_pool_destroy(h))
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
 
 
 def gen_run_db(store_root: str, ntargets: int, items, nlanes: int = 12, lanes=None, log=None) -> RunStats:

@@ -10,3 +10,14 @@ int bcpi_inject_hit(int site);
 /* Non-zero once this library initialised a HIP runtime that found a device
  * (bcp_engine.hip): a forked child could not use it. */
 int bcpi_hip_touched(void);
+
+/* The P-role settings of this process (fold mode, fold service width, test
+ * hook, window padding): a rank pool (bcp_runner.c) hands the caller's
+ * settings to its rank processes with every run. */
+typedef struct {
+    int fold_mode, fold_inflight, explicit_pad;
+    bcp_xor_hook_fn hook;
+    void *hook_ctx;
+} bcpi_settings;
+void bcpi_settings_get(bcpi_settings *s);
+int bcpi_settings_apply(const bcpi_settings *s);

@@ -30,6 +30,9 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <dlfcn.h>
+#include <poll.h>
+#include <sys/socket.h>
 #include <sys/stat.h>
 #include <sys/wait.h>
 #include <time.h>
@@ -653,44 +656,77 @@ int bcp_gen_round_pipeline(bcp_pipeline *pl, const char *store_root, int ntarget
     return round_impl(pl, 0, store_root, ntargets, events, cum_weight, 0, log, stats, nplanned);
 }
 
-/* ---- ranks as processes (bcp_gen_run_procs / bcp_rebuild_run_procs) -------
+/* ---- ranks as processes: the rank pool -----------------------------------
  * One forked process per storage target, connected by a bcp_sock_world --
  * the shape of the reference's deployment (one MPI process per target,
- * src/beegfs-parity-gen:114-127).  Children wait on a start pipe, so a failed
- * fork cancels the run before any rank has begun a task; each child reports
- * its counters through a result pipe (one record < PIPE_BUF: atomic). */
+ * src/beegfs-parity-gen:114-127).  A pool forks its ranks ONCE; every run is
+ * a command sent to each rank over its own socketpair (the work items, the
+ * lanes and the caller's P-role settings), and each rank answers with one
+ * record on a shared result pipe (< PIPE_BUF: atomic).  A rank keeps its HIP
+ * engine, fold service and registered window rows from run to run, as a
+ * long-lived MPI rank does.  A rank whose run cannot start (store missing,
+ * a lane thread not created) reports and exits: its partners see its
+ * sockets close and fail the tasks they share with it, and the pool is
+ * broken (-EPIPE for later runs).  bcp_gen_run_procs / bcp_rebuild_run_procs
+ * are one-run pools. */
 typedef struct {
     int rank;
     int error;        /* the rank's sticky error at the end */
-    int rc;           /* setup failure inside the child, 0 = ran */
+    int rc;           /* 0 = ran; < 0: the run could not start (the rank exits) */
+    uint64_t seq;     /* the command answered */
     uint64_t tasks, bytes_read, bytes_written;
 } rank_report;
 
+#define POOL_MAGIC 0x62637072u /* "bcpr" */
+enum { POOL_GEN = 1, POOL_REBUILD = 2, POOL_QUIT = 3 };
+
+typedef struct {
+    uint32_t magic, op;
+    int32_t nlanes, rebuild_target, has_lanes;
+    bcpi_settings settings;
+    uint64_t seq, nitems, root_len, corrupt_len, paths_len;
+} pool_cmd;
+
+struct bcp_rank_pool {
+    int ntargets;
+    pid_t pids[MAX_STORAGE_TARGETS]; /* -1 once reaped */
+    int cmd_fd[MAX_STORAGE_TARGETS];
+    int res_fd;
+    int broken;
+    uint64_t seq;
+    FILE *log;
+};
+
 typedef struct {
     const char *root;
-    int ntargets, nlanes, rebuilding, rebuild_target, corrupt_fd;
+    int nlanes, rebuilding, rebuild_target, corrupt_fd;
     const bcp_work_item *items;
     size_t nitems;
     const int *lanes;
     FILE *log;
 } procs_job;
 
-/* The body of rank process k+1 (never returns). */
-static void rank_child(const procs_job *J, bcp_sock_world *w, int k, int go_fd, int res_fd)
+static int io_full(int fd, void *buf, size_t n, int writing)
 {
-    rank_report rep = {k + 1, 0, 0, 0, 0, 0};
-    char go = 0;
-    ssize_t g = read(go_fd, &go, 1); /* EOF: the run was cancelled */
-    close(go_fd);
-    if (g != 1)
-        _exit(0);
-    bcp_transport_ops ops;
+    uint8_t *p = buf;
+    while (n) {
+        ssize_t r = writing ? send(fd, p, n, MSG_NOSIGNAL) : read(fd, p, n);
+        if (r < 0 && errno == EINTR)
+            continue;
+        if (r <= 0)
+            return r == 0 ? -EPIPE : -errno;
+        p += r;
+        n -= (size_t)r;
+    }
+    return 0;
+}
+
+/* One run of rank k+1 inside its process (the lanes of gen, or the single
+ * rebuild lane).  rep->rc < 0 if the run could not start. */
+static void rank_run(const procs_job *J, int k, rank_report *rep)
+{
     HostState hs;
-    int rc = bcp_sock_world_attach(w, k + 1, &ops);
-    if (!rc)
-        rc = bcp_task_set_transport(&ops);
-    if (!rc)
-        rc = open_store(J->root, k, J->rebuilding, J->corrupt_fd, J->log, &hs);
+    int rc = open_store(J->root, k, J->rebuilding, J->corrupt_fd, J->log, &hs);
     if (!rc && !J->rebuilding) {
         lane_arg *args = calloc((size_t)J->nlanes, sizeof(lane_arg));
         pthread_t *th = calloc((size_t)J->nlanes, sizeof(pthread_t));
@@ -703,16 +739,13 @@ static void rank_child(const procs_job *J, bcp_sock_world *w, int k, int go_fd, 
             if ((src = spawn(&th[l], gen_lane, &args[l])) == 0)
                 started++;
         }
-        /* A rank whose lanes cannot all start fails as a whole: its lanes
-         * are released without work, the process exits, and its partners see
-         * its sockets close and fail the tasks they share with it. */
-        gate_open(&gate, src != 0);
+        gate_open(&gate, src != 0); /* all lanes or none */
         for (int l = 0; l < started; l++)
             pthread_join(th[l], NULL);
         for (int l = 0; l < started && !src; l++) {
-            rep.tasks += args[l].tasks;
-            rep.bytes_read += args[l].sample.bytes_read;
-            rep.bytes_written += args[l].sample.bytes_written;
+            rep->tasks += args[l].tasks;
+            rep->bytes_read += args[l].sample.bytes_read;
+            rep->bytes_written += args[l].sample.bytes_written;
         }
         rc = src ? -src : 0;
         free(args);
@@ -720,118 +753,309 @@ static void rank_child(const procs_job *J, bcp_sock_world *w, int k, int go_fd, 
     } else if (!rc) {
         rebuild_arg a = {&hs, J->items, J->nitems, J->rebuild_target, k + 1, NULL, PROGRESS_SAMPLE_INIT, 0};
         rebuild_rank(&a);
-        rep.tasks = a.tasks;
-        rep.bytes_read = a.sample.bytes_read;
-        rep.bytes_written = a.sample.bytes_written;
+        rep->tasks = a.tasks;
+        rep->bytes_read = a.sample.bytes_read;
+        rep->bytes_written = a.sample.bytes_written;
     }
     if (!rc) {
-        rep.error = hs.error;
+        rep->error = hs.error;
         close_store(&hs, J->rebuilding);
     }
-    rep.rc = rc;
-    bcp_task_shutdown();
-    ssize_t wr = write(res_fd, &rep, sizeof(rep));
-    (void)wr;
-    close(res_fd);
-    bcp_sock_world_destroy(w);
-    _exit(rc ? 2 : 0);
+    rep->rc = rc;
 }
 
-static int run_procs(const procs_job *J, bcp_run_stats *stats)
+/* Read one command's payload and run it; returns the report. */
+static void rank_command(const pool_cmd *c, int cmd_fd, int k, FILE *log, rank_report *rep)
 {
+    char *root = NULL, *corrupt = NULL, *paths = NULL;
+    FileInfo *fis = NULL;
+    uint32_t *plen = NULL;
+    int32_t *lanes = NULL;
+    bcp_work_item *items = NULL;
+    const size_t n = (size_t)c->nitems;
+    int rc = 0;
+    if (c->root_len == 0 || c->root_len > 4096 || c->corrupt_len > 4096 || c->nitems > ((uint64_t)1 << 32) ||
+        c->paths_len > ((uint64_t)1 << 40)) {
+        rep->rc = -EPROTO;
+        return;
+    }
+    root = calloc(c->root_len + 1, 1);
+    corrupt = calloc(c->corrupt_len + 1, 1);
+    paths = malloc(c->paths_len + n + 1);
+    fis = malloc((n ? n : 1) * sizeof(FileInfo));
+    plen = malloc((n ? n : 1) * sizeof(uint32_t));
+    lanes = c->has_lanes ? malloc((n ? n : 1) * sizeof(int32_t)) : NULL;
+    items = malloc((n ? n : 1) * sizeof(bcp_work_item));
+    if (!root || !corrupt || !paths || !fis || !plen || !items || (c->has_lanes && !lanes))
+        rc = -ENOMEM;
+    /* a rank that cannot take its command whole (the channel would be out
+     * of step) reports and exits like any rank whose run cannot start */
+    if (!rc)
+        rc = io_full(cmd_fd, root, c->root_len, 0);
+    if (!rc && c->corrupt_len)
+        rc = io_full(cmd_fd, corrupt, c->corrupt_len, 0);
+    if (!rc)
+        rc = io_full(cmd_fd, fis, n * sizeof(FileInfo), 0);
+    if (!rc)
+        rc = io_full(cmd_fd, plen, n * sizeof(uint32_t), 0);
+    /* paths packed back to back; each gets its NUL here */
+    uint64_t total = 0;
+    for (size_t i = 0; !rc && i < n; i++)
+        total += plen[i];
+    if (!rc && total != c->paths_len)
+        rc = -EPROTO;
+    for (size_t i = 0, off = 0; !rc && i < n; i++) {
+        rc = io_full(cmd_fd, paths + off, plen[i], 0);
+        paths[off + plen[i]] = 0;
+        items[i] = (bcp_work_item){paths + off, fis[i]};
+        off += plen[i] + 1;
+    }
+    if (!rc && c->has_lanes)
+        rc = io_full(cmd_fd, lanes, n * sizeof(int32_t), 0);
+    int corrupt_fd = -1;
+    if (!rc && c->op == POOL_REBUILD) {
+        corrupt_fd = c->corrupt_len ? open(corrupt, O_WRONLY | O_CREAT | O_APPEND, S_IRUSR | S_IWUSR)
+                                    : open("/dev/null", O_WRONLY);
+        if (corrupt_fd < 0)
+            rc = -errno;
+    }
+    /* a hook is a function of the caller's process: usable here only if it
+     * was mapped when the pool forked */
+    Dl_info dl;
+    if (!rc && c->settings.hook && !dladdr((void *)c->settings.hook, &dl))
+        rc = -EFAULT;
+    if (!rc)
+        rc = bcpi_settings_apply(&c->settings);
+    if (!rc) {
+        procs_job J = {root, c->nlanes, c->op == POOL_REBUILD, c->rebuild_target, corrupt_fd, items, n,
+                       (const int *)lanes, log};
+        rank_run(&J, k, rep);
+    } else {
+        rep->rc = rc;
+    }
+    if (corrupt_fd >= 0)
+        close(corrupt_fd);
+    free(root);
+    free(corrupt);
+    free(paths);
+    free(fis);
+    free(plen);
+    free(lanes);
+    free(items);
+}
+
+/* The body of rank process k+1 (never returns): serve commands until QUIT
+ * or the caller's end closes. */
+static void rank_main(bcp_sock_world *w, int k, int cmd_fd, int res_fd, FILE *log)
+{
+    bcp_transport_ops ops;
+    int arc = bcp_sock_world_attach(w, k + 1, &ops);
+    if (!arc)
+        arc = bcp_task_set_transport(&ops);
+    for (;;) {
+        pool_cmd c;
+        if (io_full(cmd_fd, &c, sizeof(c), 0) || c.magic != POOL_MAGIC || c.op == POOL_QUIT)
+            break;
+        rank_report rep = {k + 1, 0, 0, c.seq, 0, 0, 0};
+        if (arc)
+            rep.rc = arc;
+        else
+            rank_command(&c, cmd_fd, k, log, &rep);
+        ssize_t wr = write(res_fd, &rep, sizeof(rep));
+        (void)wr;
+        if (rep.rc)
+            break; /* the run could not start: leave, so partners fail fast */
+    }
+    bcp_task_shutdown();
+    close(res_fd);
+    close(cmd_fd);
+    bcp_sock_world_destroy(w);
+    _exit(0);
+}
+
+int bcp_rank_pool_create(int ntargets, FILE *log, bcp_rank_pool **out)
+{
+    if (!out || ntargets < 1 || ntargets > MAX_STORAGE_TARGETS)
+        return -EINVAL;
+    *out = NULL;
     if (bcpi_hip_touched())
         return -EBUSY; /* children could not use the HIP runtime of this process */
-    for (int k = 0; k < MAX_STORAGE_TARGETS; k++)
-        st2rank[k] = k < J->ntargets ? k + 1 : -1;
-    bcp_sock_world *w = NULL;
-    int rc = bcp_sock_world_create(J->ntargets + 1, &w);
-    if (rc)
-        return rc;
-    int go[2] = {-1, -1}, res[2] = {-1, -1};
-    pid_t *pids = calloc((size_t)J->ntargets, sizeof(pid_t));
-    if (!pids || pipe(go) != 0 || pipe(res) != 0) {
-        rc = pids ? -errno : -ENOMEM;
-        goto out;
+    bcp_rank_pool *P = calloc(1, sizeof(*P));
+    if (!P)
+        return -ENOMEM;
+    P->ntargets = ntargets;
+    P->log = log;
+    P->res_fd = -1;
+    for (int k = 0; k < MAX_STORAGE_TARGETS; k++) {
+        P->pids[k] = -1;
+        P->cmd_fd[k] = -1;
+        st2rank[k] = k < ntargets ? k + 1 : -1; /* inherited by the ranks */
     }
-    if (J->log)
-        fflush(J->log);
+    bcp_sock_world *w = NULL;
+    int rc = bcp_sock_world_create(ntargets + 1, &w);
+    int res[2] = {-1, -1};
+    if (!rc && pipe(res) != 0)
+        rc = -errno;
+    if (rc) {
+        if (w)
+            bcp_sock_world_destroy(w);
+        free(P);
+        return rc;
+    }
+    if (log)
+        fflush(log);
     fflush(stdout);
     fflush(stderr);
-    int nforked = 0;
-    for (int k = 0; k < J->ntargets; k++) {
-        pid_t pid = fork();
-        if (pid == 0) {
-            close(go[1]);
-            close(res[0]);
-            rank_child(J, w, k, go[0], res[1]);
-        }
-        if (pid < 0) {
+    for (int k = 0; k < ntargets && !rc; k++) {
+        int sv[2];
+        if (socketpair(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC, 0, sv) != 0) {
             rc = -errno;
             break;
         }
-        pids[nforked++] = pid;
+        pid_t pid = fork();
+        if (pid == 0) {
+            close(sv[0]);
+            close(res[0]);
+            for (int j = 0; j < k; j++)
+                close(P->cmd_fd[j]); /* the other ranks' command channels */
+            rank_main(w, k, sv[1], res[1], log);
+        }
+        close(sv[1]);
+        if (pid < 0) {
+            rc = -errno;
+            close(sv[0]);
+            break;
+        }
+        P->pids[k] = pid;
+        P->cmd_fd[k] = sv[0];
     }
-    close(go[0]);
     close(res[1]);
-    go[0] = res[1] = -1;
+    P->res_fd = res[0];
     bcp_sock_world_destroy(w); /* the ranks hold their own ends now */
-    w = NULL;
+    if (rc) {
+        bcp_rank_pool_destroy(P);
+        return rc;
+    }
+    *out = P;
+    return 0;
+}
+
+static int pool_run(bcp_rank_pool *P, int op, const char *root, const bcp_work_item *items, size_t nitems,
+                    int nlanes, const int *lanes, int rebuild_target, const char *corrupt, bcp_run_stats *stats)
+{
+    if (P->broken)
+        return -EPIPE;
+    pool_cmd c;
+    memset(&c, 0, sizeof(c));
+    c.magic = POOL_MAGIC;
+    c.op = (uint32_t)op;
+    c.nlanes = nlanes;
+    c.rebuild_target = rebuild_target;
+    c.has_lanes = lanes != NULL;
+    bcpi_settings_get(&c.settings);
+    c.seq = ++P->seq;
+    c.nitems = nitems;
+    c.root_len = strlen(root);
+    c.corrupt_len = corrupt ? strlen(corrupt) : 0;
+    FileInfo *fis = malloc((nitems ? nitems : 1) * sizeof(FileInfo));
+    uint32_t *plen = malloc((nitems ? nitems : 1) * sizeof(uint32_t));
+    int32_t *ln = lanes ? malloc((nitems ? nitems : 1) * sizeof(int32_t)) : NULL;
+    if (!fis || !plen || (lanes && !ln)) {
+        free(fis);
+        free(plen);
+        free(ln);
+        return -ENOMEM;
+    }
+    for (size_t i = 0; i < nitems; i++) {
+        fis[i] = items[i].fi;
+        plen[i] = (uint32_t)strlen(items[i].path);
+        c.paths_len += plen[i];
+        if (ln)
+            ln[i] = lanes[i];
+    }
     double t0 = now_s();
-    if (!rc) {
-        char buf[MAX_STORAGE_TARGETS];
-        memset(buf, 1, sizeof(buf));
-        if (write(go[1], buf, (size_t)nforked) != (ssize_t)nforked)
-            rc = -EPIPE;
+    int rc = 0, sent[MAX_STORAGE_TARGETS] = {0};
+    for (int k = 0; k < P->ntargets; k++) {
+        const int fd = P->cmd_fd[k];
+        int e = fd < 0 ? -EPIPE : io_full(fd, &c, sizeof(c), 1);
+        if (!e)
+            e = io_full(fd, (void *)root, c.root_len, 1);
+        if (!e && c.corrupt_len)
+            e = io_full(fd, (void *)corrupt, c.corrupt_len, 1);
+        if (!e)
+            e = io_full(fd, fis, nitems * sizeof(FileInfo), 1);
+        if (!e)
+            e = io_full(fd, plen, nitems * sizeof(uint32_t), 1);
+        for (size_t i = 0; !e && i < nitems; i++)
+            e = io_full(fd, (void *)items[i].path, plen[i], 1);
+        if (!e && ln)
+            e = io_full(fd, ln, nitems * sizeof(int32_t), 1);
+        if (e && !rc)
+            rc = -ECHILD; /* a rank is gone */
+        sent[k] = !e;
     }
-    close(go[1]); /* cancels whoever has not read a go byte */
-    go[1] = -1;
-    int died = 0;
-    for (int i = 0; i < nforked; i++) {
-        int status = 0;
-        while (waitpid(pids[i], &status, 0) < 0 && errno == EINTR)
-            ;
-        if (!WIFEXITED(status) || WEXITSTATUS(status) != 0)
-            died++;
-    }
-    double secs = now_s() - t0;
+    free(fis);
+    free(plen);
+    free(ln);
+    /* one report per rank that got the command, or its death */
     bcp_run_stats st;
     memset(&st, 0, sizeof(st));
-    st.seconds = secs;
-    rank_report rep;
-    int got = 0;
-    while (read(res[0], &rep, sizeof(rep)) == (ssize_t)sizeof(rep)) {
-        got++;
-        st.tasks += rep.tasks;
-        st.bytes_read += rep.bytes_read;
-        st.bytes_written += rep.bytes_written;
-        st.errors += rep.error != 0;
-        if (rep.rc && !rc)
-            rc = rep.rc;
+    int done[MAX_STORAGE_TARGETS] = {0}, pending = 0;
+    for (int k = 0; k < P->ntargets; k++)
+        pending += sent[k];
+    while (pending > 0) {
+        struct pollfd pfd = {P->res_fd, POLLIN, 0};
+        int pr = poll(&pfd, 1, 200);
+        if (pr > 0) {
+            rank_report rep;
+            ssize_t r = read(P->res_fd, &rep, sizeof(rep));
+            if (r == (ssize_t)sizeof(rep) && rep.seq == c.seq && rep.rank >= 1 && rep.rank <= P->ntargets &&
+                sent[rep.rank - 1] && !done[rep.rank - 1]) {
+                done[rep.rank - 1] = 1;
+                pending--;
+                st.tasks += rep.tasks;
+                st.bytes_read += rep.bytes_read;
+                st.bytes_written += rep.bytes_written;
+                st.errors += rep.error != 0;
+                if (rep.rc && !rc)
+                    rc = rep.rc;
+                continue;
+            }
+            if (r == 0)
+                break; /* every rank is gone */
+            continue;
+        }
+        /* no report: has a rank that owes one died?  (its own pids only:
+         * the caller's other children are not ours to reap) */
+        for (int k = 0; k < P->ntargets; k++) {
+            int status;
+            if (P->pids[k] <= 0 || waitpid(P->pids[k], &status, WNOHANG) != P->pids[k])
+                continue;
+            P->pids[k] = -1;
+            if (sent[k] && !done[k]) {
+                done[k] = 1;
+                pending--;
+                if (!rc)
+                    rc = -ECHILD;
+            }
+        }
     }
-    if (!rc && (died || got != nforked))
-        rc = -ECHILD;
+    if (pending > 0 && !rc)
+        rc = -ECHILD; /* reports missing: every rank is gone */
+    st.seconds = now_s() - t0;
     if (stats)
         *stats = st;
-out:
-    for (int i = 0; i < 2; i++) {
-        if (go[i] >= 0)
-            close(go[i]);
-        if (res[i] >= 0)
-            close(res[i]);
-    }
-    if (w)
-        bcp_sock_world_destroy(w);
-    free(pids);
+    if (rc)
+        P->broken = 1;
     return rc;
 }
 
-int bcp_gen_run_procs(const char *store_root, int ntargets, const bcp_work_item *items, size_t nitems, int nlanes,
-                      const int *lanes_in, FILE *log, bcp_run_stats *stats)
+int bcp_rank_pool_gen(bcp_rank_pool *P, const char *store_root, const bcp_work_item *items, size_t nitems,
+                      int nlanes, const int *lanes_in, bcp_run_stats *stats)
 {
-    if (!store_root || ntargets < 1 || ntargets > MAX_STORAGE_TARGETS || nlanes < 1 || nlanes > 64 ||
-        (nitems && !items))
+    if (!P || !store_root || !*store_root || nlanes < 1 || nlanes > 64 || (nitems && !items))
         return -EINVAL;
-    int rc = check_items(ntargets, items, nitems);
+    int rc = check_items(P->ntargets, items, nitems);
     if (rc)
         return rc;
     int *lanes = NULL;
@@ -848,10 +1072,74 @@ int bcp_gen_run_procs(const char *store_root, int ntargets, const bcp_work_item 
         bcp_assign_lanes(nlanes, nitems, fis, lanes);
         free(fis);
     }
-    procs_job J = {store_root, ntargets, nlanes, 0, -1, -1, items, nitems, lanes_in ? lanes_in : lanes, log};
-    rc = run_procs(&J, stats);
+    rc = pool_run(P, POOL_GEN, store_root, items, nitems, nlanes, lanes_in ? lanes_in : lanes, -1, NULL, stats);
     free(lanes);
     return rc;
+}
+
+int bcp_rank_pool_rebuild(bcp_rank_pool *P, const char *store_root, int rebuild_target, const bcp_work_item *items,
+                          size_t nitems, const char *corrupt_list_path, bcp_run_stats *stats)
+{
+    if (!P || !store_root || !*store_root || P->ntargets < 2 || rebuild_target < 0 ||
+        rebuild_target >= P->ntargets || (nitems && !items))
+        return -EINVAL;
+    int rc = check_items(P->ntargets, items, nitems);
+    if (rc)
+        return rc;
+    if (corrupt_list_path) { /* truncated once here; the ranks append */
+        int fd = open(corrupt_list_path, O_WRONLY | O_CREAT | O_TRUNC, S_IRUSR | S_IWUSR);
+        if (fd < 0)
+            return -errno;
+        close(fd);
+    }
+    return pool_run(P, POOL_REBUILD, store_root, items, nitems, 1, NULL, rebuild_target, corrupt_list_path, stats);
+}
+
+int bcp_rank_pool_destroy(bcp_rank_pool *P)
+{
+    if (!P)
+        return 0;
+    pool_cmd q;
+    memset(&q, 0, sizeof(q));
+    q.magic = POOL_MAGIC;
+    q.op = POOL_QUIT;
+    for (int k = 0; k < P->ntargets; k++)
+        if (P->cmd_fd[k] >= 0) {
+            (void)io_full(P->cmd_fd[k], &q, sizeof(q), 1);
+            close(P->cmd_fd[k]); /* EOF: a rank that missed QUIT leaves too */
+            P->cmd_fd[k] = -1;
+        }
+    int rc = 0;
+    for (int k = 0; k < P->ntargets; k++)
+        if (P->pids[k] > 0) {
+            int status = 0;
+            while (waitpid(P->pids[k], &status, 0) < 0 && errno == EINTR)
+                ;
+            if (!WIFEXITED(status) || WEXITSTATUS(status) != 0)
+                rc = -ECHILD;
+            P->pids[k] = -1;
+        }
+    if (P->res_fd >= 0)
+        close(P->res_fd);
+    free(P);
+    return rc;
+}
+
+int bcp_gen_run_procs(const char *store_root, int ntargets, const bcp_work_item *items, size_t nitems, int nlanes,
+                      const int *lanes, FILE *log, bcp_run_stats *stats)
+{
+    if (!store_root || ntargets < 1 || ntargets > MAX_STORAGE_TARGETS || nlanes < 1 || nlanes > 64 ||
+        (nitems && !items))
+        return -EINVAL;
+    int rc = check_items(ntargets, items, nitems);
+    if (rc)
+        return rc;
+    bcp_rank_pool *P = NULL;
+    if ((rc = bcp_rank_pool_create(ntargets, log, &P)))
+        return rc;
+    rc = bcp_rank_pool_gen(P, store_root, items, nitems, nlanes, lanes, stats);
+    int drc = bcp_rank_pool_destroy(P);
+    return rc ? rc : drc;
 }
 
 int bcp_rebuild_run_procs(const char *store_root, int ntargets, int rebuild_target, const bcp_work_item *items,
@@ -863,13 +1151,10 @@ int bcp_rebuild_run_procs(const char *store_root, int ntargets, int rebuild_targ
     int rc = check_items(ntargets, items, nitems);
     if (rc)
         return rc;
-    int corrupt_fd = corrupt_list_path
-                         ? open(corrupt_list_path, O_WRONLY | O_CREAT | O_TRUNC | O_APPEND, S_IRUSR | S_IWUSR)
-                         : open("/dev/null", O_WRONLY);
-    if (corrupt_fd < 0)
-        return -errno;
-    procs_job J = {store_root, ntargets, 1, 1, rebuild_target, corrupt_fd, items, nitems, NULL, log};
-    rc = run_procs(&J, stats);
-    close(corrupt_fd);
-    return rc;
+    bcp_rank_pool *P = NULL;
+    if ((rc = bcp_rank_pool_create(ntargets, log, &P)))
+        return rc;
+    rc = bcp_rank_pool_rebuild(P, store_root, rebuild_target, items, nitems, corrupt_list_path, stats);
+    int drc = bcp_rank_pool_destroy(P);
+    return rc ? rc : drc;
 }

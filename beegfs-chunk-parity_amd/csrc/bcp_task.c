@@ -1313,3 +1313,27 @@ int process_task(HostState *hs, const char *path, const FileInfo *fi, TaskInfo t
         return 0;
     return active_ranks(fi->locations) != 0;
 }
+
+void bcpi_settings_get(bcpi_settings *s)
+{
+    pthread_mutex_lock(&g_lock);
+    s->fold_mode = g_fold_mode;
+    s->fold_inflight = g_fold_inflight;
+    s->hook = g_hook;
+    s->hook_ctx = g_hook_ctx;
+    pthread_mutex_unlock(&g_lock);
+    s->explicit_pad = __atomic_load_n(&g_explicit_pad, __ATOMIC_ACQUIRE);
+}
+
+int bcpi_settings_apply(const bcpi_settings *s)
+{
+    int rc = bcp_task_set_fold_mode(s->fold_mode);
+    if (rc >= 0)
+        rc = bcp_task_set_fold_inflight(s->fold_inflight);
+    if (rc >= 0)
+        rc = bcp_task_set_explicit_padding(s->explicit_pad);
+    if (rc < 0)
+        return rc;
+    bcp_task_set_xor_hook(s->hook, s->hook_ctx);
+    return 0;
+}

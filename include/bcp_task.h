@@ -326,6 +326,25 @@ int bcp_gen_run_procs(const char *store_root, int ntargets, const bcp_work_item 
                       int nlanes, const int *lanes, FILE *log, bcp_run_stats *stats);
 int bcp_rebuild_run_procs(const char *store_root, int ntargets, int rebuild_target, const bcp_work_item *items,
                           size_t nitems, const char *corrupt_list_path, FILE *log, bcp_run_stats *stats);
+/* The same ranks kept alive across runs (a long-lived job's ranks, as under
+ * mpirun): bcp_rank_pool_create forks one process per storage target (the
+ * caller must not have used the GPU yet: -EBUSY), and every gen / rebuild run
+ * is a command to all of them; each rank keeps its HIP engine, fold service
+ * and registered window rows from run to run.  A run takes the caller's
+ * P-role settings at the time of the call (fold mode, fold service width,
+ * window padding, test hook -- a hook's code must have been loaded before
+ * the pool was created: -EFAULT otherwise).  A rank whose run cannot start,
+ * or that dies, fails the run (-ECHILD or its -errno) and breaks the pool:
+ * later runs return -EPIPE; destroy it and create another.  The gen/rebuild
+ * _procs drivers above are one-run pools. */
+typedef struct bcp_rank_pool bcp_rank_pool;
+int bcp_rank_pool_create(int ntargets, FILE *log, bcp_rank_pool **out);
+int bcp_rank_pool_gen(bcp_rank_pool *pool, const char *store_root, const bcp_work_item *items, size_t nitems,
+                      int nlanes, const int *lanes, bcp_run_stats *stats);
+int bcp_rank_pool_rebuild(bcp_rank_pool *pool, const char *store_root, int rebuild_target,
+                          const bcp_work_item *items, size_t nitems, const char *corrupt_list_path,
+                          bcp_run_stats *stats);
+int bcp_rank_pool_destroy(bcp_rank_pool *pool);
 
 /* With the persistent state: bcp_gen_run plus, after every task of a lane
  * of rank k, the process_list DB update (gen/main.c:146-149: set when the

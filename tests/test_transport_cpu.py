@@ -121,6 +121,86 @@ def _padding_rounds(bcp, oracle, tmp_path, procs):
         assert S.read_file(S.parity_path(root, p, path)) == oracle.gen_parity_file(contents[path]), path
 
 
+@pytest.mark.timeout(300)
+def test_rank_pool_serves_many_runs(bcp, oracle, cpu_hook, tmp_path):
+    """One pool of rank processes, several runs: gen, gen again over rewritten
+    (smaller) chunks with the reference's padded wire switched on in between,
+    a rebuild with its corrupt list, a gen on another store -- every result
+    checked; the ranks' window rows and pools live across the runs."""
+    rng = np.random.default_rng(88)
+    nt = 6
+    files = _random_files(rng, nt, 30, 500_000)
+    root = str(tmp_path / "a")
+    with bcp.RankPool(nt) as pool:
+        items, contents = S.populate(root, nt, files, seed=1)
+        st = pool.gen(root, items, nlanes=5)
+        assert st.errors == 0 and st.tasks == sum(len(h) + 1 for (_, h, _, _) in files)
+        for (path, holders, p, lens) in files:
+            assert S.read_file(S.parity_path(root, p, path)) == oracle.gen_parity_file(contents[path]), path
+        small = [(path, h, p, [max(0, L // 7 - 3) for L in lens]) for (path, h, p, lens) in files]
+        items, contents = S.populate(root, nt, small, seed=2)
+        prev = bcp.set_explicit_padding(True)  # taken by the ranks with the next run
+        try:
+            assert pool.gen(root, items, nlanes=3).errors == 0
+        finally:
+            bcp.set_explicit_padding(prev)
+        for (path, holders, p, lens) in small:
+            assert S.read_file(S.parity_path(root, p, path)) == oracle.gen_parity_file(contents[path]), path
+        victim = 2
+        lost = {}
+        for (path, holders, p, lens) in small:
+            if victim in holders:
+                lost[path] = S.read_file(S.chunk_path(root, victim, path))
+                os.remove(S.chunk_path(root, victim, path))
+        corrupt = str(tmp_path / "corrupt.txt")
+        assert pool.rebuild(root, victim, items, corrupt_list=corrupt).errors == 0
+        for path, data in lost.items():
+            assert S.read_file(S.chunk_path(root, victim, path)) == data, path
+        assert open(corrupt).read() == ""
+        root_b = str(tmp_path / "b")
+        items_b, contents_b = S.populate(root_b, nt, files[:10], seed=3)
+        assert pool.gen(root_b, items_b, nlanes=12).errors == 0
+        for (path, holders, p, lens) in files[:10]:
+            assert S.read_file(S.parity_path(root_b, p, path)) == oracle.gen_parity_file(contents_b[path]), path
+
+
+@pytest.mark.timeout(120)
+def test_rank_pool_broken_by_a_rank_that_cannot_start(bcp, cpu_hook, tmp_path):
+    """Every rank fails to open a store that does not exist: the run fails
+    (no hang), the pool refuses later runs (-EPIPE) and closes cleanly."""
+    root, files, items, contents = _config(tmp_path, nfiles=6)
+    pool = bcp.RankPool(6)
+    try:
+        with pytest.raises(bcp.BcpError) as ei:
+            pool.gen(str(tmp_path / "missing"), items, nlanes=2)
+        assert ei.value.rc in (-2, -10)  # -ENOENT from a rank, or -ECHILD
+        with pytest.raises(bcp.BcpError) as ei:
+            pool.gen(root, items, nlanes=2)
+        assert ei.value.rc == -32  # -EPIPE
+    finally:
+        pool.close()
+
+
+@pytest.mark.timeout(120)
+def test_rank_pool_refuses_a_hook_loaded_after_the_fork(bcp, cpu_hook, tmp_path):
+    """The hook is code of the caller's process: a library loaded after the
+    ranks were forked is not mapped in them (-EFAULT, not a crash)."""
+    import ctypes
+    root, files, items, contents = _config(tmp_path, nfiles=4)
+    with bcp.RankPool(6) as pool:
+        src = tmp_path / "late.c"
+        src.write_text("#include <stddef.h>\n#include <stdint.h>\nint late_fold(uint8_t *d, size_t n, const uint8_t"
+                       " *s, size_t p, int k, void *c) { (void)d; (void)n; (void)s; (void)p; (void)k; (void)c;"
+                       " return 0; }\n")
+        so = tmp_path / "liblate.so"
+        subprocess.run(["gcc", "-O2", "-shared", "-fPIC", "-o", str(so), str(src)], check=True)
+        late = ctypes.CDLL(str(so))
+        bcp.set_xor_hook(ctypes.cast(late.late_fold, ctypes.c_void_p).value)
+        with pytest.raises(bcp.BcpError) as ei:
+            pool.gen(root, items, nlanes=2)
+        assert ei.value.rc in (-14, -10)  # -EFAULT from a rank, or -ECHILD
+
+
 def test_explicit_loopback_transport_and_validation(bcp, oracle, cpu_hook, tmp_path):
     import ctypes
     L = bcp.lib()
