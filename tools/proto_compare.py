@@ -22,10 +22,13 @@ targets, 8-wide stripes of log-uniform 64 KiB-4 MiB chunks, 12 lanes).
 Rate = (chunk bytes read + parity bytes written) / wall; each round runs
 every fold once in a rotating order, medians over rounds after a cold one.
 Parity of the GPU and CPU runs is checked against the oracle on a sample.
---procs: every storage target's rank is its own forked PROCESS (socketpair
-transport, bcp_gen_run_procs / bcp_rebuild_run_procs); this process never
-touches the GPU then (the ranks create their own HIP contexts), and the
-per-phase and fold-service counters live in the ranks (not reported).
+--procs: every storage target's rank is its own PROCESS (socketpair
+transport), kept alive across runs in a rank pool (bcp_rank_pool_*: HIP init
+and row registration paid once per rank, as by a long-lived job's ranks);
+--procs-cold forks fresh ranks for every run (bcp_gen_run_procs /
+bcp_rebuild_run_procs).  This process never touches the GPU then (the ranks
+create their own HIP contexts), and the per-phase and fold-service counters
+live in the ranks (not reported).
 One JSON line per (workload, fold); tools only.
 """
 import argparse
@@ -165,17 +168,33 @@ def main():
     ap.add_argument("--c1-files", type=int, default=1333)
     ap.add_argument("--c5-stripes", type=int, default=1000)
     ap.add_argument("--lanes", type=int, default=12)
-    ap.add_argument("--procs", action="store_true", help="ranks as forked processes (socketpair transport)")
+    ap.add_argument("--procs", action="store_true", help="ranks as processes kept alive across runs")
+    ap.add_argument("--procs-cold", action="store_true", help="ranks as processes forked for every run")
     a = ap.parse_args()
-    gen = bcp.gen_run_procs if a.procs else bcp.gen_run
-    rebuild = bcp.rebuild_run_procs if a.procs else bcp.rebuild_run
+    pools = {}
+
+    def pool_for(nt):
+        if nt not in pools:
+            pools[nt] = bcp.RankPool(nt)
+        return pools[nt]
+    if a.procs:
+        def gen(root, nt, items, nlanes=12):
+            return pool_for(nt).gen(root, items, nlanes=nlanes)
+
+        def rebuild(root, nt, victim, items):
+            return pool_for(nt).rebuild(root, victim, items)
+    elif a.procs_cold:
+        gen, rebuild = bcp.gen_run_procs, bcp.rebuild_run_procs
+    else:
+        gen, rebuild = bcp.gen_run, bcp.rebuild_run
     folds = a.folds.split(",")
     noop = noop_hook()
     hooks = {"cpu_reference": ctypes.cast(oracle.lib().oracle_xor_rows, ctypes.c_void_p).value,
              "noop": ctypes.cast(noop.noop_fold, ctypes.c_void_p).value}
     rng = np.random.default_rng(0)
     wl = a.workloads.split(",")
-    tr = {"transport": "socketpair rank processes" if a.procs else "loopback threads"}
+    tr = {"transport": "socketpair rank processes, pooled" if a.procs else
+          "socketpair rank processes, forked per run" if a.procs_cold else "loopback threads"}
     if "c1_gen" in wl or "c1_rebuild" in wl:
         root = os.path.join(a.root, "c1")
         shutil.rmtree(root, ignore_errors=True)
@@ -238,7 +257,9 @@ def main():
         measure("config5_gen", folds, a.rounds, run5, lambda: verify(root, files, contents, 20, rng), rd + wr, hooks,
                 {"lanes": a.lanes, "stripes": len(files), **tr}, prepare=lambda: reset_parity(root, 9))
         shutil.rmtree(root, ignore_errors=True)
-    if not a.procs:
+    for p in pools.values():
+        p.close()
+    if not (a.procs or a.procs_cold):
         bcp.task_shutdown()
 
 
