@@ -848,6 +848,16 @@ static void rank_command(const pool_cmd *c, int cmd_fd, int k, FILE *log, rank_r
  * or the caller's end closes. */
 static void rank_main(bcp_sock_world *w, int k, int cmd_fd, int res_fd, FILE *log)
 {
+    /* Every rank process holds its own HIP context on a GPU that several
+     * ranks share.  With HIP's default of 4 hardware queues each, 9 ranks on
+     * one MI355X oversubscribed its queues and the GPU fold fell to 11.9 GiB/s
+     * (config-5 shapes, below the CPU fold's 16.4); with 2 queues each it ran
+     * at 19.9 (1: 20.2) -- profiles/r02/protocol/pool_hwq_r2ab_*.  A rank
+     * needs two (a queue's compute and copy streams), so that is the default
+     * unless the caller set GPU_MAX_HW_QUEUES; HIP reads it at its first call,
+     * which comes after this in the rank. */
+    if (!getenv("GPU_MAX_HW_QUEUES"))
+        setenv("GPU_MAX_HW_QUEUES", "2", 1);
     bcp_transport_ops ops;
     int arc = bcp_sock_world_attach(w, k + 1, &ops);
     if (!arc)

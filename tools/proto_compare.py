@@ -167,6 +167,7 @@ def main():
     ap.add_argument("--workloads", default="c1_gen,c1_rebuild,c5_gen")
     ap.add_argument("--c1-files", type=int, default=1333)
     ap.add_argument("--c5-stripes", type=int, default=1000)
+    ap.add_argument("--c5-targets", type=int, default=9, help="config 5: storage targets (stripe width min(8, t-1))")
     ap.add_argument("--lanes", type=int, default=12)
     ap.add_argument("--procs", action="store_true", help="ranks as processes kept alive across runs")
     ap.add_argument("--procs-cold", action="store_true", help="ranks as processes forked for every run")
@@ -175,8 +176,14 @@ def main():
 
     def pool_for(nt):
         if nt not in pools:
+            close_pools()  # one pool at a time: idle ranks keep their GPU contexts
             pools[nt] = bcp.RankPool(nt)
         return pools[nt]
+
+    def close_pools():
+        for p in pools.values():
+            p.close()
+        pools.clear()
     if a.procs:
         def gen(root, nt, items, nlanes=12):
             return pool_for(nt).gen(root, items, nlanes=nlanes)
@@ -244,21 +251,22 @@ def main():
         shutil.rmtree(root, ignore_errors=True)
         r5 = np.random.default_rng(5)
         files = []
+        nt5, w5 = a.c5_targets, min(8, a.c5_targets - 1)
         for i in range(a.c5_stripes):
-            holders, p = S.random_layout(r5, 9, 8)
-            lens = [int(x) for x in np.exp(r5.uniform(np.log(64 * KiB), np.log(4 * MiB), size=8))]
+            holders, p = S.random_layout(r5, nt5, w5)
+            lens = [int(x) for x in np.exp(r5.uniform(np.log(64 * KiB), np.log(4 * MiB), size=w5))]
             files.append((f"u{i % 8}/{(i * 2654435761) % 65536:04X}/chunk{i}", holders, p, lens))
         contents = write_store(root, files, 2)
         items = [(path, 1_700_000_000, S.with_p(sum(1 << h for h in holders), p)) for path, holders, p, _ in files]
         rd, wr = total_bytes(root, files)
 
         def run5():
-            return gen(root, 9, items, nlanes=a.lanes)
+            return gen(root, nt5, items, nlanes=a.lanes)
         measure("config5_gen", folds, a.rounds, run5, lambda: verify(root, files, contents, 20, rng), rd + wr, hooks,
-                {"lanes": a.lanes, "stripes": len(files), **tr}, prepare=lambda: reset_parity(root, 9))
+                {"lanes": a.lanes, "stripes": len(files), "targets": nt5, **tr},
+                prepare=lambda: reset_parity(root, nt5))
         shutil.rmtree(root, ignore_errors=True)
-    for p in pools.values():
-        p.close()
+    close_pools()
     if not (a.procs or a.procs_cold):
         bcp.task_shutdown()
 
