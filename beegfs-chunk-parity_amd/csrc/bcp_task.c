@@ -658,8 +658,13 @@ static int fold_window(fold_res *R, HostState *hs, int mode, bcp_xor_hook_fn hoo
         return rc;
     if (mode == BCP_FOLD_ZERO_COPY) {
         /* rows and out are mapped pinned memory (grow): the kernel streams
-         * them over PCIe, no copy commands */
-        if ((rc = bcp_xor_strided_async(R->q, out, pitch, rows, pitch * (size_t)n, pitch, 1, (uint32_t)n, nbytes)))
+         * row j's data bytes (valid[j]) over PCIe, no copy commands; the
+         * zeros past them are the kernel's */
+        bcp_stripe st = {(uint64_t)(uintptr_t)out, nbytes, 0, (uint32_t)n, 0};
+        bcp_source so[MAX_STORAGE_TARGETS];
+        for (int j = 0; j < n; j++)
+            so[j] = (bcp_source){(uint64_t)(uintptr_t)(rows + (size_t)j * pitch), valid[j]};
+        if ((rc = bcp_xor_stripes_async(R->q, &st, 1, so, (uint32_t)n)))
             return rc;
         return bcp_queue_sync(R->q);
     }
@@ -991,9 +996,8 @@ static void parity_generator(const bcp_transport_ops *T, const char *path, const
         }
     }
 
-    /* folds that read whole rows (the test hook, ZERO_COPY, STAGED) */
-    const int pad_rows = implicit_pad && !res_rc &&
-                         (hook != NULL || (mode != BCP_FOLD_BATCHED && mode != BCP_FOLD_DEVICE_ROWS && !streamed));
+    /* folds that read whole rows (the test hook, STAGED) */
+    const int pad_rows = implicit_pad && !res_rc && (hook != NULL || mode == BCP_FOLD_STAGED);
     phase_add(BCP_PHASE_P_OPEN, &tph);
     if (res_rc) {
         int drc = drain_windows(T, ranks, n, buffer_size, expected_messages, ti.tag);

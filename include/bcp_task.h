@@ -99,8 +99,9 @@ int process_task(HostState *hs, const char *path, const FileInfo *fi, TaskInfo t
  * given, else st % device_count.  Engines are created lazily, one per device. */
 int bcp_task_set_device_map(const int *devices, int ntargets);
 /* How the P role folds a window on the GPU.  ZERO_COPY: the kernel reads the
- * pinned window rows and writes the pinned parity block in place over PCIe,
- * one launch + one sync per window on the lane's own queue.  STAGED: H2D of
+ * pinned window rows (their data bytes) and writes the pinned parity block
+ * in place over PCIe, one launch + one sync per window on the lane's own
+ * queue.  STAGED: H2D of
  * the rows, kernel on device buffers, D2H (three commands per window).
  * BATCHED: the window is handed to the device's fold service (flat
  * combining, no thread of its own): a waiting lane leads a launch that folds
