@@ -222,6 +222,7 @@ typedef struct fold_job {
     int n;
     uint8_t *out;
     int done, rc;
+    pthread_cond_t cv; /* its lane sleeps here: woken when done, or to lead */
 } fold_job;
 
 #define MAX_INFLIGHT 16
@@ -240,7 +241,6 @@ typedef struct {
     int max_inflight; /* concurrent batches, each on its own slot's queue */
     fold_slot slot[MAX_INFLIGHT];
     pthread_mutex_t mu;
-    pthread_cond_t cv_done;
     fold_job *head, *tail;
     uint64_t windows, launches;
 } fold_svc;
@@ -319,7 +319,6 @@ static void svc_destroy(fold_svc *S)
         free(S->slot[i].st);
         free(S->slot[i].so);
     }
-    pthread_cond_destroy(&S->cv_done);
     pthread_mutex_destroy(&S->mu);
     free(S);
 }
@@ -338,7 +337,6 @@ static int svc_get(int dev, bcp_engine *e, fold_svc **out)
             S->eng = e;
             S->max_inflight = g_fold_inflight;
             pthread_mutex_init(&S->mu, NULL);
-            pthread_cond_init(&S->cv_done, NULL);
             g_svc[dev] = S;
         }
     }
@@ -347,10 +345,15 @@ static int svc_get(int dev, bcp_engine *e, fold_svc **out)
     return rc;
 }
 
+/* Wakeups are targeted: a leader wakes exactly the lanes whose windows it
+ * folded, and the lane at the head of the pending list to lead the next
+ * batch -- not every waiting lane (up to 12 lanes x every rank) on every
+ * completion. */
 static int fold_batched(fold_svc *S, const uint8_t *rows, size_t pitch, const size_t *valid, size_t nbytes, int n,
                         uint8_t *out)
 {
-    fold_job j = {NULL, rows, pitch, nbytes, valid, n, out, 0, 0};
+    fold_job j = {.rows = rows, .pitch = pitch, .nbytes = nbytes, .valid = valid, .n = n, .out = out};
+    pthread_cond_init(&j.cv, NULL);
     pthread_mutex_lock(&S->mu);
     if (S->tail)
         S->tail->next = &j;
@@ -359,7 +362,7 @@ static int fold_batched(fold_svc *S, const uint8_t *rows, size_t pitch, const si
     S->tail = &j;
     while (!j.done) {
         if (S->inflight >= S->max_inflight || !S->head) {
-            pthread_cond_wait(&S->cv_done, &S->mu);
+            pthread_cond_wait(&j.cv, &S->mu);
             continue;
         }
         /* lead a batch: everything pending (this window, if no other leader
@@ -380,14 +383,18 @@ static int fold_batched(fold_svc *S, const uint8_t *rows, size_t pitch, const si
             nx = x->next; /* x lives on its lane's stack: read next before done */
             x->rc = rc;
             x->done = 1;
+            if (x != &j)
+                pthread_cond_signal(&x->cv); /* its lane runs once we unlock */
         }
         S->windows += nb;
         S->launches += 1;
         S->inflight--;
         F->busy = 0;
-        pthread_cond_broadcast(&S->cv_done);
+        if (S->head)
+            pthread_cond_signal(&S->head->cv); /* windows that came meanwhile: a leader */
     }
     pthread_mutex_unlock(&S->mu);
+    pthread_cond_destroy(&j.cv);
     return j.rc;
 }
 
