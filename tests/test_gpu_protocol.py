@@ -294,6 +294,55 @@ def test_db_round_then_partial_round_then_rebuild(bcp, oracle, tmp_path, engine_
         assert S.read_file(S.chunk_path(root, victim, path)) == data, path
 
 
+POOL_SCRIPT = r"""
+import os, sys
+root = sys.argv[1]
+here = sys.argv[2]
+sys.path[:0] = [os.path.join(here, "..", "beegfs-chunk-parity_amd"), os.path.join(here, "..", "oracle")]
+import numpy as np
+import bcp_ctypes as bcp, bcp_store as S, oracle
+rng = np.random.default_rng(7)
+nt = 6
+files = []
+for i in range(24):
+    holders, p = S.random_layout(rng, nt, int(rng.integers(2, 6)))
+    files.append((f"q{i % 3}/c{i}", holders, p, [int(x) for x in rng.integers(1, 900_000, size=len(holders))]))
+def check(files, contents):
+    for (path, holders, p, lens) in files:
+        assert S.read_file(S.parity_path(root, p, path)) == oracle.gen_parity_file(contents[path]), path
+with bcp.RankPool(nt) as pool:   # this process never touches the GPU; the ranks do
+    items, contents = S.populate(root, nt, files, seed=1)
+    assert pool.gen(root, items, nlanes=4).errors == 0
+    check(files, contents)
+    small = [(path, h, p, [L // 5 + 1 for L in lens]) for (path, h, p, lens) in files]
+    items, contents = S.populate(root, nt, small, seed=2)
+    assert pool.gen(root, items, nlanes=4).errors == 0
+    check(small, contents)
+    victim, lost = 1, {}
+    for (path, holders, p, lens) in small:
+        if victim in holders:
+            lost[path] = S.read_file(S.chunk_path(root, victim, path))
+            os.remove(S.chunk_path(root, victim, path))
+    assert lost and pool.rebuild(root, victim, items).errors == 0
+    for path, data in lost.items():
+        assert S.read_file(S.chunk_path(root, victim, path)) == data, path
+print("pool ok")
+"""
+
+
+def test_rank_pool_on_device(tmp_path):
+    """Rank processes kept alive across runs with their HIP contexts: two gen
+    runs over different data and a rebuild through ONE pool, the P roles
+    folding on the device (default batched service), parity and rebuilt
+    chunks checked against the oracle.  In a fresh process: a pool cannot be
+    forked from one that has used the GPU."""
+    import subprocess
+    import sys
+    r = subprocess.run([sys.executable, "-c", POOL_SCRIPT, str(tmp_path), HERE], capture_output=True, text=True,
+                       timeout=240)
+    assert r.returncode == 0 and "pool ok" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]
+
+
 @pytest.mark.parametrize("engine_kind", ["protocol", "pipeline", "procs", "procs_device_rows"])
 def test_cli_complete_partial_rebuild(bcp, oracle, tmp_path, engine_kind):
     """bin/bcp end to end on the device: --complete (scan of every target),
