@@ -562,25 +562,58 @@ int bcp_store_cum_weights(const char *store_root, int ntargets, int *cum_weight)
 }
 
 /* Apply the process_list DB update (gen/main.c:146-149) for every processed
- * item to every replica (the batched pipeline has no per-rank lanes). */
-static int update_replicas(const char *root, int ntargets, const bcp_work_item *items, size_t n)
+ * item to every replica (the batched pipeline has no per-rank lanes).  The
+ * replicas are independent files: one thread each (a changelog round's
+ * updates otherwise cost a serial open + replay + append per target). */
+typedef struct {
+    const char *root;
+    int k;
+    const bcp_work_item *items;
+    size_t n;
+    int rc;
+} replica_job;
+
+static void *update_replica(void *p)
 {
-    int rc = 0;
-    for (int k = 0; k < ntargets && !rc; k++) {
-        char dp[4096];
-        bcp_pdb *db = NULL;
-        if ((rc = db_path(root, k, dp, sizeof(dp))) || (rc = bcp_pdb_open(dp, DB_VERSION, &db)))
-            break;
-        for (size_t i = 0; i < n && !rc; i++) {
-            if ((uint64_t)GET_P(items[i].fi.locations) == NO_P)
-                continue;
-            const char *key = items[i].path;
-            rc = (items[i].fi.locations & L_MASK) ? bcp_pdb_set(db, key, strlen(key), &items[i].fi)
-                                                  : bcp_pdb_del(db, key, strlen(key));
-        }
+    replica_job *J = p;
+    char dp[4096];
+    bcp_pdb *db = NULL;
+    int rc = db_path(J->root, J->k, dp, sizeof(dp));
+    if (!rc)
+        rc = bcp_pdb_open(dp, DB_VERSION, &db);
+    for (size_t i = 0; i < J->n && !rc; i++) {
+        if ((uint64_t)GET_P(J->items[i].fi.locations) == NO_P)
+            continue;
+        const char *key = J->items[i].path;
+        rc = (J->items[i].fi.locations & L_MASK) ? bcp_pdb_set(db, key, strlen(key), &J->items[i].fi)
+                                                 : bcp_pdb_del(db, key, strlen(key));
+    }
+    if (db) {
         int crc = bcp_pdb_close(db);
         if (!rc)
             rc = crc;
+    }
+    J->rc = rc;
+    return NULL;
+}
+
+static int update_replicas(const char *root, int ntargets, const bcp_work_item *items, size_t n)
+{
+    replica_job jobs[MAX_STORAGE_TARGETS];
+    pthread_t th[MAX_STORAGE_TARGETS];
+    int started[MAX_STORAGE_TARGETS] = {0};
+    for (int k = 0; k < ntargets; k++) {
+        jobs[k] = (replica_job){root, k, items, n, 0};
+        started[k] = pthread_create(&th[k], NULL, update_replica, &jobs[k]) == 0;
+        if (!started[k])
+            update_replica(&jobs[k]); /* no thread: on this one */
+    }
+    int rc = 0;
+    for (int k = 0; k < ntargets; k++) {
+        if (started[k])
+            pthread_join(th[k], NULL);
+        if (jobs[k].rc && !rc)
+            rc = jobs[k].rc;
     }
     return rc;
 }
