@@ -307,7 +307,8 @@ def config5(a):
     pl.close()
     ok2, bad2 = verify(root, sub_files, contents, a.verify, rng)
     emit(config=5, path="changelog_round_pipeline(events->plan vs DB->pipeline->DB)", stripes=len(sub),
-         plan_matches=plan_ok, seconds=round(dt, 3), GiBps=round((srd + swr) / dt / GiB, 3), bytes_read=srd,
+         plan_matches=plan_ok, seconds=round(dt, 3), pipeline_seconds=round(st.seconds, 4),
+         outside_pipeline_seconds=round(dt - st.seconds, 4), GiBps=round((srd + swr) / dt / GiB, 3), bytes_read=srd,
          bytes_written=swr, tasks=int(st.tasks), verified=ok2, bad=bad2)
     es.close()
     if not a.keep:
