@@ -118,6 +118,7 @@ _SIGS = {
     "bcp_task_set_xor_hook": ([_V, _V], None),
     "bcp_task_set_fold_mode": ([ctypes.c_int], ctypes.c_int),
     "bcp_task_set_explicit_padding": ([ctypes.c_int], ctypes.c_int),
+    "bcp_task_pipe_stats": ([ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)], ctypes.c_int),
     "bcp_task_set_fold_inflight": ([ctypes.c_int], ctypes.c_int),
     "bcp_task_fold_stats": ([ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)], ctypes.c_int),
     "bcp_task_inject_failure": ([ctypes.c_int, ctypes.c_int, ctypes.c_int], ctypes.c_int),
@@ -672,8 +673,8 @@ def set_xor_hook(fn_addr: int | None, ctx: int | None = None):
     lib().bcp_task_set_xor_hook(_V(fn_addr) if fn_addr else None, _V(ctx) if ctx else None)
 
 
-FOLD_ZERO_COPY, FOLD_STAGED, FOLD_BATCHED, FOLD_STREAMED, FOLD_DEVICE_ROWS = 0, 1, 2, 3, 4
-INJECT_FOLD_RES, INJECT_DRAIN_ROW, INJECT_SEND_BUF, INJECT_THREAD = 1, 2, 4, 8
+FOLD_ZERO_COPY, FOLD_STAGED, FOLD_BATCHED, FOLD_STREAMED, FOLD_DEVICE_ROWS, FOLD_PIPELINED = 0, 1, 2, 3, 4, 5
+INJECT_FOLD_RES, INJECT_DRAIN_ROW, INJECT_SEND_BUF, INJECT_THREAD, INJECT_READ = 1, 2, 4, 8, 16
 
 
 def set_fold_mode(mode: int) -> int:
@@ -683,6 +684,13 @@ def set_fold_mode(mode: int) -> int:
     if rc < 0:
         raise BcpError("bcp_task_set_fold_mode", rc)
     return rc
+
+
+def pipe_stats() -> tuple:
+    """(windows folded by following their rows, range folds launched) -- FOLD_PIPELINED."""
+    w, r = ctypes.c_uint64(0), ctypes.c_uint64(0)
+    lib().bcp_task_pipe_stats(ctypes.byref(w), ctypes.byref(r))
+    return w.value, r.value
 
 
 def set_explicit_padding(on: bool) -> bool:

@@ -73,6 +73,119 @@ static int g_tp_set = 0;
  * (zero pages until read; .bss costs no file or resident memory). */
 static uint8_t g_zero_window[BCP_WINDOW_BYTES];
 
+/* ---- row watches (BCP_FOLD_PIPELINED) ------------------------------------
+ * A P role that folds its window range by range registers the window's rows
+ * here, keyed by row address; a source that fills one of them directly
+ * (send_fill) reads its chunk in pieces and publishes, after each, how many
+ * leading bytes of the row are final.  Open addressing with backward-shift
+ * deletion; the live count lets every other fill skip the lock. */
+struct fold_res;
+typedef struct {
+    pthread_mutex_t mu;
+    size_t prog[MAX_STORAGE_TARGETS];
+    int redo; /* a published prefix was replaced (read error: zeros): fold it all again */
+    int err;  /* first range-fold launch error */
+    /* the window's fold: whoever completes a range launches it (range_claim) */
+    struct fold_res *R;
+    bcp_xor_hook_fn hook;
+    void *hook_ctx;
+    const uint8_t *rows;
+    size_t pitch, nbytes, lo; /* lo: bytes folded or claimed */
+    const size_t *valid;
+    uint8_t *out;
+    int n;
+} row_watch;
+
+#define WATCH_SLOTS 4096u
+#define WATCH_PIECE ((size_t)256 << 10) /* bytes a source reads between publishes */
+typedef struct {
+    const void *row;
+    row_watch *w;
+    int j;
+} watch_slot;
+static watch_slot g_watch[WATCH_SLOTS];
+static pthread_mutex_t g_watch_lock = PTHREAD_MUTEX_INITIALIZER;
+static size_t g_watch_live;
+
+static size_t watch_hash(const void *p)
+{
+    uint64_t x = (uint64_t)(uintptr_t)p;
+    x ^= x >> 29;
+    x *= UINT64_C(0xbf58476d1ce4e5b9);
+    x ^= x >> 32;
+    return (size_t)x & (WATCH_SLOTS - 1);
+}
+
+/* 0, or -ENOSPC when the table is half full (the caller folds unwatched). */
+static int watch_add(const void *row, row_watch *w, int j)
+{
+    pthread_mutex_lock(&g_watch_lock);
+    if (g_watch_live * 2 >= WATCH_SLOTS) {
+        pthread_mutex_unlock(&g_watch_lock);
+        return -ENOSPC;
+    }
+    size_t i = watch_hash(row);
+    while (g_watch[i].row)
+        i = (i + 1) & (WATCH_SLOTS - 1);
+    g_watch[i] = (watch_slot){row, w, j};
+    __atomic_store_n(&g_watch_live, g_watch_live + 1, __ATOMIC_RELEASE);
+    pthread_mutex_unlock(&g_watch_lock);
+    return 0;
+}
+
+static void watch_del(const void *row)
+{
+    pthread_mutex_lock(&g_watch_lock);
+    size_t i = watch_hash(row);
+    while (g_watch[i].row && g_watch[i].row != row)
+        i = (i + 1) & (WATCH_SLOTS - 1);
+    if (g_watch[i].row) {
+        /* backward shift: pull later entries of the probe run into the hole */
+        size_t hole = i;
+        for (size_t k = (i + 1) & (WATCH_SLOTS - 1); g_watch[k].row; k = (k + 1) & (WATCH_SLOTS - 1)) {
+            const size_t home = watch_hash(g_watch[k].row);
+            if (((k - home) & (WATCH_SLOTS - 1)) >= ((k - hole) & (WATCH_SLOTS - 1))) {
+                g_watch[hole] = g_watch[k];
+                hole = k;
+            }
+        }
+        g_watch[hole].row = NULL;
+        __atomic_store_n(&g_watch_live, g_watch_live - 1, __ATOMIC_RELEASE);
+    }
+    pthread_mutex_unlock(&g_watch_lock);
+}
+
+static row_watch *watch_find(const void *row, int *j)
+{
+    if (!__atomic_load_n(&g_watch_live, __ATOMIC_ACQUIRE))
+        return NULL;
+    row_watch *w = NULL;
+    pthread_mutex_lock(&g_watch_lock);
+    for (size_t i = watch_hash(row); g_watch[i].row; i = (i + 1) & (WATCH_SLOTS - 1))
+        if (g_watch[i].row == row) {
+            w = g_watch[i].w;
+            *j = g_watch[i].j;
+            break;
+        }
+    pthread_mutex_unlock(&g_watch_lock);
+    return w;
+}
+
+static void range_claim(row_watch *w);
+
+/* A source's new final prefix of row j; the range it completes is folded
+ * by this thread (the lane of the P role may not get a CPU before the reads
+ * end: a woken source runs on the CPU of the lane that posted its receive). */
+static void watch_publish(row_watch *w, int j, size_t bytes, int redo)
+{
+    pthread_mutex_lock(&w->mu);
+    if (bytes > w->prog[j])
+        w->prog[j] = bytes;
+    w->redo |= redo;
+    range_claim(w);
+    pthread_mutex_unlock(&w->mu);
+}
+
 int bcp_task_set_device_map(const int *devices, int ntargets)
 {
     if (ntargets < 0 || ntargets > MAX_STORAGE_TARGETS || (ntargets && !devices))
@@ -88,7 +201,7 @@ int bcp_task_set_device_map(const int *devices, int ntargets)
 int bcp_task_set_fold_mode(int mode)
 {
     if (mode != BCP_FOLD_ZERO_COPY && mode != BCP_FOLD_STAGED && mode != BCP_FOLD_BATCHED &&
-        mode != BCP_FOLD_STREAMED && mode != BCP_FOLD_DEVICE_ROWS)
+        mode != BCP_FOLD_STREAMED && mode != BCP_FOLD_DEVICE_ROWS && mode != BCP_FOLD_PIPELINED)
         return -EINVAL;
     pthread_mutex_lock(&g_lock);
     int prev = g_fold_mode;
@@ -134,7 +247,7 @@ static bcp_transport_ops transport_now(void)
 }
 
 /* ---- failure injection (tests) ------------------------------------------ */
-#define NSITES 4
+#define NSITES 5
 static int g_inj_after[NSITES], g_inj_count[NSITES];
 
 static int site_index(int site)
@@ -144,6 +257,7 @@ static int site_index(int site)
     case BCP_INJECT_DRAIN_ROW: return 1;
     case BCP_INJECT_SEND_BUF: return 2;
     case BCP_INJECT_THREAD: return 3;
+    case BCP_INJECT_READ: return 4;
     default: return -1;
     }
 }
@@ -663,7 +777,7 @@ static int fold_window(fold_res *R, HostState *hs, int mode, bcp_xor_hook_fn hoo
     }
     if (!R->q && (rc = bcp_queue_create(R->eng, &R->q)))
         return rc;
-    if (mode == BCP_FOLD_ZERO_COPY) {
+    if (mode == BCP_FOLD_ZERO_COPY || mode == BCP_FOLD_PIPELINED) {
         /* rows and out are mapped pinned memory (grow): the kernel streams
          * row j's data bytes (valid[j]) over PCIe, no copy commands; the
          * zeros past them are the kernel's */
@@ -718,6 +832,108 @@ static int stream_fold(fold_res *R, int n, size_t pitch, const size_t *valid, si
         so[j] = (bcp_source){(uint64_t)(uintptr_t)((uint8_t *)R->d_src + (size_t)j * pitch), valid[j]};
     int rc = bcp_xor_stripes_async(R->q, &st, 1, so, (uint32_t)n);
     return rc ? rc : bcp_queue_sync(R->q);
+}
+
+/* ---- PIPELINED mode --------------------------------------------------------
+ * The window's rows are watched while the sources fill them: the fold of
+ * every byte range that all rows have delivered (data bytes only, valid[j])
+ * is launched on the lane's queue, without a sync, by the source whose
+ * piece completed it, so most of the rows' PCIe reads overlap the sources'
+ * file reads; after the receives the P role folds the rest (at least the
+ * last piece) and syncs once.  Short kernels only: nothing on the device
+ * waits for the host. */
+#define PIPE_STEP ((size_t)128 << 10)   /* smallest range worth a launch */
+#define PIPE_ALIGN ((size_t)4096)       /* range boundaries */
+
+static uint64_t g_pipe_windows, g_pipe_ranges; /* bcp_task_pipe_stats */
+
+int bcp_task_pipe_stats(uint64_t *windows, uint64_t *ranges)
+{
+    if (windows)
+        *windows = __atomic_load_n(&g_pipe_windows, __ATOMIC_RELAXED);
+    if (ranges)
+        *ranges = __atomic_load_n(&g_pipe_ranges, __ATOMIC_RELAXED);
+    return 0;
+}
+
+/* Fold out[lo, hi) = XOR of the rows' [lo, hi) on the lane's queue, no sync
+ * (under the test hook: the hook, at once, over whole rows whose padding the
+ * P role zeroed before the receives).  Callers hold w->mu: the queue is one
+ * lane's, and launches on it must not interleave. */
+static int launch_range(const row_watch *w, size_t lo, size_t hi)
+{
+    __atomic_fetch_add(&g_pipe_ranges, 1, __ATOMIC_RELAXED);
+    if (w->hook)
+        return w->hook(w->out + lo, hi - lo, w->rows + lo, w->pitch, w->n, w->hook_ctx);
+    bcp_stripe st = {(uint64_t)(uintptr_t)(w->out + lo), hi - lo, 0, (uint32_t)w->n, 0};
+    bcp_source so[MAX_STORAGE_TARGETS];
+    for (int j = 0; j < w->n; j++) {
+        const size_t len = w->valid[j] > lo ? MIN_(w->valid[j], hi) - lo : 0;
+        so[j] = (bcp_source){(uint64_t)(uintptr_t)(w->rows + (size_t)j * w->pitch + lo), len};
+    }
+    return bcp_xor_stripes_async(w->R->q, &st, 1, so, (uint32_t)w->n);
+}
+
+/* Under w->mu: launch every range all rows have delivered past w->lo. */
+static void range_claim(row_watch *w)
+{
+    while (!w->redo && !w->err && w->lo < w->nbytes) {
+        size_t avail = w->nbytes;
+        for (int j = 0; j < w->n; j++)
+            avail = MIN_(avail, w->prog[j] >= w->valid[j] ? w->nbytes : w->prog[j]);
+        if (avail < w->nbytes && avail < w->lo + PIPE_STEP)
+            return;
+        const size_t hi = avail >= w->nbytes ? w->nbytes : avail / PIPE_ALIGN * PIPE_ALIGN;
+        const int rc = launch_range(w, w->lo, hi);
+        if (rc)
+            w->err = rc;
+        else
+            w->lo = hi;
+    }
+}
+
+static int watch_rows(row_watch *W, fold_res *R, bcp_xor_hook_fn hook, void *hook_ctx, const uint8_t *rows,
+                      size_t pitch, const size_t *valid, int n, size_t nbytes, uint8_t *out)
+{
+    pthread_mutex_init(&W->mu, NULL);
+    memset(W->prog, 0, sizeof(W->prog));
+    W->redo = W->err = 0;
+    W->R = R;
+    W->hook = hook;
+    W->hook_ctx = hook_ctx;
+    W->rows = rows;
+    W->pitch = pitch;
+    W->nbytes = nbytes;
+    W->lo = 0;
+    W->valid = valid;
+    W->out = out;
+    W->n = n;
+    for (int j = 0; j < n; j++)
+        if (watch_add(rows + (size_t)j * pitch, W, j)) {
+            while (j-- > 0)
+                watch_del(rows + (size_t)j * pitch);
+            pthread_mutex_destroy(&W->mu);
+            return 0;
+        }
+    return 1;
+}
+
+/* After the receives (every fill has returned, so no source launches any
+ * more): unregister, fold the rest (all of it after a redo), the one sync
+ * -- also after an error, since ranges may be in flight.  fold = 0: sync
+ * only (the task failed). */
+static int finish_rows(row_watch *W, int fold)
+{
+    for (int j = 0; j < W->n; j++)
+        watch_del(W->rows + (size_t)j * W->pitch);
+    int rc = W->err;
+    const size_t lo = W->redo ? 0 : W->lo;
+    __atomic_fetch_add(&g_pipe_windows, 1, __ATOMIC_RELAXED);
+    if (fold && !rc && lo < W->nbytes)
+        rc = launch_range(W, lo, W->nbytes);
+    const int src = W->hook ? 0 : bcp_queue_sync(W->R->q);
+    pthread_mutex_destroy(&W->mu);
+    return rc ? rc : src;
 }
 
 /* ---- file helpers (task_processing.c:29-79) ----------------------------- */
@@ -1005,6 +1221,11 @@ static void parity_generator(const bcp_transport_ops *T, const char *path, const
 
     /* folds that read whole rows (the test hook, STAGED) */
     const int pad_rows = implicit_pad && !res_rc && (hook != NULL || mode == BCP_FOLD_STAGED);
+    /* PIPELINED: one window whose rows the sources fill directly (send_fill
+     * transports); otherwise it folds like ZERO_COPY */
+    int pipelined = mode == BCP_FOLD_PIPELINED && !res_rc && expected_messages == 1 && T->send_fill;
+    if (pipelined && !hook && !L->q && bcp_queue_create(L->eng, &L->q))
+        pipelined = 0;
     phase_add(BCP_PHASE_P_OPEN, &tph);
     if (res_rc) {
         int drc = drain_windows(T, ranks, n, buffer_size, expected_messages, ti.tag);
@@ -1027,8 +1248,20 @@ static void parity_generator(const bcp_transport_ops *T, const char *path, const
         /* After a transport error the loop keeps receiving every window from
          * every source (failed peers fail fast): live senders finish their
          * task instead of blocking; nothing more is folded or written. */
-        if (msg_i == 0)
+        row_watch W;
+        int watched = 0;
+        if (msg_i == 0) {
+            /* implicit padding (chunk_sender): a fold that reads whole rows
+             * gets the zeros past each chunk, written before the sources
+             * fill the data bytes; the other folds read valid[j] bytes */
+            if (pad_rows)
+                for (int j = 0; j < n; j++)
+                    if (valid[j] < buffer_size)
+                        memset(win_a + (size_t)j * pitch + valid[j], 0, buffer_size - valid[j]);
+            watched = pipelined && !have_had_error &&
+                      watch_rows(&W, L, hook, hook_ctx, win_a, pitch, valid, n, buffer_size, pblk);
             trc = post_recvs(T, req, n, win_a, pitch, buffer_size, ranks, ti.tag);
+        }
         int w = 0, crc = 0;
         if (streamed && !have_had_error && !trc)
             crc = stream_rows_in(T, L, req, n, win_a, pitch, valid, &w);
@@ -1043,12 +1276,6 @@ static void parity_generator(const bcp_transport_ops *T, const char *path, const
             int p2 = post_recvs(T, req, n, win_b, pitch, buffer_size, ranks, ti.tag);
             trc = trc ? trc : p2;
         }
-        /* implicit padding (chunk_sender): a fold that reads whole rows gets
-         * the zeros past each chunk here; the others read valid[j] bytes */
-        if (pad_rows)
-            for (int j = 0; j < n; j++)
-                if (valid[j] < buffer_size)
-                    memset(win_a + (size_t)j * pitch + valid[j], 0, buffer_size - valid[j]);
         phase_add(BCP_PHASE_P_ROWS, &tph);
         if (trc && !have_had_error) {
             have_had_error = as_errno(trc);
@@ -1056,12 +1283,15 @@ static void parity_generator(const bcp_transport_ops *T, const char *path, const
         }
         /* fold window msg_i on the GPU while the senders fill win_b */
         if (!have_had_error) {
-            int frc = streamed ? stream_fold(L, n, pitch, valid, buffer_size, pblk)
-                               : fold_window(L, hs, mode, hook, hook_ctx, win_a, pitch, valid, buffer_size, n, pblk);
+            int frc = watched    ? finish_rows(&W, 1)
+                      : streamed ? stream_fold(L, n, pitch, valid, buffer_size, pblk)
+                                 : fold_window(L, hs, mode, hook, hook_ctx, win_a, pitch, valid, buffer_size, n, pblk);
             if (frc) {
                 have_had_error = EIO;
                 LOGERR("GPU fold of '%s' failed: %s\n", path, bcp_strerror(frc));
             }
+        } else if (watched) {
+            (void)finish_rows(&W, 0); /* ranges in flight read these rows */
         }
         phase_add(BCP_PHASE_P_FOLD, &tph);
         if (!have_had_error) {
@@ -1149,23 +1379,51 @@ static void fill_bytes(window_fill *w, uint8_t *data, size_t n)
     /* the bytes this window must define: all n, or with implicit padding
      * the chunk's own (the P role supplies the zeros past them) */
     const size_t need = w->implicit_pad ? window_data_bytes(w->data_to_send, w->fd_size, w->data_sent, n) : n;
+    int wj = 0;
+    row_watch *W = watch_find(data, &wj); /* a P role folding this row as it fills */
     if (w->err != 0 || w->data_sent >= w->fd_size) {
         memset(data, 0, need);
+        if (W)
+            watch_publish(W, wj, need, 0);
         return;
     }
     /* up to the size the chunk reported (not past it should the file have
      * grown since fstat: the parity body then agrees with its header) */
     const uint64_t left = MIN_(w->data_to_send, w->fd_size) - w->data_sent;
-    ssize_t r = read(w->fd, data, (size_t)MIN_((uint64_t)n, left));
+    const size_t want = (size_t)MIN_((uint64_t)n, left);
+    ssize_t r;
+    if (!W) {
+        r = bcpi_inject_hit(BCP_INJECT_READ) ? (errno = EIO, -1) : read(w->fd, data, want);
+    } else {
+        /* in pieces, publishing the final prefix after each (EOF ends it) */
+        size_t got = 0;
+        r = 0;
+        while (got < want) {
+            ssize_t k = got && bcpi_inject_hit(BCP_INJECT_READ) ? (errno = EIO, -1)
+                                                                : read(w->fd, data + got, MIN_(WATCH_PIECE, want - got));
+            if (k <= 0) {
+                r = k < 0 ? k : (ssize_t)got;
+                break;
+            }
+            got += (size_t)k;
+            r = (ssize_t)got;
+            if (got < want)
+                watch_publish(W, wj, got, 0);
+        }
+    }
     if (r < 0) {
         w->err = errno;
         memset(data, 0, need);
         LOGERR("read of '%s' failed with %d (%s) after %llu bytes\n", w->path, errno, strerror(errno),
                (unsigned long long)w->data_sent);
+        if (W)
+            watch_publish(W, wj, need, 1); /* the zeros replace bytes already published */
         return;
     }
     if ((size_t)r < need)
         memset(data + r, 0, need - (size_t)r);
+    if (W)
+        watch_publish(W, wj, MAX_(need, (size_t)r), 0);
 }
 
 static void chunk_sender(const bcp_transport_ops *T, const char *path, const FileInfo *task, TaskInfo ti,

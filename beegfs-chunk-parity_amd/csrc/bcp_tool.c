@@ -14,7 +14,7 @@
  *       persistent state, through the per-rank protocol (default, 12 lanes;
  *       ranks as threads, or with --procs as one process per target, as
  *       under mpirun) or the batched pipeline.  --fold picks the P role's GPU
- *       fold: batched, device-rows, streamed, zero-copy or staged.  A --complete over an existing state needs
+ *       fold: batched, pipelined, device-rows, streamed, zero-copy or staged.  A --complete over an existing state needs
  *       --force and first deletes the old parity data and DBs (the script's
  *       clean_old, :94-108, :120-126).  On success <root>/last-gen-timestamp.
  *   bcp parity-rebuild [--pipeline|--procs] [--fold MODE] [--db DIR] [--corrupt FILE]
@@ -44,7 +44,7 @@ static int usage(void)
           "                      [--changelog DIR] <store_root> <ntargets>\n"
           "       bcp parity-rebuild [--pipeline|--procs] [--fold MODE] [--db DIR] [--corrupt FILE]\n"
           "                          <store_root> <ntargets> <target>\n"
-          "       MODE: batched | device-rows | streamed | zero-copy | staged\n",
+          "       MODE: batched | pipelined | device-rows | streamed | zero-copy | staged\n",
           stderr);
     return 1;
 }
@@ -57,6 +57,8 @@ static int fold_mode_arg(const char *s)
         return BCP_FOLD_STREAMED;
     if (!strcmp(s, "device-rows"))
         return BCP_FOLD_DEVICE_ROWS;
+    if (!strcmp(s, "pipelined"))
+        return BCP_FOLD_PIPELINED;
     if (!strcmp(s, "zero-copy"))
         return BCP_FOLD_ZERO_COPY;
     if (!strcmp(s, "staged"))

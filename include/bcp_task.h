@@ -128,7 +128,19 @@ int bcp_task_set_device_map(const int *devices, int ntargets);
  * output block goes to pinned host memory for the parity write.  No host
  * code reads the rows. */
 #define BCP_FOLD_DEVICE_ROWS 4
+/* PIPELINED: the fold follows the senders' reads.  The P role registers its
+ * window rows; a source filling one directly (send_fill transports) reads
+ * its chunk in 256 KiB pieces and publishes each final prefix, and the lane
+ * launches the fold of every byte range all rows have delivered on its own
+ * queue at once (no sync), so the rows' PCIe reads overlap the file reads;
+ * after the receives, the rest and one sync.  Windows it cannot follow
+ * (multi-window tasks, transports without send_fill) fold like ZERO_COPY. */
+#define BCP_FOLD_PIPELINED 5
 int bcp_task_set_fold_mode(int mode);
+/* PIPELINED counters since the process started: windows folded by following
+ * their rows, and range folds launched for them (ranges / windows > 1: the
+ * fold overlapped the reads). */
+int bcp_task_pipe_stats(uint64_t *windows, uint64_t *ranges);
 /* on = 0 (default): in a gen task with ONE window a source sends its
  * chunk's bytes only and the P role supplies the zeros past them (implicit
  * padding).  on = 1: the reference's wire exactly -- every window
@@ -179,12 +191,15 @@ void bcp_task_set_xor_hook(bcp_xor_hook_fn fn, void *ctx);
  * passes through `site` fail as if the allocation / thread creation had,
  * after `after` passes succeed.  Sites: the P role's fold resources (as
  * -ENOMEM), its single drain row (then a bounded 64 KiB per-thread drain
- * with truncated receives is used), the source role's window buffer, and the
- * runners' lane-thread creation.  count 0 clears the site. */
+ * with truncated receives is used), the source role's window buffer, the
+ * runners' lane-thread creation, and a source's chunk read into a row it
+ * fills directly (as EIO; a source reading in pieces for a PIPELINED P role
+ * fails a piece after the first).  count 0 clears the site. */
 #define BCP_INJECT_FOLD_RES 1
 #define BCP_INJECT_DRAIN_ROW 2
 #define BCP_INJECT_SEND_BUF 4
 #define BCP_INJECT_THREAD 8
+#define BCP_INJECT_READ 16
 int bcp_task_inject_failure(int site, int after, int count);
 
 /* ---- transport seam (the MPI subset process_task speaks) ---------------- */

@@ -45,7 +45,10 @@ static void write_file(const char *path, const uint8_t *d, size_t n)
 int main(int argc, char **argv)
 {
     const char *root = argc > 1 ? argv[1] : "/tmp/bcp_sanitize_store";
-    const int nt = 6, nfiles = 60;
+    /* "pipelined": the P roles fold range by range as the sources publish
+     * pieces (BCP_FOLD_PIPELINED; sources fill from many lanes at once) */
+    const int pipelined = argc > 2 && !strcmp(argv[2], "pipelined");
+    const int nt = 6, nfiles = 60, maxlen = pipelined ? 1200000 : 300000;
     char path[512];
     srand(7);
     bcp_work_item *items = calloc(nfiles, sizeof *items);
@@ -60,7 +63,7 @@ int main(int argc, char **argv)
             if (t == p || (rand() % 4) == 0)
                 continue;
             loc |= 1ull << t;
-            size_t n = (size_t)(rand() % 300000);
+            size_t n = (size_t)(rand() % maxlen);
             uint8_t *d = malloc(n + 1);
             for (size_t j = 0; j < n; j++)
                 d[j] = (uint8_t)rand();
@@ -82,6 +85,8 @@ int main(int argc, char **argv)
         mkdirs(path);
     }
     bcp_task_set_xor_hook(test_cpu_xor, NULL);
+    if (pipelined && bcp_task_set_fold_mode(BCP_FOLD_PIPELINED) < 0)
+        return 3;
     bcp_run_stats st;
     int rc = bcp_gen_run(root, nt, items, nfiles, 12, NULL, NULL, &st);
     if (rc || st.errors) {

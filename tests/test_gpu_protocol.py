@@ -23,11 +23,12 @@ def gpu_fold(bcp, engine):
     bcp.task_shutdown()
 
 
-@pytest.fixture(params=["device_rows", "streamed", "batched", "zero_copy", "staged"])
+@pytest.fixture(params=["pipelined", "device_rows", "streamed", "batched", "zero_copy", "staged"])
 def fold_mode(request, bcp):
     """Every form of the P role's GPU fold (bcp_task_set_fold_mode)."""
     mode = {"batched": bcp.FOLD_BATCHED, "zero_copy": bcp.FOLD_ZERO_COPY, "staged": bcp.FOLD_STAGED,
-            "streamed": bcp.FOLD_STREAMED, "device_rows": bcp.FOLD_DEVICE_ROWS}[request.param]
+            "streamed": bcp.FOLD_STREAMED, "device_rows": bcp.FOLD_DEVICE_ROWS,
+            "pipelined": bcp.FOLD_PIPELINED}[request.param]
     prev = bcp.set_fold_mode(mode)
     yield request.param
     bcp.set_fold_mode(prev)
@@ -209,8 +210,8 @@ def test_zero_copy_pool_reuse_with_changing_data(bcp, oracle, tmp_path):
     between modes: no fold may see a previous task's bytes."""
     root = str(tmp_path)
     rng = np.random.default_rng(77)
-    modes = [bcp.FOLD_ZERO_COPY, bcp.FOLD_DEVICE_ROWS, bcp.FOLD_STAGED, bcp.FOLD_DEVICE_ROWS, bcp.FOLD_DEVICE_ROWS,
-             bcp.FOLD_BATCHED]
+    modes = [bcp.FOLD_ZERO_COPY, bcp.FOLD_DEVICE_ROWS, bcp.FOLD_STAGED, bcp.FOLD_DEVICE_ROWS, bcp.FOLD_PIPELINED,
+             bcp.FOLD_DEVICE_ROWS, bcp.FOLD_BATCHED, bcp.FOLD_PIPELINED]
     for rnd, mode in enumerate(modes):
         files = [(f"z/{i}", [0, 1, 2], 3, [int(x) for x in rng.integers(1, 600_000, size=3)]) for i in range(24)]
         items, contents = S.populate(root, 4, files, seed=100 + rnd)

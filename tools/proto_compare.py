@@ -8,6 +8,9 @@ interleaved in ONE run on ONE box:
   gpu_staged     H2D -> kernel -> D2H per window
   gpu_streamed   each row's data bytes DMA'd to HBM as it arrives, one kernel
                  from HBM into the pinned output
+  gpu_pipelined  the fold follows the senders' reads: each range all rows
+                 have delivered is folded (by the source that completed it)
+                 while the rest is read; the P role folds the tail and syncs
   gpu_device_rows  the rows themselves in device memory the host writes
                  (BCP_FOLD_DEVICE_ROWS): chunk reads store into HBM through
                  the BAR, the fold service's kernel reads HBM
@@ -85,7 +88,7 @@ def fold_setup(fold, hooks):
     if fold.startswith("gpu_"):
         mode = {"gpu_batched": bcp.FOLD_BATCHED, "gpu_zero_copy": bcp.FOLD_ZERO_COPY,
                 "gpu_staged": bcp.FOLD_STAGED, "gpu_streamed": bcp.FOLD_STREAMED,
-                "gpu_device_rows": bcp.FOLD_DEVICE_ROWS}[fold]
+                "gpu_device_rows": bcp.FOLD_DEVICE_ROWS, "gpu_pipelined": bcp.FOLD_PIPELINED}[fold]
         prev = bcp.set_fold_mode(mode)
         return lambda: bcp.set_fold_mode(prev)
     bcp.set_xor_hook(hooks[fold])
@@ -104,11 +107,13 @@ def measure(name, folds, rounds, run_once, verify_fn, nbytes, hooks, extra=None,
             restore = fold_setup(f, hooks)
             try:
                 w0, l0 = bcp.fold_stats()
+                pw0, pr0 = bcp.pipe_stats()
                 bcp.phase_stats(reset=True)
                 t0 = time.perf_counter()
                 st = run_once()
                 dt = time.perf_counter() - t0
                 w1, l1 = bcp.fold_stats()
+                pw1, pr1 = bcp.pipe_stats()
                 ph = bcp.phase_stats()
                 if r > 0:
                     acc = phases.setdefault(f, {})
@@ -123,6 +128,10 @@ def measure(name, folds, rounds, run_once, verify_fn, nbytes, hooks, extra=None,
                 b = batching.setdefault(f, {"windows": 0, "launches": 0})
                 b["windows"] += w1 - w0
                 b["launches"] += l1 - l0
+            if f == "gpu_pipelined" and r > 0:
+                b = batching.setdefault(f, {"windows": 0, "launches": 0})
+                b["windows"] += pw1 - pw0
+                b["launches"] += pr1 - pr0
             if r == rounds and f != "noop":
                 ok, bad = verify_fn()
                 if not ok:
@@ -133,7 +142,9 @@ def measure(name, folds, rounds, run_once, verify_fn, nbytes, hooks, extra=None,
         res[f] = nbytes / warm / GiB
         line = dict(workload=name, fold=f, GiBps=round(res[f], 3), warm_median_s=round(warm, 4),
                     runs_s=[round(x, 4) for x in times[f]], cold_s=round(times[f][0], 4))
-        if batching.get(f, {}).get("launches"):
+        if f == "gpu_pipelined" and batching.get(f, {}).get("windows"):
+            line["range_folds_per_window"] = round(batching[f]["launches"] / batching[f]["windows"], 2)
+        elif batching.get(f, {}).get("launches"):
             line["windows_per_launch"] = round(batching[f]["windows"] / batching[f]["launches"], 2)
         acc = phases.get(f)
         if acc and acc.get("p_tasks"):
@@ -163,7 +174,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--root", default="/dev/shm/bcp_proto")
     ap.add_argument("--rounds", type=int, default=6)
-    ap.add_argument("--folds", default="gpu_device_rows,gpu_streamed,gpu_batched,cpu_reference,noop")
+    ap.add_argument("--folds", default="gpu_pipelined,gpu_batched,gpu_zero_copy,cpu_reference,noop")
     ap.add_argument("--workloads", default="c1_gen,c1_rebuild,c5_gen")
     ap.add_argument("--c1-files", type=int, default=1333)
     ap.add_argument("--c5-stripes", type=int, default=1000)

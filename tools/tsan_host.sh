@@ -1,7 +1,8 @@
 #!/bin/bash
 # ThreadSanitizer run of the host C layer (CPU only): the C sources and a C
 # protocol driver (tests/native/protocol_driver.c: parity gen over 12 lanes x
-# 6 loopback ranks with the CPU test-double fold, then a rebuild) are built
+# 6 loopback ranks with the CPU test-double fold, then a rebuild; again with
+# the pipelined fold) are built
 # with -fsanitize=thread and linked with the uninstrumented HIP objects.  No
 # GPU call is made.
 set -euo pipefail
@@ -24,6 +25,9 @@ gcc -fsanitize=thread -o $B/protocol_driver $B/driver.o $B/hook.o $objs $P/build
   -L/opt/rocm/lib -lamdhip64 -Wl,-rpath,/opt/rocm/lib -lstdc++ -lm -pthread
 rm -rf /tmp/bcp_tsan_store
 TSAN_OPTIONS="halt_on_error=1 second_deadlock_stack=1" $B/protocol_driver /tmp/bcp_tsan_store
+rm -rf /tmp/bcp_tsan_store
+# the pipelined fold: row watches, sources folding the ranges they complete
+TSAN_OPTIONS="halt_on_error=1 second_deadlock_stack=1" $B/protocol_driver /tmp/bcp_tsan_store pipelined
 rm -rf /tmp/bcp_tsan_store
 # ranks as processes: the C caller (its own st2rank / HostState) forks one
 # process per target on the socketpair transport; 3 lanes per rank share
