@@ -93,6 +93,7 @@ typedef struct {
     size_t pitch, nbytes, lo; /* lo: bytes folded or claimed */
     const size_t *valid;
     uint8_t *out;
+    size_t step; /* smallest range folded before the window is complete */
     int n;
 } row_watch;
 
@@ -764,7 +765,7 @@ static int fold_window(fold_res *R, HostState *hs, int mode, bcp_xor_hook_fn hoo
         return hook(out, nbytes, rows, pitch, n, ctx);
     }
     int rc;
-    if (mode == BCP_FOLD_BATCHED || mode == BCP_FOLD_DEVICE_ROWS) {
+    if (mode == BCP_FOLD_BATCHED || mode == BCP_FOLD_DEVICE_ROWS || mode == BCP_FOLD_PIPELINED) {
         /* DEVICE_ROWS: the rows were stored through the BAR by other threads
          * (write-combined); their hand-over to this one passed locked
          * instructions, and this fence drains this thread's own (a socket
@@ -777,7 +778,7 @@ static int fold_window(fold_res *R, HostState *hs, int mode, bcp_xor_hook_fn hoo
     }
     if (!R->q && (rc = bcp_queue_create(R->eng, &R->q)))
         return rc;
-    if (mode == BCP_FOLD_ZERO_COPY || mode == BCP_FOLD_PIPELINED) {
+    if (mode == BCP_FOLD_ZERO_COPY) {
         /* rows and out are mapped pinned memory (grow): the kernel streams
          * row j's data bytes (valid[j]) over PCIe, no copy commands; the
          * zeros past them are the kernel's */
@@ -842,7 +843,7 @@ static int stream_fold(fold_res *R, int n, size_t pitch, const size_t *valid, si
  * file reads; after the receives the P role folds the rest (at least the
  * last piece) and syncs once.  Short kernels only: nothing on the device
  * waits for the host. */
-#define PIPE_STEP ((size_t)128 << 10)   /* smallest range worth a launch */
+#define PIPE_STEP ((size_t)128 << 10)   /* smallest range worth a launch (also >= a quarter window) */
 #define PIPE_ALIGN ((size_t)4096)       /* range boundaries */
 
 static uint64_t g_pipe_windows, g_pipe_ranges; /* bcp_task_pipe_stats */
@@ -881,7 +882,7 @@ static void range_claim(row_watch *w)
         size_t avail = w->nbytes;
         for (int j = 0; j < w->n; j++)
             avail = MIN_(avail, w->prog[j] >= w->valid[j] ? w->nbytes : w->prog[j]);
-        if (avail < w->nbytes && avail < w->lo + PIPE_STEP)
+        if (avail < w->nbytes && avail < w->lo + w->step)
             return;
         const size_t hi = avail >= w->nbytes ? w->nbytes : avail / PIPE_ALIGN * PIPE_ALIGN;
         const int rc = launch_range(w, w->lo, hi);
@@ -907,6 +908,7 @@ static int watch_rows(row_watch *W, fold_res *R, bcp_xor_hook_fn hook, void *hoo
     W->lo = 0;
     W->valid = valid;
     W->out = out;
+    W->step = MAX_(PIPE_STEP, nbytes / 4); /* at most ~5 launches per window */
     W->n = n;
     for (int j = 0; j < n; j++)
         if (watch_add(rows + (size_t)j * pitch, W, j)) {

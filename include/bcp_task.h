@@ -130,11 +130,13 @@ int bcp_task_set_device_map(const int *devices, int ntargets);
 #define BCP_FOLD_DEVICE_ROWS 4
 /* PIPELINED: the fold follows the senders' reads.  The P role registers its
  * window rows; a source filling one directly (send_fill transports) reads
- * its chunk in 256 KiB pieces and publishes each final prefix, and the lane
- * launches the fold of every byte range all rows have delivered on its own
- * queue at once (no sync), so the rows' PCIe reads overlap the file reads;
+ * its chunk in 256 KiB pieces and publishes each final prefix; the source
+ * whose piece completes a byte range of every row (at least 128 KiB and a
+ * quarter window) launches its fold on the lane's queue (no sync), so the
+ * rows' PCIe reads overlap the file reads;
  * after the receives, the rest and one sync.  Windows it cannot follow
- * (multi-window tasks, transports without send_fill) fold like ZERO_COPY. */
+ * (multi-window tasks, transports without send_fill) go to the fold service
+ * as in BATCHED. */
 #define BCP_FOLD_PIPELINED 5
 int bcp_task_set_fold_mode(int mode);
 /* PIPELINED counters since the process started: windows folded by following
