@@ -678,7 +678,7 @@ INJECT_FOLD_RES, INJECT_DRAIN_ROW, INJECT_SEND_BUF, INJECT_THREAD, INJECT_READ =
 
 
 def set_fold_mode(mode: int) -> int:
-    """P-role fold: FOLD_BATCHED (default), FOLD_DEVICE_ROWS, FOLD_STREAMED, FOLD_ZERO_COPY or
+    """P-role fold: FOLD_PIPELINED (default), FOLD_BATCHED, FOLD_DEVICE_ROWS, FOLD_STREAMED, FOLD_ZERO_COPY or
     FOLD_STAGED; returns the previous mode."""
     rc = lib().bcp_task_set_fold_mode(mode)
     if rc < 0:

@@ -64,7 +64,7 @@ static int g_devmap[MAX_STORAGE_TARGETS];
 static int g_devmap_n = 0;
 static bcp_xor_hook_fn g_hook = NULL;
 static void *g_hook_ctx = NULL;
-static int g_fold_mode = BCP_FOLD_BATCHED;
+static int g_fold_mode = BCP_FOLD_PIPELINED;
 static int g_explicit_pad = 0; /* 1: sources pad every window, as the reference does */
 static bcp_transport_ops g_tp;
 static int g_tp_set = 0;

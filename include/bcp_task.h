@@ -108,8 +108,8 @@ int bcp_task_set_device_map(const int *devices, int ntargets);
  * EVERY window the P roles of this process have pending as ONE descriptor
  * batch (zero-copy rows, data bytes only) and wakes each lane when its own
  * window is done (process_task stays synchronous per task, as the
- * reference's window loop is, task_processing.c:203-226).  Returns the
- * previous mode, or -EINVAL. */
+ * reference's window loop is, task_processing.c:203-226).  Default:
+ * PIPELINED (below).  Returns the previous mode, or -EINVAL. */
 #define BCP_FOLD_ZERO_COPY 0
 #define BCP_FOLD_STAGED 1
 #define BCP_FOLD_BATCHED 2

@@ -85,7 +85,7 @@ int main(int argc, char **argv)
         mkdirs(path);
     }
     bcp_task_set_xor_hook(test_cpu_xor, NULL);
-    if (pipelined && bcp_task_set_fold_mode(BCP_FOLD_PIPELINED) < 0)
+    if (bcp_task_set_fold_mode(pipelined ? BCP_FOLD_PIPELINED : BCP_FOLD_BATCHED) < 0)
         return 3;
     bcp_run_stats st;
     int rc = bcp_gen_run(root, nt, items, nfiles, 12, NULL, NULL, &st);

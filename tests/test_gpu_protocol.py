@@ -334,7 +334,8 @@ print("pool ok")
 def test_rank_pool_on_device(tmp_path):
     """Rank processes kept alive across runs with their HIP contexts: two gen
     runs over different data and a rebuild through ONE pool, the P roles
-    folding on the device (default batched service), parity and rebuilt
+    folding on the device (default mode: rank processes on sockets fold
+    through the batched service), parity and rebuilt
     chunks checked against the oracle.  In a fresh process: a pool cannot be
     forked from one that has used the GPU."""
     import subprocess
