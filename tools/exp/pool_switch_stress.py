@@ -69,10 +69,10 @@ def main():
     a = ap.parse_args()
     bcp.set_xor_hook(None)
     rng = np.random.default_rng(77)
-    cycle = [bcp.FOLD_ZERO_COPY, bcp.FOLD_DEVICE_ROWS, bcp.FOLD_STAGED, bcp.FOLD_DEVICE_ROWS, bcp.FOLD_BATCHED,
-             bcp.FOLD_STREAMED]
+    cycle = [bcp.FOLD_ZERO_COPY, bcp.FOLD_DEVICE_ROWS, bcp.FOLD_STAGED, bcp.FOLD_PIPELINED, bcp.FOLD_DEVICE_ROWS,
+             bcp.FOLD_BATCHED, bcp.FOLD_STREAMED, bcp.FOLD_PIPELINED]
     names = {bcp.FOLD_ZERO_COPY: "zero_copy", bcp.FOLD_DEVICE_ROWS: "device_rows", bcp.FOLD_STAGED: "staged",
-             bcp.FOLD_BATCHED: "batched", bcp.FOLD_STREAMED: "streamed"}
+             bcp.FOLD_BATCHED: "batched", bcp.FOLD_STREAMED: "streamed", bcp.FOLD_PIPELINED: "pipelined"}
     fails = 0
     for rnd in range(a.rounds):
         mode = cycle[rnd % len(cycle)]
