@@ -328,6 +328,11 @@ def main():
     ap.add_argument("--verify", type=int, default=20)
     ap.add_argument("--keep", action="store_true")
     a = ap.parse_args()
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import box_probe
+    box = box_probe.cpu_info()
+    box.update(box_probe.pcie_rates(bcp))
+    emit(box=box)
     if a.ndevices <= 0:
         a.ndevices = max(1, bcp.device_count())
     ok = True

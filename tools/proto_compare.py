@@ -211,6 +211,11 @@ def main():
              "noop": ctypes.cast(noop.noop_fold, ctypes.c_void_p).value}
     rng = np.random.default_rng(0)
     wl = a.workloads.split(",")
+    import box_probe
+    box = box_probe.cpu_info()
+    if not (a.procs or a.procs_cold):  # rank processes need a parent that never touched the GPU
+        box.update(box_probe.pcie_rates(bcp))
+    emit(box=box)
     tr = {"transport": "socketpair rank processes, pooled" if a.procs else
           "socketpair rank processes, forked per run" if a.procs_cold else "loopback threads"}
     if "c1_gen" in wl or "c1_rebuild" in wl:
