@@ -65,7 +65,8 @@ def main():
         rel = lambda p: os.path.relpath(p, ROOT)  # noqa: E731
         subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pmc_summary.py"), "--fetch", fetch, "--write", write,
                         "--kernel", tag, "--workload-key", wkey, "--algorithmic", str(cfg["bytes_per_step_per_gpu"]),
-                        "--stats", rel(stats), "--commit", a.commit, "--files", rel(fetch), rel(write), rel(bench),
+                        "--stats", rel(stats), "--commit", a.commit, "--files", rel(fetch), rel(write),
+                        rel(os.path.join(a.dst, f"bench_{m}.json")),  # the committed copy of the bench line
                         "--out", os.path.join(a.dst, f"pmc_{m}.json")], check=True)
 
 
