@@ -94,13 +94,16 @@ def config1(a):
     rd, wr = total_bytes(root, files)
     rng = np.random.default_rng(0)
 
+    def reset_parity():
+        for p in range(4):
+            shutil.rmtree(os.path.join(root, f"st{p}", "parity"), ignore_errors=True)
+            os.makedirs(os.path.join(root, f"st{p}", "parity"))
+
     def run(label, fn):
         """first (cold: pinning, queues) run, then a.reps warm runs; median reported."""
         times = []
         for r in range(1 + a.reps):
-            for p in range(4):
-                shutil.rmtree(os.path.join(root, f"st{p}", "parity"), ignore_errors=True)
-                os.makedirs(os.path.join(root, f"st{p}", "parity"))
+            reset_parity()
             t0 = time.perf_counter()
             st = fn()
             times.append(time.perf_counter() - t0)
@@ -111,18 +114,36 @@ def config1(a):
              bytes_read=rd, bytes_written=wr, tasks=int(st.tasks), errors=int(st.errors), verified=ok, bad=bad)
         return ok
 
-    ok = run("protocol_gpu_fold(bcp_gen_run,12 lanes)", lambda: bcp.gen_run(root, 4, items, nlanes=12))
-    bcp.set_fold_mode(bcp.FOLD_STAGED)
-    try:
-        ok &= run("protocol_gpu_fold_staged(H2D,kernel,D2H; 12 lanes)", lambda: bcp.gen_run(root, 4, items, nlanes=12))
-    finally:
-        bcp.set_fold_mode(bcp.FOLD_ZERO_COPY)
+    # the per-task protocol with three folds, interleaved in rotating order
+    # (one cold round, then a.reps warm ones) so host drift lands on all
     ol = oracle.lib()
-    bcp.set_xor_hook(ctypes.cast(ol.oracle_xor_rows, ctypes.c_void_p).value)
-    try:
-        ok &= run("protocol_cpu_fold_reference(oracle_xor_rows,12 lanes)", lambda: bcp.gen_run(root, 4, items, nlanes=12))
-    finally:
-        bcp.set_xor_hook(None)
+    cpu_fold = ctypes.cast(ol.oracle_xor_rows, ctypes.c_void_p).value
+    variants = [("protocol_gpu_fold(bcp_gen_run,12 lanes)", None, None),
+                ("protocol_gpu_fold_staged(H2D,kernel,D2H; 12 lanes)", bcp.FOLD_STAGED, None),
+                ("protocol_cpu_fold_reference(oracle_xor_rows,12 lanes)", None, cpu_fold)]
+    times = {v[0]: [] for v in variants}
+    ok = True
+    for r in range(1 + a.reps):
+        for label, mode, hook in variants[r % 3:] + variants[:r % 3]:
+            reset_parity()
+            prev = bcp.set_fold_mode(mode) if mode is not None else None
+            bcp.set_xor_hook(hook)
+            try:
+                t0 = time.perf_counter()
+                st = bcp.gen_run(root, 4, items, nlanes=12)
+                times[label].append(time.perf_counter() - t0)
+            finally:
+                bcp.set_xor_hook(None)
+                if prev is not None:
+                    bcp.set_fold_mode(prev)
+            if r == a.reps:
+                okv, badv = verify(root, files, contents, a.verify, rng)
+                ok &= okv
+                warm = float(np.median(times[label][1:])) if a.reps else times[label][0]
+                emit(config=1, path=label, cold_seconds=round(times[label][0], 3), warm_seconds=round(warm, 3),
+                     GiBps=round((rd + wr) / warm / GiB, 3), runs_s=[round(x, 4) for x in times[label]],
+                     bytes_read=rd, bytes_written=wr, tasks=int(st.tasks), errors=int(st.errors), verified=okv,
+                     bad=badv, order="interleaved")
     pl = bcp.Pipeline(io_threads=a.io_threads, ndevices=a.ndevices)
     ok &= run(f"pipeline(bcp_pipeline_run,{a.ndevices} GPU)", lambda: pl.run(root, 4, items))
     pl.close()
@@ -153,37 +174,44 @@ def config1(a):
             os.remove(lost[path])
     rb_bytes = len(lost) * 3 * (512 * KiB) + len(lost) * 512 * KiB
 
-    def rebuild_protocol(label):
-        """single lane, as rebuild/main.c; cold run then a.reps warm runs"""
-        times = []
-        for r in range(1 + a.reps):
-            for fn in lost.values():
-                if os.path.exists(fn):
-                    os.remove(fn)
-            t0 = time.perf_counter()
-            st = bcp.rebuild_run(root, 4, 2, items)
-            times.append(time.perf_counter() - t0)
-        dt = float(np.median(times[1:])) if a.reps else times[0]
+    def drop_lost():
+        for fn in lost.values():
+            if os.path.exists(fn):
+                os.remove(fn)
+
+    def rebuilt_ok():
         good = 0
         for k, (path, fn) in enumerate(lost.items()):
             if k % max(1, len(lost) // a.verify) == 0:
                 holders = next(h for pth, h, _, _ in files if pth == path)
                 good += S.read_file(fn) == contents[path][holders.index(2)].tobytes()
-        emit(config=1, path=label, cold_seconds=round(times[0], 3), warm_seconds=round(dt, 3),
-             GiBps=round(rb_bytes / dt / GiB, 3), rebuilt=len(lost), errors=int(st.errors), sampled_ok=good)
-        return good == len(range(0, len(lost), max(1, len(lost) // a.verify)))
+        return good, good == len(range(0, len(lost), max(1, len(lost) // a.verify)))
 
-    ok &= rebuild_protocol("rebuild_protocol_gpu_fold(bcp_rebuild_run)")
-    bcp.set_fold_mode(bcp.FOLD_STAGED)
-    try:
-        ok &= rebuild_protocol("rebuild_protocol_gpu_fold_staged(bcp_rebuild_run)")
-    finally:
-        bcp.set_fold_mode(bcp.FOLD_ZERO_COPY)
-    bcp.set_xor_hook(ctypes.cast(ol.oracle_xor_rows, ctypes.c_void_p).value)
-    try:
-        ok &= rebuild_protocol("rebuild_protocol_cpu_fold_reference(oracle_xor_rows)")
-    finally:
-        bcp.set_xor_hook(None)
+    # single lane, as rebuild/main.c; the three folds interleaved in rotating order
+    rvariants = [("rebuild_protocol_gpu_fold(bcp_rebuild_run)", None, None),
+                 ("rebuild_protocol_gpu_fold_staged(bcp_rebuild_run)", bcp.FOLD_STAGED, None),
+                 ("rebuild_protocol_cpu_fold_reference(oracle_xor_rows)", None, cpu_fold)]
+    rtimes = {v[0]: [] for v in rvariants}
+    for r in range(1 + a.reps):
+        for label, mode, hook in rvariants[r % 3:] + rvariants[:r % 3]:
+            drop_lost()
+            prev = bcp.set_fold_mode(mode) if mode is not None else None
+            bcp.set_xor_hook(hook)
+            try:
+                t0 = time.perf_counter()
+                st = bcp.rebuild_run(root, 4, 2, items)
+                rtimes[label].append(time.perf_counter() - t0)
+            finally:
+                bcp.set_xor_hook(None)
+                if prev is not None:
+                    bcp.set_fold_mode(prev)
+            if r == a.reps:
+                good, okv = rebuilt_ok()
+                ok &= okv
+                dt = float(np.median(rtimes[label][1:])) if a.reps else rtimes[label][0]
+                emit(config=1, path=label, cold_seconds=round(rtimes[label][0], 3), warm_seconds=round(dt, 3),
+                     GiBps=round(rb_bytes / dt / GiB, 3), runs_s=[round(x, 4) for x in rtimes[label]],
+                     rebuilt=len(lost), errors=int(st.errors), sampled_ok=good, order="interleaved")
     # the same rebuild through the batched pipeline (warm median of a.reps)
     pl = bcp.Pipeline(io_threads=a.io_threads, ndevices=a.ndevices)
     ordered = sorted(items, key=lambda x: x[0].encode())
@@ -229,30 +257,34 @@ def config5(a):
     items = [(path, ts0, S.with_p(sum(1 << h for h in holders), p)) for path, holders, p, _ in files]
     rd, wr = total_bytes(root, files)
     ok_proto = True
-    # full generation through the per-task protocol first (12 lanes), GPU
-    # fold against the reference CPU fold: 8 rows of up to 4 MiB per window
+    # full generation through the per-task protocol first (12 lanes), the
+    # default GPU fold against the reference CPU fold, interleaved: 8 rows of
+    # up to 4 MiB per window
     ol = oracle.lib()
-    for label, hook in (("protocol_gpu_fold(bcp_gen_run,12 lanes)", None),
-                        ("protocol_cpu_fold_reference(oracle_xor_rows,12 lanes)",
-                         ctypes.cast(ol.oracle_xor_rows, ctypes.c_void_p).value)):
-        bcp.set_xor_hook(hook)
-        try:
-            times = []
-            for r in range(1 + a.reps):
-                for k in range(ntargets):
-                    shutil.rmtree(os.path.join(root, f"st{k}", "parity"), ignore_errors=True)
-                    os.makedirs(os.path.join(root, f"st{k}", "parity"))
+    pvariants = [("protocol_gpu_fold(bcp_gen_run,12 lanes)", None),
+                 ("protocol_cpu_fold_reference(oracle_xor_rows,12 lanes)",
+                  ctypes.cast(ol.oracle_xor_rows, ctypes.c_void_p).value)]
+    ptimes = {v[0]: [] for v in pvariants}
+    for r in range(1 + a.reps):
+        for label, hook in pvariants[r % 2:] + pvariants[:r % 2]:
+            for k in range(ntargets):
+                shutil.rmtree(os.path.join(root, f"st{k}", "parity"), ignore_errors=True)
+                os.makedirs(os.path.join(root, f"st{k}", "parity"))
+            bcp.set_xor_hook(hook)
+            try:
                 t0 = time.perf_counter()
                 st = bcp.gen_run(root, ntargets, items, nlanes=12)
-                times.append(time.perf_counter() - t0)
-        finally:
-            bcp.set_xor_hook(None)
-        dtp = float(np.median(times[1:])) if a.reps else times[0]
-        okp, badp = verify(root, files, contents, a.verify, rng)
-        ok_proto &= okp
-        emit(config=5, path=label, cold_seconds=round(times[0], 3), warm_seconds=round(dtp, 3),
-             GiBps=round((rd + wr) / dtp / GiB, 3), bytes_read=rd, bytes_written=wr, tasks=int(st.tasks),
-             errors=int(st.errors), verified=okp, bad=badp)
+                ptimes[label].append(time.perf_counter() - t0)
+            finally:
+                bcp.set_xor_hook(None)
+            if r == a.reps:
+                okp, badp = verify(root, files, contents, a.verify, rng)
+                ok_proto &= okp
+                dtp = float(np.median(ptimes[label][1:])) if a.reps else ptimes[label][0]
+                emit(config=5, path=label, cold_seconds=round(ptimes[label][0], 3), warm_seconds=round(dtp, 3),
+                     GiBps=round((rd + wr) / dtp / GiB, 3), runs_s=[round(x, 4) for x in ptimes[label]],
+                     bytes_read=rd, bytes_written=wr, tasks=int(st.tasks), errors=int(st.errors), verified=okp,
+                     bad=badp, order="interleaved")
     bcp.task_shutdown()  # the protocol's engine goes before the pipeline's comes
     pl = bcp.Pipeline(io_threads=a.io_threads, ndevices=a.ndevices)
     times = []
