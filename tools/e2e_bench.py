@@ -123,7 +123,8 @@ def config1(a):
                 ("protocol_cpu_fold_reference(oracle_xor_rows,12 lanes)", None, cpu_fold)]
     times = {v[0]: [] for v in variants}
     ok = True
-    for r in range(1 + a.reps):
+    preps = max(a.reps, 7)  # ~0.1 s runs: more rounds than the other measurements
+    for r in range(1 + preps):
         for label, mode, hook in variants[r % 3:] + variants[:r % 3]:
             reset_parity()
             prev = bcp.set_fold_mode(mode) if mode is not None else None
@@ -136,10 +137,10 @@ def config1(a):
                 bcp.set_xor_hook(None)
                 if prev is not None:
                     bcp.set_fold_mode(prev)
-            if r == a.reps:
+            if r == preps:
                 okv, badv = verify(root, files, contents, a.verify, rng)
                 ok &= okv
-                warm = float(np.median(times[label][1:])) if a.reps else times[label][0]
+                warm = float(np.median(times[label][1:]))
                 emit(config=1, path=label, cold_seconds=round(times[label][0], 3), warm_seconds=round(warm, 3),
                      GiBps=round((rd + wr) / warm / GiB, 3), runs_s=[round(x, 4) for x in times[label]],
                      bytes_read=rd, bytes_written=wr, tasks=int(st.tasks), errors=int(st.errors), verified=okv,
@@ -192,7 +193,7 @@ def config1(a):
                  ("rebuild_protocol_gpu_fold_staged(bcp_rebuild_run)", bcp.FOLD_STAGED, None),
                  ("rebuild_protocol_cpu_fold_reference(oracle_xor_rows)", None, cpu_fold)]
     rtimes = {v[0]: [] for v in rvariants}
-    for r in range(1 + a.reps):
+    for r in range(1 + preps):
         for label, mode, hook in rvariants[r % 3:] + rvariants[:r % 3]:
             drop_lost()
             prev = bcp.set_fold_mode(mode) if mode is not None else None
@@ -205,10 +206,10 @@ def config1(a):
                 bcp.set_xor_hook(None)
                 if prev is not None:
                     bcp.set_fold_mode(prev)
-            if r == a.reps:
+            if r == preps:
                 good, okv = rebuilt_ok()
                 ok &= okv
-                dt = float(np.median(rtimes[label][1:])) if a.reps else rtimes[label][0]
+                dt = float(np.median(rtimes[label][1:]))
                 emit(config=1, path=label, cold_seconds=round(rtimes[label][0], 3), warm_seconds=round(dt, 3),
                      GiBps=round(rb_bytes / dt / GiB, 3), runs_s=[round(x, 4) for x in rtimes[label]],
                      rebuilt=len(lost), errors=int(st.errors), sampled_ok=good, order="interleaved")
@@ -265,7 +266,8 @@ def config5(a):
                  ("protocol_cpu_fold_reference(oracle_xor_rows,12 lanes)",
                   ctypes.cast(ol.oracle_xor_rows, ctypes.c_void_p).value)]
     ptimes = {v[0]: [] for v in pvariants}
-    for r in range(1 + a.reps):
+    preps = max(a.reps, 5)
+    for r in range(1 + preps):
         for label, hook in pvariants[r % 2:] + pvariants[:r % 2]:
             for k in range(ntargets):
                 shutil.rmtree(os.path.join(root, f"st{k}", "parity"), ignore_errors=True)
@@ -277,10 +279,10 @@ def config5(a):
                 ptimes[label].append(time.perf_counter() - t0)
             finally:
                 bcp.set_xor_hook(None)
-            if r == a.reps:
+            if r == preps:
                 okp, badp = verify(root, files, contents, a.verify, rng)
                 ok_proto &= okp
-                dtp = float(np.median(ptimes[label][1:])) if a.reps else ptimes[label][0]
+                dtp = float(np.median(ptimes[label][1:]))
                 emit(config=5, path=label, cold_seconds=round(ptimes[label][0], 3), warm_seconds=round(dtp, 3),
                      GiBps=round((rd + wr) / dtp / GiB, 3), runs_s=[round(x, 4) for x in ptimes[label]],
                      bytes_read=rd, bytes_written=wr, tasks=int(st.tasks), errors=int(st.errors), verified=okp,
