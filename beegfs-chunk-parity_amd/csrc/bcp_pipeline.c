@@ -704,6 +704,26 @@ static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, 
     }
     in_cap = pl->in_cap;
     out_cap = pl->out_cap;
+    /* A small job (a changelog round's subset) cut at slab capacity makes a
+     * few big batches whose reads, copies, fold and writes barely overlap:
+     * aim for >= 4 batches per slot and device, >= 16 MiB each, never above
+     * the slab (the largest task still fits, ensure_slots above). */
+    uint64_t plan_in = in_cap;
+    {
+        uint64_t total_in = 0, max_in = 0;
+        for (size_t i = 0; i < nt; i++) {
+            uint64_t in = 0;
+            for (int k = 0; k < tasks[i].n; k++)
+                in += RUP(tasks[i].size[k]);
+            total_in += in;
+            max_in = in > max_in ? in : max_in;
+        }
+        const uint64_t want = (uint64_t)4 * (uint64_t)nslots * (uint64_t)pl->ndev;
+        uint64_t per = total_in / want + 1;
+        per = per < ((uint64_t)16 << 20) ? ((uint64_t)16 << 20) : per;
+        plan_in = per < plan_in ? per : plan_in;
+        plan_in = plan_in < max_in ? max_in : plan_in;
+    }
     int nbatches = 0;
     {
         uint64_t in_used = 0, out_used = 0;
@@ -712,7 +732,7 @@ static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, 
             uint64_t in = 0;
             for (int k = 0; k < t->n; k++)
                 in += RUP(t->size[k]);
-            if (i == 0 || in_used + in > in_cap || out_used + RUP(t->out_len) > out_cap) {
+            if (i == 0 || in_used + in > plan_in || out_used + RUP(t->out_len) > out_cap) {
                 nbatches++;
                 in_used = out_used = 0;
             }
