@@ -705,9 +705,12 @@ static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, 
     in_cap = pl->in_cap;
     out_cap = pl->out_cap;
     /* A small job (a changelog round's subset) cut at slab capacity makes a
-     * few big batches whose reads, copies, fold and writes barely overlap:
-     * aim for >= 4 batches per slot and device, >= 16 MiB each, never above
-     * the slab (the largest task still fits, ensure_slots above). */
+     * few big batches: on ndev GPUs (batches go round-robin) most devices
+     * would idle -- a 1 GiB round is 4 batches of 256 MiB for 8 GPUs.  Aim
+     * for >= 4 batches per slot and device, >= 16 MiB each, never above the
+     * slab (the largest task still fits, ensure_slots above).  On one GPU
+     * this changed nothing measurable (r2av: the round's pipeline 48 ms vs
+     * 46 before). */
     uint64_t plan_in = in_cap;
     {
         uint64_t total_in = 0, max_in = 0;
