@@ -85,10 +85,8 @@ typedef struct {
     size_t prog[MAX_STORAGE_TARGETS];
     int redo; /* a published prefix was replaced (read error: zeros): fold it all again */
     int err;  /* first range-fold launch error */
-    /* the window's fold: whoever completes a range launches it (range_claim)
-     * on the device's shared range queue PQ; the P role waits on R's event */
+    /* the window's fold: whoever completes a range launches it (range_claim) */
     struct fold_res *R;
-    struct pipe_queue *PQ;
     bcp_xor_hook_fn hook;
     void *hook_ctx;
     const uint8_t *rows;
@@ -343,12 +341,6 @@ typedef struct fold_job {
 } fold_job;
 
 #define MAX_INFLIGHT 16
-#define PIPE_QUEUES 4 /* per device: the queues every lane's PIPELINED range folds share */
-
-typedef struct pipe_queue {
-    bcp_queue *q;
-    pthread_mutex_t mu; /* launches and event records on q, from any lane's thread */
-} pipe_queue;
 
 typedef struct {
     bcp_queue *q;
@@ -366,8 +358,6 @@ typedef struct {
     pthread_mutex_t mu;
     fold_job *head, *tail;
     uint64_t windows, launches;
-    pipe_queue pq[PIPE_QUEUES]; /* made on first use */
-    unsigned pq_next;
 } fold_svc;
 
 static fold_svc *g_svc[MAX_DEVICES];
@@ -444,11 +434,6 @@ static void svc_destroy(fold_svc *S)
         free(S->slot[i].st);
         free(S->slot[i].so);
     }
-    for (int i = 0; i < PIPE_QUEUES; i++) {
-        if (S->pq[i].q)
-            bcp_queue_destroy(S->pq[i].q);
-        pthread_mutex_destroy(&S->pq[i].mu);
-    }
     pthread_mutex_destroy(&S->mu);
     free(S);
 }
@@ -467,8 +452,6 @@ static int svc_get(int dev, bcp_engine *e, fold_svc **out)
             S->eng = e;
             S->max_inflight = g_fold_inflight;
             pthread_mutex_init(&S->mu, NULL);
-            for (int i = 0; i < PIPE_QUEUES; i++)
-                pthread_mutex_init(&S->pq[i].mu, NULL);
             g_svc[dev] = S;
         }
     }
@@ -481,18 +464,6 @@ static int svc_get(int dev, bcp_engine *e, fold_svc **out)
  * folded, and the lane at the head of the pending list to lead the next
  * batch -- not every waiting lane (up to 12 lanes x every rank) on every
  * completion. */
-/* The next of the device's shared range queues (round robin), made on
- * first use; NULL if it cannot be made. */
-static pipe_queue *pipe_queue_get(fold_svc *S)
-{
-    pthread_mutex_lock(&S->mu);
-    pipe_queue *P = &S->pq[S->pq_next++ % PIPE_QUEUES];
-    if (!P->q && bcp_queue_create(S->eng, &P->q))
-        P = NULL;
-    pthread_mutex_unlock(&S->mu);
-    return P;
-}
-
 static int fold_batched(fold_svc *S, const uint8_t *rows, size_t pitch, const size_t *valid, size_t nbytes, int n,
                         uint8_t *out)
 {
@@ -574,7 +545,6 @@ typedef struct fold_res {
     int device;         /* -1: host-only (hook) */
     bcp_engine *eng;
     bcp_queue *q;       /* ZERO_COPY / STAGED only */
-    bcp_event *ev;      /* PIPELINED: the window's last range fold */
     uint8_t *h_win[2];  /* window rows [n][pitch] (pinned + mapped when device >= 0) */
     int rows_dev;       /* h_win are device memory the host writes (DEVICE_ROWS) */
     uint8_t *h_par;     /* fold output */
@@ -622,8 +592,6 @@ static void res_destroy(fold_res *R)
             bcp_dev_free(R->eng, R->d_out);
         if (R->q)
             bcp_queue_destroy(R->q);
-        if (R->ev)
-            bcp_event_destroy(R->ev);
     }
     free(R);
 }
@@ -889,10 +857,10 @@ int bcp_task_pipe_stats(uint64_t *windows, uint64_t *ranges)
     return 0;
 }
 
-/* Fold out[lo, hi) = XOR of the rows' [lo, hi) on the window's shared range
- * queue, no sync (under the test hook: the hook, at once, over whole rows
- * whose padding the P role zeroed before the receives).  Launches on a
- * shared queue are serialized by its mutex (lock order: w->mu, then it). */
+/* Fold out[lo, hi) = XOR of the rows' [lo, hi) on the lane's queue, no sync
+ * (under the test hook: the hook, at once, over whole rows whose padding the
+ * P role zeroed before the receives).  Callers hold w->mu: the queue is one
+ * lane's, and launches on it must not interleave. */
 static int launch_range(const row_watch *w, size_t lo, size_t hi)
 {
     __atomic_fetch_add(&g_pipe_ranges, 1, __ATOMIC_RELAXED);
@@ -904,10 +872,7 @@ static int launch_range(const row_watch *w, size_t lo, size_t hi)
         const size_t len = w->valid[j] > lo ? MIN_(w->valid[j], hi) - lo : 0;
         so[j] = (bcp_source){(uint64_t)(uintptr_t)(w->rows + (size_t)j * w->pitch + lo), len};
     }
-    pthread_mutex_lock(&w->PQ->mu);
-    const int rc = bcp_xor_stripes_async(w->PQ->q, &st, 1, so, (uint32_t)w->n);
-    pthread_mutex_unlock(&w->PQ->mu);
-    return rc;
+    return bcp_xor_stripes_async(w->R->q, &st, 1, so, (uint32_t)w->n);
 }
 
 /* Under w->mu: launch every range all rows have delivered past w->lo. */
@@ -928,14 +893,13 @@ static void range_claim(row_watch *w)
     }
 }
 
-static int watch_rows(row_watch *W, fold_res *R, pipe_queue *PQ, bcp_xor_hook_fn hook, void *hook_ctx,
-                      const uint8_t *rows, size_t pitch, const size_t *valid, int n, size_t nbytes, uint8_t *out)
+static int watch_rows(row_watch *W, fold_res *R, bcp_xor_hook_fn hook, void *hook_ctx, const uint8_t *rows,
+                      size_t pitch, const size_t *valid, int n, size_t nbytes, uint8_t *out)
 {
     pthread_mutex_init(&W->mu, NULL);
     memset(W->prog, 0, sizeof(W->prog));
     W->redo = W->err = 0;
     W->R = R;
-    W->PQ = PQ;
     W->hook = hook;
     W->hook_ctx = hook_ctx;
     W->rows = rows;
@@ -969,19 +933,7 @@ static int finish_rows(row_watch *W, int fold)
     __atomic_fetch_add(&g_pipe_windows, 1, __ATOMIC_RELAXED);
     if (fold && !rc && lo < W->nbytes)
         rc = launch_range(W, lo, W->nbytes);
-    int src = 0;
-    if (!W->hook) {
-        /* wait for this window's ranges only: an event after its last one */
-        pthread_mutex_lock(&W->PQ->mu);
-        int erc = bcp_event_record(W->R->ev, W->PQ->q);
-        if (erc)
-            src = bcp_queue_sync(W->PQ->q); /* no event: wait for the queue */
-        pthread_mutex_unlock(&W->PQ->mu);
-        if (!erc)
-            src = bcp_event_sync(W->R->ev);
-        else if (!src)
-            src = erc;
-    }
+    const int src = W->hook ? 0 : bcp_queue_sync(W->R->q);
     pthread_mutex_destroy(&W->mu);
     return rc ? rc : src;
 }
@@ -1274,13 +1226,8 @@ static void parity_generator(const bcp_transport_ops *T, const char *path, const
     /* PIPELINED: one window whose rows the sources fill directly (send_fill
      * transports); otherwise it folds like ZERO_COPY */
     int pipelined = mode == BCP_FOLD_PIPELINED && !res_rc && expected_messages == 1 && T->send_fill;
-    pipe_queue *PQ = NULL;
-    if (pipelined && !hook) {
-        fold_svc *S = NULL;
-        if (svc_get(L->device, L->eng, &S) || !(PQ = pipe_queue_get(S)) ||
-            (!L->ev && bcp_event_create(L->eng, &L->ev)))
-            pipelined = 0;
-    }
+    if (pipelined && !hook && !L->q && bcp_queue_create(L->eng, &L->q))
+        pipelined = 0;
     phase_add(BCP_PHASE_P_OPEN, &tph);
     if (res_rc) {
         int drc = drain_windows(T, ranks, n, buffer_size, expected_messages, ti.tag);
@@ -1314,7 +1261,7 @@ static void parity_generator(const bcp_transport_ops *T, const char *path, const
                     if (valid[j] < buffer_size)
                         memset(win_a + (size_t)j * pitch + valid[j], 0, buffer_size - valid[j]);
             watched = pipelined && !have_had_error &&
-                      watch_rows(&W, L, PQ, hook, hook_ctx, win_a, pitch, valid, n, buffer_size, pblk);
+                      watch_rows(&W, L, hook, hook_ctx, win_a, pitch, valid, n, buffer_size, pblk);
             trc = post_recvs(T, req, n, win_a, pitch, buffer_size, ranks, ti.tag);
         }
         int w = 0, crc = 0;
