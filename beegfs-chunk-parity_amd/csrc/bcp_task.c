@@ -99,6 +99,20 @@ typedef struct {
 
 #define WATCH_SLOTS 4096u
 #define WATCH_PIECE ((size_t)256 << 10) /* bytes a source reads between publishes */
+
+/* experiment knob BCP_PIPE_PIECE (bytes, >= 64 KiB): the piece size */
+static size_t watch_piece(void)
+{
+    static size_t piece;
+    size_t p = __atomic_load_n(&piece, __ATOMIC_RELAXED);
+    if (!p) {
+        const char *v = getenv("BCP_PIPE_PIECE");
+        p = v ? (size_t)strtoull(v, NULL, 0) : WATCH_PIECE;
+        p = p < ((size_t)64 << 10) ? WATCH_PIECE : p;
+        __atomic_store_n(&piece, p, __ATOMIC_RELAXED);
+    }
+    return p;
+}
 typedef struct {
     const void *row;
     row_watch *w;
@@ -1402,7 +1416,7 @@ static void fill_bytes(window_fill *w, uint8_t *data, size_t n)
         r = 0;
         while (got < want) {
             ssize_t k = got && bcpi_inject_hit(BCP_INJECT_READ) ? (errno = EIO, -1)
-                                                                : read(w->fd, data + got, MIN_(WATCH_PIECE, want - got));
+                                                                : read(w->fd, data + got, MIN_(watch_piece(), want - got));
             if (k <= 0) {
                 r = k < 0 ? k : (ssize_t)got;
                 break;
