@@ -225,6 +225,35 @@ def test_zero_copy_pool_reuse_with_changing_data(bcp, oracle, tmp_path):
             assert S.read_file(S.parity_path(root, p, path)) == oracle.gen_parity_file(contents[path]), (rnd, path)
 
 
+def test_pipelined_read_error_refold_on_device(bcp, oracle, tmp_path):
+    """The pipelined fold on the device when a source's read fails after
+    ranges of its row were already folded (in flight on the lane's queue):
+    the P role refolds the whole window, the failed row counts as zeros (the
+    reference's zero-filled window), the source's rank is in error."""
+    KiBl, MiBl = 1024, 1024 * 1024
+    root = str(tmp_path)
+    lens = [7, 100 * KiBl, 4 * MiBl + 3]
+    items, contents = S.populate(root, 4, [("e/x", [0, 1, 2], 3, lens)], seed=6)
+    prev = bcp.set_fold_mode(bcp.FOLD_PIPELINED)
+    bcp.inject_failure(bcp.INJECT_READ, 10, 1)
+    try:
+        st = bcp.gen_run(root, 4, items, nlanes=1)
+    finally:
+        bcp.inject_failure(bcp.INJECT_READ, 0, 0)
+        bcp.set_fold_mode(prev)
+    assert st.errors == 1
+    pf = S.read_file(S.parity_path(root, 3, "e/x"))
+    assert np.frombuffer(pf[:24], "<u8").tolist() == lens
+    expect = np.zeros(max(lens), np.uint8)
+    for c in contents["e/x"][:2]:
+        expect[:c.size] ^= c
+    assert np.array_equal(np.frombuffer(pf[24:], np.uint8), expect)
+    # and the lanes fold correctly afterwards
+    items, contents = S.populate(root, 4, [("e/y", [0, 1, 2], 3, [3 * MiBl, 5, 700 * KiBl])], seed=7)
+    assert bcp.gen_run(root, 4, items, nlanes=2).errors == 0
+    assert S.read_file(S.parity_path(root, 3, "e/y")) == oracle.gen_parity_file(contents["e/y"])
+
+
 def test_fold_mode_rejects_unknown(bcp):
     with pytest.raises(bcp.BcpError):
         bcp.set_fold_mode(7)
