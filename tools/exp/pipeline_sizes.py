@@ -26,6 +26,13 @@ for i in range(1000):
     lens = [int(x) for x in np.exp(r5.uniform(np.log(64 * KiB), np.log(4 * MiB), size=8))]
     files.append((f"u{i % 8}/{(i * 2654435761) % 65536:04X}/chunk{i}", holders, p, lens))
 write_store(root, files, 2)
+if len(sys.argv) > 1 and sys.argv[1] == "preread":  # read every chunk file once before the runs
+    for dirpath, _, names in os.walk(root):
+        for nm in names:
+            with open(os.path.join(dirpath, nm), "rb") as f:
+                while f.read(1 << 22):
+                    pass
+    print(json.dumps({"preread": True}), flush=True)
 items = [(path, 1_700_000_000, S.with_p(sum(1 << h for h in holders), p)) for path, holders, p, _ in files]
 pl = bcp.Pipeline(io_threads=16)
 for n in (100, 300, 1000, 100):
