@@ -46,5 +46,26 @@ for n in (100, 300, 1000, 100):
     print(json.dumps(dict(stripes=n, GiB=round((rd + wr) / GiB, 3), warm_ms=round(w * 1e3, 2),
                           GiBps=round((rd + wr) / w / GiB, 2), runs_ms=[round(t * 1e3, 2) for t in ts],
                           errors=int(st.errors))), flush=True)
+# the changelog round's situation: the same 100 stripes' chunks rewritten,
+# then one run -- with and without reading the rewritten files first
+for preread in (False, True, False, True):
+    rng = np.random.default_rng(11)
+    for path, holders, p, lens in files[:100]:
+        for h, L in zip(holders, lens):
+            S.write_chunk(root, h, path, rng.integers(0, 256, size=L, dtype=np.uint8))
+    if preread:
+        for path, holders, p, lens in files[:100]:
+            for h in holders:
+                with open(S.chunk_path(root, h, path), "rb") as f:
+                    while f.read(1 << 22):
+                        pass
+    t0 = time.perf_counter()
+    st = pl.run(root, 9, items[:100])
+    t1 = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    pl.run(root, 9, items[:100])
+    t2 = time.perf_counter() - t0
+    print(json.dumps(dict(after_rewrite=True, preread=preread, first_ms=round(t1 * 1e3, 2),
+                          second_ms=round(t2 * 1e3, 2), errors=int(st.errors))), flush=True)
 pl.close()
 shutil.rmtree(root, ignore_errors=True)
