@@ -558,7 +558,8 @@ typedef struct fold_res {
     struct fold_res *next;
     int device;         /* -1: host-only (hook) */
     bcp_engine *eng;
-    bcp_queue *q;       /* ZERO_COPY / STAGED only */
+    bcp_queue *q;       /* per-lane fold modes only */
+    bcp_event *ev;      /* PIPELINED: marks the ranges launched before the window's last */
     uint8_t *h_win[2];  /* window rows [n][pitch] (pinned + mapped when device >= 0) */
     int rows_dev;       /* h_win are device memory the host writes (DEVICE_ROWS) */
     uint8_t *h_par;     /* fold output */
@@ -604,6 +605,8 @@ static void res_destroy(fold_res *R)
             bcp_dev_free(R->eng, R->d_src);
         if (R->d_out)
             bcp_dev_free(R->eng, R->d_out);
+        if (R->ev)
+            bcp_event_destroy(R->ev);
         if (R->q)
             bcp_queue_destroy(R->q);
     }
@@ -935,21 +938,42 @@ static int watch_rows(row_watch *W, fold_res *R, bcp_xor_hook_fn hook, void *hoo
 }
 
 /* After the receives (every fill has returned, so no source launches any
- * more): unregister, fold the rest (all of it after a redo), the one sync
- * -- also after an error, since ranges may be in flight.  fold = 0: sync
- * only (the task failed). */
-static int finish_rows(row_watch *W, int fold)
+ * more): unregister and fold the rest (all of it after a redo).  fold = 0:
+ * nothing more (the task failed).  *pre: the leading bytes of out that the
+ * ranges launched during the receives produce, final once
+ * finish_rows_prefix() returns -- the P role writes them while the last
+ * range folds; 0 when the window does not split so. */
+static int finish_rows_launch(row_watch *W, int fold, size_t *pre)
 {
     for (int j = 0; j < W->n; j++)
         watch_del(W->rows + (size_t)j * W->pitch);
     int rc = W->err;
     const size_t lo = W->redo ? 0 : W->lo;
+    *pre = 0;
     __atomic_fetch_add(&g_pipe_windows, 1, __ATOMIC_RELAXED);
-    if (fold && !rc && lo < W->nbytes)
+    if (fold && !rc && lo < W->nbytes) {
+        /* (the hook folds at launch: its ranges are done already) */
+        if (lo > 0 && (W->hook || (W->R->ev && bcp_event_record(W->R->ev, W->R->q) == 0)))
+            *pre = lo;
         rc = launch_range(W, lo, W->nbytes);
+    }
+    return rc;
+}
+
+static int finish_rows_prefix(row_watch *W) { return W->hook ? 0 : bcp_event_sync(W->R->ev); }
+
+/* The one sync -- also after an error, since ranges may be in flight. */
+static int finish_rows_sync(row_watch *W, int rc)
+{
     const int src = W->hook ? 0 : bcp_queue_sync(W->R->q);
     pthread_mutex_destroy(&W->mu);
     return rc ? rc : src;
+}
+
+static int finish_rows(row_watch *W, int fold)
+{
+    size_t pre;
+    return finish_rows_sync(W, finish_rows_launch(W, fold, &pre));
 }
 
 /* ---- file helpers (task_processing.c:29-79) ----------------------------- */
@@ -1112,6 +1136,28 @@ static int drain_windows(const bcp_transport_ops *T, const int *ranks, int n, si
     return rc;
 }
 
+/* Once per task: open the parity chunk (open: no sticky error) and write the
+ * gen header, the chunk sizes (:199-201; hdr NULL when rebuilding), to it or
+ * to the null device. */
+static void open_parity_chunk(HostState *hs, const char *path, uint64_t final_size, int open, int *fd,
+                              int *opened, int *have_had_error, const uint64_t *hdr, int n)
+{
+    if (*opened)
+        return;
+    *opened = 1;
+    if (open) {
+        const int f = open_new_parity(hs->write_dir, path, (off_t)final_size);
+        if (f <= 0) {
+            *have_had_error = errno;
+            LOGERR("cannot open parity chunk '%s': %s\n", path, strerror(errno));
+        } else {
+            *fd = f;
+        }
+    }
+    if (hdr && write(*fd, hdr, sizeof(uint64_t) * (size_t)n) <= 0)
+        *have_had_error = errno;
+}
+
 static void parity_generator(const bcp_transport_ops *T, const char *path, const FileInfo *task, TaskInfo ti,
                              HostState *hs)
 {
@@ -1201,17 +1247,17 @@ static void parity_generator(const bcp_transport_ops *T, const char *path, const
             have_had_error = as_errno(res_rc);
     }
 
-    int P_fd = hs->fd_null;
-    if (have_had_error == 0) {
-        P_fd = open_new_parity(hs->write_dir, path, (off_t)final_size);
-        if (P_fd <= 0) {
-            have_had_error = errno;
-            LOGERR("cannot open parity chunk '%s': %s\n", path, strerror(errno));
-            P_fd = hs->fd_null;
-        }
-    } else {
+    /* The parity chunk is opened (and its gen header written) once the first
+     * window's receives are posted, so the sources read their chunks while
+     * this thread creates, truncates and allocates the file; the reference
+     * opens it before its first receive (:183-206).  Same bytes, same errors. */
+    int P_fd = hs->fd_null, opened = 0;
+    const int open_parity = have_had_error == 0;
+    /* (experiment knob BCP_TASK_SERIAL_IO: the reference's order -- open
+     * before the first receive, the whole window written after the fold) */
+    const int serial_io = getenv("BCP_TASK_SERIAL_IO") != NULL;
+    if (!open_parity)
         LOGERR("'%s' goes to the null device: error %d is sticky on this rank\n", path, have_had_error);
-    }
 
     /* STREAMED: the lane's queue and device rows; row j's data bytes.  A
      * gen-mode single-window row holds chunk_sizes[j] bytes then the
@@ -1242,6 +1288,11 @@ static void parity_generator(const bcp_transport_ops *T, const char *path, const
     int pipelined = mode == BCP_FOLD_PIPELINED && !res_rc && expected_messages == 1 && T->send_fill;
     if (pipelined && !hook && !L->q && bcp_queue_create(L->eng, &L->q))
         pipelined = 0;
+    if (pipelined && !hook && !L->ev && bcp_event_create(L->eng, &L->ev))
+        L->ev = NULL; /* no early prefix writes, nothing else */
+    if (serial_io && !res_rc)
+        open_parity_chunk(hs, path, final_size, open_parity, &P_fd, &opened, &have_had_error,
+                          ti.is_rebuilding ? NULL : chunk_sizes, n);
     phase_add(BCP_PHASE_P_OPEN, &tph);
     if (res_rc) {
         int drc = drain_windows(T, ranks, n, buffer_size, expected_messages, ti.tag);
@@ -1252,10 +1303,9 @@ static void parity_generator(const bcp_transport_ops *T, const char *path, const
         goto done;
     }
 
-    /* gen: the chunk sizes head the parity chunk (:199-201) */
-    if (!ti.is_rebuilding)
-        if (write(P_fd, chunk_sizes, sizeof(uint64_t) * (size_t)n) <= 0)
-            have_had_error = errno;
+    if (expected_messages == 0)
+        open_parity_chunk(hs, path, final_size, open_parity, &P_fd, &opened, &have_had_error,
+                          ti.is_rebuilding ? NULL : chunk_sizes, n);
 
     uint8_t *win_a = L ? L->h_win[0] : NULL, *win_b = L ? L->h_win[1] : NULL, *pblk = L ? L->h_par : NULL;
     for (int j = 0; j < n; j++)
@@ -1277,6 +1327,8 @@ static void parity_generator(const bcp_transport_ops *T, const char *path, const
             watched = pipelined && !have_had_error &&
                       watch_rows(&W, L, hook, hook_ctx, win_a, pitch, valid, n, buffer_size, pblk);
             trc = post_recvs(T, req, n, win_a, pitch, buffer_size, ranks, ti.tag);
+            open_parity_chunk(hs, path, final_size, open_parity, &P_fd, &opened, &have_had_error,
+                              ti.is_rebuilding ? NULL : chunk_sizes, n);
         }
         int w = 0, crc = 0;
         if (streamed && !have_had_error && !trc)
@@ -1298,11 +1350,33 @@ static void parity_generator(const bcp_transport_ops *T, const char *path, const
             LOGERR("windows of '%s' not received: %s\n", path, strerror(have_had_error));
         }
         /* fold window msg_i on the GPU while the senders fill win_b */
+        const size_t wsize = (size_t)MIN_((uint64_t)buffer_size, data_left);
+        size_t early = 0; /* leading bytes of wsize written while the fold finished */
         if (!have_had_error) {
-            int frc = watched    ? finish_rows(&W, 1)
-                      : streamed ? stream_fold(L, n, pitch, valid, buffer_size, pblk)
-                                 : fold_window(L, hs, mode, hook, hook_ctx, win_a, pitch, valid, buffer_size, n, pblk);
-            if (frc) {
+            int frc;
+            if (watched) {
+                /* PIPELINED: the ranges folded while the rows arrived go to
+                 * the file while the last range folds */
+                size_t pre = 0;
+                frc = finish_rows_launch(&W, 1, &pre);
+                if (serial_io)
+                    pre = 0;
+                if (!frc && pre && !(frc = finish_rows_prefix(&W))) {
+                    const ssize_t wr = write(P_fd, pblk, MIN_(pre, wsize));
+                    if (wr <= 0) {
+                        have_had_error = errno;
+                        LOGERR("write of '%s' failed with %d (%s) after %llu bytes\n", path, errno,
+                               strerror(errno), (unsigned long long)(final_size - data_left));
+                    } else {
+                        early = (size_t)wr;
+                    }
+                }
+                frc = finish_rows_sync(&W, frc);
+            } else {
+                frc = streamed ? stream_fold(L, n, pitch, valid, buffer_size, pblk)
+                               : fold_window(L, hs, mode, hook, hook_ctx, win_a, pitch, valid, buffer_size, n, pblk);
+            }
+            if (frc && !have_had_error) {
                 have_had_error = EIO;
                 LOGERR("GPU fold of '%s' failed: %s\n", path, bcp_strerror(frc));
             }
@@ -1311,12 +1385,11 @@ static void parity_generator(const bcp_transport_ops *T, const char *path, const
         }
         phase_add(BCP_PHASE_P_FOLD, &tph);
         if (!have_had_error) {
-            size_t wsize = (size_t)MIN_((uint64_t)buffer_size, data_left);
-            ssize_t wr = write(P_fd, pblk, wsize);
+            const ssize_t wr = wsize > early ? write(P_fd, pblk + early, wsize - early) : 1;
             if (wr <= 0) {
                 have_had_error = errno;
                 LOGERR("write of '%s' failed with %d (%s) after %llu bytes\n", path, errno, strerror(errno),
-                       (unsigned long long)(final_size - data_left));
+                       (unsigned long long)(final_size - data_left + early));
             }
             data_left -= wsize;
         }

@@ -161,7 +161,9 @@ int bcp_task_fold_stats(uint64_t *windows, uint64_t *launches);
 /* Wall time spent per protocol phase, summed over every task of every lane
  * since the last reset (seconds[i] for i < nphases; the last two entries are
  * task COUNTS, not seconds).  Returns BCP_PHASES.  P role: size exchange,
- * resources + parity open + header, waiting for the window rows, the fold,
+ * fold resources, waiting for the window rows (the parity open + header run
+ * after the first window's receives are posted, inside this phase), the fold
+ * (PIPELINED: with the write of the ranges folded while the rows arrived),
  * the parity write, close; source role: open + size exchange, the window
  * sends (from the P role's receive, i.e. the chunk reads). */
 #define BCP_PHASE_P_SIZES 0

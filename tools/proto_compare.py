@@ -18,6 +18,9 @@ interleaved in ONE run on ONE box:
                  fold: the reference CPU path
   noop           a fold that does nothing: the bound of the protocol itself
                  (no parity is correct; not verified)
+  <fold>_serial  the same fold with the reference's I/O order in the P role
+                 (experiment knob BCP_TASK_SERIAL_IO): the parity chunk opened
+                 before the first receive, the window written after the fold
 
 Workloads: config 1 (4 targets, 1333 x 3-wide 512 KiB stripes, 12 lanes; gen,
 and rebuild of target 2 with the single rebuild lane) and config 5 (9
@@ -75,6 +78,14 @@ def noop_hook():
 
 def fold_setup(fold, hooks):
     """Returns a context restore callable."""
+    if fold.endswith("_serial"):
+        os.environ["BCP_TASK_SERIAL_IO"] = "1"  # read by the P role per task
+        inner = fold_setup(fold[:-len("_serial")], hooks)
+
+        def restore_serial():
+            inner()
+            os.environ.pop("BCP_TASK_SERIAL_IO", None)
+        return restore_serial
     if fold.startswith("gpu_batched"):
         # gpu_batched[K]: K concurrent batches (bcp_task_set_fold_inflight)
         k = int(fold[len("gpu_batched"):] or 4)
@@ -128,11 +139,11 @@ def measure(name, folds, rounds, run_once, verify_fn, nbytes, hooks, extra=None,
                 b = batching.setdefault(f, {"windows": 0, "launches": 0})
                 b["windows"] += w1 - w0
                 b["launches"] += l1 - l0
-            if f == "gpu_pipelined" and r > 0:
+            if f.startswith("gpu_pipelined") and r > 0:
                 b = batching.setdefault(f, {"windows": 0, "launches": 0})
                 b["windows"] += pw1 - pw0
                 b["launches"] += pr1 - pr0
-            if r == rounds and f != "noop":
+            if r == rounds and not f.startswith("noop"):
                 ok, bad = verify_fn()
                 if not ok:
                     raise RuntimeError(f"{name}/{f}: parity mismatch on {bad}")
@@ -142,7 +153,7 @@ def measure(name, folds, rounds, run_once, verify_fn, nbytes, hooks, extra=None,
         res[f] = nbytes / warm / GiB
         line = dict(workload=name, fold=f, GiBps=round(res[f], 3), warm_median_s=round(warm, 4),
                     runs_s=[round(x, 4) for x in times[f]], cold_s=round(times[f][0], 4))
-        if f == "gpu_pipelined" and batching.get(f, {}).get("windows"):
+        if f.startswith("gpu_pipelined") and batching.get(f, {}).get("windows"):
             line["range_folds_per_window"] = round(batching[f]["launches"] / batching[f]["windows"], 2)
         elif batching.get(f, {}).get("launches"):
             line["windows_per_launch"] = round(batching[f]["windows"] / batching[f]["launches"], 2)
@@ -158,7 +169,7 @@ def measure(name, folds, rounds, run_once, verify_fn, nbytes, hooks, extra=None,
         emit(**line)
     if "noop" in res:
         emit(workload=name, summary={f: round(v, 3) for f, v in res.items()},
-             frac_of_noop_bound={f: round(v / res["noop"], 3) for f, v in res.items() if f != "noop"},
+             frac_of_noop_bound={f: round(v / res["noop"], 3) for f, v in res.items() if not f.startswith("noop")},
              gpu_vs_cpu={f: round(v / res["cpu_reference"], 3) for f, v in res.items() if f.startswith("gpu_")}
              if "cpu_reference" in res else None)
     return res
