@@ -94,6 +94,7 @@ typedef struct {
     const size_t *valid;
     uint8_t *out;
     size_t step; /* smallest range folded before the window is complete */
+    size_t pre;  /* out[0, pre) is final once R->ev completes (0: no mark) */
     int n;
 } row_watch;
 
@@ -892,6 +893,15 @@ static int launch_range(const row_watch *w, size_t lo, size_t hi)
     return bcp_xor_stripes_async(w->R->q, &st, 1, so, (uint32_t)w->n);
 }
 
+/* Under w->mu, before the window's last range is launched: mark what the
+ * ranges before it produce, so the P role can write that while the last one
+ * folds (the hook folds at launch: nothing to mark). */
+static void mark_prefix(row_watch *w)
+{
+    if (w->lo > 0 && (w->hook || (w->R->ev && bcp_event_record(w->R->ev, w->R->q) == 0)))
+        w->pre = w->lo;
+}
+
 /* Under w->mu: launch every range all rows have delivered past w->lo. */
 static void range_claim(row_watch *w)
 {
@@ -902,6 +912,8 @@ static void range_claim(row_watch *w)
         if (avail < w->nbytes && avail < w->lo + w->step)
             return;
         const size_t hi = avail >= w->nbytes ? w->nbytes : avail / PIPE_ALIGN * PIPE_ALIGN;
+        if (hi == w->nbytes)
+            mark_prefix(w);
         const int rc = launch_range(w, w->lo, hi);
         if (rc)
             w->err = rc;
@@ -923,6 +935,7 @@ static int watch_rows(row_watch *W, fold_res *R, bcp_xor_hook_fn hook, void *hoo
     W->pitch = pitch;
     W->nbytes = nbytes;
     W->lo = 0;
+    W->pre = 0;
     W->valid = valid;
     W->out = out;
     W->step = MAX_(PIPE_STEP, nbytes / 4); /* at most ~5 launches per window */
@@ -947,16 +960,19 @@ static int finish_rows_launch(row_watch *W, int fold, size_t *pre)
 {
     for (int j = 0; j < W->n; j++)
         watch_del(W->rows + (size_t)j * W->pitch);
+    pthread_mutex_lock(&W->mu); /* (every fill has returned; the lock orders their last writes) */
     int rc = W->err;
-    const size_t lo = W->redo ? 0 : W->lo;
-    *pre = 0;
-    __atomic_fetch_add(&g_pipe_windows, 1, __ATOMIC_RELAXED);
-    if (fold && !rc && lo < W->nbytes) {
-        /* (the hook folds at launch: its ranges are done already) */
-        if (lo > 0 && (W->hook || (W->R->ev && bcp_event_record(W->R->ev, W->R->q) == 0)))
-            *pre = lo;
-        rc = launch_range(W, lo, W->nbytes);
+    if (W->redo) {
+        W->lo = 0;
+        W->pre = 0;
     }
+    if (fold && !rc && W->lo < W->nbytes) {
+        mark_prefix(W); /* a source launched the ranges so far; the rest is ours */
+        rc = launch_range(W, W->lo, W->nbytes);
+    }
+    *pre = rc ? 0 : W->pre;
+    pthread_mutex_unlock(&W->mu);
+    __atomic_fetch_add(&g_pipe_windows, 1, __ATOMIC_RELAXED);
     return rc;
 }
 

@@ -5,8 +5,12 @@ config 1 (BASELINE.json configs[0] shape): 4 storage targets as loopback
   ranks, 3-wide stripes with P rotating over the target left out, 1333 files
   -> ~1000 x 512 KiB chunk files per target.  Timed three ways over the same
   files: the per-rank protocol with the GPU fold (bcp_gen_run), the same
-  protocol with the reference's CPU fold (oracle_xor_rows as the fold hook:
-  the "reference CPU XOR path"), and the batched pipeline (bcp_pipeline_gen).
+  protocol with the reference's CPU fold (oracle_xor_rows as the fold hook)
+  in two forms -- the reference's P role (the whole window folded after
+  every row arrived, the parity opened before the first receive:
+  protocol_cpu_fold_reference) and that fold inside this protocol's
+  pipelined P role (source threads fold ranges as rows fill:
+  protocol_cpu_fold_pipelined) -- and the batched pipeline (bcp_pipeline_gen).
   Then target 2 is lost and rebuilt through bcp_rebuild_run.
 config 5: 9 targets, 8-wide stripes, chunk sizes log-uniform in
   [64 KiB, 4 MiB] (not 16-byte rounded); full parity gen (pipeline), then a
@@ -40,6 +44,28 @@ import bcp_store as S  # noqa: E402
 import oracle  # noqa: E402  (checker + CPU fold for the reference path)
 
 KiB, MiB, GiB = 1024, 1024 ** 2, 1024 ** 3
+CPU_REF, CPU_PIPE = "protocol_cpu_fold_reference", "protocol_cpu_fold_pipelined"
+
+
+def fold_ctx(mode, hook, serial):
+    """Set a P-role fold (mode None: the default; serial: the reference's
+    protocol -- sources pad every window, the P role opens the parity before
+    the first receive and writes the window after the fold, experiment knob
+    BCP_TASK_SERIAL_IO); returns the restore callable."""
+    prev = bcp.set_fold_mode(mode) if mode is not None else None
+    bcp.set_xor_hook(hook)
+    prev_pad = bcp.set_explicit_padding(True) if serial else None
+    if serial:
+        os.environ["BCP_TASK_SERIAL_IO"] = "1"
+
+    def restore():
+        os.environ.pop("BCP_TASK_SERIAL_IO", None)
+        if prev_pad is not None:
+            bcp.set_explicit_padding(prev_pad)
+        bcp.set_xor_hook(None)
+        if prev is not None:
+            bcp.set_fold_mode(prev)
+    return restore
 
 
 def emit(**kw):
@@ -118,25 +144,24 @@ def config1(a):
     # (one cold round, then a.reps warm ones) so host drift lands on all
     ol = oracle.lib()
     cpu_fold = ctypes.cast(ol.oracle_xor_rows, ctypes.c_void_p).value
-    variants = [("protocol_gpu_fold(bcp_gen_run,12 lanes)", None, None),
-                ("protocol_gpu_fold_staged(H2D,kernel,D2H; 12 lanes)", bcp.FOLD_STAGED, None),
-                ("protocol_cpu_fold_reference(oracle_xor_rows,12 lanes)", None, cpu_fold)]
+    variants = [("protocol_gpu_fold(bcp_gen_run,12 lanes)", None, None, False),
+                ("protocol_gpu_fold_staged(H2D,kernel,D2H; 12 lanes)", bcp.FOLD_STAGED, None, False),
+                (CPU_REF + "(oracle_xor_rows,12 lanes)", bcp.FOLD_ZERO_COPY, cpu_fold, True),
+                (CPU_PIPE + "(oracle_xor_rows,12 lanes)", None, cpu_fold, False)]
     times = {v[0]: [] for v in variants}
     ok = True
     preps = max(a.reps, 7)  # ~0.1 s runs: more rounds than the other measurements
+    nv = len(variants)
     for r in range(1 + preps):
-        for label, mode, hook in variants[r % 3:] + variants[:r % 3]:
+        for label, mode, hook, serial in variants[r % nv:] + variants[:r % nv]:
             reset_parity()
-            prev = bcp.set_fold_mode(mode) if mode is not None else None
-            bcp.set_xor_hook(hook)
+            restore = fold_ctx(mode, hook, serial)
             try:
                 t0 = time.perf_counter()
                 st = bcp.gen_run(root, 4, items, nlanes=12)
                 times[label].append(time.perf_counter() - t0)
             finally:
-                bcp.set_xor_hook(None)
-                if prev is not None:
-                    bcp.set_fold_mode(prev)
+                restore()
             if r == preps:
                 okv, badv = verify(root, files, contents, a.verify, rng)
                 ok &= okv
@@ -189,23 +214,22 @@ def config1(a):
         return good, good == len(range(0, len(lost), max(1, len(lost) // a.verify)))
 
     # single lane, as rebuild/main.c; the three folds interleaved in rotating order
-    rvariants = [("rebuild_protocol_gpu_fold(bcp_rebuild_run)", None, None),
-                 ("rebuild_protocol_gpu_fold_staged(bcp_rebuild_run)", bcp.FOLD_STAGED, None),
-                 ("rebuild_protocol_cpu_fold_reference(oracle_xor_rows)", None, cpu_fold)]
+    rvariants = [("rebuild_protocol_gpu_fold(bcp_rebuild_run)", None, None, False),
+                 ("rebuild_protocol_gpu_fold_staged(bcp_rebuild_run)", bcp.FOLD_STAGED, None, False),
+                 ("rebuild_" + CPU_REF + "(oracle_xor_rows)", bcp.FOLD_ZERO_COPY, cpu_fold, True),
+                 ("rebuild_" + CPU_PIPE + "(oracle_xor_rows)", None, cpu_fold, False)]
     rtimes = {v[0]: [] for v in rvariants}
+    nv = len(rvariants)
     for r in range(1 + preps):
-        for label, mode, hook in rvariants[r % 3:] + rvariants[:r % 3]:
+        for label, mode, hook, serial in rvariants[r % nv:] + rvariants[:r % nv]:
             drop_lost()
-            prev = bcp.set_fold_mode(mode) if mode is not None else None
-            bcp.set_xor_hook(hook)
+            restore = fold_ctx(mode, hook, serial)
             try:
                 t0 = time.perf_counter()
                 st = bcp.rebuild_run(root, 4, 2, items)
                 rtimes[label].append(time.perf_counter() - t0)
             finally:
-                bcp.set_xor_hook(None)
-                if prev is not None:
-                    bcp.set_fold_mode(prev)
+                restore()
             if r == preps:
                 good, okv = rebuilt_ok()
                 ok &= okv
@@ -262,23 +286,25 @@ def config5(a):
     # default GPU fold against the reference CPU fold, interleaved: 8 rows of
     # up to 4 MiB per window
     ol = oracle.lib()
-    pvariants = [("protocol_gpu_fold(bcp_gen_run,12 lanes)", None),
-                 ("protocol_cpu_fold_reference(oracle_xor_rows,12 lanes)",
-                  ctypes.cast(ol.oracle_xor_rows, ctypes.c_void_p).value)]
+    cpu_fold = ctypes.cast(ol.oracle_xor_rows, ctypes.c_void_p).value
+    pvariants = [("protocol_gpu_fold(bcp_gen_run,12 lanes)", None, None, False),
+                 (CPU_REF + "(oracle_xor_rows,12 lanes)", bcp.FOLD_ZERO_COPY, cpu_fold, True),
+                 (CPU_PIPE + "(oracle_xor_rows,12 lanes)", None, cpu_fold, False)]
     ptimes = {v[0]: [] for v in pvariants}
     preps = max(a.reps, 5)
+    nv = len(pvariants)
     for r in range(1 + preps):
-        for label, hook in pvariants[r % 2:] + pvariants[:r % 2]:
+        for label, mode, hook, serial in pvariants[r % nv:] + pvariants[:r % nv]:
             for k in range(ntargets):
                 shutil.rmtree(os.path.join(root, f"st{k}", "parity"), ignore_errors=True)
                 os.makedirs(os.path.join(root, f"st{k}", "parity"))
-            bcp.set_xor_hook(hook)
+            restore = fold_ctx(mode, hook, serial)
             try:
                 t0 = time.perf_counter()
                 st = bcp.gen_run(root, ntargets, items, nlanes=12)
                 ptimes[label].append(time.perf_counter() - t0)
             finally:
-                bcp.set_xor_hook(None)
+                restore()
             if r == preps:
                 okp, badp = verify(root, files, contents, a.verify, rng)
                 ok_proto &= okp

@@ -14,13 +14,20 @@ interleaved in ONE run on ONE box:
   gpu_device_rows  the rows themselves in device memory the host writes
                  (BCP_FOLD_DEVICE_ROWS): chunk reads store into HBM through
                  the BAR, the fold service's kernel reads HBM
-  cpu_reference  the reference's xor_parity restated (oracle_xor_rows) as the
-                 fold: the reference CPU path
+  cpu_reference  the reference's P role: its xor_parity restated
+                 (oracle_xor_rows) over the whole window once every row has
+                 arrived, sources padding every window, the parity chunk
+                 opened before the first receive (BCP_TASK_SERIAL_IO) -- the
+                 reference CPU path
+  cpu_pipelined  the same CPU fold inside this protocol's pipelined P role:
+                 the source threads fold ranges as the rows fill (what
+                 "cpu_reference" measured from r2an to r2bg)
   noop           a fold that does nothing: the bound of the protocol itself
                  (no parity is correct; not verified)
   <fold>_serial  the same fold with the reference's I/O order in the P role
                  (experiment knob BCP_TASK_SERIAL_IO): the parity chunk opened
                  before the first receive, the window written after the fold
+                 (the padding stays implicit)
 
 Workloads: config 1 (4 targets, 1333 x 3-wide 512 KiB stripes, 12 lanes; gen,
 and rebuild of target 2 with the single rebuild lane) and config 5 (9
@@ -102,6 +109,18 @@ def fold_setup(fold, hooks):
                 "gpu_device_rows": bcp.FOLD_DEVICE_ROWS, "gpu_pipelined": bcp.FOLD_PIPELINED}[fold]
         prev = bcp.set_fold_mode(mode)
         return lambda: bcp.set_fold_mode(prev)
+    if fold == "cpu_reference":
+        prev = bcp.set_fold_mode(bcp.FOLD_ZERO_COPY)  # any non-pipelined mode: the hook folds whole windows
+        prev_pad = bcp.set_explicit_padding(True)
+        os.environ["BCP_TASK_SERIAL_IO"] = "1"
+        bcp.set_xor_hook(hooks[fold])
+
+        def restore_ref():
+            bcp.set_xor_hook(None)
+            os.environ.pop("BCP_TASK_SERIAL_IO", None)
+            bcp.set_explicit_padding(prev_pad)
+            bcp.set_fold_mode(prev)
+        return restore_ref
     bcp.set_xor_hook(hooks[fold])
     return lambda: bcp.set_xor_hook(None)
 
@@ -171,7 +190,9 @@ def measure(name, folds, rounds, run_once, verify_fn, nbytes, hooks, extra=None,
         emit(workload=name, summary={f: round(v, 3) for f, v in res.items()},
              frac_of_noop_bound={f: round(v / res["noop"], 3) for f, v in res.items() if not f.startswith("noop")},
              gpu_vs_cpu={f: round(v / res["cpu_reference"], 3) for f, v in res.items() if f.startswith("gpu_")}
-             if "cpu_reference" in res else None)
+             if "cpu_reference" in res else None,
+             gpu_vs_cpu_pipelined={f: round(v / res["cpu_pipelined"], 3) for f, v in res.items()
+                                   if f.startswith("gpu_")} if "cpu_pipelined" in res else None)
     return res
 
 
@@ -185,7 +206,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--root", default="/dev/shm/bcp_proto")
     ap.add_argument("--rounds", type=int, default=6)
-    ap.add_argument("--folds", default="gpu_pipelined,gpu_batched,gpu_zero_copy,cpu_reference,noop")
+    ap.add_argument("--folds", default="gpu_pipelined,gpu_batched,gpu_zero_copy,cpu_reference,cpu_pipelined,noop")
     ap.add_argument("--workloads", default="c1_gen,c1_rebuild,c5_gen")
     ap.add_argument("--c1-files", type=int, default=1333)
     ap.add_argument("--c5-stripes", type=int, default=1000)
@@ -219,6 +240,7 @@ def main():
     folds = a.folds.split(",")
     noop = noop_hook()
     hooks = {"cpu_reference": ctypes.cast(oracle.lib().oracle_xor_rows, ctypes.c_void_p).value,
+             "cpu_pipelined": ctypes.cast(oracle.lib().oracle_xor_rows, ctypes.c_void_p).value,
              "noop": ctypes.cast(noop.noop_fold, ctypes.c_void_p).value}
     rng = np.random.default_rng(0)
     wl = a.workloads.split(",")
