@@ -1269,9 +1269,10 @@ static void parity_generator(const bcp_transport_ops *T, const char *path, const
      * opens it before its first receive (:183-206).  Same bytes, same errors. */
     int P_fd = hs->fd_null, opened = 0;
     const int open_parity = have_had_error == 0;
-    /* (experiment knob BCP_TASK_SERIAL_IO: the reference's order -- open
-     * before the first receive, the whole window written after the fold) */
-    const int serial_io = getenv("BCP_TASK_SERIAL_IO") != NULL;
+    /* (experiment knob BCP_TASK_SERIAL_IO, bits: 1 the reference's open
+     * before the first receive, 2 the whole window written after the fold) */
+    const char *sio = getenv("BCP_TASK_SERIAL_IO");
+    const int serial_io = sio ? atoi(sio) : 0;
     if (!open_parity)
         LOGERR("'%s' goes to the null device: error %d is sticky on this rank\n", path, have_had_error);
 
@@ -1306,7 +1307,7 @@ static void parity_generator(const bcp_transport_ops *T, const char *path, const
         pipelined = 0;
     if (pipelined && !hook && !L->ev && bcp_event_create(L->eng, &L->ev))
         L->ev = NULL; /* no early prefix writes, nothing else */
-    if (serial_io && !res_rc)
+    if ((serial_io & 1) && !res_rc)
         open_parity_chunk(hs, path, final_size, open_parity, &P_fd, &opened, &have_had_error,
                           ti.is_rebuilding ? NULL : chunk_sizes, n);
     phase_add(BCP_PHASE_P_OPEN, &tph);
@@ -1375,7 +1376,7 @@ static void parity_generator(const bcp_transport_ops *T, const char *path, const
                  * the file while the last range folds */
                 size_t pre = 0;
                 frc = finish_rows_launch(&W, 1, &pre);
-                if (serial_io)
+                if (serial_io & 2)
                     pre = 0;
                 if (!frc && pre && !(frc = finish_rows_prefix(&W))) {
                     const ssize_t wr = write(P_fd, pblk, MIN_(pre, wsize));

@@ -56,7 +56,7 @@ def fold_ctx(mode, hook, serial):
     bcp.set_xor_hook(hook)
     prev_pad = bcp.set_explicit_padding(True) if serial else None
     if serial:
-        os.environ["BCP_TASK_SERIAL_IO"] = "1"
+        os.environ["BCP_TASK_SERIAL_IO"] = "3"
 
     def restore():
         os.environ.pop("BCP_TASK_SERIAL_IO", None)
