@@ -94,7 +94,6 @@ typedef struct {
     const size_t *valid;
     uint8_t *out;
     size_t step; /* smallest range folded before the window is complete */
-    size_t pre;  /* out[0, pre) is final once R->ev completes (0: no mark) */
     int n;
 } row_watch;
 
@@ -560,7 +559,6 @@ typedef struct fold_res {
     int device;         /* -1: host-only (hook) */
     bcp_engine *eng;
     bcp_queue *q;       /* per-lane fold modes only */
-    bcp_event *ev;      /* PIPELINED: marks the ranges launched before the window's last */
     uint8_t *h_win[2];  /* window rows [n][pitch] (pinned + mapped when device >= 0) */
     int rows_dev;       /* h_win are device memory the host writes (DEVICE_ROWS) */
     uint8_t *h_par;     /* fold output */
@@ -606,8 +604,6 @@ static void res_destroy(fold_res *R)
             bcp_dev_free(R->eng, R->d_src);
         if (R->d_out)
             bcp_dev_free(R->eng, R->d_out);
-        if (R->ev)
-            bcp_event_destroy(R->ev);
         if (R->q)
             bcp_queue_destroy(R->q);
     }
@@ -893,15 +889,6 @@ static int launch_range(const row_watch *w, size_t lo, size_t hi)
     return bcp_xor_stripes_async(w->R->q, &st, 1, so, (uint32_t)w->n);
 }
 
-/* Under w->mu, before the window's last range is launched: mark what the
- * ranges before it produce, so the P role can write that while the last one
- * folds (the hook folds at launch: nothing to mark). */
-static void mark_prefix(row_watch *w)
-{
-    if (w->lo > 0 && (w->hook || (w->R->ev && bcp_event_record(w->R->ev, w->R->q) == 0)))
-        w->pre = w->lo;
-}
-
 /* Under w->mu: launch every range all rows have delivered past w->lo. */
 static void range_claim(row_watch *w)
 {
@@ -912,8 +899,6 @@ static void range_claim(row_watch *w)
         if (avail < w->nbytes && avail < w->lo + w->step)
             return;
         const size_t hi = avail >= w->nbytes ? w->nbytes : avail / PIPE_ALIGN * PIPE_ALIGN;
-        if (hi == w->nbytes)
-            mark_prefix(w);
         const int rc = launch_range(w, w->lo, hi);
         if (rc)
             w->err = rc;
@@ -935,7 +920,6 @@ static int watch_rows(row_watch *W, fold_res *R, bcp_xor_hook_fn hook, void *hoo
     W->pitch = pitch;
     W->nbytes = nbytes;
     W->lo = 0;
-    W->pre = 0;
     W->valid = valid;
     W->out = out;
     W->step = MAX_(PIPE_STEP, nbytes / 4); /* at most ~5 launches per window */
@@ -951,45 +935,23 @@ static int watch_rows(row_watch *W, fold_res *R, bcp_xor_hook_fn hook, void *hoo
 }
 
 /* After the receives (every fill has returned, so no source launches any
- * more): unregister and fold the rest (all of it after a redo).  fold = 0:
- * nothing more (the task failed).  *pre: the leading bytes of out that the
- * ranges launched during the receives produce, final once
- * finish_rows_prefix() returns -- the P role writes them while the last
- * range folds; 0 when the window does not split so. */
-static int finish_rows_launch(row_watch *W, int fold, size_t *pre)
+ * more): unregister, fold the rest (all of it after a redo), the one sync
+ * -- also after an error, since ranges may be in flight.  fold = 0: sync
+ * only (the task failed).  (Writing the ranges folded so far while the last
+ * one folds, behind an event the launching source records, measured slower
+ * on every workload -- config 5 by a quarter, r2bh / r2bi -- and is gone.) */
+static int finish_rows(row_watch *W, int fold)
 {
     for (int j = 0; j < W->n; j++)
         watch_del(W->rows + (size_t)j * W->pitch);
-    pthread_mutex_lock(&W->mu); /* (every fill has returned; the lock orders their last writes) */
     int rc = W->err;
-    if (W->redo) {
-        W->lo = 0;
-        W->pre = 0;
-    }
-    if (fold && !rc && W->lo < W->nbytes) {
-        mark_prefix(W); /* a source launched the ranges so far; the rest is ours */
-        rc = launch_range(W, W->lo, W->nbytes);
-    }
-    *pre = rc ? 0 : W->pre;
-    pthread_mutex_unlock(&W->mu);
+    const size_t lo = W->redo ? 0 : W->lo;
     __atomic_fetch_add(&g_pipe_windows, 1, __ATOMIC_RELAXED);
-    return rc;
-}
-
-static int finish_rows_prefix(row_watch *W) { return W->hook ? 0 : bcp_event_sync(W->R->ev); }
-
-/* The one sync -- also after an error, since ranges may be in flight. */
-static int finish_rows_sync(row_watch *W, int rc)
-{
+    if (fold && !rc && lo < W->nbytes)
+        rc = launch_range(W, lo, W->nbytes);
     const int src = W->hook ? 0 : bcp_queue_sync(W->R->q);
     pthread_mutex_destroy(&W->mu);
     return rc ? rc : src;
-}
-
-static int finish_rows(row_watch *W, int fold)
-{
-    size_t pre;
-    return finish_rows_sync(W, finish_rows_launch(W, fold, &pre));
 }
 
 /* ---- file helpers (task_processing.c:29-79) ----------------------------- */
@@ -1269,10 +1231,9 @@ static void parity_generator(const bcp_transport_ops *T, const char *path, const
      * opens it before its first receive (:183-206).  Same bytes, same errors. */
     int P_fd = hs->fd_null, opened = 0;
     const int open_parity = have_had_error == 0;
-    /* (experiment knob BCP_TASK_SERIAL_IO, bits: 1 the reference's open
-     * before the first receive, 2 the whole window written after the fold) */
-    const char *sio = getenv("BCP_TASK_SERIAL_IO");
-    const int serial_io = sio ? atoi(sio) : 0;
+    /* (experiment knob BCP_TASK_SERIAL_IO: the reference's order, the open
+     * before the first receive) */
+    const int serial_io = getenv("BCP_TASK_SERIAL_IO") != NULL;
     if (!open_parity)
         LOGERR("'%s' goes to the null device: error %d is sticky on this rank\n", path, have_had_error);
 
@@ -1305,9 +1266,7 @@ static void parity_generator(const bcp_transport_ops *T, const char *path, const
     int pipelined = mode == BCP_FOLD_PIPELINED && !res_rc && expected_messages == 1 && T->send_fill;
     if (pipelined && !hook && !L->q && bcp_queue_create(L->eng, &L->q))
         pipelined = 0;
-    if (pipelined && !hook && !L->ev && bcp_event_create(L->eng, &L->ev))
-        L->ev = NULL; /* no early prefix writes, nothing else */
-    if ((serial_io & 1) && !res_rc)
+    if (serial_io && !res_rc)
         open_parity_chunk(hs, path, final_size, open_parity, &P_fd, &opened, &have_had_error,
                           ti.is_rebuilding ? NULL : chunk_sizes, n);
     phase_add(BCP_PHASE_P_OPEN, &tph);
@@ -1367,33 +1326,11 @@ static void parity_generator(const bcp_transport_ops *T, const char *path, const
             LOGERR("windows of '%s' not received: %s\n", path, strerror(have_had_error));
         }
         /* fold window msg_i on the GPU while the senders fill win_b */
-        const size_t wsize = (size_t)MIN_((uint64_t)buffer_size, data_left);
-        size_t early = 0; /* leading bytes of wsize written while the fold finished */
         if (!have_had_error) {
-            int frc;
-            if (watched) {
-                /* PIPELINED: the ranges folded while the rows arrived go to
-                 * the file while the last range folds */
-                size_t pre = 0;
-                frc = finish_rows_launch(&W, 1, &pre);
-                if (serial_io & 2)
-                    pre = 0;
-                if (!frc && pre && !(frc = finish_rows_prefix(&W))) {
-                    const ssize_t wr = write(P_fd, pblk, MIN_(pre, wsize));
-                    if (wr <= 0) {
-                        have_had_error = errno;
-                        LOGERR("write of '%s' failed with %d (%s) after %llu bytes\n", path, errno,
-                               strerror(errno), (unsigned long long)(final_size - data_left));
-                    } else {
-                        early = (size_t)wr;
-                    }
-                }
-                frc = finish_rows_sync(&W, frc);
-            } else {
-                frc = streamed ? stream_fold(L, n, pitch, valid, buffer_size, pblk)
-                               : fold_window(L, hs, mode, hook, hook_ctx, win_a, pitch, valid, buffer_size, n, pblk);
-            }
-            if (frc && !have_had_error) {
+            int frc = watched    ? finish_rows(&W, 1)
+                      : streamed ? stream_fold(L, n, pitch, valid, buffer_size, pblk)
+                                 : fold_window(L, hs, mode, hook, hook_ctx, win_a, pitch, valid, buffer_size, n, pblk);
+            if (frc) {
                 have_had_error = EIO;
                 LOGERR("GPU fold of '%s' failed: %s\n", path, bcp_strerror(frc));
             }
@@ -1402,11 +1339,12 @@ static void parity_generator(const bcp_transport_ops *T, const char *path, const
         }
         phase_add(BCP_PHASE_P_FOLD, &tph);
         if (!have_had_error) {
-            const ssize_t wr = wsize > early ? write(P_fd, pblk + early, wsize - early) : 1;
+            size_t wsize = (size_t)MIN_((uint64_t)buffer_size, data_left);
+            ssize_t wr = write(P_fd, pblk, wsize);
             if (wr <= 0) {
                 have_had_error = errno;
                 LOGERR("write of '%s' failed with %d (%s) after %llu bytes\n", path, errno, strerror(errno),
-                       (unsigned long long)(final_size - data_left + early));
+                       (unsigned long long)(final_size - data_left));
             }
             data_left -= wsize;
         }

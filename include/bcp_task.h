@@ -162,8 +162,7 @@ int bcp_task_fold_stats(uint64_t *windows, uint64_t *launches);
  * since the last reset (seconds[i] for i < nphases; the last two entries are
  * task COUNTS, not seconds).  Returns BCP_PHASES.  P role: size exchange,
  * fold resources, waiting for the window rows (the parity open + header run
- * after the first window's receives are posted, inside this phase), the fold
- * (PIPELINED: with the write of the ranges folded while the rows arrived),
+ * after the first window's receives are posted, inside this phase), the fold,
  * the parity write, close; source role: open + size exchange, the window
  * sends (from the P role's receive, i.e. the chunk reads). */
 #define BCP_PHASE_P_SIZES 0

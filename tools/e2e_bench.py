@@ -50,13 +50,13 @@ CPU_REF, CPU_PIPE = "protocol_cpu_fold_reference", "protocol_cpu_fold_pipelined"
 def fold_ctx(mode, hook, serial):
     """Set a P-role fold (mode None: the default; serial: the reference's
     protocol -- sources pad every window, the P role opens the parity before
-    the first receive and writes the window after the fold, experiment knob
-    BCP_TASK_SERIAL_IO); returns the restore callable."""
+    the first receive, experiment knob BCP_TASK_SERIAL_IO); returns the
+    restore callable."""
     prev = bcp.set_fold_mode(mode) if mode is not None else None
     bcp.set_xor_hook(hook)
     prev_pad = bcp.set_explicit_padding(True) if serial else None
     if serial:
-        os.environ["BCP_TASK_SERIAL_IO"] = "3"
+        os.environ["BCP_TASK_SERIAL_IO"] = "1"
 
     def restore():
         os.environ.pop("BCP_TASK_SERIAL_IO", None)

@@ -26,9 +26,7 @@ interleaved in ONE run on ONE box:
                  (no parity is correct; not verified)
   <fold>_serial  the same fold with the reference's I/O order in the P role
                  (experiment knob BCP_TASK_SERIAL_IO): the parity chunk opened
-                 before the first receive, the window written after the fold
-                 (the padding stays implicit); _serialopen / _serialwrite:
-                 only the one
+                 before the first receive (the padding stays implicit)
 
 Workloads: config 1 (4 targets, 1333 x 3-wide 512 KiB stripes, 12 lanes; gen,
 and rebuild of target 2 with the single rebuild lane) and config 5 (9
@@ -86,11 +84,9 @@ def noop_hook():
 
 def fold_setup(fold, hooks):
     """Returns a context restore callable."""
-    suffixes = {"_serial": "3", "_serialopen": "1", "_serialwrite": "2"}
-    suf = next((x for x in suffixes if fold.endswith(x)), None)
-    if suf:
-        os.environ["BCP_TASK_SERIAL_IO"] = suffixes[suf]  # read by the P role per task
-        inner = fold_setup(fold[:-len(suf)], hooks)
+    if fold.endswith("_serial"):
+        os.environ["BCP_TASK_SERIAL_IO"] = "1"  # read by the P role per task
+        inner = fold_setup(fold[:-len("_serial")], hooks)
 
         def restore_serial():
             inner()
@@ -115,7 +111,7 @@ def fold_setup(fold, hooks):
     if fold == "cpu_reference":
         prev = bcp.set_fold_mode(bcp.FOLD_ZERO_COPY)  # any non-pipelined mode: the hook folds whole windows
         prev_pad = bcp.set_explicit_padding(True)
-        os.environ["BCP_TASK_SERIAL_IO"] = "3"
+        os.environ["BCP_TASK_SERIAL_IO"] = "1"
         bcp.set_xor_hook(hooks[fold])
 
         def restore_ref():
