@@ -1,0 +1,11 @@
+# r02 call BH: P-role I/O overlap, prefix mark by the source that launches the last range;
+# prefix write under PIPELINED): protocol GPU tests, then an interleaved A/B
+# against the reference's order (BCP_TASK_SERIAL_IO).
+set -o pipefail
+R=$GRAFT_REPO_ROOT; cd $R
+O=$R/gpurun_out/r2bh; mkdir -p $O
+timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_gpu_protocol.py tests/test_gpu_ref.py -p no:cacheprovider > $O/tests.log 2>&1 || { echo TESTS_FAIL; tail -30 $O/tests.log; exit 1; }
+tail -3 $O/tests.log
+timeout -k 10 900 python -u tools/proto_compare.py --rounds 6 --folds gpu_pipelined,gpu_pipelined_serial,cpu_reference,cpu_pipelined,noop > $O/ab.jsonl 2> $O/ab.err || { echo AB_FAIL; tail -20 $O/ab.err; exit 1; }
+grep -h '"box"' $O/ab.jsonl; grep summary $O/ab.jsonl
+echo ALL_OK
