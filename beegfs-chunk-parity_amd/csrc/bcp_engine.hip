@@ -175,7 +175,7 @@ static int stream_vecs(const bcp_engine *e, uint64_t chunk_bytes, uint64_t nstri
   if (t8 < 16 * g || nsrc > 8) return 4;
   return 8;
 }
-static bool desc_vecs_ok(int v) { return v == 1 || v == 2 || v == 4 || v == 8; }
+static bool desc_vecs_ok(int v) { return v == 1 || v == 2 || v == 4 || v == 8 || v == 16; }
 
 // Vectors per lane of the descriptor kernel.  Explicit tuning wins; auto (0,
 // the default): 32 KiB tiles (U = 8) once the batch has twice as many of them
@@ -338,7 +338,7 @@ extern "C" int bcp_set_option(bcp_engine *eng, const char *key, int value) {
   else if (!strcmp(key, "stream_grab") && value >= 0 && value <= 64) eng->tuning.stream_grab = value;
   else if (!strcmp(key, "sync_mode") && (value == 0 || value == 1)) eng->tuning.sync_mode = value;
   else if (!strcmp(key, "host_registered") && (value == 0 || value == 1)) eng->tuning.host_registered = value;
-  else if (!strcmp(key, "desc_pipe") && (value == 0 || value == 2 || value == 4 || value == 5))
+  else if (!strcmp(key, "desc_pipe") && (value == 0 || value == 2 || value == 4 || value == 5 || value == 6))
     eng->tuning.desc_pipe = value;
   else if (!strcmp(key, "desc_table_host_max") && value >= 0 && value <= (1 << 24))
     eng->tuning.desc_table_host_max = value;
@@ -955,7 +955,8 @@ static int submit_desc(bcp_queue *q, const bcp_stripe *stripes, uint32_t nstripe
     return 0;
   }
   {
-    const int rc = submit_desc_args(q, stripes, nstripes, sources, vecs);
+    // the argument form is instantiated up to U = 8 (its batches are small)
+    const int rc = submit_desc_args(q, stripes, nstripes, sources, vecs > 8 ? 8 : vecs);
     if (rc <= 0) return rc;
   }
   // Staged copy: every stripe gets its own run of sources sorted by length,

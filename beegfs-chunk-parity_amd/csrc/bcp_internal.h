@@ -111,7 +111,7 @@ static_assert(kTileSrcs == 8, "xor_desc_args counts covering sources in scalar r
 // Rows (source x subtile pairs) of a grouped tile for U vectors per lane:
 // every load of the tile is in flight at once, so C*M*U <= 32 keeps the
 // fold within the register budget of the 8-source plain fold.
-__host__ __device__ constexpr int group_rows(int U) { return U >= 8 ? 4 : 8; }
+__host__ __device__ constexpr int group_rows(int U) { return U >= 16 ? 2 : U >= 8 ? 4 : 8; }
 
 // How one stripe is cut into tiles.  Shared by the host (tile counts per
 // stripe) and desc_tiles (records, one lane per subtile), so both cut

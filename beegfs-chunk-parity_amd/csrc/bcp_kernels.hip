@@ -109,13 +109,14 @@ __device__ __forceinline__ uint32_t tile_vec(uint32_t tin, int u) {
 // Shapes (the engine exposes 2, 4 and 5; 1 and 3 were r01 A/B points):
 // PIPE 1: H = U, D = 2; 2: H = U/2, D = 3; 3: H = U/2, D = 4; 4: H = U/4,
 // D = 5; 5: as 4, and tiles with more than 8 sources (desc_tile_wide)
-// through the window too.  (Grouped tiles keep all their <= 32 loads in
+// through the window too; 6: as 5 with H = U/8 (at U = 16: the loads in
+// flight of PIPE 5 at U = 8).  (Grouped tiles keep all their <= 32 loads in
 // flight: a window there cost 1.4 points, depth/ab3_group_window_probe.jsonl;
 // the same window in xor_stream measured 2 points below the compiler's own
 // schedule.)
 template <int U, int PIPE>
 struct PipeShape {
-  static constexpr int H = PIPE == 1 ? U : PIPE <= 3 ? (U >= 2 ? U / 2 : 1) : (U >= 4 ? U / 4 : 1);
+  static constexpr int H = PIPE == 1 ? U : PIPE <= 3 ? (U >= 2 ? U / 2 : 1) : PIPE == 6 ? (U >= 8 ? U / 8 : 1) : (U >= 4 ? U / 4 : 1);
   static constexpr int D = PIPE == 1 ? 2 : PIPE == 2 ? 3 : PIPE == 3 ? 4 : 5;
 };
 
@@ -526,11 +527,12 @@ __device__ __forceinline__ void desc_plain(const RT &r, uint32_t tile_bytes) {
 #pragma unroll
       for (int u = 0; u < U; u++) acc[u] = zero4();
       const uint32_t off = lane_off + j * tile_bytes;
+      constexpr int FP = U >= 16 ? PIPE : 0;  // at U = 16 all loads at once would spill
       switch (nfull) {
-        case 4: fold_cover<4, U>(acc, r.src, off); break;
-        case 3: fold_cover<3, U>(acc, r.src, off); break;
-        case 2: fold_cover<2, U>(acc, r.src, off); break;
-        default: fold_cover<1, U>(acc, r.src, off); break;
+        case 4: fold_cover<4, U, FP>(acc, r.src, off); break;
+        case 3: fold_cover<3, U, FP>(acc, r.src, off); break;
+        case 2: fold_cover<2, U, FP>(acc, r.src, off); break;
+        default: fold_cover<1, U, FP>(acc, r.src, off); break;
       }
       glob<v4u_u> *q = gp<v4u_u>(r.dst + off);
 #pragma unroll
@@ -1065,6 +1067,17 @@ hipError_t launch_xor_desc(hipStream_t st, int grid, int vecs, const DescBatch &
   if ((uint32_t)grid > b.ntiles) grid = (int)b.ntiles;
   if (ahead && pipe == 5 && vecs == 8 && b.sched == kSchedQueue) {
     hipLaunchKernelGGL((xor_desc_p<8, 5, 1>), dim3(grid), dim3(kBlock), 0, st, b);
+    return hipGetLastError();
+  }
+  if (vecs == 16) {
+    // 64 KiB subtiles (engine option desc_vecs_per_thread 16): half the queue
+    // grabs and record loads of U = 8; always through the rolling window
+    if (pipe == 6) hipLaunchKernelGGL((xor_desc_p<16, 6>), dim3(grid), dim3(kBlock), 0, st, b);
+    else hipLaunchKernelGGL((xor_desc_p<16, 5>), dim3(grid), dim3(kBlock), 0, st, b);
+    return hipGetLastError();
+  }
+  if (pipe == 6 && vecs == 8) {
+    hipLaunchKernelGGL((xor_desc_p<8, 6>), dim3(grid), dim3(kBlock), 0, st, b);
     return hipGetLastError();
   }
   if (pipe && vecs == 8) {

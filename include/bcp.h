@@ -187,7 +187,8 @@ int bcp_set_tuning(bcp_engine *eng, int blocks_per_cu, int vecs_per_thread);
 /* Named knob: "blocks_per_cu" (1..32), "vecs_per_thread" (1,2,4,8; 0 = the
  * default: 8, or 4 / 2 for batches of few tiles) of the uniform streaming
  * kernel; "desc_blocks_per_cu" (0 = the default, one per CU; 1..32),
- * "desc_vecs_per_thread" (1,2,4,8)
+ * "desc_vecs_per_thread" (1,2,4,8,16; 16 = 64 KiB subtiles, batches through
+ * desc_tiles only -- small batches in the kernel arguments use 8)
  * of the descriptor kernel; "schedule" (0 = device-wide tile work queue, the
  * default; 1 = a static contiguous tile range per workgroup, kept for A/B
  * measurements) for the uniform streaming kernel; "desc_schedule" (same
@@ -204,7 +205,8 @@ int bcp_set_tuning(bcp_engine *eng, int blocks_per_cu, int vecs_per_thread);
  * (register budget of the 8-source strided streaming kernel in waves per
  * SIMD: 0 = the compiler's, 5, 6 = default, 7), "desc_pipe" (rolling load
  * window of the descriptor kernel: 0 = every load first, 2, 4, 5 = default:
- * 4 and tiles wider than 8 sources windowed too), "stream_grab" (tiles per
+ * 4 and tiles wider than 8 sources windowed too, 6 = 5 with half the loads
+ * per unit), "stream_grab" (tiles per
  * work-queue grab of the streaming kernel for stripes of 1-4 sources, 1..64;
  * 0 = the default, 2), "sync_mode" (bcp_queue_sync: 0 = hipStreamSynchronize,
  * the default; 1 = wait on a blocking-sync event; env BCP_SYNC_MODE),

@@ -18,7 +18,7 @@ int main() {
   std::mt19937_64 rng(12345);
   long checked = 0, bad = 0;
   for (int it = 0; it < 60000; it++) {
-    const uint64_t T = 4096ull << (rng() % 4);  // U = 1, 2, 4, 8
+    const uint64_t T = 4096ull << (rng() % 5);  // U = 1, 2, 4, 8, 16
     const uint32_t nsrc = (uint32_t)(rng() % 13);
     std::vector<uint64_t> lens(nsrc);
     const int mode = (int)(rng() % 4);

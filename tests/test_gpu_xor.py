@@ -348,7 +348,7 @@ def test_descriptor_mixed_lengths_and_alignment(oracle, dev, queue, seed, desc_p
         assert np.array_equal(o, r)
 
 
-@pytest.mark.parametrize("vecs", [8, 4, 2, 1])
+@pytest.mark.parametrize("vecs", [16, 8, 4, 2, 1])
 def test_descriptor_grouped_tiles(oracle, engine, dev, queue, vecs, desc_path):
     """Staircase lengths whose covering sets hold for many consecutive
     subtiles: every grouped-tile shape (1 source x 2..8 subtiles, 2 x 2..4,
@@ -485,7 +485,7 @@ def test_survey_kats_on_gpu(oracle, dev, queue):
 
 
 @pytest.mark.parametrize("knob,value", [("stream_wpe", w) for w in (0, 5, 6, 7)] + [("table_wpe", w) for w in (5, 6, 7)] +
-                         [("desc_pipe", p) for p in (0, 2, 4, 5)])
+                         [("desc_pipe", p) for p in (0, 2, 4, 5, 6)])
 def test_schedule_variants_agree(oracle, engine, dev, queue, knob, value):
     """A/B kernel variants (register budget of xor_stream<8,8>, rolling load
     window of xor_desc<8>): same bytes as the oracle on full and partial
@@ -569,7 +569,7 @@ def test_window_replay_random_data(oracle, dev, queue, lens):
     assert out.tobytes() == ref
 
 
-@pytest.mark.parametrize("vecs", [8, 4, 1])
+@pytest.mark.parametrize("vecs", [16, 8, 4, 1])
 @pytest.mark.parametrize("window", [64 * 1024, 64 * 1024 + 16, 4 * 1024 * 1024])
 def test_window_replay_tiles(oracle, engine, dev, queue, vecs, window):
     """Replay stripes (max_cs > window) folded as plain tiles with remapped
@@ -726,7 +726,7 @@ KNOBS = {
     "blocks_per_cu": (1, [1, 2, 32], [0, 33]),
     "vecs_per_thread": (0, [0, 1, 2, 4, 8], [3, 16]),
     "desc_blocks_per_cu": (0, [0, 1, 32], [-1, 33]),
-    "desc_vecs_per_thread": (0, [0, 1, 2, 4, 8], [3, 16]),
+    "desc_vecs_per_thread": (0, [0, 1, 2, 4, 8, 16], [3, 32]),
     "desc_args_max": (16, [0, 1, 16], [-1, 17]),
     "desc_ahead": (0, [0, 1], [2]),
     "desc_side_tiles": (1, [0, 1], [2]),
@@ -741,7 +741,7 @@ KNOBS = {
     "desc_table_host_max": (128 * 1024, [0, 1 << 24], [-1]),
     "stream_wpe": (6, [0, 5, 6, 7], [1, 4, 8]),
     "table_wpe": (6, [0, 5, 6, 7], [4, 8]),
-    "desc_pipe": (5, [0, 2, 4, 5], [1, 3, 6]),
+    "desc_pipe": (5, [0, 2, 4, 5, 6], [1, 3, 7]),
     "stream_grab": (0, [0, 1, 64], [-1, 65]),
     "sync_mode": (0, [0, 1], [2]),
     "host_registered": (1, [0, 1], [2]),
@@ -844,3 +844,34 @@ def test_launch_after_pending_query_keeps_the_work_queue(bcp, engine, dev, queue
     ref = a.copy()
     ref[:999] ^= b
     assert np.array_equal(got, ref)
+
+
+@pytest.mark.parametrize("pipe", [5, 6])
+def test_descriptor_u16_mixed_batch(oracle, engine, dev, queue, pipe):
+    """64 KiB descriptor subtiles (desc_vecs_per_thread 16, rolling window 5
+    or 6) on a config-5-like batch -- log-uniform 1 KiB..1.5 MiB lengths,
+    widths 1..12 (wide tiles), misaligned sources and outputs, zero-length
+    chunks -- through desc_tiles + xor_desc_p, against the oracle."""
+    rng = np.random.default_rng(1600 + pipe)
+    stripes, refs = [], []
+    for _ in range(40):
+        n = int(rng.integers(1, 13))
+        lens = [int(x) for x in np.exp(rng.uniform(np.log(1024), np.log(1536 * 1024), size=n))]
+        if n > 2 and rng.random() < 0.2:
+            lens[-1] = 0
+        chunks = [rng.integers(0, 256, size=L, dtype=np.uint8) for L in lens]
+        pads = [int(x) for x in rng.integers(0, 16, size=n)]
+        stripes.append(dict(chunks=chunks, out_len=max(lens), pads=pads, dst_pad=int(rng.integers(0, 16))))
+        refs.append(oracle.xor_padded_np(chunks))
+    prev = {k: engine.option(k) for k in ("desc_vecs_per_thread", "desc_pipe", "desc_args_max")}
+    engine.option("desc_vecs_per_thread", 16)
+    engine.option("desc_pipe", pipe)
+    engine.option("desc_args_max", 0)
+    try:
+        outs = gpu_stripes(dev, queue, stripes)
+        assert engine.option("last_desc_vecs") == 16
+    finally:
+        for k, v in prev.items():
+            engine.option(k, v)
+    for i, (o, r) in enumerate(zip(outs, refs)):
+        assert np.array_equal(o, r), i

@@ -39,6 +39,11 @@ a = ap.parse_args()
 C = 512 * 1024
 PEAK = 8.0e12
 IN = int(a.gib * (1 << 30)) // C * C
+torch = None
+if not a.no_torch:
+    import torch as _t  # initialised before the engine: torch's HIP init fails after ours
+    torch = _t
+    torch.cuda.init()
 eng = bcp.Engine(0)
 q = eng.queue()
 src = eng.alloc(IN + (1 << 20))
@@ -46,12 +51,6 @@ out = eng.alloc(IN + (1 << 20))  # as large as the input: d2d / memset write it 
 red = eng.alloc(64)
 q.fill_synthetic(src, IN, seed=7)
 q.sync()
-
-torch = None
-if not a.no_torch:
-    import torch as _t
-    torch = _t
-
 
 def timed(fn, nbytes):
     ms = []
