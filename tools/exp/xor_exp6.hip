@@ -187,7 +187,7 @@ int main(int argc, char **argv) {
     a.base = base;
     hipLaunchKernelGGL(kV[v].fn, dim3(grid), dim3(256), 0, st, a);
     CK(hipGetLastError());
-    base += a.ntiles + grid;  // >= the grabs of any variant (units <= tiles)
+    base += (a.ntiles + a.grab - 1) / a.grab + grid;  // successful grabs + one failing grab per workgroup
   };
   // references: the shipped kernel of each width
   launch(0, ref3);
@@ -204,6 +204,7 @@ int main(int argc, char **argv) {
       if (r == 0) {
         CK(hipMemsetAsync(dst, 0, out_bytes, st));
         launch(v, dst);
+        CK(hipMemsetAsync(dcount, 0, 8, st));
         CK(bcp::launch_compare(st, grid, dst, kV[v].n == 3 ? ref3 : ref4, out_bytes, dcount));
         unsigned long long h;
         CK(hipMemcpyAsync(&h, dcount, 8, hipMemcpyDeviceToHost, st));
