@@ -749,6 +749,31 @@ extern "C" int bcp_host_free(bcp_engine *eng, void *hptr) {
   return 0;
 }
 
+extern "C" int bcp_host_register(bcp_engine *eng, void *hptr, size_t bytes) {
+  if (!eng || !hptr || !bytes) return -EINVAL;
+  int rc = set_device(eng);
+  if (rc) return rc;
+  void *dev = nullptr;
+  if (hipHostRegister(hptr, bytes, hipHostRegisterMapped | hipHostRegisterPortable) != hipSuccess) {
+    (void)hipGetLastError();
+    return -EIO;
+  }
+  if (hipHostGetDevicePointer(&dev, hptr, 0) != hipSuccess || dev != hptr) {
+    (void)hipGetLastError();
+    (void)hipHostUnregister(hptr);
+    return -EIO;  // the kernels address host rows by their host address
+  }
+  return 0;
+}
+
+extern "C" int bcp_host_unregister(bcp_engine *eng, void *hptr) {
+  if (!eng || !hptr) return -EINVAL;
+  int rc = set_device(eng);
+  if (rc) return rc;
+  HIP_RC(hipHostUnregister(hptr));
+  return 0;
+}
+
 extern "C" int bcp_h2d_async(bcp_queue *q, void *dst, const void *src, size_t bytes) {
   if (!q || (bytes && (!dst || !src))) return -EINVAL;
   if (!bytes) return 0;

@@ -21,3 +21,34 @@ typedef struct {
 } bcpi_settings;
 void bcpi_settings_get(bcpi_settings *s);
 int bcpi_settings_apply(const bcpi_settings *s);
+
+/* Shared row arena of a socket world (bcp_sock.c): memory mapped shared
+ * before the rank processes fork, so every rank sees it at the same address.
+ * A rank's P role takes its window rows from its own slice; a source of
+ * another process then reads its chunk straight into them (the socket
+ * transport's fill send) instead of sending the bytes through the socket.
+ * bcpi_arena_alloc returns NULL when this process has no slice or the slice
+ * is full (the caller allocates elsewhere); bcpi_arena_free returns 1 if p
+ * came from bcpi_arena_alloc. */
+void *bcpi_arena_alloc(size_t bytes, size_t *got);
+int bcpi_arena_free(void *p);
+/* Fill sends of this process so far: into an arena row / as a message
+ * (the receive lay outside the arena). */
+void bcpi_sock_fill_counts(uint64_t *arena, uint64_t *msg);
+/* The used arena block holding p (base, size); 0 if p is not in one. */
+int bcpi_arena_block(const void *p, void **base, size_t *size);
+/* Close every socket of w this process holds (the arena stays mapped). */
+void bcpi_sock_world_close_fds(bcp_sock_world *w);
+/* The whole arena of a world (every rank's slice); 0 if it has none. */
+int bcpi_sock_world_arena(const bcp_sock_world *w, void **lo, void **hi);
+
+/* Node fold server (bcp_task.c): ONE process holds the GPU and folds the
+ * window rows of every rank process's P role, which live in the shared
+ * arena, in batches across ranks (the fold service of BCP_FOLD_BATCHED,
+ * fed over sockets); the ranks never start a HIP runtime.  The server runs
+ * bcpi_foldsrv_main over its ends of nconn connections (one thread each)
+ * until every one is closed; a rank attaches its own connections. */
+int bcpi_foldsrv_main(int nconn, const int *fds, void *arena_lo, void *arena_hi);
+void bcpi_foldsrv_attach(int nconn, const int *fds);
+/* Windows the server folded for this process so far. */
+uint64_t bcpi_foldsrv_folds(void);

@@ -728,6 +728,7 @@ struct bcp_rank_pool {
     int broken;
     uint64_t seq;
     FILE *log;
+    pid_t srv_pid; /* node fold server (BCP_FOLD_SERVER), -1 if none */
 };
 
 typedef struct {
@@ -879,7 +880,7 @@ static void rank_command(const pool_cmd *c, int cmd_fd, int k, FILE *log, rank_r
 
 /* The body of rank process k+1 (never returns): serve commands until QUIT
  * or the caller's end closes. */
-static void rank_main(bcp_sock_world *w, int k, int cmd_fd, int res_fd, FILE *log)
+static void rank_main(bcp_sock_world *w, int k, int cmd_fd, int res_fd, FILE *log, int nconn, const int *srv_fds)
 {
     /* Every rank process holds its own HIP context on a GPU that several
      * ranks share.  With HIP's default of 4 hardware queues each, 9 ranks on
@@ -891,6 +892,11 @@ static void rank_main(bcp_sock_world *w, int k, int cmd_fd, int res_fd, FILE *lo
      * which comes after this in the rank. */
     if (!getenv("GPU_MAX_HW_QUEUES"))
         setenv("GPU_MAX_HW_QUEUES", "2", 1);
+    /* P-role rows inherited from the caller (host memory: the caller has no
+     * HIP runtime here) go; this rank takes its rows from its arena slice */
+    bcp_task_shutdown();
+    if (nconn)
+        bcpi_foldsrv_attach(nconn, srv_fds); /* folds go to the node fold server */
     bcp_transport_ops ops;
     int arc = bcp_sock_world_attach(w, k + 1, &ops);
     if (!arc)
@@ -904,6 +910,13 @@ static void rank_main(bcp_sock_world *w, int k, int cmd_fd, int res_fd, FILE *lo
             rep.rc = arc;
         else
             rank_command(&c, cmd_fd, k, log, &rep);
+        if (log && getenv("BCP_SOCK_STATS")) {
+            uint64_t fa = 0, fm = 0;
+            bcpi_sock_fill_counts(&fa, &fm);
+            fprintf(log, "rank %d: fill sends %llu into arena rows, %llu as messages; %llu windows folded by the server\n",
+                    k + 1, (unsigned long long)fa, (unsigned long long)fm, (unsigned long long)bcpi_foldsrv_folds());
+            fflush(log);
+        }
         ssize_t wr = write(res_fd, &rep, sizeof(rep));
         (void)wr;
         if (rep.rc)
@@ -934,6 +947,7 @@ int bcp_rank_pool_create(int ntargets, FILE *log, bcp_rank_pool **out)
         P->cmd_fd[k] = -1;
         st2rank[k] = k < ntargets ? k + 1 : -1; /* inherited by the ranks */
     }
+    P->srv_pid = -1;
     bcp_sock_world *w = NULL;
     int rc = bcp_sock_world_create(ntargets + 1, &w);
     int res[2] = {-1, -1};
@@ -949,6 +963,60 @@ int bcp_rank_pool_create(int ntargets, FILE *log, bcp_rank_pool **out)
         fflush(log);
     fflush(stdout);
     fflush(stderr);
+    /* Node fold server (environment BCP_FOLD_SERVER=1; needs the shared
+     * arena): one process holds the GPU for every rank's folds, over
+     * BCP_FOLD_SERVER_CONNS (default 12) connections per rank. */
+    int nconn = 0, *sfd = NULL, *rfd = NULL;
+    void *alo = NULL, *ahi = NULL;
+    const char *fs = getenv("BCP_FOLD_SERVER");
+    if (fs && atoi(fs) > 0 && bcpi_sock_world_arena(w, &alo, &ahi)) {
+        nconn = getenv("BCP_FOLD_SERVER_CONNS") ? atoi(getenv("BCP_FOLD_SERVER_CONNS")) : 12;
+        nconn = nconn < 1 ? 1 : nconn > 64 ? 64 : nconn;
+        sfd = malloc(sizeof(int) * (size_t)(ntargets * nconn));
+        rfd = malloc(sizeof(int) * (size_t)(ntargets * nconn));
+        if (!sfd || !rfd)
+            rc = -ENOMEM;
+        int made = 0;
+        for (; !rc && made < ntargets * nconn; made++) {
+            int sv[2];
+            if (socketpair(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC, 0, sv) != 0) {
+                rc = -errno;
+                break;
+            }
+            sfd[made] = sv[0];
+            rfd[made] = sv[1];
+        }
+        pid_t sp = rc ? -1 : fork();
+        if (sp == 0) {
+            close(res[0]);
+            close(res[1]);
+            for (int i = 0; i < made; i++)
+                close(rfd[i]);
+            bcpi_sock_world_close_fds(w); /* the ranks' sockets: EOF must reach partners */
+            if (getenv("GPU_MAX_HW_QUEUES") == NULL)
+                setenv("GPU_MAX_HW_QUEUES", "4", 1);
+            bcpi_foldsrv_main(made, sfd, alo, ahi);
+            _exit(0);
+        }
+        for (int i = 0; i < made; i++)
+            close(sfd[i]);
+        if (sp < 0 && !rc)
+            rc = -errno;
+        P->srv_pid = sp;
+        if (rc) {
+            for (int i = 0; i < made; i++)
+                close(rfd[i]);
+            free(sfd);
+            free(rfd);
+            close(res[0]);
+            close(res[1]);
+            bcp_sock_world_destroy(w);
+            if (sp > 0)
+                waitpid(sp, NULL, 0);
+            free(P);
+            return rc;
+        }
+    }
     for (int k = 0; k < ntargets && !rc; k++) {
         int sv[2];
         if (socketpair(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC, 0, sv) != 0) {
@@ -961,7 +1029,10 @@ int bcp_rank_pool_create(int ntargets, FILE *log, bcp_rank_pool **out)
             close(res[0]);
             for (int j = 0; j < k; j++)
                 close(P->cmd_fd[j]); /* the other ranks' command channels */
-            rank_main(w, k, sv[1], res[1], log);
+            for (int i = 0; i < ntargets * nconn; i++)
+                if (i / nconn != k)
+                    close(rfd[i]); /* the other ranks' fold-server connections */
+            rank_main(w, k, sv[1], res[1], log, nconn, nconn ? rfd + k * nconn : NULL);
         }
         close(sv[1]);
         if (pid < 0) {
@@ -974,6 +1045,10 @@ int bcp_rank_pool_create(int ntargets, FILE *log, bcp_rank_pool **out)
     }
     close(res[1]);
     P->res_fd = res[0];
+    for (int i = 0; i < ntargets * nconn; i++)
+        close(rfd[i]);
+    free(sfd);
+    free(rfd);
     bcp_sock_world_destroy(w); /* the ranks hold their own ends now */
     if (rc) {
         bcp_rank_pool_destroy(P);
@@ -1162,6 +1237,14 @@ int bcp_rank_pool_destroy(bcp_rank_pool *P)
                 rc = -ECHILD;
             P->pids[k] = -1;
         }
+    if (P->srv_pid > 0) { /* leaves once every rank closed its connections */
+        int status = 0;
+        while (waitpid(P->srv_pid, &status, 0) < 0 && errno == EINTR)
+            ;
+        if (!WIFEXITED(status) || WEXITSTATUS(status) != 0)
+            rc = -ECHILD;
+        P->srv_pid = -1;
+    }
     if (P->res_fd >= 0)
         close(P->res_fd);
     free(P);

@@ -548,6 +548,222 @@ int bcp_task_fold_stats(uint64_t *windows, uint64_t *launches)
     return 0;
 }
 
+/* ---- node fold server (rank processes; bcp_host.h) -------------------------
+ * Rank processes that each start a HIP runtime put one context per rank on
+ * the GPU (nine on one MI355X for config 5); the device's queues, not the
+ * fold, then set the rate.  With the server, the P roles'
+ * window rows and outputs live in the socket world's shared arena and every
+ * fold goes to ONE process that holds the GPU: one thread per connection
+ * reads a request (rows, pitch, data bytes per row, output), registers the
+ * arena blocks it has not seen, and folds through the fold service above
+ * (flat combining: windows of every rank share a launch); the reply carries
+ * the fold's status.  A rank has several connections (lane tag modulo their
+ * number), each used by one lane at a time, request then reply. */
+#define FS_MAGIC 0x62636673u /* "bcfs" */
+#define FS_MAX_CONN 64
+
+typedef struct {
+    uint32_t magic;
+    int32_t n, st, pad;
+    uint64_t rows, pitch, nbytes, out;
+    uint64_t rows_base, rows_size, out_base, out_size;
+} fs_req;
+
+typedef struct {
+    uint32_t magic;
+    int32_t rc;
+} fs_rep;
+
+static int fs_io(int fd, void *buf, size_t n, int wr)
+{
+    uint8_t *p = buf;
+    while (n) {
+        ssize_t r = wr ? write(fd, p, n) : read(fd, p, n);
+        if (r < 0 && errno == EINTR)
+            continue;
+        if (r <= 0)
+            return r < 0 ? -errno : -EPIPE;
+        p += r;
+        n -= (size_t)r;
+    }
+    return 0;
+}
+
+/* rank side */
+static struct {
+    int fd;
+    pthread_mutex_t mu;
+} g_srv[FS_MAX_CONN];
+static int g_srv_n;
+static __thread int t_lane_tag;
+static uint64_t g_remote_folds; /* windows folded by the server for this process */
+
+uint64_t bcpi_foldsrv_folds(void)
+{
+    return __atomic_load_n(&g_remote_folds, __ATOMIC_RELAXED);
+}
+
+static bcp_xor_hook_fn g_srv_hook; /* the test double the server inherited */
+
+void bcpi_foldsrv_attach(int nconn, const int *fds)
+{
+    pthread_mutex_lock(&g_lock);
+    g_srv_hook = g_hook; /* the server was forked from the same state */
+    pthread_mutex_unlock(&g_lock);
+    g_srv_n = 0;
+    for (int i = 0; i < nconn && i < FS_MAX_CONN; i++) {
+        g_srv[i].fd = fds[i];
+        pthread_mutex_init(&g_srv[i].mu, NULL);
+        g_srv_n++;
+    }
+}
+
+/* The fold of one window by the node fold server (rows and out in the
+ * arena); -ENXIO if they are not, so the caller folds elsewhere. */
+static int fold_remote(int st, const uint8_t *rows, size_t pitch, const size_t *valid, size_t nbytes, int n,
+                       uint8_t *out, int use_hook)
+{
+    /* use_hook: the server folds with the test double it inherited (CPU
+     * tests of this path; the rows then hold whole zero-padded windows) */
+    fs_req q = {FS_MAGIC, n, st, use_hook, (uint64_t)(uintptr_t)rows, pitch, nbytes, (uint64_t)(uintptr_t)out,
+                0, 0, 0, 0};
+    void *rb, *ob;
+    size_t rs, os;
+    if (n < 1 || n > MAX_STORAGE_TARGETS || !bcpi_arena_block(rows, &rb, &rs) || !bcpi_arena_block(out, &ob, &os))
+        return -ENXIO;
+    q.rows_base = (uint64_t)(uintptr_t)rb;
+    q.rows_size = rs;
+    q.out_base = (uint64_t)(uintptr_t)ob;
+    q.out_size = os;
+    uint64_t v[MAX_STORAGE_TARGETS];
+    for (int j = 0; j < n; j++)
+        v[j] = valid[j];
+    const int c = (t_lane_tag < 0 ? -t_lane_tag : t_lane_tag) % g_srv_n;
+    fs_rep r = {0, -EPROTO};
+    pthread_mutex_lock(&g_srv[c].mu);
+    int rc = fs_io(g_srv[c].fd, &q, sizeof(q), 1);
+    if (!rc)
+        rc = fs_io(g_srv[c].fd, v, (size_t)n * sizeof(uint64_t), 1);
+    if (!rc)
+        rc = fs_io(g_srv[c].fd, &r, sizeof(r), 0);
+    pthread_mutex_unlock(&g_srv[c].mu);
+    if (!rc && r.magic != FS_MAGIC)
+        rc = -EPROTO;
+    if (!rc && !r.rc)
+        __atomic_fetch_add(&g_remote_folds, 1, __ATOMIC_RELAXED);
+    return rc ? rc : r.rc;
+}
+
+/* server side */
+static struct {
+    uint8_t *lo, *hi;
+    pthread_mutex_t mu;
+    struct {
+        uint8_t *p;
+        size_t n;
+    } reg[4096];
+    int nreg;
+} g_fs = {.mu = PTHREAD_MUTEX_INITIALIZER};
+
+static int fs_block_ok(uint64_t base, uint64_t size, uint64_t p, uint64_t len)
+{
+    const uint64_t lo = (uint64_t)(uintptr_t)g_fs.lo, hi = (uint64_t)(uintptr_t)g_fs.hi;
+    return size > 0 && base >= lo && base <= hi && size <= hi - base && p >= base && p <= base + size &&
+           len <= base + size - p;
+}
+
+/* Register an arena block with the device once (blocks are reused at the
+ * same place and size, so a registration stays valid for the process). */
+static int fs_register(bcp_engine *e, uint64_t base, uint64_t size)
+{
+    int rc = 0;
+    pthread_mutex_lock(&g_fs.mu);
+    int i = 0;
+    for (; i < g_fs.nreg; i++)
+        if ((uint64_t)(uintptr_t)g_fs.reg[i].p == base && g_fs.reg[i].n == size)
+            break;
+    if (i == g_fs.nreg) {
+        if (g_fs.nreg == (int)(sizeof(g_fs.reg) / sizeof(g_fs.reg[0])))
+            rc = -ENOSPC;
+        else if (!(rc = bcp_host_register(e, (void *)(uintptr_t)base, (size_t)size))) {
+            g_fs.reg[g_fs.nreg].p = (uint8_t *)(uintptr_t)base;
+            g_fs.reg[g_fs.nreg].n = (size_t)size;
+            g_fs.nreg++;
+        }
+    }
+    pthread_mutex_unlock(&g_fs.mu);
+    return rc;
+}
+
+static void *fs_conn_main(void *arg)
+{
+    const int fd = (int)(intptr_t)arg;
+    for (;;) {
+        fs_req q;
+        if (fs_io(fd, &q, sizeof(q), 0))
+            break; /* the rank closed its end */
+        uint64_t v[MAX_STORAGE_TARGETS];
+        size_t valid[MAX_STORAGE_TARGETS];
+        fs_rep r = {FS_MAGIC, 0};
+        if (q.magic != FS_MAGIC || q.n < 1 || q.n > MAX_STORAGE_TARGETS)
+            break; /* out of step: drop the connection (the rank sees EPIPE) */
+        if (fs_io(fd, v, (size_t)q.n * sizeof(uint64_t), 0))
+            break;
+        int ok = fs_block_ok(q.out_base, q.out_size, q.out, q.nbytes) && q.pitch > 0 && q.nbytes <= q.pitch;
+        for (int j = 0; j < q.n && ok; j++) {
+            valid[j] = (size_t)v[j];
+            ok = v[j] <= q.pitch &&
+                 fs_block_ok(q.rows_base, q.rows_size, q.rows + (uint64_t)j * q.pitch, q.pad ? q.nbytes : v[j]);
+        }
+        bcp_engine *e = NULL;
+        fold_svc *S = NULL;
+        int dev = -1;
+        bcp_xor_hook_fn hook = NULL;
+        void *hctx = NULL;
+        if (q.pad) {
+            pthread_mutex_lock(&g_lock);
+            hook = g_hook;
+            hctx = g_hook_ctx;
+            pthread_mutex_unlock(&g_lock);
+        }
+        if (!ok)
+            r.rc = -EFAULT;
+        else if (q.pad)
+            r.rc = hook ? hook((uint8_t *)(uintptr_t)q.out, (size_t)q.nbytes, (const uint8_t *)(uintptr_t)q.rows,
+                               (size_t)q.pitch, q.n, hctx)
+                        : -ENOSYS;
+        else if (!(r.rc = engine_for_target(q.st, &e, &dev)) && !(r.rc = fs_register(e, q.rows_base, q.rows_size)) &&
+                 !(r.rc = fs_register(e, q.out_base, q.out_size)) && !(r.rc = svc_get(dev, e, &S)))
+            r.rc = fold_batched(S, (const uint8_t *)(uintptr_t)q.rows, (size_t)q.pitch, valid, (size_t)q.nbytes,
+                                q.n, (uint8_t *)(uintptr_t)q.out);
+        if (fs_io(fd, &r, sizeof(r), 1))
+            break;
+    }
+    close(fd);
+    return NULL;
+}
+
+int bcpi_foldsrv_main(int nconn, const int *fds, void *arena_lo, void *arena_hi)
+{
+    g_fs.lo = arena_lo;
+    g_fs.hi = arena_hi;
+    /* batches in flight at once (the fold service's width; every rank's
+     * windows share it): environment BCP_FOLD_SERVER_INFLIGHT */
+    if (getenv("BCP_FOLD_SERVER_INFLIGHT"))
+        (void)bcp_task_set_fold_inflight(atoi(getenv("BCP_FOLD_SERVER_INFLIGHT")));
+    pthread_t th[FS_MAX_CONN * MAX_STORAGE_TARGETS];
+    int started = 0;
+    for (int i = 0; i < nconn && i < (int)(sizeof(th) / sizeof(th[0])); i++)
+        if (pthread_create(&th[started], NULL, fs_conn_main, (void *)(intptr_t)fds[i]) == 0)
+            started++;
+        else
+            close(fds[i]); /* the rank's lanes on it see EPIPE */
+    for (int i = 0; i < started; i++)
+        pthread_join(th[i], NULL);
+    /* registrations end with the process; the fold service and engines go */
+    return bcp_task_shutdown();
+}
+
 /* ---- fold resources: a shared pool, reused across tasks, lanes and runs --
  * One resource = pinned, device-mapped window rows + output block (+ a HIP
  * queue and device buffers for the per-lane fold modes, made on first use).
@@ -580,6 +796,11 @@ static void host_free(fold_res *R, void *p)
 {
     if (!p)
         return;
+    if (bcpi_arena_free(p)) { /* a row block of the socket world's shared arena */
+        if (R->device >= 0)
+            (void)bcp_host_unregister(R->eng, p);
+        return;
+    }
     if (R->device >= 0)
         bcp_host_free(R->eng, p);
     else
@@ -664,12 +885,15 @@ static void res_release(fold_res *R)
 }
 
 /* kind: 0 host (pinned + mapped on a GPU resource), 1 device memory the
- * host writes (window rows under DEVICE_ROWS) */
+ * host writes (window rows under DEVICE_ROWS), 2 host window rows: from
+ * this rank's slice of the socket world's shared arena when there is one
+ * (other rank processes' sources then read their chunks straight into them,
+ * bcp_sock.c), registered with the GPU; else as 0 */
 static int grow(fold_res *R, uint8_t **p, size_t *cap, size_t need, int kind)
 {
     if (*cap >= need && *p)
         return 0;
-    if (kind)
+    if (kind == 1)
         bcp_dev_free(R->eng, *p);
     else
         host_free(R, *p);
@@ -681,7 +905,18 @@ static int grow(fold_res *R, uint8_t **p, size_t *cap, size_t need, int kind)
     while (c < need)
         c <<= 1;
     int rc = 0;
-    if (kind)
+    if (kind == 2 && (*p = bcpi_arena_alloc(c, &c))) {
+        if (R->device < 0 || !bcp_host_register(R->eng, *p, c)) {
+            *cap = c;
+            return 0;
+        }
+        bcpi_arena_free(*p); /* not addressable by the device: ordinary rows */
+        *p = NULL;
+        c = (size_t)1 << 20;
+        while (c < need)
+            c <<= 1;
+    }
+    if (kind == 1)
         rc = bcp_dev_alloc_hostwrite(R->eng, c, (void **)p);
     else if (R->device >= 0)
         rc = bcp_host_alloc_mapped(R->eng, c, (void **)p);
@@ -756,10 +991,11 @@ static int res_acquire(HostState *hs, int use_gpu, int dev_rows, size_t rows_byt
         R->h_cap = R->h_cap1 = 0;
         R->rows_dev = dev_rows;
     }
-    if ((rc = grow(R, &R->h_win[0], &R->h_cap, rows_bytes, dev_rows)) ||
-        (windows > 1 && (rc = grow(R, &R->h_win[1], &R->h_cap1, rows_bytes, dev_rows))) ||
-        (rc = grow(R, &R->h_par, &R->hp_cap, nbytes, 0)))
-        goto fail;
+    const int row_kind = dev_rows ? 1 : 2;
+    if ((rc = grow(R, &R->h_win[0], &R->h_cap, rows_bytes, row_kind)) ||
+        (windows > 1 && (rc = grow(R, &R->h_win[1], &R->h_cap1, rows_bytes, row_kind))) ||
+        (rc = grow(R, &R->h_par, &R->hp_cap, nbytes, dev < 0 && g_srv_n > 0 ? 2 : 0)))
+        goto fail; /* (with a node fold server the output is an arena block too) */
     *out = R;
     return 0;
 fail:
@@ -772,6 +1008,12 @@ fail:
 static int fold_window(fold_res *R, HostState *hs, int mode, bcp_xor_hook_fn hook, void *ctx, const uint8_t *rows,
                        size_t pitch, const size_t *valid, size_t nbytes, int n, uint8_t *out)
 {
+    void *ab;
+    size_t az;
+    /* the node fold server folds (with a test double only if it has the
+     * same one: it was forked when the pool was made) */
+    if (R->device < 0 && g_srv_n > 0 && (!hook || hook == g_srv_hook) && bcpi_arena_block(rows, &ab, &az))
+        return fold_remote(hs->storage_target, rows, pitch, valid, nbytes, n, out, hook != NULL);
     if (hook) {
         static int warned = 0; /* lanes race here: atomic exchange */
         if (!__atomic_exchange_n(&warned, 1, __ATOMIC_RELAXED))
@@ -1216,9 +1458,24 @@ static void parity_generator(const bcp_transport_ops *T, const char *path, const
      * kind from the fold in tools/exp measurements) */
     const int pinned_rows = hook == NULL || getenv("BCP_HOOK_PINNED_ROWS") != NULL;
     const int dev_rows = hook == NULL && mode == BCP_FOLD_DEVICE_ROWS;
-    int res_rc = expected_messages ? res_acquire(hs, pinned_rows, dev_rows, pitch * (size_t)n, buffer_size,
-                                                 expected_messages, &L)
+    /* a node fold server (rank processes) folds for the fold-service modes:
+     * rows and output from the arena, no HIP runtime in this process */
+    const int remote = g_srv_n > 0 && (hook != NULL || mode == BCP_FOLD_BATCHED || mode == BCP_FOLD_PIPELINED);
+    t_lane_tag = ti.tag;
+    int res_rc = expected_messages ? res_acquire(hs, remote ? 0 : pinned_rows, dev_rows, pitch * (size_t)n,
+                                                 buffer_size, expected_messages, &L)
                                    : 0;
+    if (remote && !res_rc && L) {
+        void *b;
+        size_t z;
+        if (!bcpi_arena_block(L->h_win[0], &b, &z) || !bcpi_arena_block(L->h_par, &b, &z) ||
+            (expected_messages > 1 && !bcpi_arena_block(L->h_win[1], &b, &z))) {
+            /* the arena slice is full: fold in this process as without a server */
+            res_release(L);
+            L = NULL;
+            res_rc = res_acquire(hs, pinned_rows, dev_rows, pitch * (size_t)n, buffer_size, expected_messages, &L);
+        }
+    }
     if (res_rc) {
         LOGERR("no fold resources for '%s' on st %d: %s\n", path, hs->storage_target, bcp_strerror(res_rc));
         if (!have_had_error)
@@ -1263,7 +1520,11 @@ static void parity_generator(const bcp_transport_ops *T, const char *path, const
     const int pad_rows = implicit_pad && !res_rc && (hook != NULL || mode == BCP_FOLD_STAGED);
     /* PIPELINED: one window whose rows the sources fill directly (send_fill
      * transports); otherwise it folds like ZERO_COPY */
-    int pipelined = mode == BCP_FOLD_PIPELINED && !res_rc && expected_messages == 1 && T->send_fill;
+    /* (the sources publish their progress through this process's watch
+     * table and launch range folds on this lane's queue: in-process ranks,
+     * i.e. the loopback transport, only) */
+    int pipelined = mode == BCP_FOLD_PIPELINED && !res_rc && expected_messages == 1 && T->send_fill &&
+                    T->send_fill == bcp_lb_transport()->send_fill;
     if (pipelined && !hook && !L->q && bcp_queue_create(L->eng, &L->q))
         pipelined = 0;
     if (serial_io && !res_rc)

@@ -126,6 +126,12 @@ int bcp_host_alloc(bcp_engine *eng, size_t bytes, void **hptr);
  * data.  Free with bcp_host_free. */
 int bcp_host_alloc_mapped(bcp_engine *eng, size_t bytes, void **hptr);
 int bcp_host_free(bcp_engine *eng, void *hptr);
+/* Register caller-owned host memory (e.g. a shared mapping other processes
+ * write) so kernels read and write it in place at the same address, like
+ * bcp_host_alloc_mapped memory; -EIO if the device cannot address it at its
+ * host address.  Unregister before the memory is unmapped or reused. */
+int bcp_host_register(bcp_engine *eng, void *hptr, size_t bytes);
+int bcp_host_unregister(bcp_engine *eng, void *hptr);
 /* Async copies, in order on q. */
 int bcp_h2d_async(bcp_queue *q, void *dst, const void *src, size_t bytes);
 int bcp_d2h_async(bcp_queue *q, void *dst, const void *src, size_t bytes);

@@ -360,17 +360,25 @@ print("pool ok")
 """
 
 
-def test_rank_pool_on_device(tmp_path):
-    """Rank processes kept alive across runs with their HIP contexts: two gen
-    runs over different data and a rebuild through ONE pool, the P roles
-    folding on the device (default mode: rank processes on sockets fold
-    through the batched service), parity and rebuilt
-    chunks checked against the oracle.  In a fresh process: a pool cannot be
-    forked from one that has used the GPU."""
+@pytest.mark.parametrize("mode", ["ranks", "fold-server", "no-arena"])
+def test_rank_pool_on_device(tmp_path, mode):
+    """Rank processes kept alive across runs: two gen runs over different
+    data and a rebuild through ONE pool, the P roles folding on the device,
+    parity and rebuilt chunks checked against the oracle.  "ranks": every
+    rank holds its own HIP context and folds through its batched service,
+    its sources filling P roles' rows in the shared arena; "fold-server":
+    one server process holds the GPU and folds every rank's windows
+    (BCP_FOLD_SERVER=1; the ranks never start HIP); "no-arena": rows in each
+    rank's own registered memory, windows through the sockets.  In a fresh
+    process: a pool cannot be forked from one that has used the GPU."""
     import subprocess
     import sys
+    env = dict(os.environ)
+    env["BCP_FOLD_SERVER"] = "1" if mode == "fold-server" else "0"
+    if mode == "no-arena":
+        env["BCP_SOCK_ARENA_MB"] = "0"
     r = subprocess.run([sys.executable, "-c", POOL_SCRIPT, str(tmp_path), HERE], capture_output=True, text=True,
-                       timeout=240)
+                       timeout=240, env=env)
     assert r.returncode == 0 and "pool ok" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]
 
 

@@ -308,3 +308,69 @@ def test_caller_defined_st2rank_and_hoststate(bcp, tmp_path):
     r = subprocess.run([str(exe), str(tmp_path / "store")], capture_output=True, text=True, timeout=180)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "caller_test ok" in r.stdout
+
+
+def _fill_counts(path):
+    arena = msg = srv = 0
+    for line in open(path):
+        if "fill sends" in line:
+            # "rank k: fill sends A into arena rows, M as messages; S windows folded by the server"
+            w = line.split()
+            arena += int(w[4])
+            msg += int(w[8])
+            srv += int(w[11])
+    return arena, msg, srv
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("arena_mb,server", [("2048", "0"), ("0", "0"), ("2048", "1"), ("0", "1")],
+                         ids=["arena", "no-arena", "arena-fold-server", "no-arena-no-server"])
+def test_rank_processes_fill_into_shared_rows(bcp, oracle, cpu_hook, tmp_path, monkeypatch, arena_mb, server):
+    """Rank processes with the shared row arena (bcp_sock.c): every
+    single-window source reads its chunk straight into the P role's row in
+    the arena (RTS / CTS / DONE over the sockets, no payload through them);
+    multi-window stripes with replay (A3-q1) still go as messages.  Without
+    the arena (BCP_SOCK_ARENA_MB=0) no fill sends at all.  With the node
+    fold server (BCP_FOLD_SERVER=1, arena only) every P role's window goes to
+    the server process over its connections (here it folds with the test
+    double it inherited).  Parity and a rebuild equal the oracle each way."""
+    import ctypes
+    monkeypatch.setenv("BCP_SOCK_STATS", "1")
+    monkeypatch.setenv("BCP_SOCK_ARENA_MB", arena_mb)
+    monkeypatch.setenv("BCP_FOLD_SERVER", server)
+    rng = np.random.default_rng(77)
+    root = str(tmp_path / "store")
+    ntargets = 5
+    files = _random_files(rng, ntargets, 40, 700_000)
+    files.append(("big/r", [0, 3], 1, [10 * MiB + 3, 21 * MiB]))
+    items, contents = S.populate(root, ntargets, files, seed=5)
+    libc = ctypes.CDLL(None)
+    libc.fopen.restype = ctypes.c_void_p
+    libc.fopen.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+    libc.fclose.argtypes = [ctypes.c_void_p]
+    logp = str(tmp_path / "ranks.log")
+    f = libc.fopen(logp.encode(), b"w")
+    try:
+        st = bcp.gen_run_procs(root, ntargets, items, nlanes=3, log=f)
+    finally:
+        libc.fclose(f)
+    assert st.errors == 0
+    for (path, holders, p, lens) in files:
+        assert S.read_file(S.parity_path(root, p, path)) == oracle.gen_parity_file(contents[path]), path
+    arena, msg, srv = _fill_counts(logp)
+    if arena_mb == "0":
+        assert arena == 0 and msg == 0 and srv == 0
+    else:
+        assert arena >= sum(len(h) for (_, h, _, _) in files[:-1]) and msg == 0
+        # one fold per window of every stripe with a source (the 21 MiB one has 3)
+        assert srv == (len([f for f in files if f[1]]) + 2 if server == "1" else 0)
+    victim = 2
+    lost = {}
+    for (path, holders, p, lens) in files:
+        if victim in holders:
+            lost[path] = S.read_file(S.chunk_path(root, victim, path))
+            os.remove(S.chunk_path(root, victim, path))
+    st = bcp.rebuild_run_procs(root, ntargets, victim, items)
+    assert st.errors == 0
+    for path, data in lost.items():
+        assert S.read_file(S.chunk_path(root, victim, path)) == data, path
