@@ -963,13 +963,15 @@ int bcp_rank_pool_create(int ntargets, FILE *log, bcp_rank_pool **out)
         fflush(log);
     fflush(stdout);
     fflush(stderr);
-    /* Node fold server (environment BCP_FOLD_SERVER=1; needs the shared
-     * arena): one process holds the GPU for every rank's folds, over
-     * BCP_FOLD_SERVER_CONNS (default 12) connections per rank. */
+    /* Node fold server (default; environment BCP_FOLD_SERVER=0 turns it
+     * off; needs the shared arena): one process holds the GPU for every
+     * rank's folds, over BCP_FOLD_SERVER_CONNS (default 12) connections per
+     * rank.  Config 5 over nine rank processes on one MI355X: 35-37 GiB/s,
+     * against 13-14 with a HIP context per rank. */
     int nconn = 0, *sfd = NULL, *rfd = NULL;
     void *alo = NULL, *ahi = NULL;
     const char *fs = getenv("BCP_FOLD_SERVER");
-    if (fs && atoi(fs) > 0 && bcpi_sock_world_arena(w, &alo, &ahi)) {
+    if ((!fs || atoi(fs) > 0) && bcpi_sock_world_arena(w, &alo, &ahi)) {
         nconn = getenv("BCP_FOLD_SERVER_CONNS") ? atoi(getenv("BCP_FOLD_SERVER_CONNS")) : 12;
         nconn = nconn < 1 ? 1 : nconn > 64 ? 64 : nconn;
         sfd = malloc(sizeof(int) * (size_t)(ntargets * nconn));
