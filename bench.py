@@ -87,9 +87,18 @@ def parse():
 def pmc_traffic(workload_key: str, kernel_tag: str):
     """Committed profile summary (tools/pmc_summary.py) of this workload and
     kernel: per-launch HBM bytes (PMC), rocprofv3 kernel-trace average, the
-    files and the code commit they came from; the newest matching one."""
+    files and the code commit they came from: from the set profiles/CURRENT_SET
+    names when it has one, else the last matching one in path order."""
     best = None
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "**", "*pmc*.json"), recursive=True)):
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "**", "*pmc*.json"), recursive=True))
+    try:
+        cur = open(os.path.join(ROOT, "profiles", "CURRENT_SET")).read().strip()
+    except OSError:
+        cur = ""
+    if cur:  # the current set last, so its match wins
+        key = os.path.join(ROOT, cur) + os.sep
+        paths = [x for x in paths if not x.startswith(key)] + [x for x in paths if x.startswith(key)]
+    for path in paths:
         try:
             doc = json.load(open(path))
         except (OSError, ValueError):
