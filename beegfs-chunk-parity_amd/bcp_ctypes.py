@@ -675,6 +675,7 @@ def set_xor_hook(fn_addr: int | None, ctx: int | None = None):
 
 FOLD_ZERO_COPY, FOLD_STAGED, FOLD_BATCHED, FOLD_STREAMED, FOLD_DEVICE_ROWS, FOLD_PIPELINED = 0, 1, 2, 3, 4, 5
 INJECT_FOLD_RES, INJECT_DRAIN_ROW, INJECT_SEND_BUF, INJECT_THREAD, INJECT_READ = 1, 2, 4, 8, 16
+INJECT_FOLD_SERVER = 32
 
 
 def set_fold_mode(mode: int) -> int:

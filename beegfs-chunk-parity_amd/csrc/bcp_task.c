@@ -31,6 +31,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/socket.h>
 #include <sys/stat.h>
 #include <sys/types.h>
 #include <time.h>
@@ -262,7 +263,7 @@ static bcp_transport_ops transport_now(void)
 }
 
 /* ---- failure injection (tests) ------------------------------------------ */
-#define NSITES 5
+#define NSITES 6
 static int g_inj_after[NSITES], g_inj_count[NSITES];
 
 static int site_index(int site)
@@ -273,6 +274,7 @@ static int site_index(int site)
     case BCP_INJECT_SEND_BUF: return 2;
     case BCP_INJECT_THREAD: return 3;
     case BCP_INJECT_READ: return 4;
+    case BCP_INJECT_FOLD_SERVER: return 5;
     default: return -1;
     }
 }
@@ -578,7 +580,7 @@ static int fs_io(int fd, void *buf, size_t n, int wr)
 {
     uint8_t *p = buf;
     while (n) {
-        ssize_t r = wr ? write(fd, p, n) : read(fd, p, n);
+        ssize_t r = wr ? send(fd, p, n, MSG_NOSIGNAL) : read(fd, p, n); /* a closed peer: EPIPE, no SIGPIPE */
         if (r < 0 && errno == EINTR)
             continue;
         if (r <= 0)
@@ -709,6 +711,8 @@ static void *fs_conn_main(void *arg)
             break; /* out of step: drop the connection (the rank sees EPIPE) */
         if (fs_io(fd, v, (size_t)q.n * sizeof(uint64_t), 0))
             break;
+        if (bcpi_inject_hit(BCP_INJECT_FOLD_SERVER))
+            break; /* (failure injection) the rank's fold sees EPIPE */
         int ok = fs_block_ok(q.out_base, q.out_size, q.out, q.nbytes) && q.pitch > 0 && q.nbytes <= q.pitch;
         for (int j = 0; j < q.n && ok; j++) {
             valid[j] = (size_t)v[j];

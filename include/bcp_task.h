@@ -197,12 +197,15 @@ void bcp_task_set_xor_hook(bcp_xor_hook_fn fn, void *ctx);
  * with truncated receives is used), the source role's window buffer, the
  * runners' lane-thread creation, and a source's chunk read into a row it
  * fills directly (as EIO; a source reading in pieces for a PIPELINED P role
- * fails a piece after the first).  count 0 clears the site. */
+ * fails a piece after the first), and the node fold server dropping a rank's
+ * connection instead of answering a fold (the server process takes the
+ * setting when a rank pool forks it).  count 0 clears the site. */
 #define BCP_INJECT_FOLD_RES 1
 #define BCP_INJECT_DRAIN_ROW 2
 #define BCP_INJECT_SEND_BUF 4
 #define BCP_INJECT_THREAD 8
 #define BCP_INJECT_READ 16
+#define BCP_INJECT_FOLD_SERVER 32
 int bcp_task_inject_failure(int site, int after, int count);
 
 /* ---- transport seam (the MPI subset process_task speaks) ---------------- */

@@ -29,7 +29,8 @@ KiB, MiB = 1024, 1024 * 1024
 @pytest.fixture(autouse=True)
 def _clean(bcp):
     yield
-    for site in (bcp.INJECT_FOLD_RES, bcp.INJECT_DRAIN_ROW, bcp.INJECT_SEND_BUF, bcp.INJECT_THREAD):
+    for site in (bcp.INJECT_FOLD_RES, bcp.INJECT_DRAIN_ROW, bcp.INJECT_SEND_BUF, bcp.INJECT_THREAD,
+                 bcp.INJECT_FOLD_SERVER):
         bcp.inject_failure(site, 0, 0)
     bcp.set_transport(None)
 
@@ -374,3 +375,26 @@ def test_rank_processes_fill_into_shared_rows(bcp, oracle, cpu_hook, tmp_path, m
     assert st.errors == 0
     for path, data in lost.items():
         assert S.read_file(S.chunk_path(root, victim, path)) == data, path
+
+
+@pytest.mark.timeout(300)
+def test_fold_server_losing_a_connection_fails_tasks_not_the_run(bcp, oracle, cpu_hook, tmp_path, monkeypatch):
+    """The node fold server drops a rank's connection instead of answering
+    (failure injection, taken by the server when the pool forks it): the
+    lanes folding through it get EPIPE -- no SIGPIPE, no hang --, their P
+    roles raise the sticky error and the run ends with errors.  A new pool
+    (a new server) then writes every parity file correctly."""
+    monkeypatch.setenv("BCP_FOLD_SERVER", "1")
+    rng = np.random.default_rng(91)
+    root = str(tmp_path)
+    ntargets = 5
+    files = _random_files(rng, ntargets, 30, 300_000)
+    items, contents = S.populate(root, ntargets, files, seed=4)
+    bcp.inject_failure(bcp.INJECT_FOLD_SERVER, 3, 1)
+    st = bcp.gen_run_procs(root, ntargets, items, nlanes=3)
+    assert st.errors > 0
+    bcp.inject_failure(bcp.INJECT_FOLD_SERVER, 0, 0)
+    st = bcp.gen_run_procs(root, ntargets, items, nlanes=3)
+    assert st.errors == 0
+    for (path, holders, p, lens) in files:
+        assert S.read_file(S.parity_path(root, p, path)) == oracle.gen_parity_file(contents[path]), path
