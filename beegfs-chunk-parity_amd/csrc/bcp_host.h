@@ -52,3 +52,10 @@ int bcpi_foldsrv_main(int nconn, const int *fds, void *arena_lo, void *arena_hi)
 void bcpi_foldsrv_attach(int nconn, const int *fds);
 /* Windows the server folded for this process so far. */
 uint64_t bcpi_foldsrv_folds(void);
+/* A fill into another process's arena row is running on this thread: report
+ * its final prefix (bcp_sock.c, PROG frames); 0 / -errno, -ENOTCONN if not. */
+int bcpi_fill_progress_on(void);
+int bcpi_fill_progress(size_t bytes, int redo);
+/* The receiving side: `bytes` leading bytes of the receive row `row` are
+ * final (redo: bytes published before were replaced) -- bcp_task.c. */
+void bcpi_row_progress(const void *row, size_t bytes, int redo);

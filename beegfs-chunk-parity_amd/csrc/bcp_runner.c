@@ -913,8 +913,13 @@ static void rank_main(bcp_sock_world *w, int k, int cmd_fd, int res_fd, FILE *lo
         if (log && getenv("BCP_SOCK_STATS")) {
             uint64_t fa = 0, fm = 0;
             bcpi_sock_fill_counts(&fa, &fm);
-            fprintf(log, "rank %d: fill sends %llu into arena rows, %llu as messages; %llu windows folded by the server\n",
-                    k + 1, (unsigned long long)fa, (unsigned long long)fm, (unsigned long long)bcpi_foldsrv_folds());
+            uint64_t pw = 0, pr = 0;
+            bcp_task_pipe_stats(&pw, &pr);
+            fprintf(log,
+                    "rank %d: fill sends %llu into arena rows, %llu as messages; %llu windows folded by the server;"
+                    " pipelined windows %llu ranges %llu\n",
+                    k + 1, (unsigned long long)fa, (unsigned long long)fm, (unsigned long long)bcpi_foldsrv_folds(),
+                    (unsigned long long)pw, (unsigned long long)pr);
             fflush(log);
         }
         ssize_t wr = write(res_fd, &rep, sizeof(rep));

@@ -53,6 +53,7 @@
 #define FRAME_RTS 0x62637072u   /* "bcpr": fill send of len bytes wants a receive */
 #define FRAME_CTS 0x62637063u   /* "bcpc": {address, capacity} of the matched receive */
 #define FRAME_DONE 0x62637064u  /* "bcpd": {bytes} filled; completes the receive */
+#define FRAME_PROG 0x62637067u  /* "bcpg": {bytes, redo} of the fill are final (pipelined fold) */
 
 typedef struct {
     uint32_t magic;
@@ -579,6 +580,22 @@ static int read_control(bcp_sock_world *w, int src, const frame_hdr *h)
         pthread_mutex_unlock(&w->mu);
         return send_cts(w, src, h->tag, addr, cap); /* addr 0: the data comes as a message */
     }
+    if (h->magic == FRAME_PROG) {
+        uint64_t pl[2];
+        if (h->len != sizeof(pl))
+            return -EPROTO;
+        if ((rc = read_all(fd, pl, sizeof(pl))))
+            return rc;
+        pthread_mutex_lock(&w->mu);
+        void *row = NULL;
+        for (sk_req *r = w->filling; r && !row; r = r->next)
+            if (r->src == src && r->tag == h->tag)
+                row = r->buf;
+        pthread_mutex_unlock(&w->mu);
+        if (row) /* the receive stays in `filling` until DONE: row is alive */
+            bcpi_row_progress(row, (size_t)pl[0], (int)pl[1]);
+        return 0;
+    }
     if (h->magic == FRAME_DONE) {
         uint64_t n = 0;
         if (h->len != sizeof(n))
@@ -756,6 +773,28 @@ static int send_zeros(bcp_sock_world *w, size_t n, int dst, int tag)
     return rc;
 }
 
+/* Progress of a fill into an arena row (a P role folding the window range by
+ * range while it fills): the fill reports, between pieces, how many leading
+ * bytes of the row are final; each report is a PROG frame on the data socket,
+ * ahead of DONE, and the receiver hands it to bcpi_row_progress. */
+static __thread struct {
+    bcp_sock_world *w;
+    int dst, tag;
+} t_prog;
+
+int bcpi_fill_progress_on(void)
+{
+    return t_prog.w != NULL;
+}
+
+int bcpi_fill_progress(size_t bytes, int redo)
+{
+    if (!t_prog.w)
+        return -ENOTCONN;
+    const uint64_t pl[2] = {(uint64_t)bytes, (uint64_t)redo};
+    return send_frame(t_prog.w, t_prog.dst, FRAME_PROG, t_prog.tag, sizeof(pl), pl, sizeof(pl));
+}
+
 /* Fill send (rendezvous, see the top of the file): fill() writes the n-byte
  * payload straight into the receiver's arena row; a receive outside the
  * arena gets an ordinary message produced by fill() into a scratch buffer.
@@ -808,7 +847,11 @@ static int sk_send_fill(void *ctx, bcp_lb_fill_fn fill, void *fctx, size_t n, in
         return -EPROTO;
     }
     if (n <= cap) {
+        t_prog.w = w; /* progress reports go to the receiver while this fill runs */
+        t_prog.dst = dst;
+        t_prog.tag = tag;
         frc = fill(fctx, addr, n);
+        t_prog.w = NULL;
     } else {
         /* truncated receive (MPI_ERR_TRUNCATE): produce all, keep cap */
         uint8_t *tmp = calloc(1, n);

@@ -96,6 +96,7 @@ typedef struct {
     uint8_t *out;
     size_t step; /* smallest range folded before the window is complete */
     int n;
+    int remote, st, tag; /* ranges go to the node fold server (connection of lane `tag`) */
 } row_watch;
 
 #define WATCH_SLOTS 4096u
@@ -200,6 +201,14 @@ static void watch_publish(row_watch *w, int j, size_t bytes, int redo)
     w->redo |= redo;
     range_claim(w);
     pthread_mutex_unlock(&w->mu);
+}
+
+void bcpi_row_progress(const void *row, size_t bytes, int redo)
+{
+    int j = 0;
+    row_watch *W = watch_find(row, &j);
+    if (W)
+        watch_publish(W, j, bytes, redo);
 }
 
 int bcp_task_set_device_map(const int *devices, int ntargets)
@@ -622,12 +631,14 @@ void bcpi_foldsrv_attach(int nconn, const int *fds)
 
 /* The fold of one window by the node fold server (rows and out in the
  * arena); -ENXIO if they are not, so the caller folds elsewhere. */
-static int fold_remote(int st, const uint8_t *rows, size_t pitch, const size_t *valid, size_t nbytes, int n,
-                       uint8_t *out, int use_hook)
+#define FS_HOOK 1  /* the server folds with the test double it inherited (CPU tests; whole rows) */
+#define FS_RANGE 2 /* a range of a pipelined window: no reply; a failure is kept for FS_FINAL */
+#define FS_FINAL 4 /* the window's last request: its reply carries the ranges' first failure */
+
+static int fold_remote(int st, int tag, const uint8_t *rows, size_t pitch, const size_t *valid, size_t nbytes, int n,
+                       uint8_t *out, int flags)
 {
-    /* use_hook: the server folds with the test double it inherited (CPU
-     * tests of this path; the rows then hold whole zero-padded windows) */
-    fs_req q = {FS_MAGIC, n, st, use_hook, (uint64_t)(uintptr_t)rows, pitch, nbytes, (uint64_t)(uintptr_t)out,
+    fs_req q = {FS_MAGIC, n, st, flags, (uint64_t)(uintptr_t)rows, pitch, nbytes, (uint64_t)(uintptr_t)out,
                 0, 0, 0, 0};
     void *rb, *ob;
     size_t rs, os;
@@ -640,13 +651,16 @@ static int fold_remote(int st, const uint8_t *rows, size_t pitch, const size_t *
     uint64_t v[MAX_STORAGE_TARGETS];
     for (int j = 0; j < n; j++)
         v[j] = valid[j];
-    const int c = (t_lane_tag < 0 ? -t_lane_tag : t_lane_tag) % g_srv_n;
-    fs_rep r = {0, -EPROTO};
+    /* the lane's own connection: a pipelined window's ranges (sent by
+     * whichever thread reads a source's progress) and its final request go
+     * down the same one, and the server handles a connection in order */
+    const int c = (tag < 0 ? -tag : tag) % g_srv_n;
+    fs_rep r = {FS_MAGIC, 0};
     pthread_mutex_lock(&g_srv[c].mu);
     int rc = fs_io(g_srv[c].fd, &q, sizeof(q), 1);
     if (!rc)
         rc = fs_io(g_srv[c].fd, v, (size_t)n * sizeof(uint64_t), 1);
-    if (!rc)
+    if (!rc && !(flags & FS_RANGE))
         rc = fs_io(g_srv[c].fd, &r, sizeof(r), 0);
     pthread_mutex_unlock(&g_srv[c].mu);
     if (!rc && r.magic != FS_MAGIC)
@@ -700,6 +714,7 @@ static int fs_register(bcp_engine *e, uint64_t base, uint64_t size)
 static void *fs_conn_main(void *arg)
 {
     const int fd = (int)(intptr_t)arg;
+    int range_err = 0; /* first failed FS_RANGE fold since the last FS_FINAL */
     for (;;) {
         fs_req q;
         if (fs_io(fd, &q, sizeof(q), 0))
@@ -717,14 +732,15 @@ static void *fs_conn_main(void *arg)
         for (int j = 0; j < q.n && ok; j++) {
             valid[j] = (size_t)v[j];
             ok = v[j] <= q.pitch &&
-                 fs_block_ok(q.rows_base, q.rows_size, q.rows + (uint64_t)j * q.pitch, q.pad ? q.nbytes : v[j]);
+                 fs_block_ok(q.rows_base, q.rows_size, q.rows + (uint64_t)j * q.pitch,
+                             (q.pad & FS_HOOK) ? q.nbytes : v[j]);
         }
         bcp_engine *e = NULL;
         fold_svc *S = NULL;
         int dev = -1;
         bcp_xor_hook_fn hook = NULL;
         void *hctx = NULL;
-        if (q.pad) {
+        if (q.pad & FS_HOOK) {
             pthread_mutex_lock(&g_lock);
             hook = g_hook;
             hctx = g_hook_ctx;
@@ -732,7 +748,9 @@ static void *fs_conn_main(void *arg)
         }
         if (!ok)
             r.rc = -EFAULT;
-        else if (q.pad)
+        else if (q.nbytes == 0)
+            r.rc = 0; /* a final request with nothing left to fold */
+        else if (q.pad & FS_HOOK)
             r.rc = hook ? hook((uint8_t *)(uintptr_t)q.out, (size_t)q.nbytes, (const uint8_t *)(uintptr_t)q.rows,
                                (size_t)q.pitch, q.n, hctx)
                         : -ENOSYS;
@@ -740,6 +758,16 @@ static void *fs_conn_main(void *arg)
                  !(r.rc = fs_register(e, q.out_base, q.out_size)) && !(r.rc = svc_get(dev, e, &S)))
             r.rc = fold_batched(S, (const uint8_t *)(uintptr_t)q.rows, (size_t)q.pitch, valid, (size_t)q.nbytes,
                                 q.n, (uint8_t *)(uintptr_t)q.out);
+        if (q.pad & FS_RANGE) {
+            if (r.rc && !range_err)
+                range_err = r.rc;
+            continue; /* folded (synchronously, in order) -- no reply */
+        }
+        if (q.pad & FS_FINAL) {
+            if (!r.rc)
+                r.rc = range_err;
+            range_err = 0;
+        }
         if (fs_io(fd, &r, sizeof(r), 1))
             break;
     }
@@ -1017,7 +1045,7 @@ static int fold_window(fold_res *R, HostState *hs, int mode, bcp_xor_hook_fn hoo
     /* the node fold server folds (with a test double only if it has the
      * same one: it was forked when the pool was made) */
     if (R->device < 0 && g_srv_n > 0 && (!hook || hook == g_srv_hook) && bcpi_arena_block(rows, &ab, &az))
-        return fold_remote(hs->storage_target, rows, pitch, valid, nbytes, n, out, hook != NULL);
+        return fold_remote(hs->storage_target, t_lane_tag, rows, pitch, valid, nbytes, n, out, hook ? FS_HOOK : 0);
     if (hook) {
         static int warned = 0; /* lanes race here: atomic exchange */
         if (!__atomic_exchange_n(&warned, 1, __ATOMIC_RELAXED))
@@ -1126,6 +1154,12 @@ static int launch_range(const row_watch *w, size_t lo, size_t hi)
     __atomic_fetch_add(&g_pipe_ranges, 1, __ATOMIC_RELAXED);
     if (w->hook)
         return w->hook(w->out + lo, hi - lo, w->rows + lo, w->pitch, w->n, w->hook_ctx);
+    if (w->remote) { /* the node fold server folds the range; no reply (FS_RANGE) */
+        size_t v[MAX_STORAGE_TARGETS];
+        for (int j = 0; j < w->n; j++)
+            v[j] = w->valid[j] > lo ? MIN_(w->valid[j], hi) - lo : 0;
+        return fold_remote(w->st, w->tag, w->rows + lo, w->pitch, v, hi - lo, w->n, w->out + lo, FS_RANGE);
+    }
     bcp_stripe st = {(uint64_t)(uintptr_t)(w->out + lo), hi - lo, 0, (uint32_t)w->n, 0};
     bcp_source so[MAX_STORAGE_TARGETS];
     for (int j = 0; j < w->n; j++) {
@@ -1154,9 +1188,13 @@ static void range_claim(row_watch *w)
 }
 
 static int watch_rows(row_watch *W, fold_res *R, bcp_xor_hook_fn hook, void *hook_ctx, const uint8_t *rows,
-                      size_t pitch, const size_t *valid, int n, size_t nbytes, uint8_t *out)
+                      size_t pitch, const size_t *valid, int n, size_t nbytes, uint8_t *out, int remote, int st,
+                      int tag)
 {
     pthread_mutex_init(&W->mu, NULL);
+    W->remote = remote;
+    W->st = st;
+    W->tag = tag;
     memset(W->prog, 0, sizeof(W->prog));
     W->redo = W->err = 0;
     W->R = R;
@@ -1193,9 +1231,23 @@ static int finish_rows(row_watch *W, int fold)
     int rc = W->err;
     const size_t lo = W->redo ? 0 : W->lo;
     __atomic_fetch_add(&g_pipe_windows, 1, __ATOMIC_RELAXED);
-    if (fold && !rc && lo < W->nbytes)
-        rc = launch_range(W, lo, W->nbytes);
-    const int src = W->hook ? 0 : bcp_queue_sync(W->R->q);
+    int src = 0;
+    if (W->remote && !W->hook) {
+        /* the tail (or nothing) as the final request: answered once the
+         * server has folded every range sent before it on the connection */
+        size_t v[MAX_STORAGE_TARGETS];
+        const size_t a = fold && !rc ? lo : W->nbytes;
+        for (int j = 0; j < W->n; j++)
+            v[j] = W->valid[j] > a ? MIN_(W->valid[j], W->nbytes) - a : 0;
+        if (a < W->nbytes)
+            __atomic_fetch_add(&g_pipe_ranges, 1, __ATOMIC_RELAXED);
+        src = fold_remote(W->st, W->tag, W->rows + (a < W->nbytes ? a : 0), W->pitch, v, W->nbytes - a, W->n,
+                          W->out + (a < W->nbytes ? a : 0), FS_FINAL);
+    } else {
+        if (fold && !rc && lo < W->nbytes)
+            rc = launch_range(W, lo, W->nbytes);
+        src = W->hook ? 0 : bcp_queue_sync(W->R->q);
+    }
     pthread_mutex_destroy(&W->mu);
     return rc ? rc : src;
 }
@@ -1527,9 +1579,15 @@ static void parity_generator(const bcp_transport_ops *T, const char *path, const
     /* (the sources publish their progress through this process's watch
      * table and launch range folds on this lane's queue: in-process ranks,
      * i.e. the loopback transport, only) */
+    void *rb_;
+    size_t rz_;
+    /* rank processes: rows in the arena, folds by the node fold server; the
+     * sources report their progress over the sockets (PROG frames) */
+    const int xproc = !res_rc && L && L->device < 0 && g_srv_n > 0 && T->send_fill &&
+                      T->send_fill != bcp_lb_transport()->send_fill && bcpi_arena_block(L->h_win[0], &rb_, &rz_);
     int pipelined = mode == BCP_FOLD_PIPELINED && !res_rc && expected_messages == 1 && T->send_fill &&
-                    T->send_fill == bcp_lb_transport()->send_fill;
-    if (pipelined && !hook && !L->q && bcp_queue_create(L->eng, &L->q))
+                    (T->send_fill == bcp_lb_transport()->send_fill || xproc);
+    if (pipelined && !hook && !xproc && !L->q && bcp_queue_create(L->eng, &L->q))
         pipelined = 0;
     if (serial_io && !res_rc)
         open_parity_chunk(hs, path, final_size, open_parity, &P_fd, &opened, &have_had_error,
@@ -1566,7 +1624,8 @@ static void parity_generator(const bcp_transport_ops *T, const char *path, const
                     if (valid[j] < buffer_size)
                         memset(win_a + (size_t)j * pitch + valid[j], 0, buffer_size - valid[j]);
             watched = pipelined && !have_had_error &&
-                      watch_rows(&W, L, hook, hook_ctx, win_a, pitch, valid, n, buffer_size, pblk);
+                      watch_rows(&W, L, hook, hook_ctx, win_a, pitch, valid, n, buffer_size, pblk, xproc && !hook,
+                                 hs->storage_target, ti.tag);
             trc = post_recvs(T, req, n, win_a, pitch, buffer_size, ranks, ti.tag);
             open_parity_chunk(hs, path, final_size, open_parity, &P_fd, &opened, &have_had_error,
                               ti.is_rebuilding ? NULL : chunk_sizes, n);
@@ -1682,6 +1741,17 @@ static int fill_window(void *ctx, void *dst, size_t n)
     return 0;
 }
 
+/* Publish a final prefix of the row being filled: to a P role of this
+ * process (its row watch), or, through the socket transport, to a P role in
+ * another process (PROG frames, bcpi_fill_progress). */
+static void fill_publish(row_watch *W, int wj, int xp, size_t bytes, int redo)
+{
+    if (W)
+        watch_publish(W, wj, bytes, redo);
+    else if (xp)
+        (void)bcpi_fill_progress(bytes, redo); /* a lost report only delays the fold to the tail */
+}
+
 static void fill_bytes(window_fill *w, uint8_t *data, size_t n)
 {
     HostState *hs = w->hs;
@@ -1690,10 +1760,10 @@ static void fill_bytes(window_fill *w, uint8_t *data, size_t n)
     const size_t need = w->implicit_pad ? window_data_bytes(w->data_to_send, w->fd_size, w->data_sent, n) : n;
     int wj = 0;
     row_watch *W = watch_find(data, &wj); /* a P role folding this row as it fills */
+    const int xp = !W && bcpi_fill_progress_on(); /* ... in another rank process */
     if (w->err != 0 || w->data_sent >= w->fd_size) {
         memset(data, 0, need);
-        if (W)
-            watch_publish(W, wj, need, 0);
+        fill_publish(W, wj, xp, need, 0);
         return;
     }
     /* up to the size the chunk reported (not past it should the file have
@@ -1701,7 +1771,7 @@ static void fill_bytes(window_fill *w, uint8_t *data, size_t n)
     const uint64_t left = MIN_(w->data_to_send, w->fd_size) - w->data_sent;
     const size_t want = (size_t)MIN_((uint64_t)n, left);
     ssize_t r;
-    if (!W) {
+    if (!W && !xp) {
         r = bcpi_inject_hit(BCP_INJECT_READ) ? (errno = EIO, -1) : read(w->fd, data, want);
     } else {
         /* in pieces, publishing the final prefix after each (EOF ends it) */
@@ -1717,7 +1787,7 @@ static void fill_bytes(window_fill *w, uint8_t *data, size_t n)
             got += (size_t)k;
             r = (ssize_t)got;
             if (got < want)
-                watch_publish(W, wj, got, 0);
+                fill_publish(W, wj, xp, got, 0);
         }
     }
     if (r < 0) {
@@ -1725,14 +1795,12 @@ static void fill_bytes(window_fill *w, uint8_t *data, size_t n)
         memset(data, 0, need);
         LOGERR("read of '%s' failed with %d (%s) after %llu bytes\n", w->path, errno, strerror(errno),
                (unsigned long long)w->data_sent);
-        if (W)
-            watch_publish(W, wj, need, 1); /* the zeros replace bytes already published */
+        fill_publish(W, wj, xp, need, 1); /* the zeros replace bytes already published */
         return;
     }
     if ((size_t)r < need)
         memset(data + r, 0, need - (size_t)r);
-    if (W)
-        watch_publish(W, wj, MAX_(need, (size_t)r), 0);
+    fill_publish(W, wj, xp, MAX_(need, (size_t)r), 0);
 }
 
 static void chunk_sender(const bcp_transport_ops *T, const char *path, const FileInfo *task, TaskInfo ti,

@@ -68,8 +68,9 @@ def test_pipelined_gen_and_rebuild(bcp, oracle, tmp_path, explicit):
 
 @pytest.mark.timeout(300)
 def test_pipelined_falls_back_where_it_cannot_follow(bcp, oracle, tmp_path):
-    """Multi-window stripes (replay) and socket-transport rank processes fold
-    whole windows like ZERO_COPY; the parity is the same."""
+    """Multi-window stripes (replay) fold whole windows like BATCHED; rank
+    processes (socket transport, node fold server) follow single windows
+    through the sources' PROG frames; the parity is the same."""
     root = str(tmp_path)
     files = [("w/a", [0, 1], 2, [10 * MiB, 25 * MiB + 5]), ("w/b", [0, 2], 1, [300 * KiB, 7])]
     items, contents = S.populate(root, 3, files, seed=5)
@@ -97,22 +98,25 @@ def test_pipelined_folds_ranges_while_a_row_is_read(bcp, oracle, tmp_path):
 
 
 @pytest.mark.timeout(120)
-def test_pipelined_read_error_refolds_the_window(bcp, oracle, tmp_path):
+@pytest.mark.parametrize("procs", [False, True], ids=["threads", "rank-processes"])
+def test_pipelined_read_error_refolds_the_window(bcp, oracle, tmp_path, procs):
     """A 4 MiB source (read in 16 pieces) fails its twelfth piece after the
     ranges it published were folded, beside two small rows complete before
     it.  Its row becomes zeros (the reference zero-fills a
     window whose read failed) although its prefix was already folded: the P
     role refolds the whole window, the parity holds the XOR of the other
-    rows, the source's rank is in error."""
+    rows, the source's rank is in error.  Rank processes: the source in
+    another process reports the refold through a PROG frame (redo)."""
     root = str(tmp_path)
     lens = [7, 100 * KiB, 4 * MiB + 3]
     items, contents = S.populate(root, 4, [("e/x", [0, 1, 2], 3, lens)], seed=6)
-    bcp.inject_failure(bcp.INJECT_READ, 10, 1)  # pieces 2..11 pass, the 12th fails
+    bcp.inject_failure(bcp.INJECT_READ, 10, 1)  # pieces 2..11 pass, the 12th fails (ranks inherit it)
     w0, r0 = bcp.pipe_stats()
-    st = bcp.gen_run(root, 4, items, nlanes=1)
+    st = (bcp.gen_run_procs if procs else bcp.gen_run)(root, 4, items, nlanes=1)
     w1, r1 = bcp.pipe_stats()
     assert st.errors == 1
-    assert w1 - w0 == 1 and r1 - r0 >= 1
+    if not procs:  # (the ranks' own counters are in the ranks)
+        assert w1 - w0 == 1 and r1 - r0 >= 1
     pf = S.read_file(S.parity_path(root, 3, "e/x"))
     assert np.frombuffer(pf[:24], "<u8").tolist() == lens  # the sizes were sent before the read
     body = np.frombuffer(pf[24:], np.uint8)

@@ -363,8 +363,10 @@ def test_rank_processes_fill_into_shared_rows(bcp, oracle, cpu_hook, tmp_path, m
         assert arena == 0 and msg == 0 and srv == 0
     else:
         assert arena >= sum(len(h) for (_, h, _, _) in files[:-1]) and msg == 0
-        # one fold per window of every stripe with a source (the 21 MiB one has 3)
-        assert srv == (len([f for f in files if f[1]]) + 2 if server == "1" else 0)
+        # with the server: single-window stripes fold range by range as the
+        # sources report progress (PROG frames; here the test double folds the
+        # ranges in the P role), the 21 MiB stripe's 3 windows go to the server
+        assert srv == (3 if server == "1" else 0)
     victim = 2
     lost = {}
     for (path, holders, p, lens) in files:
@@ -391,7 +393,11 @@ def test_fold_server_losing_a_connection_fails_tasks_not_the_run(bcp, oracle, cp
     files = _random_files(rng, ntargets, 30, 300_000)
     items, contents = S.populate(root, ntargets, files, seed=4)
     bcp.inject_failure(bcp.INJECT_FOLD_SERVER, 3, 1)
-    st = bcp.gen_run_procs(root, ntargets, items, nlanes=3)
+    prev = bcp.set_fold_mode(bcp.FOLD_BATCHED)  # every window through the server
+    try:
+        st = bcp.gen_run_procs(root, ntargets, items, nlanes=3)
+    finally:
+        bcp.set_fold_mode(prev)
     assert st.errors > 0
     bcp.inject_failure(bcp.INJECT_FOLD_SERVER, 0, 0)
     st = bcp.gen_run_procs(root, ntargets, items, nlanes=3)
