@@ -59,3 +59,5 @@ int bcpi_fill_progress(size_t bytes, int redo);
 /* The receiving side: `bytes` leading bytes of the receive row `row` are
  * final (redo: bytes published before were replaced) -- bcp_task.c. */
 void bcpi_row_progress(const void *row, size_t bytes, int redo);
+/* 1 if a P role of this process follows the fill of row `row` (its watch). */
+int bcpi_row_watched(const void *row);

@@ -54,6 +54,7 @@
 #define FRAME_CTS 0x62637063u   /* "bcpc": {address, capacity} of the matched receive */
 #define FRAME_DONE 0x62637064u  /* "bcpd": {bytes} filled; completes the receive */
 #define FRAME_PROG 0x62637067u  /* "bcpg": {bytes, redo} of the fill are final (pipelined fold) */
+#define CTS_PROGRESS (UINT64_C(1) << 63) /* in the CTS capacity: the receiver follows the fill (PROG) */
 
 typedef struct {
     uint32_t magic;
@@ -502,7 +503,8 @@ static int send_cts(bcp_sock_world *w, int src, int tag, const void *addr, size_
     struct {
         frame_hdr h;
         uint64_t pl[2];
-    } f = {{FRAME_CTS, tag, 2 * sizeof(uint64_t)}, {(uint64_t)(uintptr_t)addr, (uint64_t)cap}};
+    } f = {{FRAME_CTS, tag, 2 * sizeof(uint64_t)},
+           {(uint64_t)(uintptr_t)addr, (uint64_t)cap | (addr && bcpi_row_watched(addr) ? CTS_PROGRESS : 0)}};
     pthread_mutex_lock(&w->ctl_mu[src]);
     int rc = write_all(fd, &f, sizeof(f));
     pthread_mutex_unlock(&w->ctl_mu[src]);
@@ -823,7 +825,8 @@ static int sk_send_fill(void *ctx, bcp_lb_fill_fn fill, void *fctx, size_t n, in
     }
     rc = progress_until(w, r);
     uint8_t *addr = (uint8_t *)(uintptr_t)r->cts_addr;
-    const size_t cap = (size_t)r->cts_cap;
+    const int want_progress = (r->cts_cap & CTS_PROGRESS) != 0;
+    const size_t cap = (size_t)(r->cts_cap & ~CTS_PROGRESS);
     free(r);
     if (rc)
         return rc;
@@ -847,7 +850,7 @@ static int sk_send_fill(void *ctx, bcp_lb_fill_fn fill, void *fctx, size_t n, in
         return -EPROTO;
     }
     if (n <= cap) {
-        t_prog.w = w; /* progress reports go to the receiver while this fill runs */
+        t_prog.w = want_progress ? w : NULL; /* progress reports go to a receiver that follows the fill */
         t_prog.dst = dst;
         t_prog.tag = tag;
         frc = fill(fctx, addr, n);

@@ -203,6 +203,12 @@ static void watch_publish(row_watch *w, int j, size_t bytes, int redo)
     pthread_mutex_unlock(&w->mu);
 }
 
+int bcpi_row_watched(const void *row)
+{
+    int j = 0;
+    return watch_find(row, &j) != NULL;
+}
+
 void bcpi_row_progress(const void *row, size_t bytes, int redo)
 {
     int j = 0;
@@ -1582,8 +1588,12 @@ static void parity_generator(const bcp_transport_ops *T, const char *path, const
     void *rb_;
     size_t rz_;
     /* rank processes: rows in the arena, folds by the node fold server; the
-     * sources report their progress over the sockets (PROG frames) */
-    const int xproc = !res_rc && L && L->device < 0 && g_srv_n > 0 && T->send_fill &&
+     * sources report their progress over the sockets (PROG frames).  Opt-in
+     * (environment BCP_XPROC_PIPELINE=1): measured no faster than whole
+     * windows through the server on config 1 / 5 and slower on the one-lane
+     * rebuild (r2d0), so PIPELINED ranks fold their windows BATCHED */
+    const char *xpe = getenv("BCP_XPROC_PIPELINE"); /* read per task: ranks fork from callers that read it */
+    const int xproc = xpe && atoi(xpe) > 0 && !res_rc && L && L->device < 0 && g_srv_n > 0 && T->send_fill &&
                       T->send_fill != bcp_lb_transport()->send_fill && bcpi_arena_block(L->h_win[0], &rb_, &rz_);
     int pipelined = mode == BCP_FOLD_PIPELINED && !res_rc && expected_messages == 1 && T->send_fill &&
                     (T->send_fill == bcp_lb_transport()->send_fill || xproc);

@@ -69,8 +69,8 @@ def test_pipelined_gen_and_rebuild(bcp, oracle, tmp_path, explicit):
 @pytest.mark.timeout(300)
 def test_pipelined_falls_back_where_it_cannot_follow(bcp, oracle, tmp_path):
     """Multi-window stripes (replay) fold whole windows like BATCHED; rank
-    processes (socket transport, node fold server) follow single windows
-    through the sources' PROG frames; the parity is the same."""
+    processes (socket transport, node fold server) fold whole windows
+    through the server unless BCP_XPROC_PIPELINE=1; the parity is the same."""
     root = str(tmp_path)
     files = [("w/a", [0, 1], 2, [10 * MiB, 25 * MiB + 5]), ("w/b", [0, 2], 1, [300 * KiB, 7])]
     items, contents = S.populate(root, 3, files, seed=5)
@@ -99,7 +99,7 @@ def test_pipelined_folds_ranges_while_a_row_is_read(bcp, oracle, tmp_path):
 
 @pytest.mark.timeout(120)
 @pytest.mark.parametrize("procs", [False, True], ids=["threads", "rank-processes"])
-def test_pipelined_read_error_refolds_the_window(bcp, oracle, tmp_path, procs):
+def test_pipelined_read_error_refolds_the_window(bcp, oracle, tmp_path, procs, monkeypatch):
     """A 4 MiB source (read in 16 pieces) fails its twelfth piece after the
     ranges it published were folded, beside two small rows complete before
     it.  Its row becomes zeros (the reference zero-fills a
@@ -107,6 +107,7 @@ def test_pipelined_read_error_refolds_the_window(bcp, oracle, tmp_path, procs):
     role refolds the whole window, the parity holds the XOR of the other
     rows, the source's rank is in error.  Rank processes: the source in
     another process reports the refold through a PROG frame (redo)."""
+    monkeypatch.setenv("BCP_XPROC_PIPELINE", "1")  # rank processes: the opt-in pipelined form
     root = str(tmp_path)
     lens = [7, 100 * KiB, 4 * MiB + 3]
     items, contents = S.populate(root, 4, [("e/x", [0, 1, 2], 3, lens)], seed=6)

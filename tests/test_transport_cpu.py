@@ -363,10 +363,10 @@ def test_rank_processes_fill_into_shared_rows(bcp, oracle, cpu_hook, tmp_path, m
         assert arena == 0 and msg == 0 and srv == 0
     else:
         assert arena >= sum(len(h) for (_, h, _, _) in files[:-1]) and msg == 0
-        # with the server: single-window stripes fold range by range as the
-        # sources report progress (PROG frames; here the test double folds the
-        # ranges in the P role), the 21 MiB stripe's 3 windows go to the server
-        assert srv == (3 if server == "1" else 0)
+        # with the server every window goes to it (the pipelined form across
+        # processes is opt-in, BCP_XPROC_PIPELINE): one per window of every
+        # stripe with a source (the 21 MiB one has 3)
+        assert srv == (len([f for f in files if f[1]]) + 2 if server == "1" else 0)
     victim = 2
     lost = {}
     for (path, holders, p, lens) in files:
