@@ -124,6 +124,9 @@ _SIGS = {
     "bcp_task_inject_failure": ([ctypes.c_int, ctypes.c_int, ctypes.c_int], ctypes.c_int),
     "bcp_task_phase_stats": ([ctypes.POINTER(ctypes.c_double), ctypes.c_int, ctypes.c_int], ctypes.c_int),
     "bcp_task_set_transport": ([_V], ctypes.c_int),
+    "bcp_fold_server_serve": ([ctypes.c_char_p, ctypes.c_int], ctypes.c_int),
+    "bcp_fold_server_connect": ([ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int], ctypes.c_int),
+    "bcp_fold_server_stats": ([ctypes.POINTER(ctypes.c_uint64)], ctypes.c_int),
     "bcp_lb_transport": ([], _V),
     "bcp_gen_run_procs": ([ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(WorkItem), ctypes.c_size_t, ctypes.c_int,
                            ctypes.POINTER(ctypes.c_int), _V, ctypes.POINTER(RunStats)], ctypes.c_int),
@@ -685,6 +688,23 @@ def set_fold_mode(mode: int) -> int:
     if rc < 0:
         raise BcpError("bcp_task_set_fold_mode", rc)
     return rc
+
+
+def fold_server_serve(socket_path: str, max_conns: int = 0) -> None:
+    """Run a node fold server on a Unix socket (blocks; 0 = forever)."""
+    call("bcp_fold_server_serve", socket_path.encode(), max_conns)
+
+
+def fold_server_connect(socket_path: str, arena_bytes: int = 1 << 30, nconn: int = 12) -> None:
+    """This process's P roles fold through the node fold server at socket_path."""
+    call("bcp_fold_server_connect", socket_path.encode(), arena_bytes, nconn)
+
+
+def fold_server_stats() -> int:
+    """Windows the node fold server folded for this process."""
+    w = ctypes.c_uint64(0)
+    call("bcp_fold_server_stats", ctypes.byref(w))
+    return w.value
 
 
 def pipe_stats() -> tuple:

@@ -61,3 +61,6 @@ int bcpi_fill_progress(size_t bytes, int redo);
 void bcpi_row_progress(const void *row, size_t bytes, int redo);
 /* 1 if a P role of this process follows the fill of row `row` (its watch). */
 int bcpi_row_watched(const void *row);
+/* Make [base, base + bytes) this process's arena slice (a memfd shared with
+ * a node fold server, bcp_fold_server_connect). */
+void bcpi_arena_set(void *base, size_t bytes);

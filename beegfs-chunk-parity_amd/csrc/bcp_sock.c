@@ -154,6 +154,18 @@ int bcpi_arena_free(void *p)
     return found;
 }
 
+void bcpi_arena_set(void *base, size_t bytes)
+{
+    pthread_mutex_lock(&g_arena_mu);
+    g_arena_lo = base;
+    g_arena_hi = (uint8_t *)base + bytes;
+    g_slice = base;
+    g_slice_bytes = bytes;
+    g_slice_used = 0;
+    g_nblocks = 0;
+    pthread_mutex_unlock(&g_arena_mu);
+}
+
 int bcpi_arena_block(const void *p, void **base, size_t *size)
 {
     const uint8_t *b = p;

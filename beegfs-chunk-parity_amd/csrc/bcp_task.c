@@ -31,7 +31,9 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/mman.h>
 #include <sys/socket.h>
+#include <sys/un.h>
 #include <sys/stat.h>
 #include <sys/types.h>
 #include <time.h>
@@ -620,6 +622,14 @@ uint64_t bcpi_foldsrv_folds(void)
     return __atomic_load_n(&g_remote_folds, __ATOMIC_RELAXED);
 }
 
+int bcp_fold_server_stats(uint64_t *windows)
+{
+    if (!windows)
+        return -EINVAL;
+    *windows = bcpi_foldsrv_folds();
+    return 0;
+}
+
 static bcp_xor_hook_fn g_srv_hook; /* the test double the server inherited */
 
 void bcpi_foldsrv_attach(int nconn, const int *fds)
@@ -678,7 +688,6 @@ static int fold_remote(int st, int tag, const uint8_t *rows, size_t pitch, const
 
 /* server side */
 static struct {
-    uint8_t *lo, *hi;
     pthread_mutex_t mu;
     struct {
         uint8_t *p;
@@ -687,15 +696,34 @@ static struct {
     int nreg;
 } g_fs = {.mu = PTHREAD_MUTEX_INITIALIZER};
 
-static int fs_block_ok(uint64_t base, uint64_t size, uint64_t p, uint64_t len)
+/* A client's arena as this server sees it: the rank pool's is mapped at
+ * the same address in every process (delta 0); a connected client's memfd
+ * (bcp_fold_server_connect) is mapped here at base, its own at client_base. */
+typedef struct fs_map {
+    struct fs_map *next;
+    uint64_t token, client_base;
+    uint8_t *base;
+    size_t size;
+    int refs;
+} fs_map;
+static fs_map *g_fs_maps; /* under g_fs.mu */
+
+typedef struct {
+    int fd;
+    uint64_t lo, hi; /* client addresses a request may name */
+    int64_t delta;   /* server address = client address + delta */
+    fs_map *map;     /* NULL: the rank pool's inherited arena */
+} fs_conn;
+
+static int fs_block_ok(const fs_conn *c, uint64_t base, uint64_t size, uint64_t p, uint64_t len)
 {
-    const uint64_t lo = (uint64_t)(uintptr_t)g_fs.lo, hi = (uint64_t)(uintptr_t)g_fs.hi;
-    return size > 0 && base >= lo && base <= hi && size <= hi - base && p >= base && p <= base + size &&
+    return size > 0 && base >= c->lo && base <= c->hi && size <= c->hi - base && p >= base && p <= base + size &&
            len <= base + size - p;
 }
 
 /* Register an arena block with the device once (blocks are reused at the
- * same place and size, so a registration stays valid for the process). */
+ * same place and size, so a registration stays valid while its mapping
+ * lives). */
 static int fs_register(bcp_engine *e, uint64_t base, uint64_t size)
 {
     int rc = 0;
@@ -717,9 +745,42 @@ static int fs_register(bcp_engine *e, uint64_t base, uint64_t size)
     return rc;
 }
 
-static void *fs_conn_main(void *arg)
+/* The last connection of a client is gone: unregister its blocks, unmap. */
+static void fs_map_put(fs_map *m)
 {
-    const int fd = (int)(intptr_t)arg;
+    if (!m)
+        return;
+    pthread_mutex_lock(&g_fs.mu);
+    if (--m->refs > 0) {
+        pthread_mutex_unlock(&g_fs.mu);
+        return;
+    }
+    for (fs_map **pp = &g_fs_maps; *pp; pp = &(*pp)->next)
+        if (*pp == m) {
+            *pp = m->next;
+            break;
+        }
+    for (int i = 0; i < g_fs.nreg;)
+        if (g_fs.reg[i].p >= m->base && g_fs.reg[i].p < m->base + m->size) {
+            bcp_engine *e = NULL;
+            pthread_mutex_lock(&g_lock);
+            for (int d = 0; d < MAX_DEVICES && !e; d++)
+                e = g_engines[d];
+            pthread_mutex_unlock(&g_lock);
+            if (e)
+                (void)bcp_host_unregister(e, g_fs.reg[i].p);
+            g_fs.reg[i] = g_fs.reg[--g_fs.nreg];
+        } else {
+            i++;
+        }
+    pthread_mutex_unlock(&g_fs.mu);
+    munmap(m->base, m->size);
+    free(m);
+}
+
+static void fs_serve_conn(fs_conn *c)
+{
+    const int fd = c->fd;
     int range_err = 0; /* first failed FS_RANGE fold since the last FS_FINAL */
     for (;;) {
         fs_req q;
@@ -734,13 +795,17 @@ static void *fs_conn_main(void *arg)
             break;
         if (bcpi_inject_hit(BCP_INJECT_FOLD_SERVER))
             break; /* (failure injection) the rank's fold sees EPIPE */
-        int ok = fs_block_ok(q.out_base, q.out_size, q.out, q.nbytes) && q.pitch > 0 && q.nbytes <= q.pitch;
+        int ok = fs_block_ok(c, q.out_base, q.out_size, q.out, q.nbytes) && q.pitch > 0 && q.nbytes <= q.pitch;
         for (int j = 0; j < q.n && ok; j++) {
             valid[j] = (size_t)v[j];
-            ok = v[j] <= q.pitch &&
-                 fs_block_ok(q.rows_base, q.rows_size, q.rows + (uint64_t)j * q.pitch,
-                             (q.pad & FS_HOOK) ? q.nbytes : v[j]);
+            ok = v[j] <= q.pitch && fs_block_ok(c, q.rows_base, q.rows_size, q.rows + (uint64_t)j * q.pitch,
+                                                (q.pad & FS_HOOK) ? q.nbytes : v[j]);
         }
+        /* client addresses -> this process's */
+        q.rows += (uint64_t)c->delta;
+        q.out += (uint64_t)c->delta;
+        q.rows_base += (uint64_t)c->delta;
+        q.out_base += (uint64_t)c->delta;
         bcp_engine *e = NULL;
         fold_svc *S = NULL;
         int dev = -1;
@@ -778,28 +843,229 @@ static void *fs_conn_main(void *arg)
             break;
     }
     close(fd);
+}
+
+static void *fs_conn_main(void *arg)
+{
+    fs_conn *c = arg;
+    fs_serve_conn(c);
+    free(c);
     return NULL;
 }
 
 int bcpi_foldsrv_main(int nconn, const int *fds, void *arena_lo, void *arena_hi)
 {
-    g_fs.lo = arena_lo;
-    g_fs.hi = arena_hi;
     /* batches in flight at once (the fold service's width; every rank's
      * windows share it): environment BCP_FOLD_SERVER_INFLIGHT */
     if (getenv("BCP_FOLD_SERVER_INFLIGHT"))
         (void)bcp_task_set_fold_inflight(atoi(getenv("BCP_FOLD_SERVER_INFLIGHT")));
     pthread_t th[FS_MAX_CONN * MAX_STORAGE_TARGETS];
     int started = 0;
-    for (int i = 0; i < nconn && i < (int)(sizeof(th) / sizeof(th[0])); i++)
-        if (pthread_create(&th[started], NULL, fs_conn_main, (void *)(intptr_t)fds[i]) == 0)
+    for (int i = 0; i < nconn && i < (int)(sizeof(th) / sizeof(th[0])); i++) {
+        fs_conn *c = calloc(1, sizeof(*c));
+        if (c) {
+            c->fd = fds[i];
+            c->lo = (uint64_t)(uintptr_t)arena_lo;
+            c->hi = (uint64_t)(uintptr_t)arena_hi;
+        }
+        if (c && pthread_create(&th[started], NULL, fs_conn_main, c) == 0) {
             started++;
-        else
+        } else {
+            free(c);
             close(fds[i]); /* the rank's lanes on it see EPIPE */
+        }
+    }
     for (int i = 0; i < started; i++)
         pthread_join(th[i], NULL);
     /* registrations end with the process; the fold service and engines go */
     return bcp_task_shutdown();
+}
+
+/* ---- the node fold server for independent processes (an MPI job) -------
+ * bcp_fold_server_serve: a node's fold server on a Unix socket; a rank
+ * (bcp_fold_server_connect) sends, on each of its connections, a hello
+ * {magic, token, arena address, size} with its arena's memfd (SCM_RIGHTS);
+ * the server maps each client's arena once and translates its addresses. */
+#define FS_HELLO 0x62636668u /* "bcfh" */
+typedef struct {
+    uint32_t magic, pad;
+    uint64_t token, base, size;
+} fs_hello;
+
+static int fs_recv_hello(int fd, fs_hello *h, int *memfd)
+{
+    char cbuf[CMSG_SPACE(sizeof(int))];
+    struct iovec iov = {h, sizeof(*h)};
+    struct msghdr mh = {0};
+    mh.msg_iov = &iov;
+    mh.msg_iovlen = 1;
+    mh.msg_control = cbuf;
+    mh.msg_controllen = sizeof(cbuf);
+    *memfd = -1;
+    ssize_t r;
+    while ((r = recvmsg(fd, &mh, MSG_CMSG_CLOEXEC)) < 0 && errno == EINTR)
+        ;
+    if (r != (ssize_t)sizeof(*h) || h->magic != FS_HELLO)
+        return -EPROTO;
+    for (struct cmsghdr *cm = CMSG_FIRSTHDR(&mh); cm; cm = CMSG_NXTHDR(&mh, cm))
+        if (cm->cmsg_level == SOL_SOCKET && cm->cmsg_type == SCM_RIGHTS)
+            memcpy(memfd, CMSG_DATA(cm), sizeof(int));
+    return *memfd >= 0 ? 0 : -EPROTO;
+}
+
+static void *fs_accepted_main(void *arg)
+{
+    fs_conn *c = arg;
+    fs_hello h;
+    int memfd = -1;
+    fs_map *m = NULL;
+    if (!fs_recv_hello(c->fd, &h, &memfd) && h.size > 0) {
+        pthread_mutex_lock(&g_fs.mu);
+        for (m = g_fs_maps; m && m->token != h.token; m = m->next)
+            ;
+        if (!m && (m = calloc(1, sizeof(*m)))) {
+            void *b = mmap(NULL, (size_t)h.size, PROT_READ | PROT_WRITE, MAP_SHARED, memfd, 0);
+            if (b == MAP_FAILED) {
+                free(m);
+                m = NULL;
+            } else {
+                m->token = h.token;
+                m->client_base = h.base;
+                m->base = b;
+                m->size = (size_t)h.size;
+                m->next = g_fs_maps;
+                g_fs_maps = m;
+            }
+        }
+        if (m)
+            m->refs++;
+        pthread_mutex_unlock(&g_fs.mu);
+    }
+    if (memfd >= 0)
+        close(memfd);
+    if (m) {
+        c->map = m;
+        c->lo = m->client_base;
+        c->hi = m->client_base + m->size;
+        c->delta = (int64_t)((uint64_t)(uintptr_t)m->base - m->client_base);
+        fs_serve_conn(c);
+        fs_map_put(m);
+    } else {
+        close(c->fd);
+    }
+    free(c);
+    return NULL;
+}
+
+int bcp_fold_server_serve(const char *socket_path, int max_conns)
+{
+    if (!socket_path || strlen(socket_path) >= sizeof(((struct sockaddr_un *)0)->sun_path) || max_conns < 0)
+        return -EINVAL;
+    if (getenv("BCP_FOLD_SERVER_INFLIGHT"))
+        (void)bcp_task_set_fold_inflight(atoi(getenv("BCP_FOLD_SERVER_INFLIGHT")));
+    const int ls = socket(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC, 0);
+    if (ls < 0)
+        return -errno;
+    struct sockaddr_un a = {0};
+    a.sun_family = AF_UNIX;
+    strcpy(a.sun_path, socket_path);
+    unlink(socket_path);
+    if (bind(ls, (struct sockaddr *)&a, sizeof(a)) != 0 || listen(ls, 256) != 0) {
+        const int e = -errno;
+        close(ls);
+        return e;
+    }
+    pthread_t *th = calloc(max_conns ? (size_t)max_conns : 1, sizeof(pthread_t));
+    int n = 0, rc = th ? 0 : -ENOMEM;
+    while (!rc && (max_conns == 0 || n < max_conns)) {
+        const int fd = accept4(ls, NULL, NULL, SOCK_CLOEXEC);
+        if (fd < 0) {
+            if (errno == EINTR)
+                continue;
+            rc = -errno;
+            break;
+        }
+        fs_conn *c = calloc(1, sizeof(*c));
+        pthread_t t;
+        if (!c || pthread_create(max_conns ? &th[n] : &t, NULL, fs_accepted_main, c ? (c->fd = fd, c) : NULL) != 0) {
+            free(c);
+            close(fd);
+            continue;
+        }
+        if (!max_conns)
+            pthread_detach(t);
+        n++;
+    }
+    close(ls);
+    unlink(socket_path);
+    for (int i = 0; max_conns && i < n; i++) /* (serving forever: never here) */
+        pthread_join(th[i], NULL);
+    free(th);
+    const int src = bcp_task_shutdown();
+    return rc ? rc : src;
+}
+
+int bcp_fold_server_connect(const char *socket_path, size_t arena_bytes, int nconn)
+{
+    if (!socket_path || strlen(socket_path) >= sizeof(((struct sockaddr_un *)0)->sun_path) || nconn < 1 ||
+        nconn > FS_MAX_CONN || arena_bytes < ((size_t)2 << 20) || g_srv_n > 0)
+        return -EINVAL;
+    arena_bytes = arena_bytes / ((size_t)2 << 20) * ((size_t)2 << 20);
+    const int mfd = memfd_create("bcp-fold-rows", MFD_CLOEXEC);
+    if (mfd < 0)
+        return -errno;
+    int rc = ftruncate(mfd, (off_t)arena_bytes) ? -errno : 0;
+    void *base = rc ? MAP_FAILED : mmap(NULL, arena_bytes, PROT_READ | PROT_WRITE, MAP_SHARED, mfd, 0);
+    if (!rc && base == MAP_FAILED)
+        rc = -errno;
+    int fds[FS_MAX_CONN];
+    int made = 0;
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    const fs_hello h = {FS_HELLO, 0, ((uint64_t)getpid() << 32) ^ (uint64_t)ts.tv_nsec,
+                        (uint64_t)(uintptr_t)base, arena_bytes};
+    for (; !rc && made < nconn; made++) {
+        const int fd = socket(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC, 0);
+        struct sockaddr_un a = {0};
+        a.sun_family = AF_UNIX;
+        strcpy(a.sun_path, socket_path);
+        if (fd < 0 || connect(fd, (struct sockaddr *)&a, sizeof(a)) != 0) {
+            rc = -errno;
+            if (fd >= 0)
+                close(fd);
+            break;
+        }
+        char cbuf[CMSG_SPACE(sizeof(int))];
+        memset(cbuf, 0, sizeof(cbuf));
+        struct iovec iov = {(void *)&h, sizeof(h)};
+        struct msghdr mh = {0};
+        mh.msg_iov = &iov;
+        mh.msg_iovlen = 1;
+        mh.msg_control = cbuf;
+        mh.msg_controllen = sizeof(cbuf);
+        struct cmsghdr *cm = CMSG_FIRSTHDR(&mh);
+        cm->cmsg_level = SOL_SOCKET;
+        cm->cmsg_type = SCM_RIGHTS;
+        cm->cmsg_len = CMSG_LEN(sizeof(int));
+        memcpy(CMSG_DATA(cm), &mfd, sizeof(int));
+        if (sendmsg(fd, &mh, MSG_NOSIGNAL) != (ssize_t)sizeof(h)) {
+            rc = -errno;
+            close(fd);
+            break;
+        }
+        fds[made] = fd;
+    }
+    close(mfd); /* the mapping and the server's copies keep the memory */
+    if (rc) {
+        for (int i = 0; i < made; i++)
+            close(fds[i]);
+        if (base != MAP_FAILED)
+            munmap(base, arena_bytes);
+        return rc;
+    }
+    bcpi_arena_set(base, arena_bytes); /* this process's P-role rows and outputs come from it */
+    bcpi_foldsrv_attach(made, fds); /* (a test double set now is asked of the server too: FS_HOOK) */
+    return 0;
 }
 
 /* ---- fold resources: a shared pool, reused across tasks, lanes and runs --
@@ -1595,9 +1861,11 @@ static void parity_generator(const bcp_transport_ops *T, const char *path, const
     const char *xpe = getenv("BCP_XPROC_PIPELINE"); /* read per task: ranks fork from callers that read it */
     const int xproc = xpe && atoi(xpe) > 0 && !res_rc && L && L->device < 0 && g_srv_n > 0 && T->send_fill &&
                       T->send_fill != bcp_lb_transport()->send_fill && bcpi_arena_block(L->h_win[0], &rb_, &rz_);
+    /* folds go to a node fold server (rows in its arena): ranges too */
+    const int remote_fold = !res_rc && L && L->device < 0 && g_srv_n > 0 && bcpi_arena_block(L->h_win[0], &rb_, &rz_);
     int pipelined = mode == BCP_FOLD_PIPELINED && !res_rc && expected_messages == 1 && T->send_fill &&
                     (T->send_fill == bcp_lb_transport()->send_fill || xproc);
-    if (pipelined && !hook && !xproc && !L->q && bcp_queue_create(L->eng, &L->q))
+    if (pipelined && !hook && !remote_fold && !L->q && bcp_queue_create(L->eng, &L->q))
         pipelined = 0;
     if (serial_io && !res_rc)
         open_parity_chunk(hs, path, final_size, open_parity, &P_fd, &opened, &have_had_error,
@@ -1634,8 +1902,8 @@ static void parity_generator(const bcp_transport_ops *T, const char *path, const
                     if (valid[j] < buffer_size)
                         memset(win_a + (size_t)j * pitch + valid[j], 0, buffer_size - valid[j]);
             watched = pipelined && !have_had_error &&
-                      watch_rows(&W, L, hook, hook_ctx, win_a, pitch, valid, n, buffer_size, pblk, xproc && !hook,
-                                 hs->storage_target, ti.tag);
+                      watch_rows(&W, L, hook, hook_ctx, win_a, pitch, valid, n, buffer_size, pblk,
+                                 remote_fold && !hook, hs->storage_target, ti.tag);
             trc = post_recvs(T, req, n, win_a, pitch, buffer_size, ranks, ti.tag);
             open_parity_chunk(hs, path, final_size, open_parity, &P_fd, &opened, &have_had_error,
                               ti.is_rebuilding ? NULL : chunk_sizes, n);

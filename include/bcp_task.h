@@ -277,6 +277,21 @@ int bcp_lb_waitall(int n, bcp_lb_req **reqs);
  * fill returns 0 or a negative errno, which bcp_lb_send_fill returns. */
 int bcp_lb_send_fill(bcp_lb_fill_fn fill, void *ctx, size_t n, int dst, int tag);
 
+/* ---- node fold server for independent rank processes (an MPI job) ------
+ * One process per node serves folds for every rank on a Unix socket
+ * (bcp_fold_server_serve; it is the only process with a HIP runtime; serves
+ * max_conns connections then returns, 0 = forever).  A rank calls
+ * bcp_fold_server_connect once, before its tasks: its P-role window rows
+ * and outputs then come from an arena of arena_bytes in a memfd it shares
+ * with the server (SCM_RIGHTS), and its folds go to the server over nconn
+ * connections (lane tag modulo nconn), batched with every other rank's.
+ * Receives into the rows are the caller's (MPI_Irecv, the loopback or socket
+ * transports).  The rank pool does the same by itself (bcp_rank_pool_*). */
+int bcp_fold_server_serve(const char *socket_path, int max_conns);
+int bcp_fold_server_connect(const char *socket_path, size_t arena_bytes, int nconn);
+/* Windows the node fold server folded for this process so far. */
+int bcp_fold_server_stats(uint64_t *windows);
+
 /* ---- callers: generation lanes and rebuild (loopback drivers) ---------- */
 typedef struct {
     const char *path;   /* chunk path relative to <store>/chunks and /parity */

@@ -522,3 +522,36 @@ def test_pipeline_rebuild_matches_protocol_rebuild(bcp, oracle, tmp_path):
     got = outs["pipeline"][0]
     assert got["big/0"] == S.synthetic_chunk(5 * 1_000_003 + 30 * 61 + 1, 26 * MiB + 5).tobytes()
     assert got["big/1"] == b""   # parity gone: header reads as zeros -> empty chunk, as the reference
+
+
+@pytest.mark.parametrize("fold", ["pipelined", "batched"])
+def test_node_fold_server_for_connected_clients(tmp_path, fold):
+    """The node fold server as an MPI job would use it: a server process on a
+    Unix socket holds the GPU (bcp_fold_server_serve); two client processes
+    connect (bcp_fold_server_connect, memfd arenas the server maps at its own
+    addresses) and run gen + rebuild with loopback ranks inside; every fold
+    runs on the device in the server.  Parity and rebuilds vs the oracle."""
+    import json
+    import subprocess
+    import sys
+    import time
+    import test_fold_server_cpu as F
+    sock = str(tmp_path / "fs.sock")
+    srv = subprocess.Popen([sys.executable, "-c", F.SERVER, sock, F.ROOT, "6", "gpu", ""], stdout=subprocess.PIPE,
+                           text=True)
+    assert srv.stdout.readline().strip() == "serving"
+    for _ in range(500):
+        if os.path.exists(sock):
+            break
+        time.sleep(0.01)
+    clients = [subprocess.Popen([sys.executable, "-c", F.CLIENT, sock, F.ROOT, str(tmp_path / f"store{k}"), "gpu", "",
+                                 "3", fold, str(20 + k)], stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+               for k in range(2)]
+    for c in clients:
+        out, err = c.communicate(timeout=200)
+        assert c.returncode == 0, err[-3000:]
+        d = json.loads(out.strip().splitlines()[-1])
+        assert d["errors"] == 0 and d["rb_errors"] == 0 and d["bad"] == [], d
+        assert d["server_folds"] > 0, d
+    srv_out, _ = srv.communicate(timeout=60)
+    assert srv.returncode == 0 and "served" in srv_out
