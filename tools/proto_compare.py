@@ -213,7 +213,22 @@ def main():
     ap.add_argument("--lanes", type=int, default=12)
     ap.add_argument("--procs", action="store_true", help="ranks as processes kept alive across runs")
     ap.add_argument("--procs-cold", action="store_true", help="ranks as processes forked for every run")
+    ap.add_argument("--fold-server", action="store_true",
+                    help="ranks as threads, every GPU fold through a node fold server process on a socket "
+                         "(bcp_fold_server_connect: an MPI job's shape)")
     a = ap.parse_args()
+    server = None
+    if a.fold_server:  # before this process touches the GPU: the server is the only HIP context
+        sock = os.path.join("/tmp", f"bcp_fs_{os.getpid()}.sock")
+        code = ("import sys; sys.path.insert(0, %r); import bcp_ctypes as b; print('serving', flush=True); "
+                "b.fold_server_serve(%r, 0)" % (os.path.join(ROOT, "beegfs-chunk-parity_amd"), sock))
+        server = subprocess.Popen([sys.executable, "-c", code], stdout=subprocess.PIPE, text=True)
+        assert server.stdout.readline().strip() == "serving"
+        for _ in range(500):
+            if os.path.exists(sock):
+                break
+            time.sleep(0.01)
+        bcp.fold_server_connect(sock, 2 << 30, 12)
     pools = {}
 
     def pool_for(nt):
@@ -245,11 +260,13 @@ def main():
     wl = a.workloads.split(",")
     import box_probe
     box = box_probe.cpu_info()
-    if not (a.procs or a.procs_cold):  # rank processes need a parent that never touched the GPU
+    if not (a.procs or a.procs_cold or a.fold_server):  # those keep the GPU out of this process
         box.update(box_probe.pcie_rates(bcp))
     emit(box=box)
     tr = {"transport": "socketpair rank processes, pooled" if a.procs else
           "socketpair rank processes, forked per run" if a.procs_cold else "loopback threads"}
+    if a.fold_server:
+        tr["fold_server"] = "connected (bcp_fold_server_connect)"
     if "c1_gen" in wl or "c1_rebuild" in wl:
         root = os.path.join(a.root, "c1")
         shutil.rmtree(root, ignore_errors=True)
@@ -317,6 +334,8 @@ def main():
     close_pools()
     if not (a.procs or a.procs_cold):
         bcp.task_shutdown()
+    if server:
+        server.kill()  # serves forever; its socket file goes with /tmp
 
 
 if __name__ == "__main__":
