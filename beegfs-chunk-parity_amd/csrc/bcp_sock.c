@@ -43,6 +43,7 @@
 #include <string.h>
 #include <stdio.h>
 #include <sys/mman.h>
+#include <sys/resource.h>
 #include <sys/socket.h>
 #include <unistd.h>
 
@@ -221,6 +222,14 @@ int bcp_sock_world_create(int world_size, bcp_sock_world **out)
 {
     if (!out || world_size < 1 || world_size > 4096)
         return -EINVAL;
+    /* 2 * world * (world - 1) socket ends before fork (data + control): 57
+     * ranks need ~6,400 descriptors, beyond the usual soft limit of 1,024;
+     * raise the soft limit to the hard one (no privilege needed) */
+    struct rlimit rl;
+    if (getrlimit(RLIMIT_NOFILE, &rl) == 0 && rl.rlim_cur < rl.rlim_max) {
+        rl.rlim_cur = rl.rlim_max;
+        (void)setrlimit(RLIMIT_NOFILE, &rl);
+    }
     *out = NULL;
     bcp_sock_world *w = calloc(1, sizeof(*w));
     if (!w)

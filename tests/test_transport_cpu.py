@@ -404,3 +404,27 @@ def test_fold_server_losing_a_connection_fails_tasks_not_the_run(bcp, oracle, cp
     assert st.errors == 0
     for (path, holders, p, lens) in files:
         assert S.read_file(S.parity_path(root, p, path)) == oracle.gen_parity_file(contents[path]), path
+
+
+@pytest.mark.timeout(300)
+def test_rank_processes_wide_world(bcp, oracle, cpu_hook, tmp_path):
+    """A pool of 32 storage targets (33 rank processes, ~4,200 socket ends
+    before fork with the fold server's connections -- beyond a default soft
+    descriptor limit, which the world raises to the hard one): 16-wide
+    stripes through every rank, parity against the oracle."""
+    import resource
+    soft, hard = resource.getrlimit(resource.RLIMIT_NOFILE)
+    if hard != resource.RLIM_INFINITY and hard < 6000:
+        pytest.skip(f"hard descriptor limit {hard}")
+    rng = np.random.default_rng(5150)
+    root = str(tmp_path)
+    nt = 32
+    files = []
+    for i in range(24):
+        holders, p = S.random_layout(rng, nt, 16)
+        files.append((f"w/{i}", holders, p, [int(x) for x in rng.integers(0, 40_000, size=16)]))
+    items, contents = S.populate(root, nt, files, seed=9)
+    st = bcp.gen_run_procs(root, nt, items, nlanes=2)
+    assert st.errors == 0
+    for (path, holders, p, lens) in files:
+        assert S.read_file(S.parity_path(root, p, path)) == oracle.gen_parity_file(contents[path]), path
