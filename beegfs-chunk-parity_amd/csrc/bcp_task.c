@@ -1863,8 +1863,13 @@ static void parity_generator(const bcp_transport_ops *T, const char *path, const
                       T->send_fill != bcp_lb_transport()->send_fill && bcpi_arena_block(L->h_win[0], &rb_, &rz_);
     /* folds go to a node fold server (rows in its arena): ranges too */
     const int remote_fold = !res_rc && L && L->device < 0 && g_srv_n > 0 && bcpi_arena_block(L->h_win[0], &rb_, &rz_);
+    /* (through a server, whole windows batched across ranks beat range by
+     * range: r2d0 for rank processes, r2d3 for loopback ranks of a
+     * connected process -- config 5 41-54 vs 36-46 GiB/s; so ranges go to
+     * a server only with BCP_XPROC_PIPELINE=1) */
     int pipelined = mode == BCP_FOLD_PIPELINED && !res_rc && expected_messages == 1 && T->send_fill &&
-                    (T->send_fill == bcp_lb_transport()->send_fill || xproc);
+                    ((T->send_fill == bcp_lb_transport()->send_fill && (!remote_fold || (xpe && atoi(xpe) > 0))) ||
+                     xproc);
     if (pipelined && !hook && !remote_fold && !L->q && bcp_queue_create(L->eng, &L->q))
         pipelined = 0;
     if (serial_io && !res_rc)
