@@ -124,6 +124,7 @@ _SIGS = {
     "bcp_task_inject_failure": ([ctypes.c_int, ctypes.c_int, ctypes.c_int], ctypes.c_int),
     "bcp_task_phase_stats": ([ctypes.POINTER(ctypes.c_double), ctypes.c_int, ctypes.c_int], ctypes.c_int),
     "bcp_task_set_transport": ([_V], ctypes.c_int),
+    "bcp_task_set_rebuild_lanes": ([ctypes.c_int], ctypes.c_int),
     "bcp_fold_server_serve": ([ctypes.c_char_p, ctypes.c_int], ctypes.c_int),
     "bcp_fold_server_connect": ([ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int], ctypes.c_int),
     "bcp_fold_server_stats": ([ctypes.POINTER(ctypes.c_uint64)], ctypes.c_int),
@@ -687,6 +688,14 @@ def set_fold_mode(mode: int) -> int:
     rc = lib().bcp_task_set_fold_mode(mode)
     if rc < 0:
         raise BcpError("bcp_task_set_fold_mode", rc)
+    return rc
+
+
+def set_rebuild_lanes(n: int) -> int:
+    """Lanes per rank of the rebuild runners (1 = the reference's); returns the previous value."""
+    rc = lib().bcp_task_set_rebuild_lanes(n)
+    if rc < 0:
+        raise BcpError("bcp_task_set_rebuild_lanes", rc)
     return rc
 
 

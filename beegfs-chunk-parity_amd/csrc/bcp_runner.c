@@ -396,7 +396,27 @@ typedef struct {
     start_gate *gate;
     ProgressSample sample;
     uint64_t tasks;
+    int lane, nlanes; /* items i with i % nlanes == lane, MPI tag = lane */
 } rebuild_arg;
+
+/* Rebuild lanes (bcp_task_set_rebuild_lanes): the reference rebuilds with
+ * one lane (rebuild/main.c walks its DB in one thread, tag 0); tasks are
+ * independent, so L lanes per rank -- item i on lane i % L with tag i % L,
+ * the same on every rank since every rank walks the same list -- give the
+ * same files, the corrupt lists' lines possibly in another order. */
+static int g_rebuild_lanes = 1;
+
+int bcp_task_set_rebuild_lanes(int nlanes)
+{
+    if (nlanes < 1 || nlanes > 64)
+        return -EINVAL;
+    return __atomic_exchange_n(&g_rebuild_lanes, nlanes, __ATOMIC_ACQ_REL);
+}
+
+static int rebuild_lanes(void)
+{
+    return __atomic_load_n(&g_rebuild_lanes, __ATOMIC_ACQUIRE);
+}
 
 /* do_file (rebuild/main.c:40-89) over the whole item list, one lane. */
 static void *rebuild_rank(void *p)
@@ -407,7 +427,10 @@ static void *rebuild_rank(void *p)
     bcp_lb_set_rank(a->rank);
     const int my_st = a->hs->storage_target;
     const int victim = a->rebuild_target;
+    const int nl = a->nlanes > 1 ? a->nlanes : 1;
     for (size_t i = 0; i < a->nitems; i++) {
+        if (nl > 1 && (int)(i % (size_t)nl) != a->lane)
+            continue;
         const FileInfo *fi = &a->items[i].fi;
         const int P = GET_P(fi->locations);
         if ((uint64_t)P == NO_P || P == victim || TEST_BIT(fi->locations, victim) == 0)
@@ -418,7 +441,7 @@ static void *rebuild_rank(void *p)
         mod.locations &= ~(UINT64_C(1) << victim);
         mod.locations = WITH_P(mod.locations, (uint64_t)victim);
         const int rdir = (P == my_st) ? a->hs->read_parity_dir : a->hs->read_chunk_dir;
-        TaskInfo ti = {rdir, 1, P, 0, &a->sample};
+        TaskInfo ti = {rdir, 1, P, nl > 1 ? a->lane : 0, &a->sample};
         double t0 = now_s();
         if (process_task(a->hs, a->items[i].path, &mod, ti)) {
             a->sample.dt += now_s() - t0;
@@ -453,9 +476,10 @@ int bcp_rebuild_run(const char *store_root, int ntargets, int rebuild_target, co
         close(corrupt_fd);
         return rc;
     }
+    const int nl = rebuild_lanes();
     HostState *hs = calloc((size_t)ntargets, sizeof(HostState));
-    rebuild_arg *args = calloc((size_t)ntargets, sizeof(rebuild_arg));
-    pthread_t *th = calloc((size_t)ntargets, sizeof(pthread_t));
+    rebuild_arg *args = calloc((size_t)ntargets * (size_t)nl, sizeof(rebuild_arg));
+    pthread_t *th = calloc((size_t)ntargets * (size_t)nl, sizeof(pthread_t));
     if (!hs || !args || !th) {
         rc = -ENOMEM;
         goto out;
@@ -466,9 +490,11 @@ int bcp_rebuild_run(const char *store_root, int ntargets, int rebuild_target, co
     double t0 = now_s();
     int started = 0, spawn_rc = 0;
     start_gate gate = START_GATE_INIT;
-    for (int k = 0; k < ntargets && !spawn_rc; k++) {
-        args[k] = (rebuild_arg){&hs[k], items, nitems, rebuild_target, k + 1, &gate, PROGRESS_SAMPLE_INIT, 0};
-        if ((spawn_rc = spawn(&th[k], rebuild_rank, &args[k])) == 0)
+    for (int t = 0; t < ntargets * nl && !spawn_rc; t++) {
+        const int k = t / nl;
+        args[t] = (rebuild_arg){&hs[k], items, nitems, rebuild_target, k + 1, &gate, PROGRESS_SAMPLE_INIT, 0,
+                                t % nl, nl};
+        if ((spawn_rc = spawn(&th[t], rebuild_rank, &args[t])) == 0)
             started++;
     }
     gate_open(&gate, spawn_rc != 0);
@@ -476,20 +502,21 @@ int bcp_rebuild_run(const char *store_root, int ntargets, int rebuild_target, co
         pthread_join(th[k], NULL);
     if (spawn_rc) {
         if (log)
-            fprintf(log, "bcp_rebuild_run: rank thread %d of %d not created (%s); no task was started\n", started,
-                    ntargets, strerror(spawn_rc));
+            fprintf(log, "bcp_rebuild_run: lane thread %d of %d not created (%s); no task was started\n", started,
+                    ntargets * nl, strerror(spawn_rc));
         rc = -EAGAIN;
         goto out;
     }
     if (stats) {
         memset(stats, 0, sizeof(*stats));
         stats->seconds = now_s() - t0;
-        for (int k = 0; k < ntargets; k++) {
-            stats->tasks += args[k].tasks;
-            stats->bytes_read += args[k].sample.bytes_read;
-            stats->bytes_written += args[k].sample.bytes_written;
-            stats->errors += hs[k].error != 0;
+        for (int t = 0; t < ntargets * nl; t++) {
+            stats->tasks += args[t].tasks;
+            stats->bytes_read += args[t].sample.bytes_read;
+            stats->bytes_written += args[t].sample.bytes_written;
         }
+        for (int k = 0; k < ntargets; k++)
+            stats->errors += hs[k].error != 0;
     }
 out:
     if (hs)
@@ -785,11 +812,27 @@ static void rank_run(const procs_job *J, int k, rank_report *rep)
         free(args);
         free(th);
     } else if (!rc) {
-        rebuild_arg a = {&hs, J->items, J->nitems, J->rebuild_target, k + 1, NULL, PROGRESS_SAMPLE_INIT, 0};
-        rebuild_rank(&a);
-        rep->tasks = a.tasks;
-        rep->bytes_read = a.sample.bytes_read;
-        rep->bytes_written = a.sample.bytes_written;
+        const int nl = J->nlanes > 1 ? J->nlanes : 1; /* the caller's rebuild lanes */
+        rebuild_arg *ra = calloc((size_t)nl, sizeof(rebuild_arg));
+        pthread_t *rt = calloc((size_t)nl, sizeof(pthread_t));
+        start_gate gate = START_GATE_INIT;
+        int started = 0, src = (!ra || !rt) ? ENOMEM : 0;
+        for (int l = 0; l < nl && !src; l++) {
+            ra[l] = (rebuild_arg){&hs, J->items, J->nitems, J->rebuild_target, k + 1, &gate, PROGRESS_SAMPLE_INIT,
+                                  0, l, nl};
+            if ((src = spawn(&rt[l], rebuild_rank, &ra[l])) == 0)
+                started++;
+        }
+        gate_open(&gate, src != 0);
+        for (int l = 0; l < started; l++) {
+            pthread_join(rt[l], NULL);
+            rep->tasks += ra[l].tasks;
+            rep->bytes_read += ra[l].sample.bytes_read;
+            rep->bytes_written += ra[l].sample.bytes_written;
+        }
+        rc = src ? -src : 0;
+        free(ra);
+        free(rt);
     }
     if (!rc) {
         rep->error = hs.error;
@@ -1217,7 +1260,8 @@ int bcp_rank_pool_rebuild(bcp_rank_pool *P, const char *store_root, int rebuild_
             return -errno;
         close(fd);
     }
-    return pool_run(P, POOL_REBUILD, store_root, items, nitems, 1, NULL, rebuild_target, corrupt_list_path, stats);
+    return pool_run(P, POOL_REBUILD, store_root, items, nitems, rebuild_lanes(), NULL, rebuild_target,
+                    corrupt_list_path, stats);
 }
 
 int bcp_rank_pool_destroy(bcp_rank_pool *P)

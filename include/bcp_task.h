@@ -277,6 +277,13 @@ int bcp_lb_waitall(int n, bcp_lb_req **reqs);
  * fill returns 0 or a negative errno, which bcp_lb_send_fill returns. */
 int bcp_lb_send_fill(bcp_lb_fill_fn fill, void *ctx, size_t n, int dst, int tag);
 
+/* Lanes of the rebuild runners (bcp_rebuild_run[_db|_procs], rank pools):
+ * 1 = the reference's single lane (default); with L, item i goes to lane
+ * i % L with MPI tag i % L on every rank -- the same files (the corrupt
+ * lists' lines may come in another order).  Returns the previous value or
+ * -EINVAL (1..64). */
+int bcp_task_set_rebuild_lanes(int nlanes);
+
 /* ---- node fold server for independent rank processes (an MPI job) ------
  * One process per node serves folds for every rank on a Unix socket
  * (bcp_fold_server_serve; it is the only process with a HIP runtime; serves

@@ -428,3 +428,38 @@ def test_rank_processes_wide_world(bcp, oracle, cpu_hook, tmp_path):
     assert st.errors == 0
     for (path, holders, p, lens) in files:
         assert S.read_file(S.parity_path(root, p, path)) == oracle.gen_parity_file(contents[path]), path
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("procs", [False, True], ids=["threads", "rank-processes"])
+def test_rebuild_lanes(bcp, oracle, cpu_hook, tmp_path, procs):
+    """bcp_task_set_rebuild_lanes(4): item i on lane i % 4 with tag i % 4 on
+    every rank; the rebuilt chunks and the corrupt list (as a set of lines)
+    equal the single-lane rebuild's."""
+    rng = np.random.default_rng(4242)
+    ntargets = 6
+    files = _random_files(rng, ntargets, 40, 400_000)
+    files.append(("big/r", [0, 2, 4], 5, [10 * MiB + 7, 3, 12 * MiB]))
+    root = str(tmp_path)
+    items, contents = S.populate(root, ntargets, files, seed=12, timestamp=0)  # every chunk newer: all corrupt
+    assert (bcp.gen_run_procs if procs else bcp.gen_run)(root, ntargets, items, nlanes=3).errors == 0
+    victim = 2
+    lost = {path: S.read_file(S.chunk_path(root, victim, path)) for (path, h, p, lens) in files if victim in h}
+    results = {}
+    for lanes in (1, 4):
+        for path in lost:
+            os.remove(S.chunk_path(root, victim, path))
+        prev = bcp.set_rebuild_lanes(lanes)
+        try:
+            corrupt = str(tmp_path / f"corrupt{lanes}.txt")
+            st = (bcp.rebuild_run_procs if procs else bcp.rebuild_run)(root, ntargets, victim, items,
+                                                                         corrupt_list=corrupt)
+        finally:
+            bcp.set_rebuild_lanes(prev)
+        assert st.errors == 0 and st.tasks > 0
+        for path, data in lost.items():
+            assert S.read_file(S.chunk_path(root, victim, path)) == data, (lanes, path)
+        results[lanes] = sorted(open(corrupt).read().splitlines())
+    assert results[1] and results[1] == results[4]
+    with pytest.raises(bcp.BcpError):
+        bcp.set_rebuild_lanes(0)

@@ -213,6 +213,8 @@ def main():
     ap.add_argument("--lanes", type=int, default=12)
     ap.add_argument("--procs", action="store_true", help="ranks as processes kept alive across runs")
     ap.add_argument("--procs-cold", action="store_true", help="ranks as processes forked for every run")
+    ap.add_argument("--rebuild-lanes", type=int, default=1,
+                    help="lanes per rank of the rebuild (bcp_task_set_rebuild_lanes; 1 = the reference's)")
     ap.add_argument("--fold-server", action="store_true",
                     help="ranks as threads, every GPU fold through a node fold server process on a socket "
                          "(bcp_fold_server_connect: an MPI job's shape)")
@@ -252,6 +254,7 @@ def main():
     else:
         gen, rebuild = bcp.gen_run, bcp.rebuild_run
     folds = a.folds.split(",")
+    bcp.set_rebuild_lanes(a.rebuild_lanes)
     noop = noop_hook()
     hooks = {"cpu_reference": ctypes.cast(oracle.lib().oracle_xor_rows, ctypes.c_void_p).value,
              "cpu_pipelined": ctypes.cast(oracle.lib().oracle_xor_rows, ctypes.c_void_p).value,
@@ -308,7 +311,7 @@ def main():
                         if S.read_file(fn) != contents[path][holders.index(2)].tobytes():
                             return False, path
                 return True, None
-            measure("config1_rebuild", folds, a.rounds, run_rb, check_rb, rb_bytes, hooks, {"lanes": 1, **tr},
+            measure("config1_rebuild", folds, a.rounds, run_rb, check_rb, rb_bytes, hooks, {"lanes": a.rebuild_lanes, **tr},
                     prepare=drop_lost)
         shutil.rmtree(root, ignore_errors=True)
     if "c5_gen" in wl:
