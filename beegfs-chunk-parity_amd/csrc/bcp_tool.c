@@ -42,7 +42,7 @@ static int usage(void)
     fputs("usage: bcp find-all-chunks <chunks_dir>\n"
           "       bcp parity-gen --complete|--partial [--pipeline|--procs] [--fold MODE] [--lanes N] [--force]\n"
           "                      [--changelog DIR] <store_root> <ntargets>\n"
-          "       bcp parity-rebuild [--pipeline|--procs] [--fold MODE] [--db DIR] [--corrupt FILE]\n"
+          "       bcp parity-rebuild [--pipeline|--procs] [--fold MODE] [--lanes N] [--db DIR] [--corrupt FILE]\n"
           "                          <store_root> <ntargets> <target>\n"
           "       MODE: batched | pipelined | device-rows | streamed | zero-copy | staged\n",
           stderr);
@@ -242,6 +242,9 @@ static int cmd_rebuild(int argc, char **argv)
             use_procs = 1;
         else if (!strcmp(argv[i], "--fold") && i + 1 < argc) {
             if (fold_mode_arg(argv[++i]) < 0 || bcp_task_set_fold_mode(fold_mode_arg(argv[i])) < 0)
+                return usage();
+        } else if (!strcmp(argv[i], "--lanes") && i + 1 < argc) {
+            if (bcp_task_set_rebuild_lanes(atoi(argv[++i])) < 0) /* (the reference rebuilds with one) */
                 return usage();
         } else
             return usage();

@@ -438,7 +438,8 @@ def test_cli_complete_partial_rebuild(bcp, oracle, tmp_path, engine_kind):
         if victim in holders:
             lost[p_] = S.read_file(S.chunk_path(root, victim, p_))
             os.remove(S.chunk_path(root, victim, p_))
-    r = subprocess.run([bcp.BIN_PATH, "parity-rebuild", *flags, root, str(nt), str(victim)], capture_output=True)
+    rflags = flags + (["--lanes", "4"] if engine_kind in ("protocol", "procs") else [])  # rebuild lanes
+    r = subprocess.run([bcp.BIN_PATH, "parity-rebuild", *rflags, root, str(nt), str(victim)], capture_output=True)
     assert r.returncode == 0, r.stderr
     for p_, data in lost.items():
         assert S.read_file(S.chunk_path(root, victim, p_)) == data, p_
