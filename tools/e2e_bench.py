@@ -213,22 +213,27 @@ def config1(a):
                 good += S.read_file(fn) == contents[path][holders.index(2)].tobytes()
         return good, good == len(range(0, len(lost), max(1, len(lost) // a.verify)))
 
-    # single lane, as rebuild/main.c; the three folds interleaved in rotating order
-    rvariants = [("rebuild_protocol_gpu_fold(bcp_rebuild_run)", None, None, False),
-                 ("rebuild_protocol_gpu_fold_staged(bcp_rebuild_run)", bcp.FOLD_STAGED, None, False),
-                 ("rebuild_" + CPU_REF + "(oracle_xor_rows)", bcp.FOLD_ZERO_COPY, cpu_fold, True),
-                 ("rebuild_" + CPU_PIPE + "(oracle_xor_rows)", None, cpu_fold, False)]
+    # single lane, as rebuild/main.c, and 12 rebuild lanes (bcp_task_set_rebuild_lanes); the folds
+    # interleaved in rotating order
+    rvariants = [("rebuild_protocol_gpu_fold(bcp_rebuild_run)", None, None, False, 1),
+                 ("rebuild_protocol_gpu_fold_staged(bcp_rebuild_run)", bcp.FOLD_STAGED, None, False, 1),
+                 ("rebuild_" + CPU_REF + "(oracle_xor_rows)", bcp.FOLD_ZERO_COPY, cpu_fold, True, 1),
+                 ("rebuild_" + CPU_PIPE + "(oracle_xor_rows)", None, cpu_fold, False, 1),
+                 ("rebuild_protocol_gpu_fold(bcp_rebuild_run,12 lanes)", None, None, False, 12),
+                 ("rebuild_" + CPU_REF + "(oracle_xor_rows,12 lanes)", bcp.FOLD_ZERO_COPY, cpu_fold, True, 12)]
     rtimes = {v[0]: [] for v in rvariants}
     nv = len(rvariants)
     for r in range(1 + preps):
-        for label, mode, hook, serial in rvariants[r % nv:] + rvariants[:r % nv]:
+        for label, mode, hook, serial, lanes in rvariants[r % nv:] + rvariants[:r % nv]:
             drop_lost()
             restore = fold_ctx(mode, hook, serial)
+            prev_lanes = bcp.set_rebuild_lanes(lanes)
             try:
                 t0 = time.perf_counter()
                 st = bcp.rebuild_run(root, 4, 2, items)
                 rtimes[label].append(time.perf_counter() - t0)
             finally:
+                bcp.set_rebuild_lanes(prev_lanes)
                 restore()
             if r == preps:
                 good, okv = rebuilt_ok()
