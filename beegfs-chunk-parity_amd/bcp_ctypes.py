@@ -93,6 +93,8 @@ _SIGS = {
     "bcp_host_alloc": ([_V, ctypes.c_size_t, ctypes.POINTER(_V)], ctypes.c_int),
     "bcp_host_alloc_mapped": ([_V, ctypes.c_size_t, ctypes.POINTER(_V)], ctypes.c_int),
     "bcp_host_free": ([_V, _V], ctypes.c_int),
+    "bcp_host_register": ([_V, _V, ctypes.c_size_t], ctypes.c_int),
+    "bcp_host_unregister": ([_V, _V], ctypes.c_int),
     "bcp_h2d_async": ([_V, _V, _V, ctypes.c_size_t], ctypes.c_int),
     "bcp_d2h_async": ([_V, _V, _V, ctypes.c_size_t], ctypes.c_int),
     "bcp_d2d_async": ([_V, _V, _V, ctypes.c_size_t], ctypes.c_int),
@@ -287,6 +289,13 @@ class Engine:
 
     def host_free(self, ptr: int):
         call("bcp_host_free", self.h, _V(ptr))
+
+    def host_register(self, ptr: int, nbytes: int):
+        """Caller-owned host memory the kernels then read and write in place."""
+        call("bcp_host_register", self.h, _V(ptr), nbytes)
+
+    def host_unregister(self, ptr: int):
+        call("bcp_host_unregister", self.h, _V(ptr))
 
     def close(self):
         if self.h:

@@ -875,3 +875,32 @@ def test_descriptor_u16_mixed_batch(oracle, engine, dev, queue, pipe):
             engine.option(k, v)
     for i, (o, r) in enumerate(zip(outs, refs)):
         assert np.array_equal(o, r), i
+
+
+def test_registered_caller_memory_folds_in_place(oracle, engine, queue):
+    """bcp_host_register: a shared anonymous mapping (the kind of memory the
+    rank pool's row arena and a connected client's memfd are) registered by
+    the caller; a descriptor batch reads its rows and writes its output in
+    place over PCIe, then the memory is unregistered.  Same bytes as the
+    oracle."""
+    import mmap
+    n, L = 5, 300_000
+    m = mmap.mmap(-1, 4 << 20, flags=mmap.MAP_SHARED)
+    buf = np.frombuffer(m, dtype=np.uint8)
+    base = buf.ctypes.data
+    rng = np.random.default_rng(77)
+    rows = [rng.integers(0, 256, size=L - 1000 * k, dtype=np.uint8) for k in range(n)]
+    pitch = 320 * 1024
+    for k, r in enumerate(rows):
+        buf[k * pitch:k * pitch + r.size] = r
+    out_off = n * pitch
+    engine.host_register(base, 4 << 20)
+    try:
+        queue.xor_stripes([(base + out_off, L, 0, n, 0)], [(base + k * pitch, rows[k].size) for k in range(n)])
+        queue.sync()
+        got = buf[out_off:out_off + L].copy()
+    finally:
+        engine.host_unregister(base)
+    assert np.array_equal(got, oracle.xor_padded_np(rows))
+    del buf
+    m.close()
