@@ -556,3 +556,46 @@ def test_node_fold_server_for_connected_clients(tmp_path, fold):
         assert d["server_folds"] > 0, d
     srv_out, _ = srv.communicate(timeout=60)
     assert srv.returncode == 0 and "served" in srv_out
+
+
+POOL5_SCRIPT = r"""
+import os, sys
+root, here = sys.argv[1], sys.argv[2]
+sys.path[:0] = [os.path.join(here, "..", "beegfs-chunk-parity_amd"), os.path.join(here, "..", "oracle")]
+import numpy as np
+import bcp_ctypes as bcp, bcp_store as S, oracle
+rng = np.random.default_rng(55)
+nt, KiB, MiB = 9, 1024, 1024 * 1024
+files = []
+for i in range(150):
+    holders, p = S.random_layout(rng, nt, 8)
+    lens = [int(x) for x in np.exp(rng.uniform(np.log(64 * KiB), np.log(4 * MiB), size=8))]
+    files.append((f"c5/{i % 7}/x{i}", holders, p, lens))
+items, contents = S.populate(root, nt, files, seed=6)
+with bcp.RankPool(nt) as pool:
+    assert pool.gen(root, items, nlanes=12).errors == 0
+    for (path, holders, p, lens) in files:
+        assert S.read_file(S.parity_path(root, p, path)) == oracle.gen_parity_file(contents[path]), path
+    victim, lost = 4, {}
+    for (path, holders, p, lens) in files:
+        if victim in holders:
+            lost[path] = S.read_file(S.chunk_path(root, victim, path))
+            os.remove(S.chunk_path(root, victim, path))
+    bcp.set_rebuild_lanes(6)
+    assert lost and pool.rebuild(root, victim, items).errors == 0
+    for path, data in lost.items():
+        assert S.read_file(S.chunk_path(root, victim, path)) == data, path
+print("pool5 ok")
+"""
+
+
+def test_rank_pool_config5_shapes_every_file(tmp_path):
+    """Config-5 shapes (9 targets, 8-wide stripes of 64 KiB-4 MiB chunks,
+    150 stripes) through nine rank processes and the node fold server (the
+    default), every parity file against the oracle, then a 6-lane rebuild
+    of one target, every rebuilt chunk compared."""
+    import subprocess
+    import sys
+    r = subprocess.run([sys.executable, "-c", POOL5_SCRIPT, str(tmp_path), HERE], capture_output=True, text=True,
+                       timeout=240)
+    assert r.returncode == 0 and "pool5 ok" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]
