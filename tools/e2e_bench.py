@@ -176,12 +176,16 @@ def config1(a):
     # the whole beegfs-parity-gen --complete flow through the CLI: scan every
     # target, plan (P per select_P), run, fill the DB replicas (warm median)
     tool = os.path.join(ROOT, "beegfs-chunk-parity_amd", "bin", "bcp")
-    for label, extra in (("cli_parity_gen_complete(protocol)", []), ("cli_parity_gen_complete(pipeline)", ["--pipeline"])):
+    no_server = dict(os.environ, BCP_FOLD_SERVER="0")
+    for label, extra, env in (("cli_parity_gen_complete(protocol)", [], None),
+                              ("cli_parity_gen_complete(pipeline)", ["--pipeline"], None),
+                              ("cli_parity_gen_complete(procs, node fold server)", ["--procs"], None),
+                              ("cli_parity_gen_complete(procs, HIP context per rank)", ["--procs"], no_server)):
         times = []
         for r in range(1 + a.reps):
             t0 = time.perf_counter()
             res = subprocess.run([tool, "parity-gen", "--complete", "--force"] + extra + [root, "4"],
-                                 capture_output=True, text=True)
+                                 capture_output=True, text=True, env=env)
             times.append(time.perf_counter() - t0)
             if res.returncode != 0:
                 emit(config=1, path=label, error=res.stderr[-500:])
