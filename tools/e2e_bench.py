@@ -178,6 +178,7 @@ def config1(a):
     tool = os.path.join(ROOT, "beegfs-chunk-parity_amd", "bin", "bcp")
     no_server = dict(os.environ, BCP_FOLD_SERVER="0")
     for label, extra, env in (("cli_parity_gen_complete(protocol)", [], None),
+                              ("cli_parity_gen_complete(protocol, --fold batched)", ["--fold", "batched"], None),
                               ("cli_parity_gen_complete(pipeline)", ["--pipeline"], None),
                               ("cli_parity_gen_complete(procs, node fold server)", ["--procs"], None),
                               ("cli_parity_gen_complete(procs, HIP context per rank)", ["--procs"], no_server)):
