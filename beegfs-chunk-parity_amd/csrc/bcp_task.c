@@ -1029,8 +1029,18 @@ int bcp_fold_server_connect(const char *socket_path, size_t arena_bytes, int nco
         struct sockaddr_un a = {0};
         a.sun_family = AF_UNIX;
         strcpy(a.sun_path, socket_path);
-        if (fd < 0 || connect(fd, (struct sockaddr *)&a, sizeof(a)) != 0) {
-            rc = -errno;
+        int crc = fd < 0 ? -errno : 0;
+        /* a server still starting (socket file missing, or bound but not
+         * yet listening): retry for up to ~2 s */
+        for (int t = 0; !crc && connect(fd, (struct sockaddr *)&a, sizeof(a)) != 0; t++) {
+            if ((errno != ECONNREFUSED && errno != ENOENT && errno != EAGAIN) || t >= 200) {
+                crc = -errno;
+                break;
+            }
+            usleep(10000);
+        }
+        if (crc) {
+            rc = crc;
             if (fd >= 0)
                 close(fd);
             break;
