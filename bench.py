@@ -18,7 +18,10 @@ value = algorithmic bytes of all ranks / max-over-ranks wall time, with
 algorithmic bytes = sum of source lengths + output length per stripe
 ((N+1) x 512 KiB = 4,718,592 B for config 2).  N>1 (torchrun): each rank owns
 its own stripe shard on its own GPU (no data-path collective; gloo only for
-the start barrier and the max-time reduction), scaling "weak".
+the start barrier and the max-time reduction), scaling "weak".  `--gpus N`
+without a launcher starts the N ranks itself (a torchrun child process, before
+any HIP call) and relays rank 0's line and the exit code; it refuses when the
+ranks would share GPUs unless --allow-shared.
 
 roofline.achieved / frac (= frac_event) use the kernel's HIP-event time on the
 stream it runs on; frac_rocprof, traffic and their provenance (profile files
@@ -81,7 +84,60 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget over its three legs")
     ap.add_argument("--cpu-stripes", type=int, default=256, help="stripes in the 1-thread CPU sample pool")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--allow-shared", action="store_true",
+                    help="run N ranks even when fewer than N distinct GPUs exist (rehearsal; "
+                         "the line then says shared_gpu true and counts distinct GPUs)")
     return ap.parse_args()
+
+
+def box_of(pci_bus_id: str) -> dict:
+    """The machine this process runs on -- so figures measured on different
+    boxes read as such: the kernel's boot id (one per host boot; container host
+    names are not unique on this pool), the GPU's unique id and PCI bus id, the
+    CPU model and the host name."""
+    import socket
+
+    def read(path):
+        try:
+            return open(path).read().strip() or None
+        except OSError:
+            return None
+    model = ""
+    try:
+        model = next(l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name"))
+    except (OSError, StopIteration):
+        pass
+    bus = (pci_bus_id or "").lower()
+    return {"boot_id": read("/proc/sys/kernel/random/boot_id"),
+            "gpu_unique_id": read(f"/sys/bus/pci/devices/{bus}/unique_id") if bus else None,
+            "pci_bus_id": pci_bus_id, "cpu_model": model, "host": socket.gethostname()}
+
+
+def launch_ranks(a) -> int:
+    """`bench.py --gpus N` without a launcher (WORLD_SIZE unset): run N ranks,
+    one process per GPU, as a torchrun CHILD process and return its exit code.
+    Called before anything touches HIP (bcp_ctypes loads libbcp lazily), and
+    never by exec.  Refuses (rc 4) when fewer than N GPUs are visible, unless
+    --allow-shared; the ranks check the distinct PCI bus ids themselves too."""
+    import socket
+    import subprocess
+    if not a.allow_shared:
+        import torch  # device_count() enumerates without initialising HIP on this image
+        ndev = torch.cuda.device_count()
+        if ndev < a.gpus:
+            print(f"bench.py: --gpus {a.gpus} but {ndev} GPU(s) visible; refusing to report "
+                  f"{a.gpus} GPUs (pass --allow-shared to rehearse with shared devices)", file=sys.stderr)
+            return 4
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    env.setdefault("OMP_NUM_THREADS", "1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}",
+           os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd, env=env).returncode
 
 
 def pmc_traffic(workload_key: str, kernel_tag: str):
@@ -112,7 +168,14 @@ def pmc_traffic(workload_key: str, kernel_tag: str):
 
 def main():
     a = parse()
+    if a.gpus < 1:
+        sys.exit("bench.py: --gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        sys.exit(launch_ranks(a))
     d = Dist()
+    if d.world != a.gpus and d.rank == 0:
+        print(f"bench.py: note: launched with {d.world} ranks for --gpus {a.gpus}; "
+              f"the line reports the ranks and distinct GPUs actually used", file=sys.stderr)
     ndev = bcp.device_count()
     assert ndev > 0, "bench.py needs a HIP device (there is no CPU path)"
     eng = bcp.Engine(d.local_rank % ndev)
@@ -120,6 +183,13 @@ def main():
     bus_ids = d.gather(eng.pci_bus_id())
     n_devices = len(set(bus_ids))
     shared_gpu = n_devices < d.world
+    if shared_gpu and not a.allow_shared:
+        if d.rank == 0:
+            print(f"bench.py: {d.world} ranks but only {n_devices} distinct GPU(s) (PCI bus ids "
+                  f"{sorted(set(bus_ids))}); refusing (pass --allow-shared to rehearse)", file=sys.stderr)
+        eng.close()
+        d.close()
+        sys.exit(4)
     if a.mode == "mixed":  # the timed kernel is the descriptor kernel
         if a.blocks_per_cu:
             eng.option("desc_blocks_per_cu", a.blocks_per_cu)
@@ -381,6 +451,7 @@ def main():
         frac_rocprof = None
         if pmc and pmc.get("rocprof_avg_ns"):
             frac_rocprof = round(bytes_per_step / (pmc["rocprof_avg_ns"] * 1e-9) / 1e9 / HBM_PEAK_GBS, 4)
+        run_box = box_of(bus_ids[0])
         line = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -409,6 +480,7 @@ def main():
                 "ranks": d.world,
                 "shared_gpu": shared_gpu,
                 "device": devname,
+                "pci_bus_ids": sorted(set(bus_ids)),
                 "cus": cus,
                 "verified_on_device": ok_all,
             },
@@ -427,8 +499,14 @@ def main():
                 "traffic_source": pmc["source"] if pmc else None,
                 "profile_files": pmc.get("files") if pmc else None,
                 "profile_commit": pmc.get("code_commit") if pmc else None,
-                "frac_note": "frac = frac_event: algorithmic bytes / HIP-event kernel time in this run; "
-                             "frac_rocprof: the same bytes / the committed rocprofv3 kernel-trace average",
+                # frac_event is this run's box; frac_rocprof / traffic the profile set's box
+                "run_box": run_box,
+                "profile_box": pmc.get("box") if pmc else None,
+                "same_box": bool(pmc and pmc.get("box") and run_box["boot_id"]
+                                 and pmc["box"].get("boot_id") == run_box["boot_id"]),
+                "frac_note": "frac = frac_event: algorithmic bytes / HIP-event kernel time in this run (run_box); "
+                             "frac_rocprof and traffic: the same bytes / the committed rocprofv3 kernel-trace "
+                             "average and PMC passes, measured on profile_box (a different box unless same_box)",
             },
             "cpu_baseline": cpu,
         }

@@ -58,3 +58,46 @@ def test_gloo_world2_reductions():
         assert p.exitcode == 0
     assert [r[:3] for r in res] == [(0, 3.0, 3.0), (1, 3.0, 3.0)]
     assert all(r[3] == ("0000:00:00.0", "0000:00:00.0") for r in res)
+
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.timeout(120)
+def test_bench_gpus_n_refuses_without_enough_gpus():
+    """`python3 bench.py --gpus 2` (the driver's form) with no GPU visible: a
+    clear refusal with a non-zero exit, no bench line -- never a silent 1-GPU run."""
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--stripes", "8", "--no-cpu"], cwd=ROOT,
+                       env=env, capture_output=True, text=True, timeout=100)
+    assert r.returncode == 4, (r.returncode, r.stderr[-2000:])
+    assert "refusing" in r.stderr and "--allow-shared" in r.stderr
+    assert not [l for l in r.stdout.splitlines() if l.startswith("{")]
+
+
+def test_bench_gpus_n_launches_a_torchrun_child(monkeypatch):
+    """--gpus N without WORLD_SIZE runs N ranks as a torchrun CHILD (never an
+    exec), passes every argument through and returns the child's exit code."""
+    import subprocess
+    sys.path.insert(0, ROOT)
+    import bench
+    seen = {}
+
+    class R:
+        returncode = 7
+
+    def fake_run(cmd, env=None, **kw):
+        seen["cmd"], seen["env"] = cmd, env
+        return R()
+
+    monkeypatch.setattr(subprocess, "run", fake_run)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "8", "--steps", "5", "--allow-shared"])
+    a = bench.parse()
+    assert bench.launch_ranks(a) == 7
+    cmd = seen["cmd"]
+    assert cmd[:3] == [sys.executable, "-m", "torch.distributed.run"]
+    assert "--nproc-per-node=8" in cmd and "127.0.0.1" in cmd
+    assert cmd[-5:] == ["--gpus", "8", "--steps", "5", "--allow-shared"]
+    assert cmd[-6].endswith("bench.py")
+    assert seen["env"]["MASTER_ADDR"] == "127.0.0.1"

@@ -50,9 +50,34 @@ def test_bench_torchrun_two_ranks_labels(bcp):
     ndev = bcp.device_count()
     line = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                  "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
-                 "bench.py", "--gpus", "2", "--stripes", "64", "--steps", "2", "--warmup", "1", "--no-cpu"], 420)
+                 "bench.py", "--gpus", "2", "--stripes", "64", "--steps", "2", "--warmup", "1", "--no-cpu",
+                 "--allow-shared"], 420)
     assert line["config"]["verified_on_device"] is True
     assert line["config"]["ranks"] == 2
     distinct = min(ndev, 2)  # bench maps local rank r to device r % ndev
     assert line["n_gpus"] == distinct
     assert line["config"]["shared_gpu"] is (distinct < 2)
+    assert line["roofline"]["run_box"]["pci_bus_id"] in line["config"]["pci_bus_ids"]
+
+
+@pytest.mark.timeout(500)
+def test_bench_gpus_n_launches_its_own_ranks(bcp):
+    """The driver's form, `python3 bench.py --gpus N` with no launcher: bench.py
+    starts N ranks itself.  With fewer GPUs than N it refuses (non-zero exit,
+    no line) unless --allow-shared, which reports the ranks and the distinct GPUs."""
+    ndev = bcp.device_count()
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    env.pop("WORLD_SIZE", None)
+    args = [sys.executable, "bench.py", "--gpus", "2", "--stripes", "64", "--steps", "2", "--warmup", "1", "--no-cpu"]
+    if ndev < 2:
+        r = subprocess.run(args, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+        assert r.returncode == 4, (r.returncode, r.stdout[-2000:], r.stderr[-2000:])
+        assert "refusing" in r.stderr
+        assert not [l for l in r.stdout.splitlines() if l.startswith("{")]
+    r = subprocess.run(args + ["--allow-shared"], cwd=ROOT, env=env, capture_output=True, text=True, timeout=420)
+    assert r.returncode == 0, (r.returncode, r.stdout[-2000:], r.stderr[-4000:])
+    line = _last_json(r.stdout)
+    assert line["config"]["ranks"] == 2
+    assert line["n_gpus"] == min(ndev, 2)
+    assert line["config"]["shared_gpu"] is (ndev < 2)
+    assert line["config"]["verified_on_device"] is True

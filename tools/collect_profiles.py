@@ -68,6 +68,14 @@ def main():
                         "--stats", rel(stats), "--commit", a.commit, "--files", rel(fetch), rel(write),
                         rel(os.path.join(a.dst, f"bench_{m}.json")),  # the committed copy of the bench line
                         "--out", os.path.join(a.dst, f"pmc_{m}.json")], check=True)
+        # the box the set was measured on (bench.py's run_box), for bench.py's profile_box
+        box = line["roofline"].get("run_box")
+        if box:
+            out = os.path.join(a.dst, f"pmc_{m}.json")
+            doc = json.load(open(out))
+            doc["box"] = box
+            with open(out, "w") as f:
+                json.dump(doc, f, indent=1)
 
 
 if __name__ == "__main__":
