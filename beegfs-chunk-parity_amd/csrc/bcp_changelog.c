@@ -14,7 +14,7 @@
  * summed chunk size (gen/main.c:688, used to order the worklist).
  *
  * Worklist (gen/main.c:703-715, 768-791): PCG32 shuffle with the reference's
- * fixed seed then a stable size sort; per path, merge with the previous
+ * fixed seed then the libc qsort by size; per path, merge with the previous
  * state (fill_in_missing_fields, :92-100), drop deleted holders, choose P by
  * select_P (:388-401: PCG32 seeded with simple_hash(path), weighted by the
  * cumulative free-space weights, never a holder), and mark NO_P when the
@@ -396,30 +396,15 @@ typedef struct {
     uint64_t idx;
 } size_index;
 
-static int cmp_size_stable(const void *a, const void *b)
+/* cmp_entries (gen/main.c:179-189) */
+static int cmp_size(const void *a, const void *b)
 {
-    const size_index *x = a, *y = b;
-    if (x->size != y->size)
-        return x->size < y->size ? -1 : 1;
-    return 0;
-}
-
-/* insertion-stable merge sort on size (glibc's qsort is a merge sort too) */
-static void stable_sort(size_index *v, size_t n, size_index *tmp)
-{
-    if (n < 2)
-        return;
-    size_t h = n / 2;
-    stable_sort(v, h, tmp);
-    stable_sort(v + h, n - h, tmp);
-    size_t i = 0, j = h, k = 0;
-    while (i < h && j < n)
-        tmp[k++] = cmp_size_stable(&v[j], &v[i]) < 0 ? v[j++] : v[i++];
-    while (i < h)
-        tmp[k++] = v[i++];
-    while (j < n)
-        tmp[k++] = v[j++];
-    memcpy(v, tmp, n * sizeof(*v));
+    uint64_t x = ((const size_index *)a)->size, y = ((const size_index *)b)->size;
+    if (x < y)
+        return -1;
+    if (x == y)
+        return 0;
+    return 1;
 }
 
 int bcp_plan_worklist(const bcp_eventset *s, int ntargets, const int *cum_weight, const bcp_work_item *prev,
@@ -436,12 +421,8 @@ int bcp_plan_worklist(const bcp_eventset *s, int ntargets, const int *cum_weight
     if (out_cap < s->n)
         return out ? -ENOSPC : 0;
     size_index *order = malloc((s->n ? s->n : 1) * sizeof(size_index));
-    size_index *tmp = malloc((s->n ? s->n : 1) * sizeof(size_index));
-    if (!order || !tmp) {
-        free(order);
-        free(tmp);
+    if (!order)
         return -ENOMEM;
-    }
     for (size_t i = 0; i < s->n; i++)
         order[i] = (size_index){s->e[i].size, i};
     /* shuffle (gen/main.c:373-386, fixed seed) then sort by total size */
@@ -454,7 +435,11 @@ int bcp_plan_worklist(const bcp_eventset *s, int ntargets, const int *cum_weight
             order[i] = t;
         }
     }
-    stable_sort(order, s->n, tmp);
+    /* The reference sorts with the C library's qsort (gen/main.c:711), whose
+     * order of equal sizes is the library's: glibc <= 2.36 merge-sorts (stable),
+     * later versions do not.  Calling the same qsort with the same comparator
+     * on the same shuffled array gives the reference's order on any libc. */
+    qsort(order, s->n, sizeof(size_index), cmp_size);
     for (size_t j = 0; j < s->n; j++) {
         const ev_entry *e = &s->e[order[j].idx];
         FileInfo fi = {e->timestamp, WITH_P(e->modified, NO_P)};
@@ -470,6 +455,5 @@ int bcp_plan_worklist(const bcp_eventset *s, int ntargets, const int *cum_weight
         out[j].fi = fi;
     }
     free(order);
-    free(tmp);
     return 0;
 }

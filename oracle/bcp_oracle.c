@@ -8,11 +8,17 @@
  * CPU baseline.  The product library (beegfs-chunk-parity_amd/lib/libbcp.so)
  * never links or calls it.
  *
- * Parity pinning: the reference's task_processing.c cannot be compiled in this
- * image (it includes <mpi.h>; MPI is absent and stand-in headers are not
- * allowed), so this restatement is pinned by the known-answer SHA-256 values
- * SURVEY.md §8(c) records from the unchanged reference (KAT-1..KAT-4); see
- * tests/test_oracle_kat.py and tests/golden/kats.json.
+ * Parity pinning: the reference's own xor_parity (task_processing.c:96-109,
+ * which needs only libc headers) is compiled unchanged into
+ * oracle/_ref/libref_xor.so (oracle/Makefile `ref`); its outputs are the 77
+ * xor_parity fixtures and the folds of the 4 parity-file fixtures in
+ * tests/golden/ref_xor.json, which this restatement must reproduce
+ * (tests/test_oracle_ref.py), and where _ref is built it is also compared with
+ * the reference function directly on random misaligned shapes.  The MPI roles
+ * around the fold (window assembly, padding, replay: task_processing.c:117-322)
+ * include <mpi.h>, which is absent (stand-in headers are not allowed), so
+ * that assembly is pinned by the survey's known-answer SHA-256 values
+ * (tests/test_oracle_kat.py, tests/golden/kats.json).
  *
  * Compiled with the reference's own flags (-std=gnu99 -Os, build.sh:8) so
  * that oracle_xor_parity doubles as the CPU baseline.

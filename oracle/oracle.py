@@ -61,6 +61,39 @@ def ref_lib():
     return _ref
 
 
+REF_PLAN_PATH = os.path.join(HERE, "_ref", "libref_plan.so")  # reference's own planner functions
+_ref_plan = None
+
+
+def ref_plan_lib():
+    """The reference's own planner functions (gen/main.c simple_hash, PCG32,
+    shuffle + qsort order, select_P, fill_in_missing_fields, get_store_weight;
+    file_info_hash.c fih_add_info; assign_lanes.c) compiled unchanged into
+    oracle/_ref/libref_plan.so by `make -C oracle ref`, or None where absent."""
+    global _ref_plan
+    if _ref_plan is None and os.path.exists(REF_PLAN_PATH):
+        L = ctypes.CDLL(REF_PLAN_PATH)
+        u64, i64, P = ctypes.c_uint64, ctypes.c_int64, ctypes.POINTER
+        sig = {
+            "ref_simple_hash": ([ctypes.c_char_p, ctypes.c_int], ctypes.c_uint),
+            "ref_sts_in_use": ([u64], ctypes.c_int),
+            "ref_pcg32": ([u64, u64, ctypes.c_uint32, P(ctypes.c_uint32), ctypes.c_int], None),
+            "ref_set_st_weight": ([P(ctypes.c_int), ctypes.c_int], None),
+            "ref_select_P": ([ctypes.c_char_p, u64, ctypes.c_uint], u64),
+            "ref_fill_in_missing_fields": ([u64, u64], u64),
+            "ref_fih_add_info": ([P(i64), P(u64), P(u64), ctypes.c_int, i64, ctypes.c_int], None),
+            "ref_sort_order": ([P(u64), ctypes.c_size_t, P(u64)], None),
+            "ref_plan_item": ([ctypes.c_char_p, i64, u64, u64, ctypes.c_int, i64, u64, ctypes.c_uint], u64),
+            "ref_store_weight": ([ctypes.c_int], ctypes.c_int),
+            "assign_lanes": ([ctypes.c_int, ctypes.c_ulonglong, ctypes.c_void_p, P(ctypes.c_int)], None),
+        }
+        for name, (args, res) in sig.items():
+            fn = getattr(L, name)
+            fn.argtypes, fn.restype = args, res
+        _ref_plan = L
+    return _ref_plan
+
+
 def ref_xor_parity(data: np.ndarray, nbytes: int, nsources: int) -> np.ndarray:
     """task_processing.c:96-109 itself (oracle/_ref); raises if not built."""
     L = ref_lib()

@@ -10,10 +10,16 @@ bcp_eventset_* / bcp_plan_worklist.
   worklist item     gen/main.c:768-791 (fill_in_missing_fields :92-100,
                     select_P :388-401)
 
-Pinning: PCG32 against the pcg32 reference demo's published first outputs
-(seed 42, sequence 54); the rest has no reference fixture and no runnable
-reference here (gen/main.c needs MPI and LevelDB) -- parity unpinned beyond
-this restatement.
+Pinning: every function above against tests/golden/ref_plan.json -- outputs
+of the reference's OWN simple_hash, PCG32, shuffle + qsort, select_P,
+fill_in_missing_fields, fih_add_info and assign_lanes, compiled unchanged from
+/root/reference into oracle/_ref/libref_plan.so (oracle/Makefile `ref`,
+tests/golden/make_ref_plan_golden.py; checked by tests/test_planner_ref.py);
+PCG32 also against the pcg32 demo's published first outputs (seed 42, seq 54).
+The sort is Python's stable sort: equal to glibc <= 2.36's qsort (a merge
+sort), which this image's reference build links.  The one deviation: where no
+non-holder target carries weight select_P returns the locations unchanged
+(the reference retries forever; fixtures never contain that case).
 """
 from __future__ import annotations
 

@@ -263,24 +263,27 @@ def test_fold_mode_rejects_unknown(bcp):
 def test_db_round_then_partial_round_then_rebuild(bcp, oracle, tmp_path, engine_kind):
     """A full gen round from chunk events (plan + DB replicas), a changelog
     round that recomputes only the modified stripe, then a rebuild walking
-    the DB -- on the device, with both engines."""
+    the DB -- on the device, with both engines.  The layout (holders, weights)
+    is tests/golden/ref_round.json's, and every file's parity must land on the
+    P target the REFERENCE'S OWN select_P picks for it (gen/main.c:388-401,
+    compiled unchanged; tests/golden/make_ref_plan_golden.py)."""
+    import json
     import planner as PL
+    fx = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "ref_round.json")))
     rng = np.random.default_rng(11)
-    root, nt = str(tmp_path), 9
+    root, nt = str(tmp_path), fx["ntargets"]
     S.make_store(root, nt)
-    cw = [1000 * (k + 1) for k in range(nt)]
-    streams, contents, files = {k: [] for k in range(nt)}, {}, {}
-    for i in range(24):
-        path = f"d{i % 4}/c{i}"
-        holders = sorted(int(x) for x in rng.choice(nt, size=8, replace=False))
-        lens = [int(x) for x in np.exp(rng.uniform(np.log(1024), np.log(3 << 20), size=8))]
+    cw = fx["cum_weight"]
+    streams, contents, files, ref_p = {k: [] for k in range(nt)}, {}, {}, {}
+    for i, (path, holders, loc) in enumerate(fx["files"]):
+        lens = [int(x) for x in np.exp(rng.uniform(np.log(1024), np.log(3 << 20), size=len(holders)))]
         arrs = []
         for h, L in zip(holders, lens):
             d = S.synthetic_chunk(i * 97 + h, L)
             S.write_chunk(root, h, path, d)
             streams[h].append((1000 + i, L, "m", path))
             arrs.append(d)
-        files[path], contents[path] = holders, arrs
+        files[path], contents[path], ref_p[path] = holders, arrs, PL.get_p(loc)
     pl = bcp.Pipeline() if engine_kind == "pipeline" else None
 
     def round_(streams):
@@ -298,11 +301,13 @@ def test_db_round_then_partial_round_then_rebuild(bcp, oracle, tmp_path, engine_
         placed = {k.decode(): loc for k, _, loc in db.items()}
         db.close()
         for path, holders in files.items():
-            p = PL.get_p(placed[path])
+            p = ref_p[path]
+            assert PL.get_p(placed[path]) == p, path  # the reference's placement
             assert S.read_file(S.parity_path(root, p, path)) == oracle.gen_parity_file(contents[path]), path
         # partial round: one chunk modified
         path = "d1/c5"
         h = files[path][2]
+        assert len(files[path]) > 2
         new = S.synthetic_chunk(4242, 777_777)
         S.write_chunk(root, h, path, new)
         contents[path][2] = new
