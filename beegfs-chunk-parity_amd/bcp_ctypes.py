@@ -88,7 +88,6 @@ _SIGS = {
     "bcp_event_sync": ([_V], ctypes.c_int),
     "bcp_event_query": ([_V], ctypes.c_int),
     "bcp_dev_alloc": ([_V, ctypes.c_size_t, ctypes.POINTER(_V)], ctypes.c_int),
-    "bcp_dev_alloc_hostwrite": ([_V, ctypes.c_size_t, ctypes.POINTER(_V)], ctypes.c_int),
     "bcp_dev_free": ([_V, _V], ctypes.c_int),
     "bcp_host_alloc": ([_V, ctypes.c_size_t, ctypes.POINTER(_V)], ctypes.c_int),
     "bcp_host_alloc_mapped": ([_V, ctypes.c_size_t, ctypes.POINTER(_V)], ctypes.c_int),
@@ -270,12 +269,6 @@ class Engine:
     def alloc(self, nbytes: int) -> int:
         p = _V()
         call("bcp_dev_alloc", self.h, nbytes, ctypes.byref(p))
-        return p.value
-
-    def alloc_hostwrite(self, nbytes: int) -> int:
-        """Device memory host code may WRITE (never read back) at this address."""
-        p = _V()
-        call("bcp_dev_alloc_hostwrite", self.h, nbytes, ctypes.byref(p))
         return p.value
 
     def free(self, ptr: int):
@@ -686,14 +679,14 @@ def set_xor_hook(fn_addr: int | None, ctx: int | None = None):
     lib().bcp_task_set_xor_hook(_V(fn_addr) if fn_addr else None, _V(ctx) if ctx else None)
 
 
-FOLD_ZERO_COPY, FOLD_STAGED, FOLD_BATCHED, FOLD_STREAMED, FOLD_DEVICE_ROWS, FOLD_PIPELINED = 0, 1, 2, 3, 4, 5
+FOLD_BATCHED, FOLD_PIPELINED = 2, 5
+PAD_AUTO = -1
 INJECT_FOLD_RES, INJECT_DRAIN_ROW, INJECT_SEND_BUF, INJECT_THREAD, INJECT_READ = 1, 2, 4, 8, 16
 INJECT_FOLD_SERVER = 32
 
 
 def set_fold_mode(mode: int) -> int:
-    """P-role fold: FOLD_PIPELINED (default), FOLD_BATCHED, FOLD_DEVICE_ROWS, FOLD_STREAMED, FOLD_ZERO_COPY or
-    FOLD_STAGED; returns the previous mode."""
+    """P-role fold: FOLD_PIPELINED (default) or FOLD_BATCHED; returns the previous mode."""
     rc = lib().bcp_task_set_fold_mode(mode)
     if rc < 0:
         raise BcpError("bcp_task_set_fold_mode", rc)
@@ -732,13 +725,17 @@ def pipe_stats() -> tuple:
     return w.value, r.value
 
 
-def set_explicit_padding(on: bool) -> bool:
-    """Sources zero-pad every window as the reference does (True) or send a
-    one-window gen chunk's bytes only (False, default); returns the previous."""
-    rc = lib().bcp_task_set_explicit_padding(int(bool(on)))
-    if rc < 0:
+def set_explicit_padding(on) -> int:
+    """The wire of a one-window gen task: True / 1 the reference's (every
+    window zero-padded), False / 0 implicit padding (a chunk's bytes only),
+    PAD_AUTO (default) implicit through libbcp's own transports and the
+    reference's through a caller's table; returns the previous setting
+    (PAD_AUTO, 0 or 1)."""
+    v = PAD_AUTO if on == PAD_AUTO else int(bool(on))
+    rc = lib().bcp_task_set_explicit_padding(v)
+    if rc < PAD_AUTO:
         raise BcpError("bcp_task_set_explicit_padding", rc)
-    return bool(rc)
+    return rc
 
 
 def task_shutdown():

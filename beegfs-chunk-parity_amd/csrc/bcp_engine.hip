@@ -555,87 +555,9 @@ extern "C" int bcp_dev_alloc(bcp_engine *eng, size_t bytes, void **dptr) {
   return 0;
 }
 
-// Device memory the HOST writes through the GPU's BAR (the P role's window
-// rows in BCP_FOLD_DEVICE_ROWS): uncached device memory, so the kernels read
-// what the CPU stored with no GPU-L2 line of an earlier use in the way.  The
-// fold kernel reads it at full HBM rate (6.2 TB/s, like hipMalloc'd memory);
-// CPU stores into it run at 23-33 GB/s per thread and ~45 GB/s in total (the
-// PCIe host-to-device direction); CPU LOADS from it run at ~25 MB/s, so
-// nothing on the host may read it back (profiles/r02/protocol/vram_rows*).
-//
-// These allocations are NEVER returned to HIP while the process lives:
-// bcp_dev_free parks them on a per-device list and the next request of the
-// same power-of-two class takes them back.  Returning them let the process
-// reuse their virtual addresses for other memory (host and device address
-// ranges interleave; profiles/r02/protocol/hostwrite_free*), and under churn
-// -- a fold pool switching row kinds, engines torn down and re-created --
-// later copies and kernels on OTHER buffers at those addresses read zeros or
-// stale bytes and one run ended in a GPU memory fault
-// (profiles/r02/protocol/pool_switch*).  Parked memory keeps every such
-// address owned by its first use.
-namespace {
-struct HostWrite {
-  HostWrite *next;
-  void *p;
-  size_t bytes;
-  int device;
-  int parked;
-};
-pthread_mutex_t g_hw_lock = PTHREAD_MUTEX_INITIALIZER;
-HostWrite *g_hw = nullptr;
-
-size_t hostwrite_class(size_t bytes) {
-  size_t c = (size_t)1 << 20;
-  while (c < bytes) c <<= 1;
-  return c;
-}
-
-// 1 if p is hostwrite memory (then parked for reuse).
-int park_hostwrite(void *p) {
-  pthread_mutex_lock(&g_hw_lock);
-  HostWrite *h = g_hw;
-  while (h && h->p != p) h = h->next;
-  if (h) h->parked = 1;
-  pthread_mutex_unlock(&g_hw_lock);
-  return h != nullptr;
-}
-}  // namespace
-
-extern "C" int bcp_dev_alloc_hostwrite(bcp_engine *eng, size_t bytes, void **dptr) {
-  if (!eng || !dptr) return -EINVAL;
-  *dptr = nullptr;
-  int rc = set_device(eng);
-  if (rc) return rc;
-  const size_t cls = hostwrite_class(bytes);
-  pthread_mutex_lock(&g_hw_lock);
-  for (HostWrite *h = g_hw; h; h = h->next)
-    if (h->parked && h->device == eng->device && h->bytes == cls) {
-      h->parked = 0;
-      *dptr = h->p;
-      break;
-    }
-  pthread_mutex_unlock(&g_hw_lock);
-  if (*dptr) return 0;
-  HostWrite *h = (HostWrite *)malloc(sizeof(HostWrite));
-  if (!h) return -ENOMEM;
-  if (hipExtMallocWithFlags(dptr, cls, hipDeviceMallocUncached) != hipSuccess) {
-    const hipError_t e = hipGetLastError();
-    free(h);
-    *dptr = nullptr;
-    return hip_to_errno(e);
-  }
-  *h = HostWrite{nullptr, *dptr, cls, eng->device, 0};
-  pthread_mutex_lock(&g_hw_lock);
-  h->next = g_hw;
-  g_hw = h;
-  pthread_mutex_unlock(&g_hw_lock);
-  return 0;
-}
-
 extern "C" int bcp_dev_free(bcp_engine *eng, void *dptr) {
   if (!eng) return -EINVAL;
   if (!dptr) return 0;
-  if (park_hostwrite(dptr)) return 0;
   set_device(eng);
   HIP_RC(hipFree(dptr));
   return 0;

@@ -42,25 +42,20 @@ void bcpi_sock_world_close_fds(bcp_sock_world *w);
 /* The whole arena of a world (every rank's slice); 0 if it has none. */
 int bcpi_sock_world_arena(const bcp_sock_world *w, void **lo, void **hi);
 
-/* Node fold server (bcp_task.c): ONE process holds the GPU and folds the
+/* Node fold server (bcp_foldsrv.c): ONE process holds the GPU and folds the
  * window rows of every rank process's P role, which live in the shared
- * arena, in batches across ranks (the fold service of BCP_FOLD_BATCHED,
- * fed over sockets); the ranks never start a HIP runtime.  The server runs
+ * arena, in batches across ranks (the fold service of bcp_fold.c, fed over
+ * sockets); the ranks never start a HIP runtime.  The server runs
  * bcpi_foldsrv_main over its ends of nconn connections (one thread each)
  * until every one is closed; a rank attaches its own connections. */
 int bcpi_foldsrv_main(int nconn, const int *fds, void *arena_lo, void *arena_hi);
 void bcpi_foldsrv_attach(int nconn, const int *fds);
 /* Windows the server folded for this process so far. */
 uint64_t bcpi_foldsrv_folds(void);
-/* A fill into another process's arena row is running on this thread: report
- * its final prefix (bcp_sock.c, PROG frames); 0 / -errno, -ENOTCONN if not. */
-int bcpi_fill_progress_on(void);
-int bcpi_fill_progress(size_t bytes, int redo);
-/* The receiving side: `bytes` leading bytes of the receive row `row` are
- * final (redo: bytes published before were replaced) -- bcp_task.c. */
-void bcpi_row_progress(const void *row, size_t bytes, int redo);
-/* 1 if a P role of this process follows the fill of row `row` (its watch). */
-int bcpi_row_watched(const void *row);
+/* 1 if ops is this library's socket transport (bcp_sock_world_attach). */
+int bcpi_sock_transport_is(const bcp_transport_ops *ops);
+/* The fold service's width (bcp_task_set_fold_inflight). */
+int bcpi_fold_inflight(void);
 /* Make [base, base + bytes) this process's arena slice (a memfd shared with
  * a node fold server, bcp_fold_server_connect). */
 void bcpi_arena_set(void *base, size_t bytes);

@@ -54,8 +54,6 @@
 #define FRAME_RTS 0x62637072u   /* "bcpr": fill send of len bytes wants a receive */
 #define FRAME_CTS 0x62637063u   /* "bcpc": {address, capacity} of the matched receive */
 #define FRAME_DONE 0x62637064u  /* "bcpd": {bytes} filled; completes the receive */
-#define FRAME_PROG 0x62637067u  /* "bcpg": {bytes, redo} of the fill are final (pipelined fold) */
-#define CTS_PROGRESS (UINT64_C(1) << 63) /* in the CTS capacity: the receiver follows the fill (PROG) */
 
 typedef struct {
     uint32_t magic;
@@ -525,7 +523,7 @@ static int send_cts(bcp_sock_world *w, int src, int tag, const void *addr, size_
         frame_hdr h;
         uint64_t pl[2];
     } f = {{FRAME_CTS, tag, 2 * sizeof(uint64_t)},
-           {(uint64_t)(uintptr_t)addr, (uint64_t)cap | (addr && bcpi_row_watched(addr) ? CTS_PROGRESS : 0)}};
+           {(uint64_t)(uintptr_t)addr, (uint64_t)cap}};
     pthread_mutex_lock(&w->ctl_mu[src]);
     int rc = write_all(fd, &f, sizeof(f));
     pthread_mutex_unlock(&w->ctl_mu[src]);
@@ -602,22 +600,6 @@ static int read_control(bcp_sock_world *w, int src, const frame_hdr *h)
         }
         pthread_mutex_unlock(&w->mu);
         return send_cts(w, src, h->tag, addr, cap); /* addr 0: the data comes as a message */
-    }
-    if (h->magic == FRAME_PROG) {
-        uint64_t pl[2];
-        if (h->len != sizeof(pl))
-            return -EPROTO;
-        if ((rc = read_all(fd, pl, sizeof(pl))))
-            return rc;
-        pthread_mutex_lock(&w->mu);
-        void *row = NULL;
-        for (sk_req *r = w->filling; r && !row; r = r->next)
-            if (r->src == src && r->tag == h->tag)
-                row = r->buf;
-        pthread_mutex_unlock(&w->mu);
-        if (row) /* the receive stays in `filling` until DONE: row is alive */
-            bcpi_row_progress(row, (size_t)pl[0], (int)pl[1]);
-        return 0;
     }
     if (h->magic == FRAME_DONE) {
         uint64_t n = 0;
@@ -796,28 +778,6 @@ static int send_zeros(bcp_sock_world *w, size_t n, int dst, int tag)
     return rc;
 }
 
-/* Progress of a fill into an arena row (a P role folding the window range by
- * range while it fills): the fill reports, between pieces, how many leading
- * bytes of the row are final; each report is a PROG frame on the data socket,
- * ahead of DONE, and the receiver hands it to bcpi_row_progress. */
-static __thread struct {
-    bcp_sock_world *w;
-    int dst, tag;
-} t_prog;
-
-int bcpi_fill_progress_on(void)
-{
-    return t_prog.w != NULL;
-}
-
-int bcpi_fill_progress(size_t bytes, int redo)
-{
-    if (!t_prog.w)
-        return -ENOTCONN;
-    const uint64_t pl[2] = {(uint64_t)bytes, (uint64_t)redo};
-    return send_frame(t_prog.w, t_prog.dst, FRAME_PROG, t_prog.tag, sizeof(pl), pl, sizeof(pl));
-}
-
 /* Fill send (rendezvous, see the top of the file): fill() writes the n-byte
  * payload straight into the receiver's arena row; a receive outside the
  * arena gets an ordinary message produced by fill() into a scratch buffer.
@@ -846,8 +806,7 @@ static int sk_send_fill(void *ctx, bcp_lb_fill_fn fill, void *fctx, size_t n, in
     }
     rc = progress_until(w, r);
     uint8_t *addr = (uint8_t *)(uintptr_t)r->cts_addr;
-    const int want_progress = (r->cts_cap & CTS_PROGRESS) != 0;
-    const size_t cap = (size_t)(r->cts_cap & ~CTS_PROGRESS);
+    const size_t cap = (size_t)r->cts_cap;
     free(r);
     if (rc)
         return rc;
@@ -871,11 +830,7 @@ static int sk_send_fill(void *ctx, bcp_lb_fill_fn fill, void *fctx, size_t n, in
         return -EPROTO;
     }
     if (n <= cap) {
-        t_prog.w = want_progress ? w : NULL; /* progress reports go to a receiver that follows the fill */
-        t_prog.dst = dst;
-        t_prog.tag = tag;
         frc = fill(fctx, addr, n);
-        t_prog.w = NULL;
     } else {
         /* truncated receive (MPI_ERR_TRUNCATE): produce all, keep cap */
         uint8_t *tmp = calloc(1, n);
@@ -919,6 +874,11 @@ static int sk_recv(void *ctx, void *buf, size_t n, int src, int tag)
     void *r = NULL;
     int rc = sk_irecv(ctx, buf, n, src, tag, &r);
     return rc ? rc : sk_wait(ctx, r);
+}
+
+int bcpi_sock_transport_is(const bcp_transport_ops *ops)
+{
+    return ops && ops->send == sk_send;
 }
 
 int bcp_sock_world_attach(bcp_sock_world *w, int rank, bcp_transport_ops *ops)

@@ -44,7 +44,7 @@ static int usage(void)
           "                      [--changelog DIR] <store_root> <ntargets>\n"
           "       bcp parity-rebuild [--pipeline|--procs] [--fold MODE] [--lanes N] [--db DIR] [--corrupt FILE]\n"
           "                          <store_root> <ntargets> <target>\n"
-          "       MODE: batched | pipelined | device-rows | streamed | zero-copy | staged\n",
+          "       MODE: pipelined (default) | batched\n",
           stderr);
     return 1;
 }
@@ -53,16 +53,8 @@ static int fold_mode_arg(const char *s)
 {
     if (!strcmp(s, "batched"))
         return BCP_FOLD_BATCHED;
-    if (!strcmp(s, "streamed"))
-        return BCP_FOLD_STREAMED;
-    if (!strcmp(s, "device-rows"))
-        return BCP_FOLD_DEVICE_ROWS;
     if (!strcmp(s, "pipelined"))
         return BCP_FOLD_PIPELINED;
-    if (!strcmp(s, "zero-copy"))
-        return BCP_FOLD_ZERO_COPY;
-    if (!strcmp(s, "staged"))
-        return BCP_FOLD_STAGED;
     return -1;
 }
 

@@ -111,12 +111,6 @@ int bcp_event_query(bcp_event *ev);
 /* ---- memory ----------------------------------------------------------- */
 int bcp_dev_alloc(bcp_engine *eng, size_t bytes, void **dptr);
 int bcp_dev_free(bcp_engine *eng, void *dptr);
-/* Device memory that host threads WRITE directly (uncached device memory
- * reached through the GPU's BAR; the P role's window rows under
- * BCP_FOLD_DEVICE_ROWS): kernels read it at HBM rate, host stores cross PCIe
- * once; host loads from it are very slow -- write only.  Freed with
- * bcp_dev_free. */
-int bcp_dev_alloc_hostwrite(bcp_engine *eng, size_t bytes, void **dptr);
 /* Pinned (page-locked) host memory for staging (registered huge-page memory
  * by default, option host_registered). */
 int bcp_host_alloc(bcp_engine *eng, size_t bytes, void **hptr);

@@ -98,64 +98,54 @@ int process_task(HostState *hs, const char *path, const FileInfo *fi, TaskInfo t
 /* Device used by the P role of storage target st: devices[st] if a map was
  * given, else st % device_count.  Engines are created lazily, one per device. */
 int bcp_task_set_device_map(const int *devices, int ntargets);
-/* How the P role folds a window on the GPU.  ZERO_COPY: the kernel reads the
- * pinned window rows (their data bytes) and writes the pinned parity block
- * in place over PCIe, one launch + one sync per window on the lane's own
- * queue.  STAGED: H2D of
- * the rows, kernel on device buffers, D2H (three commands per window).
+/* How the P role folds a window on the GPU (both read the pinned window rows
+ * in place over PCIe, data bytes only, and write the parity block in place).
  * BATCHED: the window is handed to the device's fold service (flat
  * combining, no thread of its own): a waiting lane leads a launch that folds
- * EVERY window the P roles of this process have pending as ONE descriptor
- * batch (zero-copy rows, data bytes only) and wakes each lane when its own
- * window is done (process_task stays synchronous per task, as the
- * reference's window loop is, task_processing.c:203-226).  Default:
- * PIPELINED (below).  Returns the previous mode, or -EINVAL. */
-#define BCP_FOLD_ZERO_COPY 0
-#define BCP_FOLD_STAGED 1
+ * EVERY window the P roles of this process (or, through the node fold
+ * server, of every rank process) have pending as ONE descriptor batch and
+ * wakes each lane when its own window is done (process_task stays
+ * synchronous per task, as the reference's window loop is,
+ * task_processing.c:203-226).
+ * PIPELINED (default): the fold follows the senders' reads.  The P role
+ * registers its window rows; a source filling one directly (the loopback
+ * transport's send_fill) reads its chunk in 256 KiB pieces and publishes
+ * each final prefix; the source whose piece completes a byte range of every
+ * row (at least 128 KiB and a quarter window) launches its fold on the lane's
+ * queue (no sync), so the rows' PCIe reads overlap the file reads; after the
+ * receives, the rest and one sync.  Windows it cannot follow (multi-window
+ * tasks, other transports, folds by a node fold server) go to the fold
+ * service as in BATCHED.
+ * Returns the previous mode, or -EINVAL. */
 #define BCP_FOLD_BATCHED 2
-/* STREAMED: as each source's window row arrives, its DATA bytes (a gen-mode
- * single-window row holds chunk_size bytes, the rest is the sender's zero
- * padding) are DMA'd to device memory on the lane's queue, overlapping the
- * rows still being read; after the last row one kernel folds the rows from
- * HBM (padding implicit, never transferred) straight into the pinned output
- * block, then one sync.  PCIe carries the chunk bytes once, not the padding. */
-#define BCP_FOLD_STREAMED 3
-/* DEVICE_ROWS: the window rows themselves live in device memory the host
- * writes through the GPU's BAR (bcp_dev_alloc_hostwrite): the senders' chunk
- * reads (or the transport's receive copies) store straight into HBM, so the
- * row bytes cross PCIe once, as CPU stores, while they arrive; the fold is
- * then an HBM-rate kernel (the fold service's batch, data bytes only) whose
- * output block goes to pinned host memory for the parity write.  No host
- * code reads the rows. */
-#define BCP_FOLD_DEVICE_ROWS 4
-/* PIPELINED: the fold follows the senders' reads.  The P role registers its
- * window rows; a source filling one directly (send_fill transports) reads
- * its chunk in 256 KiB pieces and publishes each final prefix; the source
- * whose piece completes a byte range of every row (at least 128 KiB and a
- * quarter window) launches its fold on the lane's queue (no sync), so the
- * rows' PCIe reads overlap the file reads;
- * after the receives, the rest and one sync.  Windows it cannot follow
- * (multi-window tasks, transports without send_fill) go to the fold service
- * as in BATCHED. */
 #define BCP_FOLD_PIPELINED 5
 int bcp_task_set_fold_mode(int mode);
 /* PIPELINED counters since the process started: windows folded by following
  * their rows, and range folds launched for them (ranges / windows > 1: the
  * fold overlapped the reads). */
 int bcp_task_pipe_stats(uint64_t *windows, uint64_t *ranges);
-/* on = 0 (default): in a gen task with ONE window a source sends its
- * chunk's bytes only and the P role supplies the zeros past them (implicit
- * padding).  on = 1: the reference's wire exactly -- every window
- * zero-padded to buffer_size (task_processing.c:302-303) -- for a job whose
- * P roles run the reference's parity_generator.  The P role of this library
- * takes either.  Returns the previous value or -EINVAL. */
+/* The wire of a gen task's single window (max_cs <= 10 MiB):
+ *   BCP_PAD_AUTO (default): implicit padding -- a source sends its chunk's
+ *     bytes only and the P role supplies the zeros past them -- when the
+ *     transport is one of this library's own (loopback ranks, socketpair rank
+ *     processes: every P role is this library's); the reference's wire
+ *     (every window zero-padded to buffer_size, task_processing.c:302-303)
+ *     through any table a caller installs with bcp_task_set_transport (an MPI
+ *     binding may reach the reference's parity_generator, which folds whole
+ *     rows);
+ *   0: implicit padding through every transport (a caller whose P roles are
+ *     all this library's);
+ *   1: the reference's wire through every transport.
+ * The P role of this library takes either.  Returns the previous value or
+ * -EINVAL. */
+#define BCP_PAD_AUTO (-1)
 int bcp_task_set_explicit_padding(int on);
-/* BATCHED mode: how many batches may be on a device at once (1..16, each
+/* The fold service: how many batches may be on a device at once (1..16, each
  * led by one waiting lane on its own queue; default 1: pure flat
  * combining).  Returns the
  * previous value or -EINVAL. */
 int bcp_task_set_fold_inflight(int k);
-/* Fold-service counters since the last shutdown (BATCHED mode): windows
+/* Fold-service counters since the last shutdown: windows
  * folded and launches issued (windows / launches = the batching achieved). */
 int bcp_task_fold_stats(uint64_t *windows, uint64_t *launches);
 /* Wall time spent per protocol phase, summed over every task of every lane

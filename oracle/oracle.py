@@ -61,6 +61,17 @@ def ref_lib():
     return _ref
 
 
+def cpu_fold_hook():
+    """(address, label) of the CPU fold the tools time inside libbcp's
+    protocol (a bcp_xor_hook_fn): the reference's OWN xor_parity
+    (task_processing.c:96-109 compiled unchanged, oracle/_ref ref_xor_rows)
+    where it was built, else this restatement's oracle_xor_rows."""
+    L = ref_lib()
+    if L is not None and hasattr(L, "ref_xor_rows"):
+        return ctypes.cast(L.ref_xor_rows, ctypes.c_void_p).value, "ref_xor_parity"
+    return ctypes.cast(lib().oracle_xor_rows, ctypes.c_void_p).value, "oracle_xor_rows"
+
+
 REF_PLAN_PATH = os.path.join(HERE, "_ref", "libref_plan.so")  # reference's own planner functions
 _ref_plan = None
 

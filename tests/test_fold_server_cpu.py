@@ -102,7 +102,7 @@ def test_connected_clients_fold_through_the_server(tmp_path, fold):
         d = json.loads(out.strip().splitlines()[-1])
         assert d["errors"] == 0 and d["rb_errors"] == 0 and d["bad"] == [], d
         # every window (a P role folding through a server takes whole windows
-        # in PIPELINED mode too, unless BCP_XPROC_PIPELINE)
+        # in PIPELINED mode too)
         assert d["server_folds"] > 40, d
     srv_out, _ = srv.communicate(timeout=60)
     assert srv.returncode == 0 and "served" in srv_out

@@ -23,12 +23,10 @@ def gpu_fold(bcp, engine):
     bcp.task_shutdown()
 
 
-@pytest.fixture(params=["pipelined", "device_rows", "streamed", "batched", "zero_copy", "staged"])
+@pytest.fixture(params=["pipelined", "batched"])
 def fold_mode(request, bcp):
-    """Every form of the P role's GPU fold (bcp_task_set_fold_mode)."""
-    mode = {"batched": bcp.FOLD_BATCHED, "zero_copy": bcp.FOLD_ZERO_COPY, "staged": bcp.FOLD_STAGED,
-            "streamed": bcp.FOLD_STREAMED, "device_rows": bcp.FOLD_DEVICE_ROWS,
-            "pipelined": bcp.FOLD_PIPELINED}[request.param]
+    """Both forms of the P role's GPU fold (bcp_task_set_fold_mode)."""
+    mode = {"batched": bcp.FOLD_BATCHED, "pipelined": bcp.FOLD_PIPELINED}[request.param]
     prev = bcp.set_fold_mode(mode)
     yield request.param
     bcp.set_fold_mode(prev)
@@ -204,14 +202,15 @@ def test_protocol_repeated_runs_reuse_pool(bcp, oracle, tmp_path):
         assert S.read_file(S.parity_path(root, p, path)) == oracle.gen_parity_file(contents[path])
 
 
-def test_zero_copy_pool_reuse_with_changing_data(bcp, oracle, tmp_path):
-    """The pooled window rows (mapped host memory, or device memory the host
-    writes) are rewritten between runs and the pool switches row kinds
-    between modes: no fold may see a previous task's bytes."""
+def test_pool_reuse_with_changing_data_and_teardown(bcp, oracle, tmp_path):
+    """The pooled window rows and outputs (registered host memory) are
+    rewritten between runs, the modes alternate, and every other round tears
+    the engines, fold services and pool down and builds them again (freed
+    memory's addresses are re-issued to new allocations), with a batched
+    pipeline run between: no fold may see a previous task's bytes."""
     root = str(tmp_path)
     rng = np.random.default_rng(77)
-    modes = [bcp.FOLD_ZERO_COPY, bcp.FOLD_DEVICE_ROWS, bcp.FOLD_STAGED, bcp.FOLD_DEVICE_ROWS, bcp.FOLD_PIPELINED,
-             bcp.FOLD_DEVICE_ROWS, bcp.FOLD_BATCHED, bcp.FOLD_PIPELINED]
+    modes = [bcp.FOLD_PIPELINED, bcp.FOLD_BATCHED] * 4
     for rnd, mode in enumerate(modes):
         files = [(f"z/{i}", [0, 1, 2], 3, [int(x) for x in rng.integers(1, 600_000, size=3)]) for i in range(24)]
         items, contents = S.populate(root, 4, files, seed=100 + rnd)
@@ -223,6 +222,11 @@ def test_zero_copy_pool_reuse_with_changing_data(bcp, oracle, tmp_path):
         assert st.errors == 0
         for (path, holders, p, lens) in files:
             assert S.read_file(S.parity_path(root, p, path)) == oracle.gen_parity_file(contents[path]), (rnd, path)
+        if rnd % 2:
+            bcp.task_shutdown()
+            assert bcp.pipeline_gen(root, 4, items).errors == 0
+            for (path, holders, p, lens) in files:
+                assert S.read_file(S.parity_path(root, p, path)) == oracle.gen_parity_file(contents[path]), (rnd, path)
 
 
 def test_pipelined_read_error_refold_on_device(bcp, oracle, tmp_path):
@@ -387,14 +391,14 @@ def test_rank_pool_on_device(tmp_path, mode):
     assert r.returncode == 0 and "pool ok" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]
 
 
-@pytest.mark.parametrize("engine_kind", ["protocol", "pipeline", "procs", "procs_device_rows"])
+@pytest.mark.parametrize("engine_kind", ["protocol", "pipeline", "procs", "procs_batched"])
 def test_cli_complete_partial_rebuild(bcp, oracle, tmp_path, engine_kind):
     """bin/bcp end to end on the device: --complete (scan of every target),
     --partial from changelog record files, then parity-rebuild from the DB --
     ranks as threads, the batched pipeline, or ranks as processes (--procs:
     one forked process per target on the socketpair transport, each with its
-    own HIP context, P roles folding with the streamed GPU fold, or with rows
-    in device memory that the socket receives write)."""
+    the node fold server holding the GPU for all of them, in the default fold
+    mode or batched)."""
     import subprocess
     import planner as PL
     rng = np.random.default_rng(21)
@@ -410,8 +414,8 @@ def test_cli_complete_partial_rebuild(bcp, oracle, tmp_path, engine_kind):
             S.write_chunk(root, h, path, d)
             arrs.append(d)
         files[path], contents[path] = holders, arrs
-    flags = {"protocol": [], "pipeline": ["--pipeline"], "procs": ["--procs", "--fold", "streamed"],
-             "procs_device_rows": ["--procs", "--fold", "device-rows"]}[engine_kind]
+    flags = {"protocol": [], "pipeline": ["--pipeline"], "procs": ["--procs"],
+             "procs_batched": ["--procs", "--fold", "batched"]}[engine_kind]
     r = subprocess.run([bcp.BIN_PATH, "parity-gen", "--complete", *flags, root, str(nt)], capture_output=True)
     assert r.returncode == 0, r.stderr
     db = bcp.PDB(os.path.join(root, "st0", "db"))

@@ -78,7 +78,7 @@ def gpu_protocol(bcp, engine):
     bcp.task_shutdown()
 
 
-@pytest.mark.parametrize("mode", ["pipelined", "device_rows", "streamed", "batched", "zero_copy", "staged", "pipeline"])
+@pytest.mark.parametrize("mode", ["pipelined", "batched", "pipeline"])
 @pytest.mark.parametrize("fx", GEN, ids=lambda c: c["name"])
 def test_parity_files_match_reference_folds(bcp, oracle, tmp_path, gpu_protocol, fx, mode):
     lens = fx["lens"]
@@ -92,8 +92,7 @@ def test_parity_files_match_reference_folds(bcp, oracle, tmp_path, gpu_protocol,
         S.write_chunk(root, k, "r/e/f", c)
     items = [("r/e/f", 2**40, S.with_p((1 << n) - 1, p))]
     prev = None if mode == "pipeline" else bcp.set_fold_mode(
-        {"batched": bcp.FOLD_BATCHED, "zero_copy": bcp.FOLD_ZERO_COPY, "staged": bcp.FOLD_STAGED,
-            "streamed": bcp.FOLD_STREAMED, "device_rows": bcp.FOLD_DEVICE_ROWS, "pipelined": bcp.FOLD_PIPELINED}[mode])
+        {"batched": bcp.FOLD_BATCHED, "pipelined": bcp.FOLD_PIPELINED}[mode])
     try:
         _gen_and_rebuild(bcp, root, nt, p, items, fx, mode)
     finally:

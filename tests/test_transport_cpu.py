@@ -363,8 +363,7 @@ def test_rank_processes_fill_into_shared_rows(bcp, oracle, cpu_hook, tmp_path, m
         assert arena == 0 and msg == 0 and srv == 0
     else:
         assert arena >= sum(len(h) for (_, h, _, _) in files[:-1]) and msg == 0
-        # with the server every window goes to it (the pipelined form across
-        # processes is opt-in, BCP_XPROC_PIPELINE): one per window of every
+        # with the server every window goes to it: one per window of every
         # stripe with a source (the 21 MiB one has 3)
         assert srv == (len([f for f in files if f[1]]) + 2 if server == "1" else 0)
     victim = 2
@@ -463,3 +462,24 @@ def test_rebuild_lanes(bcp, oracle, cpu_hook, tmp_path, procs):
     assert results[1] and results[1] == results[4]
     with pytest.raises(bcp.BcpError):
         bcp.set_rebuild_lanes(0)
+
+
+@pytest.mark.timeout(120)
+@pytest.mark.parametrize("pad,expect", [("auto", "foreign_wire ok"), ("implicit", "foreign_wire mismatch")])
+def test_foreign_transport_gets_the_reference_wire(bcp, tmp_path, pad, expect):
+    """libbcp senders through a caller's transport table (an MPI binding's
+    shape) to a P role shaped like the reference's parity_generator, which
+    folds whole buffer_size rows it never clears (task_processing.c:176-211):
+    by default (BCP_PAD_AUTO) the senders use the reference's zero-padded
+    windows (:302-303) through such a table and every parity is exact; with
+    implicit padding forced the stale row bytes are folded (the hazard)."""
+    exe = tmp_path / "fw"
+    lib = bcp.LIB_PATH
+    san = ["-fsanitize=address,undefined"] if "asan" in os.path.basename(lib) else []
+    subprocess.run(["gcc", "-std=gnu99", "-O1", "-Wall", "-Werror", "-pthread", *san, "-I",
+                    os.path.join(ROOT, "include"), "-o", str(exe),
+                    os.path.join(ROOT, "tests", "native", "foreign_wire_test.c"), lib,
+                    f"-Wl,-rpath,{os.path.dirname(lib)}"], check=True)
+    r = subprocess.run([str(exe), str(tmp_path / "store"), pad], capture_output=True, text=True, timeout=100)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.strip() == expect, r.stdout + r.stderr

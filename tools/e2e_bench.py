@@ -5,12 +5,16 @@ config 1 (BASELINE.json configs[0] shape): 4 storage targets as loopback
   ranks, 3-wide stripes with P rotating over the target left out, 1333 files
   -> ~1000 x 512 KiB chunk files per target.  Timed three ways over the same
   files: the per-rank protocol with the GPU fold (bcp_gen_run), the same
-  protocol with the reference's CPU fold (oracle_xor_rows as the fold hook)
-  in two forms -- the reference's P role (the whole window folded after
-  every row arrived, the parity opened before the first receive:
-  protocol_cpu_fold_reference) and that fold inside this protocol's
-  pipelined P role (source threads fold ranges as rows fill:
-  protocol_cpu_fold_pipelined) -- and the batched pipeline (bcp_pipeline_gen).
+  protocol with the reference's own CPU fold as the P role's fold hook (the
+  reference's xor_parity compiled unchanged, oracle/_ref ref_xor_rows, where
+  built; else the oracle's restatement, oracle_xor_rows -- the line names
+  which) in two forms -- folded like the reference's P role (the whole
+  window once every row has arrived, senders on the reference's zero-padded
+  wire: "reference fold in libbcp's protocol", protocol_cpu_fold_reference)
+  and the restated fold inside this protocol's pipelined P role (source
+  threads fold ranges as rows fill: protocol_cpu_fold_pipelined) -- and the
+  batched pipeline (bcp_pipeline_gen).  Neither CPU line is the reference
+  PROGRAM (its roles need MPI): the protocol around the fold is libbcp's.
   Then target 2 is lost and rebuilt through bcp_rebuild_run.
 config 5: 9 targets, 8-wide stripes, chunk sizes log-uniform in
   [64 KiB, 4 MiB] (not 16-byte rounded); full parity gen (pipeline), then a
@@ -47,19 +51,15 @@ KiB, MiB, GiB = 1024, 1024 ** 2, 1024 ** 3
 CPU_REF, CPU_PIPE = "protocol_cpu_fold_reference", "protocol_cpu_fold_pipelined"
 
 
-def fold_ctx(mode, hook, serial):
-    """Set a P-role fold (mode None: the default; serial: the reference's
-    protocol -- sources pad every window, the P role opens the parity before
-    the first receive, experiment knob BCP_TASK_SERIAL_IO); returns the
-    restore callable."""
+def fold_ctx(mode, hook, ref_wire):
+    """Set a P-role fold (mode None: the default; ref_wire: the senders pad
+    every window as the reference's do, task_processing.c:302-303); returns
+    the restore callable."""
     prev = bcp.set_fold_mode(mode) if mode is not None else None
     bcp.set_xor_hook(hook)
-    prev_pad = bcp.set_explicit_padding(True) if serial else None
-    if serial:
-        os.environ["BCP_TASK_SERIAL_IO"] = "1"
+    prev_pad = bcp.set_explicit_padding(True) if ref_wire else None
 
     def restore():
-        os.environ.pop("BCP_TASK_SERIAL_IO", None)
         if prev_pad is not None:
             bcp.set_explicit_padding(prev_pad)
         bcp.set_xor_hook(None)
@@ -142,20 +142,20 @@ def config1(a):
 
     # the per-task protocol with three folds, interleaved in rotating order
     # (one cold round, then a.reps warm ones) so host drift lands on all
-    ol = oracle.lib()
-    cpu_fold = ctypes.cast(ol.oracle_xor_rows, ctypes.c_void_p).value
+    ref_fold, ref_name = oracle.cpu_fold_hook()
+    pipe_fold = ctypes.cast(oracle.lib().oracle_xor_rows, ctypes.c_void_p).value  # takes ranges (any pitch)
     variants = [("protocol_gpu_fold(bcp_gen_run,12 lanes)", None, None, False),
-                ("protocol_gpu_fold_staged(H2D,kernel,D2H; 12 lanes)", bcp.FOLD_STAGED, None, False),
-                (CPU_REF + "(oracle_xor_rows,12 lanes)", bcp.FOLD_ZERO_COPY, cpu_fold, True),
-                (CPU_PIPE + "(oracle_xor_rows,12 lanes)", None, cpu_fold, False)]
+                ("protocol_gpu_fold_batched(12 lanes)", bcp.FOLD_BATCHED, None, False),
+                (CPU_REF + f"({ref_name},reference wire,12 lanes)", bcp.FOLD_BATCHED, ref_fold, True),
+                (CPU_PIPE + "(oracle_xor_rows,12 lanes)", None, pipe_fold, False)]
     times = {v[0]: [] for v in variants}
     ok = True
     preps = max(a.reps, 7)  # ~0.1 s runs: more rounds than the other measurements
     nv = len(variants)
     for r in range(1 + preps):
-        for label, mode, hook, serial in variants[r % nv:] + variants[:r % nv]:
+        for label, mode, hook, ref_wire in variants[r % nv:] + variants[:r % nv]:
             reset_parity()
-            restore = fold_ctx(mode, hook, serial)
+            restore = fold_ctx(mode, hook, ref_wire)
             try:
                 t0 = time.perf_counter()
                 st = bcp.gen_run(root, 4, items, nlanes=12)
@@ -221,17 +221,16 @@ def config1(a):
     # single lane, as rebuild/main.c, and 12 rebuild lanes (bcp_task_set_rebuild_lanes); the folds
     # interleaved in rotating order
     rvariants = [("rebuild_protocol_gpu_fold(bcp_rebuild_run)", None, None, False, 1),
-                 ("rebuild_protocol_gpu_fold_staged(bcp_rebuild_run)", bcp.FOLD_STAGED, None, False, 1),
-                 ("rebuild_" + CPU_REF + "(oracle_xor_rows)", bcp.FOLD_ZERO_COPY, cpu_fold, True, 1),
-                 ("rebuild_" + CPU_PIPE + "(oracle_xor_rows)", None, cpu_fold, False, 1),
+                 ("rebuild_" + CPU_REF + f"({ref_name})", bcp.FOLD_BATCHED, ref_fold, True, 1),
+                 ("rebuild_" + CPU_PIPE + "(oracle_xor_rows)", None, pipe_fold, False, 1),
                  ("rebuild_protocol_gpu_fold(bcp_rebuild_run,12 lanes)", None, None, False, 12),
-                 ("rebuild_" + CPU_REF + "(oracle_xor_rows,12 lanes)", bcp.FOLD_ZERO_COPY, cpu_fold, True, 12)]
+                 ("rebuild_" + CPU_REF + f"({ref_name},12 lanes)", bcp.FOLD_BATCHED, ref_fold, True, 12)]
     rtimes = {v[0]: [] for v in rvariants}
     nv = len(rvariants)
     for r in range(1 + preps):
-        for label, mode, hook, serial, lanes in rvariants[r % nv:] + rvariants[:r % nv]:
+        for label, mode, hook, ref_wire, lanes in rvariants[r % nv:] + rvariants[:r % nv]:
             drop_lost()
-            restore = fold_ctx(mode, hook, serial)
+            restore = fold_ctx(mode, hook, ref_wire)
             prev_lanes = bcp.set_rebuild_lanes(lanes)
             try:
                 t0 = time.perf_counter()
@@ -295,20 +294,20 @@ def config5(a):
     # full generation through the per-task protocol first (12 lanes), the
     # default GPU fold against the reference CPU fold, interleaved: 8 rows of
     # up to 4 MiB per window
-    ol = oracle.lib()
-    cpu_fold = ctypes.cast(ol.oracle_xor_rows, ctypes.c_void_p).value
+    ref_fold, ref_name = oracle.cpu_fold_hook()
+    pipe_fold = ctypes.cast(oracle.lib().oracle_xor_rows, ctypes.c_void_p).value
     pvariants = [("protocol_gpu_fold(bcp_gen_run,12 lanes)", None, None, False),
-                 (CPU_REF + "(oracle_xor_rows,12 lanes)", bcp.FOLD_ZERO_COPY, cpu_fold, True),
-                 (CPU_PIPE + "(oracle_xor_rows,12 lanes)", None, cpu_fold, False)]
+                 (CPU_REF + f"({ref_name},reference wire,12 lanes)", bcp.FOLD_BATCHED, ref_fold, True),
+                 (CPU_PIPE + "(oracle_xor_rows,12 lanes)", None, pipe_fold, False)]
     ptimes = {v[0]: [] for v in pvariants}
     preps = max(a.reps, 5)
     nv = len(pvariants)
     for r in range(1 + preps):
-        for label, mode, hook, serial in pvariants[r % nv:] + pvariants[:r % nv]:
+        for label, mode, hook, ref_wire in pvariants[r % nv:] + pvariants[:r % nv]:
             for k in range(ntargets):
                 shutil.rmtree(os.path.join(root, f"st{k}", "parity"), ignore_errors=True)
                 os.makedirs(os.path.join(root, f"st{k}", "parity"))
-            restore = fold_ctx(mode, hook, serial)
+            restore = fold_ctx(mode, hook, ref_wire)
             try:
                 t0 = time.perf_counter()
                 st = bcp.gen_run(root, ntargets, items, nlanes=12)

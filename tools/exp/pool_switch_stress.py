@@ -1,8 +1,10 @@
 #!/usr/bin/env python3
-"""Stress (tools/exp): the per-task protocol switching fold modes -- and so
-the pooled window rows between mapped host memory and device memory the host
-writes -- round after round (tests/test_gpu_protocol.py
-::test_zero_copy_pool_reuse_with_changing_data, longer).  On a mismatch it
+"""Stress (tools/exp): the per-task protocol switching fold modes round after
+round, optionally tearing the engines, fold services and row pool down after
+every round (--shutdown: freed memory's addresses are re-issued) and running
+the batched pipeline over the same files (--pipeline) -- the r02 fault
+hunt's run (tests/test_gpu_protocol.py
+::test_pool_reuse_with_changing_data_and_teardown, longer).  On a mismatch it
 describes the wrong bytes: ranges, zeros or not, and whether the got bytes
 equal the XOR of a subset of the sources (a source missing from the fold)."""
 import argparse
@@ -69,10 +71,8 @@ def main():
     a = ap.parse_args()
     bcp.set_xor_hook(None)
     rng = np.random.default_rng(77)
-    cycle = [bcp.FOLD_ZERO_COPY, bcp.FOLD_DEVICE_ROWS, bcp.FOLD_STAGED, bcp.FOLD_PIPELINED, bcp.FOLD_DEVICE_ROWS,
-             bcp.FOLD_BATCHED, bcp.FOLD_STREAMED, bcp.FOLD_PIPELINED]
-    names = {bcp.FOLD_ZERO_COPY: "zero_copy", bcp.FOLD_DEVICE_ROWS: "device_rows", bcp.FOLD_STAGED: "staged",
-             bcp.FOLD_BATCHED: "batched", bcp.FOLD_STREAMED: "streamed", bcp.FOLD_PIPELINED: "pipelined"}
+    cycle = [bcp.FOLD_PIPELINED, bcp.FOLD_BATCHED]
+    names = {bcp.FOLD_BATCHED: "batched", bcp.FOLD_PIPELINED: "pipelined"}
     fails = 0
     for rnd in range(a.rounds):
         mode = cycle[rnd % len(cycle)]

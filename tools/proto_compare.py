@@ -2,31 +2,25 @@
 """Per-task protocol (process_task over loopback ranks) with every P-role fold,
 interleaved in ONE run on ONE box:
 
-  gpu_batched    BCP_FOLD_BATCHED: the device's fold service batches the
-                 pending windows of every lane into one launch (default)
-  gpu_zero_copy  one zero-copy launch + sync per window on the lane's queue
-  gpu_staged     H2D -> kernel -> D2H per window
-  gpu_streamed   each row's data bytes DMA'd to HBM as it arrives, one kernel
-                 from HBM into the pinned output
-  gpu_pipelined  the fold follows the senders' reads: each range all rows
-                 have delivered is folded (by the source that completed it)
-                 while the rest is read; the P role folds the tail and syncs
-  gpu_device_rows  the rows themselves in device memory the host writes
-                 (BCP_FOLD_DEVICE_ROWS): chunk reads store into HBM through
-                 the BAR, the fold service's kernel reads HBM
-  cpu_reference  the reference's P role: its xor_parity restated
-                 (oracle_xor_rows) over the whole window once every row has
-                 arrived, sources padding every window, the parity chunk
-                 opened before the first receive (BCP_TASK_SERIAL_IO) -- the
-                 reference CPU path
-  cpu_pipelined  the same CPU fold inside this protocol's pipelined P role:
-                 the source threads fold ranges as the rows fill (what
-                 "cpu_reference" measured from r2an to r2bg)
+  gpu_pipelined  BCP_FOLD_PIPELINED (default): the fold follows the senders'
+                 reads -- each range all rows have delivered is folded (by
+                 the source that completed it) while the rest is read; the P
+                 role folds the tail and syncs
+  gpu_batched[K] BCP_FOLD_BATCHED: the device's fold service batches the
+                 pending windows of every lane into one launch (K batches in
+                 flight, default 4)
+  cpu_reference  the reference fold in libbcp's protocol: the reference's own
+                 xor_parity (task_processing.c:96-109 compiled unchanged,
+                 oracle/_ref ref_xor_rows; the restatement oracle_xor_rows
+                 where _ref was not built -- the line says which) over the
+                 whole window once every row has arrived, with the senders on
+                 the reference's zero-padded wire.  Not the reference PROGRAM:
+                 its roles need MPI; the protocol around the fold is libbcp's
+  cpu_pipelined  the restated CPU fold (oracle_xor_rows) inside this
+                 protocol's pipelined P role: the source threads fold ranges
+                 as the rows fill
   noop           a fold that does nothing: the bound of the protocol itself
                  (no parity is correct; not verified)
-  <fold>_serial  the same fold with the reference's I/O order in the P role
-                 (experiment knob BCP_TASK_SERIAL_IO): the parity chunk opened
-                 before the first receive (the padding stays implicit)
 
 Workloads: config 1 (4 targets, 1333 x 3-wide 512 KiB stripes, 12 lanes; gen,
 and rebuild of target 2 with the single rebuild lane) and config 5 (9
@@ -84,14 +78,6 @@ def noop_hook():
 
 def fold_setup(fold, hooks):
     """Returns a context restore callable."""
-    if fold.endswith("_serial"):
-        os.environ["BCP_TASK_SERIAL_IO"] = "1"  # read by the P role per task
-        inner = fold_setup(fold[:-len("_serial")], hooks)
-
-        def restore_serial():
-            inner()
-            os.environ.pop("BCP_TASK_SERIAL_IO", None)
-        return restore_serial
     if fold.startswith("gpu_batched"):
         # gpu_batched[K]: K concurrent batches (bcp_task_set_fold_inflight)
         k = int(fold[len("gpu_batched"):] or 4)
@@ -102,26 +88,26 @@ def fold_setup(fold, hooks):
             bcp.set_fold_mode(prev)
             bcp.set_fold_inflight(prev_k)
         return restore
-    if fold.startswith("gpu_"):
-        mode = {"gpu_batched": bcp.FOLD_BATCHED, "gpu_zero_copy": bcp.FOLD_ZERO_COPY,
-                "gpu_staged": bcp.FOLD_STAGED, "gpu_streamed": bcp.FOLD_STREAMED,
-                "gpu_device_rows": bcp.FOLD_DEVICE_ROWS, "gpu_pipelined": bcp.FOLD_PIPELINED}[fold]
-        prev = bcp.set_fold_mode(mode)
+    if fold == "gpu_pipelined":
+        prev = bcp.set_fold_mode(bcp.FOLD_PIPELINED)
         return lambda: bcp.set_fold_mode(prev)
     if fold == "cpu_reference":
-        prev = bcp.set_fold_mode(bcp.FOLD_ZERO_COPY)  # any non-pipelined mode: the hook folds whole windows
-        prev_pad = bcp.set_explicit_padding(True)
-        os.environ["BCP_TASK_SERIAL_IO"] = "1"
+        prev = bcp.set_fold_mode(bcp.FOLD_BATCHED)  # the hook folds whole windows after every row arrived
+        prev_pad = bcp.set_explicit_padding(True)  # the reference's wire
         bcp.set_xor_hook(hooks[fold])
 
         def restore_ref():
             bcp.set_xor_hook(None)
-            os.environ.pop("BCP_TASK_SERIAL_IO", None)
             bcp.set_explicit_padding(prev_pad)
             bcp.set_fold_mode(prev)
         return restore_ref
+    prev = bcp.set_fold_mode(bcp.FOLD_PIPELINED)
     bcp.set_xor_hook(hooks[fold])
-    return lambda: bcp.set_xor_hook(None)
+
+    def restore_hook():
+        bcp.set_xor_hook(None)
+        bcp.set_fold_mode(prev)
+    return restore_hook
 
 
 def measure(name, folds, rounds, run_once, verify_fn, nbytes, hooks, extra=None, prepare=None):
@@ -205,7 +191,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--root", default="/dev/shm/bcp_proto")
     ap.add_argument("--rounds", type=int, default=6)
-    ap.add_argument("--folds", default="gpu_pipelined,gpu_batched,gpu_zero_copy,cpu_reference,cpu_pipelined,noop")
+    ap.add_argument("--folds", default="gpu_pipelined,gpu_batched,cpu_reference,cpu_pipelined,noop")
     ap.add_argument("--workloads", default="c1_gen,c1_rebuild,c5_gen")
     ap.add_argument("--c1-files", type=int, default=1333)
     ap.add_argument("--c5-stripes", type=int, default=1000)
@@ -256,7 +242,8 @@ def main():
     folds = a.folds.split(",")
     bcp.set_rebuild_lanes(a.rebuild_lanes)
     noop = noop_hook()
-    hooks = {"cpu_reference": ctypes.cast(oracle.lib().oracle_xor_rows, ctypes.c_void_p).value,
+    ref_fold, ref_name = oracle.cpu_fold_hook()
+    hooks = {"cpu_reference": ref_fold,
              "cpu_pipelined": ctypes.cast(oracle.lib().oracle_xor_rows, ctypes.c_void_p).value,
              "noop": ctypes.cast(noop.noop_fold, ctypes.c_void_p).value}
     rng = np.random.default_rng(0)
@@ -265,7 +252,7 @@ def main():
     box = box_probe.cpu_info()
     if not (a.procs or a.procs_cold or a.fold_server):  # those keep the GPU out of this process
         box.update(box_probe.pcie_rates(bcp))
-    emit(box=box)
+    emit(box=box, cpu_reference_fold=ref_name)
     tr = {"transport": "socketpair rank processes, pooled" if a.procs else
           "socketpair rank processes, forked per run" if a.procs_cold else "loopback threads"}
     if a.fold_server:
@@ -287,7 +274,7 @@ def main():
                     hooks, {"lanes": a.lanes, **tr}, prepare=lambda: reset_parity(root, 4))
         if "c1_rebuild" in wl:
             # parity from a correct run, then rebuild target 2 again and again
-            bcp.set_xor_hook(hooks["cpu_reference"])
+            bcp.set_xor_hook(hooks["cpu_pipelined"])  # (takes ranges of any pitch)
             try:
                 reset_parity(root, 4)
                 gen(root, 4, items, nlanes=a.lanes)
