@@ -921,6 +921,35 @@ static void rank_command(const pool_cmd *c, int cmd_fd, int k, FILE *log, rank_r
     free(items);
 }
 
+/* In a child just forked from a possibly multithreaded caller: set an
+ * environment default without setenv, whose lock another thread of the
+ * parent may have held at the fork (only this thread exists in the child,
+ * and glibc's malloc is made usable again across fork).  The new environ
+ * array is the child's for the rest of its life. */
+static void child_env_default(const char *name, const char *value)
+{
+    extern char **environ;
+    if (getenv(name))
+        return;
+    size_t n = 0;
+    while (environ && environ[n])
+        n++;
+    char **env = malloc((n + 2) * sizeof(char *));
+    const size_t len = strlen(name) + strlen(value) + 2;
+    char *kv = malloc(len);
+    if (!env || !kv) {
+        free(env);
+        free(kv);
+        return;
+    }
+    snprintf(kv, len, "%s=%s", name, value);
+    for (size_t i = 0; i < n; i++)
+        env[i] = environ[i];
+    env[n] = kv;
+    env[n + 1] = NULL;
+    environ = env;
+}
+
 /* The body of rank process k+1 (never returns): serve commands until QUIT
  * or the caller's end closes. */
 static void rank_main(bcp_sock_world *w, int k, int cmd_fd, int res_fd, FILE *log, int nconn, const int *srv_fds)
@@ -933,8 +962,7 @@ static void rank_main(bcp_sock_world *w, int k, int cmd_fd, int res_fd, FILE *lo
      * needs two (a queue's compute and copy streams), so that is the default
      * unless the caller set GPU_MAX_HW_QUEUES; HIP reads it at its first call,
      * which comes after this in the rank. */
-    if (!getenv("GPU_MAX_HW_QUEUES"))
-        setenv("GPU_MAX_HW_QUEUES", "2", 1);
+    child_env_default("GPU_MAX_HW_QUEUES", "2");
     /* P-role rows inherited from the caller (host memory: the caller has no
      * HIP runtime here) go; this rank takes its rows from its arena slice */
     bcp_task_shutdown();
@@ -1043,8 +1071,7 @@ int bcp_rank_pool_create(int ntargets, FILE *log, bcp_rank_pool **out)
             for (int i = 0; i < made; i++)
                 close(rfd[i]);
             bcpi_sock_world_close_fds(w); /* the ranks' sockets: EOF must reach partners */
-            if (getenv("GPU_MAX_HW_QUEUES") == NULL)
-                setenv("GPU_MAX_HW_QUEUES", "4", 1);
+            child_env_default("GPU_MAX_HW_QUEUES", "4");
             bcpi_foldsrv_main(made, sfd, alo, ahi);
             _exit(0);
         }

@@ -216,18 +216,56 @@ static int in_arena(const void *p, size_t n)
 
 static sk_req g_sent; /* the completed request every isend returns (eager) */
 
+/* 2 * world * (world - 1) socket ends exist before fork (data + control): 57
+ * ranks need ~6,400 descriptors, beyond the usual soft limit of 1,024.  The
+ * soft limit is raised (no privilege needed) only as far as the worlds alive
+ * need -- their ends plus headroom for the caller's own -- and the caller's
+ * limit is restored when the last world is destroyed. */
+static pthread_mutex_t g_nofile_mu = PTHREAD_MUTEX_INITIALIZER;
+static int g_nofile_worlds;
+static size_t g_nofile_need;
+static struct rlimit g_nofile_saved;
+static int g_nofile_raised;
+
+static void nofile_raise(size_t ends)
+{
+    pthread_mutex_lock(&g_nofile_mu);
+    struct rlimit rl;
+    if (g_nofile_worlds++ == 0) {
+        g_nofile_need = 0;
+        g_nofile_raised = getrlimit(RLIMIT_NOFILE, &g_nofile_saved) == 0;
+    }
+    g_nofile_need += ends;
+    if (g_nofile_raised && getrlimit(RLIMIT_NOFILE, &rl) == 0) {
+        const rlim_t want = (rlim_t)(g_nofile_saved.rlim_cur + g_nofile_need + 256);
+        if (rl.rlim_cur < want) {
+            rl.rlim_cur = want < rl.rlim_max ? want : rl.rlim_max;
+            (void)setrlimit(RLIMIT_NOFILE, &rl);
+        }
+    }
+    pthread_mutex_unlock(&g_nofile_mu);
+}
+
+static void nofile_release(size_t ends)
+{
+    pthread_mutex_lock(&g_nofile_mu);
+    g_nofile_need -= ends < g_nofile_need ? ends : g_nofile_need;
+    if (--g_nofile_worlds == 0 && g_nofile_raised) {
+        struct rlimit rl;
+        if (getrlimit(RLIMIT_NOFILE, &rl) == 0) {
+            rl.rlim_cur = g_nofile_saved.rlim_cur;
+            (void)setrlimit(RLIMIT_NOFILE, &rl);
+        }
+        g_nofile_raised = 0;
+    }
+    pthread_mutex_unlock(&g_nofile_mu);
+}
+
 int bcp_sock_world_create(int world_size, bcp_sock_world **out)
 {
     if (!out || world_size < 1 || world_size > 4096)
         return -EINVAL;
-    /* 2 * world * (world - 1) socket ends before fork (data + control): 57
-     * ranks need ~6,400 descriptors, beyond the usual soft limit of 1,024;
-     * raise the soft limit to the hard one (no privilege needed) */
-    struct rlimit rl;
-    if (getrlimit(RLIMIT_NOFILE, &rl) == 0 && rl.rlim_cur < rl.rlim_max) {
-        rl.rlim_cur = rl.rlim_max;
-        (void)setrlimit(RLIMIT_NOFILE, &rl);
-    }
+    nofile_raise((size_t)2 * (size_t)world_size * (size_t)(world_size - 1));
     *out = NULL;
     bcp_sock_world *w = calloc(1, sizeof(*w));
     if (!w)
@@ -315,6 +353,7 @@ int bcp_sock_world_destroy(bcp_sock_world *w)
     }
     free(w->fds);
     free(w->cfds);
+    nofile_release((size_t)2 * (size_t)w->world * (size_t)(w->world - 1));
     free(w->send_mu);
     free(w->ctl_mu);
     free(w->reading);
@@ -758,8 +797,17 @@ static int sk_irecv(void *ctx, void *buf, size_t n, int src, int tag, void **req
     *req = r;
     if (rts) {
         free(m);
-        /* a sender waits for this answer (a failure shows as its dead socket) */
-        (void)send_cts(w, src, tag, fill ? buf : NULL, fill ? n : 0);
+        /* a sender waits for this answer; if it cannot be sent, the peer is
+         * failed here as the read path fails it (its sockets are unusable
+         * for this rendezvous): r completes with the error when waited for */
+        const int crc = send_cts(w, src, tag, fill ? buf : NULL, fill ? n : 0);
+        if (crc) {
+            pthread_mutex_lock(&w->mu);
+            if (!w->dead[src])
+                w->dead[src] = crc < 0 ? -crc : EIO;
+            pthread_cond_broadcast(&w->cv);
+            pthread_mutex_unlock(&w->mu);
+        }
     }
     return 0;
 }

@@ -355,7 +355,13 @@ int bcp_rebuild_run(const char *store_root, int ntargets, int rebuild_target, co
  * reports its counters to the caller through a pipe.  The calling process
  * must not have used the GPU yet (a forked child cannot use a HIP runtime
  * its parent initialised): -EBUSY if this library already did.  -ECHILD if a
- * rank process died. */
+ * rank process died.  Fork safety: the caller may be multithreaded; between
+ * fork and their work the children use only what survives fork in one
+ * thread (glibc's malloc, fresh mutexes, threads they create; environment
+ * defaults are set without setenv's lock) -- but a caller's OWN locks held
+ * by another thread at the fork (stdio on the log FILE, say) stay held in
+ * the children, so do not write to `log` from another thread while a pool
+ * is being created. */
 int bcp_gen_run_procs(const char *store_root, int ntargets, const bcp_work_item *items, size_t nitems,
                       int nlanes, const int *lanes, FILE *log, bcp_run_stats *stats);
 int bcp_rebuild_run_procs(const char *store_root, int ntargets, int rebuild_target, const bcp_work_item *items,

@@ -19,8 +19,21 @@ import pytest
 import planner as PL
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-DOC = json.load(open(os.path.join(HERE, "golden", "ref_plan.json")))
 U64 = (1 << 64) - 1
+
+
+class _Doc:
+    """tests/golden/ref_plan.json, read on first use (CPU tests only: the
+    file stays off the GPU box, so collection must not need it)."""
+    _d = None
+
+    def __getitem__(self, k):
+        if _Doc._d is None:
+            _Doc._d = json.load(open(os.path.join(HERE, "golden", "ref_plan.json")))
+        return _Doc._d[k]
+
+
+DOC = _Doc()
 
 
 def _plan_product(bcp, case):
