@@ -119,6 +119,7 @@ _SIGS = {
     "bcp_task_set_xor_hook": ([_V, _V], None),
     "bcp_task_set_fold_mode": ([ctypes.c_int], ctypes.c_int),
     "bcp_task_set_explicit_padding": ([ctypes.c_int], ctypes.c_int),
+    "bcp_task_watch_live": ([], ctypes.c_size_t),
     "bcp_task_pipe_stats": ([ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)], ctypes.c_int),
     "bcp_task_set_fold_inflight": ([ctypes.c_int], ctypes.c_int),
     "bcp_task_fold_stats": ([ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)], ctypes.c_int),

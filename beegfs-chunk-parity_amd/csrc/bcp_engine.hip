@@ -52,6 +52,8 @@ struct DescSlot {
   bool used = false;
   DescTile *tiles = nullptr;    // this slot's tile records (desc_tiles -> xor_desc)
   size_t tiles_cap = 0;         // in records
+  uint64_t rec_key = 0;         // desc_reuse_records: the staged tables the records were made from
+  bool rec_ok = false;
 };
 
 }  // namespace
@@ -338,6 +340,7 @@ extern "C" int bcp_set_option(bcp_engine *eng, const char *key, int value) {
   else if (!strcmp(key, "stream_grab") && value >= 0 && value <= 64) eng->tuning.stream_grab = value;
   else if (!strcmp(key, "sync_mode") && (value == 0 || value == 1)) eng->tuning.sync_mode = value;
   else if (!strcmp(key, "host_registered") && (value == 0 || value == 1)) eng->tuning.host_registered = value;
+  else if (!strcmp(key, "desc_reuse_records") && (value == 0 || value == 1)) eng->tuning.desc_reuse_records = value;
   else if (!strcmp(key, "desc_pipe") && (value == 0 || value == 2 || value == 4 || value == 5 || value == 6))
     eng->tuning.desc_pipe = value;
   else if (!strcmp(key, "desc_table_host_max") && value >= 0 && value <= (1 << 24))
@@ -373,6 +376,7 @@ extern "C" int bcp_get_option(bcp_engine *eng, const char *key, int *value) {
   else if (!strcmp(key, "stream_grab")) *value = t.stream_grab;
   else if (!strcmp(key, "sync_mode")) *value = t.sync_mode;
   else if (!strcmp(key, "host_registered")) *value = t.host_registered;
+  else if (!strcmp(key, "desc_reuse_records")) *value = t.desc_reuse_records;
   else if (!strcmp(key, "desc_table_host_max")) *value = t.desc_table_host_max;
   else if (!strcmp(key, "last_stream_vecs")) *value = eng->last_stream_vecs.load(std::memory_order_relaxed);
   else if (!strcmp(key, "last_desc_vecs")) *value = eng->last_desc_vecs.load(std::memory_order_relaxed);
@@ -951,6 +955,15 @@ static int submit_desc(bcp_queue *q, const bcp_stripe *stripes, uint32_t nstripe
   }
   const uint32_t acc = (uint32_t)acc64;
   ts[nstripes] = acc;
+  // desc_reuse_records: the same tables on this slot as last time -> its records stand
+  uint64_t key = 0;
+  if (e->tuning.desc_reuse_records) {
+    key = 1469598103934665603ull ^ ((uint64_t)acc << 32) ^ tile_bytes ^ ((uint64_t)vecs << 20);
+    const uint64_t *w = (const uint64_t *)h;
+    for (size_t i = 0; i < bytes / 8; i++) key = (key ^ w[i]) * 1099511628211ull;
+  }
+  const bool reuse = e->tuning.desc_reuse_records && slot->rec_ok && slot->rec_key == key && slot->tiles_cap >= acc;
+  slot->rec_ok = false;
   if (slot->tiles_cap < acc) {
     // the slot's previous kernels have finished (ring_acquire waited)
     if (slot->tiles) HIP_RC(hipFree(slot->tiles));
@@ -971,7 +984,9 @@ static int submit_desc(bcp_queue *q, const bcp_stripe *stripes, uint32_t nstripe
   char *d = nullptr;
   // Host-resident tables only when desc_tiles alone reads them: the general
   // and wide tile paths read them again per tile.
-  if ((rc = stage_tables(q, slot, bytes, plain ? (size_t)e->tuning.desc_table_host_max : 0, &d, !side))) return rc;
+  const size_t host_max = plain ? (size_t)e->tuning.desc_table_host_max : 0;
+  if (reuse) d = bytes <= host_max ? (char *)slot->host : (char *)slot->dev;  // uploaded last time, unchanged
+  else if ((rc = stage_tables(q, slot, bytes, host_max, &d, !side))) return rc;
   DescBatch b;
   b.stripes = (const bcp_stripe *)d;
   b.sources = (const bcp_source *)(d + off_src);
@@ -986,7 +1001,8 @@ static int submit_desc(bcp_queue *q, const bcp_stripe *stripes, uint32_t nstripe
   b.base = q->qbase;
   if (q->broken) return -EIO;
   (void)hipGetLastError();  // see launch_stream
-  if (side) {
+  if (reuse) {
+  } else if (side) {
     if (!q->copy_stream) HIP_RC(hipStreamCreateWithFlags(&q->copy_stream, hipStreamNonBlocking));
     HIP_RC(launch_desc_tiles(q->copy_stream, b));
     HIP_RC(hipEventRecord(slot->copied, q->copy_stream));
@@ -1004,6 +1020,8 @@ static int submit_desc(bcp_queue *q, const bcp_stripe *stripes, uint32_t nstripe
   if (rc) return rc;
   HIP_RC(hipEventRecord(slot->done, q->stream));
   slot->used = true;
+  slot->rec_key = key;
+  slot->rec_ok = e->tuning.desc_reuse_records != 0;
   return 0;
 }
 

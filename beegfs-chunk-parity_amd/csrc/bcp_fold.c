@@ -485,6 +485,11 @@ int bcp_task_pipe_stats(uint64_t *windows, uint64_t *ranges)
     return 0;
 }
 
+size_t bcp_task_watch_live(void)
+{
+    return __atomic_load_n(&g_watch_live, __ATOMIC_ACQUIRE);
+}
+
 static size_t watch_hash(const void *p)
 {
     uint64_t x = (uint64_t)(uintptr_t)p;

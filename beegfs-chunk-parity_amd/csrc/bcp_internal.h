@@ -58,6 +58,10 @@ struct Tuning {
     // registered with HIP (CPU copies into and out of it run at malloc speed),
     // 0 = hipHostMalloc.
     int host_registered = 1;
+    // xor_desc: a batch resubmitted on a ring slot with byte-identical staged
+    // tables reuses that slot's tile records (no table upload, no desc_tiles):
+    // the A/B of desc_tiles' concurrent HBM traffic (tools/exp/desc_records_ab.py).
+    int desc_reuse_records = 0;
 };
 
 // Arguments of the streaming kernel (xor_stream).

@@ -124,6 +124,12 @@ int bcp_task_set_fold_mode(int mode);
  * their rows, and range folds launched for them (ranges / windows > 1: the
  * fold overlapped the reads). */
 int bcp_task_pipe_stats(uint64_t *windows, uint64_t *ranges);
+/* Row watches registered right now (PIPELINED windows between their first
+ * receive and their fold): 0 whenever no task runs -- a watch that outlived
+ * its window would let a later fill into memory at the same address publish
+ * to a dead P role (tests check it after every pipelined run, failures and
+ * drains included). */
+size_t bcp_task_watch_live(void);
 /* The wire of a gen task's single window (max_cs <= 10 MiB):
  *   BCP_PAD_AUTO (default): implicit padding -- a source sends its chunk's
  *     bytes only and the P role supplies the zeros past them -- when the

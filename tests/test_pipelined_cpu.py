@@ -24,6 +24,30 @@ def pipelined(bcp, cpu_hook):
     bcp.set_fold_mode(prev)
     bcp.inject_failure(bcp.INJECT_READ, 0, 0)
     bcp.set_transport(None)
+    # every row watch ended with its window (successful, failed or drained):
+    # none may outlive it into memory a later task reuses
+    assert bcp.lib().bcp_task_watch_live() == 0
+
+
+@pytest.mark.timeout(120)
+def test_row_watches_end_with_their_windows_on_failures(bcp, oracle, tmp_path):
+    """Watches are removed on every path out of a pipelined window: fold
+    resources missing (the P role drains), a read error mid-row, and normal
+    completion -- then a run over the same (pooled) rows folds correctly."""
+    root = str(tmp_path)
+    files = [(f"q/{i}", [0, 1, 2], 3, [64 * KiB * (i + 1), 7, 300 * KiB]) for i in range(6)]
+    items, contents = S.populate(root, 4, files, seed=9)
+    bcp.inject_failure(bcp.INJECT_FOLD_RES, 2, 1)
+    assert bcp.gen_run(root, 4, items, nlanes=2).errors >= 1
+    bcp.inject_failure(bcp.INJECT_FOLD_RES, 0, 0)
+    assert bcp.lib().bcp_task_watch_live() == 0
+    bcp.inject_failure(bcp.INJECT_READ, 1, 1)
+    assert bcp.gen_run(root, 4, items, nlanes=2).errors >= 1
+    bcp.inject_failure(bcp.INJECT_READ, 0, 0)
+    assert bcp.lib().bcp_task_watch_live() == 0
+    assert bcp.gen_run(root, 4, items, nlanes=2).errors == 0
+    for (path, holders, p, lens) in files:
+        assert S.read_file(S.parity_path(root, p, path)) == oracle.gen_parity_file(contents[path]), path
 
 
 def _files(rng, nt, nfiles, hi):
