@@ -433,6 +433,48 @@ def test_large_mixed_batch_side_stream_tiles(oracle, engine, dev, queue, side, a
         assert np.array_equal(x, r) and np.array_equal(y, r), i
 
 
+def test_reused_tile_records_follow_data_and_table_changes(oracle, engine, dev, queue):
+    """desc_reuse_records (the desc_tiles A/B option): a batch resubmitted with
+    identical tables on a ring slot folds from that slot's records -- the
+    records hold addresses, so new input bytes are still folded -- and any
+    change of the tables (here an output length) makes records afresh."""
+    rng = np.random.default_rng(313)
+    stripes, chunks_all = [], []
+    for _ in range(60):
+        lens = [int(x) for x in np.exp(rng.uniform(np.log(64 * KiB), np.log(4 * MiB), size=8))]
+        chunks_all.append([rng.integers(0, 256, size=L, dtype=np.uint8) for L in lens])
+    descs, sources, outs = [], [], []
+    for chunks in chunks_all:
+        first = len(sources)
+        for c in chunks:
+            sources.append((dev.put(c), len(c)))
+        m = max(len(c) for c in chunks)
+        dptr = dev.alloc(m + 32)
+        outs.append((dptr, m))
+        descs.append((dptr, m, first, len(chunks), 0))
+    prev = engine.option("desc_reuse_records")
+    engine.option("desc_reuse_records", 1)
+    try:
+        for rnd in range(10):  # 4 ring slots: from the 5th launch on, records are reused
+            if rnd == 7:  # new bytes in one source: the reused records must fold them
+                chunks_all[3][2] = rng.integers(0, 256, size=len(chunks_all[3][2]), dtype=np.uint8)
+                queue.h2d(sources[3 * 8 + 2][0], chunks_all[3][2])
+            d = list(descs)
+            if rnd == 9:  # a changed table: out_len of stripe 5 shortened
+                dptr, m, first, n, w = d[5]
+                d[5] = (dptr, m - 4097, first, n, w)
+            for o, n in outs:
+                queue.memset(o, 0xA5, n)
+            queue.xor_stripes(d, sources)
+            queue.sync()
+            for i, (o, n) in enumerate(outs):
+                n_i = d[i][1]
+                ref = oracle.xor_padded_np(chunks_all[i])[:n_i]
+                assert np.array_equal(dev.get(o, n_i), ref), (rnd, i)
+    finally:
+        engine.option("desc_reuse_records", prev)
+
+
 @pytest.mark.parametrize("n", [9, 12, 20, 56])
 def test_descriptor_wide_stripes(oracle, dev, queue, n):
     """Stripes wider than a tile record holds (> 8 sources reaching into a
@@ -745,6 +787,7 @@ KNOBS = {
     "stream_grab": (0, [0, 1, 64], [-1, 65]),
     "sync_mode": (0, [0, 1], [2]),
     "host_registered": (1, [0, 1], [2]),
+    "desc_reuse_records": (0, [0, 1], [2, -1]),
 }
 
 
