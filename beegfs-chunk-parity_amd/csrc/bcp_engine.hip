@@ -284,14 +284,8 @@ extern "C" int bcp_engine_create(int device, bcp_engine **out) {
   e->device = device;
   e->num_cus = prop.multiProcessorCount;
   snprintf(e->name, sizeof(e->name), "%s (%s)", prop.name, prop.gcnArchName);
-  if (const char *v = getenv("BCP_BLOCKS_PER_CU")) e->tuning.blocks_per_cu = atoi(v);
-  if (const char *v = getenv("BCP_VECS_PER_THREAD")) e->tuning.vecs_per_thread = atoi(v);
-  const Tuning defaults;
-  if (e->tuning.blocks_per_cu < 1 || e->tuning.blocks_per_cu > 32) e->tuning.blocks_per_cu = defaults.blocks_per_cu;
-  if (e->tuning.vecs_per_thread && !stream_vecs_ok(e->tuning.vecs_per_thread))
-    e->tuning.vecs_per_thread = defaults.vecs_per_thread;
-  if (const char *v = getenv("BCP_SCHEDULE")) e->tuning.schedule = atoi(v) == kSchedStatic ? kSchedStatic : kSchedQueue;
-  if (const char *v = getenv("BCP_SYNC_MODE")) e->tuning.sync_mode = atoi(v) == 1 ? 1 : 0;
+  // (engine options are set with bcp_set_option; the one environment default
+  // left is the host memory kind, for processes a caller cannot reach: ranks)
   if (const char *v = getenv("BCP_HOST_REGISTERED")) e->tuning.host_registered = atoi(v) ? 1 : 0;
   *out = e;
   return 0;
@@ -646,23 +640,14 @@ int free_registered(void *p) {
 // the per-task protocol lost ~40 % with the CPU fold itself unchanged
 // (config 5, same box, same run: 14.8-18.2 against 24.8-29.7 GiB/s over
 // ordinary memory; profiles/r02/protocol/host_kind_ab*.jsonl).  Falls back to
-// hipHostMalloc.  Experiment knob BCP_MAPPED_FLAGS: 0 hipHostMalloc coherent,
-// 1 non-coherent, 2 coherent + NUMA placement by the calling thread's
-// policy, 3 non-coherent + NUMA by policy, 4 registered.
+// hipHostMalloc (coherent, mapped).
 extern "C" int bcp_host_alloc_mapped(bcp_engine *eng, size_t bytes, void **hptr) {
   if (!eng || !hptr) return -EINVAL;
   *hptr = nullptr;
   int rc = set_device(eng);
   if (rc) return rc;
-  unsigned flags = hipHostMallocMapped | hipHostMallocCoherent;
-  int registered = eng->tuning.host_registered;
-  if (const char *v = getenv("BCP_MAPPED_FLAGS")) {
-    const int k = atoi(v);
-    registered = k == 4;
-    flags = hipHostMallocMapped | ((k & 1) ? hipHostMallocNonCoherent : hipHostMallocCoherent) |
-            ((k & 2) ? hipHostMallocNumaUser : 0u);
-  }
-  if (registered && alloc_registered(bytes ? bytes : 16, hptr) == 0) return 0;
+  const unsigned flags = hipHostMallocMapped | hipHostMallocCoherent;
+  if (eng->tuning.host_registered && alloc_registered(bytes ? bytes : 16, hptr) == 0) return 0;
   HIP_RC(hipHostMalloc(hptr, bytes ? bytes : 16, flags));
   return 0;
 }

@@ -209,7 +209,7 @@ int bcp_set_tuning(bcp_engine *eng, int blocks_per_cu, int vecs_per_thread);
  * per unit), "stream_grab" (tiles per
  * work-queue grab of the streaming kernel for stripes of 1-4 sources, 1..64;
  * 0 = the default, 2), "sync_mode" (bcp_queue_sync: 0 = hipStreamSynchronize,
- * the default; 1 = wait on a blocking-sync event; env BCP_SYNC_MODE),
+ * the default; 1 = wait on a blocking-sync event),
  * "host_registered" (bcp_host_alloc / bcp_host_alloc_mapped: 1 = ordinary
  * huge-page memory registered with HIP, the default -- CPU copies into and
  * out of it run at malloc speed; 0 = hipHostMalloc; env BCP_HOST_REGISTERED). */

@@ -7,7 +7,7 @@
 # profiles/<round>/final/ with provenance (commit, files).
 set -o pipefail
 R=$GRAFT_REPO_ROOT; cd $R
-T=${PROF_TAG:-r02}
+T=${PROF_TAG:-r03}
 O=$R/gpurun_out/prof_$T
 mkdir -p $O
 timeout -k 10 300 python -u bench.py > $O/bench_gen.json 2> $O/bench_gen.err || { echo BENCH_FAIL; exit 1; }
