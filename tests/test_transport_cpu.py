@@ -483,3 +483,32 @@ def test_foreign_transport_gets_the_reference_wire(bcp, tmp_path, pad, expect):
     r = subprocess.run([str(exe), str(tmp_path / "store"), pad], capture_output=True, text=True, timeout=100)
     assert r.returncode == 0, r.stdout + r.stderr
     assert r.stdout.strip() == expect, r.stdout + r.stderr
+
+
+def test_sock_world_raises_nofile_only_as_needed_and_restores_it(bcp):
+    """bcp_sock_world_create raises the soft RLIMIT_NOFILE only as far as the
+    live worlds' socket ends need (not to the hard limit), and the last
+    bcp_sock_world_destroy restores the caller's limit."""
+    import ctypes
+    import resource
+    L = bcp.lib()
+    L.bcp_sock_world_create.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]
+    L.bcp_sock_world_destroy.argtypes = [ctypes.c_void_p]
+    soft0, hard = resource.getrlimit(resource.RLIMIT_NOFILE)
+    low = min(soft0, 1024)
+    resource.setrlimit(resource.RLIMIT_NOFILE, (low, hard))
+    try:
+        worlds = []
+        for n in (30, 20):  # 2*30*29 + 2*20*19 ends: beyond 1,024
+            w = ctypes.c_void_p()
+            assert L.bcp_sock_world_create(n, ctypes.byref(w)) == 0
+            worlds.append(w)
+        soft1, _ = resource.getrlimit(resource.RLIMIT_NOFILE)
+        need = 2 * 30 * 29 + 2 * 20 * 19
+        assert soft1 >= min(hard, low + need)
+        assert soft1 <= low + need + 256 or hard <= low + need + 256
+        for w in worlds:
+            assert L.bcp_sock_world_destroy(w) == 0
+        assert resource.getrlimit(resource.RLIMIT_NOFILE)[0] == low
+    finally:
+        resource.setrlimit(resource.RLIMIT_NOFILE, (soft0, hard))
