@@ -61,15 +61,17 @@ def test_bench_torchrun_two_ranks_labels(bcp):
 
 
 @pytest.mark.timeout(500)
-def test_bench_gpus_n_launches_its_own_ranks(bcp):
+@pytest.mark.parametrize("n", [2, 4])
+def test_bench_gpus_n_launches_its_own_ranks(bcp, n):
     """The driver's form, `python3 bench.py --gpus N` with no launcher: bench.py
     starts N ranks itself.  With fewer GPUs than N it refuses (non-zero exit,
     no line) unless --allow-shared, which reports the ranks and the distinct GPUs."""
     ndev = bcp.device_count()
     env = dict(os.environ, MASTER_ADDR="127.0.0.1")
     env.pop("WORLD_SIZE", None)
-    args = [sys.executable, "bench.py", "--gpus", "2", "--stripes", "64", "--steps", "2", "--warmup", "1", "--no-cpu"]
-    if ndev < 2:
+    args = [sys.executable, "bench.py", "--gpus", str(n), "--stripes", "64", "--steps", "2", "--warmup", "1",
+            "--no-cpu"]
+    if ndev < n:
         r = subprocess.run(args, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
         assert r.returncode == 4, (r.returncode, r.stdout[-2000:], r.stderr[-2000:])
         assert "refusing" in r.stderr
@@ -77,7 +79,10 @@ def test_bench_gpus_n_launches_its_own_ranks(bcp):
     r = subprocess.run(args + ["--allow-shared"], cwd=ROOT, env=env, capture_output=True, text=True, timeout=420)
     assert r.returncode == 0, (r.returncode, r.stdout[-2000:], r.stderr[-4000:])
     line = _last_json(r.stdout)
-    assert line["config"]["ranks"] == 2
-    assert line["n_gpus"] == min(ndev, 2)
-    assert line["config"]["shared_gpu"] is (ndev < 2)
+    assert line["config"]["ranks"] == n
+    assert line["n_gpus"] == min(ndev, n)
+    assert line["config"]["shared_gpu"] is (ndev < n)
     assert line["config"]["verified_on_device"] is True
+    assert line["config"]["bytes_per_step_per_gpu"] * n * line["steps"] / 2**30 / (line["ms_per_step"] *
+                                                                                   line["steps"] * 1e-3) == \
+        pytest.approx(line["value"], rel=1e-3)  # value = the whole job's bytes / the slowest rank's time
