@@ -85,4 +85,4 @@ def test_bench_gpus_n_launches_its_own_ranks(bcp, n):
     assert line["config"]["verified_on_device"] is True
     assert line["config"]["bytes_per_step_per_gpu"] * n * line["steps"] / 2**30 / (line["ms_per_step"] *
                                                                                    line["steps"] * 1e-3) == \
-        pytest.approx(line["value"], rel=1e-3)  # value = the whole job's bytes / the slowest rank's time
+        pytest.approx(line["value"], rel=5e-3)  # value = the whole job's bytes / the slowest rank's time
