@@ -58,6 +58,19 @@ def cpu_hook_lib(bcp, tmp_path_factory):
     return ctypes.CDLL(str(out))
 
 
+@pytest.fixture(scope="session")
+def foreign_ops_addr(bcp, tmp_path_factory):
+    """Address of a caller's transport table (tests/native/foreign_ops.c: the
+    loopback ranks behind wrappers, no send_fill -- an MPI binding's shape)."""
+    out = tmp_path_factory.mktemp("fops") / "libforeignops.so"
+    subprocess.run(["gcc", "-O2", "-shared", "-fPIC", "-I", os.path.join(ROOT, "include"), "-o", str(out),
+                    os.path.join(os.path.dirname(__file__), "native", "foreign_ops.c"), bcp.LIB_PATH,
+                    f"-Wl,-rpath,{os.path.dirname(bcp.LIB_PATH)}"], check=True)
+    L = ctypes.CDLL(str(out))
+    L.foreign_ops.restype = ctypes.c_void_p
+    return L.foreign_ops()
+
+
 @pytest.fixture
 def cpu_hook(bcp, cpu_hook_lib):
     """Route the P role's fold to the CPU test double for one test (host-logic

@@ -608,3 +608,37 @@ def test_rank_pool_config5_shapes_every_file(tmp_path):
     r = subprocess.run([sys.executable, "-c", POOL5_SCRIPT, str(tmp_path), HERE], capture_output=True, text=True,
                        timeout=240)
     assert r.returncode == 0 and "pool5 ok" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]
+
+
+def test_caller_transport_table_on_device(bcp, oracle, tmp_path, foreign_ops_addr, fold_mode):
+    """process_task over a caller's transport table (an MPI binding's shape:
+    no send_fill) with the GPU fold: the reference's padded wire, every window
+    through the device's fold service (the pipelined fold cannot follow such a
+    transport), multi-window replay; parity and rebuild exact."""
+    rng = np.random.default_rng(707)
+    nt = 8
+    files = []
+    for i in range(40):
+        holders, p = S.random_layout(rng, nt, int(rng.integers(1, 7)))
+        lens = [int(x) for x in np.exp(rng.uniform(np.log(1024), np.log(4 << 20), size=len(holders)))]
+        files.append((f"g/{i % 5}/c{i}", holders, p, lens))
+    files[0] = ("g/big", [0, 1, 3], 2, [10 << 20, (21 << 20) + 9, 5])
+    root = str(tmp_path)
+    items, contents = S.populate(root, nt, files, seed=71)
+    bcp.set_transport(foreign_ops_addr)
+    try:
+        assert bcp.gen_run(root, nt, items, nlanes=6).errors == 0
+        for (path, holders, p, lens) in files:
+            assert S.read_file(S.parity_path(root, p, path)) == oracle.gen_parity_file(contents[path]), path
+        victim = 3
+        lost = {}
+        for (path, holders, p, lens) in files:
+            if victim in holders:
+                lost[path] = S.read_file(S.chunk_path(root, victim, path))
+                os.remove(S.chunk_path(root, victim, path))
+        assert lost
+        assert bcp.rebuild_run(root, nt, victim, items).errors == 0
+        for path, data in lost.items():
+            assert S.read_file(S.chunk_path(root, victim, path)) == data, path
+    finally:
+        bcp.set_transport(None)

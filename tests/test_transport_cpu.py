@@ -512,3 +512,37 @@ def test_sock_world_raises_nofile_only_as_needed_and_restores_it(bcp):
         assert resource.getrlimit(resource.RLIMIT_NOFILE)[0] == low
     finally:
         resource.setrlimit(resource.RLIMIT_NOFILE, (soft0, hard))
+
+
+@pytest.mark.timeout(200)
+def test_caller_transport_table_gen_and_rebuild(bcp, oracle, cpu_hook, foreign_ops_addr, tmp_path):
+    """process_task over a caller's transport table (an MPI binding's shape:
+    no send_fill): the sources send the reference's padded windows (the
+    default for a foreign table), the P role folds whole windows through the
+    fold service, multi-window stripes replay -- parity and rebuild exact."""
+    rng = np.random.default_rng(606)
+    nt = 7
+    files = []
+    for i in range(30):
+        holders, p = S.random_layout(rng, nt, int(rng.integers(1, 6)))
+        lens = [int(x) for x in rng.integers(0, 900_000, size=len(holders))]
+        files.append((f"f/{i % 3}/c{i}", holders, p, lens))
+    files[0] = ("f/big", [0, 1], 2, [10 * 1024 * 1024, 25 * 1024 * 1024 + 5])
+    root = str(tmp_path)
+    items, contents = S.populate(root, nt, files, seed=61)
+    bcp.set_transport(foreign_ops_addr)
+    try:
+        assert bcp.gen_run(root, nt, items, nlanes=4).errors == 0
+        for (path, holders, p, lens) in files:
+            assert S.read_file(S.parity_path(root, p, path)) == oracle.gen_parity_file(contents[path]), path
+        victim = 1
+        lost = {}
+        for (path, holders, p, lens) in files:
+            if victim in holders:
+                lost[path] = S.read_file(S.chunk_path(root, victim, path))
+                os.remove(S.chunk_path(root, victim, path))
+        assert bcp.rebuild_run(root, nt, victim, items).errors == 0
+        for path, data in lost.items():
+            assert S.read_file(S.chunk_path(root, victim, path)) == data, path
+    finally:
+        bcp.set_transport(None)
