@@ -407,6 +407,12 @@ def main():
     total_bytes = d.sum(float(bytes_per_step * a.steps))
     ok_all = d.sum(1.0 if verified else 0.0) == d.world
     kern_ms_max = d.max(kern_ms)
+    # every rank's own figures (per-GPU rates of the N-GPU line): bus id, HIP-event
+    # kernel time, its share of the wall clock
+    per_rank = d.gather({"rank": d.rank, "pci_bus_id": bus_ids[d.rank], "kernel_ms": round(kern_ms, 4),
+                         "GiBps": round(bytes_per_step * a.steps / wall / GiB, 2),
+                         "pct_hbm_peak": round(100.0 * bytes_per_step / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 2),
+                         "verified": bool(verified)})
 
     cpu = None
     if d.rank == 0 and d.world == 1 and not a.no_cpu and a.mode != "mixed":
@@ -483,6 +489,7 @@ def main():
                 "pci_bus_ids": sorted(set(bus_ids)),
                 "cus": cus,
                 "verified_on_device": ok_all,
+                "per_rank": per_rank if d.world > 1 else None,
             },
             "roofline": {
                 "bound": "hbm",

@@ -83,6 +83,8 @@ def test_bench_gpus_n_launches_its_own_ranks(bcp, n):
     assert line["n_gpus"] == min(ndev, n)
     assert line["config"]["shared_gpu"] is (ndev < n)
     assert line["config"]["verified_on_device"] is True
+    per = line["config"]["per_rank"]  # each GPU's own rate in the N-GPU line
+    assert [r["rank"] for r in per] == list(range(n)) and all(r["verified"] and r["GiBps"] > 0 for r in per)
     assert line["config"]["bytes_per_step_per_gpu"] * n * line["steps"] / 2**30 / (line["ms_per_step"] *
                                                                                    line["steps"] * 1e-3) == \
         pytest.approx(line["value"], rel=5e-3)  # value = the whole job's bytes / the slowest rank's time
