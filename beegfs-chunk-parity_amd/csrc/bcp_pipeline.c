@@ -561,11 +561,17 @@ int bcp_pipeline_create(const bcp_pipeline_opts *opts_in, bcp_pipeline **out)
     if (!out)
         return -EINVAL;
     *out = NULL;
-    bcp_pipeline_opts o = {0, 256u << 20, 8, 3, 1};
+    bcp_pipeline_opts o = {0, 256u << 20, 0, 3, 1};
     if (opts_in)
         o = *opts_in;
     if (o.ndevices < 1)
         o.ndevices = 1;
+    /* io threads 0 = auto: 8 readers and 8 writers per GPU.  One GPU's PCIe
+     * link takes what ~8 threads copy out of the page cache (8 beat 16 on a
+     * 16-CPU share, profiles/r02/protocol/pipeline_io_threads_ab_r2e4.jsonl),
+     * and every further GPU brings its own link and its own CPU share. */
+    if (o.io_threads == 0)
+        o.io_threads = 8 * o.ndevices;
     int ndev_vis = 0;
     bcp_device_count(&ndev_vis);
     if (o.device < 0 || o.ndevices > 64)

@@ -58,6 +58,16 @@ static int fold_mode_arg(const char *s)
     return -1;
 }
 
+/* The batched pipeline on every visible GPU (each brings its own PCIe link;
+ * io threads scale with them). */
+static int pipeline_on_all_gpus(bcp_pipeline **pl)
+{
+    int ndev = 0;
+    bcp_device_count(&ndev);
+    const bcp_pipeline_opts o = {0, (size_t)256 << 20, 0, 3, ndev > 0 ? ndev : 1};
+    return bcp_pipeline_create(&o, pl);
+}
+
 static int fail(const char *what, int rc)
 {
     fprintf(stderr, "bcp: %s: %s\n", what, strerror(rc < 0 ? -rc : rc));
@@ -185,7 +195,7 @@ static int cmd_gen(int argc, char **argv)
     size_t planned = 0;
     if (use_pipeline) {
         bcp_pipeline *pl = NULL;
-        rc = bcp_pipeline_create(NULL, &pl);
+        rc = pipeline_on_all_gpus(&pl);
         t_setup = now_s();
         if (!rc)
             rc = bcp_gen_round_pipeline(pl, root, ntargets, es, NULL, stderr, &st, &planned);
@@ -269,7 +279,7 @@ static int cmd_rebuild(int argc, char **argv)
             rc = bcp_rebuild_run_procs(root, ntargets, target, items, n, corrupt, stderr, &st);
         } else if (!rc) {
             bcp_pipeline *pl = NULL;
-            rc = bcp_pipeline_create(NULL, &pl);
+            rc = pipeline_on_all_gpus(&pl);
             if (!rc)
                 rc = bcp_pipeline_rebuild(pl, root, ntargets, target, items, n, corrupt, stderr, &st);
             if (pl)

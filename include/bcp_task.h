@@ -459,7 +459,7 @@ int bcp_gen_round_procs(const char *store_root, int ntargets, const bcp_eventset
 typedef struct {
     int device;          /* HIP device */
     size_t slab_bytes;   /* pinned / device slab per slot (grown to the largest stripe) */
-    int io_threads;      /* reader and writer threads (each) */
+    int io_threads;      /* reader and writer threads (each); 0 = 8 per GPU (capped at 64) */
     int nslots;          /* slabs in flight per device (2..8) */
     int ndevices;        /* GPUs device .. device+ndevices-1 (mod the visible count),
                             batches round-robin (0 = 1) */
@@ -471,7 +471,7 @@ typedef struct {
  * another side queue and written as parity chunk files -- byte-identical
  * to bcp_gen_run's (same header, padding and window replay).  NO_P items are
  * skipped; items without holders unlink their parity chunk.  opts may be
- * NULL ({0, 256 MiB, 8, 3, 1}). */
+ * NULL ({0, 256 MiB, 0, 3, 1}). */
 int bcp_pipeline_gen(const char *store_root, int ntargets, const bcp_work_item *items, size_t nitems,
                      const bcp_pipeline_opts *opts, FILE *log, bcp_run_stats *stats);
 /* The same as a long-lived object: engine, queues, io threads and pinned /

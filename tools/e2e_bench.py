@@ -391,7 +391,7 @@ def main():
     ap.add_argument("--configs", default="1,5")
     ap.add_argument("--c1-files", type=int, default=1333)
     ap.add_argument("--c5-stripes", type=int, default=1000)
-    ap.add_argument("--io-threads", type=int, default=16)
+    ap.add_argument("--io-threads", type=int, default=0, help="pipeline io threads (0: the library's 8 per GPU)")
     ap.add_argument("--ndevices", type=int, default=0, help="GPUs for the pipeline (0 = all visible)")
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--verify", type=int, default=20)
