@@ -67,7 +67,6 @@ struct bcp_queue {
   unsigned long long qbase = 0;        // its value when the next launch starts
   hipEvent_t timer[kTimerSlots] = {};
   hipStream_t copy_stream = nullptr;   // descriptor-table uploads (created on first use)
-  hipEvent_t sync_ev = nullptr;        // blocking-sync event (sync_mode 1; created on first use)
   bool broken = false;                 // work-queue counter could not be restarted after a failed launch
 };
 
@@ -137,7 +136,7 @@ static int grid_for(const bcp_engine *e) {
 }
 
 // Workgroups of the descriptor kernel.  Auto (desc_blocks_per_cu 0): one
-// per CU on every CU.  With the rolling load window (desc_pipe) that is the
+// per CU on every CU.  With the rolling load window (PIPE 5) that is the
 // best grid for every non-uniform shape measured -- config-5 shapes +1.3
 // points over the earlier 2 per CU, 1-4 MiB mixed +0.4, equal-length mixed
 // +0.5 over 15/16 of the CUs, 16-wide +0.8 (tools/exp/desc_probe.py,
@@ -319,24 +318,12 @@ extern "C" int bcp_set_option(bcp_engine *eng, const char *key, int value) {
   else if (!strcmp(key, "desc_blocks_per_cu") && value >= 0 && value <= 32) eng->tuning.desc_blocks_per_cu = value;
   else if (!strcmp(key, "desc_vecs_per_thread") && (value == 0 || desc_vecs_ok(value))) eng->tuning.desc_vecs = value;
   else if (!strcmp(key, "desc_args_max") && value >= 0 && value <= kArgStripes) eng->tuning.desc_args_max = value;
-  else if (!strcmp(key, "desc_side_tiles") && (value == 0 || value == 1)) eng->tuning.desc_side_tiles = value;
-  else if (!strcmp(key, "desc_ahead") && (value == 0 || value == 1)) eng->tuning.desc_ahead = value;
-  else if (!strcmp(key, "schedule") && (value == kSchedQueue || value == kSchedStatic)) eng->tuning.schedule = value;
-  else if (!strcmp(key, "desc_schedule") && (value == kSchedQueue || value == kSchedStatic)) eng->tuning.desc_schedule = value;
-  else if (!strcmp(key, "desc_grab") && value >= 1 && value <= 64) eng->tuning.desc_grab = value;
-  else if (!strcmp(key, "desc_force") && (value == 0 || value == 1)) eng->tuning.desc_force = value;
   else if (!strcmp(key, "stream_grid") && value >= 0 && value <= 65536) eng->tuning.stream_grid = value;
   else if (!strcmp(key, "desc_grid") && value >= 0 && value <= 65536) eng->tuning.desc_grid = value;
   else if (!strcmp(key, "contiguous_alloc") && (value == 0 || value == 1)) eng->tuning.contiguous_alloc = value;
   else if (!strcmp(key, "table_host_max") && value >= 0 && value <= (1 << 24)) eng->tuning.table_host_max = value;
-  else if (!strcmp(key, "stream_wpe") && (value == 0 || (value >= 5 && value <= 7))) eng->tuning.stream_wpe = value;
-  else if (!strcmp(key, "table_wpe") && (value == 0 || (value >= 5 && value <= 7))) eng->tuning.table_wpe = value;
-  else if (!strcmp(key, "stream_grab") && value >= 0 && value <= 64) eng->tuning.stream_grab = value;
-  else if (!strcmp(key, "sync_mode") && (value == 0 || value == 1)) eng->tuning.sync_mode = value;
   else if (!strcmp(key, "host_registered") && (value == 0 || value == 1)) eng->tuning.host_registered = value;
   else if (!strcmp(key, "desc_reuse_records") && (value == 0 || value == 1)) eng->tuning.desc_reuse_records = value;
-  else if (!strcmp(key, "desc_pipe") && (value == 0 || value == 2 || value == 4 || value == 5 || value == 6))
-    eng->tuning.desc_pipe = value;
   else if (!strcmp(key, "desc_table_host_max") && value >= 0 && value <= (1 << 24))
     eng->tuning.desc_table_host_max = value;
   else rc = -EINVAL;
@@ -351,24 +338,13 @@ extern "C" int bcp_get_option(bcp_engine *eng, const char *key, int *value) {
   const Tuning &t = eng->tuning;
   if (!strcmp(key, "blocks_per_cu")) *value = t.blocks_per_cu;
   else if (!strcmp(key, "vecs_per_thread")) *value = t.vecs_per_thread;
-  else if (!strcmp(key, "schedule")) *value = t.schedule;
   else if (!strcmp(key, "desc_blocks_per_cu")) *value = t.desc_blocks_per_cu;
   else if (!strcmp(key, "desc_vecs_per_thread")) *value = t.desc_vecs;
   else if (!strcmp(key, "desc_args_max")) *value = t.desc_args_max;
-  else if (!strcmp(key, "desc_side_tiles")) *value = t.desc_side_tiles;
-  else if (!strcmp(key, "desc_ahead")) *value = t.desc_ahead;
-  else if (!strcmp(key, "desc_schedule")) *value = t.desc_schedule;
-  else if (!strcmp(key, "desc_grab")) *value = t.desc_grab;
-  else if (!strcmp(key, "desc_force")) *value = t.desc_force;
   else if (!strcmp(key, "stream_grid")) *value = t.stream_grid;
   else if (!strcmp(key, "desc_grid")) *value = t.desc_grid;
   else if (!strcmp(key, "contiguous_alloc")) *value = t.contiguous_alloc;
   else if (!strcmp(key, "table_host_max")) *value = t.table_host_max;
-  else if (!strcmp(key, "stream_wpe")) *value = t.stream_wpe;
-  else if (!strcmp(key, "table_wpe")) *value = t.table_wpe;
-  else if (!strcmp(key, "desc_pipe")) *value = t.desc_pipe;
-  else if (!strcmp(key, "stream_grab")) *value = t.stream_grab;
-  else if (!strcmp(key, "sync_mode")) *value = t.sync_mode;
   else if (!strcmp(key, "host_registered")) *value = t.host_registered;
   else if (!strcmp(key, "desc_reuse_records")) *value = t.desc_reuse_records;
   else if (!strcmp(key, "desc_table_host_max")) *value = t.desc_table_host_max;
@@ -433,28 +409,16 @@ extern "C" int bcp_queue_destroy(bcp_queue *q) {
   for (auto &t : q->timer)
     if (t) (void)hipEventDestroy(t);
   if (q->qctr) (void)hipFree(q->qctr);
-  if (q->sync_ev) (void)hipEventDestroy(q->sync_ev);
   (void)hipStreamDestroy(q->stream);
   delete q;
   return 0;
 }
 
-// sync_mode 0: hipStreamSynchronize (the runtime's spin-then-yield wait);
-// 1: a blocking-sync event, so a waiting host thread sleeps instead of
-// competing for cores with the threads that feed the GPU (the per-task
-// protocol's 12 lanes and their senders on a 16-core share).
+// hipStreamSynchronize (the runtime's spin-then-yield wait; a blocking-sync
+// event measured no better for the per-task protocol's 12 lanes on a 16-core
+// share, r02).
 extern "C" int bcp_queue_sync(bcp_queue *q) {
   if (!q) return -EINVAL;
-  if (q->eng->tuning.sync_mode == 1) {
-    if (!q->sync_ev) {
-      const int rc = set_device(q->eng);  // the event must belong to the queue's device
-      if (rc) return rc;
-      HIP_RC(hipEventCreateWithFlags(&q->sync_ev, hipEventBlockingSync | hipEventDisableTiming));
-    }
-    HIP_RC(hipEventRecord(q->sync_ev, q->stream));
-    HIP_RC(hipEventSynchronize(q->sync_ev));
-    return 0;
-  }
   HIP_RC(hipStreamSynchronize(q->stream));
   return 0;
 }
@@ -726,30 +690,24 @@ extern "C" int bcp_memset_async(bcp_queue *q, void *dst, int value, size_t bytes
 // XOR submission
 // ---------------------------------------------------------------------------
 
-// Launch the streaming kernel on q (work-queue or static schedule).
+// Launch the streaming kernel on q (device-wide work queue).
 static int launch_stream(bcp_queue *q, bool gather, int vecs, StreamArgs a, uint64_t ntiles) {
   bcp_engine *e = q->eng;
   if (ntiles == 0) return 0;
   if (ntiles > 0xFFFFFFF0ull) return -EINVAL;
   a.ntiles = (uint32_t)ntiles;
-  a.sched = e->tuning.schedule;
   a.ctr = q->qctr;
   a.base = q->qbase;
   // Tiles per grab: the kernels for 1-4 sources take several (stream_body).
-  a.grab = 1;
-  if (a.nsrc >= 1 && a.nsrc <= 4 && a.sched == kSchedQueue)
-    a.grab = e->tuning.stream_grab > 0 ? (uint32_t)e->tuning.stream_grab : stream_grab_auto(a.nsrc);
+  a.grab = stream_grab_auto(a.nsrc);
   const uint64_t nunits = (ntiles + a.grab - 1) / a.grab;
   int grid = grid_for(e);
   if ((uint64_t)grid > nunits) grid = (int)nunits;
   if (q->broken) return -EIO;
   (void)hipGetLastError();  // an error left by an earlier call must not read as this launch's
-  const hipError_t le =
-      launch_xor_stream(q->stream, grid, vecs, gather, a, gather ? e->tuning.table_wpe : e->tuning.stream_wpe);
+  const hipError_t le = launch_xor_stream(q->stream, grid, vecs, gather, a);
   if (le == hipSuccess) e->last_stream_vecs.store(vecs, std::memory_order_relaxed);
-  if (a.sched == kSchedQueue) return queue_launched(q, le, nunits + (uint64_t)grid);
-  HIP_RC(le);
-  return 0;
+  return queue_launched(q, le, nunits + (uint64_t)grid);
 }
 
 // A batch is uniform when every stripe has the same nsrc and out_len, every
@@ -862,7 +820,7 @@ static int submit_desc(bcp_queue *q, const bcp_stripe *stripes, uint32_t nstripe
   if (tiles8 > 0xFFFFFFF0ull / 4) return -EINVAL;
   const int vecs = desc_vecs_for(e, tiles8);
   const uint32_t tile_bytes = desc_tile_bytes(vecs);
-  if (!e->tuning.desc_force && uniform_batch(stripes, nstripes, sources)) {
+  if (uniform_batch(stripes, nstripes, sources)) {
     const uint64_t len = stripes[0].out_len;
     const int sv = stream_vecs(e, len, nstripes, stripes[0].nsrc);
     const uint32_t tps = stream_tiles_per_stripe(len, sv);
@@ -958,14 +916,13 @@ static int submit_desc(bcp_queue *q, const bcp_stripe *stripes, uint32_t nstripe
     HIP_RC(hipMalloc((void **)&slot->tiles, cap * sizeof(DescTile)));
     slot->tiles_cap = cap;
   }
-  const uint32_t nunits = e->tuning.desc_schedule == kSchedQueue ? (acc + e->tuning.desc_grab - 1) / e->tuning.desc_grab : acc;
   int grid = desc_grid_for(e);
-  if ((uint32_t)grid > nunits) grid = (int)nunits;
+  if ((uint32_t)grid > acc) grid = (int)acc;
   // Large batches: desc_tiles on the copy stream (after the table upload),
   // so it overlaps the previous batch's fold on the compute stream instead of
   // sitting between two folds; the fold waits for it by event.  Small batches
   // keep it in line (a cross-stream wait costs more than it hides).
-  const bool side = e->tuning.desc_side_tiles && acc >= 2u * (uint32_t)grid;
+  const bool side = acc >= 2u * (uint32_t)grid;
   char *d = nullptr;
   // Host-resident tables only when desc_tiles alone reads them: the general
   // and wide tile paths read them again per tile.
@@ -980,8 +937,6 @@ static int submit_desc(bcp_queue *q, const bcp_stripe *stripes, uint32_t nstripe
   b.nstripes = nstripes;
   b.ntiles = acc;
   b.tile_bytes = tile_bytes;
-  b.sched = e->tuning.desc_schedule;
-  b.grab = (uint32_t)e->tuning.desc_grab;
   b.ctr = q->qctr;
   b.base = q->qbase;
   if (q->broken) return -EIO;
@@ -995,14 +950,12 @@ static int submit_desc(bcp_queue *q, const bcp_stripe *stripes, uint32_t nstripe
   } else {
     HIP_RC(launch_desc_tiles(q->stream, b));
   }
-  const hipError_t le = launch_xor_desc(q->stream, grid, vecs, b, e->tuning.desc_pipe, e->tuning.desc_ahead);
+  const hipError_t le = launch_xor_desc(q->stream, grid, vecs, b);
   if (le == hipSuccess) {
     e->last_desc_vecs.store(vecs, std::memory_order_relaxed);
     e->last_desc_form.store(1, std::memory_order_relaxed);
   }
-  if (b.sched == kSchedQueue) rc = queue_launched(q, le, (uint64_t)nunits + (uint64_t)grid);
-  else rc = hip_to_errno(le);
-  if (rc) return rc;
+  if ((rc = queue_launched(q, le, (uint64_t)acc + (uint64_t)grid))) return rc;
   HIP_RC(hipEventRecord(slot->done, q->stream));
   slot->used = true;
   slot->rec_key = key;

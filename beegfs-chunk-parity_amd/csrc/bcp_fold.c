@@ -320,9 +320,15 @@ static void host_free(fold_res *R, void *p)
 {
     if (!p)
         return;
-    if (bcpi_arena_free(p)) { /* a block of the shared arena: the mapping stays */
+    void *ab;
+    size_t az;
+    if (bcpi_arena_block(p, &ab, &az) && ab == p) {
+        /* a block of the shared arena: the mapping stays.  Unregistered before
+         * it goes back to the arena, so another lane that takes the block next
+         * registers it for itself and no unregister of ours can follow that. */
         if (R->device >= 0)
             (void)bcp_host_unregister(R->eng, p);
+        bcpi_arena_free(p);
         return;
     }
     if (R->device >= 0)

@@ -114,7 +114,8 @@ int bcpf_fold_remote(int st, int tag, const uint8_t *rows, size_t pitch, const s
                 (uint64_t)(uintptr_t)out, 0, 0, 0, 0};
     void *rb, *ob;
     size_t rs, os;
-    if (n < 1 || n > MAX_STORAGE_TARGETS || !bcpi_arena_block(rows, &rb, &rs) || !bcpi_arena_block(out, &ob, &os))
+    if (g_srv_n < 1 || n < 1 || n > MAX_STORAGE_TARGETS || !bcpi_arena_block(rows, &rb, &rs) ||
+        !bcpi_arena_block(out, &ob, &os))
         return -ENXIO;
     q.rows_base = (uint64_t)(uintptr_t)rb;
     q.rows_size = rs;

@@ -13,29 +13,23 @@ namespace bcp {
 constexpr int kBlock = 256;        // threads per workgroup (4 waves of 64)
 constexpr int kMaxVecsPerThread = 8;     // xor_stream and xor_desc
 
-// Tile schedules of the streaming kernel.
-constexpr int kSchedQueue = 0;   // device-wide work queue (default)
-constexpr int kSchedStatic = 1;  // contiguous tile range per workgroup (r01 design; A/B only)
-
-// Defaults from the r01 interleaved sweeps on MI355X (profiles/r01/):
-// xor_stream: one 256-thread workgroup per CU with 8 vectors per lane (the
-// fewer tiles in flight, the narrower the queue's address window:
-// kernel_exp_6/7), work-queue schedule, non-temporal loads and stores.
+// Defaults from the r01-r03 interleaved sweeps on MI355X (profiles/r01/,
+// DESIGN.md section 4): xor_stream runs one 256-thread workgroup per CU with 8
+// vectors per lane (the fewer tiles in flight, the narrower the work queue's
+// address window: kernel_exp_6/7), non-temporal loads and stores.  The
+// schedules and load shapes that lost those sweeps (static tile ranges,
+// grab-ahead, other rolling windows and register budgets, blocking-sync
+// waits) are gone from the engine; their numbers stay in profiles/ and
+// DESIGN.md.
 struct Tuning {
     int blocks_per_cu = 1;      // xor_stream: 256-thread workgroups launched per CU
     int vecs_per_thread = 0;    // xor_stream: 16-byte vectors per lane per tile (1, 2, 4, 8; 0 = by batch size)
-    int schedule = kSchedQueue; // xor_stream: kSched*
     // xor_desc (tools/exp/desc_probe.py, profiles/r01/mixed/, depth/): 8
     // vectors per lane, one 32 KiB tile per queue grab; workgroups per CU
     // 0 = auto (desc_grid_for: one per CU).
     int desc_blocks_per_cu = 0;
-    int desc_vecs = 0;          // 1, 2, 4, 8; 0 = by batch size (desc_vecs_for)
+    int desc_vecs = 0;          // 1, 2, 4, 8, 16; 0 = by batch size (desc_vecs_for)
     int desc_args_max = 16;     // batches of at most this many stripes go in the kernel arguments (0 = never)
-    int desc_ahead = 0;         // xor_desc: take the next tile and touch its record before folding the current one
-    int desc_side_tiles = 1;    // large batches: desc_tiles on the copy stream, overlapping the previous fold
-    int desc_grab = 1;          // tiles per work-queue grab
-    int desc_schedule = kSchedQueue;
-    int desc_force = 0;         // 1: uniform batches take xor_desc too (A/B only)
     int stream_grid = 0;        // xor_stream: explicit workgroup count (0: 29/32 of CUs x blocks_per_cu)
     int desc_grid = 0;          // xor_desc: explicit workgroup count (0: desc_grid_for)
     int contiguous_alloc = 0;   // 1: bcp_dev_alloc asks for physically contiguous buffers >= 64 MiB
@@ -44,15 +38,6 @@ struct Tuning {
     // the pointer-table xor_stream reads its table once per tile (a win up
     // to ~16 stripes of 8), desc_tiles once per batch (a win up to >= 512).
     int table_host_max = 4096;
-    // Loads in flight per lane (profiles/r01/depth/): register budget of
-    // xor_stream<8,8> in waves per SIMD (0: the compiler's own target; 5,
-    // 6, 7; same-allocation A/B: gen +0.8, rebuild +0.1 point at 6) and the rolling load window of xor_desc<8> (0: every
-    // load of the tile first; 2, 4, 5: PipeShape in bcp_kernels.hip).
-    int stream_wpe = 6;         // strided form (config-2 gen)
-    int table_wpe = 6;          // pointer-table form (rebuild)
-    int desc_pipe = 5;
-    int stream_grab = 0;        // xor_stream, 1-4 sources: tiles per queue grab (0: auto)
-    int sync_mode = 0;          // bcp_queue_sync: 0 hipStreamSynchronize, 1 blocking-sync event
     int desc_table_host_max = 128 * 1024;
     // bcp_host_alloc / bcp_host_alloc_mapped: 1 = ordinary huge-page memory
     // registered with HIP (CPU copies into and out of it run at malloc speed),
@@ -81,7 +66,6 @@ struct StreamArgs {
     uint32_t dense;             // GATHER = 1: stripes[s].first_src == s * nsrc for every s
     unsigned long long *ctr;    // work-queue counter (per queue)
     unsigned long long base;    // counter value at the start of this launch
-    int sched;                  // kSched*
     uint32_t grab;              // tiles per queue grab (NSRC 1..4 instantiations; others take 1)
 };
 
@@ -198,8 +182,6 @@ struct DescBatch {
     uint32_t tile_bytes;        // bytes of output per tile
     unsigned long long *ctr;    // work-queue counter (per queue), as StreamArgs
     unsigned long long base;
-    int sched;                  // kSched*
-    uint32_t grab;              // kSchedQueue: tiles per grab
 };
 
 // A small descriptor batch passed whole in the kernel arguments
@@ -221,17 +203,15 @@ struct DescArgs {
 };
 
 // Kernel launchers (bcp_kernels.hip).  All return hipError_t.
-// Streaming fold.  Consumes ntiles + grid counts of a.ctr when a.sched is
-// kSchedQueue; the caller clamps grid to [1, ntiles].
-hipError_t launch_xor_stream(hipStream_t st, int grid, int vecs, bool gather,
-                             const StreamArgs &a, int wpe = 0);
+// Streaming fold.  Consumes ceil(ntiles / grab) + grid counts of a.ctr; the
+// caller clamps grid to [1, ntiles].
+hipError_t launch_xor_stream(hipStream_t st, int grid, int vecs, bool gather, const StreamArgs &a);
 uint32_t stream_tiles_per_stripe(uint64_t chunk_bytes, int vecs);
 // Descriptor batch: desc_tiles (one wave per stripe writes its tile records
 // into b.tiles), then the fold; same work-queue accounting as
 // launch_xor_stream.
 hipError_t launch_desc_tiles(hipStream_t st, const DescBatch &b);
-hipError_t launch_xor_desc(hipStream_t st, int grid, int vecs,
-                           const DescBatch &b, int pipe = 0, int ahead = 0);
+hipError_t launch_xor_desc(hipStream_t st, int grid, int vecs, const DescBatch &b);
 // Small batch in the arguments; same work-queue accounting (ntiles + grid).
 hipError_t launch_xor_desc_args(hipStream_t st, int grid, int vecs, const DescArgs &a);
 hipError_t launch_fill_synthetic(hipStream_t st, int grid, char *dst,

@@ -95,29 +95,25 @@ __device__ __forceinline__ uint32_t tile_vec(uint32_t tin, int u) {
 }
 
 // Rolling load window of the descriptor kernel's covering-source fold
-// (PIPE > 0; engine option desc_pipe, default 5).  Folds G sources x U
-// vectors per lane into acc, issuing the loads as units of H vectors with D
-// units in flight: unit j + D - 1 goes out before unit j is XORed, and
-// sched_barrier keeps the compiler from hoisting every load of the tile
-// above the XORs (which it does when the kernel runs at one wave per SIMD
-// anyway), so (D - 1) * H .. D * H loads per lane are outstanding.  Every
-// load of a tile in flight at once widens the chip's address window and
-// costs HBM rate: PIPE 4 (H = 2, D = 5: 8-10 loads) +1.3 points on config-5
-// shapes, +1.8 on config-2 shapes through xor_desc; PIPE 5 (the default)
-// also windows tiles with more than 8 sources: 16-wide stripes 69 -> 81 %
-// (profiles/r01/depth/).
-// Shapes (the engine exposes 2, 4 and 5; 1 and 3 were r01 A/B points):
-// PIPE 1: H = U, D = 2; 2: H = U/2, D = 3; 3: H = U/2, D = 4; 4: H = U/4,
-// D = 5; 5: as 4, and tiles with more than 8 sources (desc_tile_wide)
-// through the window too; 6: as 5 with H = U/8 (at U = 16: the loads in
-// flight of PIPE 5 at U = 8).  (Grouped tiles keep all their <= 32 loads in
-// flight: a window there cost 1.4 points, depth/ab3_group_window_probe.jsonl;
-// the same window in xor_stream measured 2 points below the compiler's own
-// schedule.)
+// (PIPE > 0: xor_desc_p<U, 5>, the shipped form at U = 8 and 16).  Folds G
+// sources x U vectors per lane into acc, issuing the loads as units of H =
+// U/4 vectors with D = 5 units in flight: unit j + D - 1 goes out before unit
+// j is XORed, and sched_barrier keeps the compiler from hoisting every load
+// of the tile above the XORs (which it does when the kernel runs at one wave
+// per SIMD anyway), so (D - 1) * H .. D * H loads per lane are outstanding.
+// Every load of a tile in flight at once widens the chip's address window and
+// costs HBM rate: the window is +1.3 points on config-5 shapes, +1.8 on
+// config-2 shapes through xor_desc, and on tiles with more than 8 sources
+// (desc_tile_wide) 16-wide stripes 69 -> 81 % (profiles/r01/depth/; the other
+// unit shapes measured there -- H = U, U/2, U/8 with D = 2..5 -- lost and are
+// gone).  Grouped tiles keep all their <= 32 loads in flight: a window there
+// cost 1.4 points (depth/ab3_group_window_probe.jsonl); the same window in
+// xor_stream measured 2 points below the compiler's own schedule.
 template <int U, int PIPE>
 struct PipeShape {
-  static constexpr int H = PIPE == 1 ? U : PIPE <= 3 ? (U >= 2 ? U / 2 : 1) : PIPE == 6 ? (U >= 8 ? U / 8 : 1) : (U >= 4 ? U / 4 : 1);
-  static constexpr int D = PIPE == 1 ? 2 : PIPE == 2 ? 3 : PIPE == 3 ? 4 : 5;
+  static_assert(PIPE == 5, "one rolling-window shape");
+  static constexpr int H = U >= 4 ? U / 4 : 1;
+  static constexpr int D = 5;
 };
 
 template <int G, int U, int PIPE, typename V, typename F>
@@ -246,52 +242,45 @@ __device__ __forceinline__ uint32_t queue_grab(unsigned long long *ctr, unsigned
   return v > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)v;
 }
 
-// KIND: kQueueFull (work queue, every tile full: the config-2 shapes),
-// kQueuePartial (work queue, stripes end in a partial tile), kStatic
-// (contiguous tile range per workgroup; A/B only).  Separate instantiations
-// because the partial-tile and static code paths cost ~15-25 VGPRs at U = 8
-// even when never taken.
-constexpr int kQueueFull = 0, kQueuePartial = 1, kStatic = 2;
+// KIND: kQueueFull (every tile full: the config-2 shapes), kQueuePartial
+// (stripes end in a partial tile).  Separate instantiations because the
+// partial-tile code path costs ~15-25 VGPRs at U = 8 even when never taken.
+// (r01's static schedule -- a contiguous tile range per workgroup -- lost to
+// the work queue by 12-14 % and is gone.)
+constexpr int kQueueFull = 0, kQueuePartial = 1;
 
 template <int NSRC, int U, int GATHER, int KIND>
 __device__ __forceinline__ void stream_body(const StreamArgs &a) {
   constexpr bool PARTIAL = KIND != kQueueFull;
-  if constexpr (KIND == kStatic) {
-    // Workgroup b owns tiles [b*T/G, (b+1)*T/G) (the r01 schedule; A/B only).
-    const uint32_t t0 = (uint32_t)(((uint64_t)blockIdx.x * a.ntiles) / gridDim.x);
-    const uint32_t t1 = (uint32_t)(((uint64_t)(blockIdx.x + 1) * a.ntiles) / gridDim.x);
-    for (uint32_t t = t0; t < t1; t++) stream_tile<NSRC, U, GATHER, true>(a, t);
+  // Two LDS slots: thread 0 writes slot i+1 only after the barrier that
+  // every wave reaches after reading slot i, so one barrier per tile is enough.
+  __shared__ uint32_t next[2];
+  if (threadIdx.x == 0) next[0] = queue_grab(a.ctr, a.base);
+  __syncthreads();
+  uint32_t t = __builtin_amdgcn_readfirstlane(next[0]);
+  int slot = 0;
+  if constexpr (NSRC >= 1 && NSRC <= 4) {
+    // Narrow stripes: a.grab consecutive tiles per queue grab (a tile moves
+    // only (NSRC + 1) x 32 KiB at U = 8, and one counter serves ~60-80
+    // grabs per microsecond: at one tile per grab, N = 1..2 are
+    // counter-bound).
+    const uint32_t g = a.grab ? a.grab : 1u;  // the host always sets >= 1; never divide by 0
+    const uint32_t nunits = (a.ntiles + g - 1) / g;
+    while (t < nunits) {
+      const uint32_t t0 = t * g, t1 = min(t0 + g, a.ntiles);
+      for (uint32_t x = t0; x < t1; x++) stream_tile<NSRC, U, GATHER, PARTIAL>(a, x);
+      slot ^= 1;
+      if (threadIdx.x == 0) next[slot] = queue_grab(a.ctr, a.base);
+      __syncthreads();
+      t = __builtin_amdgcn_readfirstlane(next[slot]);
+    }
   } else {
-    // Two LDS slots: thread 0 writes slot i+1 only after the barrier that
-    // every wave reaches after reading slot i, so one barrier per tile is enough.
-    __shared__ uint32_t next[2];
-    if (threadIdx.x == 0) next[0] = queue_grab(a.ctr, a.base);
-    __syncthreads();
-    uint32_t t = __builtin_amdgcn_readfirstlane(next[0]);
-    int slot = 0;
-    if constexpr (NSRC >= 1 && NSRC <= 4) {
-      // Narrow stripes: a.grab consecutive tiles per queue grab (a tile moves
-      // only (NSRC + 1) x 32 KiB at U = 8, and one counter serves ~60-80
-      // grabs per microsecond: at one tile per grab, N = 1..2 are
-      // counter-bound).
-      const uint32_t g = a.grab ? a.grab : 1u;  // the host always sets >= 1; never divide by 0
-      const uint32_t nunits = (a.ntiles + g - 1) / g;
-      while (t < nunits) {
-        const uint32_t t0 = t * g, t1 = min(t0 + g, a.ntiles);
-        for (uint32_t x = t0; x < t1; x++) stream_tile<NSRC, U, GATHER, PARTIAL>(a, x);
-        slot ^= 1;
-        if (threadIdx.x == 0) next[slot] = queue_grab(a.ctr, a.base);
-        __syncthreads();
-        t = __builtin_amdgcn_readfirstlane(next[slot]);
-      }
-    } else {
-      while (t < a.ntiles) {
-        stream_tile<NSRC, U, GATHER, PARTIAL>(a, t);
-        slot ^= 1;
-        if (threadIdx.x == 0) next[slot] = queue_grab(a.ctr, a.base);
-        __syncthreads();
-        t = __builtin_amdgcn_readfirstlane(next[slot]);
-      }
+    while (t < a.ntiles) {
+      stream_tile<NSRC, U, GATHER, PARTIAL>(a, t);
+      slot ^= 1;
+      if (threadIdx.x == 0) next[slot] = queue_grab(a.ctr, a.base);
+      __syncthreads();
+      t = __builtin_amdgcn_readfirstlane(next[slot]);
     }
   }
 }
@@ -302,7 +291,7 @@ __global__ __launch_bounds__(kBlock) void xor_stream(StreamArgs a) {
 }
 
 // The same kernel with a register budget of W waves per SIMD
-// (amdgpu_waves_per_eu; engine option stream_wpe).  The body says "every
+// (amdgpu_waves_per_eu; W = 6 where it won, launch_xor_stream).  The body says "every
 // load of the tile first"; the compiler software-pipelines it into the
 // budget it aims for, so W sets how many loads per lane stay in flight: no
 // budget (its own occupancy target) ~5-9, W = 6 ~14, W = 7 8, W = 1-2 ~43.
@@ -351,8 +340,7 @@ __device__ __forceinline__ void store_tail(glob<unsigned char> *d, uint64_t out_
 // ---------------------------------------------------------------------------
 // Descriptor kernel.  Tiles of tile_bytes output bytes are numbered across the
 // batch (tile_start prefix) and handed out by the same work queue as
-// xor_stream (kSchedQueue) or as a contiguous range per workgroup
-// (kSchedStatic).  A small setup kernel (desc_tiles) first writes one 16-byte
+// xor_stream, one tile per grab.  A small setup kernel (desc_tiles) first writes one 16-byte
 // record per tile (stripe, tile index, coverage counts, source run), so a
 // tile costs one scalar load before its stripe and source loads, instead of a
 // search over tile_start.  Lanes are wave-contiguous as in xor_stream.  Per
@@ -457,7 +445,7 @@ struct RunAt {
 template <int U, int PIPE>
 __device__ __noinline__ void desc_tile_wide(const DescBatch &b, uint32_t stripe, uint32_t sub, uint32_t first_src,
                                             uint32_t nfull, uint32_t nany) {
-  constexpr int WP = PIPE >= 5 ? 4 : 0;
+  constexpr int WP = PIPE;  // the window also over the eight-at-a-time covering folds
   const_as<bcp_stripe> *dp_ = cst(b.stripes) + stripe;
   const_as<bcp_source> *srcs = cst(b.sources) + first_src;
   const uint64_t tile_off = (uint64_t)sub * b.tile_bytes;
@@ -599,66 +587,22 @@ __device__ __forceinline__ void desc_tile(const DescBatch &b, uint32_t t) {
   desc_plain<U, PIPE>(r, b.tile_bytes);
 }
 
-template <int U, int PIPE, int AHEAD = 0>
+template <int U, int PIPE>
 __device__ __forceinline__ void desc_body(const DescBatch &b) {
-  if (b.sched == kSchedStatic) {
-    const uint32_t g = gridDim.x;
-    const uint32_t t_begin = (uint32_t)(((uint64_t)blockIdx.x * b.ntiles) / g);
-    const uint32_t t_end = (uint32_t)(((uint64_t)(blockIdx.x + 1) * b.ntiles) / g);
-    for (uint32_t t = t_begin; t < t_end; t++) desc_tile<U, PIPE>(b, t);
-    return;
-  }
-  const uint32_t nchunks = (b.ntiles + b.grab - 1) / b.grab;
-  if constexpr (AHEAD) {
-    // Grab-ahead (engine option desc_ahead): the next tile is taken before
-    // the current one is folded and the first line of its record touched, so
-    // the queue atomic and the dependent record load overlap the current
-    // tile's data loads instead of sitting between two tiles.  Exactly one
-    // failing grab per workgroup, as the host's counter accounting expects:
-    // no further grab once one has failed.
-    __shared__ uint32_t next[2];
-    if (threadIdx.x == 0) {
-      next[0] = queue_grab(b.ctr, b.base);
-      next[1] = next[0] < nchunks ? queue_grab(b.ctr, b.base) : 0xFFFFFFFFu;
-    }
-    __syncthreads();
-    uint32_t c = __builtin_amdgcn_readfirstlane(next[0]);
-    uint32_t n1 = __builtin_amdgcn_readfirstlane(next[1]);
-    __syncthreads();  // both slots read before thread 0 rewrites one
-    while (c < nchunks) {
-      uint32_t g = 0xFFFFFFFFu;
-      if (threadIdx.x == 0 && n1 < nchunks) g = queue_grab(b.ctr, b.base);
-      // the next record's first line into the scalar cache: issued here (a
-      // volatile load is neither dropped nor sunk), consumed after the tile
-      uint32_t touch = 0;
-      if (n1 < nchunks)
-        touch = ((const volatile __attribute__((address_space(4))) uint32_t *)&cst(b.tiles)[n1 * b.grab].meta)[0];
-      const uint32_t t0 = c * b.grab;
-      const uint32_t t1 = min(t0 + b.grab, b.ntiles);
-      for (uint32_t t = t0; t < t1; t++) desc_tile<U, PIPE>(b, t);
-      __asm__ volatile("" ::"s"(touch));
-      if (threadIdx.x == 0) next[0] = g;
-      __syncthreads();
-      c = n1;
-      n1 = __builtin_amdgcn_readfirstlane(next[0]);
-      __syncthreads();  // every wave has read next[0] before it is rewritten
-    }
-    return;
-  }
-  // Work queue in grabs of b.grab consecutive tiles.
+  // Work queue, one tile per grab (two LDS slots as in stream_body).  A
+  // grab-ahead form (the next tile taken and its record touched before the
+  // current one is folded) measured no gain and is gone.
   __shared__ uint32_t next[2];
   if (threadIdx.x == 0) next[0] = queue_grab(b.ctr, b.base);
   __syncthreads();
-  uint32_t c = __builtin_amdgcn_readfirstlane(next[0]);
+  uint32_t t = __builtin_amdgcn_readfirstlane(next[0]);
   int slot = 0;
-  while (c < nchunks) {
-    const uint32_t t0 = c * b.grab;
-    const uint32_t t1 = min(t0 + b.grab, b.ntiles);
-    for (uint32_t t = t0; t < t1; t++) desc_tile<U, PIPE>(b, t);
+  while (t < b.ntiles) {
+    desc_tile<U, PIPE>(b, t);
     slot ^= 1;
     if (threadIdx.x == 0) next[slot] = queue_grab(b.ctr, b.base);
     __syncthreads();
-    c = __builtin_amdgcn_readfirstlane(next[slot]);
+    t = __builtin_amdgcn_readfirstlane(next[slot]);
   }
 }
 
@@ -667,11 +611,10 @@ __global__ __launch_bounds__(kBlock) void xor_desc(DescBatch b) {
   desc_body<U, 0>(b);
 }
 
-// Rolling-window load variants (A/B: engine option desc_pipe; fold_cover),
-// and the grab-ahead form (desc_ahead).
-template <int U, int PIPE, int AHEAD = 0>
+// The rolling-window form (PipeShape): U = 8 and 16.
+template <int U, int PIPE>
 __global__ __launch_bounds__(kBlock) void xor_desc_p(DescBatch b) {
-  desc_body<U, PIPE, AHEAD>(b);
+  desc_body<U, PIPE>(b);
 }
 
 // ---------------------------------------------------------------------------
@@ -973,18 +916,8 @@ static hipError_t launch_stream_nu(hipStream_t st, int grid, const StreamArgs &a
   return hipGetLastError();
 }
 
-template <int NSRC, int U, int GATHER>
-static hipError_t launch_static_nu(hipStream_t st, int grid, const StreamArgs &a) {
-  hipLaunchKernelGGL((xor_stream<NSRC, U, GATHER, kStatic>), dim3(grid), dim3(kBlock), 0, st, a);
-  return hipGetLastError();
-}
-
 template <int U, int GATHER>
 static hipError_t launch_stream_u(hipStream_t st, int grid, const StreamArgs &a) {
-  // The static schedule (A/B only) is instantiated for the hot width and the
-  // runtime-width kernel only.
-  if (a.sched == kSchedStatic)
-    return a.nsrc == 8 ? launch_static_nu<8, U, GATHER>(st, grid, a) : launch_static_nu<0, U, GATHER>(st, grid, a);
 #define BCP_NSRC_CASE(n) \
   case n: return launch_stream_nu<n, U, GATHER>(st, grid, a);
   switch (a.nsrc) {
@@ -1003,40 +936,31 @@ uint32_t stream_tiles_per_stripe(uint64_t chunk_bytes, int vecs) {
   return (uint32_t)((vps + tile_v - 1) / tile_v);
 }
 
-hipError_t launch_xor_stream(hipStream_t st, int grid, int vecs, bool gather, const StreamArgs &a, int wpe) {
+hipError_t launch_xor_stream(hipStream_t st, int grid, int vecs, bool gather, const StreamArgs &a) {
   if (a.ntiles == 0) return hipSuccess;
-  // Register budget (stream_wpe / table_wpe; profiles/r01/depth/ab18_wpe_widths.jsonl):
-  // W = 6 is +0.8 (N = 8), +0.9..+6.6 (N = 5..7 at U = 8) and +0.3..+3.8
-  // (N = 9..12, 16 at U = 4; ab19) on the strided form, but -1.4 / -4.5 at N = 3 / 4
-  // (W = 5 / 7 there: -1.1 / -1.6 at N = 3, -1.7 / +0.45 at N = 4; ab20),
-  // which keep the compiler's schedule; the pointer-table form has it for
-  // N = 8 (+0.1).  W = 5 / 7 exist for N = 8 as A/B points.
-  if (wpe && a.sched == kSchedQueue) {
-    if (vecs == 8 && a.nsrc == 8) {
-      switch (wpe) {
-        case 5: return gather ? launch_stream_w<8, 8, 1, 5>(st, grid, a) : launch_stream_w<8, 8, 0, 5>(st, grid, a);
-        case 6: return gather ? launch_stream_w<8, 8, 1, 6>(st, grid, a) : launch_stream_w<8, 8, 0, 6>(st, grid, a);
-        case 7: return gather ? launch_stream_w<8, 8, 1, 7>(st, grid, a) : launch_stream_w<8, 8, 0, 7>(st, grid, a);
-        default: break;
-      }
+  // Register budget W = 6 (profiles/r01/depth/ab18_wpe_widths.jsonl): +0.8
+  // (N = 8), +0.9..+6.6 (N = 5..7 at U = 8) and +0.3..+3.8 (N = 9..12, 16 at
+  // U = 4; ab19) on the strided form, but -1.4 / -4.5 at N = 3 / 4 (W = 5 /
+  // 7 there: -1.1 / -1.6 at N = 3, -1.7 / +0.45 at N = 4; ab20), which keep
+  // the compiler's schedule; the pointer-table form takes it for N = 8 (+0.1).
+  if (vecs == 8 && a.nsrc == 8)
+    return gather ? launch_stream_w<8, 8, 1, 6>(st, grid, a) : launch_stream_w<8, 8, 0, 6>(st, grid, a);
+  if (!gather && vecs == 8) {
+    switch (a.nsrc) {
+      case 5: return launch_stream_w<5, 8, 0, 6>(st, grid, a);
+      case 6: return launch_stream_w<6, 8, 0, 6>(st, grid, a);
+      case 7: return launch_stream_w<7, 8, 0, 6>(st, grid, a);
+      default: break;
     }
-    if (wpe == 6 && !gather && vecs == 8) {
-      switch (a.nsrc) {
-        case 5: return launch_stream_w<5, 8, 0, 6>(st, grid, a);
-        case 6: return launch_stream_w<6, 8, 0, 6>(st, grid, a);
-        case 7: return launch_stream_w<7, 8, 0, 6>(st, grid, a);
-        default: break;
-      }
-    }
-    if (wpe == 6 && !gather && vecs == 4) {
-      switch (a.nsrc) {
-        case 9: return launch_stream_w<9, 4, 0, 6>(st, grid, a);
-        case 10: return launch_stream_w<10, 4, 0, 6>(st, grid, a);
-        case 11: return launch_stream_w<11, 4, 0, 6>(st, grid, a);
-        case 12: return launch_stream_w<12, 4, 0, 6>(st, grid, a);
-        case 16: return launch_stream_w<16, 4, 0, 6>(st, grid, a);
-        default: break;
-      }
+  }
+  if (!gather && vecs == 4) {
+    switch (a.nsrc) {
+      case 9: return launch_stream_w<9, 4, 0, 6>(st, grid, a);
+      case 10: return launch_stream_w<10, 4, 0, 6>(st, grid, a);
+      case 11: return launch_stream_w<11, 4, 0, 6>(st, grid, a);
+      case 12: return launch_stream_w<12, 4, 0, 6>(st, grid, a);
+      case 16: return launch_stream_w<16, 4, 0, 6>(st, grid, a);
+      default: break;
     }
   }
   if (gather) {
@@ -1062,36 +986,22 @@ hipError_t launch_desc_tiles(hipStream_t st, const DescBatch &b) {
   return hipGetLastError();
 }
 
-hipError_t launch_xor_desc(hipStream_t st, int grid, int vecs, const DescBatch &b, int pipe, int ahead) {
+hipError_t launch_xor_desc(hipStream_t st, int grid, int vecs, const DescBatch &b) {
   if (b.ntiles == 0) return hipSuccess;
   if ((uint32_t)grid > b.ntiles) grid = (int)b.ntiles;
-  if (ahead && pipe == 5 && vecs == 8 && b.sched == kSchedQueue) {
-    hipLaunchKernelGGL((xor_desc_p<8, 5, 1>), dim3(grid), dim3(kBlock), 0, st, b);
-    return hipGetLastError();
-  }
   if (vecs == 16) {
     // 64 KiB subtiles (engine option desc_vecs_per_thread 16): half the queue
-    // grabs and record loads of U = 8; always through the rolling window
-    if (pipe == 6) hipLaunchKernelGGL((xor_desc_p<16, 6>), dim3(grid), dim3(kBlock), 0, st, b);
-    else hipLaunchKernelGGL((xor_desc_p<16, 5>), dim3(grid), dim3(kBlock), 0, st, b);
+    // grabs and record loads of U = 8
+    hipLaunchKernelGGL((xor_desc_p<16, 5>), dim3(grid), dim3(kBlock), 0, st, b);
     return hipGetLastError();
   }
-  if (pipe == 6 && vecs == 8) {
-    hipLaunchKernelGGL((xor_desc_p<8, 6>), dim3(grid), dim3(kBlock), 0, st, b);
+  if (vecs == 8) {
+    hipLaunchKernelGGL((xor_desc_p<8, 5>), dim3(grid), dim3(kBlock), 0, st, b);
     return hipGetLastError();
-  }
-  if (pipe && vecs == 8) {
-    switch (pipe) {
-      case 2: hipLaunchKernelGGL((xor_desc_p<8, 2>), dim3(grid), dim3(kBlock), 0, st, b); return hipGetLastError();
-      case 4: hipLaunchKernelGGL((xor_desc_p<8, 4>), dim3(grid), dim3(kBlock), 0, st, b); return hipGetLastError();
-      case 5: hipLaunchKernelGGL((xor_desc_p<8, 5>), dim3(grid), dim3(kBlock), 0, st, b); return hipGetLastError();
-      default: break;
-    }
   }
   switch (vecs) {
     case 1: hipLaunchKernelGGL((xor_desc<1>), dim3(grid), dim3(kBlock), 0, st, b); break;
     case 4: hipLaunchKernelGGL((xor_desc<4>), dim3(grid), dim3(kBlock), 0, st, b); break;
-    case 8: hipLaunchKernelGGL((xor_desc<8>), dim3(grid), dim3(kBlock), 0, st, b); break;
     default: hipLaunchKernelGGL((xor_desc<2>), dim3(grid), dim3(kBlock), 0, st, b); break;
   }
   return hipGetLastError();

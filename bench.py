@@ -74,9 +74,6 @@ def parse():
     ap.add_argument("--chunk", type=int, default=512 * KiB)
     ap.add_argument("--blocks-per-cu", type=int, default=0)
     ap.add_argument("--vecs", type=int, default=0)
-    ap.add_argument("--schedule", type=int, default=-1,
-                    help="tile schedule of the timed kernel: 0 work queue, 1 static ranges (default: engine's)")
-    ap.add_argument("--grab", type=int, default=0, help="tiles per work-queue grab of the descriptor kernel")
     ap.add_argument("--grid", type=int, default=0, help="explicit workgroup count of the streaming kernel (A/B)")
     ap.add_argument("--contig", action="store_true", help="physically contiguous device allocations (A/B knob)")
     ap.add_argument("--opt", action="append", default=[], metavar="KEY=VALUE",
@@ -197,8 +194,6 @@ def main():
             eng.option("desc_vecs_per_thread", a.vecs)
     elif a.blocks_per_cu or a.vecs:
         eng.tune(a.blocks_per_cu, a.vecs)
-    if a.grab:
-        eng.option("desc_grab", a.grab)
     if a.grid:
         eng.option("stream_grid", a.grid)
     if a.contig:
@@ -206,8 +201,6 @@ def main():
     for kv in a.opt:
         k, v = kv.split("=")
         eng.option(k, int(v))
-    if a.schedule >= 0:
-        eng.option("schedule" if a.mode != "mixed" else "desc_schedule", a.schedule)
     cus, devname = eng.info()
     q = eng.queue()
     # config 2 (100k chunks per GPU) up to 4 GPUs; at 8 GPUs config 4: 1,000,000
@@ -268,7 +261,6 @@ def main():
         bytes_per_step = S * (N + 1) * C
         kernel = "xor_stream<{N},{U},strided>"
         kernel_tag = "xor_stream<{N}, {U}, 0, "
-        wpe = eng.option("stream_wpe")
         cfg = "config4" if d.world == 8 and S == 15_625 else "config2"
         workload = f"{cfg}: parity gen, {S} stripes x {N} x {C // KiB} KiB device-resident per GPU"
     else:
@@ -309,7 +301,6 @@ def main():
         bytes_per_step = S * (N + 1) * C
         kernel = "xor_stream<{N},{U},gather>"
         kernel_tag = "xor_stream<{N}, {U}, 1, "
-        wpe = eng.option("table_wpe")
         workload = (f"config3: rebuild, {S} stripes x ({N - 1} survivors + parity) x {C // KiB} KiB device-resident, "
                     f"{a.rebuild_layout} layout")
 
@@ -331,23 +322,21 @@ def main():
     kern_ms = q.elapsed_ms(0, 1) / a.steps  # avg launch duration on the kernel's stream
     if a.mode == "mixed":  # the descriptor kernel's form and tile size of the timed launches
         U = eng.option("last_desc_vecs")
-        pipe = eng.option("desc_pipe") if U == 8 else 0
+        pipe = 5 if U >= 8 else 0  # the rolling-window form at U = 8 and 16 (launch_xor_desc)
         if eng.option("last_desc_form") == 2:
             kernel, kernel_tag = f"xor_desc_args<{U}>", f"xor_desc_args<{U}>"
         else:
-            ahead = eng.option("desc_ahead") if pipe == 5 else 0
             kernel = f"xor_desc_p<{U},{pipe}>" if pipe else f"xor_desc<{U}>"
-            kernel_tag = f"xor_desc_p<{U}, {pipe}, {ahead}>" if pipe else f"xor_desc<{U}>"
+            kernel_tag = f"xor_desc_p<{U}, {pipe}>" if pipe else f"xor_desc<{U}>"
     if a.mode != "mixed":  # tile size the engine chose for the timed launches
         U = eng.option("last_stream_vecs")
-        # register-budget instantiations (launch_xor_stream in bcp_kernels.hip)
-        budget = a.schedule <= 0 and wpe and (
-            (N == 8 and U == 8) or (a.mode == "gen" and wpe == 6 and ((5 <= N <= 7 and U == 8) or
-                                                                      (N in (9, 10, 11, 12, 16) and U == 4))))
+        # register-budget (W = 6) instantiations (launch_xor_stream in bcp_kernels.hip)
+        budget = (N == 8 and U == 8) or (a.mode == "gen" and ((5 <= N <= 7 and U == 8) or
+                                                              (N in (9, 10, 11, 12, 16) and U == 4)))
         if budget:
             form, g = ("gather", 1) if a.mode == "rebuild" else ("strided", 0)
-            kernel = "xor_stream_w<{N},{U},%s,wpe%d>" % (form, wpe)
-            kernel_tag = "xor_stream_w<{N}, {U}, %d, 0, %d>" % (g, wpe)
+            kernel = "xor_stream_w<{N},{U},%s,wpe6>" % form
+            kernel_tag = "xor_stream_w<{N}, {U}, %d, 0, 6>" % g
         NS = N if (1 <= N <= 12 or N == 16) else 0  # widths without a specialisation run xor_stream<0, ...>
         kernel, kernel_tag = kernel.format(N=NS, U=U), kernel_tag.format(N=NS, U=U)
 

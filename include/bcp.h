@@ -184,38 +184,37 @@ int bcp_queue_elapsed_ms(bcp_queue *q, int slot_from, int slot_to,
 
 /* Tuning knobs for the fast path (bench / autotune only; 0 = default). */
 int bcp_set_tuning(bcp_engine *eng, int blocks_per_cu, int vecs_per_thread);
-/* Named knob: "blocks_per_cu" (1..32), "vecs_per_thread" (1,2,4,8; 0 = the
- * default: 8, or 4 / 2 for batches of few tiles) of the uniform streaming
- * kernel; "desc_blocks_per_cu" (0 = the default, one per CU; 1..32),
- * "desc_vecs_per_thread" (1,2,4,8,16; 16 = 64 KiB subtiles, batches through
- * desc_tiles only -- small batches in the kernel arguments use 8)
- * of the descriptor kernel; "schedule" (0 = device-wide tile work queue, the
- * default; 1 = a static contiguous tile range per workgroup, kept for A/B
- * measurements) for the uniform streaming kernel; "desc_schedule" (same
- * values, default 0), "desc_grab" (tiles per work-queue grab, 1..64, default
- * 1) and "desc_force" (1 = uniform batches take the descriptor kernel too;
- * A/B only) for the descriptor kernel (mixed sizes, windows, unaligned);
- * "stream_grid" (explicit workgroup count of the streaming kernel; 0 = the
- * default, blocks_per_cu on 29 of every 32 CUs), "desc_grid" (the same for
- * the descriptor kernel), "contiguous_alloc" (1: bcp_dev_alloc requests
- * physically contiguous memory for buffers of 64 MiB and more; default 0),
- * "table_host_max" / "desc_table_host_max" (bytes: staged descriptor tables
- * up to this size are read by the kernels from pinned host memory instead of
- * being copied to the device first; defaults 4096 / 131072), "stream_wpe"
- * (register budget of the 8-source strided streaming kernel in waves per
- * SIMD: 0 = the compiler's, 5, 6 = default, 7), "desc_pipe" (rolling load
- * window of the descriptor kernel: 0 = every load first, 2, 4, 5 = default:
- * 4 and tiles wider than 8 sources windowed too, 6 = 5 with half the loads
- * per unit), "stream_grab" (tiles per
- * work-queue grab of the streaming kernel for stripes of 1-4 sources, 1..64;
- * 0 = the default, 2), "sync_mode" (bcp_queue_sync: 0 = hipStreamSynchronize,
- * the default; 1 = wait on a blocking-sync event),
- * "host_registered" (bcp_host_alloc / bcp_host_alloc_mapped: 1 = ordinary
- * huge-page memory registered with HIP, the default -- CPU copies into and
- * out of it run at malloc speed; 0 = hipHostMalloc; env BCP_HOST_REGISTERED). */
+/* Named knob (unknown keys and out-of-range values: -EINVAL):
+ *  uniform streaming kernel: "blocks_per_cu" (1..32, default 1),
+ *   "vecs_per_thread" (1, 2, 4, 8; 0 = the default: 8, or 4 / 2 for batches
+ *   of few tiles), "stream_grid" (explicit workgroup count; 0 = the default,
+ *   blocks_per_cu on 29 of every 32 CUs), "table_host_max" (bytes: a
+ *   pointer table up to this size is read from pinned host memory instead of
+ *   being copied first; default 4096);
+ *  descriptor kernel (mixed sizes, windows, unaligned): "desc_blocks_per_cu"
+ *   (0 = the default, one per CU; 1..32), "desc_vecs_per_thread" (1, 2, 4,
+ *   8, 16; 0 = by batch size; 16 = 64 KiB subtiles, batches through
+ *   desc_tiles only -- small batches in the kernel arguments use 8),
+ *   "desc_grid" (explicit workgroup count; 0 = default), "desc_args_max"
+ *   (batches of at most this many stripes, 0..16, travel in the kernel
+ *   arguments; default 16), "desc_table_host_max" (as table_host_max;
+ *   default 131072), "desc_reuse_records" (1: a batch resubmitted on a ring
+ *   slot with byte-identical staged tables reuses that slot's tile records;
+ *   default 0, an A/B knob);
+ *  memory: "contiguous_alloc" (1: bcp_dev_alloc requests physically
+ *   contiguous memory for buffers of 64 MiB and more; default 0),
+ *   "host_registered" (bcp_host_alloc / bcp_host_alloc_mapped: 1 = ordinary
+ *   huge-page memory registered with HIP, the default -- CPU copies into and
+ *   out of it run at malloc speed; 0 = hipHostMalloc; env
+ *   BCP_HOST_REGISTERED).
+ * The kernels' schedule (device-wide tile work queue), register budgets and
+ * load windows are fixed: the alternatives lost the r01-r03 sweeps
+ * (DESIGN.md section 4). */
 int bcp_set_option(bcp_engine *eng, const char *key, int value);
-/* Current value of a named knob (same keys; "last_stream_vecs": the
- * vecs_per_thread of the engine's latest streaming-kernel launch). */
+/* Current value of a named knob (same keys), or of the engine's latest
+ * launch: "last_stream_vecs" (vecs_per_thread of the streaming kernel),
+ * "last_desc_vecs" and "last_desc_form" (descriptor kernel: 1 = desc_tiles +
+ * xor_desc, 2 = xor_desc_args). */
 int bcp_get_option(bcp_engine *eng, const char *key, int *value);
 /* Timer slots for bcp_queue_mark / bcp_queue_elapsed_ms. */
 #define BCP_TIMER_SLOTS 64

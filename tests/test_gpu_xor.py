@@ -155,17 +155,14 @@ def test_strided_layout(oracle, dev, queue):
         assert np.array_equal(out[s * pitch:s * pitch + chunk], ref)
 
 
-@pytest.mark.parametrize("sched", [0, 1])
 @pytest.mark.parametrize("bpc,vecs", [(1, 1), (2, 4), (4, 2), (8, 1), (16, 4), (1, 8), (3, 8)])
-def test_tuning_variants_agree(oracle, engine, dev, queue, bpc, vecs, sched):
+def test_tuning_variants_agree(oracle, engine, dev, queue, bpc, vecs):
     nstripes, nsrc, chunk = 7, 8, 524288 + 4096
-    rng = np.random.default_rng(bpc * 10 + vecs + 100 * sched)
+    rng = np.random.default_rng(bpc * 10 + vecs)
     data = rng.integers(0, 256, size=nstripes * nsrc * chunk, dtype=np.uint8)
     src = dev.put(data)
     dst = dev.alloc(nstripes * chunk)
     engine.tune(bpc, vecs)
-    engine.option("schedule", sched)
-    engine.option("desc_schedule", sched)
     engine.option("desc_blocks_per_cu", bpc)
     engine.option("desc_vecs_per_thread", vecs)
     try:
@@ -175,8 +172,6 @@ def test_tuning_variants_agree(oracle, engine, dev, queue, bpc, vecs, sched):
         res = gpu_stripes(dev, queue, [dict(chunks=[data[:1000], data[5:70000], None], out_len=70000 - 5)])
     finally:
         engine.tune(0, 0)
-        engine.option("schedule", 0)
-        engine.option("desc_schedule", 0)
         engine.option("desc_blocks_per_cu", 0)
         engine.option("desc_vecs_per_thread", 0)
     ref = np.bitwise_xor.reduce(data.reshape(nstripes, nsrc, chunk), axis=1).reshape(-1)
@@ -272,8 +267,9 @@ def test_uniform_batch_with_byte_tail(oracle, dev, queue, out_len):
 
 def test_work_queue_back_to_back_and_two_queues(oracle, engine, dev, queue):
     """The work-queue counter is monotone per queue: many launches in a row on
-    one queue, a second queue interleaved, and a switch to the static schedule
-    and back must all cover every tile exactly once."""
+    one queue, a second queue interleaved, and a change of tile size and grid
+    (different tile and failing-grab counts per launch) and back must all cover
+    every tile exactly once."""
     rng = np.random.default_rng(77)
     q2 = engine.queue()
     try:
@@ -285,9 +281,9 @@ def test_work_queue_back_to_back_and_two_queues(oracle, engine, dev, queue):
             queue.sync()  # the upload ran on `queue`; q2's kernel must see it
             q = queue if i % 3 else q2
             if i == 10:
-                engine.option("schedule", 1)
+                engine.tune(3, 2)
             if i == 14:
-                engine.option("schedule", 0)
+                engine.tune(0, 0)
             q.xor_uniform(dst, src, ns, n, chunk)
             jobs.append((data, dst, ns, n, chunk))
         q2.sync()
@@ -296,7 +292,7 @@ def test_work_queue_back_to_back_and_two_queues(oracle, engine, dev, queue):
             ref = np.bitwise_xor.reduce(data.reshape(ns, n, chunk), axis=1).reshape(-1)
             assert np.array_equal(out, ref)
     finally:
-        engine.option("schedule", 0)
+        engine.tune(0, 0)
         q2.close()
 
 
@@ -407,28 +403,24 @@ def test_small_batches_in_kernel_arguments(oracle, engine, dev, queue, nstripes,
             assert np.array_equal(o, r), (scale, i)
 
 
-@pytest.mark.parametrize("ahead", [0, 1])
 @pytest.mark.parametrize("side", [1, 0])
-def test_large_mixed_batch_side_stream_tiles(oracle, engine, dev, queue, side, ahead):
+def test_large_mixed_batch_side_stream_tiles(oracle, engine, dev, queue, side):
     """A batch large enough for desc_tiles to run on the side stream (>= 2 x
-    grid tiles), submitted twice back to back (the second desc_tiles overlaps
-    the first fold, on another ring slot's records): both outputs exact."""
+    grid tiles; side 1), or one past the argument form but below that (side 0:
+    desc_tiles in line), submitted twice back to back (the second desc_tiles
+    overlaps the first fold, on another ring slot's records): both outputs
+    exact."""
     rng = np.random.default_rng(77 + side)
-    prev = engine.option("desc_side_tiles")
-    engine.option("desc_side_tiles", side)
-    engine.option("desc_ahead", ahead)
-    try:
-        stripes, refs = [], []
-        for _ in range(60):
-            lens = [int(x) for x in np.exp(rng.uniform(np.log(64 * KiB), np.log(4 * MiB), size=8))]
-            chunks = [rng.integers(0, 256, size=L, dtype=np.uint8) for L in lens]
-            stripes.append(dict(chunks=chunks, out_len=max(lens)))
-            refs.append(oracle.xor_padded_np(chunks))
-        a = gpu_stripes(dev, queue, stripes)
-        b = gpu_stripes(dev, queue, stripes)
-    finally:
-        engine.option("desc_side_tiles", prev)
-        engine.option("desc_ahead", 0)
+    nstripes, top = (60, 4 * MiB) if side else (20, 256 * KiB)
+    stripes, refs = [], []
+    for _ in range(nstripes):
+        lens = [int(x) for x in np.exp(rng.uniform(np.log(64 * KiB), np.log(top), size=8))]
+        chunks = [rng.integers(0, 256, size=L, dtype=np.uint8) for L in lens]
+        stripes.append(dict(chunks=chunks, out_len=max(lens)))
+        refs.append(oracle.xor_padded_np(chunks))
+    a = gpu_stripes(dev, queue, stripes)
+    assert engine.option("last_desc_form") == 1
+    b = gpu_stripes(dev, queue, stripes)
     for i, (x, y, r) in enumerate(zip(a, b, refs)):
         assert np.array_equal(x, r) and np.array_equal(y, r), i
 
@@ -526,18 +518,20 @@ def test_survey_kats_on_gpu(oracle, dev, queue):
         assert hashlib.sha256(hdr + out.tobytes()).hexdigest() == k["sha256"], name
 
 
-@pytest.mark.parametrize("knob,value", [("stream_wpe", w) for w in (0, 5, 6, 7)] + [("table_wpe", w) for w in (5, 6, 7)] +
-                         [("desc_pipe", p) for p in (0, 2, 4, 5, 6)])
-def test_schedule_variants_agree(oracle, engine, dev, queue, knob, value):
-    """A/B kernel variants (register budget of xor_stream<8,8>, rolling load
-    window of xor_desc<8>): same bytes as the oracle on full and partial
-    streaming tiles (strided and pointer table) and on descriptor tiles with
-    1..8 covering sources."""
-    rng = np.random.default_rng(value * 7 + len(knob))
+@pytest.mark.parametrize("args_max", [16, 0])
+@pytest.mark.parametrize("knob,value", [("vecs_per_thread", v) for v in (1, 2, 4, 8)] +
+                         [("desc_vecs_per_thread", v) for v in (1, 2, 4, 8, 16)])
+def test_kernel_forms_agree(oracle, engine, dev, queue, knob, value, args_max):
+    """Every instantiated tile size of both kernels -- xor_stream<8,U> and its
+    register-budget form at U = 8 (strided and pointer table, full and partial
+    tiles), xor_desc<U> and the rolling-window xor_desc_p<8|16, 5>, through
+    desc_tiles (args_max 0) or the argument form -- gives the oracle's bytes on
+    descriptor tiles with 1..8 covering sources."""
+    rng = np.random.default_rng(value * 7 + len(knob) + args_max)
     nstripes, nsrc = 5, 8
     default = engine.option(knob)
     engine.option(knob, value)
-    engine.tune(0, 8)
+    engine.option("desc_args_max", args_max)
     try:
         res = {}
         for chunk in (512 * KiB, 512 * KiB + 4096 + 16):
@@ -557,9 +551,13 @@ def test_schedule_variants_agree(oracle, engine, dev, queue, knob, value):
         stripes = [dict(chunks=[rng.integers(0, 256, size=L, dtype=np.uint8) for L in lens], out_len=max(lens))
                    for lens in shapes]
         outs = gpu_stripes(dev, queue, stripes)
+        if knob == "desc_vecs_per_thread":
+            form = engine.option("last_desc_form")
+            assert form == (1 if args_max == 0 else 2)  # (the argument form runs U = 16 as 8)
+            assert engine.option("last_desc_vecs") == (value if form == 1 else min(value, 8))
     finally:
         engine.option(knob, default)
-        engine.tune(0, 0)
+        engine.option("desc_args_max", 16)
     for o, st in zip(outs, stripes):
         assert np.array_equal(o, oracle.xor_padded_np(st["chunks"]))
 
@@ -770,22 +768,11 @@ KNOBS = {
     "desc_blocks_per_cu": (0, [0, 1, 32], [-1, 33]),
     "desc_vecs_per_thread": (0, [0, 1, 2, 4, 8, 16], [3, 32]),
     "desc_args_max": (16, [0, 1, 16], [-1, 17]),
-    "desc_ahead": (0, [0, 1], [2]),
-    "desc_side_tiles": (1, [0, 1], [2]),
-    "schedule": (0, [0, 1], [2]),
-    "desc_schedule": (0, [0, 1], [2]),
-    "desc_grab": (1, [1, 64], [0, 65]),
-    "desc_force": (0, [0, 1], [2]),
     "stream_grid": (0, [0, 1, 65536], [-1, 65537]),
     "desc_grid": (0, [0, 7], [-1]),
     "contiguous_alloc": (0, [0, 1], [2]),
     "table_host_max": (4096, [0, 1 << 24], [-1, (1 << 24) + 1]),
     "desc_table_host_max": (128 * 1024, [0, 1 << 24], [-1]),
-    "stream_wpe": (6, [0, 5, 6, 7], [1, 4, 8]),
-    "table_wpe": (6, [0, 5, 6, 7], [4, 8]),
-    "desc_pipe": (5, [0, 2, 4, 5, 6], [1, 3, 7]),
-    "stream_grab": (0, [0, 1, 64], [-1, 65]),
-    "sync_mode": (0, [0, 1], [2]),
     "host_registered": (1, [0, 1], [2]),
     "desc_reuse_records": (0, [0, 1], [2, -1]),
 }
@@ -814,15 +801,14 @@ def test_unknown_knob_refused(bcp, engine):
         engine.option("no_such_knob")
 
 
-@pytest.mark.parametrize("grab", [0, 1, 2, 3, 8])
+@pytest.mark.parametrize("vecs", [0, 1, 8])
 @pytest.mark.parametrize("nsrc", [1, 2, 3, 4])
-def test_narrow_stripes_multi_tile_grabs(engine, dev, queue, nsrc, grab):
-    """Stripes of 1-4 sources take several tiles per work-queue grab
-    (stream_grab; 0 = auto): every tile folded exactly once, full and
-    partial last tiles, strided and pointer-table forms."""
-    default = engine.option("stream_grab")
-    rng = np.random.default_rng(nsrc * 10 + grab)
-    engine.option("stream_grab", grab)
+def test_narrow_stripes_multi_tile_grabs(engine, dev, queue, nsrc, vecs):
+    """Stripes of 1-4 sources take two tiles per work-queue grab: every tile
+    folded exactly once (odd and even tile counts, full and partial last
+    tiles), strided and pointer-table forms."""
+    rng = np.random.default_rng(nsrc * 10 + vecs)
+    engine.tune(0, vecs)
     try:
         for nstripes, chunk in ((37, 512 * KiB), (5, 3 * 32 * KiB + 48), (1, 16)):
             data = rng.integers(0, 256, size=nstripes * nsrc * chunk, dtype=np.uint8)
@@ -836,7 +822,7 @@ def test_narrow_stripes_multi_tile_grabs(engine, dev, queue, nsrc, grab):
                               [(src + (s * nsrc + k) * chunk, chunk) for s in range(nstripes) for k in range(nsrc)])
             assert np.array_equal(dev.get(dst2, nstripes * chunk), ref), (nstripes, chunk)
     finally:
-        engine.option("stream_grab", default)
+        engine.tune(0, 0)
 
 
 @pytest.mark.parametrize("nsrc", [5, 6, 7, 9, 10, 11, 12, 16])
@@ -889,13 +875,12 @@ def test_launch_after_pending_query_keeps_the_work_queue(bcp, engine, dev, queue
     assert np.array_equal(got, ref)
 
 
-@pytest.mark.parametrize("pipe", [5, 6])
-def test_descriptor_u16_mixed_batch(oracle, engine, dev, queue, pipe):
-    """64 KiB descriptor subtiles (desc_vecs_per_thread 16, rolling window 5
-    or 6) on a config-5-like batch -- log-uniform 1 KiB..1.5 MiB lengths,
+def test_descriptor_u16_mixed_batch(oracle, engine, dev, queue):
+    """64 KiB descriptor subtiles (desc_vecs_per_thread 16, the rolling
+    window) on a config-5-like batch -- log-uniform 1 KiB..1.5 MiB lengths,
     widths 1..12 (wide tiles), misaligned sources and outputs, zero-length
     chunks -- through desc_tiles + xor_desc_p, against the oracle."""
-    rng = np.random.default_rng(1600 + pipe)
+    rng = np.random.default_rng(1605)
     stripes, refs = [], []
     for _ in range(40):
         n = int(rng.integers(1, 13))
@@ -906,9 +891,8 @@ def test_descriptor_u16_mixed_batch(oracle, engine, dev, queue, pipe):
         pads = [int(x) for x in rng.integers(0, 16, size=n)]
         stripes.append(dict(chunks=chunks, out_len=max(lens), pads=pads, dst_pad=int(rng.integers(0, 16))))
         refs.append(oracle.xor_padded_np(chunks))
-    prev = {k: engine.option(k) for k in ("desc_vecs_per_thread", "desc_pipe", "desc_args_max")}
+    prev = {k: engine.option(k) for k in ("desc_vecs_per_thread", "desc_args_max")}
     engine.option("desc_vecs_per_thread", 16)
-    engine.option("desc_pipe", pipe)
     engine.option("desc_args_max", 0)
     try:
         outs = gpu_stripes(dev, queue, stripes)

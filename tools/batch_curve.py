@@ -5,10 +5,11 @@ stripes, device-resident.  For each batch size and each entry point:
   stream  bcp_xor_uniform_async (xor_stream<8,U>, the config-2 kernel)
   table   bcp_xor_stripes_async with a descriptor table of the same stripes
           (uniform: host staging + the pointer-table xor_stream, the rebuild form)
-  desc    the same call with engine option desc_force = 1: the descriptor
-          kernel (batches of <= 16 stripes in the kernel arguments, xor_desc_args;
+  desc    the same stripes with the first stripe's last source 16 bytes short
+          (zero padding: not uniform, so the descriptor kernel takes the batch;
+          batches of <= 16 stripes in the kernel arguments, xor_desc_args;
           larger ones host staging + desc_tiles + xor_desc, the config-5 kernel)
-  desc_tiles  desc_force = 1 and desc_args_max = 0: always desc_tiles + xor_desc
+  desc_tiles  as desc with desc_args_max = 0: always desc_tiles + xor_desc
 
 two figures:
   pipelined_us  launches back to back, HIP-event time per launch on the queue
@@ -53,31 +54,33 @@ q.fill_synthetic(src, smax * N * C, seed=1)
 q.sync()
 
 
-def tables(s):
+def tables(s, short=0):
     stripes = (bcp.Stripe * s)(*[bcp.Stripe(dst + i * C, C, i * N, N, 0) for i in range(s)])
-    sources = (bcp.Source * (s * N))(*[bcp.Source(src + (i * N + k) * C, C) for i in range(s) for k in range(N)])
+    sources = (bcp.Source * (s * N))(*[bcp.Source(src + (i * N + k) * C, C - (short if i * N + k == N - 1 else 0))
+                                        for i in range(s) for k in range(N)])
     return stripes, sources
 
 
 for s in batches:
     nbytes = s * (N + 1) * C
     st, so = tables(s)
+    dst_, dso = tables(s, short=16)
     L = bcp.lib()
     table = lambda: bcp.check("xor_stripes", L.bcp_xor_stripes_async(q.h, st, s, so, s * N))  # noqa: E731
+    desc = lambda: bcp.check("xor_stripes", L.bcp_xor_stripes_async(q.h, dst_, s, dso, s * N))  # noqa: E731
     entry = {
         "stream": lambda: q.xor_uniform(dst, src, s, N, C),
         "table": table,
-        "desc": table,
-        "desc_tiles": table,
+        "desc": desc,
+        "desc_tiles": desc,
     }
     runs = [(n, entry[n], None) for n in a.entries.split(",") if n]
     for thm in filter(None, a.table_host_max.split(",")):
-        runs += [("table", table, ("thm", int(thm))), ("desc", table, ("thm", int(thm)))]
+        runs += [("table", table, ("thm", int(thm))), ("desc", desc, ("thm", int(thm)))]
     for tun in filter(None, a.tunings.split(",")):
         u, bpc = (int(x) for x in tun.split(":"))
         runs.append(("stream", entry["stream"], (u, bpc)))
     for name, fn, tun in runs:
-        eng.option("desc_force", 1 if name.startswith("desc") else 0)
         eng.option("desc_args_max", 0 if name == "desc_tiles" else 16)
         if tun and tun[0] == "thm":
             eng.option("table_host_max", tun[1])

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Interleaved A/B sweep of the 8-wide fast-path knobs in ONE process
-(cdna_hip_programming.md §5.4 rule 24): blocks_per_cu x vecs_per_thread x
-schedule (0 work queue, 1 static contiguous), each launch timed alone with HIP events on the kernel's stream.
+(cdna_hip_programming.md §5.4 rule 24): blocks_per_cu x vecs_per_thread,
+each launch timed alone with HIP events on the kernel's stream.  (r01 also
+swept a static tile schedule, since removed: profiles/r01/sweep_fast*.jsonl.)
 Also compares back-to-back launches with isolated ones.
 
     python tools/sweep_fast.py [--stripes 12500] [--reps 5] > sweep.jsonl
@@ -23,9 +24,8 @@ ap.add_argument("--stripes", type=int, default=12500)
 ap.add_argument("--nsrc", type=int, default=8)
 ap.add_argument("--chunk", type=int, default=512 * 1024)
 ap.add_argument("--reps", type=int, default=5)
-ap.add_argument("--bpc", default="4,7,8,16")
-ap.add_argument("--vecs", default="1,2,4")
-ap.add_argument("--sched", default="0,1")
+ap.add_argument("--bpc", default="1,2,4")
+ap.add_argument("--vecs", default="2,4,8")
 a = ap.parse_args()
 
 eng = bcp.Engine(0)
@@ -36,14 +36,12 @@ out = eng.alloc(S * C)
 q.fill_synthetic(src, S * N * C, 1)
 q.sync()
 bytes_per = S * (N + 1) * C
-variants = list(itertools.product([int(x) for x in a.bpc.split(",")], [int(x) for x in a.vecs.split(",")],
-                                  [int(x) for x in a.sched.split(",")]))
+variants = list(itertools.product([int(x) for x in a.bpc.split(",")], [int(x) for x in a.vecs.split(",")]))
 res = {v: [] for v in variants}
 t_start = time.time()
 for rep in range(a.reps):
     for v in variants:
         eng.tune(v[0], v[1])
-        eng.option("schedule", v[2])
         q.xor_uniform(out, src, S, N, C)  # warm this variant
         q.mark(0)
         q.xor_uniform(out, src, S, N, C)
@@ -54,7 +52,7 @@ for rep in range(a.reps):
 rows = []
 for v, ts in res.items():
     med = statistics.median(ts)
-    rows.append({"blocks_per_cu": v[0], "vecs": v[1], "schedule": v[2], "median_ms": round(med, 4),
+    rows.append({"blocks_per_cu": v[0], "vecs": v[1], "median_ms": round(med, 4),
                  "min_ms": round(min(ts), 4), "GBps_median": round(bytes_per / med / 1e6, 1),
                  "frac_8TBs": round(bytes_per / med / 1e6 / 8000, 4)})
 rows.sort(key=lambda r: r["median_ms"])
@@ -62,9 +60,8 @@ for r in rows:
     print(json.dumps(r))
 
 # back-to-back vs isolated for the best and the default variant
-for v in (tuple(rows[0][k] for k in ("blocks_per_cu", "vecs", "schedule")), (16, 4, 1)):
+for v in (tuple(rows[0][k] for k in ("blocks_per_cu", "vecs")), (0, 0)):
     eng.tune(v[0], v[1])
-    eng.option("schedule", v[2])
     q.mark(2)
     for i in range(10):
         q.xor_uniform(out, src, S, N, C)
