@@ -14,7 +14,7 @@
  * connections (lane tag modulo their number) under a per-connection mutex
  * held from request to reply.
  *
- * Two ways to reach it: a rank pool (bcp_runner.c) forks the server with the
+ * Two ways to reach it: a rank pool (bcp_pool.c) forks the server with the
  * socket world's arena mapped at the same address in every process; an
  * independent process (an MPI rank) connects to a server on a Unix socket
  * (bcp_fold_server_connect) and passes its arena as a memfd, which the

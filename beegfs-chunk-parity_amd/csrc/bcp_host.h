@@ -12,7 +12,7 @@ int bcpi_inject_hit(int site);
 int bcpi_hip_touched(void);
 
 /* The P-role settings of this process (fold mode, fold service width, test
- * hook, window padding): a rank pool (bcp_runner.c) hands the caller's
+ * hook, window padding): a rank pool (bcp_pool.c) hands the caller's
  * settings to its rank processes with every run. */
 typedef struct {
     int fold_mode, fold_inflight, explicit_pad;
