@@ -346,8 +346,8 @@ int bcp_rank_pool_create(int ntargets, FILE *log, bcp_rank_pool **out)
     /* Node fold server (default; environment BCP_FOLD_SERVER=0 turns it
      * off; needs the shared arena): one process holds the GPU for every
      * rank's folds, over BCP_FOLD_SERVER_CONNS (default 12) connections per
-     * rank.  Config 5 over nine rank processes on one MI355X: 35-37 GiB/s,
-     * against 13-14 with a HIP context per rank (DESIGN.md §6.1 item 7). */
+     * rank.  Config 5 over nine rank processes on one MI355X (r02): 35-37 GiB/s,
+     * against 13-14 with a HIP context per rank (DESIGN.md §6.5). */
     int nconn = 0, *sfd = NULL, *rfd = NULL;
     void *alo = NULL, *ahi = NULL;
     const char *fs = getenv("BCP_FOLD_SERVER");
