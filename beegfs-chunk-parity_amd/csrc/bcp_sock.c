@@ -78,6 +78,7 @@ typedef struct sk_req {
     int done;
     uint64_t cts_addr, cts_cap; /* fill-send side: the receiver's answer */
     int ctl;                    /* waits on the control socket (a fill send's CTS) */
+    int busy;                   /* its payload is being read into buf by the socket's reader */
 } sk_req;
 
 struct bcp_sock_world {
@@ -265,11 +266,12 @@ int bcp_sock_world_create(int world_size, bcp_sock_world **out)
 {
     if (!out || world_size < 1 || world_size > 4096)
         return -EINVAL;
-    nofile_raise((size_t)2 * (size_t)world_size * (size_t)(world_size - 1));
     *out = NULL;
     bcp_sock_world *w = calloc(1, sizeof(*w));
     if (!w)
         return -ENOMEM;
+    /* from here every failure goes through bcp_sock_world_destroy, which releases it */
+    nofile_raise((size_t)2 * (size_t)world_size * (size_t)(world_size - 1));
     w->world = world_size;
     w->rank = -1;
     w->fds = malloc((size_t)world_size * (size_t)world_size * sizeof(int));
@@ -672,6 +674,8 @@ static int read_one(bcp_sock_world *w, int src)
         return read_control(w, src, &h);
     pthread_mutex_lock(&w->mu);
     sk_req *r = take_posted(w, src, h.tag);
+    if (r)
+        r->busy = 1; /* its waiter leaves it to us, even if the peer is failed meanwhile */
     pthread_mutex_unlock(&w->mu);
     if (r) {
         size_t c = h.len <= r->cap ? (size_t)h.len : r->cap;
@@ -681,6 +685,7 @@ static int read_one(bcp_sock_world *w, int src)
         pthread_mutex_lock(&w->mu);
         r->received = c;
         r->status = rc ? rc : (h.len <= r->cap ? 0 : -EMSGSIZE);
+        r->busy = 0;
         r->done = 1;
         pthread_mutex_unlock(&w->mu);
         return rc;
@@ -723,14 +728,17 @@ static int progress_until(bcp_sock_world *w, sk_req *r)
     pthread_mutex_lock(&w->mu);
     while (!r->done) {
         const int s = r->src;
-        if (w->dead[s]) {
+        if (w->dead[s] && !r->busy) {
+            /* (a request whose payload the reader is still copying is left
+             * to it: the peer can be failed by another thread -- a CTS that
+             * could not be sent, sk_irecv -- while that copy runs) */
             unlink_req(w, r); /* so nobody completes it after it is freed */
             r->status = -w->dead[s];
             r->done = 1;
             break;
         }
         int *rd = r->ctl ? &w->reading_ctl[s] : &w->reading[s];
-        if (*rd) {
+        if (*rd || r->busy) {
             pthread_cond_wait(&w->cv, &w->mu);
             continue;
         }
