@@ -1081,8 +1081,8 @@ struct DropinState {
   size_t cap = 0;
   ~DropinState() {
     if (q) {
+      bcp_queue_destroy(q);  // synchronises first: nothing uses dev below
       if (dev) bcp_dev_free(g_engine, dev);
-      bcp_queue_destroy(q);
     }
   }
 };
@@ -1111,10 +1111,12 @@ extern "C" int bcp_xor_parity(uint8_t *dst, size_t nbytes, const uint8_t *data, 
     st.cap = need;
   }
   char *dv = (char *)st.dev;
-  if ((rc = bcp_h2d_2d_async(st.q, dv, pitch, data, nbytes, nbytes, (size_t)nsources))) return rc;
   char *dout = dv + pitch * (size_t)nsources;
-  if ((rc = bcp_xor_strided_async(st.q, dout, pitch, dv, pitch * nsources, pitch, 1, (uint32_t)nsources, nbytes)))
-    return rc;
-  if ((rc = bcp_d2h_async(st.q, dst, dout, nbytes))) return rc;
-  return bcp_queue_sync(st.q);
+  if (!(rc = bcp_h2d_2d_async(st.q, dv, pitch, data, nbytes, nbytes, (size_t)nsources)) &&
+      !(rc = bcp_xor_strided_async(st.q, dout, pitch, dv, pitch * nsources, pitch, 1, (uint32_t)nsources, nbytes)))
+    rc = bcp_d2h_async(st.q, dst, dout, nbytes);
+  // also after a failed submission: nothing of this call stays in flight on
+  // the caller's buffers or the thread's device rows
+  const int src = bcp_queue_sync(st.q);
+  return rc ? rc : src;
 }

@@ -513,7 +513,8 @@ int bcp_pipeline_destroy(bcp_pipeline *pl)
         pool_stop(&pl->writers);
     }
     if (pl->dev) {
-        free_slots(pl);
+        /* queues first (each synchronises its streams): no copy or kernel may
+         * still use a slot when its memory goes */
         for (int d = 0; d < pl->ndev; d++) {
             dev_lane *L = &pl->dev[d];
             if (L->qh)
@@ -522,9 +523,12 @@ int bcp_pipeline_destroy(bcp_pipeline *pl)
                 bcp_queue_destroy(L->qk);
             if (L->qd)
                 bcp_queue_destroy(L->qd);
-            if (L->eng)
-                bcp_engine_destroy(L->eng);
+            L->qh = L->qk = L->qd = NULL;
         }
+        free_slots(pl);
+        for (int d = 0; d < pl->ndev; d++)
+            if (pl->dev[d].eng)
+                bcp_engine_destroy(pl->dev[d].eng);
         free(pl->dev);
     }
     free(pl->st);
@@ -837,6 +841,14 @@ static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, 
                 S->busy = 0;
             }
         }
+    /* after a failed submission part of a batch may still be on the device:
+     * nothing of this run stays in flight on the slots past its return */
+    for (int d = 0; d < pl->ndev; d++) {
+        dev_lane *L = &pl->dev[d];
+        const int s1 = bcp_queue_sync(L->qh), s2 = bcp_queue_sync(L->qk), s3 = bcp_queue_sync(L->qd);
+        if (!rc && !dev_rc)
+            dev_rc = s1 ? s1 : s2 ? s2 : s3;
+    }
     if (!rc && dev_rc)
         rc = dev_rc;
     if (stats) {
