@@ -57,11 +57,14 @@ static double now_s(void)
     return (double)t.tv_sec + (double)t.tv_nsec * 1e-9;
 }
 
-/* ---- a small job pool --------------------------------------------------- */
+/* ---- a small job pool ---------------------------------------------------
+ * Jobs are intrusive: every argument struct starts with a `job`, and the
+ * caller owns its storage (arrays sized before a run starts), so pushing a
+ * job cannot fail half way through a batch and leave a latch that never
+ * reaches zero. */
 typedef struct job {
     struct job *next;
-    void (*fn)(void *);
-    void *arg;
+    void (*fn)(struct job *);
 } job;
 
 typedef struct {
@@ -89,34 +92,37 @@ static void *pool_main(void *p)
         if (!P->head)
             P->tail = NULL;
         pthread_mutex_unlock(&P->lock);
-        j->fn(j->arg);
-        free(j);
+        j->fn(j);
     }
 }
 
+static void pool_stop(pool *P);
+
+/* All n threads or none: a partial start joins what it started. */
 static int pool_start(pool *P, int n)
 {
     memset(P, 0, sizeof(*P));
     pthread_mutex_init(&P->lock, NULL);
     pthread_cond_init(&P->cv, NULL);
     P->th = calloc((size_t)n, sizeof(pthread_t));
-    if (!P->th)
+    if (!P->th) {
+        pthread_mutex_destroy(&P->lock);
+        pthread_cond_destroy(&P->cv);
         return -ENOMEM;
+    }
     for (int i = 0; i < n; i++) {
-        if (pthread_create(&P->th[i], NULL, pool_main, P) != 0)
+        if (pthread_create(&P->th[i], NULL, pool_main, P) != 0) {
+            pool_stop(P);
             return -EAGAIN;
+        }
         P->nthreads++;
     }
     return 0;
 }
 
-static int pool_push(pool *P, void (*fn)(void *), void *arg)
+static void pool_push(pool *P, job *j, void (*fn)(job *))
 {
-    job *j = malloc(sizeof(*j));
-    if (!j)
-        return -ENOMEM;
     j->fn = fn;
-    j->arg = arg;
     j->next = NULL;
     pthread_mutex_lock(&P->lock);
     if (P->tail)
@@ -126,7 +132,6 @@ static int pool_push(pool *P, void (*fn)(void *), void *arg)
     P->tail = j;
     pthread_cond_signal(&P->cv);
     pthread_mutex_unlock(&P->lock);
-    return 0;
 }
 
 static void pool_stop(pool *P)
@@ -195,6 +200,7 @@ typedef struct {
 } task;
 
 typedef struct {
+    job j;                               /* first: the pool's link */
     const char *root;
     task *t;
     latch *done;
@@ -211,6 +217,7 @@ typedef struct {
 } slot;
 
 typedef struct {
+    job j;
     const char *root;
     task *t;
     int k;
@@ -220,6 +227,7 @@ typedef struct {
 } read_arg;
 
 typedef struct {
+    job j;
     const char *root;
     task *t;
     const uint8_t *body;
@@ -229,9 +237,11 @@ typedef struct {
 } write_arg;
 
 typedef struct {
+    job j;
     slot *S;
     const char *root;
     task *tasks;
+    write_arg *wa;        /* one per task of the run */
     size_t first, last;
     pool *writers;
     FILE *log;
@@ -262,9 +272,9 @@ static void push_corrupt(int fd, const char *path)
     free(line);
 }
 
-static void do_stat(void *p)
+static void do_stat(job *p)
 {
-    stat_arg *a = p;
+    stat_arg *a = (stat_arg *)p;
     task *t = a->t;
     char fn[4352];
     t->max_cs = 0;
@@ -328,9 +338,9 @@ static void do_stat(void *p)
     latch_down(a->done);
 }
 
-static void do_read(void *p)
+static void do_read(job *p)
 {
-    read_arg *a = p;
+    read_arg *a = (read_arg *)p;
     task *t = a->t;
     uint64_t want = t->size[a->k], got = 0;
     if (want) {
@@ -356,7 +366,6 @@ static void do_read(void *p)
     *a->bytes += got;
     pthread_mutex_unlock(&g_stat_lock);
     latch_down(a->done);
-    free(a);
 }
 
 static void mkdir_parents(char *fn)
@@ -369,9 +378,9 @@ static void mkdir_parents(char *fn)
         }
 }
 
-static void do_write(void *p)
+static void do_write(job *p)
 {
-    write_arg *a = p;
+    write_arg *a = (write_arg *)p;
     task *t = a->t;
     char fn[4352];
     chunk_file(fn, sizeof(fn), a->root, t->p, t->rebuild ? "chunks" : "parity", t->path);
@@ -415,32 +424,30 @@ static void do_write(void *p)
         pthread_mutex_unlock(&g_stat_lock);
     }
     latch_down(a->done);
-    free(a);
 }
-
-static void do_write(void *p);
 
 /* Completion stage (one thread, batches in order): wait for the batch's D2H,
  * then hand its parity files to the writer pool. */
-static void do_complete(void *p)
+static void do_complete(job *p)
 {
-    complete_arg *a = p;
-    int rc = bcp_event_sync(a->S->ev_d);
+    /* The run frees its job arrays once every write of the batch has counted
+     * down, which may be before this function returns: copy what it needs
+     * and touch neither `a` nor a pushed write job after handing it over. */
+    const complete_arg a = *(complete_arg *)p;
+    int rc = bcp_event_sync(a.S->ev_d);
     if (rc) {
         pthread_mutex_lock(&g_stat_lock);
-        *a->dev_rc = rc;
+        *a.dev_rc = rc;
         pthread_mutex_unlock(&g_stat_lock);
-        for (size_t i = a->first; i < a->last; i++)
-            latch_down(&a->S->writes);
+        for (size_t i = a.first; i < a.last; i++)
+            latch_down(&a.S->writes);
     } else {
-        for (size_t i = a->first; i < a->last; i++) {
-            write_arg *w = malloc(sizeof(*w));
-            *w = (write_arg){a->root, &a->tasks[i], a->S->h_out + a->tasks[i].out_off, &a->S->writes, a->log,
-                             a->errors};
-            pool_push(a->writers, do_write, w);
+        for (size_t i = a.first; i < a.last; i++) {
+            write_arg *w = &a.wa[i];
+            *w = (write_arg){{0}, a.root, &a.tasks[i], a.S->h_out + a.tasks[i].out_off, &a.S->writes, a.log, a.errors};
+            pool_push(a.writers, &w->j, do_write);
         }
     }
-    free(a);
 }
 
 static int slot_alloc(bcp_engine *e, slot *s, size_t in_cap, size_t out_cap)
@@ -507,11 +514,13 @@ int bcp_pipeline_destroy(bcp_pipeline *pl)
 {
     if (!pl)
         return -EINVAL;
-    if (pl->pools) {
+    /* only the pools that started (pool_start is all or nothing) */
+    if (pl->pools & 1)
         pool_stop(&pl->readers);
+    if (pl->pools & 4)
         pool_stop(&pl->completer);
+    if (pl->pools & 2)
         pool_stop(&pl->writers);
-    }
     if (pl->dev) {
         /* queues first (each synchronises its streams): no copy or kernel may
          * still use a slot when its memory goes */
@@ -610,10 +619,15 @@ int bcp_pipeline_create(const bcp_pipeline_opts *opts_in, bcp_pipeline **out)
             (rc = bcp_queue_create(L->eng, &L->qk)) || (rc = bcp_queue_create(L->eng, &L->qd)))
             goto fail;
     }
-    if ((rc = pool_start(&pl->readers, o.io_threads)) || (rc = pool_start(&pl->writers, o.io_threads)) ||
-        (rc = pool_start(&pl->completer, 1)))
+    if ((rc = pool_start(&pl->readers, o.io_threads)))
         goto fail;
-    pl->pools = 1;
+    pl->pools |= 1;
+    if ((rc = pool_start(&pl->writers, o.io_threads)))
+        goto fail;
+    pl->pools |= 2;
+    if ((rc = pool_start(&pl->completer, 1)))
+        goto fail;
+    pl->pools |= 4;
     if ((rc = ensure_slots(pl, o.slab_bytes, o.slab_bytes)))
         goto fail;
     *out = pl;
@@ -690,8 +704,8 @@ static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, 
             return -ENOMEM;
         }
         for (size_t i = 0; i < nt; i++) {
-            args[i] = (stat_arg){store_root, &tasks[i], &l, corrupt_fd};
-            pool_push(&pl->readers, do_stat, &args[i]);
+            args[i] = (stat_arg){{0}, store_root, &tasks[i], &l, corrupt_fd};
+            pool_push(&pl->readers, &args[i].j, do_stat);
         }
         latch_wait(&l);
         latch_destroy(&l);
@@ -770,6 +784,20 @@ static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, 
     }
     bcp_stripe *st = pl->st;
     bcp_source *so = pl->so;
+    /* every job of the run, before the first one is queued */
+    size_t nreads_all = 0;
+    for (size_t i = 0; i < nt; i++)
+        nreads_all += (size_t)tasks[i].n;
+    read_arg *ra = calloc(nreads_all ? nreads_all : 1, sizeof(read_arg));
+    write_arg *wa = calloc(nt ? nt : 1, sizeof(write_arg));
+    complete_arg *cargs = calloc(nbatches ? (size_t)nbatches : 1, sizeof(complete_arg));
+    if (!ra || !wa || !cargs) {
+        free(ra);
+        free(wa);
+        free(cargs);
+        return -ENOMEM;
+    }
+    size_t rnext = 0;
 
     /* 3. stream the batches through the slots */
     size_t first = 0;
@@ -791,9 +819,10 @@ static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, 
         uint64_t in_used = 0;
         for (size_t i = first; i < last; i++)
             for (int k = 0; k < tasks[i].n; k++) {
-                read_arg *a = malloc(sizeof(*a));
-                *a = (read_arg){store_root, &tasks[i], k, S->h_in + tasks[i].in_off[k], &bytes_read, &S->reads};
-                pool_push(&pl->readers, do_read, a);
+                read_arg *a = &ra[rnext++];
+                *a = (read_arg){{0}, store_root, &tasks[i], k, S->h_in + tasks[i].in_off[k], &bytes_read,
+                                &S->reads};
+                pool_push(&pl->readers, &a->j, do_read);
                 uint64_t end = tasks[i].in_off[k] + RUP(tasks[i].size[k]);
                 if (end > in_used)
                     in_used = end;
@@ -824,9 +853,9 @@ static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, 
          * the host moves on to reading batch b+1 meanwhile */
         latch_init(&S->writes, (long)(last - first));
         S->busy = 1;
-        complete_arg *ca = malloc(sizeof(*ca));
-        *ca = (complete_arg){S, store_root, tasks, first, last, &pl->writers, log, &errors, &dev_rc};
-        pool_push(&pl->completer, do_complete, ca);
+        complete_arg *ca = &cargs[b];
+        *ca = (complete_arg){{0}, S, store_root, tasks, wa, first, last, &pl->writers, log, &errors, &dev_rc};
+        pool_push(&pl->completer, &ca->j, do_complete);
         for (size_t i = first; i < last; i++)
             bytes_written += (tasks[i].rebuild ? 0 : 8u * (uint64_t)tasks[i].n) + tasks[i].out_len;
         ntasks += last - first;
@@ -849,6 +878,10 @@ static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, 
         if (!rc && !dev_rc)
             dev_rc = s1 ? s1 : s2 ? s2 : s3;
     }
+    /* every job has run: the writes latched above, the completions before them */
+    free(ra);
+    free(wa);
+    free(cargs);
     if (!rc && dev_rc)
         rc = dev_rc;
     if (stats) {
