@@ -45,6 +45,12 @@ class RunStats(ctypes.Structure):
                 ("bytes_written", ctypes.c_uint64), ("errors", ctypes.c_int)]
 
 
+class PipelineTiming(ctypes.Structure):
+    _fields_ = [("stat", ctypes.c_double), ("read_wait", ctypes.c_double), ("slot_wait", ctypes.c_double),
+                ("submit", ctypes.c_double), ("drain", ctypes.c_double), ("batches", ctypes.c_uint32),
+                ("read_jobs", ctypes.c_uint32)]
+
+
 class PipelineOpts(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int), ("slab_bytes", ctypes.c_size_t), ("io_threads", ctypes.c_int),
                 ("nslots", ctypes.c_int), ("ndevices", ctypes.c_int)]
@@ -152,6 +158,7 @@ _SIGS = {
     "bcp_pipeline_run": ([_V, ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(WorkItem), ctypes.c_size_t, _V,
                           ctypes.POINTER(RunStats)], ctypes.c_int),
     "bcp_pipeline_destroy": ([_V], ctypes.c_int),
+    "bcp_pipeline_last_timing": ([_V, ctypes.POINTER(PipelineTiming)], ctypes.c_int),
     "bcp_pipeline_rebuild": ([_V, ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.POINTER(WorkItem),
                               ctypes.c_size_t, ctypes.c_char_p, _V, ctypes.POINTER(RunStats)], ctypes.c_int),
     "bcp_lb_init": ([ctypes.c_int], ctypes.c_int),
@@ -668,6 +675,13 @@ class Pipeline:
         call("bcp_gen_round_pipeline", self.h, store_root.encode(), ntargets, events.h, cw, log, ctypes.byref(st),
              ctypes.byref(n))
         return st, n.value
+
+    def last_timing(self) -> dict:
+        """bcp_pipeline_last_timing: the host thread's wall time of the last run by stage."""
+        t = PipelineTiming()
+        call("bcp_pipeline_last_timing", self.h, ctypes.byref(t))
+        return {f: round(getattr(t, f), 5) if isinstance(getattr(t, f), float) else getattr(t, f)
+                for f, _ in PipelineTiming._fields_}
 
     def close(self):
         if self.h:

@@ -125,8 +125,9 @@ def config1(a):
             shutil.rmtree(os.path.join(root, f"st{p}", "parity"), ignore_errors=True)
             os.makedirs(os.path.join(root, f"st{p}", "parity"))
 
-    def run(label, fn):
-        """first (cold: pinning, queues) run, then a.reps warm runs; median reported."""
+    def run(label, fn, extra=None):
+        """first (cold: pinning, queues) run, then a.reps warm runs; median reported;
+        extra() adds fields (the pipeline's stage timing of its last run)."""
         times = []
         for r in range(1 + a.reps):
             reset_parity()
@@ -137,7 +138,8 @@ def config1(a):
         warm = float(np.median(times[1:])) if a.reps else times[0]
         emit(config=1, path=label, cold_seconds=round(times[0], 3), warm_seconds=round(warm, 3),
              GiBps=round((rd + wr) / warm / GiB, 3), cold_GiBps=round((rd + wr) / times[0] / GiB, 3),
-             bytes_read=rd, bytes_written=wr, tasks=int(st.tasks), errors=int(st.errors), verified=ok, bad=bad)
+             bytes_read=rd, bytes_written=wr, tasks=int(st.tasks), errors=int(st.errors), verified=ok, bad=bad,
+             **(extra() if extra else {}))
         return ok
 
     # the per-task protocol with three folds, interleaved in rotating order
@@ -171,7 +173,8 @@ def config1(a):
                      bytes_read=rd, bytes_written=wr, tasks=int(st.tasks), errors=int(st.errors), verified=okv,
                      bad=badv, order="interleaved")
     pl = bcp.Pipeline(io_threads=a.io_threads, ndevices=a.ndevices)
-    ok &= run(f"pipeline(bcp_pipeline_run,{a.ndevices} GPU)", lambda: pl.run(root, 4, items))
+    ok &= run(f"pipeline(bcp_pipeline_run,{a.ndevices} GPU)", lambda: pl.run(root, 4, items),
+              lambda: {"last_run_timing": pl.last_timing()})
     pl.close()
     # the whole beegfs-parity-gen --complete flow through the CLI: scan every
     # target, plan (P per select_P), run, fill the DB replicas (warm median)
@@ -333,7 +336,7 @@ def config5(a):
     ok, bad = verify(root, files, contents, a.verify, rng)
     emit(config=5, path=f"pipeline_full_gen({a.ndevices} GPU)", cold_seconds=round(times[0], 3), warm_seconds=round(dt, 3),
          GiBps=round((rd + wr) / dt / GiB, 3), bytes_read=rd, bytes_written=wr, tasks=int(st.tasks), verified=ok,
-         bad=bad)
+         bad=bad, runs_s=[round(x, 4) for x in times], last_run_timing=pl.last_timing())
     ok &= ok_proto
     # changelog: a seeded 10 % of stripes rewritten -> record streams per target
     sub = sorted(int(x) for x in rng.choice(len(files), size=max(1, len(files) // 10), replace=False))
@@ -350,21 +353,32 @@ def config5(a):
         contents[path] = new
     # persistent state: seed every target's DB replica with the state of the
     # full generation above (what that round's process_list updates leave)
+    def seed_dbs():
+        for k in range(ntargets):
+            db = bcp.PDB(os.path.join(root, f"st{k}", "db"))
+            for path, ts, loc in items:
+                db.set(path, ts, loc)
+            db.close()
     t0 = time.perf_counter()
-    for k in range(ntargets):
-        db = bcp.PDB(os.path.join(root, f"st{k}", "db"))
-        for path, ts, loc in items:
-            db.set(path, ts, loc)
-        db.close()
+    seed_dbs()
     emit(config=5, stage="db_seeded", replicas=ntargets, entries=len(items), seconds=round(time.perf_counter() - t0, 3))
-    # changelog round: events -> plan against the DB -> pipeline -> DB update
+    # changelog round: events -> plan against the DB -> pipeline -> DB update;
+    # a first round, then a.reps more, each after re-seeding the replicas
+    # (outside the timing) so that every round plans the same subset
     cum = list(np.cumsum([1000] * ntargets))
-    t0 = time.perf_counter()
-    es = bcp.EventSet()
-    for t, recs in streams.items():
-        es.feed(t, bcp.pack_records(recs))
-    st, nplanned = pl.round(root, ntargets, es, cum_weight=cum)
-    dt = time.perf_counter() - t0
+    rtimes, rpipe, rtiming = [], [], []
+    for r in range(1 + a.reps):
+        if r:
+            seed_dbs()
+        t0 = time.perf_counter()
+        es = bcp.EventSet()
+        for t, recs in streams.items():
+            es.feed(t, bcp.pack_records(recs))
+        st, nplanned = pl.round(root, ntargets, es, cum_weight=cum)
+        rtimes.append(time.perf_counter() - t0)
+        es.close()
+        rpipe.append(st.seconds)
+        rtiming.append(pl.last_timing())
     # the planner keeps each stripe's P (fill_in_missing_fields) -> same targets
     db = bcp.PDB(os.path.join(root, "st0", "db"))
     state = {k.decode(): (ts, loc) for k, ts, loc in db.items()}
@@ -375,11 +389,14 @@ def config5(a):
     srd, swr = total_bytes(root, sub_files)
     pl.close()
     ok2, bad2 = verify(root, sub_files, contents, a.verify, rng)
+    dt = float(np.median(rtimes[1:])) if a.reps else rtimes[0]
+    dtp = float(np.median(rpipe[1:])) if a.reps else rpipe[0]
     emit(config=5, path="changelog_round_pipeline(events->plan vs DB->pipeline->DB)", stripes=len(sub),
-         plan_matches=plan_ok, seconds=round(dt, 3), pipeline_seconds=round(st.seconds, 4),
-         outside_pipeline_seconds=round(dt - st.seconds, 4), GiBps=round((srd + swr) / dt / GiB, 3), bytes_read=srd,
-         bytes_written=swr, tasks=int(st.tasks), verified=ok2, bad=bad2)
-    es.close()
+         plan_matches=plan_ok, seconds=round(dt, 4), cold_seconds=round(rtimes[0], 4), pipeline_seconds=round(dtp, 4),
+         outside_pipeline_seconds=round(dt - dtp, 4), GiBps=round((srd + swr) / dt / GiB, 3),
+         cold_GiBps=round((srd + swr) / rtimes[0] / GiB, 3), runs_s=[round(x, 4) for x in rtimes],
+         bytes_read=srd, bytes_written=swr, tasks=int(st.tasks), verified=ok2, bad=bad2,
+         pipeline_timing=rtiming[-1])
     if not a.keep:
         shutil.rmtree(root, ignore_errors=True)
     return ok and ok2 and plan_ok
