@@ -770,17 +770,36 @@ static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, 
         plan_in = per < plan_in ? per : plan_in;
         plan_in = plan_in < max_in ? max_in : plan_in;
     }
+    /* Ramps.  Once the reads outrun the link, the run is the host-to-device
+     * copies back to back plus what cannot overlap them: the first batch's
+     * reads before the first copy, and after the last copy the last batch's
+     * kernel, D2H and parity writes.  Both scale with the batch, so batches
+     * start at RAMP_MIN and double (a batch holds at most what the run has
+     * consumed so far, per device) and end halving (at most half of what
+     * remains, per device): r03 timing showed 6-10 ms of a 51 ms config-1
+     * run spent in the drain behind 160 MiB batches. */
+    const uint64_t RAMP_MIN = (uint64_t)16 << 20;
+    uint64_t total_in_all = 0;
+    for (size_t i = 0; i < nt; i++)
+        for (int k = 0; k < tasks[i].n; k++)
+            total_in_all += RUP(tasks[i].size[k]);
     int nbatches = 0;
     {
-        uint64_t in_used = 0, out_used = 0;
+        uint64_t in_used = 0, out_used = 0, consumed = 0, limit = plan_in;
         for (size_t i = 0; i < nt; i++) {
             task *t = &tasks[i];
             uint64_t in = 0;
             for (int k = 0; k < t->n; k++)
                 in += RUP(t->size[k]);
-            if (i == 0 || in_used + in > plan_in || out_used + RUP(t->out_len) > out_cap) {
+            if (i == 0 || in_used + in > limit || out_used + RUP(t->out_len) > out_cap) {
                 nbatches++;
+                consumed += in_used;
                 in_used = out_used = 0;
+                const uint64_t up = consumed / (uint64_t)pl->ndev;
+                const uint64_t down = (total_in_all - consumed) / (2u * (uint64_t)pl->ndev);
+                limit = up < down ? up : down;
+                limit = limit < RAMP_MIN ? RAMP_MIN : limit;
+                limit = limit > plan_in ? plan_in : limit;
             }
             t->batch = nbatches - 1;
             for (int k = 0; k < t->n; k++) {
