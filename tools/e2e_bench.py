@@ -404,7 +404,9 @@ def config5(a):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--root", default=os.environ.get("TMPDIR", "/tmp") + "/bcp_e2e")
+    # stores in memory (page cache without a disk behind it): /dev/shm where it exists
+    ap.add_argument("--root", default=("/dev/shm" if os.path.isdir("/dev/shm") else os.environ.get("TMPDIR", "/tmp"))
+                    + "/bcp_e2e")
     ap.add_argument("--configs", default="1,5")
     ap.add_argument("--c1-files", type=int, default=1333)
     ap.add_argument("--c5-stripes", type=int, default=1000)

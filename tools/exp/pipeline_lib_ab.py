@@ -71,7 +71,8 @@ def main():
     probe = ctypes.CDLL(bcp.LIB_PATH)
     for name in [n for n in bcp._SIGS if not hasattr(probe, n)]:
         del bcp._SIGS[name]
-    pl = bcp.Pipeline()
+    nslots = int(os.environ.get("PLAB_NSLOTS", "3"))  # the .sh's "lib@nslots" entries
+    pl = bcp.Pipeline(nslots=nslots)
     try:
         for name, (nt, files) in L.items():
             root = os.path.join(a.run, "config1" if name == "config1" else "config5_full")
@@ -92,7 +93,7 @@ def main():
                 chunks = [np.fromfile(S.chunk_path(root, h, path), dtype=np.uint8) for h in hs]
                 bad += S.read_file(S.parity_path(root, P, path)) != oracle.gen_parity_file(chunks)
             w = float(np.median(ts[1:]))
-            print(json.dumps({"label": a.label, "lib": os.environ.get("BCP_LIB", "in-tree"), "workload": name,
+            print(json.dumps({"label": a.label, "lib": os.environ.get("BCP_LIB", "in-tree"), "nslots": nslots,"workload": name,
                               "stripes": len(files), "warm_s": round(w, 5), "GiBps": round((rd + wr) / w / GiB, 2),
                               "cold_s": round(ts[0], 5), "runs": [round(x, 5) for x in ts], "timing": tm,
                               "verified": bad == 0}), flush=True)

@@ -6,12 +6,13 @@
 # bcp_pipeline_last_timing print timing null.  The order rotates per round.
 set -o pipefail
 LIBS=${LIBS:-"${LIB_A:?} beegfs-chunk-parity_amd/lib/libbcp.so"}
-D=${STORE:-${TMPDIR:-/tmp}/bcp_plab}
+D=${STORE:-/dev/shm/bcp_plab}  # in memory: no disk writeback behind the page cache
 timeout -k 10 300 python -u tools/exp/pipeline_lib_ab.py --make $D || exit 1
 set -- $LIBS
 for r in $(seq 1 ${ROUNDS:-3}); do
-  for lib in "$@"; do
-    BCP_LIB=$lib timeout -k 10 240 python -u tools/exp/pipeline_lib_ab.py --run $D --label "r$r" || exit 1
+  for ent in "$@"; do  # "lib" or "lib@nslots"
+    lib=${ent%@*}; ns=3; [ "$ent" != "$lib" ] && ns=${ent#*@}
+    PLAB_NSLOTS=$ns BCP_LIB=$lib timeout -k 10 240 python -u tools/exp/pipeline_lib_ab.py --run $D --label "r$r" || exit 1
   done
   set -- "${@:2}" "$1"
 done
