@@ -49,7 +49,6 @@
 #define ROW 256u
 #define WINDOW ((uint64_t)BCP_WINDOW_BYTES)
 #define RUP(x) (((x) + ROW - 1) / ROW * ROW)
-#define READ_PIECE ((uint64_t)1 << 20) /* largest read job */
 
 static double now_s(void)
 {
@@ -214,7 +213,6 @@ typedef struct {
     size_t in_cap, out_cap;
     bcp_event *ev_h, *ev_k, *ev_d;
     latch reads, writes;
-    int reading;          /* reads of a batch issued, not yet waited for */
     int busy;             /* writes of the previous batch pending */
 } slot;
 
@@ -222,8 +220,7 @@ typedef struct {
     job j;
     const char *root;
     task *t;
-    int k;
-    uint64_t off, len;    /* piece of source k's data */
+    int k;                /* source */
     uint8_t *dst;         /* its place in the slab */
     uint64_t *bytes;      /* accumulated under lock */
     latch *done;
@@ -341,15 +338,11 @@ static void do_stat(job *p)
     latch_down(a->done);
 }
 
-/* One piece [off, off + len) of source k's data (a whole chunk up to
- * READ_PIECE bytes, else one of its READ_PIECE pieces: a batch of mixed
- * sizes then ends with the pool's threads evenly loaded, not waiting on the
- * one thread that drew a 4 MiB chunk last). */
 static void do_read(job *p)
 {
     read_arg *a = (read_arg *)p;
     task *t = a->t;
-    uint64_t want = a->len, got = 0;
+    uint64_t want = t->size[a->k], got = 0;
     if (want) {
         char fn[4352];
         const int is_parity = t->rebuild && a->k == t->parity_src;
@@ -357,17 +350,15 @@ static void do_read(job *p)
         int fd = open(fn, O_RDONLY);
         if (fd >= 0) {
             posix_fadvise(fd, 0, 0, POSIX_FADV_SEQUENTIAL);
-            const uint64_t base = t->src_off[a->k] + a->off;
             while (got < want) {
-                ssize_t r = pread(fd, a->dst + got, (size_t)(want - got), (off_t)(base + got));
+                ssize_t r = pread(fd, a->dst + got, (size_t)(want - got), (off_t)(t->src_off[a->k] + got));
                 if (r <= 0)
                     break;
                 got += (uint64_t)r;
             }
             close(fd);
         }
-        /* a short read is zero padded, as chunk_sender does (:302-303):
-         * bytes past the file's end read as zeros, piece by piece */
+        /* a short read is zero padded, as chunk_sender does (:302-303) */
         if (got < want)
             memset(a->dst + got, 0, (size_t)(want - got));
     }
@@ -823,89 +814,72 @@ static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, 
     bcp_stripe *st = pl->st;
     bcp_source *so = pl->so;
     /* every job of the run, before the first one is queued: a read job per
-     * READ_PIECE of every source, a write job per task, a completion per batch */
+     * source, a write job per task, a completion per batch */
     size_t nreads_all = 0;
     for (size_t i = 0; i < nt; i++)
-        for (int k = 0; k < tasks[i].n; k++)
-            nreads_all += (size_t)((tasks[i].size[k] + READ_PIECE - 1) / READ_PIECE);
+        nreads_all += (size_t)tasks[i].n;
     read_arg *ra = calloc(nreads_all ? nreads_all : 1, sizeof(read_arg));
     write_arg *wa = calloc(nt ? nt : 1, sizeof(write_arg));
     complete_arg *cargs = calloc(nbatches ? (size_t)nbatches : 1, sizeof(complete_arg));
-    size_t *bfirst = calloc((size_t)nbatches + 1, sizeof(size_t));
-    if (!ra || !wa || !cargs || !bfirst) {
+    if (!ra || !wa || !cargs) {
         free(ra);
         free(wa);
         free(cargs);
-        free(bfirst);
         return -ENOMEM;
     }
-    for (size_t i = nt; i-- > 0;)
-        bfirst[tasks[i].batch] = i;
-    bfirst[nbatches] = nt;
     size_t rnext = 0;
     bcp_pipeline_timing tm = {0};
     tm.stat = now_s() - t_stat;
     tm.batches = (uint32_t)nbatches;
 
-    /* 3. stream the batches through the slots.  Reads run ahead of the
-     * submissions: while the host thread waits for batch b's reads, batches
-     * b+1 .. b+LOOKAHEAD-1 are queued behind them, so no io thread idles at
-     * the end of a batch (its slowest reads) or while the host submits.  The
-     * reads of batch b+LOOKAHEAD are issued once b is submitted (top of the
-     * next iteration); they take the slot of batch b-ndev (slots go
-     * round-robin per device), submitted an iteration earlier -- never the
-     * slot of b itself, whose H2D may still be running.  That slot's writes
-     * (and so its H2D, kernel and D2H) are waited for first. */
-    const int LOOKAHEAD = pl->ndev * (nslots - 1);
-#define SLOT_OF(b) (&pl->dev[(b) % pl->ndev].slots[((b) / pl->ndev) % nslots])
-    int issued = 0;
+    /* 3. stream the batches through the slots: batch b is read while b-1
+     * is on the device and b-2 is being written (3 slots).  (Reading ahead
+     * of the submissions, nslots-1 batches deep in 1 MiB pieces, measured
+     * no different in r03 -- the reads are not the bound, section 6.7 of
+     * DESIGN.md -- and is not kept.) */
+    size_t first = 0;
     for (int b = 0; b < nbatches && !rc; b++) {
-        for (; issued < nbatches && issued < b + LOOKAHEAD; issued++) {
-            slot *S = SLOT_OF(issued);
-            double tw = now_s();
-            if (S->busy) { /* writes of that slot's previous batch */
-                latch_wait(&S->writes);
-                latch_destroy(&S->writes);
-                S->busy = 0;
-            }
-            tm.slot_wait += now_s() - tw;
-            long npieces = 0;
-            for (size_t i = bfirst[issued]; i < bfirst[issued + 1]; i++)
-                for (int k = 0; k < tasks[i].n; k++)
-                    npieces += (long)((tasks[i].size[k] + READ_PIECE - 1) / READ_PIECE);
-            latch_init(&S->reads, npieces);
-            S->reading = 1;
-            for (size_t i = bfirst[issued]; i < bfirst[issued + 1]; i++)
-                for (int k = 0; k < tasks[i].n; k++)
-                    for (uint64_t off = 0; off < tasks[i].size[k]; off += READ_PIECE) {
-                        const uint64_t len = tasks[i].size[k] - off < READ_PIECE ? tasks[i].size[k] - off : READ_PIECE;
-                        read_arg *a = &ra[rnext++];
-                        *a = (read_arg){{0}, store_root, &tasks[i], k, off, len, S->h_in + tasks[i].in_off[k] + off,
-                                        &bytes_read, &S->reads};
-                        pool_push(&pl->readers, &a->j, do_read);
-                    }
-            tm.read_jobs += (uint32_t)npieces;
-        }
         dev_lane *L = &pl->dev[b % pl->ndev];
-        slot *S = SLOT_OF(b);
-        const size_t first = bfirst[b], last = bfirst[b + 1];
+        slot *S = &L->slots[(b / pl->ndev) % nslots];
         double tw = now_s();
+        if (S->busy) { /* writes of batch b - nslots still running */
+            latch_wait(&S->writes);
+            latch_destroy(&S->writes);
+            S->busy = 0;
+        }
+        tm.slot_wait += now_s() - tw;
+        size_t last = first;
+        while (last < nt && tasks[last].batch == b)
+            last++;
+        long nreads = 0;
+        for (size_t i = first; i < last; i++)
+            nreads += tasks[i].n;
+        tw = now_s();
+        latch_init(&S->reads, nreads);
+        uint64_t in_used = 0;
+        for (size_t i = first; i < last; i++)
+            for (int k = 0; k < tasks[i].n; k++) {
+                read_arg *a = &ra[rnext++];
+                *a = (read_arg){{0}, store_root, &tasks[i], k, S->h_in + tasks[i].in_off[k], &bytes_read,
+                                &S->reads};
+                pool_push(&pl->readers, &a->j, do_read);
+                uint64_t end = tasks[i].in_off[k] + RUP(tasks[i].size[k]);
+                if (end > in_used)
+                    in_used = end;
+            }
+        tm.read_jobs += (uint32_t)nreads;
         latch_wait(&S->reads);
         latch_destroy(&S->reads);
-        S->reading = 0;
         const double ts = now_s();
         tm.read_wait += ts - tw;
         uint32_t ns = 0, nsrc = 0;
-        uint64_t in_used = 0, out_used = 0;
+        uint64_t out_used = 0;
         for (size_t i = first; i < last; i++) {
             task *t = &tasks[i];
             st[ns] = (bcp_stripe){(uint64_t)S->d_out + t->out_off, t->out_len, nsrc, (uint32_t)t->n,
                                   t->max_cs > WINDOW ? WINDOW : 0};
-            for (int k = 0; k < t->n; k++) {
+            for (int k = 0; k < t->n; k++)
                 so[nsrc++] = (bcp_source){(uint64_t)S->d_in + t->in_off[k], t->size[k]};
-                if (t->in_off[k] + RUP(t->size[k]) > in_used)
-                    in_used = t->in_off[k] + RUP(t->size[k]);
-            }
             ns++;
             if (t->out_off + RUP(t->out_len) > out_used)
                 out_used = t->out_off + RUP(t->out_len);
@@ -918,7 +892,8 @@ static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, 
             (rc = bcp_d2h_async(L->qd, S->h_out, S->d_out, (size_t)out_used)) ||
             (rc = bcp_event_record(S->ev_d, L->qd)))
             break;
-        /* writers start once the batch's D2H is done (completion thread) */
+        /* writers start once the batch's D2H is done (completion thread);
+         * the host moves on to reading batch b+1 meanwhile */
         latch_init(&S->writes, (long)(last - first));
         S->busy = 1;
         complete_arg *ca = &cargs[b];
@@ -927,21 +902,10 @@ static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, 
         for (size_t i = first; i < last; i++)
             bytes_written += (tasks[i].rebuild ? 0 : 8u * (uint64_t)tasks[i].n) + tasks[i].out_len;
         ntasks += last - first;
+        first = last;
         tm.submit += now_s() - ts;
     }
-#undef SLOT_OF
     const double td = now_s();
-    /* a failed submission leaves reads of later batches in flight: they
-     * write into the slabs, so they end before anything returns */
-    for (int d = 0; d < pl->ndev; d++)
-        for (int s = 0; s < nslots; s++) {
-            slot *S = &pl->dev[d].slots[s];
-            if (S->reading) {
-                latch_wait(&S->reads);
-                latch_destroy(&S->reads);
-                S->reading = 0;
-            }
-        }
     for (int d = 0; d < pl->ndev; d++)
         for (int s = 0; s < nslots; s++) {
             slot *S = &pl->dev[d].slots[s];
@@ -963,7 +927,6 @@ static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, 
     free(ra);
     free(wa);
     free(cargs);
-    free(bfirst);
     tm.drain = now_s() - td;
     pl->last = tm;
     if (!rc && dev_rc)

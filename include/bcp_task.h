@@ -483,13 +483,14 @@ int bcp_pipeline_run(bcp_pipeline *pl, const char *store_root, int ntargets, con
                      size_t nitems, FILE *log, bcp_run_stats *stats);
 int bcp_pipeline_destroy(bcp_pipeline *pl);
 /* Where the host thread of the pipeline's last run spent its wall time
- * (seconds; for tools): stat phase, waiting for a batch's reads, waiting for
- * a slot's previous writes before reading into it, building and submitting
- * batches, and the drain after the last submission. */
+ * (seconds; for tools): stat phase, reading a batch (from issuing its reads
+ * to the last one's end), waiting for a slot's previous batch to be written
+ * before reading into it, building and submitting batches, and the drain
+ * after the last submission. */
 typedef struct {
     double stat, read_wait, slot_wait, submit, drain;
     uint32_t batches;    /* device batches */
-    uint32_t read_jobs;  /* io jobs (chunks cut into pieces of at most 1 MiB) */
+    uint32_t read_jobs;  /* io read jobs (one per chunk of every stripe) */
 } bcp_pipeline_timing;
 int bcp_pipeline_last_timing(const bcp_pipeline *pl, bcp_pipeline_timing *out);
 /* Rebuild of one lost target with the batched pipeline (do_file's selection
