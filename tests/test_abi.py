@@ -76,6 +76,9 @@ def test_argument_validation_without_device(bcp):
     assert L.bcp_engine_create(0, None) == -errno.EINVAL
     assert L.bcp_queue_sync(None) == -errno.EINVAL
     assert L.bcp_strerror(-errno.ENODEV) == b"no usable HIP device"
+    t = bcp.PipelineTiming()
+    assert L.bcp_pipeline_last_timing(None, ctypes.byref(t)) == -errno.EINVAL
+    assert L.bcp_pipeline_destroy(None) == -errno.EINVAL
 
 
 def test_host_buffer_bounds_checked(bcp):
