@@ -703,6 +703,7 @@ static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, 
     int rc = 0, errors = 0, dev_rc = 0;
     uint64_t bytes_read = 0, bytes_written = 0, ntasks = 0;
     const double t_stat = now_s();
+    memset(&pl->last, 0, sizeof(pl->last)); /* a run that fails early reports zeros, not the previous run */
 
     /* 1. stat every chunk (parallel) */
     {
