@@ -192,6 +192,25 @@ static int add_event(bcp_eventset *s, int st, const char *path, size_t len, int6
     return 0;
 }
 
+/* A record's path becomes <store>/st<k>/{chunks,parity}/<path> on every
+ * target: beyond the reference's check (relative, gen/main.c:306) it must
+ * not carry a NUL (the C string would name another file) or a ".."
+ * component (it would name a file outside the store). */
+static int path_ok(const char *p, size_t n)
+{
+    if (memchr(p, 0, n))
+        return 0;
+    for (size_t i = 0; i < n;) {
+        size_t j = i;
+        while (j < n && p[j] != '/')
+            j++;
+        if (j - i == 2 && p[i] == '.' && p[i + 1] == '.')
+            return 0;
+        i = j + 1;
+    }
+    return 1;
+}
+
 /* Parse whole records from buf; a trailing partial record is kept for the
  * next call on the same target (feed_targets_with keeps it in its buffer). */
 static int parse(bcp_eventset *s, int st, const uint8_t *buf, size_t len, size_t *used)
@@ -211,6 +230,8 @@ static int parse(bcp_eventset *s, int st, const uint8_t *buf, size_t len, size_t
         const char *path = (const char *)buf + off + 32;
         if (path[0] == '/')
             return -EINVAL; /* paths are relative to the chunk dir (gen/main.c:306) */
+        if (!path_ok(path, (size_t)plen))
+            return -EINVAL;
         int rc = add_event(s, st, path, (size_t)plen, ts, size, ev);
         if (rc)
             return rc;

@@ -107,6 +107,20 @@ def test_absolute_paths_rejected(bcp):
     es.close()
 
 
+@pytest.mark.parametrize("bad", ["../x", "a/../../x", "a/..", "..", "a\0b"])
+def test_paths_leaving_the_store_rejected(bcp, bad):
+    """A record path names <store>/st<k>/chunks/<path> and the parity file on
+    P: no ".." component and no embedded NUL."""
+    es = bcp.EventSet()
+    with pytest.raises(bcp.BcpError):
+        es.feed(0, bcp.pack_records([(1, 2, "m", bad)]))
+    es.close()
+    es = bcp.EventSet()
+    es.feed(0, bcp.pack_records([(1, 2, "m", "a/..b/c..d/...")]))  # dots inside names are fine
+    assert [e[0] for e in es.entries()] == ["a/..b/c..d/..."]
+    es.close()
+
+
 def test_store_weight(bcp, tmp_path):
     fd = os.open(str(tmp_path), os.O_DIRECTORY | os.O_RDONLY)
     try:
