@@ -459,8 +459,8 @@ def test_cli_complete_partial_rebuild(bcp, oracle, tmp_path, engine_kind):
         assert S.read_file(S.chunk_path(root, victim, p_)) == data, p_
 
 
-@pytest.mark.parametrize("ndevices", [2, 3])
-def test_pipeline_multi_device_lanes(bcp, oracle, tmp_path, ndevices):
+@pytest.mark.parametrize("ndevices,nslots", [(2, 2), (3, 2), (8, 3)])
+def test_pipeline_multi_device_lanes(bcp, oracle, tmp_path, ndevices, nslots):
     """Batches round-robin over several device lanes (on a one-GPU box the
     lanes wrap onto the same GPU, each with its own engine, queues and
     slots); small slabs force many batches so every lane and slot recycles."""
@@ -471,7 +471,7 @@ def test_pipeline_multi_device_lanes(bcp, oracle, tmp_path, ndevices):
         files.append((f"m/{i}", holders, p, [int(x) for x in rng.integers(0, 400_000, size=len(holders))]))
     root = str(tmp_path)
     items, contents = S.populate(root, 9, files, seed=ndevices)
-    pl = bcp.Pipeline(slab_bytes=1 << 20, io_threads=4, nslots=2, ndevices=ndevices)
+    pl = bcp.Pipeline(slab_bytes=1 << 20, io_threads=4, nslots=nslots, ndevices=ndevices)
     try:
         for _ in range(2):
             st = pl.run(root, 9, items)
