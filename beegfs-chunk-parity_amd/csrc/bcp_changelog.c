@@ -29,7 +29,7 @@
 #include <sys/statvfs.h>
 #include <unistd.h>
 
-#include "bcp_task.h"
+#include "bcp_host.h"
 
 /* ---- PCG32 (pcg-random.org minimal C, as used at gen/main.c:338-372) ---- */
 typedef struct {
@@ -195,10 +195,15 @@ static int add_event(bcp_eventset *s, int st, const char *path, size_t len, int6
 /* A record's path becomes <store>/st<k>/{chunks,parity}/<path> on every
  * target: beyond the reference's check (relative, gen/main.c:306) it must
  * not carry a NUL (the C string would name another file) or a ".."
- * component (it would name a file outside the store). */
-static int path_ok(const char *p, size_t n)
+ * component (it would name a file outside the store).  process_task
+ * applies the same rule. */
+int bcpi_path_ok(const char *p, size_t n)
 {
-    if (memchr(p, 0, n))
+    if (n == (size_t)-1)
+        n = strlen(p);
+    else if (memchr(p, 0, n))
+        return 0;
+    if (n == 0 || p[0] == '/')
         return 0;
     for (size_t i = 0; i < n;) {
         size_t j = i;
@@ -228,10 +233,8 @@ static int parse(bcp_eventset *s, int st, const uint8_t *buf, size_t len, size_t
         if (len - off - 32 < plen)
             break;
         const char *path = (const char *)buf + off + 32;
-        if (path[0] == '/')
-            return -EINVAL; /* paths are relative to the chunk dir (gen/main.c:306) */
-        if (!path_ok(path, (size_t)plen))
-            return -EINVAL;
+        if (!bcpi_path_ok(path, (size_t)plen))
+            return -EINVAL; /* relative to the chunk dir (gen/main.c:306), and inside it */
         int rc = add_event(s, st, path, (size_t)plen, ts, size, ev);
         if (rc)
             return rc;

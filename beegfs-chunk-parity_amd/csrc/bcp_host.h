@@ -59,3 +59,8 @@ int bcpi_fold_inflight(void);
 /* Make [base, base + bytes) this process's arena slice (a memfd shared with
  * a node fold server, bcp_fold_server_connect). */
 void bcpi_arena_set(void *base, size_t bytes);
+
+/* 1 if path (n bytes, or up to its NUL when n is (size_t)-1) names a file
+ * inside a target's chunks / parity directory: relative, no ".." component,
+ * no embedded NUL (bcp_changelog.c). */
+int bcpi_path_ok(const char *path, size_t n);

@@ -44,7 +44,7 @@
 #include <time.h>
 #include <unistd.h>
 
-#include "bcp_task.h"
+#include "bcp_host.h"
 
 #define ROW 256u
 #define WINDOW ((uint64_t)BCP_WINDOW_BYTES)
@@ -676,6 +676,11 @@ int bcp_pipeline_run(bcp_pipeline *pl, const char *store_root, int ntargets, con
         int P = GET_P(loc);
         if ((uint64_t)P == NO_P)
             continue;
+        if (!bcpi_path_ok(items[i].path, (size_t)-1)) { /* as process_task: refused, skipped */
+            if (log)
+                fprintf(log, "bcp_pipeline: refusing '%s': not a path inside the store\n", items[i].path);
+            continue;
+        }
         if ((loc & L_MASK) == 0) {
             char fn[4352];
             chunk_file(fn, sizeof(fn), store_root, P, "parity", items[i].path);
@@ -978,6 +983,11 @@ int bcp_pipeline_rebuild(bcp_pipeline *pl, const char *store_root, int ntargets,
         /* do_file's skip rules (rebuild/main.c:48-51) */
         if ((uint64_t)P == NO_P || P == rebuild_target || !TEST_BIT(fi->locations, rebuild_target))
             continue;
+        if (!bcpi_path_ok(items[i].path, (size_t)-1)) { /* as process_task: refused, skipped */
+            if (log)
+                fprintf(log, "bcp_pipeline: refusing '%s': not a path inside the store\n", items[i].path);
+            continue;
+        }
         task *t = &tasks[nt++];
         t->path = items[i].path;
         t->p = rebuild_target;

@@ -859,6 +859,14 @@ int process_task(HostState *hs, const char *path, const FileInfo *fi, TaskInfo t
     assert(P_IS_INVALID(fi->locations) == 0);
     assert(hs->storage_target >= 0);
 
+    /* A path that would name a file outside the rank's chunk / parity
+     * directories (absolute, "..") is refused -- by every rank alike, so the
+     * task is skipped everywhere and no message goes unanswered.  (The
+     * reference trusts its worklist here.) */
+    if (!bcpi_path_ok(path, (size_t)-1)) {
+        LOGERR("refusing '%s': not a path inside the store\n", path);
+        return 0;
+    }
     task_settings ts;
     settings_now(&ts);
     if (GET_P(fi->locations) == hs->storage_target)

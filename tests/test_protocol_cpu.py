@@ -177,6 +177,29 @@ def test_rebuild_skip_rules_and_corrupt_list(bcp, oracle, cpu_hook, tmp_path):
     assert corrupt == ["a", "a"]  # targets 0 and 2 (chunks), not the parity holder
 
 
+@pytest.mark.parametrize("bad", ["../outside/x", "/abs/x", "a/../../outside/x"])
+def test_paths_outside_the_store_are_refused_by_every_rank(bcp, oracle, cpu_hook, tmp_path, bad):
+    """process_task refuses a path that would leave the targets' chunks /
+    parity directories -- on every rank, so the task is skipped everywhere
+    (nothing unanswered) and the next task runs; the reference trusts its
+    worklist here."""
+    root = str(tmp_path)
+    items, contents = S.populate(root, 4, [("ok", [0, 1], 2, [5000, 7000])])
+    for h in (0, 1):  # the chunks the escaping path would read, if it were taken
+        os.makedirs(os.path.join(root, f"st{h}", "outside"), exist_ok=True)
+        with open(os.path.join(root, f"st{h}", "outside", "x"), "wb") as f:
+            f.write(b"z" * 100)
+    items = [(bad, 2**40, S.with_p(0b11, 2))] + items
+    st = bcp.gen_run(root, 4, items, nlanes=1)
+    assert st.errors == 0 and st.tasks == 3  # "ok" only: P 2 and sources 0, 1
+    assert parity_of(root, 2, "ok") == oracle.gen_parity_file(contents["ok"])
+    assert not os.path.exists(os.path.join(root, "st2", "outside"))
+    os.remove(S.chunk_path(root, 1, "ok"))
+    st = bcp.rebuild_run(root, 4, 1, items)
+    assert st.errors == 0 and S.read_file(S.chunk_path(root, 1, "ok")) == contents["ok"][1].tobytes()
+    assert S.read_file(os.path.join(root, "st1", "outside", "x")) == b"z" * 100
+
+
 def test_unreadable_parity_root_is_an_error(bcp, tmp_path):
     with pytest.raises(bcp.BcpError):
         bcp.gen_run(str(tmp_path / "missing"), 3, [("x", 0, S.with_p(1, 2))])
