@@ -174,6 +174,31 @@ def test_pipeline_multiwindow_and_delete(bcp, oracle, tmp_path):
     assert not os.path.exists(S.parity_path(root, 3, "small"))
 
 
+def test_pipeline_refuses_paths_outside_the_store(bcp, oracle, tmp_path):
+    """As process_task: an item whose path would leave the targets'
+    directories is skipped (gen and rebuild); the others run."""
+    root = str(tmp_path)
+    items, contents = S.populate(root, 4, [("ok", [0, 1], 2, [5000, 7000])])
+    for h in (0, 1):
+        os.makedirs(os.path.join(root, f"st{h}", "outside"), exist_ok=True)
+        with open(os.path.join(root, f"st{h}", "outside", "x"), "wb") as f:
+            f.write(b"z" * 100)
+    items = [("../outside/x", 2**40, S.with_p(0b11, 2))] + items
+    st = bcp.pipeline_gen(root, 4, items)
+    assert st.errors == 0 and st.tasks == 1
+    assert S.read_file(S.parity_path(root, 2, "ok")) == oracle.gen_parity_file(contents["ok"])
+    assert not os.path.exists(os.path.join(root, "st2", "outside"))
+    os.remove(S.chunk_path(root, 1, "ok"))
+    pl = bcp.Pipeline()
+    try:
+        st = pl.rebuild(root, 4, 1, items)
+    finally:
+        pl.close()
+    assert st.errors == 0 and st.tasks == 1
+    assert S.read_file(S.chunk_path(root, 1, "ok")) == contents["ok"][1].tobytes()
+    assert S.read_file(os.path.join(root, "st1", "outside", "x")) == b"z" * 100
+
+
 def test_pipeline_object_reuse_and_growth(bcp, oracle, tmp_path):
     """One long-lived pipeline, several runs; the second needs bigger slabs."""
     root = str(tmp_path)
