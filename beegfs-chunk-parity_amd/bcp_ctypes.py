@@ -628,7 +628,7 @@ class PDB:
 
 
 def pipeline_gen(store_root: str, ntargets: int, items, device: int = 0, slab_bytes: int = 256 << 20,
-                 io_threads: int = 0, nslots: int = 3, log=None, ndevices: int = 1) -> RunStats:
+                 io_threads: int = 0, nslots: int = 4, log=None, ndevices: int = 1) -> RunStats:
     """Batched end-to-end parity generation (bcp_pipeline_gen)."""
     arr, keep = _items(items)
     st = RunStats()
@@ -643,7 +643,7 @@ def pipeline_gen(store_root: str, ntargets: int, items, device: int = 0, slab_by
 class Pipeline:
     """Long-lived batched pipeline (bcp_pipeline_create / run / destroy)."""
 
-    def __init__(self, device: int = 0, slab_bytes: int = 256 << 20, io_threads: int = 0, nslots: int = 3,
+    def __init__(self, device: int = 0, slab_bytes: int = 256 << 20, io_threads: int = 0, nslots: int = 4,
                  ndevices: int = 1):
         h = _V()
         opts = PipelineOpts(device, slab_bytes, io_threads, nslots, ndevices)

@@ -471,7 +471,8 @@ typedef struct {
  * another side queue and written as parity chunk files -- byte-identical
  * to bcp_gen_run's (same header, padding and window replay).  NO_P items are
  * skipped; items without holders unlink their parity chunk.  opts may be
- * NULL ({0, 256 MiB, 0, 3, 1}). */
+ * NULL ({0, 256 MiB, 0, 4, 1}: 4 slots beat 3 by 8-15 % on every
+ * workload in two interleaved A/Bs). */
 int bcp_pipeline_gen(const char *store_root, int ntargets, const bcp_work_item *items, size_t nitems,
                      const bcp_pipeline_opts *opts, FILE *log, bcp_run_stats *stats);
 /* The same as a long-lived object: engine, queues, io threads and pinned /

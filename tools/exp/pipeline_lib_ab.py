@@ -71,7 +71,7 @@ def main():
     probe = ctypes.CDLL(bcp.LIB_PATH)
     for name in [n for n in bcp._SIGS if not hasattr(probe, n)]:
         del bcp._SIGS[name]
-    nslots = int(os.environ.get("PLAB_NSLOTS", "3"))  # the .sh's "lib@nslots" entries
+    nslots = int(os.environ.get("PLAB_NSLOTS", "4"))  # the .sh's "lib@nslots" entries
     pl = bcp.Pipeline(nslots=nslots)
     try:
         for name, (nt, files) in L.items():

@@ -11,7 +11,7 @@ timeout -k 10 300 python -u tools/exp/pipeline_lib_ab.py --make $D || exit 1
 set -- $LIBS
 for r in $(seq 1 ${ROUNDS:-3}); do
   for ent in "$@"; do  # "lib" or "lib@nslots"
-    lib=${ent%@*}; ns=3; [ "$ent" != "$lib" ] && ns=${ent#*@}
+    lib=${ent%@*}; ns=4; [ "$ent" != "$lib" ] && ns=${ent#*@}
     PLAB_NSLOTS=$ns BCP_LIB=$lib timeout -k 10 240 python -u tools/exp/pipeline_lib_ab.py --run $D --label "r$r" || exit 1
   done
   set -- "${@:2}" "$1"
