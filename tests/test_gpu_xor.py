@@ -87,6 +87,22 @@ def test_dropin_xor_parity(bcp, oracle, engine, n, nbytes):
     assert np.array_equal(dst, oracle.xor_parity(data, nbytes, n))
 
 
+@pytest.mark.parametrize("doff,soff", [(1, 3), (7, 0), (0, 15), (13, 9)])
+def test_dropin_misaligned_host_buffers(bcp, oracle, engine, doff, soff):
+    """The reference's callers pass data_a + src*buffer_size and a malloc'd
+    P_block: any alignment.  The drop-in stages rows to 256-byte device
+    pitch, so host buffers at odd addresses and bytes around the
+    destination stay as they were."""
+    rng = np.random.default_rng(doff * 31 + soff)
+    for n, nb in ((3, 100003), (8, 4097), (1, 17)):
+        sbuf = rng.integers(0, 256, size=n * nb + soff, dtype=np.uint8)
+        dbuf = np.full(nb + doff + 16, 0x5A, dtype=np.uint8)
+        data, dst = sbuf[soff:soff + n * nb], dbuf[doff:doff + nb]
+        bcp.xor_parity(dst, nb, data, n)
+        assert np.array_equal(dst, oracle.xor_parity(np.ascontiguousarray(data), nb, n))
+        assert (dbuf[:doff] == 0x5A).all() and (dbuf[doff + nb:] == 0x5A).all()
+
+
 def test_dropin_golden_edge_vectors(bcp, oracle, engine):
     for fx in GOLD["edge"]:
         if fx["kind"] != "xor_parity":
