@@ -42,7 +42,7 @@ class WorkItem(ctypes.Structure):
 
 class RunStats(ctypes.Structure):
     _fields_ = [("seconds", ctypes.c_double), ("tasks", ctypes.c_uint64), ("bytes_read", ctypes.c_uint64),
-                ("bytes_written", ctypes.c_uint64), ("errors", ctypes.c_int)]
+                ("bytes_written", ctypes.c_uint64), ("errors", ctypes.c_int), ("refused", ctypes.c_uint64)]
 
 
 class PipelineTiming(ctypes.Structure):

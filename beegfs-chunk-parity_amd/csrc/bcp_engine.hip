@@ -52,7 +52,12 @@ struct DescSlot {
   bool used = false;
   DescTile *tiles = nullptr;    // this slot's tile records (desc_tiles -> xor_desc)
   size_t tiles_cap = 0;         // in records
-  uint64_t rec_key = 0;         // desc_reuse_records: the staged tables the records were made from
+  // desc_reuse_records: the launch parameters and a copy of the staged
+  // tables the records were made from; rec_ok only while `dev` and `tiles`
+  // still hold them (any other use of the slot clears it)
+  uint64_t rec_key = 0;
+  void *rec_copy = nullptr;
+  size_t rec_len = 0;
   bool rec_ok = false;
 };
 
@@ -194,6 +199,7 @@ static int ring_acquire(bcp_queue *q, size_t bytes, DescSlot **out) {
   q->next_slot = (q->next_slot + 1) % kRingSlots;
   if (s->used) HIP_RC(hipEventSynchronize(s->done));
   if (s->cap < bytes) {
+    s->rec_ok = false;
     if (s->host) HIP_RC(hipHostFree(s->host));
     if (s->dev) HIP_RC(hipFree(s->dev));
     s->host = s->dev = nullptr;
@@ -404,6 +410,7 @@ extern "C" int bcp_queue_destroy(bcp_queue *q) {
     if (s.done) (void)hipEventDestroy(s.done);
     if (s.copied) (void)hipEventDestroy(s.copied);
     if (s.tiles) (void)hipFree(s.tiles);
+    free(s.rec_copy);
   }
   if (q->copy_stream) (void)hipStreamDestroy(q->copy_stream);
   for (auto &t : q->timer)
@@ -829,6 +836,7 @@ static int submit_desc(bcp_queue *q, const bcp_stripe *stripes, uint32_t nstripe
     DescSlot *slot = nullptr;
     int rc = ring_acquire(q, bytes, &slot);
     if (rc) return rc;
+    slot->rec_ok = false;  // its tables and records are about to be overwritten
     memcpy(slot->host, stripes, (size_t)nstripes * sizeof(bcp_stripe));
     memcpy((char *)slot->host + off_src, sources, (size_t)nsources * sizeof(bcp_source));
     char *d = nullptr;
@@ -898,14 +906,17 @@ static int submit_desc(bcp_queue *q, const bcp_stripe *stripes, uint32_t nstripe
   }
   const uint32_t acc = (uint32_t)acc64;
   ts[nstripes] = acc;
-  // desc_reuse_records: the same tables on this slot as last time -> its records stand
-  uint64_t key = 0;
-  if (e->tuning.desc_reuse_records) {
-    key = 1469598103934665603ull ^ ((uint64_t)acc << 32) ^ tile_bytes ^ ((uint64_t)vecs << 20);
-    const uint64_t *w = (const uint64_t *)h;
-    for (size_t i = 0; i < bytes / 8; i++) key = (key ^ w[i]) * 1099511628211ull;
-  }
-  const bool reuse = e->tuning.desc_reuse_records && slot->rec_ok && slot->rec_key == key && slot->tiles_cap >= acc;
+  // Host-resident tables only when desc_tiles alone reads them: the general
+  // and wide tile paths read them again per tile.
+  const size_t host_max = plain ? (size_t)e->tuning.desc_table_host_max : 0;
+  // desc_reuse_records: byte-identical tables and launch parameters on this
+  // slot as the last descriptor batch it ran -> its records stand (where the
+  // tables are read from is part of the key: the device copy exists only if
+  // they were uploaded)
+  const uint64_t key = ((uint64_t)acc << 32) ^ ((uint64_t)tile_bytes << 5) ^ ((uint64_t)vecs << 1) ^
+                       (uint64_t)(bytes <= host_max);
+  const bool reuse = e->tuning.desc_reuse_records && slot->rec_ok && slot->rec_key == key &&
+                     slot->rec_len == bytes && slot->tiles_cap >= acc && memcmp(slot->rec_copy, h, bytes) == 0;
   slot->rec_ok = false;
   if (slot->tiles_cap < acc) {
     // the slot's previous kernels have finished (ring_acquire waited)
@@ -924,9 +935,6 @@ static int submit_desc(bcp_queue *q, const bcp_stripe *stripes, uint32_t nstripe
   // keep it in line (a cross-stream wait costs more than it hides).
   const bool side = acc >= 2u * (uint32_t)grid;
   char *d = nullptr;
-  // Host-resident tables only when desc_tiles alone reads them: the general
-  // and wide tile paths read them again per tile.
-  const size_t host_max = plain ? (size_t)e->tuning.desc_table_host_max : 0;
   if (reuse) d = bytes <= host_max ? (char *)slot->host : (char *)slot->dev;  // uploaded last time, unchanged
   else if ((rc = stage_tables(q, slot, bytes, host_max, &d, !side))) return rc;
   DescBatch b;
@@ -958,8 +966,21 @@ static int submit_desc(bcp_queue *q, const bcp_stripe *stripes, uint32_t nstripe
   if ((rc = queue_launched(q, le, (uint64_t)acc + (uint64_t)grid))) return rc;
   HIP_RC(hipEventRecord(slot->done, q->stream));
   slot->used = true;
-  slot->rec_key = key;
-  slot->rec_ok = e->tuning.desc_reuse_records != 0;
+  if (e->tuning.desc_reuse_records && !reuse) {
+    if (slot->rec_len < bytes || !slot->rec_copy) {
+      free(slot->rec_copy);
+      slot->rec_copy = malloc(bytes);
+      slot->rec_len = 0;
+    }
+    if (slot->rec_copy) {
+      memcpy(slot->rec_copy, h, bytes);
+      slot->rec_len = bytes;
+      slot->rec_key = key;
+      slot->rec_ok = true;
+    }
+  } else if (reuse) {
+    slot->rec_ok = true;
+  }
   return 0;
 }
 

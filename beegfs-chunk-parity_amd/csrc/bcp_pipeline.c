@@ -45,6 +45,7 @@
 #include <unistd.h>
 
 #include "bcp_host.h"
+#include "bcp_runner.h"
 
 #define ROW 256u
 #define WINDOW ((uint64_t)BCP_WINDOW_BYTES)
@@ -696,6 +697,8 @@ int bcp_pipeline_run(bcp_pipeline *pl, const char *store_root, int ntargets, con
     }
     rc = pipeline_exec(pl, store_root, tasks, nt, -1, log, stats, t0);
     free(tasks);
+    if (stats)
+        stats->refused = bcpr_count_refused(items, nitems, -1);
     return rc;
 }
 
@@ -1008,6 +1011,8 @@ int bcp_pipeline_rebuild(bcp_pipeline *pl, const char *store_root, int ntargets,
     }
     int rc = pipeline_exec(pl, store_root, tasks, nt, corrupt_fd, log, stats, t0);
     free(tasks);
+    if (stats)
+        stats->refused = bcpr_count_refused(items, nitems, rebuild_target);
     if (corrupt_fd >= 0)
         close(corrupt_fd);
     return rc;

@@ -542,6 +542,7 @@ static int pool_run(bcp_rank_pool *P, int op, const char *root, const bcp_work_i
     if (pending > 0 && !rc)
         rc = -ECHILD; /* reports missing: every rank is gone */
     st.seconds = bcpr_now_s() - t0;
+    st.refused = bcpr_count_refused(items, nitems, op == POOL_REBUILD ? rebuild_target : -1);
     if (stats)
         *stats = st;
     if (rc)

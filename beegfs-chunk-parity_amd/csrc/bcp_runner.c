@@ -183,6 +183,24 @@ int bcpr_spawn(pthread_t *th, void *(*fn)(void *), void *arg)
 
 /* ---- generation lanes --------------------------------------------------- */
 
+/* Items a run skips for their path (process_task refuses a path that would
+ * leave the store on every rank): gen counts every item with a P, rebuild
+ * the items do_file's skip rules keep (rebuild_target >= 0). */
+uint64_t bcpr_count_refused(const bcp_work_item *items, size_t nitems, int rebuild_target)
+{
+    uint64_t n = 0;
+    for (size_t i = 0; i < nitems; i++) {
+        const uint64_t loc = items[i].fi.locations;
+        const int P = GET_P(loc);
+        if ((uint64_t)P == NO_P)
+            continue;
+        if (rebuild_target >= 0 && (P == rebuild_target || !TEST_BIT(loc, rebuild_target)))
+            continue;
+        n += !bcpi_path_ok(items[i].path, (size_t)-1);
+    }
+    return n;
+}
+
 /* process_list (gen/main.c:116-164) for one lane of one rank. */
 void *bcpr_gen_lane(void *p)
 {
@@ -198,8 +216,9 @@ void *bcpr_gen_lane(void *p)
             continue;
         double t0 = bcpr_now_s();
         int report = process_task(a->hs, a->items[i].path, &a->items[i].fi, ti);
-        if (a->db) {
-            /* gen/main.c:146-149: keep the entry while it has holders */
+        if (a->db && bcpi_path_ok(a->items[i].path, (size_t)-1)) {
+            /* gen/main.c:146-149: keep the entry while it has holders (a
+             * refused path got no parity: the DB must not claim it has) */
             const char *key = a->items[i].path;
             int rc = (a->items[i].fi.locations & L_MASK) ? bcp_pdb_set(a->db, key, strlen(key), &a->items[i].fi)
                                                           : bcp_pdb_del(a->db, key, strlen(key));
@@ -336,6 +355,7 @@ static int gen_run_impl(const char *store_root, int ntargets, const bcp_work_ite
         }
         for (int k = 0; k < ntargets; k++)
             stats->errors += hs[k].error != 0;
+        stats->refused = bcpr_count_refused(items, nitems, -1);
     }
     for (int i = 0; i < started && !rc; i++)
         rc = args[i].db_rc;
@@ -483,6 +503,7 @@ int bcp_rebuild_run(const char *store_root, int ntargets, int rebuild_target, co
         }
         for (int k = 0; k < ntargets; k++)
             stats->errors += hs[k].error != 0;
+        stats->refused = bcpr_count_refused(items, nitems, rebuild_target);
     }
 out:
     if (hs)
@@ -575,7 +596,7 @@ static void *update_replica(void *p)
     if (!rc)
         rc = bcp_pdb_open(dp, DB_VERSION, &db);
     for (size_t i = 0; i < J->n && !rc; i++) {
-        if ((uint64_t)GET_P(J->items[i].fi.locations) == NO_P)
+        if ((uint64_t)GET_P(J->items[i].fi.locations) == NO_P || !bcpi_path_ok(J->items[i].path, (size_t)-1))
             continue;
         const char *key = J->items[i].path;
         rc = (J->items[i].fi.locations & L_MASK) ? bcp_pdb_set(db, key, strlen(key), &J->items[i].fi)

@@ -59,3 +59,4 @@ int bcpr_rebuild_lanes(void);
 /* -EINVAL for an item process_task would assert on or that names a target
  * outside the world */
 int bcpr_check_items(int ntargets, const bcp_work_item *items, size_t nitems);
+uint64_t bcpr_count_refused(const bcp_work_item *items, size_t nitems, int rebuild_target);

@@ -5,23 +5,30 @@
  *
  *   bcp find-all-chunks <chunks_dir>
  *       bp-find-all-chunks: the record stream on stdout.
- *   bcp parity-gen --complete|--partial [--pipeline|--procs] [--fold MODE] [--lanes N]
- *                  [--force] [--changelog DIR] <store_root> <ntargets>
+ *   bcp parity-gen --complete|--partial [--pipeline|--protocol|--procs] [--fold MODE]
+ *                  [--lanes N] [--force] [--changelog DIR] <store_root> <ntargets>
  *       beegfs-parity-gen + bp-parity-gen (src/beegfs-parity-gen:1-135,
  *       gen/main.c): target bookkeeping, phase 1 from a scan of every
  *       target (--complete) or from record files DIR/st<k> (--partial,
  *       default DIR = <root>/changelog), then one round against the
- *       persistent state, through the per-rank protocol (default, 12 lanes;
- *       ranks as threads, or with --procs as one process per target, as
- *       under mpirun) or the batched pipeline.  --fold picks the P role's GPU
- *       fold: batched, pipelined, device-rows, streamed, zero-copy or staged.  A --complete over an existing state needs
- *       --force and first deletes the old parity data and DBs (the script's
- *       clean_old, :94-108, :120-126).  On success <root>/last-gen-timestamp.
- *   bcp parity-rebuild [--pipeline|--procs] [--fold MODE] [--db DIR] [--corrupt FILE]
- *                      <store_root> <ntargets> <target>
+ *       persistent state.  Engines (byte-identical output):
+ *         --pipeline (default): the batched pipeline on every visible GPU --
+ *           the faster engine for local stores;
+ *         --protocol: the per-rank protocol (process_task, 12 lanes per rank,
+ *           ranks as threads) -- the reference's interface;
+ *         --procs: the same with one process per target, as under mpirun.
+ *       --fold picks the protocol P role's GPU fold: pipelined (default) or
+ *       batched.  A --complete over an existing state needs --force and first
+ *       deletes the old parity data and DBs (the script's clean_old,
+ *       :94-108, :120-126).  On success <root>/last-gen-timestamp.
+ *   bcp parity-rebuild [--pipeline|--protocol|--procs] [--fold MODE] [--lanes N] [--db DIR]
+ *                      [--corrupt FILE] <store_root> <ntargets> <target>
  *       beegfs-parity-rebuild + bp-parity-rebuild (rebuild/main.c), through
- *       the per-rank protocol (default; --procs: rank processes) or the
- *       batched pipeline.
+ *       the batched pipeline (default), the per-rank protocol (--protocol)
+ *       or rank processes (--procs).
+ *
+ * Items whose path would leave the store (absolute, "..") are skipped and
+ * counted as refused; a run with refused items exits 1.
  *
  * Exit status 0 on success, 1 on any error (message on stderr).
  */
@@ -40,11 +47,13 @@
 static int usage(void)
 {
     fputs("usage: bcp find-all-chunks <chunks_dir>\n"
-          "       bcp parity-gen --complete|--partial [--pipeline|--procs] [--fold MODE] [--lanes N] [--force]\n"
-          "                      [--changelog DIR] <store_root> <ntargets>\n"
-          "       bcp parity-rebuild [--pipeline|--procs] [--fold MODE] [--lanes N] [--db DIR] [--corrupt FILE]\n"
-          "                          <store_root> <ntargets> <target>\n"
-          "       MODE: pipelined (default) | batched\n",
+          "       bcp parity-gen --complete|--partial [--pipeline|--protocol|--procs] [--fold MODE] [--lanes N]\n"
+          "                      [--force] [--changelog DIR] <store_root> <ntargets>\n"
+          "       bcp parity-rebuild [--pipeline|--protocol|--procs] [--fold MODE] [--lanes N] [--db DIR]\n"
+          "                          [--corrupt FILE] <store_root> <ntargets> <target>\n"
+          "       engine: --pipeline (default: batched pipeline on every GPU) | --protocol (per-rank\n"
+          "               process_task, ranks as threads) | --procs (ranks as processes)\n"
+          "       MODE (protocol P-role fold): pipelined (default) | batched\n",
           stderr);
     return 1;
 }
@@ -109,7 +118,7 @@ static double now_s(void)
 static int cmd_gen(int argc, char **argv)
 {
     const double t_start = now_s();
-    int complete = -1, use_pipeline = 0, use_procs = 0, lanes = 12, force = 0;
+    int complete = -1, engines = 0, use_pipeline = 1, use_procs = 0, lanes = 12, force = 0;
     const char *changelog = NULL;
     int i = 0;
     for (; i < argc && argv[i][0] == '-'; i++) {
@@ -118,9 +127,11 @@ static int cmd_gen(int argc, char **argv)
         else if (!strcmp(argv[i], "--partial"))
             complete = 0;
         else if (!strcmp(argv[i], "--pipeline"))
-            use_pipeline = 1;
+            engines++, use_pipeline = 1;
+        else if (!strcmp(argv[i], "--protocol"))
+            engines++, use_pipeline = 0;
         else if (!strcmp(argv[i], "--procs"))
-            use_procs = 1;
+            engines++, use_pipeline = 0, use_procs = 1;
         else if (!strcmp(argv[i], "--fold") && i + 1 < argc) {
             if (fold_mode_arg(argv[++i]) < 0 || bcp_task_set_fold_mode(fold_mode_arg(argv[i])) < 0)
                 return usage();
@@ -134,7 +145,7 @@ static int cmd_gen(int argc, char **argv)
         else
             return usage();
     }
-    if (complete < 0 || argc - i != 2 || (use_pipeline && use_procs))
+    if (complete < 0 || argc - i != 2 || engines > 1)
         return usage();
     const char *root = argv[i];
     const int ntargets = atoi(argv[i + 1]);
@@ -211,13 +222,18 @@ static int cmd_gen(int argc, char **argv)
     if (rc)
         return fail("parity generation", rc);
     const double t_end = now_s();
-    printf("worklist %zu items, %llu tasks, %.3f s, %.1f MiB read, %.1f MiB written, %d rank errors\n", planned,
-           (unsigned long long)st.tasks, st.seconds, st.bytes_read / 1048576.0, st.bytes_written / 1048576.0,
-           st.errors);
+    printf("worklist %zu items, %llu tasks, %.3f s, %.1f MiB read, %.1f MiB written, %d rank errors, "
+           "%llu refused (%s)\n",
+           planned, (unsigned long long)st.tasks, st.seconds, st.bytes_read / 1048576.0,
+           st.bytes_written / 1048576.0, st.errors, (unsigned long long)st.refused,
+           use_pipeline ? "pipeline" : use_procs ? "rank processes" : "protocol");
     /* stage timings, as the reference's rank 0 prints them (gen/main.c:920-928) */
     printf("timings: init %.3f s, phase1 %.3f s, engine setup %.3f s, round %.3f s (run %.3f s), total %.3f s\n",
            t_phase1 - t_start, t_round - t_phase1, t_setup - t_round, t_end - t_setup, st.seconds, t_end - t_start);
-    if (st.errors)
+    if (st.refused)
+        fprintf(stderr, "bcp: %llu item(s) refused: paths outside the store have no parity\n",
+                (unsigned long long)st.refused);
+    if (st.errors || st.refused)
         return 1;
     FILE *f = fopen(ts_path, "w");
     if (!f)
@@ -231,7 +247,7 @@ static int cmd_gen(int argc, char **argv)
 static int cmd_rebuild(int argc, char **argv)
 {
     const char *db = NULL, *corrupt = NULL;
-    int use_pipeline = 0, use_procs = 0;
+    int engines = 0, use_pipeline = 1, use_procs = 0;
     int i = 0;
     for (; i < argc && argv[i][0] == '-'; i++) {
         if (!strcmp(argv[i], "--db") && i + 1 < argc)
@@ -239,9 +255,11 @@ static int cmd_rebuild(int argc, char **argv)
         else if (!strcmp(argv[i], "--corrupt") && i + 1 < argc)
             corrupt = argv[++i];
         else if (!strcmp(argv[i], "--pipeline"))
-            use_pipeline = 1;
+            engines++, use_pipeline = 1;
+        else if (!strcmp(argv[i], "--protocol"))
+            engines++, use_pipeline = 0;
         else if (!strcmp(argv[i], "--procs"))
-            use_procs = 1;
+            engines++, use_pipeline = 0, use_procs = 1;
         else if (!strcmp(argv[i], "--fold") && i + 1 < argc) {
             if (fold_mode_arg(argv[++i]) < 0 || bcp_task_set_fold_mode(fold_mode_arg(argv[i])) < 0)
                 return usage();
@@ -251,7 +269,7 @@ static int cmd_rebuild(int argc, char **argv)
         } else
             return usage();
     }
-    if (argc - i != 3 || (use_pipeline && use_procs))
+    if (argc - i != 3 || engines > 1)
         return usage();
     const char *root = argv[i];
     const int ntargets = atoi(argv[i + 1]), target = atoi(argv[i + 2]);
@@ -292,10 +310,12 @@ static int cmd_rebuild(int argc, char **argv)
     }
     if (rc)
         return fail("rebuild", rc);
-    printf("rebuilt target %d: %llu tasks, %.3f s, %.1f MiB read, %.1f MiB written, %d rank errors\n", target,
-           (unsigned long long)st.tasks, st.seconds, st.bytes_read / 1048576.0, st.bytes_written / 1048576.0,
-           st.errors);
-    return st.errors ? 1 : 0;
+    printf("rebuilt target %d: %llu tasks, %.3f s, %.1f MiB read, %.1f MiB written, %d rank errors, "
+           "%llu refused (%s)\n",
+           target, (unsigned long long)st.tasks, st.seconds, st.bytes_read / 1048576.0,
+           st.bytes_written / 1048576.0, st.errors, (unsigned long long)st.refused,
+           use_pipeline ? "pipeline" : use_procs ? "rank processes" : "protocol");
+    return (st.errors || st.refused) ? 1 : 0;
 }
 
 int main(int argc, char **argv)

@@ -30,12 +30,21 @@ kernel-trace stats and PMC passes of the same command (profiles/**/*pmc*.json,
 tools/pmc_summary.py) when they match this workload, else null.
 n_gpus counts DISTINCT devices (PCI bus ids gathered over gloo): ranks that
 share a GPU are flagged shared_gpu instead of being reported as more GPUs.
-cpu_baseline: rank 0 at N=1 times the reference's OWN xor_parity
+cpu_baseline (every N and every mode): after the device timing and its
+verification, rank 0 times the reference's OWN xor_parity
 (task_processing.c:96-109 compiled unchanged -std=gnu99 -Os into oracle/_ref,
 kind "reference"; the oracle's restatement, kind "port", where _ref was not
-built) on a bounded sample of the same stripe shape at 1 thread, 16 threads
-(the box's CPU share for one GPU) and len(sched_getaffinity) threads; value =
-the fastest of those legs, nproc and the affinity count stated.
+built) on a bounded sample of the same stripe shapes -- mixed mode: each stripe
+one window of max_cs per source, zero-padded rows, as the reference's P role
+folds them -- while the other ranks wait at a gloo barrier.  Legs at 1 thread
+and at the CPUs this process may really use (affinity capped by the cgroup CPU
+quota, /sys/fs/cgroup/cpu.max; the quota is stated); value = the faster leg.
+e2e (every N, out of `value`): each rank then runs the batched pipeline on its
+own GPU over its own store of chunk files in /dev/shm (config-5 shapes, about
+--e2e-gib GiB per rank, created and removed by the rank): gen (cold + warm
+runs) and the rebuild of one lost target, all ranks at once, sampled parity
+files and rebuilt chunks checked with numpy; rates against the H2D link each
+rank measures over pinned memory at the same time.
 The output is verified after timing: cleared, one more step, then fold
 conservation plus sampled stripes compared byte for byte with numpy.
 """
@@ -78,9 +87,14 @@ def parse():
     ap.add_argument("--contig", action="store_true", help="physically contiguous device allocations (A/B knob)")
     ap.add_argument("--opt", action="append", default=[], metavar="KEY=VALUE",
                     help="engine option (bcp_set_option) for A/B runs; repeatable")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget over its three legs")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget over its legs")
     ap.add_argument("--cpu-stripes", type=int, default=256, help="stripes in the 1-thread CPU sample pool")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--e2e-gib", type=float, default=2.0, help="chunk bytes per rank in the end-to-end store")
+    ap.add_argument("--e2e-reps", type=int, default=3, help="warm end-to-end gen runs (after one cold run)")
+    ap.add_argument("--e2e-dir", default="/dev/shm", help="where the end-to-end stores are created")
+    ap.add_argument("--e2e-max-s", type=float, default=150.0, help="wall-time cap of the end-to-end leg")
+    ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--allow-shared", action="store_true",
                     help="run N ranks even when fewer than N distinct GPUs exist (rehearsal; "
                          "the line then says shared_gpu true and counts distinct GPUs)")
@@ -110,17 +124,75 @@ def box_of(pci_bus_id: str) -> dict:
             "pci_bus_id": pci_bus_id, "cpu_model": model, "host": socket.gethostname()}
 
 
+KFD_NODES = "/sys/class/kfd/kfd/topology/nodes"
+
+
+def kfd_gpus(nodes_dir: str = KFD_NODES, dri_dir: str = "/dev/dri", env=None) -> int:
+    """GPUs this process could use, counted WITHOUT touching HIP: KFD topology
+    nodes with a non-zero gfx_target_version whose render node exists here and
+    is read-write (a container sees every node of the host in sysfs but only
+    its own render nodes), capped by ROCR_/HIP_/CUDA_VISIBLE_DEVICES when set."""
+    env = os.environ if env is None else env
+    n = 0
+    for p in sorted(glob.glob(os.path.join(nodes_dir, "*", "properties"))):
+        kv = {}
+        try:
+            for line in open(p):
+                k, _, v = line.strip().partition(" ")
+                kv[k] = v
+        except OSError:
+            continue
+        try:
+            gfx, minor = int(kv.get("gfx_target_version", "0")), int(kv.get("drm_render_minor", "0"))
+        except ValueError:
+            continue
+        dri = os.path.join(dri_dir, f"renderD{minor}")
+        if gfx > 0 and minor > 0 and os.access(dri, os.R_OK | os.W_OK):
+            n += 1
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = env.get(var)
+        if v is not None:
+            n = min(n, len([x for x in v.split(",") if x.strip()]))
+    return n
+
+
+def cpu_quota(cgroup_root: str = "/sys/fs/cgroup"):
+    """CPUs the cgroup quota allows (cgroup v2 cpu.max, else v1 cfs), or None."""
+    try:
+        q, per = open(os.path.join(cgroup_root, "cpu.max")).read().split()[:2]
+        return None if q == "max" else int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(open(os.path.join(cgroup_root, "cpu", "cpu.cfs_quota_us")).read())
+        per = int(open(os.path.join(cgroup_root, "cpu", "cpu.cfs_period_us")).read())
+        return None if q <= 0 else q / per
+    except (OSError, ValueError):
+        return None
+
+
+def usable_cpus() -> tuple[int, int, float | None]:
+    """(threads worth running, affinity count, quota) -- affinity capped by the
+    quota: threads beyond the quota only measure oversubscription."""
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = os.cpu_count() or 1
+    quota = cpu_quota()
+    use = affinity if quota is None else max(1, min(affinity, int(quota + 0.5)))
+    return min(use, 256), affinity, quota
+
+
 def launch_ranks(a) -> int:
     """`bench.py --gpus N` without a launcher (WORLD_SIZE unset): run N ranks,
     one process per GPU, as a torchrun CHILD process and return its exit code.
-    Called before anything touches HIP (bcp_ctypes loads libbcp lazily), and
-    never by exec.  Refuses (rc 4) when fewer than N GPUs are visible, unless
-    --allow-shared; the ranks check the distinct PCI bus ids themselves too."""
+    This parent never touches HIP or torch: the GPUs are counted from KFD
+    sysfs (kfd_gpus).  Refuses (rc 4) when fewer than N GPUs are visible,
+    unless --allow-shared; the ranks check the distinct PCI bus ids themselves too."""
     import socket
     import subprocess
     if not a.allow_shared:
-        import torch  # device_count() enumerates without initialising HIP on this image
-        ndev = torch.cuda.device_count()
+        ndev = kfd_gpus()
         if ndev < a.gpus:
             print(f"bench.py: --gpus {a.gpus} but {ndev} GPU(s) visible; refusing to report "
                   f"{a.gpus} GPUs (pass --allow-shared to rehearse with shared devices)", file=sys.stderr)
@@ -161,6 +233,250 @@ def pmc_traffic(workload_key: str, kernel_tag: str):
             doc.setdefault("files", {})["pmc_summary"] = os.path.relpath(path, ROOT)
             best = doc
     return best
+
+
+def cpu_baseline(a, N: int, C: int, lens_all) -> dict:
+    """The reference CPU path on this box's host cores (rank 0, after the
+    device timing): its own xor_parity over a bounded sample of the timed
+    workload's stripe shapes, at 1 thread and at usable_cpus() threads."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # cpu_baseline leg only
+    use_ref = oracle.ref_lib() is not None
+    use, affinity, quota = usable_cpus()
+    legs_t = sorted({1, use})
+    leg_s = a.cpu_seconds / len(legs_t)
+    legs = []
+    if lens_all is not None:
+        import numpy as np
+        shapes = np.asarray(lens_all[:min(len(lens_all), 64)], dtype=np.uint64)
+        for t in legs_t:
+            bps = oracle.bench_xor_shapes(t, shapes, leg_s, use_ref=use_ref)
+            legs.append({"threads": t, "value": round(bps / GiB, 3), "stripe_shapes": int(len(shapes))})
+        what = (f"each thread folds its share of the first {len(shapes)} timed stripe shapes ({N} chunks, "
+                f"log-uniform 64 KiB-4 MiB) as the reference's P role does: one window of max_cs per source, "
+                f"zero-padded rows; sum of lengths + max_cs bytes per stripe")
+    else:
+        for t in legs_t:
+            # private pool per thread: ~2 GiB in all at 16 threads (out of
+            # cache), at least 4 stripes each when many threads run
+            per_thread = a.cpu_stripes if t == 1 else max(4, a.cpu_stripes * 2 // t)
+            bps = oracle.bench_xor(t, per_thread, N, C, leg_s, use_ref=use_ref)
+            legs.append({"threads": t, "value": round(bps / GiB, 3), "pool_stripes_per_thread": per_thread})
+        what = (f"each thread folds a private pool of {N} x {C // KiB} KiB synthetic stripes; "
+                f"(N+1)*S bytes per stripe")
+    best = max(legs, key=lambda x: x["value"])
+    model = ""
+    try:
+        model = next(l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name"))
+    except (OSError, StopIteration):
+        pass
+    fn = ("the reference's own xor_parity (task_processing.c:96-109 compiled unchanged, -std=gnu99 -Os, "
+          "oracle/_ref)") if use_ref else "oracle_xor_parity (the reference's xor_parity restated, -std=gnu99 -Os)"
+    return {"value": best["value"], "unit": "GiB/s", "cores": best["threads"],
+            "kind": "reference" if use_ref else "port",
+            "sample": f"{fn}: {what}, in a loop for >= {leg_s:g} s per leg; legs at 1 thread and at the "
+                      f"usable CPUs (affinity capped by the cgroup quota), value = the faster leg; "
+                      f"rank 0, after the device timing",
+            "legs": legs, "nproc": os.cpu_count(), "affinity_cpus": affinity,
+            "quota_cpus": None if quota is None else round(quota, 2), "cpu_model": model}
+
+
+def e2e_leg(a, d, device: int, bus_id: str):
+    """End to end from chunk files, every rank on its own GPU at once: a store
+    of config-5 shapes (8-wide stripes, chunk lengths log-uniform in
+    [64 KiB, 4 MiB], 9 storage targets, P rotating over the one left out) of
+    about --e2e-gib per rank in --e2e-dir; the batched pipeline generates every
+    parity file (one cold run, --e2e-reps warm), then target 4 is lost (its
+    chunk files deleted, outside the timing) and rebuilt.  The reference's
+    I/O path: task_processing.c:62-79,186,199-226 (read, fold, write).
+    Returns the rank-0 summary (None elsewhere); never part of `value`."""
+    import concurrent.futures as cf
+    import shutil
+
+    import numpy as np
+    import bcp_store as BS
+    t_start = time.perf_counter()
+    NT, W, VICTIM = 9, 8, 4
+    rank_root = os.path.join(a.e2e_dir, f"bcp_bench_e2e_{os.getppid()}_{d.rank}")
+    want = int(a.e2e_gib * GiB)
+    reason = None
+    try:
+        stv = os.statvfs(a.e2e_dir)
+        free = stv.f_bavail * stv.f_frsize
+        # chunks + parity (~35 % of the chunk bytes at these shapes) + one rebuilt target
+        room = int(free / (1.7 * d.world))
+        if room < want:
+            want = room
+        if want < (64 << 20):
+            reason = f"{a.e2e_dir}: {free / GiB:.1f} GiB free for {d.world} rank stores"
+    except OSError as e:
+        reason = f"{a.e2e_dir}: {e}"
+    # every rank agrees to run (or not): a rank that skipped would leave the
+    # others waiting at the barriers below
+    if d.sum(0.0 if reason else 1.0) != d.world:
+        if d.rank == 0:
+            return {"skipped": reason or "another rank could not create its store"}
+        return None
+    rng = np.random.default_rng(5 + d.rank)
+    lens, tot = [], 0
+    while tot < want:
+        ls = np.exp(rng.uniform(np.log(64 * KiB), np.log(4 * 1024 * KiB), size=W)).astype(np.int64)
+        lens.append(ls)
+        tot += int(ls.sum())
+    nst = len(lens)
+    block = rng.integers(0, 256, size=12 << 20, dtype=np.uint8)
+    files = []
+    for i in range(nst):
+        p = i % NT
+        files.append((f"e2e/{i % 64:02x}/chunk{i}", [t for t in range(NT) if t != p], p))
+
+    def chunk_of(i, k):
+        off = ((i * W + k) * 40961) % (8 << 20)
+        return block[off:off + int(lens[i][k])]
+
+    def write_stripe(i):
+        path, holders, _ = files[i]
+        for k, h in enumerate(holders):
+            fn = BS.chunk_path(rank_root, h, path)
+            os.makedirs(os.path.dirname(fn), exist_ok=True)
+            with open(fn, "wb") as f:
+                f.write(memoryview(chunk_of(i, k)))
+
+    out = {}
+    pl = None
+    try:
+        shutil.rmtree(rank_root, ignore_errors=True)
+        BS.make_store(rank_root, NT)
+        t0 = time.perf_counter()
+        with cf.ThreadPoolExecutor(8) as ex:
+            list(ex.map(write_stripe, range(nst)))
+        t_store = time.perf_counter() - t0
+        ts = int(time.time()) + 3600
+        items = [(path, ts, BS.with_p(sum(1 << h for h in hs), p)) for path, hs, p in files]
+        rd = int(sum(int(x.sum()) for x in lens))
+        wr = int(sum(8 * W + int(x.max()) for x in lens))
+        # the H2D / D2H link of this rank's GPU, measured by every rank at once
+        eng = bcp.Engine(device)
+        q = eng.queue()
+        nb = 256 << 20
+        h = eng.host_alloc(nb)
+        dv = eng.alloc(nb)
+        link = {}
+        d.barrier()
+        for name, fn in (("h2d_GBps", lambda: q.h2d(dv, h, nb)), ("d2h_GBps", lambda: q.d2h(h, dv, nb))):
+            tt = []
+            for _ in range(5):
+                q.sync()
+                t0 = time.perf_counter()
+                fn()
+                q.sync()
+                tt.append(time.perf_counter() - t0)
+            link[name] = round(nb / float(np.median(tt)) / 1e9, 2)
+        eng.free(dv)
+        eng.host_free(h)
+        q.close()
+        eng.close()
+        pl = bcp.Pipeline(device=device)
+
+        def timed(fn, before=None):
+            if before:
+                before()
+            d.barrier()
+            t0 = time.perf_counter()
+            st = fn()
+            dt = time.perf_counter() - t0
+            return st, dt, d.max(dt), pl.last_timing()
+
+        # ---- gen: one cold run, then warm runs
+        runs, tasks_ok = [], True
+        for r in range(1 + max(1, a.e2e_reps)):
+            if r > 1 and d.max(time.perf_counter() - t_start) > a.e2e_max_s:
+                break
+            st, dt, dmax, tim = timed(lambda: pl.run(rank_root, NT, items))
+            tasks_ok = tasks_ok and st.errors == 0 and st.tasks == nst and st.bytes_read == rd
+            runs.append((dt, dmax, tim))
+        vr = np.random.default_rng(11 + d.rank)
+        sample = sorted({0, nst - 1} | {int(x) for x in vr.integers(0, nst, 6)})
+
+        def parity_ok(i):
+            ch = [chunk_of(i, k) for k in range(W)]
+            m = max(len(c) for c in ch)
+            body = np.zeros(m, dtype=np.uint8)
+            for c in ch:
+                body[:len(c)] ^= c
+            want_file = np.asarray([len(c) for c in ch], dtype="<u8").tobytes() + body.tobytes()
+            return BS.read_file(BS.parity_path(rank_root, files[i][2], files[i][0])) == want_file
+        gen_ok = tasks_ok and all(parity_ok(i) for i in sample)
+        warm = [x[1] for x in runs[1:]] or [runs[0][1]]
+        warm_own = [x[0] for x in runs[1:]] or [runs[0][0]]
+        gen = {"cold_s": round(runs[0][1], 4), "warm_s": round(float(np.median(warm)), 4),
+               "runs_s": [round(x[1], 4) for x in runs], "own_warm_s": round(float(np.median(warm_own)), 4),
+               "timing": runs[-1][2], "verified": gen_ok}
+
+        # ---- rebuild target VICTIM from 7 survivors + parity
+        lost = [i for i in range(nst) if VICTIM in files[i][1]]
+        ordered = sorted(items, key=lambda x: x[0].encode())  # DB key order (rebuild/main.c:223-225)
+        rd3 = sum(int(lens[i].sum()) - int(lens[i][files[i][1].index(VICTIM)]) + int(lens[i].max()) + 8 * W
+                  for i in lost)
+        wr3 = sum(int(lens[i][files[i][1].index(VICTIM)]) for i in lost)
+
+        def drop_victim():
+            with cf.ThreadPoolExecutor(8) as ex:
+                list(ex.map(lambda i: os.remove(BS.chunk_path(rank_root, VICTIM, files[i][0])), lost))
+        rruns, rok = [], True
+        for r in range(2):
+            st, dt, dmax, tim = timed(lambda: pl.rebuild(rank_root, NT, VICTIM, ordered), before=drop_victim)
+            rok = rok and st.errors == 0 and st.tasks == len(lost)
+            rruns.append((dt, dmax, tim))
+        rsample = [i for i in sample if i in set(lost)] or lost[:2]
+        rok = rok and all(BS.read_file(BS.chunk_path(rank_root, VICTIM, files[i][0])) ==
+                          chunk_of(i, files[i][1].index(VICTIM)).tobytes() for i in rsample)
+        reb = {"cold_s": round(rruns[0][1], 4), "warm_s": round(rruns[-1][1], 4),
+               "own_warm_s": round(rruns[-1][0], 4), "timing": rruns[-1][2], "verified": rok}
+
+        mine = {"rank": d.rank, "pci_bus_id": bus_id, **link, "stripes": nst, "bytes_read": rd, "bytes_written": wr,
+                "gen_own_warm_s": gen["own_warm_s"], "gen_GiBps": round((rd + wr) / gen["own_warm_s"] / GiB, 2),
+                "gen_input_over_link": round(rd / gen["own_warm_s"] / (link["h2d_GBps"] * 1e9), 3),
+                "rebuild_bytes_read": rd3, "rebuild_bytes_written": wr3, "rebuild_own_warm_s": reb["own_warm_s"],
+                "gen_verified": gen_ok, "rebuild_verified": rok, "store_write_s": round(t_store, 2)}
+        out = {"mine": mine, "gen": gen, "rebuild": reb}
+    finally:
+        if pl is not None:
+            pl.close()
+        shutil.rmtree(rank_root, ignore_errors=True)
+    ranks = d.gather(out.get("mine"))
+    if d.rank != 0:
+        return None
+    gen, reb = out["gen"], out["rebuild"]
+    rd_all = sum(r["bytes_read"] for r in ranks)
+    wr_all = sum(r["bytes_written"] for r in ranks)
+    rd3_all = sum(r["rebuild_bytes_read"] for r in ranks)
+    wr3_all = sum(r["rebuild_bytes_written"] for r in ranks)
+    h2d_all = sum(r["h2d_GBps"] for r in ranks) * 1e9
+    return {
+        "path": ("bcp_pipeline_run / bcp_pipeline_rebuild on every rank's own GPU: chunk files (tmpfs) -> "
+                 "pinned slabs (io threads) -> H2D on a side queue -> xor_desc -> D2H on a side queue -> "
+                 "parity files / rebuilt chunks"),
+        "store": {"dir": a.e2e_dir, "shapes": "config 5: 8-wide stripes, chunks log-uniform 64 KiB-4 MiB, "
+                                              "9 targets, P rotating", "stripes_per_rank": ranks[0]["stripes"],
+                  "chunk_GiB_per_rank": round(ranks[0]["bytes_read"] / GiB, 3)},
+        "ranks": d.world,
+        "gen": {**gen, "bytes_read": rd_all, "bytes_written": wr_all,
+                "GiBps": round((rd_all + wr_all) / gen["warm_s"] / GiB, 2),
+                "input_GiBps": round(rd_all / gen["warm_s"] / GiB, 2),
+                "input_over_link": round(rd_all / gen["warm_s"] / h2d_all, 3),
+                "verified": all(r["gen_verified"] for r in ranks)},
+        "rebuild": {**reb, "target": VICTIM, "bytes_read": rd3_all, "bytes_written": wr3_all,
+                    "GiBps": round((rd3_all + wr3_all) / reb["warm_s"] / GiB, 2),
+                    "input_over_link": round(rd3_all / reb["warm_s"] / h2d_all, 3),
+                    "verified": all(r["rebuild_verified"] for r in ranks)},
+        "link_h2d_GBps_sum": round(h2d_all / 1e9, 2),
+        "rate_note": "GiBps = (chunk bytes read + parity bytes written) of all ranks / the slowest rank's warm "
+                     "run (median); input_over_link = input bytes / that time / the summed H2D rates the ranks "
+                     "measured together over pinned memory; timing = rank 0's host-thread stages (seconds)",
+        "wall_s": round(time.perf_counter() - t_start, 1),
+        "per_rank": ranks,
+    }
 
 
 def main():
@@ -210,6 +526,7 @@ def main():
         a.stripes = hi - lo if d.world == 8 else 12_500
     S, N, C = a.stripes, a.nsrc, a.chunk
     chk = eng.alloc(64)
+    lens_all = None
     if a.mode == "mixed":
         import numpy as np
         rng = np.random.default_rng(3 + d.rank)
@@ -403,39 +720,17 @@ def main():
                          "pct_hbm_peak": round(100.0 * bytes_per_step / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 2),
                          "verified": bool(verified)})
 
+    # end to end from chunk files (every rank on its own GPU, all at once)
+    e2e = None
+    if not a.no_e2e:
+        q.sync()
+        e2e = e2e_leg(a, d, eng.device, bus_ids[d.rank])
+    # the reference CPU path, rank 0 only, after every device figure; the
+    # other ranks wait at the barrier
     cpu = None
-    if d.rank == 0 and d.world == 1 and not a.no_cpu and a.mode != "mixed":
-        sys.path.insert(0, os.path.join(ROOT, "oracle"))
-        import oracle  # cpu_baseline leg only
-        use_ref = oracle.ref_lib() is not None
-        nproc = os.cpu_count() or 1
-        try:
-            affinity = len(os.sched_getaffinity(0))
-        except (AttributeError, OSError):
-            affinity = nproc
-        legs_t = sorted({1, min(16, affinity), affinity})
-        leg_s = a.cpu_seconds / len(legs_t)
-        legs = []
-        for t in legs_t:
-            # private pool per thread: ~2 GiB in all at 16 threads (out of
-            # cache), at least 4 stripes each when the affinity set is large
-            per_thread = a.cpu_stripes if t == 1 else max(4, a.cpu_stripes * 2 // t)
-            bps = oracle.bench_xor(t, per_thread, N, C, leg_s, use_ref=use_ref)
-            legs.append({"threads": t, "value": round(bps / GiB, 3), "pool_stripes_per_thread": per_thread})
-        best = max(legs, key=lambda x: x["value"])
-        model = ""
-        try:
-            model = next(l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name"))
-        except (OSError, StopIteration):
-            pass
-        fn = ("the reference's own xor_parity (task_processing.c:96-109 compiled unchanged, -std=gnu99 -Os, "
-              "oracle/_ref)") if use_ref else "oracle_xor_parity (the reference's xor_parity restated, -std=gnu99 -Os)"
-        cpu = {"value": best["value"], "unit": "GiB/s", "cores": best["threads"],
-               "kind": "reference" if use_ref else "port",
-               "sample": f"{fn}: each thread folds a private pool of {N} x {C // KiB} KiB synthetic stripes "
-                         f"in a loop for >= {leg_s:g} s; (N+1)*S bytes per stripe; legs at 1, 16 and "
-                         f"sched_getaffinity threads, value = the fastest leg",
-               "legs": legs, "nproc": nproc, "affinity_cpus": affinity, "cpu_model": model}
+    if d.rank == 0 and not a.no_cpu:
+        cpu = cpu_baseline(a, N, C, lens_all if a.mode == "mixed" else None)
+    d.barrier()
 
     if d.rank == 0:
         value = total_bytes / wall_max / GiB
@@ -478,7 +773,7 @@ def main():
                 "pci_bus_ids": sorted(set(bus_ids)),
                 "cus": cus,
                 "verified_on_device": ok_all,
-                "per_rank": per_rank if d.world > 1 else None,
+                "per_rank": per_rank,
             },
             "roofline": {
                 "bound": "hbm",
@@ -505,6 +800,8 @@ def main():
                              "average and PMC passes, measured on profile_box (a different box unless same_box)",
             },
             "cpu_baseline": cpu,
+            "per_rank": per_rank,
+            "e2e": e2e,
         }
         print(json.dumps(line), flush=True)
     q.close()

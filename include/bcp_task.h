@@ -307,6 +307,9 @@ typedef struct {
     uint64_t bytes_read;       /* ProgressSample totals over every rank/lane */
     uint64_t bytes_written;
     int errors;                /* ranks that ended with a sticky error */
+    uint64_t refused;          /* items skipped because their path would leave the
+                                  store (absolute, ".."): no parity was written and
+                                  no DB entry made for them (ABI version 2) */
 } bcp_run_stats;
 
 /* ---- persistent chunk state (persistent_db.{c,h}) ---------------------- */
@@ -439,7 +442,7 @@ int bcp_eventset_scan(bcp_eventset *s, int st, const char *chunks_dir, uint64_t 
  * from st<k>/targetNumID (k+1 when absent), checked against and saved to
  * run_data_path.  -EEXIST duplicate id, -ENODEV fewer targets or a target
  * whose id changed ("Storage target missing!"), -EPROTO version stamp. */
-#define BCP_TASK_ABI_VERSION 1
+#define BCP_TASK_ABI_VERSION 2
 int bcp_check_targets(const char *store_root, int ntargets, const char *run_data_path, FILE *log);
 
 /* Cumulative store weights st_weight (gen/main.c:485, 528-536) of

@@ -376,3 +376,120 @@ double oracle_bench_xor(int nthreads, uint64_t nstripes, int nsrc,
 {
     return oracle_bench_xor_fn(NULL, nthreads, nstripes, nsrc, chunk, seconds);
 }
+
+/*
+ * Mixed chunk sizes (config 5), as the reference's P role folds them: per
+ * stripe one window of max_cs = max(len_k) bytes per source, each source's
+ * bytes followed by zeros (chunk_sender zero-pads a short read,
+ * task_processing.c:302-303), folded by fn = xor_parity(dst, max_cs, rows, n)
+ * (task_processing.c:209).  lens is [nshapes][nsrc]; thread t folds the
+ * shapes t, t+nthreads, ... (at least one each, cycled) from private buffers
+ * for at least `seconds`.  Returns aggregate algorithmic bytes/s (sum of the
+ * lengths + max_cs per stripe: the padding is not data) or < 0.  Every shape
+ * must be <= one 10 MiB window (config 5's are <= 4 MiB).
+ */
+typedef struct {
+    xor_fn fn;
+    int nsrc;
+    uint64_t nshapes;       /* this thread's shapes */
+    uint8_t **rows;         /* [nshapes] -> nsrc * max_cs bytes */
+    uint8_t *out;           /* largest max_cs */
+    uint64_t *max_cs, *alg; /* [nshapes] */
+    double seconds, elapsed, bytes;
+} shape_arg;
+
+static void *shape_thread(void *p)
+{
+    shape_arg *a = p;
+    double t0 = now_s(), t, bytes = 0;
+    do {
+        for (uint64_t s = 0; s < a->nshapes; s++) {
+            a->fn(a->out, a->max_cs[s], a->rows[s], a->nsrc);
+            bytes += (double)a->alg[s];
+        }
+        t = now_s();
+    } while (t - t0 < a->seconds);
+    a->bytes = bytes;
+    a->elapsed = t - t0;
+    return NULL;
+}
+
+double oracle_bench_xor_shapes_fn(void *fn, int nthreads, const uint64_t *lens, uint64_t nshapes, int nsrc,
+                                  double seconds)
+{
+    if (nthreads < 1 || nthreads > 256 || nsrc < 1 || nshapes < 1 || !lens)
+        return -1.0;
+    static shape_arg args[256];
+    pthread_t th[256];
+    double rc = 0;
+    memset(args, 0, sizeof(args));
+    for (int t = 0; t < nthreads; t++) {
+        shape_arg *a = &args[t];
+        a->fn = fn ? (xor_fn)fn : oracle_xor_parity;
+        a->nsrc = nsrc;
+        a->seconds = seconds;
+        a->nshapes = nshapes > (uint64_t)nthreads ? (nshapes - (uint64_t)t + (uint64_t)nthreads - 1) / (uint64_t)nthreads : 1;
+        a->rows = calloc(a->nshapes, sizeof(uint8_t *));
+        a->max_cs = calloc(a->nshapes, sizeof(uint64_t));
+        a->alg = calloc(a->nshapes, sizeof(uint64_t));
+        if (!a->rows || !a->max_cs || !a->alg) {
+            rc = -2.0;
+            goto out;
+        }
+        uint64_t biggest = 1;
+        for (uint64_t s = 0; s < a->nshapes; s++) {
+            const uint64_t *l = lens + ((t + s * (uint64_t)nthreads) % nshapes) * (uint64_t)nsrc;
+            uint64_t m = 0, sum = 0;
+            for (int k = 0; k < nsrc; k++) {
+                m = l[k] > m ? l[k] : m;
+                sum += l[k];
+            }
+            if (m > 10u * 1024u * 1024u) {
+                rc = -1.0;
+                goto out;
+            }
+            a->max_cs[s] = m;
+            a->alg[s] = sum + m;
+            biggest = m > biggest ? m : biggest;
+            a->rows[s] = malloc((size_t)(m ? m : 1) * (size_t)nsrc);
+            if (!a->rows[s]) {
+                rc = -2.0;
+                goto out;
+            }
+            for (int k = 0; k < nsrc; k++) {
+                uint8_t *row = a->rows[s] + (size_t)k * m;
+                for (uint64_t i = 0; i < l[k]; i += 8) {
+                    const uint64_t w = splitmix64(i / 8 + 7919ull * (uint64_t)k + 104729ull * s);
+                    memcpy(row + i, &w, l[k] - i < 8 ? (size_t)(l[k] - i) : 8u);
+                }
+                memset(row + l[k], 0, (size_t)(m - l[k]));
+            }
+        }
+        a->out = malloc((size_t)biggest);
+        if (!a->out) {
+            rc = -2.0;
+            goto out;
+        }
+    }
+    for (int t = 0; t < nthreads; t++)
+        pthread_create(&th[t], NULL, shape_thread, &args[t]);
+    double bytes = 0, worst = 0;
+    for (int t = 0; t < nthreads; t++) {
+        pthread_join(th[t], NULL);
+        bytes += args[t].bytes;
+        worst = args[t].elapsed > worst ? args[t].elapsed : worst;
+    }
+    rc = bytes / worst;
+out:
+    for (int t = 0; t < nthreads; t++) {
+        shape_arg *a = &args[t];
+        if (a->rows)
+            for (uint64_t s = 0; s < a->nshapes; s++)
+                free(a->rows[s]);
+        free(a->rows);
+        free(a->max_cs);
+        free(a->alg);
+        free(a->out);
+    }
+    return rc;
+}

@@ -143,6 +143,9 @@ def lib() -> ctypes.CDLL:
         L.oracle_bench_xor_fn.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_uint64, ctypes.c_int,
                                           ctypes.c_uint64, ctypes.c_double]
         L.oracle_bench_xor_fn.restype = ctypes.c_double
+        L.oracle_bench_xor_shapes_fn.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64,
+                                                 ctypes.c_int, ctypes.c_double]
+        L.oracle_bench_xor_shapes_fn.restype = ctypes.c_double
         del u8p
         _lib = L
     return _lib
@@ -255,4 +258,23 @@ def bench_xor(nthreads: int, nstripes: int, nsrc: int, chunk: int, seconds: floa
     r = lib().oracle_bench_xor_fn(fn, nthreads, nstripes, nsrc, chunk, seconds)
     if r < 0:
         raise MemoryError(f"oracle_bench_xor_fn: {r}")
+    return r
+
+
+def bench_xor_shapes(nthreads: int, lens, seconds: float, use_ref: bool = False) -> float:
+    """Algorithmic bytes/s (sum of lengths + max per stripe) of the reference's
+    fold over mixed chunk sizes as its P role runs it: each stripe one window
+    of max_cs bytes per source, zero-padded rows (task_processing.c:209,
+    302-303).  lens: [nstripes][nsrc] chunk lengths (each <= one window)."""
+    arr = np.ascontiguousarray(np.asarray(lens, dtype=np.uint64))
+    assert arr.ndim == 2 and arr.size
+    fn = None
+    if use_ref:
+        L = ref_lib()
+        if L is None:
+            raise FileNotFoundError(REF_LIB_PATH)
+        fn = ctypes.cast(L.ref_xor_parity, ctypes.c_void_p).value
+    r = lib().oracle_bench_xor_shapes_fn(fn, nthreads, arr.ctypes.data, arr.shape[0], arr.shape[1], seconds)
+    if r < 0:
+        raise MemoryError(f"oracle_bench_xor_shapes_fn: {r}")
     return r

@@ -101,3 +101,62 @@ def test_bench_gpus_n_launches_a_torchrun_child(monkeypatch):
     assert cmd[-5:] == ["--gpus", "8", "--steps", "5", "--allow-shared"]
     assert cmd[-6].endswith("bench.py")
     assert seen["env"]["MASTER_ADDR"] == "127.0.0.1"
+
+
+def _props(root, node, gfx, minor):
+    d = os.path.join(root, "nodes", str(node))
+    os.makedirs(d)
+    with open(os.path.join(d, "properties"), "w") as f:
+        f.write(f"cpu_cores_count 0\ngfx_target_version {gfx}\ndrm_render_minor {minor}\n")
+
+
+def test_kfd_gpus_counts_usable_gpu_nodes_without_hip(tmp_path):
+    """The launcher counts GPUs from KFD sysfs: GPU nodes (gfx_target_version
+    > 0) whose render node is usable here; CPU nodes and GPUs of other
+    containers (no render node) do not count; *_VISIBLE_DEVICES caps it."""
+    sys.path.insert(0, ROOT)
+    import bench
+    root, dri = str(tmp_path / "kfd"), tmp_path / "dri"
+    dri.mkdir()
+    _props(root, 0, 0, 0)          # CPU node
+    _props(root, 1, 90500, 128)    # this container's GPU
+    _props(root, 2, 90500, 136)    # this container's GPU
+    _props(root, 3, 90500, 144)    # another container's GPU: no render node here
+    for m in (128, 136):
+        (dri / f"renderD{m}").write_text("")
+    nodes = os.path.join(root, "nodes")
+    assert bench.kfd_gpus(nodes, str(dri), env={}) == 2
+    assert bench.kfd_gpus(nodes, str(dri), env={"HIP_VISIBLE_DEVICES": "0"}) == 1
+    assert bench.kfd_gpus(nodes, str(dri), env={"ROCR_VISIBLE_DEVICES": "0,1,2,3"}) == 2
+    assert bench.kfd_gpus(str(tmp_path / "absent"), str(dri), env={}) == 0
+
+
+def test_cpu_quota_caps_the_cpu_baseline_threads(tmp_path, monkeypatch):
+    sys.path.insert(0, ROOT)
+    import bench
+    (tmp_path / "cpu.max").write_text("1600000 100000\n")
+    assert bench.cpu_quota(str(tmp_path)) == 16.0
+    (tmp_path / "cpu.max").write_text("max 100000\n")
+    assert bench.cpu_quota(str(tmp_path)) is None
+    assert bench.cpu_quota(str(tmp_path / "none")) is None
+    monkeypatch.setattr(bench, "cpu_quota", lambda: 16.0)
+    monkeypatch.setattr(os, "sched_getaffinity", lambda pid: set(range(256)))
+    assert bench.usable_cpus() == (16, 256, 16.0)
+    monkeypatch.setattr(bench, "cpu_quota", lambda: None)
+    monkeypatch.setattr(os, "sched_getaffinity", lambda pid: set(range(8)))
+    assert bench.usable_cpus() == (8, 8, None)
+
+
+def test_launcher_parent_never_imports_torch():
+    """The launcher parent (bench.py --gpus N, no WORLD_SIZE) refuses or
+    starts its ranks without importing torch or loading libbcp: nothing in it
+    can initialise HIP."""
+    import subprocess
+    code = ("import sys, runpy; sys.argv = ['bench.py', '--gpus', '2', '--stripes', '8', '--no-cpu'];\n"
+            "try:\n    runpy.run_path('bench.py', run_name='__main__')\n"
+            "except SystemExit as e:\n    rc = e.code\n"
+            "import bcp_ctypes\n"
+            "print('RC', rc, 'TORCH', 'torch' in sys.modules, 'LIB', bcp_ctypes._lib is not None)\n")
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=env, capture_output=True, text=True, timeout=100)
+    assert "RC 4 TORCH False LIB False" in r.stdout, (r.stdout, r.stderr[-2000:])

@@ -39,7 +39,7 @@ def _run(cmd, timeout):
 @pytest.mark.parametrize("mode", ["gen", "rebuild", "mixed"])
 def test_bench_one_rank_small(bcp, mode):
     line = _run([sys.executable, "bench.py", "--stripes", "64", "--steps", "2", "--warmup", "1", "--no-cpu",
-                 "--mode", mode], 300)
+                 "--no-e2e", "--mode", mode], 300)
     assert line["config"]["verified_on_device"] is True
     assert line["n_gpus"] == 1 and line["config"]["ranks"] == 1 and line["config"]["shared_gpu"] is False
     assert line["roofline"]["frac"] == line["roofline"]["frac_event"] > 0
@@ -51,7 +51,7 @@ def test_bench_torchrun_two_ranks_labels(bcp):
     line = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                  "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
                  "bench.py", "--gpus", "2", "--stripes", "64", "--steps", "2", "--warmup", "1", "--no-cpu",
-                 "--allow-shared"], 420)
+                 "--no-e2e", "--allow-shared"], 420)
     assert line["config"]["verified_on_device"] is True
     assert line["config"]["ranks"] == 2
     distinct = min(ndev, 2)  # bench maps local rank r to device r % ndev
@@ -70,7 +70,7 @@ def test_bench_gpus_n_launches_its_own_ranks(bcp, n):
     env = dict(os.environ, MASTER_ADDR="127.0.0.1")
     env.pop("WORLD_SIZE", None)
     args = [sys.executable, "bench.py", "--gpus", str(n), "--stripes", "64", "--steps", "2", "--warmup", "1",
-            "--no-cpu"]
+            "--cpu-seconds", "1", "--cpu-stripes", "16", "--e2e-gib", "0.25", "--e2e-reps", "1"]
     if ndev < n:
         r = subprocess.run(args, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
         assert r.returncode == 4, (r.returncode, r.stdout[-2000:], r.stderr[-2000:])
@@ -85,6 +85,29 @@ def test_bench_gpus_n_launches_its_own_ranks(bcp, n):
     assert line["config"]["verified_on_device"] is True
     per = line["config"]["per_rank"]  # each GPU's own rate in the N-GPU line
     assert [r["rank"] for r in per] == list(range(n)) and all(r["verified"] and r["GiBps"] > 0 for r in per)
+    # the N-GPU line is complete: per-rank rates, the reference CPU path timed
+    # in the same run, and the end-to-end figure at every N
+    assert line["per_rank"] == per
+    cpu = line["cpu_baseline"]
+    assert cpu["kind"] == "reference" and cpu["value"] > 0 and cpu["cores"] >= 1
+    assert cpu["legs"][0]["threads"] == 1 and "quota_cpus" in cpu
+    e2e = line["e2e"]
+    assert e2e["ranks"] == n and len(e2e["per_rank"]) == n
+    assert e2e["gen"]["verified"] is True and e2e["rebuild"]["verified"] is True
+    assert e2e["gen"]["GiBps"] > 0 and e2e["rebuild"]["GiBps"] > 0
+    assert e2e["gen"]["bytes_read"] == sum(r["bytes_read"] for r in e2e["per_rank"])
     assert line["config"]["bytes_per_step_per_gpu"] * n * line["steps"] / 2**30 / (line["ms_per_step"] *
                                                                                    line["steps"] * 1e-3) == \
         pytest.approx(line["value"], rel=5e-3)  # value = the whole job's bytes / the slowest rank's time
+
+
+@pytest.mark.timeout(400)
+def test_bench_mixed_line_carries_cpu_baseline_and_e2e(bcp):
+    """Mixed mode (config-5 shapes): the reference's fold timed over the same
+    zero-padded stripe shapes, and the end-to-end leg, in the one-rank line."""
+    line = _run([sys.executable, "bench.py", "--mode", "mixed", "--stripes", "64", "--steps", "2", "--warmup", "1",
+                 "--cpu-seconds", "1", "--e2e-gib", "0.25", "--e2e-reps", "1"], 300)
+    cpu = line["cpu_baseline"]
+    assert cpu["kind"] == "reference" and cpu["value"] > 0 and "stripe_shapes" in cpu["legs"][0]
+    assert line["e2e"]["gen"]["verified"] is True and line["e2e"]["rebuild"]["verified"] is True
+    assert line["per_rank"][0]["verified"] is True

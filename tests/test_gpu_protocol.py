@@ -185,7 +185,7 @@ def test_pipeline_refuses_paths_outside_the_store(bcp, oracle, tmp_path):
             f.write(b"z" * 100)
     items = [("../outside/x", 2**40, S.with_p(0b11, 2))] + items
     st = bcp.pipeline_gen(root, 4, items)
-    assert st.errors == 0 and st.tasks == 1
+    assert st.errors == 0 and st.tasks == 1 and st.refused == 1
     assert S.read_file(S.parity_path(root, 2, "ok")) == oracle.gen_parity_file(contents["ok"])
     assert not os.path.exists(os.path.join(root, "st2", "outside"))
     os.remove(S.chunk_path(root, 1, "ok"))
@@ -194,7 +194,7 @@ def test_pipeline_refuses_paths_outside_the_store(bcp, oracle, tmp_path):
         st = pl.rebuild(root, 4, 1, items)
     finally:
         pl.close()
-    assert st.errors == 0 and st.tasks == 1
+    assert st.errors == 0 and st.tasks == 1 and st.refused == 1
     assert S.read_file(S.chunk_path(root, 1, "ok")) == contents["ok"][1].tobytes()
     assert S.read_file(os.path.join(root, "st1", "outside", "x")) == b"z" * 100
 
@@ -421,7 +421,7 @@ def test_rank_pool_on_device(tmp_path, mode):
     assert r.returncode == 0 and "pool ok" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]
 
 
-@pytest.mark.parametrize("engine_kind", ["protocol", "pipeline", "procs", "procs_batched"])
+@pytest.mark.parametrize("engine_kind", ["default", "protocol", "pipeline", "procs", "procs_batched"])
 def test_cli_complete_partial_rebuild(bcp, oracle, tmp_path, engine_kind):
     """bin/bcp end to end on the device: --complete (scan of every target),
     --partial from changelog record files, then parity-rebuild from the DB --
@@ -444,10 +444,13 @@ def test_cli_complete_partial_rebuild(bcp, oracle, tmp_path, engine_kind):
             S.write_chunk(root, h, path, d)
             arrs.append(d)
         files[path], contents[path] = holders, arrs
-    flags = {"protocol": [], "pipeline": ["--pipeline"], "procs": ["--procs"],
+    flags = {"default": [], "protocol": ["--protocol"], "pipeline": ["--pipeline"], "procs": ["--procs"],
              "procs_batched": ["--procs", "--fold", "batched"]}[engine_kind]
     r = subprocess.run([bcp.BIN_PATH, "parity-gen", "--complete", *flags, root, str(nt)], capture_output=True)
     assert r.returncode == 0, r.stderr
+    engine_named = {"default": b"(pipeline)", "pipeline": b"(pipeline)", "protocol": b"(protocol)"}.get(
+        engine_kind, b"(rank processes)")
+    assert engine_named in r.stdout, r.stdout  # the batched pipeline is the default engine
     db = bcp.PDB(os.path.join(root, "st0", "db"))
     placed = {k.decode(): loc for k, _, loc in db.items()}
     db.close()

@@ -483,6 +483,55 @@ def test_reused_tile_records_follow_data_and_table_changes(oracle, engine, dev, 
         engine.option("desc_reuse_records", prev)
 
 
+def test_reused_tile_records_never_follow_a_uniform_batch_on_the_slot(oracle, engine, dev, queue):
+    """desc_reuse_records with device-resident tables: a uniform batch that
+    took the same ring slot in between (it uploads its own tables over the
+    slot's) must make the descriptor batch stage and cut its tables afresh,
+    even though the descriptor tables are byte-identical to that slot's last
+    descriptor batch (stale tables reused)."""
+    rng = np.random.default_rng(515)
+    chunks_all = [[rng.integers(0, 256, size=int(x), dtype=np.uint8)
+                   for x in rng.integers(70_000, 300_000, size=6)] for _ in range(24)]
+    descs, sources, outs = [], [], []
+    for chunks in chunks_all:
+        first = len(sources)
+        for c in chunks:
+            sources.append((dev.put(c), len(c)))
+        m = max(len(c) for c in chunks)
+        dptr = dev.alloc(m + 32)
+        outs.append((dptr, m))
+        descs.append((dptr, m, first, len(chunks), 0))
+    # a uniform batch of 64 stripes x 8 x 64 KiB (pointer tables > table_host_max: uploaded)
+    C, NS, NU = 64 * KiB, 8, 64
+    ubuf = rng.integers(0, 256, size=NU * NS * C, dtype=np.uint8)
+    usrc = dev.put(ubuf)
+    uout = dev.alloc(NU * C)
+    ustripes = [(uout + s * C, C, s * NS, NS, 0) for s in range(NU)]
+    usources = [(usrc + (s * NS + k) * C, C) for s in range(NU) for k in range(NS)]
+    keys = ("desc_reuse_records", "desc_table_host_max")
+    prev = [engine.option(k) for k in keys]
+    engine.option("desc_reuse_records", 1)
+    engine.option("desc_table_host_max", 0)  # descriptor tables read from the slot's device copy
+    try:
+        for rnd in range(3):
+            for o, n in outs:
+                queue.memset(o, 0xA5, n)
+            queue.xor_stripes(descs, sources)  # slot s (rnd > 0: the same tables as last time on s)
+            queue.sync()
+            for i, (o, n) in enumerate(outs):
+                assert np.array_equal(dev.get(o, n), oracle.xor_padded_np(chunks_all[i])), (rnd, i)
+            for _ in range(7):  # slots s+1 .. s+3, s (overwritten), s+1 .. s+3
+                queue.xor_stripes(ustripes, usources)
+            queue.sync()
+            got = dev.get(uout, NU * C)
+            for s_ in (0, NU - 1):
+                ref = np.bitwise_xor.reduce(ubuf[s_ * NS * C:(s_ + 1) * NS * C].reshape(NS, C), axis=0)
+                assert np.array_equal(got[s_ * C:(s_ + 1) * C], ref), (rnd, s_)
+    finally:
+        for k, v in zip(keys, prev):
+            engine.option(k, v)
+
+
 @pytest.mark.parametrize("n", [9, 12, 20, 56])
 def test_descriptor_wide_stripes(oracle, dev, queue, n):
     """Stripes wider than a tile record holds (> 8 sources reaching into a

@@ -192,12 +192,33 @@ def test_paths_outside_the_store_are_refused_by_every_rank(bcp, oracle, cpu_hook
     items = [(bad, 2**40, S.with_p(0b11, 2))] + items
     st = bcp.gen_run(root, 4, items, nlanes=1)
     assert st.errors == 0 and st.tasks == 3  # "ok" only: P 2 and sources 0, 1
+    assert st.refused == 1  # reported to the caller, not only logged
     assert parity_of(root, 2, "ok") == oracle.gen_parity_file(contents["ok"])
     assert not os.path.exists(os.path.join(root, "st2", "outside"))
     os.remove(S.chunk_path(root, 1, "ok"))
     st = bcp.rebuild_run(root, 4, 1, items)
     assert st.errors == 0 and S.read_file(S.chunk_path(root, 1, "ok")) == contents["ok"][1].tobytes()
+    assert st.refused == 1
     assert S.read_file(os.path.join(root, "st1", "outside", "x")) == b"z" * 100
+
+
+def test_refused_paths_get_no_db_entry(bcp, oracle, cpu_hook, tmp_path):
+    """With the persistent state (process_list's pdb_set, gen/main.c:146-149):
+    a refused item got no parity, so no replica may record it as protected
+    (a later rebuild would refuse it too and the chunk would be lost
+    silently); the caller sees it in stats.refused."""
+    root = str(tmp_path)
+    items, contents = S.populate(root, 4, [("ok", [0, 1], 2, [5000, 7000])])
+    items = [("../outside/x", 2**40, S.with_p(0b11, 2)), ("/abs/y", 2**40, S.with_p(0b101, 1))] + items
+    st = bcp.gen_run_db(root, 4, items, nlanes=2)
+    assert st.errors == 0 and st.refused == 2
+    for k in range(4):
+        db = bcp.PDB(os.path.join(root, f"st{k}", "db"))
+        try:
+            assert len(db) == 1 and db.get("ok") is not None
+            assert db.get("../outside/x") is None and db.get("/abs/y") is None
+        finally:
+            db.close()
 
 
 def test_unreadable_parity_root_is_an_error(bcp, tmp_path):
