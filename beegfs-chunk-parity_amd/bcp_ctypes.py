@@ -174,6 +174,11 @@ _SIGS = {
     "bcp_store_weight": ([ctypes.c_int], ctypes.c_int),
     "bcp_plan_worklist": ([_V, ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(WorkItem), ctypes.c_size_t,
                            ctypes.POINTER(WorkItem), ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
+    "bcp_plan_rounds": ([_V, ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(WorkItem), ctypes.c_size_t,
+                         ctypes.POINTER(WorkItem), ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t),
+                         ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
+    "bcp_assign_lanes_rounds": ([ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(FileInfo),
+                                 ctypes.POINTER(ctypes.c_int)], None),
     "bcp_lb_finalize": ([], ctypes.c_int),
     "bcp_pdb_open": ([ctypes.c_char_p, ctypes.c_uint64, ctypes.POINTER(_V)], ctypes.c_int),
     "bcp_pdb_close": ([_V], ctypes.c_int),
@@ -439,6 +444,16 @@ def _items(items):
         arr[i].fi.timestamp = ts
         arr[i].fi.locations = loc
     return arr, keep
+
+
+def assign_lanes_rounds(nlanes: int, round_start, locations) -> list:
+    """bcp_assign_lanes_rounds: assign_lanes over each round separately."""
+    n = len(locations)
+    fis = (FileInfo * max(n, 1))(*[FileInfo(0, x) for x in locations])
+    out = (ctypes.c_int * max(n, 1))()
+    rs = (ctypes.c_size_t * len(round_start))(*round_start)
+    lib().bcp_assign_lanes_rounds(nlanes, len(round_start) - 1, rs, fis, out)
+    return list(out)[:n]
 
 
 def assign_lanes(nlanes: int, locations) -> list:
@@ -845,15 +860,22 @@ class EventSet:
 
     def plan(self, ntargets: int, cum_weight, prev=()):
         """prev: iterable of (path, timestamp, locations); returns [(path, timestamp, locations)]."""
+        return self.plan_rounds(ntargets, cum_weight, prev)[0]
+
+    def plan_rounds(self, ntargets: int, cum_weight, prev=()):
+        """bcp_plan_rounds: (worklist, round_start) -- the coordinators' rounds
+        back to back, round k = worklist[round_start[k]:round_start[k+1]]."""
         prev = sorted(prev, key=lambda x: x[0].encode())
         parr, keep = _items(prev)
         cw = (ctypes.c_int * ntargets)(*cum_weight)
         n = ctypes.c_size_t(0)
         call("bcp_plan_worklist", self.h, ntargets, cw, parr, len(prev), None, 0, ctypes.byref(n))
         out = (WorkItem * max(n.value, 1))()
-        call("bcp_plan_worklist", self.h, ntargets, cw, parr, len(prev), out, n.value, ctypes.byref(n))
+        rs = (ctypes.c_size_t * (ntargets + 1))()
+        call("bcp_plan_rounds", self.h, ntargets, cw, parr, len(prev), out, n.value, ctypes.byref(n), rs)
         del keep
-        return [(out[i].path.decode(), out[i].fi.timestamp, out[i].fi.locations) for i in range(n.value)]
+        return ([(out[i].path.decode(), out[i].fi.timestamp, out[i].fi.locations) for i in range(n.value)],
+                list(rs))
 
     def close(self):
         if self.h:

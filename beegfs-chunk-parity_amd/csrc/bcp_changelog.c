@@ -431,8 +431,20 @@ static int cmp_size(const void *a, const void *b)
     return 1;
 }
 
-int bcp_plan_worklist(const bcp_eventset *s, int ntargets, const int *cum_weight, const bcp_work_item *prev,
-                      size_t nprev, bcp_work_item *out, size_t out_cap, size_t *nout)
+/*
+ * Phase 2's worklist as the reference's coordinators produce it.  Phase 1
+ * sends every path to eater simple_hash(path) % ntargets (gen/main.c:310);
+ * each eater keeps its paths in arrival order, shuffles them with the
+ * fixed-seed PCG32 and sorts them by total size (:710-711); then the eaters
+ * broadcast their lists one round at a time, in rank order (:758-797), and
+ * every round is planned item by item against the DB (:772-788) and given
+ * its own lanes (:823).  Here eater k = storage target k and arrival order =
+ * the event set's first-seen order (targets fed 0, 1, ...: the reference's
+ * interleaving of several feeders is not deterministic).  round_start[k] is
+ * where round k begins in out; round_start[ntargets] = *nout.
+ */
+int bcp_plan_rounds(const bcp_eventset *s, int ntargets, const int *cum_weight, const bcp_work_item *prev,
+                    size_t nprev, bcp_work_item *out, size_t out_cap, size_t *nout, size_t *round_start)
 {
     if (!s || ntargets < 1 || ntargets > MAX_STORAGE_TARGETS || !cum_weight || (nprev && !prev) || !nout)
         return -EINVAL;
@@ -445,39 +457,64 @@ int bcp_plan_worklist(const bcp_eventset *s, int ntargets, const int *cum_weight
     if (out_cap < s->n)
         return out ? -ENOSPC : 0;
     size_index *order = malloc((s->n ? s->n : 1) * sizeof(size_index));
-    if (!order)
+    uint32_t *eater = malloc((s->n ? s->n : 1) * sizeof(uint32_t));
+    if (!order || !eater) {
+        free(order);
+        free(eater);
         return -ENOMEM;
+    }
     for (size_t i = 0; i < s->n; i++)
-        order[i] = (size_index){s->e[i].size, i};
-    /* shuffle (gen/main.c:373-386, fixed seed) then sort by total size */
-    if (s->n > 1) {
-        pcg32 rng = {0x853c49e6748fea9bULL, 0xda3e39cb94b95bdbULL};
-        for (size_t i = s->n - 1; i > 0; i--) {
-            size_t j = pcg32_next(&rng) % (i + 1);
-            size_index t = order[j];
-            order[j] = order[i];
-            order[i] = t;
+        eater[i] = bcp_path_hash(s->e[i].path, strlen(s->e[i].path)) % (uint32_t)ntargets;
+    size_t j = 0;
+    for (int k = 0; k < ntargets; k++) {
+        if (round_start)
+            round_start[k] = j;
+        size_t m = 0;
+        size_index *mine = order + j;
+        for (size_t i = 0; i < s->n; i++)
+            if (eater[i] == (uint32_t)k)
+                mine[m++] = (size_index){s->e[i].size, i};
+        /* shuffle (gen/main.c:373-386, a fresh fixed-seed generator per
+         * eater) then sort by total size */
+        if (m > 1) {
+            pcg32 rng = {0x853c49e6748fea9bULL, 0xda3e39cb94b95bdbULL};
+            for (size_t i = m - 1; i > 0; i--) {
+                size_t r = pcg32_next(&rng) % (i + 1);
+                size_index t = mine[r];
+                mine[r] = mine[i];
+                mine[i] = t;
+            }
+        }
+        /* The reference sorts with the C library's qsort (gen/main.c:711),
+         * whose order of equal sizes is the library's: glibc <= 2.36
+         * merge-sorts (stable), later versions do not.  Calling the same qsort
+         * with the same comparator on the same shuffled array gives the
+         * reference's order on any libc. */
+        qsort(mine, m, sizeof(size_index), cmp_size);
+        for (size_t t = 0; t < m; t++, j++) {
+            const ev_entry *e = &s->e[mine[t].idx];
+            FileInfo fi = {e->timestamp, WITH_P(e->modified, NO_P)};
+            const bcp_work_item *old = find_prev(prev, nprev, e->path);
+            if (old)
+                fill_in_missing(&fi, &old->fi);
+            fi.locations &= ~e->deleted;
+            if (P_IS_INVALID(fi.locations))
+                select_p(e->path, &fi, ntargets, cum_weight);
+            if (old && old->fi.timestamp == fi.timestamp && old->fi.locations == fi.locations)
+                fi.locations = WITH_P(fi.locations, NO_P);
+            out[j].path = e->path; /* owned by the event set */
+            out[j].fi = fi;
         }
     }
-    /* The reference sorts with the C library's qsort (gen/main.c:711), whose
-     * order of equal sizes is the library's: glibc <= 2.36 merge-sorts (stable),
-     * later versions do not.  Calling the same qsort with the same comparator
-     * on the same shuffled array gives the reference's order on any libc. */
-    qsort(order, s->n, sizeof(size_index), cmp_size);
-    for (size_t j = 0; j < s->n; j++) {
-        const ev_entry *e = &s->e[order[j].idx];
-        FileInfo fi = {e->timestamp, WITH_P(e->modified, NO_P)};
-        const bcp_work_item *old = find_prev(prev, nprev, e->path);
-        if (old)
-            fill_in_missing(&fi, &old->fi);
-        fi.locations &= ~e->deleted;
-        if (P_IS_INVALID(fi.locations))
-            select_p(e->path, &fi, ntargets, cum_weight);
-        if (old && old->fi.timestamp == fi.timestamp && old->fi.locations == fi.locations)
-            fi.locations = WITH_P(fi.locations, NO_P);
-        out[j].path = e->path; /* owned by the event set */
-        out[j].fi = fi;
-    }
+    if (round_start)
+        round_start[ntargets] = j;
     free(order);
+    free(eater);
     return 0;
+}
+
+int bcp_plan_worklist(const bcp_eventset *s, int ntargets, const int *cum_weight, const bcp_work_item *prev,
+                      size_t nprev, bcp_work_item *out, size_t out_cap, size_t *nout)
+{
+    return bcp_plan_rounds(s, ntargets, cum_weight, prev, nprev, out, out_cap, nout, NULL);
 }

@@ -88,6 +88,13 @@ void bcp_assign_lanes(int nlanes, uint64_t njobs, const FileInfo *jobs, int *lan
     free(prev);
 }
 
+void bcp_assign_lanes_rounds(int nlanes, int nrounds, const size_t *round_start, const FileInfo *jobs, int *lane)
+{
+    for (int r = 0; r < nrounds; r++)
+        bcp_assign_lanes(nlanes, (uint64_t)(round_start[r + 1] - round_start[r]), jobs + round_start[r],
+                         lane + round_start[r]);
+}
+
 double bcpr_now_s(void)
 {
     struct timespec t;
@@ -657,20 +664,36 @@ static int round_impl(bcp_pipeline *pl, int procs, const char *store_root, int n
     bcp_pdb_close(db);
     if (rc)
         return rc;
-    size_t n = 0;
+    size_t n = 0, round_start[MAX_STORAGE_TARGETS + 1];
     bcp_work_item *work = NULL;
+    int *lanes = NULL;
     rc = bcp_plan_worklist(events, ntargets, cw, prev, nprev, NULL, 0, &n);
     if (!rc) {
         work = malloc((n ? n : 1) * sizeof(bcp_work_item));
-        rc = work ? bcp_plan_worklist(events, ntargets, cw, prev, nprev, work, n, &n) : -ENOMEM;
+        rc = work ? bcp_plan_rounds(events, ntargets, cw, prev, nprev, work, n, &n, round_start) : -ENOMEM;
+    }
+    if (!rc && !pl) {
+        /* lanes per coordinator round (gen/main.c:823); the lanes walk the
+         * rounds back to back (the reference barriers between rounds, :789;
+         * every rank walks the same list, so the messages match either way) */
+        FileInfo *fis = malloc((n ? n : 1) * sizeof(FileInfo));
+        lanes = malloc((n ? n : 1) * sizeof(int));
+        if (!fis || !lanes) {
+            rc = -ENOMEM;
+        } else {
+            for (size_t i = 0; i < n; i++)
+                fis[i] = work[i].fi;
+            bcp_assign_lanes_rounds(nlanes, ntargets, round_start, fis, lanes);
+        }
+        free(fis);
     }
     if (!rc && !pl && !procs)
-        rc = bcp_gen_run_db(store_root, ntargets, work, n, nlanes, NULL, log, stats);
+        rc = bcp_gen_run_db(store_root, ntargets, work, n, nlanes, lanes, log, stats);
     if (!rc && (pl || procs)) {
         bcp_run_stats st;
         memset(&st, 0, sizeof(st));
         rc = pl ? bcp_pipeline_run(pl, store_root, ntargets, work, n, log, &st)
-                : bcp_gen_run_procs(store_root, ntargets, work, n, nlanes, NULL, log, &st);
+                : bcp_gen_run_procs(store_root, ntargets, work, n, nlanes, lanes, log, &st);
         if (!rc && st.errors == 0)
             rc = update_replicas(store_root, ntargets, work, n); /* only after the parity is on disk */
         if (stats)
@@ -678,6 +701,7 @@ static int round_impl(bcp_pipeline *pl, int procs, const char *store_root, int n
     }
     if (nplanned)
         *nplanned = n;
+    free(lanes);
     free(work);
     bcp_pdb_items_free(prev);
     return rc;

@@ -424,13 +424,25 @@ int bcp_eventset_get(const bcp_eventset *s, size_t i, const char **path, int64_t
 uint32_t bcp_path_hash(const char *p, size_t len);
 /* get_store_weight of gen/main.c:403-427 for a store directory fd. */
 int bcp_store_weight(int dirfd);
-/* The worklist of one gen round (gen/main.c:703-715, 768-791): events in
- * shuffled-then-size order; each merged with the previous state `prev`
- * (sorted by path), deleted holders dropped, P chosen by select_P with the
- * cumulative weights cum_weight[0..ntargets-1], NO_P when unchanged.
- * out[i].path points into the event set.  *nout = number of events. */
+/* The worklist of one gen run, in the reference's per-coordinator rounds:
+ * path -> eater simple_hash(path) % ntargets (gen/main.c:310); per eater,
+ * arrival (= the event set's first-seen) order shuffled with the fixed-seed
+ * PCG32 then sorted by total size (:710-711); the eaters' lists one round
+ * after another in target order (:758-797).  Each item merged with the
+ * previous state `prev` (sorted by path), deleted holders dropped, P chosen
+ * by select_P with the cumulative weights cum_weight[0..ntargets-1], NO_P
+ * when unchanged (:772-788).  out[i].path points into the event set.
+ * *nout = number of events; round_start (NULL or ntargets + 1 entries):
+ * round k is out[round_start[k] .. round_start[k+1]) -- lanes are assigned
+ * per round (:823). */
+int bcp_plan_rounds(const bcp_eventset *s, int ntargets, const int *cum_weight, const bcp_work_item *prev,
+                    size_t nprev, bcp_work_item *out, size_t out_cap, size_t *nout, size_t *round_start);
+/* The same without the round boundaries. */
 int bcp_plan_worklist(const bcp_eventset *s, int ntargets, const int *cum_weight, const bcp_work_item *prev,
                       size_t nprev, bcp_work_item *out, size_t out_cap, size_t *nout);
+/* bcp_assign_lanes over each round separately (gen/main.c:823): lane[i] for
+ * the whole list; round_start as bcp_plan_rounds fills it. */
+void bcp_assign_lanes_rounds(int nlanes, int nrounds, const size_t *round_start, const FileInfo *jobs, int *lane);
 
 /* bp-find-all-chunks (src/bp-find-all-chunks/main.c:17-45): one 'm' record
  * per regular file under chunks_dir, path relative to it, written to out_fd

@@ -6,7 +6,8 @@ bcp_eventset_* / bcp_plan_worklist.
   aggregation       gen/file_info_hash.c:24-31 (fih_add_info), gen/main.c:688
   simple_hash       gen/main.c:67-74
   PCG32             gen/main.c:338-372 (pcg-random.org minimal C)
-  shuffle + sort    gen/main.c:373-386, 703-715
+  shuffle + sort    gen/main.c:373-386, 703-715, per eater
+  rounds            gen/main.c:310 (eater = simple_hash % ntargets), 758-797
   worklist item     gen/main.c:768-791 (fill_in_missing_fields :92-100,
                     select_P :388-401)
 
@@ -131,16 +132,31 @@ def fill_in_missing(dst: int, src: int) -> int:
     return with_p(loc, old_p) if not test_bit(loc, old_p) else with_p(loc, NO_P)
 
 
-def plan(agg, ntargets: int, cum_weight, prev: dict):
-    """-> list of (path bytes, timestamp, locations) in worklist order."""
+def round_order(entries, ntargets: int):
+    """-> (entry indices in worklist order, round_start): eater k gets the
+    paths with simple_hash % ntargets == k in arrival order (gen/main.c:310),
+    shuffles them with a fresh fixed-seed PCG32 and sorts them by total size
+    (:710-711); the eaters' lists follow each other in target order (:758)."""
+    order, starts = [], []
+    for k in range(ntargets):
+        starts.append(len(order))
+        mine = [i for i, (path, _) in enumerate(entries) if simple_hash(path) % ntargets == k]
+        if len(mine) > 1:
+            rng = PCG32(0x853C49E6748FEA9B, 0xDA3E39CB94B95BDB)
+            for i in range(len(mine) - 1, 0, -1):
+                j = rng.next() % (i + 1)
+                mine[i], mine[j] = mine[j], mine[i]
+        mine.sort(key=lambda i: entries[i][1][3])      # stable
+        order += mine
+    starts.append(len(order))
+    return order, starts
+
+
+def plan(agg, ntargets: int, cum_weight, prev: dict, rounds: bool = False):
+    """-> list of (path bytes, timestamp, locations) in worklist order
+    (rounds=True: and the round starts)."""
     entries = list(agg.items())
-    order = list(range(len(entries)))
-    if len(order) > 1:
-        rng = PCG32(0x853C49E6748FEA9B, 0xDA3E39CB94B95BDB)
-        for i in range(len(order) - 1, 0, -1):
-            j = rng.next() % (i + 1)
-            order[i], order[j] = order[j], order[i]
-    order.sort(key=lambda i: entries[i][1][3])      # stable
+    order, starts = round_order(entries, ntargets)
     out = []
     for i in order:
         path, (ts, mod, dele, size) = entries[i]
@@ -154,4 +170,4 @@ def plan(agg, ntargets: int, cum_weight, prev: dict):
         if old is not None and old[0] == ts and old[1] == loc:
             loc = with_p(loc, NO_P)
         out.append((path, ts, loc))
-    return out
+    return (out, starts) if rounds else out

@@ -102,6 +102,35 @@ void ref_sort_order(const uint64_t *sizes, size_t n, uint64_t *idx)
     free(a);
 }
 
+/* gen/main.c:310 + 710-711 + 758: the coordinators' rounds.  paths[i]
+ * (NUL-terminated, arrival order) goes to eater simple_hash % ntargets
+ * (:310); each eater shuffles and qsorts its own SizeIndex array (:710-711);
+ * the eaters broadcast one after another in rank order (:758), eater k =
+ * storage target k here.  idx[] gets the indices in worklist order,
+ * round_start[0..ntargets] the rounds' bounds. */
+void ref_round_order(const char *const *paths, const uint64_t *sizes, size_t n, unsigned ntargets, uint64_t *idx,
+                     size_t *round_start)
+{
+    SizeIndex *a = malloc((n ? n : 1) * sizeof(SizeIndex));
+    size_t j = 0;
+    for (unsigned k = 0; k < ntargets; k++) {
+        round_start[k] = j;
+        size_t m = 0;
+        for (size_t i = 0; i < n; i++)
+            if (simple_hash(paths[i], (int)strlen(paths[i])) % ntargets == k) {
+                a[m].size = sizes[i];
+                a[m].idx = i;
+                m++;
+            }
+        shuffle(a, m);
+        qsort(a, m, sizeof(SizeIndex), cmp_entries);
+        for (size_t t = 0; t < m; t++)
+            idx[j++] = a[t].idx;
+    }
+    round_start[ntargets] = j;
+    free(a);
+}
+
 /* gen/main.c:772-788, one worklist item: the new FileInfo, merged with the
  * previous DB value when there is one (pdb_get), deleted holders dropped, P
  * chosen when invalid, NO_P when unchanged.  UINT64_MAX where select_P would

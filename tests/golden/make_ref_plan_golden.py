@@ -18,7 +18,10 @@ are data: inputs and the reference's outputs -- no reference text.
   "plan"        record streams per target (records name paths by index into
                 "paths") + previous DB state + weights ->
                 the whole worklist: order, timestamps, locations with P / NO_P
-                (gen/main.c:688 aggregation, :710-711 order, :772-788 items)
+                (gen/main.c:688 aggregation, :310 eater = simple_hash %
+                ntargets, :710-711 order per eater, :758-797 the eaters'
+                rounds in target order, :772-788 items), the rounds' bounds
+                and the 12 lanes of every round (:823)
 
     make -C oracle ref && python tests/golden/make_ref_plan_golden.py
 """
@@ -93,11 +96,23 @@ def r_aggregate(L, streams):
     return agg
 
 
-def r_plan(L, streams, ntargets, cum, prev):
-    """The worklist of one gen round: list of (path, timestamp, locations)."""
+def r_rounds(L, paths, sizes, ntargets):
+    """ref_round_order: (indices in worklist order, round_start)."""
+    n = len(paths)
+    enc = [p.encode() for p in paths]
+    arr = (ctypes.c_char_p * max(n, 1))(*enc)
+    idx = (ctypes.c_uint64 * max(n, 1))()
+    rs = (ctypes.c_size_t * (ntargets + 1))()
+    L.ref_round_order(arr, (ctypes.c_uint64 * max(n, 1))(*sizes), n, ntargets, idx, rs)
+    return list(idx)[:n], list(rs)
+
+
+def r_plan(L, streams, ntargets, cum, prev, rounds=False):
+    """The worklist of one gen run: list of (path, timestamp, locations), the
+    coordinators' rounds back to back (rounds=True: and the round starts)."""
     agg = r_aggregate(L, streams)
     paths = list(agg)
-    order = r_order(L, [agg[p][3] for p in paths])
+    order, starts = r_rounds(L, paths, [agg[p][3] for p in paths], ntargets)
     r_set_weights(L, cum)
     out = []
     for i in order:
@@ -107,7 +122,7 @@ def r_plan(L, streams, ntargets, cum, prev):
         loc = L.ref_plan_item(p.encode(), ts, mod, dele, 1 if old else 0,
                               old[0] if old else 0, old[1] if old else 0, ntargets)
         out.append((p, ts, loc))
-    return out
+    return (out, starts) if rounds else out
 
 
 # ---- inputs --------------------------------------------------------------------
@@ -227,13 +242,17 @@ def main():
                 free = [t for t in range(nt) if not held >> t & 1]
                 p_old = free[int(rng.integers(0, len(free)))] if free else None
             prev[p] = [ts if rng.random() < 0.6 else ts - 1, with_p(held, NO_P if p_old is None else p_old)]
-        plan = r_plan(L, expand, nt, cum, prev)
+        plan, starts = r_plan(L, expand, nt, cum, prev, rounds=True)
         if any(loc == (1 << 64) - 1 for _, _, loc in plan):
             continue
+        lanes12 = []
+        for k in range(nt):
+            lanes12 += r_lanes(L, 12, [loc for _, _, loc in plan[starts[k]:starts[k + 1]]])
         pidx = {p: i for i, p in enumerate(paths)}
         plans.append({"ntargets": nt, "cum_weight": cum, "paths": paths, "streams": streams,
                       "prev": [[pidx[p], ts, loc] for p, (ts, loc) in sorted(prev.items())],
-                      "worklist": [[pidx[p], ts, loc] for p, ts, loc in plan]})
+                      "worklist": [[pidx[p], ts, loc] for p, ts, loc in plan],
+                      "round_start": starts, "lanes12": lanes12})
     doc["plan"] = plans
 
     out = os.path.join(HERE, "ref_plan.json")

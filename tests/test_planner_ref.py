@@ -44,7 +44,7 @@ def _plan_product(bcp, case):
             if recs:
                 es.feed(st, bcp.pack_records([(ts, size, ev, paths[pi]) for ts, size, ev, pi in recs]))
         prev = [(paths[pi], ts, loc) for pi, ts, loc in case["prev"]]
-        return es.plan(case["ntargets"], case["cum_weight"], prev)
+        return es.plan_rounds(case["ntargets"], case["cum_weight"], prev)
     finally:
         es.close()
 
@@ -98,19 +98,20 @@ def test_fill_in_missing_fixtures():
 
 def test_worklist_order_fixtures(bcp):
     """shuffle (fixed seed) then qsort by total size, many equal sizes: the
-    order of ties is exactly the reference's."""
+    order of ties is exactly the reference's (one target: one eater, one
+    round holding every path)."""
     for sizes, order in DOC["order"]:
         es = bcp.EventSet()
         try:
             recs = [(1, s, "m", f"p{i}") for i, s in enumerate(sizes)]
             if recs:
                 es.feed(0, bcp.pack_records(recs))
-            got = [int(p[1:]) for p, _, _ in es.plan(2, [1, 2])]
+            got = [int(p[1:]) for p, _, _ in es.plan(1, [1])]
         finally:
             es.close()
         assert got == order, len(sizes)
         agg = {f"p{i}".encode(): [1, 1, 0, s] for i, s in enumerate(sizes)}
-        assert [int(p[1:]) for p, _, _ in PL.plan(agg, 2, [1, 2], {})] == order
+        assert [int(p[1:]) for p, _, _ in PL.plan(agg, 1, [1], {})] == order
 
 
 def test_assign_lanes_fixtures(bcp):
@@ -119,22 +120,28 @@ def test_assign_lanes_fixtures(bcp):
 
 
 def test_whole_worklist_fixtures(bcp):
-    """Record streams -> aggregation -> order -> merge with the previous DB
-    state -> P or NO_P: the whole phase-2 worklist, item for item."""
-    nitems = nnop = 0
+    """Record streams -> aggregation -> eaters (simple_hash % ntargets) ->
+    order per eater -> the coordinators' rounds -> merge with the previous DB
+    state -> P or NO_P: the whole phase-2 worklist item for item, the rounds'
+    bounds and the 12 lanes of every round."""
+    nitems = nnop = nrounds = 0
     for case in DOC["plan"]:
         paths = case["paths"]
         want = [(paths[pi], ts, loc) for pi, ts, loc in case["worklist"]]
-        assert _plan_product(bcp, case) == want
+        got, starts = _plan_product(bcp, case)
+        assert got == want and starts == case["round_start"]
+        assert bcp.assign_lanes_rounds(12, starts, [loc for _, _, loc in got]) == case["lanes12"]
+        nrounds += sum(1 for a, b in zip(starts, starts[1:]) if b > a)
         packed = [(st, bcp.pack_records([(ts, size, ev, paths[pi]) for ts, size, ev, pi in recs]))
                   for st, recs in case["streams"]]
         agg = PL.aggregate(packed)
         prev = {paths[pi].encode(): (ts, loc) for pi, ts, loc in case["prev"]}
-        assert PL.plan(agg, case["ntargets"], case["cum_weight"], prev) == \
-            [(p.encode(), ts, loc) for p, ts, loc in want]
+        assert PL.plan(agg, case["ntargets"], case["cum_weight"], prev, rounds=True) == \
+            ([(p.encode(), ts, loc) for p, ts, loc in want], case["round_start"])
         nitems += len(want)
         nnop += sum(1 for _, _, loc in want if loc >> 56 == 0xFF)
     assert nitems > 3000 and nnop > 300  # unchanged items (NO_P) are covered
+    assert nrounds > 150  # non-empty rounds, 2..19 targets
 
 
 # ---- against the reference functions directly (container: oracle/_ref) ------------
@@ -166,7 +173,7 @@ def test_random_worklists_against_reference_functions(bcp, seed):
     prev = {p: [ts - int(rng.integers(0, 2)), G.with_p(m & ~d, G.NO_P if rng.random() < 0.3 else
                                                     next((t for t in range(nt) if not (m & ~d) >> t & 1), G.NO_P))]
             for p, (ts, m, d, _) in list(agg.items())[::3]}
-    want = G.r_plan(L, streams, nt, cum, prev)
+    want, starts = G.r_plan(L, streams, nt, cum, prev, rounds=True)
     if any(loc == U64 for _, _, loc in want):
         pytest.skip("select_P would not terminate for this draw")
     es = bcp.EventSet()
@@ -174,13 +181,17 @@ def test_random_worklists_against_reference_functions(bcp, seed):
         for st, recs in streams:
             if recs:
                 es.feed(st, bcp.pack_records(recs))
-        got = es.plan(nt, cum, [(p, ts, loc) for p, (ts, loc) in prev.items()])
+        got, got_starts = es.plan_rounds(nt, cum, [(p, ts, loc) for p, (ts, loc) in prev.items()])
     finally:
         es.close()
-    assert got == want
+    assert got == want and got_starts == starts
     locs = [loc for _, _, loc in want]
     for nlanes in (1, 3, 12):
         assert bcp.assign_lanes(nlanes, locs) == G.r_lanes(L, nlanes, locs)
+        per_round = []
+        for k in range(nt):
+            per_round += G.r_lanes(L, nlanes, locs[starts[k]:starts[k + 1]])
+        assert bcp.assign_lanes_rounds(nlanes, starts, locs) == per_round
 
 
 def test_store_weight_against_reference_function(bcp, tmp_path):
