@@ -48,12 +48,16 @@ class RunStats(ctypes.Structure):
 class PipelineTiming(ctypes.Structure):
     _fields_ = [("stat", ctypes.c_double), ("read_wait", ctypes.c_double), ("slot_wait", ctypes.c_double),
                 ("submit", ctypes.c_double), ("drain", ctypes.c_double), ("batches", ctypes.c_uint32),
-                ("read_jobs", ctypes.c_uint32)]
+                ("read_jobs", ctypes.c_uint32), ("map", ctypes.c_double), ("mapped_bytes", ctypes.c_uint64),
+                ("map_fallbacks", ctypes.c_uint32), ("read_mode", ctypes.c_int)]
 
 
 class PipelineOpts(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int), ("slab_bytes", ctypes.c_size_t), ("io_threads", ctypes.c_int),
-                ("nslots", ctypes.c_int), ("ndevices", ctypes.c_int)]
+                ("nslots", ctypes.c_int), ("ndevices", ctypes.c_int), ("read_mode", ctypes.c_int)]
+
+
+READ_AUTO, READ_COPY, READ_MAP = 0, 1, 2
 
 
 XOR_HOOK = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t,
@@ -99,6 +103,7 @@ _SIGS = {
     "bcp_host_alloc_mapped": ([_V, ctypes.c_size_t, ctypes.POINTER(_V)], ctypes.c_int),
     "bcp_host_free": ([_V, _V], ctypes.c_int),
     "bcp_host_register": ([_V, _V, ctypes.c_size_t], ctypes.c_int),
+    "bcp_host_register_dma_src": ([_V, _V, ctypes.c_size_t], ctypes.c_int),
     "bcp_host_unregister": ([_V, _V], ctypes.c_int),
     "bcp_h2d_async": ([_V, _V, _V, ctypes.c_size_t], ctypes.c_int),
     "bcp_d2h_async": ([_V, _V, _V, ctypes.c_size_t], ctypes.c_int),
@@ -643,11 +648,11 @@ class PDB:
 
 
 def pipeline_gen(store_root: str, ntargets: int, items, device: int = 0, slab_bytes: int = 256 << 20,
-                 io_threads: int = 0, nslots: int = 4, log=None, ndevices: int = 1) -> RunStats:
+                 io_threads: int = 0, nslots: int = 4, log=None, ndevices: int = 1, read_mode: int = 0) -> RunStats:
     """Batched end-to-end parity generation (bcp_pipeline_gen)."""
     arr, keep = _items(items)
     st = RunStats()
-    opts = PipelineOpts(device, slab_bytes, io_threads, nslots, ndevices)
+    opts = PipelineOpts(device, slab_bytes, io_threads, nslots, ndevices, read_mode)
     rc = lib().bcp_pipeline_gen(store_root.encode(), ntargets, arr, len(items), ctypes.byref(opts), log,
                                 ctypes.byref(st))
     check("bcp_pipeline_gen", rc)
@@ -659,9 +664,9 @@ class Pipeline:
     """Long-lived batched pipeline (bcp_pipeline_create / run / destroy)."""
 
     def __init__(self, device: int = 0, slab_bytes: int = 256 << 20, io_threads: int = 0, nslots: int = 4,
-                 ndevices: int = 1):
+                 ndevices: int = 1, read_mode: int = 0):
         h = _V()
-        opts = PipelineOpts(device, slab_bytes, io_threads, nslots, ndevices)
+        opts = PipelineOpts(device, slab_bytes, io_threads, nslots, ndevices, read_mode)
         call("bcp_pipeline_create", ctypes.byref(opts), ctypes.byref(h))
         self.h = h
 

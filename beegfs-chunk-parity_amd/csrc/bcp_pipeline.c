@@ -39,6 +39,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/mman.h>
 #include <sys/stat.h>
 #include <sys/uio.h>
 #include <time.h>
@@ -48,8 +49,10 @@
 #include "bcp_runner.h"
 
 #define ROW 256u
+#define PAGE 4096u
 #define WINDOW ((uint64_t)BCP_WINDOW_BYTES)
 #define RUP(x) (((x) + ROW - 1) / ROW * ROW)
+#define RUP_PAGE(x) (((x) + PAGE - 1) / PAGE * PAGE)
 
 static double now_s(void)
 {
@@ -153,6 +156,7 @@ typedef struct {
     pthread_mutex_t lock;
     pthread_cond_t cv;
     long left;
+    double t_zero;        /* when the count reached zero */
 } latch;
 
 static void latch_init(latch *l, long n)
@@ -160,12 +164,15 @@ static void latch_init(latch *l, long n)
     pthread_mutex_init(&l->lock, NULL);
     pthread_cond_init(&l->cv, NULL);
     l->left = n;
+    l->t_zero = n ? 0.0 : now_s();
 }
 static void latch_down(latch *l)
 {
     pthread_mutex_lock(&l->lock);
-    if (--l->left == 0)
+    if (--l->left == 0) {
+        l->t_zero = now_s();
         pthread_cond_broadcast(&l->cv);
+    }
     pthread_mutex_unlock(&l->lock);
 }
 static void latch_wait(latch *l)
@@ -195,7 +202,9 @@ typedef struct {
     uint64_t src_off[MAX_STORAGE_TARGETS];/* file offset of the source data (parity body: 8n) */
     uint64_t max_cs;
     uint64_t out_len;                    /* gen: max_cs; rebuild: header[victim index] */
-    uint64_t in_off[MAX_STORAGE_TARGETS];/* offsets in the input slab */
+    uint64_t in_off[MAX_STORAGE_TARGETS];/* offsets in the input slab (MAP layout: of the
+                                            file's first byte, page-aligned; the data
+                                            then starts src_off further) */
     uint64_t out_off;                    /* offset in the output slab */
     int batch;
 } task;
@@ -215,6 +224,11 @@ typedef struct {
     bcp_event *ev_h, *ev_k, *ev_d;
     latch reads, writes;
     int busy;             /* writes of the previous batch pending */
+    /* MAP read mode: a reserved range of in_cap bytes the batch's mapped
+     * chunk files are placed in (PROT_NONE when idle) */
+    uint8_t *va;
+    size_t reg_lo, reg_len; /* registered part [reg_lo, reg_lo + reg_len) */
+    int mapped;
 } slot;
 
 typedef struct {
@@ -451,7 +465,7 @@ static void do_complete(job *p)
     }
 }
 
-static int slot_alloc(bcp_engine *e, slot *s, size_t in_cap, size_t out_cap)
+static int slot_alloc(bcp_engine *e, slot *s, size_t in_cap, size_t out_cap, int map_mode)
 {
     int rc;
     memset(s, 0, sizeof(*s));
@@ -462,11 +476,34 @@ static int slot_alloc(bcp_engine *e, slot *s, size_t in_cap, size_t out_cap)
         return rc;
     s->in_cap = in_cap;
     s->out_cap = out_cap;
+    if (map_mode) {
+        void *va = mmap(NULL, in_cap, PROT_NONE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
+        if (va == MAP_FAILED)
+            return -errno;
+        s->va = va;
+    }
     return 0;
+}
+
+/* MAP mode: drop the slot's batch mappings (its H2D has finished: the
+ * caller waited for the slot's writes, or synchronised the queues). */
+static void slot_unmap(bcp_engine *e, slot *s)
+{
+    if (s->reg_len)
+        bcp_host_unregister(e, s->va + s->reg_lo);
+    s->reg_len = 0;
+    if (s->mapped) /* one call replaces every file mapping of the range */
+        (void)mmap(s->va, s->in_cap, PROT_NONE, MAP_FIXED | MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
+    s->mapped = 0;
 }
 
 static void slot_free(bcp_engine *e, slot *s)
 {
+    if (s->va) {
+        slot_unmap(e, s);
+        munmap(s->va, s->in_cap);
+        s->va = NULL;
+    }
     bcp_host_free(e, s->h_in);
     bcp_host_free(e, s->h_out);
     bcp_dev_free(e, s->d_in);
@@ -488,6 +525,8 @@ typedef struct {
 
 struct bcp_pipeline {
     bcp_pipeline_opts o;
+    int map_mode;       /* read_mode resolved: 1 = MAP */
+    double map_share;   /* MAP: share of a batch's input bytes mapped (adapted per batch) */
     int ndev;
     dev_lane *dev;
     pool readers, writers, completer;
@@ -569,7 +608,7 @@ static int ensure_slots(bcp_pipeline *pl, size_t in_cap, size_t out_cap)
         if (!L->slots)
             return -ENOMEM;
         for (int s = 0; s < pl->o.nslots; s++) {
-            int rc = slot_alloc(L->eng, &L->slots[s], in_cap, out_cap);
+            int rc = slot_alloc(L->eng, &L->slots[s], in_cap, out_cap, pl->map_mode);
             if (rc)
                 return rc;
         }
@@ -584,9 +623,15 @@ int bcp_pipeline_create(const bcp_pipeline_opts *opts_in, bcp_pipeline **out)
     if (!out)
         return -EINVAL;
     *out = NULL;
-    bcp_pipeline_opts o = {0, 256u << 20, 0, 4, 1};
+    bcp_pipeline_opts o = {0, 256u << 20, 0, 4, 1, BCP_READ_AUTO};
     if (opts_in)
         o = *opts_in;
+    if (o.read_mode < BCP_READ_AUTO || o.read_mode > BCP_READ_MAP)
+        return -EINVAL;
+    if (o.read_mode == BCP_READ_AUTO) {
+        const char *env = getenv("BCP_PIPELINE_READ");
+        o.read_mode = (env && !strcmp(env, "map")) ? BCP_READ_MAP : BCP_READ_COPY;
+    }
     if (o.ndevices < 1)
         o.ndevices = 1;
     /* io threads 0 = auto: 8 readers and 8 writers per GPU.  One GPU's PCIe
@@ -613,6 +658,8 @@ int bcp_pipeline_create(const bcp_pipeline_opts *opts_in, bcp_pipeline **out)
     if (!pl)
         return -ENOMEM;
     pl->o = o;
+    pl->map_mode = o.read_mode == BCP_READ_MAP;
+    pl->map_share = 0.3;
     int rc = 0;
     pl->dev = calloc((size_t)o.ndevices, sizeof(dev_lane));
     if (!pl->dev) {
@@ -649,6 +696,50 @@ fail:
 
 static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, size_t nt, int corrupt_fd,
                          FILE *log, bcp_run_stats *stats, double t0);
+
+/* Bytes source k of t takes in the input slab: its data at 256-byte pitch
+ * (COPY), or the whole file prefix up to the data's end at page pitch (MAP:
+ * files are mapped from offset 0, the rebuild parity body sits 8n in). */
+static uint64_t span_of(const task *t, int k, int map_layout)
+{
+    if (!map_layout)
+        return RUP(t->size[k]);
+    return t->size[k] ? RUP_PAGE(t->src_off[k] + t->size[k]) : 0;
+}
+
+/* Where source k's data starts, relative to the slab. */
+static uint64_t data_off(const task *t, int k, int map_layout)
+{
+    return t->in_off[k] + (map_layout ? t->src_off[k] : 0);
+}
+
+/* MAP mode: place every source of tasks [a, b) in the slot's range (file
+ * offset 0 at in_off, read-only, populated).  Returns 0, or -errno when a
+ * file could not be opened or mapped (the caller reads the batch instead). */
+static int map_tasks(slot *S, const char *root, task *tasks, size_t a, size_t b)
+{
+    char fn[4352];
+    S->mapped = 1;
+    for (size_t i = a; i < b; i++) {
+        task *t = &tasks[i];
+        for (int k = 0; k < t->n; k++) {
+            const uint64_t len = span_of(t, k, 1);
+            if (!len)
+                continue;
+            const int is_parity = t->rebuild && k == t->parity_src;
+            chunk_file(fn, sizeof(fn), root, t->holders[k], is_parity ? "parity" : "chunks", t->path);
+            int fd = open(fn, O_RDONLY);
+            if (fd < 0)
+                return -errno;
+            void *m = mmap(S->va + t->in_off[k], (size_t)len, PROT_READ, MAP_SHARED | MAP_FIXED | MAP_POPULATE, fd, 0);
+            const int e = errno;
+            close(fd);
+            if (m == MAP_FAILED)
+                return -e;
+        }
+    }
+    return 0;
+}
 
 int bcp_pipeline_run(bcp_pipeline *pl, const char *store_root, int ntargets, const bcp_work_item *items,
                      size_t nitems, FILE *log, bcp_run_stats *stats)
@@ -731,12 +822,14 @@ static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, 
         free(args);
     }
 
-    /* 2. plan batches: inputs at 256-byte pitch, outputs likewise */
+    /* 2. plan batches: inputs at 256-byte pitch (MAP: page pitch), outputs
+     * at 256 */
+    const int ml = pl->map_mode;
     size_t in_cap = pl->in_cap, out_cap = pl->out_cap;
     for (size_t i = 0; i < nt; i++) {
         uint64_t in = 0;
         for (int k = 0; k < tasks[i].n; k++)
-            in += RUP(tasks[i].size[k]);
+            in += span_of(&tasks[i], k, ml);
         if (in > in_cap)
             in_cap = (size_t)in;
         if (RUP(tasks[i].out_len) > out_cap)
@@ -760,7 +853,7 @@ static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, 
         for (size_t i = 0; i < nt; i++) {
             uint64_t in = 0;
             for (int k = 0; k < tasks[i].n; k++)
-                in += RUP(tasks[i].size[k]);
+                in += span_of(&tasks[i], k, ml);
             total_in += in;
             max_in = in > max_in ? in : max_in;
         }
@@ -782,7 +875,7 @@ static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, 
     uint64_t total_in_all = 0;
     for (size_t i = 0; i < nt; i++)
         for (int k = 0; k < tasks[i].n; k++)
-            total_in_all += RUP(tasks[i].size[k]);
+            total_in_all += span_of(&tasks[i], k, ml);
     int nbatches = 0;
     {
         uint64_t in_used = 0, out_used = 0, consumed = 0, limit = plan_in;
@@ -790,7 +883,7 @@ static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, 
             task *t = &tasks[i];
             uint64_t in = 0;
             for (int k = 0; k < t->n; k++)
-                in += RUP(t->size[k]);
+                in += span_of(t, k, ml);
             if (i == 0 || in_used + in > limit || out_used + RUP(t->out_len) > out_cap) {
                 nbatches++;
                 consumed += in_used;
@@ -804,7 +897,7 @@ static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, 
             t->batch = nbatches - 1;
             for (int k = 0; k < t->n; k++) {
                 t->in_off[k] = in_used;
-                in_used += RUP(t->size[k]);
+                in_used += span_of(t, k, ml);
             }
             t->out_off = out_used;
             out_used += RUP(t->out_len);
@@ -858,29 +951,101 @@ static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, 
             latch_destroy(&S->writes);
             S->busy = 0;
         }
+        if (S->mapped) /* its H2D ended before its D2H, before its writes */
+            slot_unmap(L->eng, S);
         tm.slot_wait += now_s() - tw;
         size_t last = first;
         while (last < nt && tasks[last].batch == b)
             last++;
-        long nreads = 0;
-        for (size_t i = first; i < last; i++)
-            nreads += tasks[i].n;
-        tw = now_s();
-        latch_init(&S->reads, nreads);
         uint64_t in_used = 0;
         for (size_t i = first; i < last; i++)
             for (int k = 0; k < tasks[i].n; k++) {
-                read_arg *a = &ra[rnext++];
-                *a = (read_arg){{0}, store_root, &tasks[i], k, S->h_in + tasks[i].in_off[k], &bytes_read,
-                                &S->reads};
-                pool_push(&pl->readers, &a->j, do_read);
-                uint64_t end = tasks[i].in_off[k] + RUP(tasks[i].size[k]);
+                const uint64_t end = tasks[i].in_off[k] + span_of(&tasks[i], k, ml);
                 if (end > in_used)
                     in_used = end;
             }
+        /* MAP: the batch's tail tasks [split, last), about map_share of its
+         * input bytes, are mapped by this thread while the io threads read
+         * the head into the slab */
+        size_t split = last;
+        if (ml && last > first) {
+            const uint64_t from = in_used - (uint64_t)(pl->map_share * (double)in_used);
+            split = first;
+            while (split < last && tasks[split].in_off[0] < from)
+                split++;
+        }
+        const uint64_t reg_lo = split < last ? tasks[split].in_off[0] : in_used;
+        long nreads = 0;
+        for (size_t i = first; i < split; i++)
+            nreads += tasks[i].n;
+        tw = now_s();
+        latch_init(&S->reads, nreads);
+        for (size_t i = first; i < split; i++)
+            for (int k = 0; k < tasks[i].n; k++) {
+                read_arg *a = &ra[rnext++];
+                *a = (read_arg){{0}, store_root, &tasks[i], k, S->h_in + data_off(&tasks[i], k, ml), &bytes_read,
+                                &S->reads};
+                pool_push(&pl->readers, &a->j, do_read);
+            }
         tm.read_jobs += (uint32_t)nreads;
+        double map_s = 0;
+        int mapped_ok = 0;
+        if (split < last) {
+            const double tm0 = now_s();
+            int mrc = map_tasks(S, store_root, tasks, split, last);
+            if (!mrc && in_used > reg_lo) {
+                mrc = bcp_host_register_dma_src(L->eng, S->va + reg_lo, (size_t)(in_used - reg_lo));
+                if (!mrc) {
+                    S->reg_lo = (size_t)reg_lo;
+                    S->reg_len = (size_t)(in_used - reg_lo);
+                }
+            }
+            map_s = now_s() - tm0;
+            tm.map += map_s;
+            mapped_ok = !mrc;
+            if (!mapped_ok) {
+                slot_unmap(L->eng, S);
+                tm.map_fallbacks++;
+            }
+        }
         latch_wait(&S->reads);
+        const double t_read_end = S->reads.t_zero;
         latch_destroy(&S->reads);
+        if (split < last && !mapped_ok) { /* read what could not be mapped */
+            long n2 = 0;
+            for (size_t i = split; i < last; i++)
+                n2 += tasks[i].n;
+            latch_init(&S->reads, n2);
+            for (size_t i = split; i < last; i++)
+                for (int k = 0; k < tasks[i].n; k++) {
+                    read_arg *a = &ra[rnext++];
+                    *a = (read_arg){{0}, store_root, &tasks[i], k, S->h_in + data_off(&tasks[i], k, ml),
+                                    &bytes_read, &S->reads};
+                    pool_push(&pl->readers, &a->j, do_read);
+                }
+            tm.read_jobs += (uint32_t)n2;
+            latch_wait(&S->reads);
+            latch_destroy(&S->reads);
+        }
+        if (split < last && mapped_ok) {
+            uint64_t got = 0;
+            for (size_t i = split; i < last; i++)
+                for (int k = 0; k < tasks[i].n; k++)
+                    got += tasks[i].size[k];
+            pthread_mutex_lock(&g_stat_lock);
+            bytes_read += got;
+            pthread_mutex_unlock(&g_stat_lock);
+            tm.mapped_bytes += in_used - reg_lo;
+            /* next share: the two paths' rates in this batch, balanced so
+             * both finish together (smoothed; a batch with nothing read
+             * gives no reader rate) */
+            const double rd_s = t_read_end - tw;
+            if (split > first && rd_s > 0 && map_s > 0) {
+                const double rr = (double)reg_lo / rd_s, rm = (double)(in_used - reg_lo) / map_s;
+                double f = 0.5 * pl->map_share + 0.5 * rm / (rm + rr);
+                pl->map_share = f < 0.05 ? 0.05 : f > 0.95 ? 0.95 : f;
+            }
+        }
         const double ts = now_s();
         tm.read_wait += ts - tw;
         uint32_t ns = 0, nsrc = 0;
@@ -890,13 +1055,17 @@ static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, 
             st[ns] = (bcp_stripe){(uint64_t)S->d_out + t->out_off, t->out_len, nsrc, (uint32_t)t->n,
                                   t->max_cs > WINDOW ? WINDOW : 0};
             for (int k = 0; k < t->n; k++)
-                so[nsrc++] = (bcp_source){(uint64_t)S->d_in + t->in_off[k], t->size[k]};
+                so[nsrc++] = (bcp_source){(uint64_t)S->d_in + data_off(t, k, ml), t->size[k]};
             ns++;
             if (t->out_off + RUP(t->out_len) > out_used)
                 out_used = t->out_off + RUP(t->out_len);
         }
-        /* device: H2D (side queue) -> kernel -> D2H (side queue) */
-        if ((rc = bcp_h2d_async(L->qh, S->d_in, S->h_in, (size_t)in_used)) ||
+        /* device: H2D (side queue; the slab's part, then the mapped part
+         * straight out of the page cache) -> kernel -> D2H (side queue) */
+        const uint8_t *tail_src = (mapped_ok ? S->va : S->h_in) + reg_lo;
+        if ((reg_lo && (rc = bcp_h2d_async(L->qh, S->d_in, S->h_in, (size_t)reg_lo))) ||
+            (in_used > reg_lo &&
+             (rc = bcp_h2d_async(L->qh, (uint8_t *)S->d_in + reg_lo, tail_src, (size_t)(in_used - reg_lo)))) ||
             (rc = bcp_event_record(S->ev_h, L->qh)) || (rc = bcp_queue_wait_event(L->qk, S->ev_h)) ||
             (rc = bcp_xor_stripes_async(L->qk, st, ns, so, nsrc)) || (rc = bcp_event_record(S->ev_k, L->qk)) ||
             (rc = bcp_queue_wait_event(L->qd, S->ev_k)) ||
@@ -933,12 +1102,16 @@ static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, 
         const int s1 = bcp_queue_sync(L->qh), s2 = bcp_queue_sync(L->qk), s3 = bcp_queue_sync(L->qd);
         if (!rc && !dev_rc)
             dev_rc = s1 ? s1 : s2 ? s2 : s3;
+        for (int k = 0; k < nslots; k++) /* no mapping outlives the run */
+            if (L->slots[k].mapped)
+                slot_unmap(L->eng, &L->slots[k]);
     }
     /* every job has run: the writes latched above, the completions before them */
     free(ra);
     free(wa);
     free(cargs);
     tm.drain = now_s() - td;
+    tm.read_mode = ml ? BCP_READ_MAP : BCP_READ_COPY;
     pl->last = tm;
     if (!rc && dev_rc)
         rc = dev_rc;

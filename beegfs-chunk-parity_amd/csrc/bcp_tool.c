@@ -73,7 +73,7 @@ static int pipeline_on_all_gpus(bcp_pipeline **pl)
 {
     int ndev = 0;
     bcp_device_count(&ndev);
-    const bcp_pipeline_opts o = {0, (size_t)256 << 20, 0, 4, ndev > 0 ? ndev : 1};
+    const bcp_pipeline_opts o = {0, (size_t)256 << 20, 0, 4, ndev > 0 ? ndev : 1, BCP_READ_AUTO};
     return bcp_pipeline_create(&o, pl);
 }
 

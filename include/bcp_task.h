@@ -478,7 +478,22 @@ typedef struct {
     int nslots;          /* slabs in flight per device (2..8) */
     int ndevices;        /* GPUs device .. device+ndevices-1 (mod the visible count),
                             batches round-robin (0 = 1) */
+    int read_mode;       /* how chunk bytes reach the device (BCP_READ_*; ABI version 2) */
 } bcp_pipeline_opts;
+/* Read paths of the pipeline's input:
+ *   COPY: io threads read() each chunk into the slot's pinned slab, one H2D
+ *     per batch (page cache -> slab -> device: the CPU copies every byte);
+ *   MAP:  a share of every batch is mmap'ed (MAP_FIXED, one reserved range per
+ *     slot), registered read-only (bcp_host_register_dma_src) and copied to the
+ *     device straight out of the page cache, while the io threads read the
+ *     rest; the share follows the measured rates of the two (mapping and
+ *     pinning is serial per process).  A batch whose mapping cannot be
+ *     registered (a file truncated meanwhile) is read instead.  Input offsets
+ *     are page-aligned in this mode.
+ *   AUTO (0): COPY; env BCP_PIPELINE_READ=copy|map overrides AUTO. */
+#define BCP_READ_AUTO 0
+#define BCP_READ_COPY 1
+#define BCP_READ_MAP 2
 
 /* Parity generation for local stores without per-task messaging: chunk
  * files are read by io threads into pinned slabs, copied H2D on a side
@@ -486,8 +501,14 @@ typedef struct {
  * another side queue and written as parity chunk files -- byte-identical
  * to bcp_gen_run's (same header, padding and window replay).  NO_P items are
  * skipped; items without holders unlink their parity chunk.  opts may be
- * NULL ({0, 256 MiB, 0, 4, 1}: 4 slots beat 3 by 8-15 % on every
- * workload in two interleaved A/Bs). */
+ * NULL ({0, 256 MiB, 0, 4, 1, AUTO}: 4 slots beat 3 by 8-15 % on every
+ * workload in two interleaved A/Bs).
+ * Footprint per device: nslots x (input + output slab) of pinned host memory
+ * and the same of HBM -- 4 x 2 x 256 MiB = 2 GiB pinned + 2 GiB HBM by
+ * default, 16 GiB pinned over 8 GPUs (slabs grow to the largest stripe's
+ * inputs) -- plus io_threads readers and as many writers (8 + 8 per GPU by
+ * default, each pool capped at 64 threads); MAP mode adds a reserved (not
+ * committed) address range of the input slab's size per slot. */
 int bcp_pipeline_gen(const char *store_root, int ntargets, const bcp_work_item *items, size_t nitems,
                      const bcp_pipeline_opts *opts, FILE *log, bcp_run_stats *stats);
 /* The same as a long-lived object: engine, queues, io threads and pinned /
@@ -500,13 +521,19 @@ int bcp_pipeline_run(bcp_pipeline *pl, const char *store_root, int ntargets, con
 int bcp_pipeline_destroy(bcp_pipeline *pl);
 /* Where the host thread of the pipeline's last run spent its wall time
  * (seconds; for tools): stat phase, reading a batch (from issuing its reads
- * to the last one's end), waiting for a slot's previous batch to be written
- * before reading into it, building and submitting batches, and the drain
- * after the last submission. */
+ * to the last one's end, MAP mode's mapping included), waiting for a slot's
+ * previous batch to be written before reading into it, building and
+ * submitting batches, and the drain after the last submission; MAP mode:
+ * the host thread's mapping + registering time (inside read_wait), the bytes
+ * copied out of mappings, and batches that fell back to reading. */
 typedef struct {
     double stat, read_wait, slot_wait, submit, drain;
     uint32_t batches;    /* device batches */
-    uint32_t read_jobs;  /* io read jobs (one per chunk of every stripe) */
+    uint32_t read_jobs;  /* io read jobs (one per chunk read into a slab) */
+    double map;
+    uint64_t mapped_bytes;
+    uint32_t map_fallbacks;
+    int read_mode;       /* the mode the run used (BCP_READ_COPY / BCP_READ_MAP) */
 } bcp_pipeline_timing;
 int bcp_pipeline_last_timing(const bcp_pipeline *pl, bcp_pipeline_timing *out);
 /* Rebuild of one lost target with the batched pipeline (do_file's selection

@@ -24,6 +24,15 @@ def gpu_fold(bcp, engine):
     bcp.task_shutdown()
 
 
+@pytest.fixture(params=["copy", "map"])
+def read_path(request, monkeypatch):
+    """Both read paths of the batched pipeline (bcp_pipeline_opts.read_mode
+    AUTO resolves through BCP_PIPELINE_READ): chunks read into pinned slabs,
+    or a share of every batch mapped and copied from the page cache."""
+    monkeypatch.setenv("BCP_PIPELINE_READ", request.param)
+    return request.param
+
+
 @pytest.fixture(params=["pipelined", "batched"])
 def fold_mode(request, bcp):
     """Both forms of the P role's GPU fold (bcp_task_set_fold_mode)."""
@@ -104,6 +113,7 @@ def test_config1_shape_small(bcp, oracle, tmp_path):
 # batched pipeline (bcp_pipeline_gen): same files as the per-task protocol
 # --------------------------------------------------------------------------
 @pytest.mark.parametrize("slab", [1 << 20, 64 << 20])
+@pytest.mark.usefixtures("read_path")
 def test_pipeline_matches_oracle_mixed_sizes(bcp, oracle, tmp_path, slab):
     rng = np.random.default_rng(77)
     ntargets = 10
@@ -124,6 +134,7 @@ def test_pipeline_matches_oracle_mixed_sizes(bcp, oracle, tmp_path, slab):
         assert S.read_file(S.parity_path(root, p, path)) == oracle.gen_parity_file(contents[path]), path
 
 
+@pytest.mark.usefixtures("read_path")
 def test_pipeline_wide_and_windowed_stripes(bcp, oracle, tmp_path):
     """The batched pipeline on stripes wider than a tile record (up to 15
     sources), chunks past the 10 MiB transfer window (replay) and grouped
@@ -161,6 +172,7 @@ def test_pipeline_wide_and_windowed_stripes(bcp, oracle, tmp_path):
         assert S.read_file(S.chunk_path(root, victim, path)) == data, path
 
 
+@pytest.mark.usefixtures("read_path")
 def test_pipeline_multiwindow_and_delete(bcp, oracle, tmp_path):
     root = str(tmp_path)
     files = [("big/a", [0, 1], 4, [10485760, 26214405]),
@@ -174,6 +186,7 @@ def test_pipeline_multiwindow_and_delete(bcp, oracle, tmp_path):
     assert not os.path.exists(S.parity_path(root, 3, "small"))
 
 
+@pytest.mark.usefixtures("read_path")
 def test_pipeline_refuses_paths_outside_the_store(bcp, oracle, tmp_path):
     """As process_task: an item whose path would leave the targets'
     directories is skipped (gen and rebuild); the others run."""
@@ -199,6 +212,7 @@ def test_pipeline_refuses_paths_outside_the_store(bcp, oracle, tmp_path):
     assert S.read_file(os.path.join(root, "st1", "outside", "x")) == b"z" * 100
 
 
+@pytest.mark.usefixtures("read_path")
 def test_pipeline_object_reuse_and_growth(bcp, oracle, tmp_path):
     """One long-lived pipeline, several runs; the second needs bigger slabs."""
     root = str(tmp_path)
@@ -488,6 +502,7 @@ def test_cli_complete_partial_rebuild(bcp, oracle, tmp_path, engine_kind):
 
 
 @pytest.mark.parametrize("ndevices,nslots", [(2, 2), (3, 2), (8, 3)])
+@pytest.mark.usefixtures("read_path")
 def test_pipeline_multi_device_lanes(bcp, oracle, tmp_path, ndevices, nslots):
     """Batches round-robin over several device lanes (on a one-GPU box the
     lanes wrap onto the same GPU, each with its own engine, queues and
@@ -510,6 +525,7 @@ def test_pipeline_multi_device_lanes(bcp, oracle, tmp_path, ndevices, nslots):
         pl.close()
 
 
+@pytest.mark.usefixtures("read_path")
 def test_pipeline_rebuild_matches_protocol_rebuild(bcp, oracle, tmp_path):
     """bcp_pipeline_rebuild == bcp_rebuild_run byte for byte: mixed sizes,
     multi-window stripes (replay), a missing survivor, a survivor rewritten
@@ -675,3 +691,56 @@ def test_caller_transport_table_on_device(bcp, oracle, tmp_path, foreign_ops_add
             assert S.read_file(S.chunk_path(root, victim, path)) == data, path
     finally:
         bcp.set_transport(None)
+
+
+@pytest.mark.parametrize("mode", ["map", "copy"])
+def test_pipeline_read_modes_byte_identical_and_fallback(bcp, oracle, tmp_path, mode):
+    """read_mode MAP: part of every batch goes to the device straight out of
+    mapped chunk files (timing.mapped_bytes), the output is the COPY path's
+    byte for byte; a chunk that cannot be opened (mode 000: stat works, open
+    does not) makes its batch fall back to reading, with the same result --
+    the source counts as unreadable (zeros) exactly as in COPY mode."""
+    rng = np.random.default_rng(4242)
+    nt = 9
+    files = []
+    for i in range(120):
+        holders, p = S.random_layout(rng, nt, 8)
+        lens = [int(x) for x in np.exp(rng.uniform(np.log(64 * KiB), np.log(4 * 1024 * KiB), size=8))]
+        files.append((f"r/{i % 7}/c{i}", holders, p, lens))
+    root = str(tmp_path / "store")
+    items, contents = S.populate(root, nt, files, seed=17)
+    bad = S.chunk_path(root, files[40][1][2], files[40][0])
+    want_mode = {"map": bcp.READ_MAP, "copy": bcp.READ_COPY}[mode]
+    outs = {}
+    for locked in (False, True):
+        if locked:
+            if os.geteuid() == 0:
+                pytest.skip("root opens mode-000 files")
+            os.chmod(bad, 0)
+        pl = bcp.Pipeline(slab_bytes=16 << 20, io_threads=4, nslots=3, read_mode=want_mode)
+        try:
+            st = pl.run(root, nt, items)
+            tm = pl.last_timing()
+        finally:
+            pl.close()
+            os.chmod(bad, 0o600)
+        assert st.errors == 0 and st.tasks == len(files)
+        assert tm["read_mode"] == want_mode and tm["batches"] > 4
+        if mode == "map":
+            assert tm["mapped_bytes"] > 0 and tm["map"] > 0
+            if not locked:  # (locked: the bad chunk's batch falls back if that task was to be mapped)
+                assert tm["map_fallbacks"] == 0
+        else:
+            assert tm["mapped_bytes"] == 0 and tm["map_fallbacks"] == 0
+        outs[locked] = {path: S.read_file(S.parity_path(root, p, path)) for path, _, p, _ in files}
+    for path, holders, p, lens in files:
+        assert outs[False][path] == oracle.gen_parity_file(contents[path]), path
+    # the unreadable chunk: every other file unchanged, its own as COPY mode gives it
+    diff = [path for path in outs[False] if outs[False][path] != outs[True][path]]
+    assert diff == [files[40][0]]
+    body = np.frombuffer(outs[True][files[40][0]][64:], dtype=np.uint8)
+    chunks = [c for k, c in enumerate(contents[files[40][0]]) if k != 2]
+    ref = np.zeros(len(body), dtype=np.uint8)
+    for c in chunks:
+        ref[:len(c)] ^= c
+    assert np.array_equal(body, ref)

@@ -10,6 +10,11 @@ Sampled stripes are checked against the oracle, sampled rebuilt chunks
 against the originals.  Rates: (chunk bytes read + bytes written) / wall
 time; the host-to-device link's bound beside them (tools/box_probe.py).
 One JSON line per measurement.
+
+--modes copy,map: the pipeline's read paths (bcp_pipeline_opts.read_mode),
+interleaved run by run; --contend 0,16: with N host threads memcpy'ing
+64 MiB buffers meanwhile (host memory bandwidth taken, as by the other GPUs'
+pipelines of one node), also interleaved.
 """
 import argparse
 import concurrent.futures as cf
@@ -46,7 +51,12 @@ def main():
     ap.add_argument("--victim", type=int, default=4)
     ap.add_argument("--sample", type=int, default=16)
     ap.add_argument("--threads", type=int, default=16)
+    ap.add_argument("--modes", default="copy")
+    ap.add_argument("--contend", default="0")
     a = ap.parse_args()
+    modes = {"copy": bcp.READ_COPY, "map": bcp.READ_MAP}
+    mode_list = a.modes.split(",")
+    contend_list = [int(x) for x in a.contend.split(",")]
     import box_probe
     box = box_probe.cpu_info()
     box.update(box_probe.pcie_rates(bcp))
@@ -85,54 +95,88 @@ def main():
     sample = sorted({0, a.stripes - 1} | {int(x) for x in rng.choice(a.stripes, size=a.sample, replace=False)})
     h2d = box["h2d_GBps"] * 1e9
 
-    pl = bcp.Pipeline()
+    import ctypes
+    import threading
+
+    class Contention:
+        """n threads copying 64 MiB buffers (ctypes.memmove drops the GIL)."""
+
+        def __init__(self, n):
+            self.n, self.stop, self.th = n, False, []
+            self.bufs = [(np.ones(64 * MiB, np.uint8), np.zeros(64 * MiB, np.uint8)) for _ in range(n)]
+
+        def run(self, i):
+            a, b = self.bufs[i]
+            while not self.stop:
+                ctypes.memmove(b.ctypes.data, a.ctypes.data, a.nbytes)
+
+        def __enter__(self):
+            self.th = [threading.Thread(target=self.run, args=(i,)) for i in range(self.n)]
+            for t in self.th:
+                t.start()
+            return self
+
+        def __exit__(self, *exc):
+            self.stop = True
+            for t in self.th:
+                t.join()
+
+    pls = {m: bcp.Pipeline(read_mode=modes[m]) for m in mode_list}
     try:
-        # ---- config 2: parity gen over the whole store
         rd = a.stripes * 8 * C
         wr = a.stripes * (8 * 8 + C)
-        times, timing = [], []
-        for r in range(1 + a.reps):
-            t0 = time.perf_counter()
-            st = pl.run(a.root, NT, items)
-            times.append(time.perf_counter() - t0)
-            timing.append(pl.last_timing())
-            if st.errors or st.tasks != a.stripes:
-                sys.exit(f"gen run: errors {st.errors}, tasks {st.tasks}")
-        bad = [files[i][0] for i in sample
-               if S.read_file(S.parity_path(a.root, files[i][2], files[i][0]))
-               != oracle.gen_parity_file([chunk_of(i, k) for k in range(8)])]
-        w = float(np.median(times[1:])) if a.reps else times[0]
-        emit(config=2, path="pipeline_gen(1 GPU, full size)", stripes=a.stripes, bytes_read=rd, bytes_written=wr,
-             cold_seconds=round(times[0], 4), warm_seconds=round(w, 4), runs_s=[round(x, 4) for x in times],
-             GiBps=round((rd + wr) / w / GiB, 2), h2d_bound_seconds=round(rd / h2d, 4),
-             input_over_link=round(rd / w / h2d, 3), timing=timing[-1], verified=not bad, bad=bad[:3])
-        # ---- config 3: lose target victim, rebuild it from 7 survivors + parity
         v = a.victim
         lost = [i for i in range(a.stripes) if v in files[i][1]]
         keep = {i: chunk_of(i, files[i][1].index(v)) for i in sample if v in files[i][1]}
         ordered = sorted(items, key=lambda x: x[0].encode())  # DB key order (rebuild/main.c:223-225)
         rd3 = len(lost) * (8 * C + 8 * 8)     # 7 survivors + parity body, + the header
         wr3 = len(lost) * C
-        times, timing = [], []
+        res = {}
         for r in range(1 + a.reps):
-            with cf.ThreadPoolExecutor(a.threads) as ex:
-                list(ex.map(lambda i: os.remove(S.chunk_path(a.root, v, files[i][0])), lost))
-            t0 = time.perf_counter()
-            st = pl.rebuild(a.root, NT, v, ordered)
-            times.append(time.perf_counter() - t0)
-            timing.append(pl.last_timing())
-            if st.errors or st.tasks != len(lost):
-                sys.exit(f"rebuild run: errors {st.errors}, tasks {st.tasks}")
-        bad = [files[i][0] for i, want in keep.items()
-               if S.read_file(S.chunk_path(a.root, v, files[i][0])) != want.tobytes()]
-        w = float(np.median(times[1:])) if a.reps else times[0]
-        emit(config=3, path=f"pipeline_rebuild(1 GPU, full size, target {v})", stripes=len(lost), bytes_read=rd3,
-             bytes_written=wr3, cold_seconds=round(times[0], 4), warm_seconds=round(w, 4),
-             runs_s=[round(x, 4) for x in times], GiBps=round((rd3 + wr3) / w / GiB, 2),
-             h2d_bound_seconds=round(rd3 / h2d, 4), input_over_link=round(rd3 / w / h2d, 3), timing=timing[-1],
-             verified=not bad and len(keep) > 0, bad=bad[:3], sampled=len(keep))
+            for nc in contend_list:
+                for m in mode_list:
+                    pl = pls[m]
+                    with Contention(nc):
+                        # ---- config 2: parity gen over the whole store
+                        t0 = time.perf_counter()
+                        st = pl.run(a.root, NT, items)
+                        tg = time.perf_counter() - t0
+                        tmg = pl.last_timing()
+                        if st.errors or st.tasks != a.stripes:
+                            sys.exit(f"gen run: errors {st.errors}, tasks {st.tasks}")
+                    bad = [files[i][0] for i in sample
+                           if S.read_file(S.parity_path(a.root, files[i][2], files[i][0]))
+                           != oracle.gen_parity_file([chunk_of(i, k) for k in range(8)])]
+                    # ---- config 3: lose target v, rebuild it (the deletion untimed)
+                    with cf.ThreadPoolExecutor(a.threads) as ex:
+                        list(ex.map(lambda i: os.remove(S.chunk_path(a.root, v, files[i][0])), lost))
+                    with Contention(nc):
+                        t0 = time.perf_counter()
+                        st = pl.rebuild(a.root, NT, v, ordered)
+                        tr = time.perf_counter() - t0
+                        tmr = pl.last_timing()
+                        if st.errors or st.tasks != len(lost):
+                            sys.exit(f"rebuild run: errors {st.errors}, tasks {st.tasks}")
+                    bad3 = [files[i][0] for i, want in keep.items()
+                            if S.read_file(S.chunk_path(a.root, v, files[i][0])) != want.tobytes()]
+                    key = (m, nc)
+                    res.setdefault(key, {"gen": [], "rebuild": []})
+                    res[key]["gen"].append(tg)
+                    res[key]["rebuild"].append(tr)
+                    emit(rep=r, mode=m, contend=nc, gen_s=round(tg, 4), rebuild_s=round(tr, 4),
+                         gen_GiBps=round((rd + wr) / tg / GiB, 2), rebuild_GiBps=round((rd3 + wr3) / tr / GiB, 2),
+                         gen_input_over_link=round(rd / tg / h2d, 3), rebuild_input_over_link=round(rd3 / tr / h2d, 3),
+                         gen_timing=tmg, rebuild_timing=tmr, verified=not bad and not bad3 and len(keep) > 0)
+        for (m, nc), d in res.items():
+            g = float(np.median(d["gen"][1:])) if a.reps else d["gen"][0]
+            rb = float(np.median(d["rebuild"][1:])) if a.reps else d["rebuild"][0]
+            emit(summary=True, mode=m, contend=nc, stripes=a.stripes, warm_gen_s=round(g, 4),
+                 gen_GiBps=round((rd + wr) / g / GiB, 2), gen_input_over_link=round(rd / g / h2d, 3),
+                 warm_rebuild_s=round(rb, 4), rebuild_GiBps=round((rd3 + wr3) / rb / GiB, 2),
+                 rebuild_input_over_link=round(rd3 / rb / h2d, 3), cold_gen_s=round(d["gen"][0], 4))
     finally:
-        pl.close()
+        for pl in pls.values():
+            pl.close()
         shutil.rmtree(a.root, ignore_errors=True)
 
 
