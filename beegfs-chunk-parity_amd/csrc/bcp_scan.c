@@ -12,9 +12,14 @@
  *       may be added, never lost, duplicated or moved.
  *
  * The reference's phase-1 scatter (feeders -> eaters by simple_hash(path) %
- * ntargets, gen/main.c:238-336, 576-699) exists to spread aggregation over
- * MPI ranks; with loopback ranks every target's stream is fed into one event
- * set, which aggregates identically (fih_add_info is per path).
+ * ntargets, gen/main.c:238-336, 576-699) spreads aggregation over MPI ranks;
+ * here every target's stream is fed into one event set, target 0 first.  The
+ * aggregation is identical (fih_add_info is per path), and so is the order:
+ * bcp_plan_rounds re-partitions the event set by the same hash, keeps each
+ * eater's paths in first-seen order (= arrival order if feeder k's records
+ * reach the eaters before feeder k+1's -- the reference's own interleaving of
+ * concurrent feeders is not deterministic) and emits the eaters' rounds in
+ * target order (gen/main.c:710-711, 758).
  */
 #define _GNU_SOURCE
 #include <errno.h>
