@@ -94,6 +94,8 @@ def parse():
     ap.add_argument("--e2e-reps", type=int, default=3, help="warm end-to-end gen runs (after one cold run)")
     ap.add_argument("--e2e-dir", default="/dev/shm", help="where the end-to-end stores are created")
     ap.add_argument("--e2e-max-s", type=float, default=150.0, help="wall-time cap of the end-to-end leg")
+    ap.add_argument("--e2e-modes", default="copy,map",
+                    help="pipeline read paths timed end to end, interleaved; the first is the headline")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--allow-shared", action="store_true",
                     help="run N ranks even when fewer than N distinct GPUs exist (rehearsal; "
@@ -287,7 +289,9 @@ def e2e_leg(a, d, device: int, bus_id: str):
     [64 KiB, 4 MiB], 9 storage targets, P rotating over the one left out) of
     about --e2e-gib per rank in --e2e-dir; the batched pipeline generates every
     parity file (one cold run, --e2e-reps warm), then target 4 is lost (its
-    chunk files deleted, outside the timing) and rebuilt.  The reference's
+    chunk files deleted, outside the timing) and rebuilt -- each through the
+    pipeline's read paths of --e2e-modes, interleaved (the first is the
+    headline `gen` / `rebuild`, the others in `by_read_mode`).  The reference's
     I/O path: task_processing.c:62-79,186,199-226 (read, fold, write).
     Returns the rank-0 summary (None elsewhere); never part of `value`."""
     import concurrent.futures as cf
@@ -297,20 +301,27 @@ def e2e_leg(a, d, device: int, bus_id: str):
     import bcp_store as BS
     t_start = time.perf_counter()
     NT, W, VICTIM = 9, 8, 4
-    rank_root = os.path.join(a.e2e_dir, f"bcp_bench_e2e_{os.getppid()}_{d.rank}")
     want = int(a.e2e_gib * GiB)
-    reason = None
-    try:
-        stv = os.statvfs(a.e2e_dir)
-        free = stv.f_bavail * stv.f_frsize
-        # chunks + parity (~35 % of the chunk bytes at these shapes) + one rebuilt target
-        room = int(free / (1.7 * d.world))
-        if room < want:
-            want = room
-        if want < (64 << 20):
-            reason = f"{a.e2e_dir}: {free / GiB:.1f} GiB free for {d.world} rank stores"
-    except OSError as e:
-        reason = f"{a.e2e_dir}: {e}"
+    reason, base, room = None, None, 0
+    # the store's directory: --e2e-dir (tmpfs by default), else the temp dir,
+    # whichever has room for every rank's store (chunks + parity, ~35 % of the
+    # chunk bytes at these shapes, + one rebuilt target)
+    import tempfile
+    for cand in dict.fromkeys([a.e2e_dir, tempfile.gettempdir()]):
+        try:
+            stv = os.statvfs(cand)
+        except OSError as e:
+            reason = f"{cand}: {e}"
+            continue
+        r = int(stv.f_bavail * stv.f_frsize / (1.7 * d.world))
+        if r > room:
+            base, room = cand, r
+        if r >= want:
+            break
+    if base is not None:
+        want = min(want, room)
+        reason = None if want >= (64 << 20) else f"{base}: {room * 1.7 * d.world / GiB:.1f} GiB free for {d.world} stores"
+    rank_root = os.path.join(base or a.e2e_dir, f"bcp_bench_e2e_{os.getppid()}_{d.rank}")
     # every rank agrees to run (or not): a rank that skipped would leave the
     # others waiting at the barriers below
     if d.sum(0.0 if reason else 1.0) != d.world:
@@ -343,7 +354,7 @@ def e2e_leg(a, d, device: int, bus_id: str):
                 f.write(memoryview(chunk_of(i, k)))
 
     out = {}
-    pl = None
+    pls = {}
     try:
         shutil.rmtree(rank_root, ignore_errors=True)
         BS.make_store(rank_root, NT)
@@ -376,9 +387,11 @@ def e2e_leg(a, d, device: int, bus_id: str):
         eng.host_free(h)
         q.close()
         eng.close()
-        pl = bcp.Pipeline(device=device)
+        modes = [m for m in a.e2e_modes.split(",") if m]
+        pls = {m: bcp.Pipeline(device=device, read_mode={"copy": bcp.READ_COPY, "map": bcp.READ_MAP}[m])
+               for m in modes}
 
-        def timed(fn, before=None):
+        def timed(pl, fn, before=None):
             if before:
                 before()
             d.barrier()
@@ -387,14 +400,6 @@ def e2e_leg(a, d, device: int, bus_id: str):
             dt = time.perf_counter() - t0
             return st, dt, d.max(dt), pl.last_timing()
 
-        # ---- gen: one cold run, then warm runs
-        runs, tasks_ok = [], True
-        for r in range(1 + max(1, a.e2e_reps)):
-            if r > 1 and d.max(time.perf_counter() - t_start) > a.e2e_max_s:
-                break
-            st, dt, dmax, tim = timed(lambda: pl.run(rank_root, NT, items))
-            tasks_ok = tasks_ok and st.errors == 0 and st.tasks == nst and st.bytes_read == rd
-            runs.append((dt, dmax, tim))
         vr = np.random.default_rng(11 + d.rank)
         sample = sorted({0, nst - 1} | {int(x) for x in vr.integers(0, nst, 6)})
 
@@ -406,14 +411,24 @@ def e2e_leg(a, d, device: int, bus_id: str):
                 body[:len(c)] ^= c
             want_file = np.asarray([len(c) for c in ch], dtype="<u8").tobytes() + body.tobytes()
             return BS.read_file(BS.parity_path(rank_root, files[i][2], files[i][0])) == want_file
-        gen_ok = tasks_ok and all(parity_ok(i) for i in sample)
-        warm = [x[1] for x in runs[1:]] or [runs[0][1]]
-        warm_own = [x[0] for x in runs[1:]] or [runs[0][0]]
-        gen = {"cold_s": round(runs[0][1], 4), "warm_s": round(float(np.median(warm)), 4),
-               "runs_s": [round(x[1], 4) for x in runs], "own_warm_s": round(float(np.median(warm_own)), 4),
-               "timing": runs[-1][2], "verified": gen_ok}
 
-        # ---- rebuild target VICTIM from 7 survivors + parity
+        # ---- gen: one cold run, then warm runs, the read paths interleaved
+        runs = {m: [] for m in modes}
+        ok = {m: True for m in modes}
+        nrep = 1 + max(1, a.e2e_reps)
+        for r in range(nrep):
+            last_rep = r == nrep - 1 or (r > 1 and d.max(time.perf_counter() - t_start) > a.e2e_max_s)
+            for m in modes:
+                pl = pls[m]
+                st, dt, dmax, tim = timed(pl, lambda: pl.run(rank_root, NT, items))
+                ok[m] = ok[m] and st.errors == 0 and st.tasks == nst and st.bytes_read == rd
+                runs[m].append((dt, dmax, tim))
+                if last_rep:  # this mode's files, checked before the next mode rewrites them
+                    ok[m] = ok[m] and all(parity_ok(i) for i in sample)
+            if last_rep:
+                break
+
+        # ---- rebuild target VICTIM from 7 survivors + parity, each read path
         lost = [i for i in range(nst) if VICTIM in files[i][1]]
         ordered = sorted(items, key=lambda x: x[0].encode())  # DB key order (rebuild/main.c:223-225)
         rd3 = sum(int(lens[i].sum()) - int(lens[i][files[i][1].index(VICTIM)]) + int(lens[i].max()) + 8 * W
@@ -423,53 +438,82 @@ def e2e_leg(a, d, device: int, bus_id: str):
         def drop_victim():
             with cf.ThreadPoolExecutor(8) as ex:
                 list(ex.map(lambda i: os.remove(BS.chunk_path(rank_root, VICTIM, files[i][0])), lost))
-        rruns, rok = [], True
-        for r in range(2):
-            st, dt, dmax, tim = timed(lambda: pl.rebuild(rank_root, NT, VICTIM, ordered), before=drop_victim)
-            rok = rok and st.errors == 0 and st.tasks == len(lost)
-            rruns.append((dt, dmax, tim))
         rsample = [i for i in sample if i in set(lost)] or lost[:2]
-        rok = rok and all(BS.read_file(BS.chunk_path(rank_root, VICTIM, files[i][0])) ==
-                          chunk_of(i, files[i][1].index(VICTIM)).tobytes() for i in rsample)
-        reb = {"cold_s": round(rruns[0][1], 4), "warm_s": round(rruns[-1][1], 4),
-               "own_warm_s": round(rruns[-1][0], 4), "timing": rruns[-1][2], "verified": rok}
+        rruns = {m: [] for m in modes}
+        rok = {m: True for m in modes}
+        for r in range(2):
+            for m in modes:
+                pl = pls[m]
+                st, dt, dmax, tim = timed(pl, lambda: pl.rebuild(rank_root, NT, VICTIM, ordered), before=drop_victim)
+                rok[m] = rok[m] and st.errors == 0 and st.tasks == len(lost)
+                rruns[m].append((dt, dmax, tim))
+                if r == 1:
+                    rok[m] = rok[m] and all(BS.read_file(BS.chunk_path(rank_root, VICTIM, files[i][0])) ==
+                                            chunk_of(i, files[i][1].index(VICTIM)).tobytes() for i in rsample)
 
+        def summary(m):
+            g, rb = runs[m], rruns[m]
+            warm = [x[1] for x in g[1:]] or [g[0][1]]
+            warm_own = [x[0] for x in g[1:]] or [g[0][0]]
+            return ({"read_mode": m, "cold_s": round(g[0][1], 4), "warm_s": round(float(np.median(warm)), 4),
+                     "runs_s": [round(x[1], 4) for x in g], "own_warm_s": round(float(np.median(warm_own)), 4),
+                     "timing": g[-1][2], "verified": ok[m]},
+                    {"read_mode": m, "cold_s": round(rb[0][1], 4), "warm_s": round(rb[-1][1], 4),
+                     "own_warm_s": round(rb[-1][0], 4), "timing": rb[-1][2], "verified": rok[m]})
+        per_mode = {m: summary(m) for m in modes}
+        gen, reb = per_mode[modes[0]]
         mine = {"rank": d.rank, "pci_bus_id": bus_id, **link, "stripes": nst, "bytes_read": rd, "bytes_written": wr,
                 "gen_own_warm_s": gen["own_warm_s"], "gen_GiBps": round((rd + wr) / gen["own_warm_s"] / GiB, 2),
                 "gen_input_over_link": round(rd / gen["own_warm_s"] / (link["h2d_GBps"] * 1e9), 3),
                 "rebuild_bytes_read": rd3, "rebuild_bytes_written": wr3, "rebuild_own_warm_s": reb["own_warm_s"],
-                "gen_verified": gen_ok, "rebuild_verified": rok, "store_write_s": round(t_store, 2)}
-        out = {"mine": mine, "gen": gen, "rebuild": reb}
+                "gen_verified": all(ok.values()), "rebuild_verified": all(rok.values()),
+                "store_write_s": round(t_store, 2),
+                "own_warm_s_by_mode": {m: [per_mode[m][0]["own_warm_s"], per_mode[m][1]["own_warm_s"]]
+                                       for m in modes}}
+        out = {"mine": mine, "per_mode": per_mode, "modes": modes}
     finally:
-        if pl is not None:
-            pl.close()
+        for p_ in pls.values():
+            p_.close()
         shutil.rmtree(rank_root, ignore_errors=True)
     ranks = d.gather(out.get("mine"))
     if d.rank != 0:
         return None
-    gen, reb = out["gen"], out["rebuild"]
+    modes = out["modes"]
     rd_all = sum(r["bytes_read"] for r in ranks)
     wr_all = sum(r["bytes_written"] for r in ranks)
     rd3_all = sum(r["rebuild_bytes_read"] for r in ranks)
     wr3_all = sum(r["rebuild_bytes_written"] for r in ranks)
     h2d_all = sum(r["h2d_GBps"] for r in ranks) * 1e9
+
+    def rates(m):
+        gen, reb = out["per_mode"][m]
+        return ({**gen, "bytes_read": rd_all, "bytes_written": wr_all,
+                 "GiBps": round((rd_all + wr_all) / gen["warm_s"] / GiB, 2),
+                 "input_GiBps": round(rd_all / gen["warm_s"] / GiB, 2),
+                 "input_over_link": round(rd_all / gen["warm_s"] / h2d_all, 3),
+                 "verified": all(r["gen_verified"] for r in ranks)},
+                {**reb, "target": VICTIM, "bytes_read": rd3_all, "bytes_written": wr3_all,
+                 "GiBps": round((rd3_all + wr3_all) / reb["warm_s"] / GiB, 2),
+                 "input_over_link": round(rd3_all / reb["warm_s"] / h2d_all, 3),
+                 "verified": all(r["rebuild_verified"] for r in ranks)})
+    by_mode = {m: rates(m) for m in modes}
+    gen, reb = by_mode[modes[0]]
     return {
         "path": ("bcp_pipeline_run / bcp_pipeline_rebuild on every rank's own GPU: chunk files (tmpfs) -> "
-                 "pinned slabs (io threads) -> H2D on a side queue -> xor_desc -> D2H on a side queue -> "
-                 "parity files / rebuilt chunks"),
-        "store": {"dir": a.e2e_dir, "shapes": "config 5: 8-wide stripes, chunks log-uniform 64 KiB-4 MiB, "
+                 "pinned slabs (io threads; read_mode map: part of every batch straight from the page cache) -> "
+                 "H2D on a side queue -> xor_desc -> D2H on a side queue -> parity files / rebuilt chunks"),
+        "store": {"dir": os.path.dirname(rank_root), "shapes": "config 5: 8-wide stripes, chunks log-uniform 64 KiB-4 MiB, "
                                               "9 targets, P rotating", "stripes_per_rank": ranks[0]["stripes"],
                   "chunk_GiB_per_rank": round(ranks[0]["bytes_read"] / GiB, 3)},
         "ranks": d.world,
-        "gen": {**gen, "bytes_read": rd_all, "bytes_written": wr_all,
-                "GiBps": round((rd_all + wr_all) / gen["warm_s"] / GiB, 2),
-                "input_GiBps": round(rd_all / gen["warm_s"] / GiB, 2),
-                "input_over_link": round(rd_all / gen["warm_s"] / h2d_all, 3),
-                "verified": all(r["gen_verified"] for r in ranks)},
-        "rebuild": {**reb, "target": VICTIM, "bytes_read": rd3_all, "bytes_written": wr3_all,
-                    "GiBps": round((rd3_all + wr3_all) / reb["warm_s"] / GiB, 2),
-                    "input_over_link": round(rd3_all / reb["warm_s"] / h2d_all, 3),
-                    "verified": all(r["rebuild_verified"] for r in ranks)},
+        "read_mode": modes[0],
+        "gen": gen,
+        "rebuild": reb,
+        "by_read_mode": {m: {"gen_GiBps": by_mode[m][0]["GiBps"], "gen_input_over_link": by_mode[m][0]["input_over_link"],
+                             "gen_warm_s": by_mode[m][0]["warm_s"], "rebuild_GiBps": by_mode[m][1]["GiBps"],
+                             "rebuild_warm_s": by_mode[m][1]["warm_s"],
+                             "mapped_bytes_last_gen": by_mode[m][0]["timing"].get("mapped_bytes")}
+                         for m in modes},
         "link_h2d_GBps_sum": round(h2d_all / 1e9, 2),
         "rate_note": "GiBps = (chunk bytes read + parity bytes written) of all ranks / the slowest rank's warm "
                      "run (median); input_over_link = input bytes / that time / the summed H2D rates the ranks "

@@ -96,6 +96,8 @@ def test_bench_gpus_n_launches_its_own_ranks(bcp, n):
     assert e2e["gen"]["verified"] is True and e2e["rebuild"]["verified"] is True
     assert e2e["gen"]["GiBps"] > 0 and e2e["rebuild"]["GiBps"] > 0
     assert e2e["gen"]["bytes_read"] == sum(r["bytes_read"] for r in e2e["per_rank"])
+    assert set(e2e["by_read_mode"]) == {"copy", "map"} and e2e["read_mode"] == "copy"
+    assert e2e["by_read_mode"]["map"]["mapped_bytes_last_gen"] > 0
     assert line["config"]["bytes_per_step_per_gpu"] * n * line["steps"] / 2**30 / (line["ms_per_step"] *
                                                                                    line["steps"] * 1e-3) == \
         pytest.approx(line["value"], rel=5e-3)  # value = the whole job's bytes / the slowest rank's time
