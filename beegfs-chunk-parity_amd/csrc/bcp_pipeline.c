@@ -224,12 +224,21 @@ typedef struct {
     bcp_event *ev_h, *ev_k, *ev_d;
     latch reads, writes;
     int busy;             /* writes of the previous batch pending */
-    /* MAP read mode: a reserved range of in_cap bytes the batch's mapped
-     * chunk files are placed in (PROT_NONE when idle) */
-    uint8_t *va;
-    size_t reg_lo, reg_len; /* registered part [reg_lo, reg_lo + reg_len) */
-    int mapped;
 } slot;
+
+/* MAP read mode: one batch's mapped tail -- a range of its own holding the
+ * chunk files (MAP_FIXED, read-only) and registered for the DMA engine.  A
+ * range lives until the run's end: hipHostUnregister waits for ALL work on
+ * the device (74.6 ms behind a 4 GiB copy against 0.001 ms for a register,
+ * profiles/r04/probe/unreg.jsonl), so unregistering at slot reuse would drain
+ * the pipeline every batch; the run unregisters them all once its queues are
+ * idle. */
+typedef struct {
+    bcp_engine *eng;
+    uint8_t *va;
+    size_t len;
+    int registered;
+} map_range;
 
 typedef struct {
     job j;
@@ -465,7 +474,7 @@ static void do_complete(job *p)
     }
 }
 
-static int slot_alloc(bcp_engine *e, slot *s, size_t in_cap, size_t out_cap, int map_mode)
+static int slot_alloc(bcp_engine *e, slot *s, size_t in_cap, size_t out_cap)
 {
     int rc;
     memset(s, 0, sizeof(*s));
@@ -476,34 +485,21 @@ static int slot_alloc(bcp_engine *e, slot *s, size_t in_cap, size_t out_cap, int
         return rc;
     s->in_cap = in_cap;
     s->out_cap = out_cap;
-    if (map_mode) {
-        void *va = mmap(NULL, in_cap, PROT_NONE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
-        if (va == MAP_FAILED)
-            return -errno;
-        s->va = va;
-    }
     return 0;
 }
 
-/* MAP mode: drop the slot's batch mappings (its H2D has finished: the
- * caller waited for the slot's writes, or synchronised the queues). */
-static void slot_unmap(bcp_engine *e, slot *s)
+/* The device no longer reads r (its queues were synchronised). */
+static void map_release(map_range *r)
 {
-    if (s->reg_len)
-        bcp_host_unregister(e, s->va + s->reg_lo);
-    s->reg_len = 0;
-    if (s->mapped) /* one call replaces every file mapping of the range */
-        (void)mmap(s->va, s->in_cap, PROT_NONE, MAP_FIXED | MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
-    s->mapped = 0;
+    if (r->registered)
+        bcp_host_unregister(r->eng, r->va);
+    if (r->va)
+        munmap(r->va, r->len);
+    memset(r, 0, sizeof(*r));
 }
 
 static void slot_free(bcp_engine *e, slot *s)
 {
-    if (s->va) {
-        slot_unmap(e, s);
-        munmap(s->va, s->in_cap);
-        s->va = NULL;
-    }
     bcp_host_free(e, s->h_in);
     bcp_host_free(e, s->h_out);
     bcp_dev_free(e, s->d_in);
@@ -527,6 +523,8 @@ struct bcp_pipeline {
     bcp_pipeline_opts o;
     int map_mode;       /* read_mode resolved: 1 = MAP */
     double map_share;   /* MAP: share of a batch's input bytes mapped (adapted per batch) */
+    map_range *maps;    /* MAP: this run's ranges (released at its end) */
+    size_t nmaps, maps_cap;
     int ndev;
     dev_lane *dev;
     pool readers, writers, completer;
@@ -583,12 +581,16 @@ int bcp_pipeline_destroy(bcp_pipeline *pl)
                 bcp_queue_destroy(L->qd);
             L->qh = L->qk = L->qd = NULL;
         }
+        for (size_t i = 0; i < pl->nmaps; i++) /* (a run releases its own; engines still live here) */
+            map_release(&pl->maps[i]);
+        pl->nmaps = 0;
         free_slots(pl);
         for (int d = 0; d < pl->ndev; d++)
             if (pl->dev[d].eng)
                 bcp_engine_destroy(pl->dev[d].eng);
         free(pl->dev);
     }
+    free(pl->maps);
     free(pl->st);
     free(pl->so);
     free(pl);
@@ -608,7 +610,7 @@ static int ensure_slots(bcp_pipeline *pl, size_t in_cap, size_t out_cap)
         if (!L->slots)
             return -ENOMEM;
         for (int s = 0; s < pl->o.nslots; s++) {
-            int rc = slot_alloc(L->eng, &L->slots[s], in_cap, out_cap, pl->map_mode);
+            int rc = slot_alloc(L->eng, &L->slots[s], in_cap, out_cap);
             if (rc)
                 return rc;
         }
@@ -713,13 +715,12 @@ static uint64_t data_off(const task *t, int k, int map_layout)
     return t->in_off[k] + (map_layout ? t->src_off[k] : 0);
 }
 
-/* MAP mode: place every source of tasks [a, b) in the slot's range (file
- * offset 0 at in_off, read-only, populated).  Returns 0, or -errno when a
- * file could not be opened or mapped (the caller reads the batch instead). */
-static int map_tasks(slot *S, const char *root, task *tasks, size_t a, size_t b)
+/* MAP mode: place every source of tasks [a, b) in va (file offset 0 at
+ * in_off - base, read-only, populated).  Returns 0, or -errno when a file
+ * could not be opened or mapped (the caller reads those tasks instead). */
+static int map_tasks(uint8_t *va, uint64_t base, const char *root, task *tasks, size_t a, size_t b)
 {
     char fn[4352];
-    S->mapped = 1;
     for (size_t i = a; i < b; i++) {
         task *t = &tasks[i];
         for (int k = 0; k < t->n; k++) {
@@ -731,7 +732,8 @@ static int map_tasks(slot *S, const char *root, task *tasks, size_t a, size_t b)
             int fd = open(fn, O_RDONLY);
             if (fd < 0)
                 return -errno;
-            void *m = mmap(S->va + t->in_off[k], (size_t)len, PROT_READ, MAP_SHARED | MAP_FIXED | MAP_POPULATE, fd, 0);
+            void *m = mmap(va + (t->in_off[k] - base), (size_t)len, PROT_READ, MAP_SHARED | MAP_FIXED | MAP_POPULATE,
+                           fd, 0);
             const int e = errno;
             close(fd);
             if (m == MAP_FAILED)
@@ -795,9 +797,28 @@ int bcp_pipeline_run(bcp_pipeline *pl, const char *store_root, int ntargets, con
 
 /* Stat, batch and stream the tasks through the slots (both modes).  Takes
  * no ownership of tasks. */
+/* MAP mode's per-run caps: the mappings stay registered (page-cache pages
+ * pinned) until the run ends, and each chunk file is a mapping of its own
+ * (vm.max_map_count is 65530 by default); past either cap the rest of the
+ * run is read. */
+#define MAP_RUN_BYTES_MAX ((uint64_t)64 << 30)
+#define MAP_RUN_FILES_MAX ((uint64_t)24576)
+
+static int grow_maps(bcp_pipeline *pl)
+{
+    const size_t cap = pl->maps_cap ? 2 * pl->maps_cap : 64;
+    map_range *m = realloc(pl->maps, cap * sizeof(map_range));
+    if (!m)
+        return -ENOMEM;
+    pl->maps = m;
+    pl->maps_cap = cap;
+    return 0;
+}
+
 static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, size_t nt, int corrupt_fd,
                          FILE *log, bcp_run_stats *stats, double t0)
 {
+    uint64_t run_map_bytes = 0, run_map_files = 0;
     const int nslots = pl->o.nslots;
     int rc = 0, errors = 0, dev_rc = 0;
     uint64_t bytes_read = 0, bytes_written = 0, ntasks = 0;
@@ -951,8 +972,6 @@ static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, 
             latch_destroy(&S->writes);
             S->busy = 0;
         }
-        if (S->mapped) /* its H2D ended before its D2H, before its writes */
-            slot_unmap(L->eng, S);
         tm.slot_wait += now_s() - tw;
         size_t last = first;
         while (last < nt && tasks[last].batch == b)
@@ -966,9 +985,11 @@ static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, 
             }
         /* MAP: the batch's tail tasks [split, last), about map_share of its
          * input bytes, are mapped by this thread while the io threads read
-         * the head into the slab */
+         * the head into the slab (within the run's caps on mapped bytes and
+         * mappings, which stay until the run's end) */
         size_t split = last;
-        if (ml && last > first) {
+        if (ml && last > first && run_map_bytes < MAP_RUN_BYTES_MAX && run_map_files < MAP_RUN_FILES_MAX &&
+            (pl->nmaps < pl->maps_cap || grow_maps(pl) == 0)) {
             const uint64_t from = in_used - (uint64_t)(pl->map_share * (double)in_used);
             split = first;
             while (split < last && tasks[split].in_off[0] < from)
@@ -990,23 +1011,38 @@ static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, 
         tm.read_jobs += (uint32_t)nreads;
         double map_s = 0;
         int mapped_ok = 0;
+        uint8_t *map_va = NULL;
         if (split < last) {
             const double tm0 = now_s();
-            int mrc = map_tasks(S, store_root, tasks, split, last);
-            if (!mrc && in_used > reg_lo) {
-                mrc = bcp_host_register_dma_src(L->eng, S->va + reg_lo, (size_t)(in_used - reg_lo));
+            const size_t map_len = (size_t)(in_used - reg_lo);
+            map_range *R = &pl->maps[pl->nmaps];
+            int mrc = 0;
+            void *va = mmap(NULL, map_len, PROT_NONE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
+            if (va == MAP_FAILED) {
+                mrc = -errno;
+            } else {
+                *R = (map_range){L->eng, va, map_len, 0};
+                pl->nmaps++;
+                mrc = map_tasks(va, reg_lo, store_root, tasks, split, last);
+                if (!mrc)
+                    mrc = bcp_host_register_dma_src(L->eng, va, map_len);
                 if (!mrc) {
-                    S->reg_lo = (size_t)reg_lo;
-                    S->reg_len = (size_t)(in_used - reg_lo);
+                    R->registered = 1;
+                    map_va = va;
+                } else { /* nothing registered: releasing it waits for nothing */
+                    map_release(R);
+                    pl->nmaps--;
                 }
             }
+            for (size_t i = split; i < last && !mrc; i++)
+                run_map_files += (uint64_t)tasks[i].n;
+            if (!mrc)
+                run_map_bytes += map_len;
             map_s = now_s() - tm0;
             tm.map += map_s;
             mapped_ok = !mrc;
-            if (!mapped_ok) {
-                slot_unmap(L->eng, S);
+            if (!mapped_ok)
                 tm.map_fallbacks++;
-            }
         }
         latch_wait(&S->reads);
         const double t_read_end = S->reads.t_zero;
@@ -1062,7 +1098,7 @@ static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, 
         }
         /* device: H2D (side queue; the slab's part, then the mapped part
          * straight out of the page cache) -> kernel -> D2H (side queue) */
-        const uint8_t *tail_src = (mapped_ok ? S->va : S->h_in) + reg_lo;
+        const uint8_t *tail_src = mapped_ok ? map_va : S->h_in + reg_lo;
         if ((reg_lo && (rc = bcp_h2d_async(L->qh, S->d_in, S->h_in, (size_t)reg_lo))) ||
             (in_used > reg_lo &&
              (rc = bcp_h2d_async(L->qh, (uint8_t *)S->d_in + reg_lo, tail_src, (size_t)(in_used - reg_lo)))) ||
@@ -1102,10 +1138,11 @@ static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, 
         const int s1 = bcp_queue_sync(L->qh), s2 = bcp_queue_sync(L->qk), s3 = bcp_queue_sync(L->qd);
         if (!rc && !dev_rc)
             dev_rc = s1 ? s1 : s2 ? s2 : s3;
-        for (int k = 0; k < nslots; k++) /* no mapping outlives the run */
-            if (L->slots[k].mapped)
-                slot_unmap(L->eng, &L->slots[k]);
     }
+    /* no mapping outlives the run (the queues are idle: cheap unregisters) */
+    for (size_t i = 0; i < pl->nmaps; i++)
+        map_release(&pl->maps[i]);
+    pl->nmaps = 0;
     /* every job has run: the writes latched above, the completions before them */
     free(ra);
     free(wa);

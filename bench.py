@@ -512,7 +512,8 @@ def e2e_leg(a, d, device: int, bus_id: str):
         "by_read_mode": {m: {"gen_GiBps": by_mode[m][0]["GiBps"], "gen_input_over_link": by_mode[m][0]["input_over_link"],
                              "gen_warm_s": by_mode[m][0]["warm_s"], "rebuild_GiBps": by_mode[m][1]["GiBps"],
                              "rebuild_warm_s": by_mode[m][1]["warm_s"],
-                             "mapped_bytes_last_gen": by_mode[m][0]["timing"].get("mapped_bytes")}
+                             "mapped_bytes_last_gen": by_mode[m][0]["timing"].get("mapped_bytes"),
+                             "gen_timing": by_mode[m][0]["timing"]}
                          for m in modes},
         "link_h2d_GBps_sum": round(h2d_all / 1e9, 2),
         "rate_note": "GiBps = (chunk bytes read + parity bytes written) of all ranks / the slowest rank's warm "

@@ -483,13 +483,15 @@ typedef struct {
 /* Read paths of the pipeline's input:
  *   COPY: io threads read() each chunk into the slot's pinned slab, one H2D
  *     per batch (page cache -> slab -> device: the CPU copies every byte);
- *   MAP:  a share of every batch is mmap'ed (MAP_FIXED, one reserved range per
- *     slot), registered read-only (bcp_host_register_dma_src) and copied to the
+ *   MAP:  a share of every batch is mmap'ed (MAP_FIXED into a range of its
+ *     own), registered read-only (bcp_host_register_dma_src) and copied to the
  *     device straight out of the page cache, while the io threads read the
  *     rest; the share follows the measured rates of the two (mapping and
- *     pinning is serial per process).  A batch whose mapping cannot be
- *     registered (a file truncated meanwhile) is read instead.  Input offsets
- *     are page-aligned in this mode.
+ *     pinning is serial per process).  The ranges stay registered until the
+ *     run ends (unregistering waits for the whole device), at most 64 GiB /
+ *     24,576 files per run, past which the run reads.  A batch whose mapping
+ *     cannot be registered (a file truncated meanwhile) is read instead.
+ *     Input offsets are page-aligned in this mode.
  *   AUTO (0): COPY; env BCP_PIPELINE_READ=copy|map overrides AUTO. */
 #define BCP_READ_AUTO 0
 #define BCP_READ_COPY 1
