@@ -226,19 +226,7 @@ typedef struct {
     int busy;             /* writes of the previous batch pending */
 } slot;
 
-/* MAP read mode: one batch's mapped tail -- a range of its own holding the
- * chunk files (MAP_FIXED, read-only) and registered for the DMA engine.  A
- * range lives until the run's end: hipHostUnregister waits for ALL work on
- * the device (74.6 ms behind a 4 GiB copy against 0.001 ms for a register,
- * profiles/r04/probe/unreg.jsonl), so unregistering at slot reuse would drain
- * the pipeline every batch; the run unregisters them all once its queues are
- * idle. */
-typedef struct {
-    bcp_engine *eng;
-    uint8_t *va;
-    size_t len;
-    int registered;
-} map_range;
+
 
 typedef struct {
     job j;
@@ -260,9 +248,27 @@ typedef struct {
     int *errors;
 } write_arg;
 
+/* MAP read mode: one batch's mapped tail -- a range of its own holding the
+ * chunk files (MAP_FIXED, read-only) and registered for the DMA engine.
+ * hipHostUnregister waits for ALL work on the device (74.6 ms behind a 4 GiB
+ * copy against 0.001 ms for a register, profiles/r04/probe/unreg.jsonl) but
+ * blocks only its caller (unreg_thread.jsonl): so a range is released by the
+ * pipeline's releaser thread once its batch's copies are done, never by the
+ * thread that submits. */
+typedef struct {
+    job j;                /* first: the releaser pool's link */
+    bcp_engine *eng;
+    uint8_t *va;
+    size_t len;
+    int registered;
+    int released;         /* set by whoever released it */
+} map_range;
+
 typedef struct {
     job j;
     slot *S;
+    map_range *map;       /* MAP: the batch's mapped range, or NULL */
+    pool *releaser;
     const char *root;
     task *tasks;
     write_arg *wa;        /* one per task of the run */
@@ -452,6 +458,13 @@ static void do_write(job *p)
 
 /* Completion stage (one thread, batches in order): wait for the batch's D2H,
  * then hand its parity files to the writer pool. */
+static void map_release(map_range *r);
+
+static void do_release(job *p)
+{
+    map_release((map_range *)p);
+}
+
 static void do_complete(job *p)
 {
     /* The run frees its job arrays once every write of the batch has counted
@@ -459,6 +472,8 @@ static void do_complete(job *p)
      * and touch neither `a` nor a pushed write job after handing it over. */
     const complete_arg a = *(complete_arg *)p;
     int rc = bcp_event_sync(a.S->ev_d);
+    if (a.map) /* its H2D is done: the releaser may unregister and unmap it */
+        pool_push(a.releaser, &a.map->j, do_release);
     if (rc) {
         pthread_mutex_lock(&g_stat_lock);
         *a.dev_rc = rc;
@@ -491,11 +506,15 @@ static int slot_alloc(bcp_engine *e, slot *s, size_t in_cap, size_t out_cap)
 /* The device no longer reads r (its queues were synchronised). */
 static void map_release(map_range *r)
 {
+    if (r->released)
+        return;
     if (r->registered)
         bcp_host_unregister(r->eng, r->va);
     if (r->va)
         munmap(r->va, r->len);
-    memset(r, 0, sizeof(*r));
+    r->registered = 0;
+    r->va = NULL;
+    r->released = 1;
 }
 
 static void slot_free(bcp_engine *e, slot *s)
@@ -523,8 +542,7 @@ struct bcp_pipeline {
     bcp_pipeline_opts o;
     int map_mode;       /* read_mode resolved: 1 = MAP */
     double map_share;   /* MAP: share of a batch's input bytes mapped (adapted per batch) */
-    map_range *maps;    /* MAP: this run's ranges (released at its end) */
-    size_t nmaps, maps_cap;
+    pool releaser;      /* MAP: releases the ranges (one thread) */
     int ndev;
     dev_lane *dev;
     pool readers, writers, completer;
@@ -566,6 +584,8 @@ int bcp_pipeline_destroy(bcp_pipeline *pl)
         pool_stop(&pl->readers);
     if (pl->pools & 4)
         pool_stop(&pl->completer);
+    if (pl->pools & 8)
+        pool_stop(&pl->releaser);
     if (pl->pools & 2)
         pool_stop(&pl->writers);
     if (pl->dev) {
@@ -581,16 +601,12 @@ int bcp_pipeline_destroy(bcp_pipeline *pl)
                 bcp_queue_destroy(L->qd);
             L->qh = L->qk = L->qd = NULL;
         }
-        for (size_t i = 0; i < pl->nmaps; i++) /* (a run releases its own; engines still live here) */
-            map_release(&pl->maps[i]);
-        pl->nmaps = 0;
         free_slots(pl);
         for (int d = 0; d < pl->ndev; d++)
             if (pl->dev[d].eng)
                 bcp_engine_destroy(pl->dev[d].eng);
         free(pl->dev);
     }
-    free(pl->maps);
     free(pl->st);
     free(pl->so);
     free(pl);
@@ -687,6 +703,11 @@ int bcp_pipeline_create(const bcp_pipeline_opts *opts_in, bcp_pipeline **out)
     if ((rc = pool_start(&pl->completer, 1)))
         goto fail;
     pl->pools |= 4;
+    if (pl->map_mode) {
+        if ((rc = pool_start(&pl->releaser, 1)))
+            goto fail;
+        pl->pools |= 8;
+    }
     if ((rc = ensure_slots(pl, o.slab_bytes, o.slab_bytes)))
         goto fail;
     *out = pl;
@@ -804,15 +825,26 @@ int bcp_pipeline_run(bcp_pipeline *pl, const char *store_root, int ntargets, con
 #define MAP_RUN_BYTES_MAX ((uint64_t)64 << 30)
 #define MAP_RUN_FILES_MAX ((uint64_t)24576)
 
-static int grow_maps(bcp_pipeline *pl)
+/* Wait until every release pushed so far has run (the pool is FIFO, one
+ * thread). */
+typedef struct {
+    job j;
+    latch *l;
+} mark_job;
+
+static void do_mark(job *p)
 {
-    const size_t cap = pl->maps_cap ? 2 * pl->maps_cap : 64;
-    map_range *m = realloc(pl->maps, cap * sizeof(map_range));
-    if (!m)
-        return -ENOMEM;
-    pl->maps = m;
-    pl->maps_cap = cap;
-    return 0;
+    latch_down(((mark_job *)p)->l);
+}
+
+static void releaser_drain(pool *P)
+{
+    latch l;
+    latch_init(&l, 1);
+    mark_job m = {{0}, &l};
+    pool_push(P, &m.j, do_mark);
+    latch_wait(&l);
+    latch_destroy(&l);
 }
 
 static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, size_t nt, int corrupt_fd,
@@ -944,12 +976,15 @@ static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, 
     read_arg *ra = calloc(nreads_all ? nreads_all : 1, sizeof(read_arg));
     write_arg *wa = calloc(nt ? nt : 1, sizeof(write_arg));
     complete_arg *cargs = calloc(nbatches ? (size_t)nbatches : 1, sizeof(complete_arg));
-    if (!ra || !wa || !cargs) {
+    map_range *maps = ml ? calloc(nbatches ? (size_t)nbatches : 1, sizeof(map_range)) : NULL;
+    if (!ra || !wa || !cargs || (ml && !maps)) {
         free(ra);
         free(wa);
         free(cargs);
+        free(maps);
         return -ENOMEM;
     }
+    size_t nmaps = 0;
     size_t rnext = 0;
     bcp_pipeline_timing tm = {0};
     tm.stat = now_s() - t_stat;
@@ -988,8 +1023,7 @@ static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, 
          * the head into the slab (within the run's caps on mapped bytes and
          * mappings, which stay until the run's end) */
         size_t split = last;
-        if (ml && last > first && run_map_bytes < MAP_RUN_BYTES_MAX && run_map_files < MAP_RUN_FILES_MAX &&
-            (pl->nmaps < pl->maps_cap || grow_maps(pl) == 0)) {
+        if (ml && last > first && run_map_bytes < MAP_RUN_BYTES_MAX && run_map_files < MAP_RUN_FILES_MAX) {
             const uint64_t from = in_used - (uint64_t)(pl->map_share * (double)in_used);
             split = first;
             while (split < last && tasks[split].in_off[0] < from)
@@ -1012,26 +1046,27 @@ static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, 
         double map_s = 0;
         int mapped_ok = 0;
         uint8_t *map_va = NULL;
+        map_range *batch_map = NULL;
         if (split < last) {
             const double tm0 = now_s();
             const size_t map_len = (size_t)(in_used - reg_lo);
-            map_range *R = &pl->maps[pl->nmaps];
+            map_range *R = &maps[nmaps];
             int mrc = 0;
             void *va = mmap(NULL, map_len, PROT_NONE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
             if (va == MAP_FAILED) {
                 mrc = -errno;
             } else {
-                *R = (map_range){L->eng, va, map_len, 0};
-                pl->nmaps++;
+                *R = (map_range){{0}, L->eng, va, map_len, 0, 0};
+                nmaps++;
                 mrc = map_tasks(va, reg_lo, store_root, tasks, split, last);
                 if (!mrc)
                     mrc = bcp_host_register_dma_src(L->eng, va, map_len);
                 if (!mrc) {
                     R->registered = 1;
                     map_va = va;
+                    batch_map = R;
                 } else { /* nothing registered: releasing it waits for nothing */
                     map_release(R);
-                    pl->nmaps--;
                 }
             }
             for (size_t i = split; i < last && !mrc; i++)
@@ -1113,7 +1148,8 @@ static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, 
         latch_init(&S->writes, (long)(last - first));
         S->busy = 1;
         complete_arg *ca = &cargs[b];
-        *ca = (complete_arg){{0}, S, store_root, tasks, wa, first, last, &pl->writers, log, &errors, &dev_rc};
+        *ca = (complete_arg){{0}, S, batch_map, &pl->releaser, store_root, tasks, wa, first, last, &pl->writers, log,
+                             &errors, &dev_rc};
         pool_push(&pl->completer, &ca->j, do_complete);
         for (size_t i = first; i < last; i++)
             bytes_written += (tasks[i].rebuild ? 0 : 8u * (uint64_t)tasks[i].n) + tasks[i].out_len;
@@ -1139,14 +1175,19 @@ static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, 
         if (!rc && !dev_rc)
             dev_rc = s1 ? s1 : s2 ? s2 : s3;
     }
-    /* no mapping outlives the run (the queues are idle: cheap unregisters) */
-    for (size_t i = 0; i < pl->nmaps; i++)
-        map_release(&pl->maps[i]);
-    pl->nmaps = 0;
+    /* no mapping outlives the run: the releaser's queue first (the
+     * completions that pushed to it have all run: their writes latched
+     * above), then whatever a failed submission left (the queues are idle) */
+    if (ml) {
+        releaser_drain(&pl->releaser);
+        for (size_t i = 0; i < nmaps; i++)
+            map_release(&maps[i]);
+    }
     /* every job has run: the writes latched above, the completions before them */
     free(ra);
     free(wa);
     free(cargs);
+    free(maps);
     tm.drain = now_s() - td;
     tm.read_mode = ml ? BCP_READ_MAP : BCP_READ_COPY;
     pl->last = tm;
