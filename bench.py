@@ -283,6 +283,33 @@ def cpu_baseline(a, N: int, C: int, lens_all) -> dict:
             "quota_cpus": None if quota is None else round(quota, 2), "cpu_model": model}
 
 
+def e2e_store_dir(dirs, world: int, want: int):
+    """(directory, bytes per rank, reason or None) for the ranks' end-to-end
+    stores: the first of dirs, then the temp dir, with room for every rank's
+    store (chunks + parity, ~35 % of the chunk bytes at config-5 shapes, + one
+    rebuilt target: 1.7x the chunk bytes), else the roomiest, the stores shrunk
+    to fit; a reason when not even 64 MiB per rank fit."""
+    import tempfile
+    base, room, reason = None, 0, None
+    for cand in dict.fromkeys(list(dirs) + [tempfile.gettempdir()]):
+        try:
+            stv = os.statvfs(cand)
+        except OSError as e:
+            reason = f"{cand}: {e}"
+            continue
+        r = int(stv.f_bavail * stv.f_frsize / (1.7 * world))
+        if r > room:
+            base, room = cand, r
+        if r >= want:
+            break
+    if base is None:
+        return dirs[0], 0, reason or "no directory for the stores"
+    want = min(want, room)
+    if want < (64 << 20):
+        return base, want, f"{base}: {room * 1.7 * world / GiB:.1f} GiB free for {world} stores"
+    return base, want, None
+
+
 def e2e_leg(a, d, device: int, bus_id: str):
     """End to end from chunk files, every rank on its own GPU at once: a store
     of config-5 shapes (8-wide stripes, chunk lengths log-uniform in
@@ -301,27 +328,8 @@ def e2e_leg(a, d, device: int, bus_id: str):
     import bcp_store as BS
     t_start = time.perf_counter()
     NT, W, VICTIM = 9, 8, 4
-    want = int(a.e2e_gib * GiB)
-    reason, base, room = None, None, 0
-    # the store's directory: --e2e-dir (tmpfs by default), else the temp dir,
-    # whichever has room for every rank's store (chunks + parity, ~35 % of the
-    # chunk bytes at these shapes, + one rebuilt target)
-    import tempfile
-    for cand in dict.fromkeys([a.e2e_dir, tempfile.gettempdir()]):
-        try:
-            stv = os.statvfs(cand)
-        except OSError as e:
-            reason = f"{cand}: {e}"
-            continue
-        r = int(stv.f_bavail * stv.f_frsize / (1.7 * d.world))
-        if r > room:
-            base, room = cand, r
-        if r >= want:
-            break
-    if base is not None:
-        want = min(want, room)
-        reason = None if want >= (64 << 20) else f"{base}: {room * 1.7 * d.world / GiB:.1f} GiB free for {d.world} stores"
-    rank_root = os.path.join(base or a.e2e_dir, f"bcp_bench_e2e_{os.getppid()}_{d.rank}")
+    base, want, reason = e2e_store_dir([a.e2e_dir], d.world, int(a.e2e_gib * GiB))
+    rank_root = os.path.join(base, f"bcp_bench_e2e_{os.getppid()}_{d.rank}")
     # every rank agrees to run (or not): a rank that skipped would leave the
     # others waiting at the barriers below
     if d.sum(0.0 if reason else 1.0) != d.world:

@@ -160,3 +160,28 @@ def test_launcher_parent_never_imports_torch():
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=env, capture_output=True, text=True, timeout=100)
     assert "RC 4 TORCH False LIB False" in r.stdout, (r.stdout, r.stderr[-2000:])
+
+
+def test_e2e_store_dir_fits_every_rank(tmp_path, monkeypatch):
+    """The end-to-end stores go where every rank's store fits: the asked
+    directory, else the temp dir, else the roomiest, shrunk; a reason when
+    nothing fits."""
+    import collections
+    sys.path.insert(0, ROOT)
+    import bench
+    GiB = 1 << 30
+    free = {"/shm": 3 * GiB, "/tmpdir": 100 * GiB}
+    St = collections.namedtuple("St", "f_bavail f_frsize")
+    monkeypatch.setattr(os, "statvfs", lambda p: St(free[p] // 4096, 4096) if p in free else (_ for _ in ()).throw(
+        FileNotFoundError(p)))
+    import tempfile
+    monkeypatch.setattr(tempfile, "gettempdir", lambda: "/tmpdir")
+    assert bench.e2e_store_dir(["/shm"], 1, 1 * GiB) == ("/shm", 1 * GiB, None)
+    base, want, why = bench.e2e_store_dir(["/shm"], 8, 2 * GiB)   # 8 x 2 GiB x 1.7 > 3 GiB
+    assert base == "/tmpdir" and want == 2 * GiB and why is None
+    free["/tmpdir"] = 1 * GiB
+    base, want, why = bench.e2e_store_dir(["/shm"], 8, 2 * GiB)   # neither fits: the roomiest, shrunk
+    assert base == "/shm" and want == int(3 * GiB / (1.7 * 8)) and why is None
+    free["/shm"] = free["/tmpdir"] = 16 << 20
+    assert bench.e2e_store_dir(["/shm"], 8, 2 * GiB)[2] is not None
+    assert bench.e2e_store_dir(["/absent"], 1, GiB)[0] == "/tmpdir"

@@ -206,7 +206,9 @@ int main(int argc, char **argv) {
     }
   }
 
-  // ---- one region of MAP_FIXED file mappings, registered once
+  // ---- one region of MAP_FIXED file mappings, registered once (populated
+  // by mmap, or -- pop 0 -- faulted in by the registration itself)
+  for (int pop : {1, 0})
   for (unsigned fl : flagsets) {
     for (int r = 0; r < reps; r++) {
       CK(hipMemset(dev, 0, total));
@@ -216,7 +218,7 @@ int main(int argc, char **argv) {
       for (int i = 0; i < g_F; i++) {
         fname(fn, sizeof fn, i);
         int fd = open(fn, O_RDONLY);
-        void *m = mmap(base + (size_t)i * g_S, g_S, PROT_READ, MAP_SHARED | MAP_FIXED | MAP_POPULATE, fd, 0);
+        void *m = mmap(base + (size_t)i * g_S, g_S, PROT_READ, MAP_SHARED | MAP_FIXED | (pop ? MAP_POPULATE : 0), fd, 0);
         close(fd);
         if (m == MAP_FAILED) mfail++;
       }
@@ -238,10 +240,10 @@ int main(int argc, char **argv) {
       }
       munmap(base, total);
       double t5 = now();
-      printf("{\"variant\":\"region_register\",\"flags\":%u,\"files\":%d,\"mmap_s\":%.5f,\"reg_s\":%.5f,"
+      printf("{\"variant\":\"region_register\",\"populate\":%d,\"flags\":%u,\"files\":%d,\"mmap_s\":%.5f,\"reg_s\":%.5f,"
              "\"h2d_s\":%.5f,\"h2d_GBps\":%.2f,\"unreg_s\":%.5f,\"munmap_s\":%.5f,\"total_GBps\":%.2f,"
              "\"map_fail\":%d,\"reg_rc\":%d,\"ok\":%d}\n",
-             fl, g_F, t1 - t0, t2 - t1, t3 - t2, e == hipSuccess ? total / (t3 - t2) / 1e9 : 0.0, t4 - t3, t5 - t4,
+             pop, fl, g_F, t1 - t0, t2 - t1, t3 - t2, e == hipSuccess ? total / (t3 - t2) / 1e9 : 0.0, t4 - t3, t5 - t4,
              e == hipSuccess ? total / (t5 - t0) / 1e9 : 0.0, mfail, (int)e, ok);
       fflush(stdout);
     }
