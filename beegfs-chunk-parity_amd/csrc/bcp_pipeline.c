@@ -260,6 +260,8 @@ typedef struct {
     bcp_engine *eng;
     uint8_t *va;
     size_t len;
+    uint64_t nfiles;
+    uint64_t *out;        /* the run's outstanding {bytes, mappings}, decremented on release */
     int registered;
     int released;         /* set by whoever released it */
 } map_range;
@@ -512,8 +514,13 @@ static void map_release(map_range *r)
         bcp_host_unregister(r->eng, r->va);
     if (r->va)
         munmap(r->va, r->len);
+    if (r->out) {
+        __atomic_sub_fetch(&r->out[0], (uint64_t)r->len, __ATOMIC_RELAXED);
+        __atomic_sub_fetch(&r->out[1], r->nfiles, __ATOMIC_RELAXED);
+    }
     r->registered = 0;
     r->va = NULL;
+    r->out = NULL;
     r->released = 1;
 }
 
@@ -818,12 +825,12 @@ int bcp_pipeline_run(bcp_pipeline *pl, const char *store_root, int ntargets, con
 
 /* Stat, batch and stream the tasks through the slots (both modes).  Takes
  * no ownership of tasks. */
-/* MAP mode's per-run caps: the mappings stay registered (page-cache pages
- * pinned) until the run ends, and each chunk file is a mapping of its own
- * (vm.max_map_count is 65530 by default); past either cap the rest of the
- * run is read. */
-#define MAP_RUN_BYTES_MAX ((uint64_t)64 << 30)
-#define MAP_RUN_FILES_MAX ((uint64_t)24576)
+/* MAP mode's caps on what is mapped at once: registered ranges pin their
+ * page-cache pages until the releaser gets to them, and each chunk file is a
+ * mapping of its own (vm.max_map_count is 65530 by default); at either cap a
+ * batch is read instead. */
+#define MAP_OUT_BYTES_MAX ((uint64_t)16 << 30)
+#define MAP_OUT_FILES_MAX ((uint64_t)24576)
 
 /* Wait until every release pushed so far has run (the pool is FIFO, one
  * thread). */
@@ -850,7 +857,7 @@ static void releaser_drain(pool *P)
 static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, size_t nt, int corrupt_fd,
                          FILE *log, bcp_run_stats *stats, double t0)
 {
-    uint64_t run_map_bytes = 0, run_map_files = 0;
+    uint64_t map_out[2] = {0, 0}; /* outstanding mapped bytes, mappings (the releaser decrements) */
     const int nslots = pl->o.nslots;
     int rc = 0, errors = 0, dev_rc = 0;
     uint64_t bytes_read = 0, bytes_written = 0, ntasks = 0;
@@ -1020,10 +1027,10 @@ static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, 
             }
         /* MAP: the batch's tail tasks [split, last), about map_share of its
          * input bytes, are mapped by this thread while the io threads read
-         * the head into the slab (within the run's caps on mapped bytes and
-         * mappings, which stay until the run's end) */
+         * the head into the slab (within the caps on what is mapped at once) */
         size_t split = last;
-        if (ml && last > first && run_map_bytes < MAP_RUN_BYTES_MAX && run_map_files < MAP_RUN_FILES_MAX) {
+        if (ml && last > first && __atomic_load_n(&map_out[0], __ATOMIC_RELAXED) < MAP_OUT_BYTES_MAX &&
+            __atomic_load_n(&map_out[1], __ATOMIC_RELAXED) < MAP_OUT_FILES_MAX) {
             const uint64_t from = in_used - (uint64_t)(pl->map_share * (double)in_used);
             split = first;
             while (split < last && tasks[split].in_off[0] < from)
@@ -1056,7 +1063,12 @@ static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, 
             if (va == MAP_FAILED) {
                 mrc = -errno;
             } else {
-                *R = (map_range){{0}, L->eng, va, map_len, 0, 0};
+                uint64_t nf = 0;
+                for (size_t i = split; i < last; i++)
+                    nf += (uint64_t)tasks[i].n;
+                *R = (map_range){{0}, L->eng, va, map_len, nf, map_out, 0, 0};
+                __atomic_add_fetch(&map_out[0], (uint64_t)map_len, __ATOMIC_RELAXED);
+                __atomic_add_fetch(&map_out[1], nf, __ATOMIC_RELAXED);
                 nmaps++;
                 mrc = map_tasks(va, reg_lo, store_root, tasks, split, last);
                 if (!mrc)
@@ -1069,10 +1081,6 @@ static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, 
                     map_release(R);
                 }
             }
-            for (size_t i = split; i < last && !mrc; i++)
-                run_map_files += (uint64_t)tasks[i].n;
-            if (!mrc)
-                run_map_bytes += map_len;
             map_s = now_s() - tm0;
             tm.map += map_s;
             mapped_ok = !mrc;

@@ -487,10 +487,12 @@ typedef struct {
  *     own), registered read-only (bcp_host_register_dma_src) and copied to the
  *     device straight out of the page cache, while the io threads read the
  *     rest; the share follows the measured rates of the two (mapping and
- *     pinning is serial per process).  The ranges stay registered until the
- *     run ends (unregistering waits for the whole device), at most 64 GiB /
- *     24,576 files per run, past which the run reads.  A batch whose mapping
- *     cannot be registered (a file truncated meanwhile) is read instead.
+ *     pinning is serial per process).  A releaser thread unregisters and
+ *     unmaps each batch's range once its copy is done (unregistering waits
+ *     for the whole device, so the submitting thread never does it); at most
+ *     16 GiB / 24,576 files are mapped at once, beyond which batches are read.
+ *     A batch whose mapping cannot be registered (a file truncated meanwhile)
+ *     is read instead.
  *     Input offsets are page-aligned in this mode.
  *   AUTO (0): COPY; env BCP_PIPELINE_READ=copy|map overrides AUTO. */
 #define BCP_READ_AUTO 0
