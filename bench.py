@@ -320,7 +320,10 @@ def e2e_leg(a, d, device: int, bus_id: str):
     pipeline's read paths of --e2e-modes, interleaved (the first is the
     headline `gen` / `rebuild`, the others in `by_read_mode`).  The reference's
     I/O path: task_processing.c:62-79,186,199-226 (read, fold, write).
-    Returns the rank-0 summary (None elsewhere); never part of `value`."""
+    Returns the rank-0 summary (None elsewhere); never part of `value`.
+    A failure on any rank is reported in the block (`errors`), never raised:
+    every rank keeps making the same collective calls, so the bench line of
+    the device-resident measurement is printed whatever happens here."""
     import concurrent.futures as cf
     import shutil
 
@@ -328,6 +331,7 @@ def e2e_leg(a, d, device: int, bus_id: str):
     import bcp_store as BS
     t_start = time.perf_counter()
     NT, W, VICTIM = 9, 8, 4
+    modes = [m for m in a.e2e_modes.split(",") if m in ("copy", "map")] or ["copy"]
     base, want, reason = e2e_store_dir([a.e2e_dir], d.world, int(a.e2e_gib * GiB))
     rank_root = os.path.join(base, f"bcp_bench_e2e_{os.getppid()}_{d.rank}")
     # every rank agrees to run (or not): a rank that skipped would leave the
@@ -336,6 +340,15 @@ def e2e_leg(a, d, device: int, bus_id: str):
         if d.rank == 0:
             return {"skipped": reason or "another rank could not create its store"}
         return None
+    errors = []
+
+    def guard(what, fn, default=None):
+        try:
+            return fn()
+        except Exception as e:  # reported in the block, never raised (see above)
+            errors.append(f"{what}: {type(e).__name__}: {e}")
+            return default
+
     rng = np.random.default_rng(5 + d.rank)
     lens, tot = [], 0
     while tot < want:
@@ -348,171 +361,195 @@ def e2e_leg(a, d, device: int, bus_id: str):
     for i in range(nst):
         p = i % NT
         files.append((f"e2e/{i % 64:02x}/chunk{i}", [t for t in range(NT) if t != p], p))
+    ts = int(time.time()) + 3600
+    items = [(path, ts, BS.with_p(sum(1 << h for h in hs), p)) for path, hs, p in files]
+    rd = int(sum(int(x.sum()) for x in lens))
+    wr = int(sum(8 * W + int(x.max()) for x in lens))
+    lost = [i for i in range(nst) if VICTIM in files[i][1]]
+    ordered = sorted(items, key=lambda x: x[0].encode())  # DB key order (rebuild/main.c:223-225)
+    rd3 = sum(int(lens[i].sum()) - int(lens[i][files[i][1].index(VICTIM)]) + int(lens[i].max()) + 8 * W
+              for i in lost)
+    wr3 = sum(int(lens[i][files[i][1].index(VICTIM)]) for i in lost)
+    vr = np.random.default_rng(11 + d.rank)
+    sample = sorted({0, nst - 1} | {int(x) for x in vr.integers(0, nst, 6)})
+    rsample = [i for i in sample if i in set(lost)] or lost[:2]
 
     def chunk_of(i, k):
         off = ((i * W + k) * 40961) % (8 << 20)
         return block[off:off + int(lens[i][k])]
 
-    def write_stripe(i):
-        path, holders, _ = files[i]
-        for k, h in enumerate(holders):
-            fn = BS.chunk_path(rank_root, h, path)
-            os.makedirs(os.path.dirname(fn), exist_ok=True)
-            with open(fn, "wb") as f:
-                f.write(memoryview(chunk_of(i, k)))
-
-    out = {}
-    pls = {}
-    try:
+    def write_store():
+        if os.environ.get("BCP_BENCH_E2E_FAIL_RANK") == str(d.rank):  # test hook: a rank whose store fails
+            raise OSError(f"injected store failure on rank {d.rank}")
         shutil.rmtree(rank_root, ignore_errors=True)
         BS.make_store(rank_root, NT)
+
+        def write_stripe(i):
+            path, holders, _ = files[i]
+            for k, h in enumerate(holders):
+                fn = BS.chunk_path(rank_root, h, path)
+                os.makedirs(os.path.dirname(fn), exist_ok=True)
+                with open(fn, "wb") as f:
+                    f.write(memoryview(chunk_of(i, k)))
         t0 = time.perf_counter()
         with cf.ThreadPoolExecutor(8) as ex:
             list(ex.map(write_stripe, range(nst)))
-        t_store = time.perf_counter() - t0
-        ts = int(time.time()) + 3600
-        items = [(path, ts, BS.with_p(sum(1 << h for h in hs), p)) for path, hs, p in files]
-        rd = int(sum(int(x.sum()) for x in lens))
-        wr = int(sum(8 * W + int(x.max()) for x in lens))
-        # the H2D / D2H link of this rank's GPU, measured by every rank at once
+        return time.perf_counter() - t0
+
+    def link_rates():
+        """This rank's H2D / D2H over pinned memory (every rank at once)."""
         eng = bcp.Engine(device)
         q = eng.queue()
         nb = 256 << 20
         h = eng.host_alloc(nb)
         dv = eng.alloc(nb)
-        link = {}
+        out = {}
+        try:
+            for name, fn in (("h2d_GBps", lambda: q.h2d(dv, h, nb)), ("d2h_GBps", lambda: q.d2h(h, dv, nb))):
+                tt = []
+                for _ in range(5):
+                    q.sync()
+                    t0 = time.perf_counter()
+                    fn()
+                    q.sync()
+                    tt.append(time.perf_counter() - t0)
+                out[name] = round(nb / float(np.median(tt)) / 1e9, 2)
+        finally:
+            q.sync()
+            eng.free(dv)
+            eng.host_free(h)
+            q.close()
+            eng.close()
+        return out
+
+    def parity_ok(i):
+        ch = [chunk_of(i, k) for k in range(W)]
+        m = max(len(c) for c in ch)
+        body = np.zeros(m, dtype=np.uint8)
+        for c in ch:
+            body[:len(c)] ^= c
+        want_file = np.asarray([len(c) for c in ch], dtype="<u8").tobytes() + body.tobytes()
+        return BS.read_file(BS.parity_path(rank_root, files[i][2], files[i][0])) == want_file
+
+    def rebuilt_ok(i):
+        return BS.read_file(BS.chunk_path(rank_root, VICTIM, files[i][0])) == \
+            chunk_of(i, files[i][1].index(VICTIM)).tobytes()
+
+    def drop_victim():
+        with cf.ThreadPoolExecutor(8) as ex:
+            list(ex.map(lambda i: os.remove(BS.chunk_path(rank_root, VICTIM, files[i][0])), lost))
+
+    pls = {}
+    runs = {m: [] for m in modes}
+    rruns = {m: [] for m in modes}
+    ok = {m: True for m in modes}
+    rok = {m: True for m in modes}
+
+    def timed(m, what, before=None):
+        """One run of mode m on every rank at once: (own s, slowest rank's s, timing)."""
+        pl = pls.get(m)
+        if before and pl is not None:
+            guard("delete the lost target", before)
         d.barrier()
-        for name, fn in (("h2d_GBps", lambda: q.h2d(dv, h, nb)), ("d2h_GBps", lambda: q.d2h(h, dv, nb))):
-            tt = []
-            for _ in range(5):
-                q.sync()
-                t0 = time.perf_counter()
-                fn()
-                q.sync()
-                tt.append(time.perf_counter() - t0)
-            link[name] = round(nb / float(np.median(tt)) / 1e9, 2)
-        eng.free(dv)
-        eng.host_free(h)
-        q.close()
-        eng.close()
-        modes = [m for m in a.e2e_modes.split(",") if m]
-        pls = {m: bcp.Pipeline(device=device, read_mode={"copy": bcp.READ_COPY, "map": bcp.READ_MAP}[m])
-               for m in modes}
+        t0 = time.perf_counter()
+        st = guard(f"{what} ({m})", (lambda: pl.run(rank_root, NT, items)) if what == "gen" else
+                   (lambda: pl.rebuild(rank_root, NT, VICTIM, ordered))) if pl is not None else None
+        dt = time.perf_counter() - t0
+        dmax = d.max(dt)
+        tim = guard("timing", pl.last_timing, {}) if pl is not None else {}
+        good = st is not None and st.errors == 0 and st.tasks == (nst if what == "gen" else len(lost))
+        if what == "gen":
+            good = good and st.bytes_read == rd
+        return (dt, dmax, tim), good
 
-        def timed(pl, fn, before=None):
-            if before:
-                before()
-            d.barrier()
-            t0 = time.perf_counter()
-            st = fn()
-            dt = time.perf_counter() - t0
-            return st, dt, d.max(dt), pl.last_timing()
-
-        vr = np.random.default_rng(11 + d.rank)
-        sample = sorted({0, nst - 1} | {int(x) for x in vr.integers(0, nst, 6)})
-
-        def parity_ok(i):
-            ch = [chunk_of(i, k) for k in range(W)]
-            m = max(len(c) for c in ch)
-            body = np.zeros(m, dtype=np.uint8)
-            for c in ch:
-                body[:len(c)] ^= c
-            want_file = np.asarray([len(c) for c in ch], dtype="<u8").tobytes() + body.tobytes()
-            return BS.read_file(BS.parity_path(rank_root, files[i][2], files[i][0])) == want_file
-
+    try:
+        t_store = guard("writing the store", write_store, 0.0)
+        d.barrier()
+        link = guard("link probe", link_rates, {}) or {}
+        for m in modes:
+            pl = guard(f"pipeline ({m})", lambda: bcp.Pipeline(
+                device=device, read_mode={"copy": bcp.READ_COPY, "map": bcp.READ_MAP}[m]))
+            if pl is not None:
+                pls[m] = pl
         # ---- gen: one cold run, then warm runs, the read paths interleaved
-        runs = {m: [] for m in modes}
-        ok = {m: True for m in modes}
         nrep = 1 + max(1, a.e2e_reps)
         for r in range(nrep):
             last_rep = r == nrep - 1 or (r > 1 and d.max(time.perf_counter() - t_start) > a.e2e_max_s)
             for m in modes:
-                pl = pls[m]
-                st, dt, dmax, tim = timed(pl, lambda: pl.run(rank_root, NT, items))
-                ok[m] = ok[m] and st.errors == 0 and st.tasks == nst and st.bytes_read == rd
-                runs[m].append((dt, dmax, tim))
+                res, good = timed(m, "gen")
+                runs[m].append(res)
+                ok[m] = ok[m] and good
                 if last_rep:  # this mode's files, checked before the next mode rewrites them
-                    ok[m] = ok[m] and all(parity_ok(i) for i in sample)
+                    ok[m] = ok[m] and bool(guard("checking parity", lambda: all(parity_ok(i) for i in sample)))
             if last_rep:
                 break
-
         # ---- rebuild target VICTIM from 7 survivors + parity, each read path
-        lost = [i for i in range(nst) if VICTIM in files[i][1]]
-        ordered = sorted(items, key=lambda x: x[0].encode())  # DB key order (rebuild/main.c:223-225)
-        rd3 = sum(int(lens[i].sum()) - int(lens[i][files[i][1].index(VICTIM)]) + int(lens[i].max()) + 8 * W
-                  for i in lost)
-        wr3 = sum(int(lens[i][files[i][1].index(VICTIM)]) for i in lost)
-
-        def drop_victim():
-            with cf.ThreadPoolExecutor(8) as ex:
-                list(ex.map(lambda i: os.remove(BS.chunk_path(rank_root, VICTIM, files[i][0])), lost))
-        rsample = [i for i in sample if i in set(lost)] or lost[:2]
-        rruns = {m: [] for m in modes}
-        rok = {m: True for m in modes}
         for r in range(2):
             for m in modes:
-                pl = pls[m]
-                st, dt, dmax, tim = timed(pl, lambda: pl.rebuild(rank_root, NT, VICTIM, ordered), before=drop_victim)
-                rok[m] = rok[m] and st.errors == 0 and st.tasks == len(lost)
-                rruns[m].append((dt, dmax, tim))
+                res, good = timed(m, "rebuild", before=drop_victim)
+                rruns[m].append(res)
+                rok[m] = rok[m] and good
                 if r == 1:
-                    rok[m] = rok[m] and all(BS.read_file(BS.chunk_path(rank_root, VICTIM, files[i][0])) ==
-                                            chunk_of(i, files[i][1].index(VICTIM)).tobytes() for i in rsample)
-
-        def summary(m):
-            g, rb = runs[m], rruns[m]
-            warm = [x[1] for x in g[1:]] or [g[0][1]]
-            warm_own = [x[0] for x in g[1:]] or [g[0][0]]
-            return ({"read_mode": m, "cold_s": round(g[0][1], 4), "warm_s": round(float(np.median(warm)), 4),
-                     "runs_s": [round(x[1], 4) for x in g], "own_warm_s": round(float(np.median(warm_own)), 4),
-                     "timing": g[-1][2], "verified": ok[m]},
-                    {"read_mode": m, "cold_s": round(rb[0][1], 4), "warm_s": round(rb[-1][1], 4),
-                     "own_warm_s": round(rb[-1][0], 4), "timing": rb[-1][2], "verified": rok[m]})
-        per_mode = {m: summary(m) for m in modes}
-        gen, reb = per_mode[modes[0]]
-        mine = {"rank": d.rank, "pci_bus_id": bus_id, **link, "stripes": nst, "bytes_read": rd, "bytes_written": wr,
-                "gen_own_warm_s": gen["own_warm_s"], "gen_GiBps": round((rd + wr) / gen["own_warm_s"] / GiB, 2),
-                "gen_input_over_link": round(rd / gen["own_warm_s"] / (link["h2d_GBps"] * 1e9), 3),
-                "rebuild_bytes_read": rd3, "rebuild_bytes_written": wr3, "rebuild_own_warm_s": reb["own_warm_s"],
-                "gen_verified": all(ok.values()), "rebuild_verified": all(rok.values()),
-                "store_write_s": round(t_store, 2),
-                "own_warm_s_by_mode": {m: [per_mode[m][0]["own_warm_s"], per_mode[m][1]["own_warm_s"]]
-                                       for m in modes}}
-        out = {"mine": mine, "per_mode": per_mode, "modes": modes}
+                    rok[m] = rok[m] and bool(guard("checking rebuilt chunks",
+                                                   lambda: all(rebuilt_ok(i) for i in rsample)))
     finally:
         for p_ in pls.values():
-            p_.close()
+            guard("closing a pipeline", p_.close)
         shutil.rmtree(rank_root, ignore_errors=True)
-    ranks = d.gather(out.get("mine"))
+
+    def summary(m):
+        g, rb = runs[m], rruns[m]
+        warm = [x[1] for x in g[1:]] or [g[0][1]]
+        warm_own = [x[0] for x in g[1:]] or [g[0][0]]
+        return ({"read_mode": m, "cold_s": round(g[0][1], 4), "warm_s": round(float(np.median(warm)), 4),
+                 "runs_s": [round(x[1], 4) for x in g], "own_warm_s": round(float(np.median(warm_own)), 4),
+                 "timing": g[-1][2], "verified": ok[m]},
+                {"read_mode": m, "cold_s": round(rb[0][1], 4), "warm_s": round(rb[-1][1], 4),
+                 "own_warm_s": round(rb[-1][0], 4), "timing": rb[-1][2], "verified": rok[m]})
+    per_mode = {m: summary(m) for m in modes}
+    gen, reb = per_mode[modes[0]]
+    mine = {"rank": d.rank, "pci_bus_id": bus_id, **link, "stripes": nst, "bytes_read": rd, "bytes_written": wr,
+            "gen_own_warm_s": gen["own_warm_s"], "gen_GiBps": round((rd + wr) / gen["own_warm_s"] / GiB, 2),
+            "gen_input_over_link": (round(rd / gen["own_warm_s"] / (link["h2d_GBps"] * 1e9), 3)
+                                    if link.get("h2d_GBps") else None),
+            "rebuild_bytes_read": rd3, "rebuild_bytes_written": wr3, "rebuild_own_warm_s": reb["own_warm_s"],
+            "gen_verified": all(ok.values()), "rebuild_verified": all(rok.values()),
+            "store_write_s": round(t_store, 2),
+            "own_warm_s_by_mode": {m: [per_mode[m][0]["own_warm_s"], per_mode[m][1]["own_warm_s"]] for m in modes},
+            "errors": errors or None}
+    ranks = d.gather(mine)
     if d.rank != 0:
         return None
-    modes = out["modes"]
     rd_all = sum(r["bytes_read"] for r in ranks)
     wr_all = sum(r["bytes_written"] for r in ranks)
     rd3_all = sum(r["rebuild_bytes_read"] for r in ranks)
     wr3_all = sum(r["rebuild_bytes_written"] for r in ranks)
-    h2d_all = sum(r["h2d_GBps"] for r in ranks) * 1e9
+    h2d_all = sum(r.get("h2d_GBps") or 0.0 for r in ranks) * 1e9
+    all_errors = {r["rank"]: r["errors"] for r in ranks if r.get("errors")}
+
+    def over_link(b, t):
+        return round(b / t / h2d_all, 3) if h2d_all > 0 and not all_errors else None
 
     def rates(m):
-        gen, reb = out["per_mode"][m]
+        gen, reb = per_mode[m]
         return ({**gen, "bytes_read": rd_all, "bytes_written": wr_all,
                  "GiBps": round((rd_all + wr_all) / gen["warm_s"] / GiB, 2),
                  "input_GiBps": round(rd_all / gen["warm_s"] / GiB, 2),
-                 "input_over_link": round(rd_all / gen["warm_s"] / h2d_all, 3),
-                 "verified": all(r["gen_verified"] for r in ranks)},
+                 "input_over_link": over_link(rd_all, gen["warm_s"]),
+                 "verified": all(r["gen_verified"] for r in ranks) and not all_errors},
                 {**reb, "target": VICTIM, "bytes_read": rd3_all, "bytes_written": wr3_all,
                  "GiBps": round((rd3_all + wr3_all) / reb["warm_s"] / GiB, 2),
-                 "input_over_link": round(rd3_all / reb["warm_s"] / h2d_all, 3),
-                 "verified": all(r["rebuild_verified"] for r in ranks)})
+                 "input_over_link": over_link(rd3_all, reb["warm_s"]),
+                 "verified": all(r["rebuild_verified"] for r in ranks) and not all_errors})
     by_mode = {m: rates(m) for m in modes}
     gen, reb = by_mode[modes[0]]
     return {
         "path": ("bcp_pipeline_run / bcp_pipeline_rebuild on every rank's own GPU: chunk files (tmpfs) -> "
                  "pinned slabs (io threads; read_mode map: part of every batch straight from the page cache) -> "
                  "H2D on a side queue -> xor_desc -> D2H on a side queue -> parity files / rebuilt chunks"),
-        "store": {"dir": os.path.dirname(rank_root), "shapes": "config 5: 8-wide stripes, chunks log-uniform 64 KiB-4 MiB, "
-                                              "9 targets, P rotating", "stripes_per_rank": ranks[0]["stripes"],
-                  "chunk_GiB_per_rank": round(ranks[0]["bytes_read"] / GiB, 3)},
+        "store": {"dir": os.path.dirname(rank_root), "shapes": "config 5: 8-wide stripes, chunks log-uniform "
+                                                               "64 KiB-4 MiB, 9 targets, P rotating",
+                  "stripes_per_rank": ranks[0]["stripes"], "chunk_GiB_per_rank": round(ranks[0]["bytes_read"] / GiB, 3)},
         "ranks": d.world,
         "read_mode": modes[0],
         "gen": gen,
@@ -524,13 +561,13 @@ def e2e_leg(a, d, device: int, bus_id: str):
                              "gen_timing": by_mode[m][0]["timing"]}
                          for m in modes},
         "link_h2d_GBps_sum": round(h2d_all / 1e9, 2),
+        "errors": all_errors or None,
         "rate_note": "GiBps = (chunk bytes read + parity bytes written) of all ranks / the slowest rank's warm "
                      "run (median); input_over_link = input bytes / that time / the summed H2D rates the ranks "
                      "measured together over pinned memory; timing = rank 0's host-thread stages (seconds)",
         "wall_s": round(time.perf_counter() - t_start, 1),
         "per_rank": ranks,
     }
-
 
 def main():
     a = parse()
@@ -782,7 +819,10 @@ def main():
     # other ranks wait at the barrier
     cpu = None
     if d.rank == 0 and not a.no_cpu:
-        cpu = cpu_baseline(a, N, C, lens_all if a.mode == "mixed" else None)
+        try:
+            cpu = cpu_baseline(a, N, C, lens_all if a.mode == "mixed" else None)
+        except Exception as e:  # a reported baseline: never worth the device line
+            cpu = {"error": f"{type(e).__name__}: {e}"}
     d.barrier()
 
     if d.rank == 0:

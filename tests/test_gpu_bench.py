@@ -113,3 +113,21 @@ def test_bench_mixed_line_carries_cpu_baseline_and_e2e(bcp):
     assert cpu["kind"] == "reference" and cpu["value"] > 0 and "stripe_shapes" in cpu["legs"][0]
     assert line["e2e"]["gen"]["verified"] is True and line["e2e"]["rebuild"]["verified"] is True
     assert line["per_rank"][0]["verified"] is True
+
+
+@pytest.mark.timeout(400)
+def test_bench_line_survives_an_e2e_failure_on_one_rank(bcp):
+    """The end-to-end leg never costs the N-GPU line: a rank whose store
+    cannot be written (injected) keeps making the collective calls, and rank 0
+    prints the device line with the failure reported inside `e2e`."""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", BCP_BENCH_E2E_FAIL_RANK="1")
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--allow-shared", "--stripes", "64", "--steps", "2",
+                        "--warmup", "1", "--no-cpu", "--e2e-gib", "0.25", "--e2e-reps", "1"],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=360)
+    assert r.returncode == 0, (r.returncode, r.stdout[-2000:], r.stderr[-4000:])
+    line = _last_json(r.stdout)
+    assert line["config"]["verified_on_device"] is True and line["value"] > 0
+    e2e = line["e2e"]
+    assert list(e2e["errors"]) in (["1"], [1]) and "injected" in str(e2e["errors"])
+    assert e2e["gen"]["verified"] is False and e2e["per_rank"][0]["errors"] is None
