@@ -228,15 +228,26 @@ typedef struct {
 
 
 
+/* One read job: bytes [off, off + len) of source k's data, into dst (its
+ * place in the slab + off).  Sources are read in pieces of at most PIECE
+ * bytes, so a batch's big chunks spread over the io threads instead of one
+ * thread finishing a 4 MiB chunk while the others idle. */
+#define PIECE ((uint64_t)1 << 20)
 typedef struct {
     job j;
     const char *root;
     task *t;
     int k;                /* source */
-    uint8_t *dst;         /* its place in the slab */
+    uint64_t off, len;
+    uint8_t *dst;
     uint64_t *bytes;      /* accumulated under lock */
     latch *done;
 } read_arg;
+
+static uint64_t pieces_of(uint64_t size)
+{
+    return (size + PIECE - 1) / PIECE;
+}
 
 typedef struct {
     job j;
@@ -374,16 +385,17 @@ static void do_read(job *p)
 {
     read_arg *a = (read_arg *)p;
     task *t = a->t;
-    uint64_t want = t->size[a->k], got = 0;
+    const uint64_t want = a->len;
+    uint64_t got = 0;
     if (want) {
         char fn[4352];
         const int is_parity = t->rebuild && a->k == t->parity_src;
         chunk_file(fn, sizeof(fn), a->root, t->holders[a->k], is_parity ? "parity" : "chunks", t->path);
         int fd = open(fn, O_RDONLY);
         if (fd >= 0) {
-            posix_fadvise(fd, 0, 0, POSIX_FADV_SEQUENTIAL);
+            posix_fadvise(fd, (off_t)(t->src_off[a->k] + a->off), (off_t)want, POSIX_FADV_SEQUENTIAL);
             while (got < want) {
-                ssize_t r = pread(fd, a->dst + got, (size_t)(want - got), (off_t)(t->src_off[a->k] + got));
+                ssize_t r = pread(fd, a->dst + got, (size_t)(want - got), (off_t)(t->src_off[a->k] + a->off + got));
                 if (r <= 0)
                     break;
                 got += (uint64_t)r;
@@ -854,6 +866,17 @@ static void releaser_drain(pool *P)
     latch_destroy(&l);
 }
 
+/* One batch between queueing its reads and submitting it. */
+typedef struct {
+    size_t first, last, split; /* tasks; [split, last) mapped (MAP) */
+    uint64_t in_used, reg_lo;  /* input bytes; where the mapped tail starts */
+    double tw;                 /* reads queued at */
+    int need_map;
+    int reads_live;            /* S->reads initialised and not yet waited for */
+    dev_lane *L;
+    slot *S;
+} bstate;
+
 static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, size_t nt, int corrupt_fd,
                          FILE *log, bcp_run_stats *stats, double t0)
 {
@@ -976,10 +999,13 @@ static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, 
     bcp_stripe *st = pl->st;
     bcp_source *so = pl->so;
     /* every job of the run, before the first one is queued: a read job per
-     * source, a write job per task, a completion per batch */
+     * piece of every source (read into the slab or, after a failed mapping,
+     * instead of it -- never both), a write job per task, a completion per
+     * batch */
     size_t nreads_all = 0;
     for (size_t i = 0; i < nt; i++)
-        nreads_all += (size_t)tasks[i].n;
+        for (int k = 0; k < tasks[i].n; k++)
+            nreads_all += (size_t)pieces_of(tasks[i].size[k]);
     read_arg *ra = calloc(nreads_all ? nreads_all : 1, sizeof(read_arg));
     write_arg *wa = calloc(nt ? nt : 1, sizeof(write_arg));
     complete_arg *cargs = calloc(nbatches ? (size_t)nbatches : 1, sizeof(complete_arg));
@@ -997,64 +1023,98 @@ static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, 
     tm.stat = now_s() - t_stat;
     tm.batches = (uint32_t)nbatches;
 
-    /* 3. stream the batches through the slots: batch b is read while b-1
-     * is on the device and earlier ones are being written (4 slots by
-     * default: a slot's parity writes gate its reuse, and a fourth slot
-     * took 8-15 % off every workload against three).  (Reading ahead
-     * of the submissions, nslots-1 batches deep in 1 MiB pieces, measured
-     * no different in r03 -- the reads are not the bound, section 6.7 of
-     * DESIGN.md -- and is not kept.) */
-    size_t first = 0;
+    /* 3. stream the batches through the slots.  Batch b+1's reads are
+     * queued before the host waits for batch b's, so the io threads go from
+     * one batch to the next without idling at a batch's last chunks; b is on
+     * the device meanwhile and earlier batches are being written (4 slots by
+     * default: a slot's parity writes gate its reuse). */
+    bstate *bs = calloc(nbatches ? (size_t)nbatches : 1, sizeof(bstate));
+    if (!bs) {
+        free(ra);
+        free(wa);
+        free(cargs);
+        free(maps);
+        return -ENOMEM;
+    }
+    {
+        size_t first = 0;
+        for (int b = 0; b < nbatches; b++) {
+            bs[b].first = first;
+            while (first < nt && tasks[first].batch == b)
+                first++;
+            bs[b].last = first;
+        }
+    }
+    /* queue batch b's reads into its slot (after the slot's previous batch
+     * has been written); MAP mode: decide the mapped tail */
+    #define PUSH_READS(B, A, Z)                                                                          \
+        for (size_t i_ = (A); i_ < (Z); i_++)                                                              \
+            for (int k_ = 0; k_ < tasks[i_].n; k_++)                                                       \
+                for (uint64_t o_ = 0; o_ < tasks[i_].size[k_]; o_ += PIECE) {                              \
+                    read_arg *a_ = &ra[rnext++];                                                           \
+                    const uint64_t l_ = tasks[i_].size[k_] - o_ < PIECE ? tasks[i_].size[k_] - o_ : PIECE; \
+                    *a_ = (read_arg){{0}, store_root, &tasks[i_], k_, o_, l_,                              \
+                                     (B)->S->h_in + data_off(&tasks[i_], k_, ml) + o_, &bytes_read,        \
+                                     &(B)->S->reads};                                                      \
+                    pool_push(&pl->readers, &a_->j, do_read);                                              \
+                }
+    int started = 0; /* batches whose reads are queued */
     for (int b = 0; b < nbatches && !rc; b++) {
-        dev_lane *L = &pl->dev[b % pl->ndev];
-        slot *S = &L->slots[(b / pl->ndev) % nslots];
-        double tw = now_s();
-        if (S->busy) { /* writes of batch b - nslots still running */
-            latch_wait(&S->writes);
-            latch_destroy(&S->writes);
-            S->busy = 0;
-        }
-        tm.slot_wait += now_s() - tw;
-        size_t last = first;
-        while (last < nt && tasks[last].batch == b)
-            last++;
-        uint64_t in_used = 0;
-        for (size_t i = first; i < last; i++)
-            for (int k = 0; k < tasks[i].n; k++) {
-                const uint64_t end = tasks[i].in_off[k] + span_of(&tasks[i], k, ml);
-                if (end > in_used)
-                    in_used = end;
+        for (; started < nbatches && started <= b + 1; started++) {
+            bstate *B = &bs[started];
+            B->L = &pl->dev[started % pl->ndev];
+            B->S = &B->L->slots[(started / pl->ndev) % nslots];
+            double tw = now_s();
+            if (B->S->busy) { /* writes of batch started - nslots still running */
+                latch_wait(&B->S->writes);
+                latch_destroy(&B->S->writes);
+                B->S->busy = 0;
             }
-        /* MAP: the batch's tail tasks [split, last), about map_share of its
-         * input bytes, are mapped by this thread while the io threads read
-         * the head into the slab (within the caps on what is mapped at once) */
-        size_t split = last;
-        if (ml && last > first && __atomic_load_n(&map_out[0], __ATOMIC_RELAXED) < MAP_OUT_BYTES_MAX &&
-            __atomic_load_n(&map_out[1], __ATOMIC_RELAXED) < MAP_OUT_FILES_MAX) {
-            const uint64_t from = in_used - (uint64_t)(pl->map_share * (double)in_used);
-            split = first;
-            while (split < last && tasks[split].in_off[0] < from)
-                split++;
-        }
-        const uint64_t reg_lo = split < last ? tasks[split].in_off[0] : in_used;
-        long nreads = 0;
-        for (size_t i = first; i < split; i++)
-            nreads += tasks[i].n;
-        tw = now_s();
-        latch_init(&S->reads, nreads);
-        for (size_t i = first; i < split; i++)
-            for (int k = 0; k < tasks[i].n; k++) {
-                read_arg *a = &ra[rnext++];
-                *a = (read_arg){{0}, store_root, &tasks[i], k, S->h_in + data_off(&tasks[i], k, ml), &bytes_read,
-                                &S->reads};
-                pool_push(&pl->readers, &a->j, do_read);
+            tm.slot_wait += now_s() - tw;
+            uint64_t in_used = 0;
+            for (size_t i = B->first; i < B->last; i++)
+                for (int k = 0; k < tasks[i].n; k++) {
+                    const uint64_t end = tasks[i].in_off[k] + span_of(&tasks[i], k, ml);
+                    if (end > in_used)
+                        in_used = end;
+                }
+            B->in_used = in_used;
+            /* MAP: the batch's tail tasks [split, last), about map_share of
+             * its input bytes, are mapped by this thread while the io
+             * threads read the head (within the caps on what is mapped at
+             * once) */
+            B->split = B->last;
+            if (ml && B->last > B->first && __atomic_load_n(&map_out[0], __ATOMIC_RELAXED) < MAP_OUT_BYTES_MAX &&
+                __atomic_load_n(&map_out[1], __ATOMIC_RELAXED) < MAP_OUT_FILES_MAX) {
+                const uint64_t from = in_used - (uint64_t)(pl->map_share * (double)in_used);
+                B->split = B->first;
+                while (B->split < B->last && tasks[B->split].in_off[0] < from)
+                    B->split++;
             }
-        tm.read_jobs += (uint32_t)nreads;
+            B->reg_lo = B->split < B->last ? tasks[B->split].in_off[0] : in_used;
+            long nreads = 0;
+            for (size_t i = B->first; i < B->split; i++)
+                for (int k = 0; k < tasks[i].n; k++)
+                    nreads += (long)pieces_of(tasks[i].size[k]);
+            B->tw = now_s();
+            latch_init(&B->S->reads, nreads);
+            B->reads_live = 1;
+            PUSH_READS(B, B->first, B->split);
+            tm.read_jobs += (uint32_t)nreads;
+            B->need_map = B->split < B->last;
+        }
+        bstate *B = &bs[b];
+        dev_lane *L = B->L;
+        slot *S = B->S;
+        const uint64_t in_used = B->in_used, reg_lo = B->reg_lo;
+        const size_t first = B->first, last = B->last, split = B->split;
+        const double tw = B->tw;
+        /* MAP: this batch's tail, mapped now (batch b+1's reads are queued) */
         double map_s = 0;
         int mapped_ok = 0;
         uint8_t *map_va = NULL;
         map_range *batch_map = NULL;
-        if (split < last) {
+        if (B->need_map) {
             const double tm0 = now_s();
             const size_t map_len = (size_t)(in_used - reg_lo);
             map_range *R = &maps[nmaps];
@@ -1090,18 +1150,14 @@ static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, 
         latch_wait(&S->reads);
         const double t_read_end = S->reads.t_zero;
         latch_destroy(&S->reads);
+        B->reads_live = 0;
         if (split < last && !mapped_ok) { /* read what could not be mapped */
             long n2 = 0;
             for (size_t i = split; i < last; i++)
-                n2 += tasks[i].n;
+                for (int k = 0; k < tasks[i].n; k++)
+                    n2 += (long)pieces_of(tasks[i].size[k]);
             latch_init(&S->reads, n2);
-            for (size_t i = split; i < last; i++)
-                for (int k = 0; k < tasks[i].n; k++) {
-                    read_arg *a = &ra[rnext++];
-                    *a = (read_arg){{0}, store_root, &tasks[i], k, S->h_in + data_off(&tasks[i], k, ml),
-                                    &bytes_read, &S->reads};
-                    pool_push(&pl->readers, &a->j, do_read);
-                }
+            PUSH_READS(B, split, last);
             tm.read_jobs += (uint32_t)n2;
             latch_wait(&S->reads);
             latch_destroy(&S->reads);
@@ -1149,10 +1205,13 @@ static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, 
             (rc = bcp_xor_stripes_async(L->qk, st, ns, so, nsrc)) || (rc = bcp_event_record(S->ev_k, L->qk)) ||
             (rc = bcp_queue_wait_event(L->qd, S->ev_k)) ||
             (rc = bcp_d2h_async(L->qd, S->h_out, S->d_out, (size_t)out_used)) ||
-            (rc = bcp_event_record(S->ev_d, L->qd)))
+            (rc = bcp_event_record(S->ev_d, L->qd))) {
+            if (batch_map) /* never submitted: nothing on the device reads it */
+                map_release(batch_map);
             break;
+        }
         /* writers start once the batch's D2H is done (completion thread);
-         * the host moves on to reading batch b+1 meanwhile */
+         * the host moves on to batch b+1 meanwhile */
         latch_init(&S->writes, (long)(last - first));
         S->busy = 1;
         complete_arg *ca = &cargs[b];
@@ -1162,9 +1221,18 @@ static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, 
         for (size_t i = first; i < last; i++)
             bytes_written += (tasks[i].rebuild ? 0 : 8u * (uint64_t)tasks[i].n) + tasks[i].out_len;
         ntasks += last - first;
-        first = last;
         tm.submit += now_s() - ts;
     }
+    #undef PUSH_READS
+    /* a failed submission leaves batch b+1's reads queued: let them finish
+     * before the slab and the jobs go away */
+    for (int b = 0; b < started; b++)
+        if (bs[b].reads_live) {
+            latch_wait(&bs[b].S->reads);
+            latch_destroy(&bs[b].S->reads);
+            bs[b].reads_live = 0;
+        }
+    free(bs);
     const double td = now_s();
     for (int d = 0; d < pl->ndev; d++)
         for (int s = 0; s < nslots; s++) {
