@@ -533,7 +533,7 @@ int bcp_pipeline_destroy(bcp_pipeline *pl);
 typedef struct {
     double stat, read_wait, slot_wait, submit, drain;
     uint32_t batches;    /* device batches */
-    uint32_t read_jobs;  /* io read jobs (one per chunk read into a slab) */
+    uint32_t read_jobs;  /* io read jobs (one per 1 MiB piece of a chunk read into a slab) */
     double map;
     uint64_t mapped_bytes;
     uint32_t map_fallbacks;
