@@ -1147,6 +1147,7 @@ static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, 
             if (!mapped_ok)
                 tm.map_fallbacks++;
         }
+        const double t_wait0 = now_s();
         latch_wait(&S->reads);
         const double t_read_end = S->reads.t_zero;
         latch_destroy(&S->reads);
@@ -1182,7 +1183,7 @@ static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, 
             }
         }
         const double ts = now_s();
-        tm.read_wait += ts - tw;
+        tm.read_wait += ts - t_wait0; /* blocked on this batch's reads (its fallback reads included) */
         uint32_t ns = 0, nsrc = 0;
         uint64_t out_used = 0;
         for (size_t i = first; i < last; i++) {

@@ -524,12 +524,12 @@ int bcp_pipeline_run(bcp_pipeline *pl, const char *store_root, int ntargets, con
                      size_t nitems, FILE *log, bcp_run_stats *stats);
 int bcp_pipeline_destroy(bcp_pipeline *pl);
 /* Where the host thread of the pipeline's last run spent its wall time
- * (seconds; for tools): stat phase, reading a batch (from issuing its reads
- * to the last one's end, MAP mode's mapping included), waiting for a slot's
- * previous batch to be written before reading into it, building and
- * submitting batches, and the drain after the last submission; MAP mode:
- * the host thread's mapping + registering time (inside read_wait), the bytes
- * copied out of mappings, and batches that fell back to reading. */
+ * (seconds; for tools): stat phase, blocked on a batch's reads (the next
+ * batch's reads are already queued then), waiting for a slot's previous
+ * batch to be written before queueing reads into it, building and submitting
+ * batches, and the drain after the last submission; MAP mode: the host
+ * thread's mapping + registering time, the bytes copied out of mappings, and
+ * batches that fell back to reading. */
 typedef struct {
     double stat, read_wait, slot_wait, submit, drain;
     uint32_t batches;    /* device batches */
