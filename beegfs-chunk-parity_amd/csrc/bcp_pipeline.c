@@ -39,7 +39,9 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <linux/magic.h>
 #include <sys/mman.h>
+#include <sys/vfs.h>
 #include <sys/stat.h>
 #include <sys/uio.h>
 #include <time.h>
@@ -257,6 +259,7 @@ typedef struct {
     latch *done;
     FILE *log;
     int *errors;
+    int prealloc;         /* posix_fallocate first (not on tmpfs: see do_write) */
 } write_arg;
 
 /* MAP read mode: one batch's mapped tail -- a range of its own holding the
@@ -290,6 +293,7 @@ typedef struct {
     FILE *log;
     int *errors;
     int *dev_rc;
+    int prealloc;
 } complete_arg;
 
 static pthread_mutex_t g_stat_lock = PTHREAD_MUTEX_INITIALIZER;
@@ -435,7 +439,12 @@ static void do_write(job *p)
         /* gen: u64 sizes header + body; rebuild: the chunk itself */
         const size_t hdr = t->rebuild ? 0 : 8u * (size_t)t->n;
         uint64_t total = hdr + t->out_len;
-        if (total)
+        /* The reference reserves the file's space first (task_processing.c:186):
+         * on a disk that keeps it in one extent and fails early when full.  On
+         * tmpfs it makes the kernel allocate and ZERO every page before the
+         * write fills it again -- one more pass over the parity bytes for
+         * nothing -- so it is skipped there (the file is the same). */
+        if (total && a->prealloc)
             posix_fallocate(fd, 0, (off_t)total);
         struct iovec iov[2] = {{t->size, hdr}, {(void *)a->body, (size_t)t->out_len}};
         uint64_t done = 0;
@@ -497,7 +506,8 @@ static void do_complete(job *p)
     } else {
         for (size_t i = a.first; i < a.last; i++) {
             write_arg *w = &a.wa[i];
-            *w = (write_arg){{0}, a.root, &a.tasks[i], a.S->h_out + a.tasks[i].out_off, &a.S->writes, a.log, a.errors};
+            *w = (write_arg){{0}, a.root, &a.tasks[i], a.S->h_out + a.tasks[i].out_off, &a.S->writes, a.log, a.errors,
+                             a.prealloc};
             pool_push(a.writers, &w->j, do_write);
         }
     }
@@ -881,6 +891,12 @@ static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, 
                          FILE *log, bcp_run_stats *stats, double t0)
 {
     uint64_t map_out[2] = {0, 0}; /* outstanding mapped bytes, mappings (the releaser decrements) */
+    int prealloc = 1;
+    {
+        struct statfs sf;
+        if (statfs(store_root, &sf) == 0 && sf.f_type == TMPFS_MAGIC)
+            prealloc = 0;
+    }
     const int nslots = pl->o.nslots;
     int rc = 0, errors = 0, dev_rc = 0;
     uint64_t bytes_read = 0, bytes_written = 0, ntasks = 0;
@@ -1217,7 +1233,7 @@ static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, 
         S->busy = 1;
         complete_arg *ca = &cargs[b];
         *ca = (complete_arg){{0}, S, batch_map, &pl->releaser, store_root, tasks, wa, first, last, &pl->writers, log,
-                             &errors, &dev_rc};
+                             &errors, &dev_rc, prealloc};
         pool_push(&pl->completer, &ca->j, do_complete);
         for (size_t i = first; i < last; i++)
             bytes_written += (tasks[i].rebuild ? 0 : 8u * (uint64_t)tasks[i].n) + tasks[i].out_len;
