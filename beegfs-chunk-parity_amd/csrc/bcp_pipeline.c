@@ -432,8 +432,14 @@ static void do_write(job *p)
     task *t = a->t;
     char fn[4352];
     chunk_file(fn, sizeof(fn), a->root, t->p, t->rebuild ? "chunks" : "parity", t->path);
-    mkdir_parents(fn);
+    /* directories only when the file cannot be created (mkdir_for_file,
+     * task_processing.c:30-40, does every level first: a lookup per level
+     * per file) */
     int fd = open(fn, O_CREAT | O_WRONLY | O_TRUNC, S_IRUSR | S_IWUSR);
+    if (fd < 0 && errno == ENOENT) {
+        mkdir_parents(fn);
+        fd = open(fn, O_CREAT | O_WRONLY | O_TRUNC, S_IRUSR | S_IWUSR);
+    }
     int bad = fd < 0;
     if (!bad) {
         /* gen: u64 sizes header + body; rebuild: the chunk itself */
