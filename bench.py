@@ -97,6 +97,9 @@ def parse():
     ap.add_argument("--e2e-modes", default="copy,map",
                     help="pipeline read paths timed end to end, interleaved; the first is the headline")
     ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--no-prof", action="store_true",
+                    help="skip the live rocprofv3 kernel-trace and PMC passes of this workload on this box")
+    ap.add_argument("--prof-steps", type=int, default=5, help="steps of each profiled child run")
     ap.add_argument("--allow-shared", action="store_true",
                     help="run N ranks even when fewer than N distinct GPUs exist (rehearsal; "
                          "the line then says shared_gpu true and counts distinct GPUs)")
@@ -235,6 +238,90 @@ def pmc_traffic(workload_key: str, kernel_tag: str):
             doc.setdefault("files", {})["pmc_summary"] = os.path.relpath(path, ROOT)
             best = doc
     return best
+
+
+def live_profile(a, stripes_arg: int, kernel_tag: str, bytes_per_step: int) -> dict:
+    """The same workload on THIS box, now, under rocprofv3 (rank 0, after the
+    device timing): one kernel-trace + stats run and the two PMC passes
+    (FETCH_SIZE, WRITE_SIZE: counters in runs of their own, as
+    MI355X_MICROARCH.md's HBM recipe prescribes), each a child process
+    `rocprofv3 ... -- python3 bench.py <same workload> --no-e2e --no-cpu
+    --no-prof` under its own time limit; HBM bytes per launch with the gfx950
+    corrections of tools/pmc_summary.py (FETCH_SIZE x2, KiB).  So the line's
+    frac_rocprof and traffic come from the machine its frac_event does."""
+    import csv
+    import shutil
+    import signal
+    import statistics
+    import subprocess
+    import tempfile
+    exe = shutil.which("rocprofv3")
+    if not exe:
+        return {"skipped": "rocprofv3 not on PATH"}
+    t0 = time.perf_counter()
+    out = tempfile.mkdtemp(prefix="bcp_bench_prof_")
+    child = [sys.executable, os.path.abspath(__file__), "--gpus", "1", "--mode", a.mode, "--stripes", str(stripes_arg),
+             "--nsrc", str(a.nsrc), "--chunk", str(a.chunk), "--rebuild-layout", a.rebuild_layout,
+             "--warmup", "1", "--no-cpu", "--no-e2e", "--no-prof"]
+    for flag, val in (("--blocks-per-cu", a.blocks_per_cu), ("--vecs", a.vecs), ("--grid", a.grid)):
+        if val:
+            child += [flag, str(val)]
+    if a.contig:
+        child.append("--contig")
+    for kv in a.opt:
+        child += ["--opt", kv]
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK",
+                        "MASTER_ADDR", "MASTER_PORT") and not k.startswith("TORCHELASTIC")}
+
+    def run(tag, args, steps):
+        d_ = os.path.join(out, tag)
+        cmd = [exe] + args + ["-d", d_, "-o", "run", "--output-format", "csv", "--"] + child + ["--steps", str(steps)]
+        p = subprocess.Popen(cmd, env=env, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True,
+                             start_new_session=True)
+        try:
+            _, err = p.communicate(timeout=150)
+        except subprocess.TimeoutExpired:
+            os.killpg(p.pid, signal.SIGKILL)
+            p.wait()
+            raise RuntimeError(f"rocprofv3 {tag}: time limit")
+        if p.returncode:
+            raise RuntimeError(f"rocprofv3 {tag}: exit {p.returncode}: {err[-300:]}")
+        return d_
+
+    def one(d_, pattern):
+        hits = sorted(glob.glob(os.path.join(d_, "**", pattern), recursive=True))
+        if not hits:
+            raise RuntimeError(f"no {pattern} under {d_}")
+        return hits[-1]
+
+    def counter(path, name):
+        vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(path))
+                if r["Counter_Name"] == name and kernel_tag in r["Kernel_Name"]]
+        if not vals:
+            raise RuntimeError(f"no {name} rows for {kernel_tag}")
+        return statistics.median(vals), len(vals)
+
+    try:
+        stats = one(run("trace", ["--kernel-trace", "--stats"], a.prof_steps), "*kernel_stats.csv")
+        row = next((r for r in csv.DictReader(open(stats)) if kernel_tag in r["Name"]), None)
+        if row is None:
+            raise RuntimeError(f"{kernel_tag} not in the kernel statistics")
+        fetch, nf = counter(one(run("pmc_fetch", ["--pmc", "FETCH_SIZE"], 3), "*counter_collection.csv"), "FETCH_SIZE")
+        write, nw = counter(one(run("pmc_write", ["--pmc", "WRITE_SIZE"], 3), "*counter_collection.csv"), "WRITE_SIZE")
+        traffic = fetch * 1024 * 2 + write * 1024
+        return {"rocprof_avg_ns": float(row["AverageNs"]), "rocprof_calls": int(row["Calls"]),
+                "rocprof_min_ns": float(row["MinNs"]), "traffic": round(traffic),
+                "traffic_over_algorithmic": round(traffic / bytes_per_step, 5),
+                "dispatches": {"fetch": nf, "write": nw},
+                "source": "live: rocprofv3 --kernel-trace --stats, then --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate "
+                          "child runs of this workload on this box); FETCH_SIZE x2 (gfx950 wide-read correction), "
+                          "WRITE_SIZE x1; KiB->B x1024",
+                "wall_s": round(time.perf_counter() - t0, 1)}
+    except Exception as e:  # reported, never fatal: the committed set stands in
+        return {"error": f"{type(e).__name__}: {e}", "wall_s": round(time.perf_counter() - t0, 1)}
+    finally:
+        shutil.rmtree(out, ignore_errors=True)
 
 
 def cpu_baseline(a, N: int, C: int, lens_all) -> dict:
@@ -614,6 +701,7 @@ def main():
     if not a.stripes:
         lo, hi = shard_range(125_000, d.world, d.rank)
         a.stripes = hi - lo if d.world == 8 else 12_500
+    stripes_arg = a.stripes
     S, N, C = a.stripes, a.nsrc, a.chunk
     chk = eng.alloc(64)
     lens_all = None
@@ -823,6 +911,14 @@ def main():
             cpu = cpu_baseline(a, N, C, lens_all if a.mode == "mixed" else None)
         except Exception as e:  # a reported baseline: never worth the device line
             cpu = {"error": f"{type(e).__name__}: {e}"}
+    # rocprofv3 on this box: rank 0's device, child processes (the device
+    # buffers of this run are released first)
+    live = None
+    if d.rank == 0 and not a.no_prof:
+        for ptr in (src, out):
+            eng.free(ptr)
+        src = out = None
+        live = live_profile(a, stripes_arg, kernel_tag, bytes_per_step)
     d.barrier()
 
     if d.rank == 0:
@@ -831,10 +927,13 @@ def main():
         mode_key = "rebuild_packed" if (a.mode == "rebuild" and a.rebuild_layout == "packed") else a.mode
         wkey = f"{mode_key}:{S}x{N}x{C}"
         pmc = pmc_traffic(wkey, kernel_tag)
-        frac_rocprof = None
-        if pmc and pmc.get("rocprof_avg_ns"):
-            frac_rocprof = round(bytes_per_step / (pmc["rocprof_avg_ns"] * 1e-9) / 1e9 / HBM_PEAK_GBS, 4)
         run_box = box_of(bus_ids[0])
+        live_ok = bool(live and live.get("traffic"))
+        frac_rocprof = None
+        if live_ok:
+            frac_rocprof = round(bytes_per_step / (live["rocprof_avg_ns"] * 1e-9) / 1e9 / HBM_PEAK_GBS, 4)
+        elif pmc and pmc.get("rocprof_avg_ns"):
+            frac_rocprof = round(bytes_per_step / (pmc["rocprof_avg_ns"] * 1e-9) / 1e9 / HBM_PEAK_GBS, 4)
         line = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -879,18 +978,24 @@ def main():
                 "frac_event": round(achieved / HBM_PEAK_GBS, 4),
                 "frac_rocprof": frac_rocprof,
                 "kernel_ms": round(kern_ms_max, 4),
-                "traffic": pmc["hbm_bytes_per_launch"] if pmc else None,
-                "traffic_source": pmc["source"] if pmc else None,
+                "traffic": (live["traffic"] if live_ok else pmc["hbm_bytes_per_launch"] if pmc else None),
+                "traffic_source": (live["source"] if live_ok else pmc["source"] if pmc else None),
+                "live_profile": live,
                 "profile_files": pmc.get("files") if pmc else None,
                 "profile_commit": pmc.get("code_commit") if pmc else None,
-                # frac_event is this run's box; frac_rocprof / traffic the profile set's box
                 "run_box": run_box,
-                "profile_box": pmc.get("box") if pmc else None,
-                "same_box": bool(pmc and pmc.get("box") and run_box["boot_id"]
-                                 and pmc["box"].get("boot_id") == run_box["boot_id"]),
+                "profile_box": run_box if live_ok else (pmc.get("box") if pmc else None),
+                "same_box": live_ok or bool(pmc and pmc.get("box") and run_box["boot_id"]
+                                            and pmc["box"].get("boot_id") == run_box["boot_id"]),
+                "committed_set": ({"frac_rocprof": round(bytes_per_step / (pmc["rocprof_avg_ns"] * 1e-9) / 1e9 /
+                                                         HBM_PEAK_GBS, 4) if pmc.get("rocprof_avg_ns") else None,
+                                   "traffic": pmc.get("hbm_bytes_per_launch"), "box": pmc.get("box")}
+                                  if pmc else None),
                 "frac_note": "frac = frac_event: algorithmic bytes / HIP-event kernel time in this run (run_box); "
-                             "frac_rocprof and traffic: the same bytes / the committed rocprofv3 kernel-trace "
-                             "average and PMC passes, measured on profile_box (a different box unless same_box)",
+                             "frac_rocprof and traffic: the same bytes / the rocprofv3 kernel-trace average and the "
+                             "PMC passes of this workload -- live child runs on this box after the timing "
+                             "(live_profile; same_box) or, where those failed or --no-prof, the committed profile "
+                             "set (profile_files, measured on profile_box)",
             },
             "cpu_baseline": cpu,
             "per_rank": per_rank,

@@ -39,7 +39,7 @@ def _run(cmd, timeout):
 @pytest.mark.parametrize("mode", ["gen", "rebuild", "mixed"])
 def test_bench_one_rank_small(bcp, mode):
     line = _run([sys.executable, "bench.py", "--stripes", "64", "--steps", "2", "--warmup", "1", "--no-cpu",
-                 "--no-e2e", "--mode", mode], 300)
+                 "--no-e2e", "--no-prof", "--mode", mode], 300)
     assert line["config"]["verified_on_device"] is True
     assert line["n_gpus"] == 1 and line["config"]["ranks"] == 1 and line["config"]["shared_gpu"] is False
     assert line["roofline"]["frac"] == line["roofline"]["frac_event"] > 0
@@ -51,7 +51,7 @@ def test_bench_torchrun_two_ranks_labels(bcp):
     line = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                  "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
                  "bench.py", "--gpus", "2", "--stripes", "64", "--steps", "2", "--warmup", "1", "--no-cpu",
-                 "--no-e2e", "--allow-shared"], 420)
+                 "--no-e2e", "--no-prof", "--allow-shared"], 420)
     assert line["config"]["verified_on_device"] is True
     assert line["config"]["ranks"] == 2
     distinct = min(ndev, 2)  # bench maps local rank r to device r % ndev
@@ -70,7 +70,7 @@ def test_bench_gpus_n_launches_its_own_ranks(bcp, n):
     env = dict(os.environ, MASTER_ADDR="127.0.0.1")
     env.pop("WORLD_SIZE", None)
     args = [sys.executable, "bench.py", "--gpus", str(n), "--stripes", "64", "--steps", "2", "--warmup", "1",
-            "--cpu-seconds", "1", "--cpu-stripes", "16", "--e2e-gib", "0.25", "--e2e-reps", "1"]
+            "--cpu-seconds", "1", "--cpu-stripes", "16", "--e2e-gib", "0.25", "--e2e-reps", "1", "--no-prof"]
     if ndev < n:
         r = subprocess.run(args, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
         assert r.returncode == 4, (r.returncode, r.stdout[-2000:], r.stderr[-2000:])
@@ -108,7 +108,7 @@ def test_bench_mixed_line_carries_cpu_baseline_and_e2e(bcp):
     """Mixed mode (config-5 shapes): the reference's fold timed over the same
     zero-padded stripe shapes, and the end-to-end leg, in the one-rank line."""
     line = _run([sys.executable, "bench.py", "--mode", "mixed", "--stripes", "64", "--steps", "2", "--warmup", "1",
-                 "--cpu-seconds", "1", "--e2e-gib", "0.25", "--e2e-reps", "1"], 300)
+                 "--cpu-seconds", "1", "--e2e-gib", "0.25", "--e2e-reps", "1", "--no-prof"], 300)
     cpu = line["cpu_baseline"]
     assert cpu["kind"] == "reference" and cpu["value"] > 0 and "stripe_shapes" in cpu["legs"][0]
     assert line["e2e"]["gen"]["verified"] is True and line["e2e"]["rebuild"]["verified"] is True
@@ -123,7 +123,7 @@ def test_bench_line_survives_an_e2e_failure_on_one_rank(bcp):
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", BCP_BENCH_E2E_FAIL_RANK="1")
     env.pop("WORLD_SIZE", None)
     r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--allow-shared", "--stripes", "64", "--steps", "2",
-                        "--warmup", "1", "--no-cpu", "--e2e-gib", "0.25", "--e2e-reps", "1"],
+                        "--warmup", "1", "--no-cpu", "--e2e-gib", "0.25", "--e2e-reps", "1", "--no-prof"],
                        cwd=ROOT, env=env, capture_output=True, text=True, timeout=360)
     assert r.returncode == 0, (r.returncode, r.stdout[-2000:], r.stderr[-4000:])
     line = _last_json(r.stdout)
@@ -131,3 +131,20 @@ def test_bench_line_survives_an_e2e_failure_on_one_rank(bcp):
     e2e = line["e2e"]
     assert list(e2e["errors"]) in (["1"], [1]) and "injected" in str(e2e["errors"])
     assert e2e["gen"]["verified"] is False and e2e["per_rank"][0]["errors"] is None
+
+
+@pytest.mark.timeout(500)
+@pytest.mark.parametrize("mode", ["gen", "mixed"])
+def test_bench_live_profile_on_its_own_box(bcp, mode):
+    """The roofline's rocprof figures come from this box: the same workload
+    under rocprofv3 in child processes (kernel trace, then the two PMC passes),
+    traffic within 1 % of the algorithmic bytes, same_box set."""
+    line = _run([sys.executable, "bench.py", "--mode", mode, "--stripes", "256", "--steps", "3", "--warmup", "1",
+                 "--no-cpu", "--no-e2e", "--prof-steps", "3"], 450)
+    rf = line["roofline"]
+    live = rf["live_profile"]
+    assert live and "error" not in live, live
+    assert live["rocprof_calls"] >= 3 and live["rocprof_avg_ns"] > 0
+    assert 0.99 < live["traffic_over_algorithmic"] < 1.02, live
+    assert rf["same_box"] is True and rf["traffic"] == live["traffic"]
+    assert rf["frac_rocprof"] > 0 and rf["profile_box"] == rf["run_box"]

@@ -20,11 +20,11 @@ for m in gen rebuild mixed config4; do
   [ $m = config4 ] && args="--mode gen --stripes 15625"
   mkdir -p $O/$m
   if [ $m != gen ]; then
-    timeout -k 10 300 python3 $R/bench.py $args --no-cpu --no-e2e > $O/$m/bench.json 2> $O/$m/bench.err || { echo BENCH_${m}_FAIL; exit 1; }
+    timeout -k 10 300 python3 $R/bench.py $args --no-cpu --no-e2e --no-prof > $O/$m/bench.json 2> $O/$m/bench.err || { echo BENCH_${m}_FAIL; exit 1; }
   fi
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/$m/trace -o run --output-format csv -- python3 $R/bench.py $args --no-cpu --no-e2e > $O/$m/trace.log 2>&1 || { echo PROF_${m}_FAIL; exit 1; }
-  timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/$m/pmc_fetch -o run -- python3 $R/bench.py $args --steps 3 --warmup 1 --no-cpu --no-e2e > $O/$m/pmc_fetch.log 2>&1 || { echo PMC1_${m}_FAIL; exit 1; }
-  timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/$m/pmc_write -o run -- python3 $R/bench.py $args --steps 3 --warmup 1 --no-cpu --no-e2e > $O/$m/pmc_write.log 2>&1 || { echo PMC2_${m}_FAIL; exit 1; }
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/$m/trace -o run --output-format csv -- python3 $R/bench.py $args --no-cpu --no-e2e --no-prof > $O/$m/trace.log 2>&1 || { echo PROF_${m}_FAIL; exit 1; }
+  timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/$m/pmc_fetch -o run -- python3 $R/bench.py $args --steps 3 --warmup 1 --no-cpu --no-e2e --no-prof > $O/$m/pmc_fetch.log 2>&1 || { echo PMC1_${m}_FAIL; exit 1; }
+  timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/$m/pmc_write -o run -- python3 $R/bench.py $args --steps 3 --warmup 1 --no-cpu --no-e2e --no-prof > $O/$m/pmc_write.log 2>&1 || { echo PMC2_${m}_FAIL; exit 1; }
   echo PROF_${m}_OK
 done
 echo ALL_OK
