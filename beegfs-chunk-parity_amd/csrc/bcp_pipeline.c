@@ -851,8 +851,6 @@ int bcp_pipeline_run(bcp_pipeline *pl, const char *store_root, int ntargets, con
     return rc;
 }
 
-/* Stat, batch and stream the tasks through the slots (both modes).  Takes
- * no ownership of tasks. */
 /* MAP mode's caps on what is mapped at once: registered ranges pin their
  * page-cache pages until the releaser gets to them, and each chunk file is a
  * mapping of its own (vm.max_map_count is 65530 by default); at either cap a
@@ -893,6 +891,8 @@ typedef struct {
     slot *S;
 } bstate;
 
+/* Stat, batch and stream the tasks through the slots (both modes).  Takes
+ * no ownership of tasks. */
 static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, size_t nt, int corrupt_fd,
                          FILE *log, bcp_run_stats *stats, double t0)
 {
