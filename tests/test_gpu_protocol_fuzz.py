@@ -8,7 +8,8 @@ quirk A3-q1; a chunk file missing after planning), the P-role fold
 wire (implicit / the reference's) and the fold service width; every parity
 file must equal the oracle's (oracle.gen_parity_file, the reference's
 parity_generator restated).  Then a random target is lost and rebuilt by
-the protocol (1..4 rebuild lanes) or the pipeline; every lost chunk of a
+the protocol (1..4 rebuild lanes) or the pipeline (either read path, COPY or
+MAP); every lost chunk of a
 stripe without a missing chunk must come back byte for byte."""
 import os
 import shutil
@@ -85,9 +86,12 @@ def fuzz_rounds(bcp, oracle, tmp_path, budget, seed, engines):
             bcp.set_explicit_padding(pad)
             bcp.set_fold_inflight(int(rng.choice([1, 1, 2, 4])))
             what = f"seed {seed} round {rounds} {how} pad {pad}"
+            read_mode = int(rng.choice([bcp.READ_COPY, bcp.READ_MAP]))  # the pipeline's read path
             if how == "pipeline":
+                what += f" read_mode {read_mode}"
                 st = bcp.pipeline_gen(root, ntargets, items, slab_bytes=int(rng.choice([1, 8, 64])) << 20,
-                                      io_threads=int(rng.integers(1, 9)), nslots=int(rng.integers(2, 5)))
+                                      io_threads=int(rng.integers(1, 9)), nslots=int(rng.integers(2, 5)),
+                                      read_mode=read_mode)
             else:
                 bcp.set_fold_mode(bcp.FOLD_PIPELINED if how == "pipelined" else bcp.FOLD_BATCHED)
                 st = bcp.gen_run(root, ntargets, items, nlanes=int(rng.integers(1, 13)))
@@ -103,7 +107,7 @@ def fuzz_rounds(bcp, oracle, tmp_path, budget, seed, engines):
                     os.remove(S.chunk_path(root, victim, path))
             ordered = sorted(items, key=lambda x: x[0].encode())  # a DB walk: key order
             if how == "pipeline" and rng.random() < 0.7:
-                pl = bcp.Pipeline(io_threads=int(rng.integers(1, 9)))
+                pl = bcp.Pipeline(io_threads=int(rng.integers(1, 9)), read_mode=read_mode)
                 try:
                     st = pl.rebuild(root, ntargets, victim, ordered)
                 finally:
