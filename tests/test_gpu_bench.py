@@ -70,7 +70,8 @@ def test_bench_gpus_n_launches_its_own_ranks(bcp, n):
     env = dict(os.environ, MASTER_ADDR="127.0.0.1")
     env.pop("WORLD_SIZE", None)
     args = [sys.executable, "bench.py", "--gpus", str(n), "--stripes", "64", "--steps", "2", "--warmup", "1",
-            "--cpu-seconds", "1", "--cpu-stripes", "16", "--e2e-gib", "0.25", "--e2e-reps", "1", "--no-prof"]
+            "--cpu-seconds", "1", "--cpu-stripes", "16", "--e2e-gib", "0.25", "--e2e-reps", "1"]
+    args += ["--prof-steps", "2"] if n == 2 else ["--no-prof"]  # the live profile from rank 0 of an N-rank job
     if ndev < n:
         r = subprocess.run(args, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
         assert r.returncode == 4, (r.returncode, r.stdout[-2000:], r.stderr[-2000:])
@@ -98,6 +99,9 @@ def test_bench_gpus_n_launches_its_own_ranks(bcp, n):
     assert e2e["gen"]["bytes_read"] == sum(r["bytes_read"] for r in e2e["per_rank"])
     assert set(e2e["by_read_mode"]) == {"copy", "map"} and e2e["read_mode"] == "copy"
     assert e2e["by_read_mode"]["map"]["mapped_bytes_last_gen"] > 0
+    if n == 2:
+        live = line["roofline"]["live_profile"]
+        assert live and "error" not in live and line["roofline"]["same_box"] is True, live
     assert line["config"]["bytes_per_step_per_gpu"] * n * line["steps"] / 2**30 / (line["ms_per_step"] *
                                                                                    line["steps"] * 1e-3) == \
         pytest.approx(line["value"], rel=5e-3)  # value = the whole job's bytes / the slowest rank's time
