@@ -749,3 +749,37 @@ def test_pipeline_read_modes_byte_identical_and_fallback(bcp, oracle, tmp_path, 
     for c in chunks:
         ref[:len(c)] ^= c
     assert np.array_equal(body, ref)
+
+
+@pytest.mark.usefixtures("read_path")
+def test_pipeline_overwrites_shorter_parity_files_exactly(bcp, oracle, tmp_path):
+    """Parity files are overwritten in place and cut to their new length: a
+    second run after the chunks shrank (a partial round's changed chunks)
+    leaves exactly the new file, no stale tail; a rebuilt chunk likewise."""
+    root = str(tmp_path)
+    files = [("o/a", [0, 1, 2], 3, [300_000, 200_000, 5]), ("o/b", [1, 2, 3], 0, [4 * MiB, 1, 70_000])]
+    items, contents = S.populate(root, 4, files, seed=3)
+    pl = bcp.Pipeline(io_threads=3)
+    try:
+        assert pl.run(root, 4, items).errors == 0
+        for (path, holders, p, lens) in files:
+            assert S.read_file(S.parity_path(root, p, path)) == oracle.gen_parity_file(contents[path])
+        # every chunk shorter now
+        for (path, holders, p, lens) in files:
+            for k, h in enumerate(holders):
+                short = contents[path][k][: len(contents[path][k]) // 3]
+                S.write_chunk(root, h, path, short)
+                contents[path][k] = short
+        assert pl.run(root, 4, items).errors == 0
+        for (path, holders, p, lens) in files:
+            assert S.read_file(S.parity_path(root, p, path)) == oracle.gen_parity_file(contents[path]), path
+        # a rebuilt chunk written over a longer stale file of the same name
+        victim_path, holders, p, _ = files[1]
+        stale = S.chunk_path(root, 2, victim_path)
+        want = S.read_file(stale)
+        with open(stale, "wb") as f:
+            f.write(b"x" * (len(want) * 5 + 123))
+        assert pl.rebuild(root, 4, 2, sorted(items, key=lambda x: x[0].encode())).errors == 0
+        assert S.read_file(stale) == want
+    finally:
+        pl.close()
