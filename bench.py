@@ -24,10 +24,13 @@ any HIP call) and relays rank 0's line and the exit code; it refuses when the
 ranks would share GPUs unless --allow-shared.
 
 roofline.achieved / frac (= frac_event) use the kernel's HIP-event time on the
-stream it runs on; frac_rocprof, traffic and their provenance (profile files
-and the code commit they were measured at) come from the committed rocprofv3
-kernel-trace stats and PMC passes of the same command (profiles/**/*pmc*.json,
-tools/pmc_summary.py) when they match this workload, else null.
+stream it runs on; frac_rocprof and traffic come from a live profile on this
+box (rank 0, after the timing: the same workload under rocprofv3 in child
+processes -- kernel trace + stats, then --pmc FETCH_SIZE and --pmc WRITE_SIZE
+in runs of their own; roofline.live_profile, same_box true), or, with
+--no-prof or when a child run fails, from the committed profile set of the
+same workload (profiles/CURRENT_SET, profiles/**/*pmc*.json,
+tools/pmc_summary.py), reported beside it as roofline.committed_set.
 n_gpus counts DISTINCT devices (PCI bus ids gathered over gloo): ranks that
 share a GPU are flagged shared_gpu instead of being reported as more GPUs.
 cpu_baseline (every N and every mode): after the device timing and its
