@@ -180,9 +180,10 @@ def config1(a):
     # target, plan (P per select_P), run, fill the DB replicas (warm median)
     tool = os.path.join(ROOT, "beegfs-chunk-parity_amd", "bin", "bcp")
     no_server = dict(os.environ, BCP_FOLD_SERVER="0")
-    for label, extra, env in (("cli_parity_gen_complete(protocol)", [], None),
-                              ("cli_parity_gen_complete(protocol, --fold batched)", ["--fold", "batched"], None),
-                              ("cli_parity_gen_complete(pipeline)", ["--pipeline"], None),
+    for label, extra, env in (("cli_parity_gen_complete(protocol)", ["--protocol"], None),
+                              ("cli_parity_gen_complete(protocol, --fold batched)", ["--protocol", "--fold", "batched"],
+                               None),
+                              ("cli_parity_gen_complete(pipeline, the default engine)", [], None),
                               ("cli_parity_gen_complete(procs, node fold server)", ["--procs"], None),
                               ("cli_parity_gen_complete(procs, HIP context per rank)", ["--procs"], no_server)):
         times = []
