@@ -49,7 +49,8 @@ class PipelineTiming(ctypes.Structure):
     _fields_ = [("stat", ctypes.c_double), ("read_wait", ctypes.c_double), ("slot_wait", ctypes.c_double),
                 ("submit", ctypes.c_double), ("drain", ctypes.c_double), ("batches", ctypes.c_uint32),
                 ("read_jobs", ctypes.c_uint32), ("map", ctypes.c_double), ("mapped_bytes", ctypes.c_uint64),
-                ("map_fallbacks", ctypes.c_uint32), ("read_mode", ctypes.c_int)]
+                ("map_fallbacks", ctypes.c_uint32), ("read_mode", ctypes.c_int),
+                ("direct_bytes", ctypes.c_uint64), ("direct_fallbacks", ctypes.c_uint32)]
 
 
 class PipelineOpts(ctypes.Structure):
@@ -57,7 +58,7 @@ class PipelineOpts(ctypes.Structure):
                 ("nslots", ctypes.c_int), ("ndevices", ctypes.c_int), ("read_mode", ctypes.c_int)]
 
 
-READ_AUTO, READ_COPY, READ_MAP = 0, 1, 2
+READ_AUTO, READ_COPY, READ_MAP, READ_DIRECT = 0, 1, 2, 3
 
 
 XOR_HOOK = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t,

@@ -204,9 +204,9 @@ typedef struct {
     uint64_t src_off[MAX_STORAGE_TARGETS];/* file offset of the source data (parity body: 8n) */
     uint64_t max_cs;
     uint64_t out_len;                    /* gen: max_cs; rebuild: header[victim index] */
-    uint64_t in_off[MAX_STORAGE_TARGETS];/* offsets in the input slab (MAP layout: of the
-                                            file's first byte, page-aligned; the data
-                                            then starts src_off further) */
+    uint64_t in_off[MAX_STORAGE_TARGETS];/* offsets in the input slab (page layout, MAP and
+                                            DIRECT: of the file's first byte, page-aligned;
+                                            the data then starts src_off further) */
     uint64_t out_off;                    /* offset in the output slab */
     int batch;
 } task;
@@ -233,7 +233,9 @@ typedef struct {
 /* One read job: bytes [off, off + len) of source k's data, into dst (its
  * place in the slab + off).  Sources are read in pieces of at most PIECE
  * bytes, so a batch's big chunks spread over the io threads instead of one
- * thread finishing a 4 MiB chunk while the others idle. */
+ * thread finishing a 4 MiB chunk while the others idle.  DIRECT mode: off and
+ * len are of the file itself (page-aligned, the page layout puts the file's
+ * first byte at a page of the slab), read with O_DIRECT. */
 #define PIECE ((uint64_t)1 << 20)
 typedef struct {
     job j;
@@ -242,13 +244,24 @@ typedef struct {
     int k;                /* source */
     uint64_t off, len;
     uint8_t *dst;
-    uint64_t *bytes;      /* accumulated under lock */
+    uint64_t *bytes;      /* accumulated under lock: {data bytes, of them read with O_DIRECT,
+                             DIRECT pieces read through the page cache instead} */
     latch *done;
+    int direct;
 } read_arg;
 
 static uint64_t pieces_of(uint64_t size)
 {
     return (size + PIECE - 1) / PIECE;
+}
+
+/* Read jobs of source k: PIECE-sized pieces of its data, or (DIRECT) of the
+ * file prefix up to the data's end, page-rounded. */
+static uint64_t read_extent(const task *t, int k, int direct)
+{
+    if (!t->size[k])
+        return 0;
+    return direct ? RUP_PAGE(t->src_off[k] + t->size[k]) : t->size[k];
 }
 
 typedef struct {
@@ -390,28 +403,71 @@ static void do_read(job *p)
     read_arg *a = (read_arg *)p;
     task *t = a->t;
     const uint64_t want = a->len;
+    const uint64_t foff = a->direct ? a->off : t->src_off[a->k] + a->off; /* file offset of dst[0] */
     uint64_t got = 0;
+    int direct = 0, fell_back = 0;
     if (want) {
         char fn[4352];
         const int is_parity = t->rebuild && a->k == t->parity_src;
         chunk_file(fn, sizeof(fn), a->root, t->holders[a->k], is_parity ? "parity" : "chunks", t->path);
-        int fd = open(fn, O_RDONLY);
-        if (fd >= 0) {
-            posix_fadvise(fd, (off_t)(t->src_off[a->k] + a->off), (off_t)want, POSIX_FADV_SEQUENTIAL);
-            while (got < want) {
-                ssize_t r = pread(fd, a->dst + got, (size_t)(want - got), (off_t)(t->src_off[a->k] + a->off + got));
-                if (r <= 0)
-                    break;
-                got += (uint64_t)r;
-            }
-            close(fd);
+        int fd = -1;
+        if (a->direct) {
+            fd = open(fn, O_RDONLY | O_DIRECT);
+            direct = fd >= 0;
+            fell_back = !direct;
         }
-        /* a short read is zero padded, as chunk_sender does (:302-303) */
-        if (got < want)
-            memset(a->dst + got, 0, (size_t)(want - got));
+        if (fd < 0)
+            fd = open(fn, O_RDONLY);
+        if (fd >= 0) {
+            if (!direct)
+                posix_fadvise(fd, (off_t)foff, (off_t)want, POSIX_FADV_SEQUENTIAL);
+            while (got < want) {
+                ssize_t r = pread(fd, a->dst + got, (size_t)(want - got), (off_t)(foff + got));
+                if (r > 0)
+                    got += (uint64_t)r;
+                struct stat sb;
+                if (direct && (r < 0 || (got % PAGE && got < want && fstat(fd, &sb) == 0 &&
+                                         (uint64_t)sb.st_size > foff + got))) {
+                    /* refused (EINVAL: alignment the filesystem wants bigger,
+                     * EFAULT: memory it cannot pin) or short before the end
+                     * of the file: the rest of the piece through the page cache */
+                    close(fd);
+                    fd = open(fn, O_RDONLY);
+                    direct = 0;
+                    fell_back = 1;
+                    if (fd < 0)
+                        break;
+                    continue;
+                }
+                if (r <= 0 || (direct && got % PAGE))
+                    break; /* end of file (an O_DIRECT read ends short there) */
+            }
+            if (fd >= 0)
+                close(fd);
+        }
+    }
+    /* the source's data inside this piece; what the file no longer holds is
+     * zero padded, as chunk_sender does (:302-303) */
+    const uint64_t d_lo = a->direct ? t->src_off[a->k] : foff;
+    const uint64_t d_hi = a->direct ? d_lo + t->size[a->k] : foff + want;
+    const uint64_t lo = d_lo > foff ? d_lo : foff;
+    const uint64_t hi = d_hi < foff + want ? d_hi : foff + want;
+    const uint64_t have = foff + got;
+    uint64_t data = 0;
+    if (hi > lo) {
+        const uint64_t z = have > lo ? have : lo;
+        if (z < hi)
+            memset(a->dst + (z - foff), 0, (size_t)(hi - z));
+        data = (have < hi ? have : hi) > lo ? (have < hi ? have : hi) - lo : 0;
     }
     pthread_mutex_lock(&g_stat_lock);
-    *a->bytes += got;
+    a->bytes[0] += data;
+    if (a->direct) {
+        if (fell_back)
+            a->bytes[2]++;
+        else
+            a->bytes[1] += data;
+    }
     pthread_mutex_unlock(&g_stat_lock);
     latch_down(a->done);
 }
@@ -577,7 +633,7 @@ typedef struct {
 
 struct bcp_pipeline {
     bcp_pipeline_opts o;
-    int map_mode;       /* read_mode resolved: 1 = MAP */
+    int read_mode;      /* resolved: BCP_READ_COPY / MAP / DIRECT */
     double map_share;   /* MAP: share of a batch's input bytes mapped (adapted per batch) */
     pool releaser;      /* MAP: releases the ranges (one thread) */
     int ndev;
@@ -681,11 +737,14 @@ int bcp_pipeline_create(const bcp_pipeline_opts *opts_in, bcp_pipeline **out)
     bcp_pipeline_opts o = {0, 256u << 20, 0, 4, 1, BCP_READ_AUTO};
     if (opts_in)
         o = *opts_in;
-    if (o.read_mode < BCP_READ_AUTO || o.read_mode > BCP_READ_MAP)
+    if (o.read_mode < BCP_READ_AUTO || o.read_mode > BCP_READ_DIRECT)
         return -EINVAL;
     if (o.read_mode == BCP_READ_AUTO) {
         const char *env = getenv("BCP_PIPELINE_READ");
-        o.read_mode = (env && !strcmp(env, "map")) ? BCP_READ_MAP : BCP_READ_COPY;
+        o.read_mode = !env                     ? BCP_READ_COPY
+                      : !strcmp(env, "map")    ? BCP_READ_MAP
+                      : !strcmp(env, "direct") ? BCP_READ_DIRECT
+                                               : BCP_READ_COPY;
     }
     if (o.ndevices < 1)
         o.ndevices = 1;
@@ -713,7 +772,7 @@ int bcp_pipeline_create(const bcp_pipeline_opts *opts_in, bcp_pipeline **out)
     if (!pl)
         return -ENOMEM;
     pl->o = o;
-    pl->map_mode = o.read_mode == BCP_READ_MAP;
+    pl->read_mode = o.read_mode;
     pl->map_share = 0.3;
     int rc = 0;
     pl->dev = calloc((size_t)o.ndevices, sizeof(dev_lane));
@@ -740,7 +799,7 @@ int bcp_pipeline_create(const bcp_pipeline_opts *opts_in, bcp_pipeline **out)
     if ((rc = pool_start(&pl->completer, 1)))
         goto fail;
     pl->pools |= 4;
-    if (pl->map_mode) {
+    if (pl->read_mode == BCP_READ_MAP) {
         if ((rc = pool_start(&pl->releaser, 1)))
             goto fail;
         pl->pools |= 8;
@@ -758,8 +817,9 @@ static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, 
                          FILE *log, bcp_run_stats *stats, double t0);
 
 /* Bytes source k of t takes in the input slab: its data at 256-byte pitch
- * (COPY), or the whole file prefix up to the data's end at page pitch (MAP:
- * files are mapped from offset 0, the rebuild parity body sits 8n in). */
+ * (COPY), or the whole file prefix up to the data's end at page pitch (MAP and
+ * DIRECT: files are mapped / read from offset 0, the rebuild parity body sits
+ * 8n in). */
 static uint64_t span_of(const task *t, int k, int map_layout)
 {
     if (!map_layout)
@@ -907,7 +967,7 @@ static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, 
     }
     const int nslots = pl->o.nslots;
     int rc = 0, errors = 0, dev_rc = 0;
-    uint64_t bytes_read = 0, bytes_written = 0, ntasks = 0;
+    uint64_t rd[3] = {0, 0, 0}, bytes_written = 0, ntasks = 0; /* rd: see read_arg.bytes */
     const double t_stat = now_s();
     memset(&pl->last, 0, sizeof(pl->last)); /* a run that fails early reports zeros, not the previous run */
 
@@ -931,7 +991,8 @@ static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, 
 
     /* 2. plan batches: inputs at 256-byte pitch (MAP: page pitch), outputs
      * at 256 */
-    const int ml = pl->map_mode;
+    const int mapm = pl->read_mode == BCP_READ_MAP, dir = pl->read_mode == BCP_READ_DIRECT;
+    const int ml = mapm || dir; /* page layout */
     size_t in_cap = pl->in_cap, out_cap = pl->out_cap;
     for (size_t i = 0; i < nt; i++) {
         uint64_t in = 0;
@@ -1029,12 +1090,12 @@ static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, 
     size_t nreads_all = 0;
     for (size_t i = 0; i < nt; i++)
         for (int k = 0; k < tasks[i].n; k++)
-            nreads_all += (size_t)pieces_of(tasks[i].size[k]);
+            nreads_all += (size_t)pieces_of(read_extent(&tasks[i], k, dir));
     read_arg *ra = calloc(nreads_all ? nreads_all : 1, sizeof(read_arg));
     write_arg *wa = calloc(nt ? nt : 1, sizeof(write_arg));
     complete_arg *cargs = calloc(nbatches ? (size_t)nbatches : 1, sizeof(complete_arg));
-    map_range *maps = ml ? calloc(nbatches ? (size_t)nbatches : 1, sizeof(map_range)) : NULL;
-    if (!ra || !wa || !cargs || (ml && !maps)) {
+    map_range *maps = mapm ? calloc(nbatches ? (size_t)nbatches : 1, sizeof(map_range)) : NULL;
+    if (!ra || !wa || !cargs || (mapm && !maps)) {
         free(ra);
         free(wa);
         free(cargs);
@@ -1073,15 +1134,17 @@ static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, 
      * has been written); MAP mode: decide the mapped tail */
     #define PUSH_READS(B, A, Z)                                                                          \
         for (size_t i_ = (A); i_ < (Z); i_++)                                                              \
-            for (int k_ = 0; k_ < tasks[i_].n; k_++)                                                       \
-                for (uint64_t o_ = 0; o_ < tasks[i_].size[k_]; o_ += PIECE) {                              \
+            for (int k_ = 0; k_ < tasks[i_].n; k_++) {                                                     \
+                const uint64_t e_ = read_extent(&tasks[i_], k_, dir);                                      \
+                uint8_t *d_ = (B)->S->h_in + (dir ? tasks[i_].in_off[k_] : data_off(&tasks[i_], k_, ml));  \
+                for (uint64_t o_ = 0; o_ < e_; o_ += PIECE) {                                              \
                     read_arg *a_ = &ra[rnext++];                                                           \
-                    const uint64_t l_ = tasks[i_].size[k_] - o_ < PIECE ? tasks[i_].size[k_] - o_ : PIECE; \
-                    *a_ = (read_arg){{0}, store_root, &tasks[i_], k_, o_, l_,                              \
-                                     (B)->S->h_in + data_off(&tasks[i_], k_, ml) + o_, &bytes_read,        \
-                                     &(B)->S->reads};                                                      \
+                    const uint64_t l_ = e_ - o_ < PIECE ? e_ - o_ : PIECE;                                 \
+                    *a_ = (read_arg){{0}, store_root, &tasks[i_], k_, o_, l_, d_ + o_, rd,                 \
+                                     &(B)->S->reads, dir};                                                 \
                     pool_push(&pl->readers, &a_->j, do_read);                                              \
-                }
+                }                                                                                          \
+            }
     int started = 0; /* batches whose reads are queued */
     for (int b = 0; b < nbatches && !rc; b++) {
         for (; started < nbatches && started <= b + 1; started++) {
@@ -1108,7 +1171,7 @@ static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, 
              * threads read the head (within the caps on what is mapped at
              * once) */
             B->split = B->last;
-            if (ml && B->last > B->first && __atomic_load_n(&map_out[0], __ATOMIC_RELAXED) < MAP_OUT_BYTES_MAX &&
+            if (mapm && B->last > B->first && __atomic_load_n(&map_out[0], __ATOMIC_RELAXED) < MAP_OUT_BYTES_MAX &&
                 __atomic_load_n(&map_out[1], __ATOMIC_RELAXED) < MAP_OUT_FILES_MAX) {
                 const uint64_t from = in_used - (uint64_t)(pl->map_share * (double)in_used);
                 B->split = B->first;
@@ -1119,7 +1182,7 @@ static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, 
             long nreads = 0;
             for (size_t i = B->first; i < B->split; i++)
                 for (int k = 0; k < tasks[i].n; k++)
-                    nreads += (long)pieces_of(tasks[i].size[k]);
+                    nreads += (long)pieces_of(read_extent(&tasks[i], k, dir));
             B->tw = now_s();
             latch_init(&B->S->reads, nreads);
             B->reads_live = 1;
@@ -1180,7 +1243,7 @@ static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, 
             long n2 = 0;
             for (size_t i = split; i < last; i++)
                 for (int k = 0; k < tasks[i].n; k++)
-                    n2 += (long)pieces_of(tasks[i].size[k]);
+                    n2 += (long)pieces_of(read_extent(&tasks[i], k, dir));
             latch_init(&S->reads, n2);
             PUSH_READS(B, split, last);
             tm.read_jobs += (uint32_t)n2;
@@ -1193,7 +1256,7 @@ static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, 
                 for (int k = 0; k < tasks[i].n; k++)
                     got += tasks[i].size[k];
             pthread_mutex_lock(&g_stat_lock);
-            bytes_read += got;
+            rd[0] += got;
             pthread_mutex_unlock(&g_stat_lock);
             tm.mapped_bytes += in_used - reg_lo;
             /* next share: the two paths' rates in this batch, balanced so
@@ -1279,7 +1342,7 @@ static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, 
     /* no mapping outlives the run: the releaser's queue first (the
      * completions that pushed to it have all run: their writes latched
      * above), then whatever a failed submission left (the queues are idle) */
-    if (ml) {
+    if (mapm) {
         releaser_drain(&pl->releaser);
         for (size_t i = 0; i < nmaps; i++)
             map_release(&maps[i]);
@@ -1290,7 +1353,9 @@ static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, 
     free(cargs);
     free(maps);
     tm.drain = now_s() - td;
-    tm.read_mode = ml ? BCP_READ_MAP : BCP_READ_COPY;
+    tm.read_mode = pl->read_mode;
+    tm.direct_bytes = rd[1];
+    tm.direct_fallbacks = (uint32_t)rd[2];
     pl->last = tm;
     if (!rc && dev_rc)
         rc = dev_rc;
@@ -1298,7 +1363,7 @@ static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, 
         memset(stats, 0, sizeof(*stats));
         stats->seconds = now_s() - t0;
         stats->tasks = ntasks;
-        stats->bytes_read = bytes_read;
+        stats->bytes_read = rd[0];
         stats->bytes_written = bytes_written;
         stats->errors = errors;
     }

@@ -421,7 +421,7 @@ def e2e_leg(a, d, device: int, bus_id: str):
     import bcp_store as BS
     t_start = time.perf_counter()
     NT, W, VICTIM = 9, 8, 4
-    modes = [m for m in a.e2e_modes.split(",") if m in ("copy", "map")] or ["copy"]
+    modes = [m for m in a.e2e_modes.split(",") if m in ("copy", "map", "direct")] or ["copy"]
     base, want, reason = e2e_store_dir([a.e2e_dir], d.world, int(a.e2e_gib * GiB))
     rank_root = os.path.join(base, f"bcp_bench_e2e_{os.getppid()}_{d.rank}")
     # every rank agrees to run (or not): a rank that skipped would leave the
@@ -558,7 +558,7 @@ def e2e_leg(a, d, device: int, bus_id: str):
         link = guard("link probe", link_rates, {}) or {}
         for m in modes:
             pl = guard(f"pipeline ({m})", lambda: bcp.Pipeline(
-                device=device, read_mode={"copy": bcp.READ_COPY, "map": bcp.READ_MAP}[m]))
+                device=device, read_mode={"copy": bcp.READ_COPY, "map": bcp.READ_MAP, "direct": bcp.READ_DIRECT}[m]))
             if pl is not None:
                 pls[m] = pl
         # ---- gen: one cold run, then warm runs, the read paths interleaved

@@ -494,10 +494,18 @@ typedef struct {
  *     A batch whose mapping cannot be registered (a file truncated meanwhile)
  *     is read instead.
  *     Input offsets are page-aligned in this mode.
- *   AUTO (0): COPY; env BCP_PIPELINE_READ=copy|map overrides AUTO. */
+ *   DIRECT: the io threads read each chunk file with O_DIRECT straight into
+ *     the pinned slab (page layout as MAP): on a disk-backed store the
+ *     storage device's DMA fills the slab and no CPU copies the bytes.  A
+ *     file the filesystem will not read that way (open or read refused) is
+ *     read through the page cache instead, piece by piece.  O_DIRECT reads
+ *     bypass the page cache: for a store whose chunks are cached (just
+ *     written, or on tmpfs) COPY is the faster choice.
+ *   AUTO (0): COPY; env BCP_PIPELINE_READ=copy|map|direct overrides AUTO. */
 #define BCP_READ_AUTO 0
 #define BCP_READ_COPY 1
 #define BCP_READ_MAP 2
+#define BCP_READ_DIRECT 3
 
 /* Parity generation for local stores without per-task messaging: chunk
  * files are read by io threads into pinned slabs, copied H2D on a side
@@ -529,7 +537,8 @@ int bcp_pipeline_destroy(bcp_pipeline *pl);
  * batch to be written before queueing reads into it, building and submitting
  * batches, and the drain after the last submission; MAP mode: the host
  * thread's mapping + registering time, the bytes copied out of mappings, and
- * batches that fell back to reading. */
+ * batches that fell back to reading; DIRECT mode: the data bytes read with
+ * O_DIRECT and the pieces read through the page cache instead. */
 typedef struct {
     double stat, read_wait, slot_wait, submit, drain;
     uint32_t batches;    /* device batches */
@@ -537,7 +546,9 @@ typedef struct {
     double map;
     uint64_t mapped_bytes;
     uint32_t map_fallbacks;
-    int read_mode;       /* the mode the run used (BCP_READ_COPY / BCP_READ_MAP) */
+    int read_mode;       /* the mode the run used (BCP_READ_COPY / MAP / DIRECT) */
+    uint64_t direct_bytes;
+    uint32_t direct_fallbacks;
 } bcp_pipeline_timing;
 int bcp_pipeline_last_timing(const bcp_pipeline *pl, bcp_pipeline_timing *out);
 /* Rebuild of one lost target with the batched pipeline (do_file's selection

@@ -24,11 +24,12 @@ def gpu_fold(bcp, engine):
     bcp.task_shutdown()
 
 
-@pytest.fixture(params=["copy", "map"])
+@pytest.fixture(params=["copy", "map", "direct"])
 def read_path(request, monkeypatch):
-    """Both read paths of the batched pipeline (bcp_pipeline_opts.read_mode
+    """Every read path of the batched pipeline (bcp_pipeline_opts.read_mode
     AUTO resolves through BCP_PIPELINE_READ): chunks read into pinned slabs,
-    or a share of every batch mapped and copied from the page cache."""
+    a share of every batch mapped and copied from the page cache, or chunks
+    read with O_DIRECT into the slabs."""
     monkeypatch.setenv("BCP_PIPELINE_READ", request.param)
     return request.param
 
@@ -228,7 +229,8 @@ def test_pipeline_object_reuse_and_growth(bcp, oracle, tmp_path):
             for (path, holders, p, lens) in files:
                 assert S.read_file(S.parity_path(root, p, path)) == oracle.gen_parity_file(contents[path]), path
             # one io read job per 1 MiB piece of every chunk read into a slab
-            # (bcp_pipeline_last_timing); MAP mode reads only the unmapped ones
+            # (bcp_pipeline_last_timing); MAP mode reads only the unmapped ones;
+            # DIRECT reads the page-rounded file, the same pieces for a gen
             tm = pl.last_timing()
             pieces = sum((n + MiB - 1) // MiB for f in files for n in f[3])
             if os.environ.get("BCP_PIPELINE_READ") == "map":
@@ -698,13 +700,15 @@ def test_caller_transport_table_on_device(bcp, oracle, tmp_path, foreign_ops_add
         bcp.set_transport(None)
 
 
-@pytest.mark.parametrize("mode", ["map", "copy"])
+@pytest.mark.parametrize("mode", ["map", "copy", "direct"])
 def test_pipeline_read_modes_byte_identical_and_fallback(bcp, oracle, tmp_path, mode):
     """read_mode MAP: part of every batch goes to the device straight out of
     mapped chunk files (timing.mapped_bytes), the output is the COPY path's
     byte for byte; a chunk that cannot be opened (mode 000: stat works, open
     does not) makes its batch fall back to reading, with the same result --
-    the source counts as unreadable (zeros) exactly as in COPY mode."""
+    the source counts as unreadable (zeros) exactly as in COPY mode.  DIRECT:
+    every chunk is read with O_DIRECT (timing.direct_bytes), or through the
+    page cache where the filesystem refuses it, with the same output."""
     rng = np.random.default_rng(4242)
     nt = 9
     files = []
@@ -715,7 +719,7 @@ def test_pipeline_read_modes_byte_identical_and_fallback(bcp, oracle, tmp_path, 
     root = str(tmp_path / "store")
     items, contents = S.populate(root, nt, files, seed=17)
     bad = S.chunk_path(root, files[40][1][2], files[40][0])
-    want_mode = {"map": bcp.READ_MAP, "copy": bcp.READ_COPY}[mode]
+    want_mode = {"map": bcp.READ_MAP, "copy": bcp.READ_COPY, "direct": bcp.READ_DIRECT}[mode]
     outs = {}
     for locked in (False, True):
         if locked:
@@ -737,6 +741,15 @@ def test_pipeline_read_modes_byte_identical_and_fallback(bcp, oracle, tmp_path, 
                 assert tm["map_fallbacks"] == 0
         else:
             assert tm["mapped_bytes"] == 0 and tm["map_fallbacks"] == 0
+        if mode == "direct":
+            total = sum(sum(f[3]) for f in files)
+            # all of it with O_DIRECT, or pieces through the page cache (a
+            # filesystem without O_DIRECT; locked: the unopenable chunk)
+            assert tm["direct_bytes"] == st.bytes_read or tm["direct_fallbacks"] > 0, tm
+            if not locked:
+                assert st.bytes_read == total
+        else:
+            assert tm["direct_bytes"] == 0 and tm["direct_fallbacks"] == 0
         outs[locked] = {path: S.read_file(S.parity_path(root, p, path)) for path, _, p, _ in files}
     for path, holders, p, lens in files:
         assert outs[False][path] == oracle.gen_parity_file(contents[path]), path

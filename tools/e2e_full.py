@@ -15,6 +15,12 @@ One JSON line per measurement.
 interleaved run by run; --contend 0,16: with N host threads memcpy'ing
 64 MiB buffers meanwhile (host memory bandwidth taken, as by the other GPUs'
 pipelines of one node), also interleaved.
+
+--modes copy,direct --evict --root <a disk-backed directory>: every file of
+the store is written back and dropped from the page cache (fsync +
+POSIX_FADV_DONTNEED, untimed) before each timed run, so COPY reads from the
+disk through the page cache and DIRECT with O_DIRECT into the slabs -- the
+cold store a storage server sees, instead of the warm tmpfs of the default.
 """
 import argparse
 import concurrent.futures as cf
@@ -53,13 +59,18 @@ def main():
     ap.add_argument("--threads", type=int, default=16)
     ap.add_argument("--modes", default="copy")
     ap.add_argument("--contend", default="0")
+    ap.add_argument("--evict", action="store_true")
     a = ap.parse_args()
-    modes = {"copy": bcp.READ_COPY, "map": bcp.READ_MAP}
+    modes = {"copy": bcp.READ_COPY, "map": bcp.READ_MAP, "direct": bcp.READ_DIRECT}
     mode_list = a.modes.split(",")
     contend_list = [int(x) for x in a.contend.split(",")]
     import box_probe
     box = box_probe.cpu_info()
     box.update(box_probe.pcie_rates(bcp))
+    os.makedirs(a.root, exist_ok=True)
+    sf = os.statvfs(a.root)
+    box["store_root"] = a.root
+    box["store_free_GiB"] = round(sf.f_bavail * sf.f_frsize / GiB, 1)
     emit(box=box)
     C = a.chunk
     shutil.rmtree(a.root, ignore_errors=True)
@@ -121,6 +132,22 @@ def main():
             for t in self.th:
                 t.join()
 
+    def evict():
+        """Every file under the store: written back and dropped from the page cache."""
+        t0 = time.perf_counter()
+        names = [os.path.join(d, f) for d, _, fs in os.walk(a.root) for f in fs]
+
+        def drop(fn):
+            fd = os.open(fn, os.O_RDONLY)
+            try:
+                os.fsync(fd)
+                os.posix_fadvise(fd, 0, 0, os.POSIX_FADV_DONTNEED)
+            finally:
+                os.close(fd)
+        with cf.ThreadPoolExecutor(a.threads) as ex:
+            list(ex.map(drop, names))
+        return round(time.perf_counter() - t0, 2)
+
     pls = {m: bcp.Pipeline(read_mode=modes[m]) for m in mode_list}
     try:
         rd = a.stripes * 8 * C
@@ -136,6 +163,7 @@ def main():
             for nc in contend_list:
                 for m in mode_list:
                     pl = pls[m]
+                    ev = evict() if a.evict else None
                     with Contention(nc):
                         # ---- config 2: parity gen over the whole store
                         t0 = time.perf_counter()
@@ -150,6 +178,7 @@ def main():
                     # ---- config 3: lose target v, rebuild it (the deletion untimed)
                     with cf.ThreadPoolExecutor(a.threads) as ex:
                         list(ex.map(lambda i: os.remove(S.chunk_path(a.root, v, files[i][0])), lost))
+                    ev3 = evict() if a.evict else None
                     with Contention(nc):
                         t0 = time.perf_counter()
                         st = pl.rebuild(a.root, NT, v, ordered)
@@ -163,7 +192,7 @@ def main():
                     res.setdefault(key, {"gen": [], "rebuild": []})
                     res[key]["gen"].append(tg)
                     res[key]["rebuild"].append(tr)
-                    emit(rep=r, mode=m, contend=nc, gen_s=round(tg, 4), rebuild_s=round(tr, 4),
+                    emit(rep=r, mode=m, contend=nc, evict_s=[ev, ev3], gen_s=round(tg, 4), rebuild_s=round(tr, 4),
                          gen_GiBps=round((rd + wr) / tg / GiB, 2), rebuild_GiBps=round((rd3 + wr3) / tr / GiB, 2),
                          gen_input_over_link=round(rd / tg / h2d, 3), rebuild_input_over_link=round(rd3 / tr / h2d, 3),
                          gen_timing=tmg, rebuild_timing=tmr, verified=not bad and not bad3 and len(keep) > 0)
