@@ -6,7 +6,7 @@
  *   bcp find-all-chunks <chunks_dir>
  *       bp-find-all-chunks: the record stream on stdout.
  *   bcp parity-gen --complete|--partial [--pipeline|--protocol|--procs] [--fold MODE]
- *                  [--lanes N] [--force] [--changelog DIR] <store_root> <ntargets>
+ *                  [--read PATH] [--lanes N] [--force] [--changelog DIR] <store_root> <ntargets>
  *       beegfs-parity-gen + bp-parity-gen (src/beegfs-parity-gen:1-135,
  *       gen/main.c): target bookkeeping, phase 1 from a scan of every
  *       target (--complete) or from record files DIR/st<k> (--partial,
@@ -18,11 +18,13 @@
  *           ranks as threads) -- the reference's interface;
  *         --procs: the same with one process per target, as under mpirun.
  *       --fold picks the protocol P role's GPU fold: pipelined (default) or
- *       batched.  A --complete over an existing state needs --force and first
+ *       batched; --read the pipeline's read path (bcp_pipeline_opts.read_mode):
+ *       copy (default), map, or direct (O_DIRECT: for disk-backed stores whose
+ *       chunks are not in the page cache).  A --complete over an existing state needs --force and first
  *       deletes the old parity data and DBs (the script's clean_old,
  *       :94-108, :120-126).  On success <root>/last-gen-timestamp.
- *   bcp parity-rebuild [--pipeline|--protocol|--procs] [--fold MODE] [--lanes N] [--db DIR]
- *                      [--corrupt FILE] <store_root> <ntargets> <target>
+ *   bcp parity-rebuild [--pipeline|--protocol|--procs] [--fold MODE] [--read PATH] [--lanes N]
+ *                      [--db DIR] [--corrupt FILE] <store_root> <ntargets> <target>
  *       beegfs-parity-rebuild + bp-parity-rebuild (rebuild/main.c), through
  *       the batched pipeline (default), the per-rank protocol (--protocol)
  *       or rank processes (--procs).
@@ -47,15 +49,29 @@
 static int usage(void)
 {
     fputs("usage: bcp find-all-chunks <chunks_dir>\n"
-          "       bcp parity-gen --complete|--partial [--pipeline|--protocol|--procs] [--fold MODE] [--lanes N]\n"
-          "                      [--force] [--changelog DIR] <store_root> <ntargets>\n"
-          "       bcp parity-rebuild [--pipeline|--protocol|--procs] [--fold MODE] [--lanes N] [--db DIR]\n"
-          "                          [--corrupt FILE] <store_root> <ntargets> <target>\n"
+          "       bcp parity-gen --complete|--partial [--pipeline|--protocol|--procs] [--fold MODE] [--read PATH]\n"
+          "                      [--lanes N] [--force] [--changelog DIR] <store_root> <ntargets>\n"
+          "       bcp parity-rebuild [--pipeline|--protocol|--procs] [--fold MODE] [--read PATH] [--lanes N]\n"
+          "                          [--db DIR] [--corrupt FILE] <store_root> <ntargets> <target>\n"
           "       engine: --pipeline (default: batched pipeline on every GPU) | --protocol (per-rank\n"
           "               process_task, ranks as threads) | --procs (ranks as processes)\n"
-          "       MODE (protocol P-role fold): pipelined (default) | batched\n",
+          "       MODE (protocol P-role fold): pipelined (default) | batched\n"
+          "       PATH (pipeline read path): copy (default) | map | direct (O_DIRECT, cold disk stores)\n",
           stderr);
     return 1;
+}
+
+static int g_read_mode = BCP_READ_AUTO;
+
+static int read_mode_arg(const char *s)
+{
+    if (!strcmp(s, "copy"))
+        return BCP_READ_COPY;
+    if (!strcmp(s, "map"))
+        return BCP_READ_MAP;
+    if (!strcmp(s, "direct"))
+        return BCP_READ_DIRECT;
+    return -1;
 }
 
 static int fold_mode_arg(const char *s)
@@ -73,7 +89,7 @@ static int pipeline_on_all_gpus(bcp_pipeline **pl)
 {
     int ndev = 0;
     bcp_device_count(&ndev);
-    const bcp_pipeline_opts o = {0, (size_t)256 << 20, 0, 4, ndev > 0 ? ndev : 1, BCP_READ_AUTO};
+    const bcp_pipeline_opts o = {0, (size_t)256 << 20, 0, 4, ndev > 0 ? ndev : 1, g_read_mode};
     return bcp_pipeline_create(&o, pl);
 }
 
@@ -134,6 +150,10 @@ static int cmd_gen(int argc, char **argv)
             engines++, use_pipeline = 0, use_procs = 1;
         else if (!strcmp(argv[i], "--fold") && i + 1 < argc) {
             if (fold_mode_arg(argv[++i]) < 0 || bcp_task_set_fold_mode(fold_mode_arg(argv[i])) < 0)
+                return usage();
+        }
+        else if (!strcmp(argv[i], "--read") && i + 1 < argc) {
+            if ((g_read_mode = read_mode_arg(argv[++i])) < 0)
                 return usage();
         }
         else if (!strcmp(argv[i], "--force"))
@@ -262,6 +282,9 @@ static int cmd_rebuild(int argc, char **argv)
             engines++, use_pipeline = 0, use_procs = 1;
         else if (!strcmp(argv[i], "--fold") && i + 1 < argc) {
             if (fold_mode_arg(argv[++i]) < 0 || bcp_task_set_fold_mode(fold_mode_arg(argv[i])) < 0)
+                return usage();
+        } else if (!strcmp(argv[i], "--read") && i + 1 < argc) {
+            if ((g_read_mode = read_mode_arg(argv[++i])) < 0)
                 return usage();
         } else if (!strcmp(argv[i], "--lanes") && i + 1 < argc) {
             if (bcp_task_set_rebuild_lanes(atoi(argv[++i])) < 0) /* (the reference rebuilds with one) */

@@ -442,7 +442,8 @@ def test_rank_pool_on_device(tmp_path, mode):
     assert r.returncode == 0 and "pool ok" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]
 
 
-@pytest.mark.parametrize("engine_kind", ["default", "protocol", "pipeline", "procs", "procs_batched"])
+@pytest.mark.parametrize("engine_kind", ["default", "protocol", "pipeline", "pipeline_map", "pipeline_direct", "procs",
+                                         "procs_batched"])
 def test_cli_complete_partial_rebuild(bcp, oracle, tmp_path, engine_kind):
     """bin/bcp end to end on the device: --complete (scan of every target),
     --partial from changelog record files, then parity-rebuild from the DB --
@@ -465,12 +466,13 @@ def test_cli_complete_partial_rebuild(bcp, oracle, tmp_path, engine_kind):
             S.write_chunk(root, h, path, d)
             arrs.append(d)
         files[path], contents[path] = holders, arrs
-    flags = {"default": [], "protocol": ["--protocol"], "pipeline": ["--pipeline"], "procs": ["--procs"],
-             "procs_batched": ["--procs", "--fold", "batched"]}[engine_kind]
+    flags = {"default": [], "protocol": ["--protocol"], "pipeline": ["--pipeline"],
+             "pipeline_map": ["--pipeline", "--read", "map"], "pipeline_direct": ["--read", "direct"],
+             "procs": ["--procs"], "procs_batched": ["--procs", "--fold", "batched"]}[engine_kind]
     r = subprocess.run([bcp.BIN_PATH, "parity-gen", "--complete", *flags, root, str(nt)], capture_output=True)
     assert r.returncode == 0, r.stderr
-    engine_named = {"default": b"(pipeline)", "pipeline": b"(pipeline)", "protocol": b"(protocol)"}.get(
-        engine_kind, b"(rank processes)")
+    engine_named = {"protocol": b"(protocol)"}.get(
+        engine_kind, b"(rank processes)" if engine_kind.startswith("procs") else b"(pipeline)")
     assert engine_named in r.stdout, r.stdout  # the batched pipeline is the default engine
     db = bcp.PDB(os.path.join(root, "st0", "db"))
     placed = {k.decode(): loc for k, _, loc in db.items()}

@@ -87,6 +87,9 @@ def test_cli_usage_and_loud_failure_without_gpu(bcp, tmp_path):
     assert r.returncode == 1 and b"usage" in r.stderr
     r = subprocess.run([bcp.BIN_PATH, "parity-gen", str(tmp_path), "3"], capture_output=True)
     assert r.returncode == 1                         # neither --complete nor --partial
+    for bad in (["--read", "mmap"], ["--read"]):     # an unknown read path, a missing one
+        r = subprocess.run([bcp.BIN_PATH, "parity-gen", "--complete", *bad, str(tmp_path), "3"], capture_output=True)
+        assert r.returncode == 1 and b"usage" in r.stderr
     if bcp.device_count() > 0:
         pytest.skip("GPU present: the GPU run is in test_gpu_protocol.py")
     rng = np.random.default_rng(2)
