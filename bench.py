@@ -97,7 +97,7 @@ def parse():
     ap.add_argument("--e2e-reps", type=int, default=3, help="warm end-to-end gen runs (after one cold run)")
     ap.add_argument("--e2e-dir", default="/dev/shm", help="where the end-to-end stores are created")
     ap.add_argument("--e2e-max-s", type=float, default=150.0, help="wall-time cap of the end-to-end leg")
-    ap.add_argument("--e2e-modes", default="copy,map",
+    ap.add_argument("--e2e-modes", default="copy,map,direct",
                     help="pipeline read paths timed end to end, interleaved; the first is the headline")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-prof", action="store_true",
@@ -635,7 +635,7 @@ def e2e_leg(a, d, device: int, bus_id: str):
     gen, reb = by_mode[modes[0]]
     return {
         "path": ("bcp_pipeline_run / bcp_pipeline_rebuild on every rank's own GPU: chunk files (tmpfs) -> "
-                 "pinned slabs (io threads; read_mode map: part of every batch straight from the page cache) -> "
+                 "pinned slabs (io threads; read_mode map: part of every batch straight from the page cache; direct: O_DIRECT reads) -> "
                  "H2D on a side queue -> xor_desc -> D2H on a side queue -> parity files / rebuilt chunks"),
         "store": {"dir": os.path.dirname(rank_root), "shapes": "config 5: 8-wide stripes, chunks log-uniform "
                                                                "64 KiB-4 MiB, 9 targets, P rotating",

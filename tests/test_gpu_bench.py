@@ -97,8 +97,10 @@ def test_bench_gpus_n_launches_its_own_ranks(bcp, n):
     assert e2e["gen"]["verified"] is True and e2e["rebuild"]["verified"] is True
     assert e2e["gen"]["GiBps"] > 0 and e2e["rebuild"]["GiBps"] > 0
     assert e2e["gen"]["bytes_read"] == sum(r["bytes_read"] for r in e2e["per_rank"])
-    assert set(e2e["by_read_mode"]) == {"copy", "map"} and e2e["read_mode"] == "copy"
+    assert set(e2e["by_read_mode"]) == {"copy", "map", "direct"} and e2e["read_mode"] == "copy"
     assert e2e["by_read_mode"]["map"]["mapped_bytes_last_gen"] > 0
+    dt = e2e["by_read_mode"]["direct"]["gen_timing"]
+    assert dt["read_mode"] == 3 and (dt["direct_bytes"] > 0 or dt["direct_fallbacks"] > 0), dt
     if n == 2:
         live = line["roofline"]["live_profile"]
         assert live and "error" not in live and line["roofline"]["same_box"] is True, live
