@@ -11,7 +11,7 @@ against the originals.  Rates: (chunk bytes read + bytes written) / wall
 time; the host-to-device link's bound beside them (tools/box_probe.py).
 One JSON line per measurement.
 
---modes copy,map: the pipeline's read paths (bcp_pipeline_opts.read_mode),
+--modes copy,map,direct: the pipeline's read paths (bcp_pipeline_opts.read_mode),
 interleaved run by run; --contend 0,16: with N host threads memcpy'ing
 64 MiB buffers meanwhile (host memory bandwidth taken, as by the other GPUs'
 pipelines of one node), also interleaved.
