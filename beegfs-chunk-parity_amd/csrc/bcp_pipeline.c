@@ -423,6 +423,13 @@ static void do_read(job *p)
                 posix_fadvise(fd, (off_t)foff, (off_t)want, POSIX_FADV_SEQUENTIAL);
             while (got < want) {
                 ssize_t r = pread(fd, a->dst + got, (size_t)(want - got), (off_t)(foff + got));
+                if (direct && r > 3000 && bcpi_inject_hit(BCP_INJECT_DIRECT_READ)) {
+                    /* (failure injection) short before the end: what the read
+                     * did deliver past the cut is spoilt, the fallback must
+                     * read it again */
+                    memset(a->dst + got + 3000, 0xA5, (size_t)r - 3000);
+                    r = 3000;
+                }
                 if (r > 0)
                     got += (uint64_t)r;
                 struct stat sb;

@@ -151,7 +151,7 @@ static void settings_now(task_settings *s)
 }
 
 /* ---- failure injection (tests) ------------------------------------------ */
-#define NSITES 6
+#define NSITES 7
 static int g_inj_after[NSITES], g_inj_count[NSITES];
 
 static int site_index(int site)
@@ -163,6 +163,7 @@ static int site_index(int site)
     case BCP_INJECT_THREAD: return 3;
     case BCP_INJECT_READ: return 4;
     case BCP_INJECT_FOLD_SERVER: return 5;
+    case BCP_INJECT_DIRECT_READ: return 6;
     default: return -1;
     }
 }

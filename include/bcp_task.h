@@ -195,13 +195,17 @@ void bcp_task_set_xor_hook(bcp_xor_hook_fn fn, void *ctx);
  * fills directly (as EIO; a source reading in pieces for a PIPELINED P role
  * fails a piece after the first), and the node fold server dropping a rank's
  * connection instead of answering a fold (the server process takes the
- * setting when a rank pool forks it).  count 0 clears the site. */
+ * setting when a rank pool forks it), and the pipeline's O_DIRECT read of a
+ * piece ending short before the end of its file (DIRECT read mode: the rest
+ * of the piece is then read through the page cache).  count 0 clears the
+ * site. */
 #define BCP_INJECT_FOLD_RES 1
 #define BCP_INJECT_DRAIN_ROW 2
 #define BCP_INJECT_SEND_BUF 4
 #define BCP_INJECT_THREAD 8
 #define BCP_INJECT_READ 16
 #define BCP_INJECT_FOLD_SERVER 32
+#define BCP_INJECT_DIRECT_READ 64
 int bcp_task_inject_failure(int site, int after, int count);
 
 /* ---- transport seam (the MPI subset process_task speaks) ---------------- */

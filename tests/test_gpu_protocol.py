@@ -766,6 +766,59 @@ def test_pipeline_read_modes_byte_identical_and_fallback(bcp, oracle, tmp_path, 
     assert np.array_equal(body, ref)
 
 
+@pytest.mark.parametrize("slab", ["registered", "hipHostMalloc"])
+def test_pipeline_direct_reads_fall_back_piece_by_piece(bcp, oracle, tmp_path, monkeypatch, slab):
+    """DIRECT read mode: an O_DIRECT read that ends short before the end of
+    its file (injected: the bytes it did deliver past the cut are spoilt) is
+    finished through the page cache from the cut -- the same parity files and
+    rebuilt chunks, one fallback per injected piece.  Over either kind of
+    pinned slab (BCP_HOST_REGISTERED: registered THP memory, the default, or
+    hipHostMalloc'd memory, which O_DIRECT may refuse: then every piece falls
+    back, with the same output)."""
+    monkeypatch.setenv("BCP_HOST_REGISTERED", "1" if slab == "registered" else "0")
+    rng = np.random.default_rng(99)
+    nt = 9
+    files = []
+    for i in range(40):
+        holders, p = S.random_layout(rng, nt, 8)
+        lens = [int(x) for x in rng.integers(1, 3 * MiB, size=8)]
+        files.append((f"d/{i % 5}/c{i}", holders, p, lens))
+    root = str(tmp_path / "store")
+    items, contents = S.populate(root, nt, files, seed=23)
+    pl = bcp.Pipeline(slab_bytes=16 << 20, io_threads=4, nslots=3, read_mode=bcp.READ_DIRECT)
+    try:
+        bcp.inject_failure(bcp.INJECT_DIRECT_READ, 5, 3)
+        st = pl.run(root, nt, items)
+        tm = pl.last_timing()
+        bcp.inject_failure(bcp.INJECT_DIRECT_READ, 0, 0)
+        assert st.errors == 0 and st.tasks == len(files)
+        assert st.bytes_read == sum(sum(f[3]) for f in files)
+        if tm["direct_bytes"]:  # O_DIRECT worked: exactly the injected pieces fell back
+            assert tm["direct_fallbacks"] == 3, tm
+        else:
+            assert tm["direct_fallbacks"] > 3, tm
+        for path, holders, p, lens in files:
+            assert S.read_file(S.parity_path(root, p, path)) == oracle.gen_parity_file(contents[path]), path
+        # rebuild through the same fallback (parity bodies start 8n into their files)
+        victim = 4
+        lost = {path: S.read_file(S.chunk_path(root, victim, path)) for path, holders, _, _ in files
+                if victim in holders}
+        for path in lost:
+            os.remove(S.chunk_path(root, victim, path))
+        bcp.inject_failure(bcp.INJECT_DIRECT_READ, 2, 2)
+        st = pl.rebuild(root, nt, victim, sorted(items, key=lambda x: x[0].encode()))
+        tm = pl.last_timing()
+        bcp.inject_failure(bcp.INJECT_DIRECT_READ, 0, 0)
+        assert st.errors == 0 and st.tasks == len(lost)
+        if tm["direct_bytes"]:
+            assert tm["direct_fallbacks"] == 2, tm
+        for path, data in lost.items():
+            assert S.read_file(S.chunk_path(root, victim, path)) == data, path
+    finally:
+        bcp.inject_failure(bcp.INJECT_DIRECT_READ, 0, 0)
+        pl.close()
+
+
 @pytest.mark.usefixtures("read_path")
 def test_pipeline_overwrites_shorter_parity_files_exactly(bcp, oracle, tmp_path):
     """Parity files are overwritten in place and cut to their new length: a
