@@ -36,6 +36,7 @@
 #include <errno.h>
 #include <fcntl.h>
 #include <pthread.h>
+#include <sched.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -736,6 +737,39 @@ static int ensure_slots(bcp_pipeline *pl, size_t in_cap, size_t out_cap)
     return 0;
 }
 
+/* CPUs this process may use: its affinity mask, capped by the cgroup's CPU
+ * quota (v2 cpu.max, else v1 cfs). */
+static int usable_cpus(void)
+{
+    cpu_set_t set;
+    int n = sched_getaffinity(0, sizeof(set), &set) == 0 ? CPU_COUNT(&set) : 0;
+    if (n <= 0)
+        n = (int)sysconf(_SC_NPROCESSORS_ONLN);
+    long long q = -1, per = 0;
+    FILE *f = fopen("/sys/fs/cgroup/cpu.max", "r");
+    if (f) {
+        char qs[32];
+        if (fscanf(f, "%31s %lld", qs, &per) == 2 && strcmp(qs, "max"))
+            q = atoll(qs);
+        fclose(f);
+    } else if ((f = fopen("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", "r"))) {
+        if (fscanf(f, "%lld", &q) != 1)
+            q = -1;
+        fclose(f);
+        if ((f = fopen("/sys/fs/cgroup/cpu/cpu.cfs_period_us", "r"))) {
+            if (fscanf(f, "%lld", &per) != 1)
+                per = 0;
+            fclose(f);
+        }
+    }
+    if (q > 0 && per > 0) {
+        const long long c = (q + per / 2) / per;
+        if (c >= 1 && c < n)
+            n = (int)c;
+    }
+    return n > 0 ? n : 1;
+}
+
 int bcp_pipeline_create(const bcp_pipeline_opts *opts_in, bcp_pipeline **out)
 {
     if (!out)
@@ -758,9 +792,15 @@ int bcp_pipeline_create(const bcp_pipeline_opts *opts_in, bcp_pipeline **out)
     /* io threads 0 = auto: 8 readers and 8 writers per GPU.  One GPU's PCIe
      * link takes what ~8 threads copy out of the page cache (8 beat 16 on a
      * 16-CPU share, profiles/r02/protocol/pipeline_io_threads_ab_r2e4.jsonl),
-     * and every further GPU brings its own link and its own CPU share. */
-    if (o.io_threads == 0)
+     * and every further GPU brings its own link and its own CPU share -- but
+     * never more readers (and writers) than half the CPUs this process may
+     * run on: beyond that the threads only measure oversubscription. */
+    if (o.io_threads == 0) {
+        const int half = usable_cpus() / 2;
         o.io_threads = 8 * o.ndevices;
+        if (o.io_threads > half)
+            o.io_threads = half > 2 ? half : 2;
+    }
     int ndev_vis = 0;
     bcp_device_count(&ndev_vis);
     if (o.device < 0 || o.ndevices > 64)

@@ -552,13 +552,18 @@ def e2e_leg(a, d, device: int, bus_id: str):
             good = good and st.bytes_read == rd
         return (dt, dmax, tim), good
 
+    # every rank's pipeline in the host's CPU share: readers and writers each
+    # half of the rank's part of it, 2..8 (the library's own rule for one
+    # process, which cannot see its sibling ranks)
+    io_threads = max(2, min(8, usable_cpus()[0] // (2 * d.world)))
     try:
         t_store = guard("writing the store", write_store, 0.0)
         d.barrier()
         link = guard("link probe", link_rates, {}) or {}
         for m in modes:
             pl = guard(f"pipeline ({m})", lambda: bcp.Pipeline(
-                device=device, read_mode={"copy": bcp.READ_COPY, "map": bcp.READ_MAP, "direct": bcp.READ_DIRECT}[m]))
+                device=device, io_threads=io_threads,
+                read_mode={"copy": bcp.READ_COPY, "map": bcp.READ_MAP, "direct": bcp.READ_DIRECT}[m]))
             if pl is not None:
                 pls[m] = pl
         # ---- gen: one cold run, then warm runs, the read paths interleaved
@@ -641,6 +646,7 @@ def e2e_leg(a, d, device: int, bus_id: str):
                                                                "64 KiB-4 MiB, 9 targets, P rotating",
                   "stripes_per_rank": ranks[0]["stripes"], "chunk_GiB_per_rank": round(ranks[0]["bytes_read"] / GiB, 3)},
         "ranks": d.world,
+        "io_threads_per_rank": io_threads,
         "read_mode": modes[0],
         "gen": gen,
         "rebuild": reb,

@@ -478,7 +478,8 @@ int bcp_gen_round_procs(const char *store_root, int ntargets, const bcp_eventset
 typedef struct {
     int device;          /* HIP device */
     size_t slab_bytes;   /* pinned / device slab per slot (grown to the largest stripe) */
-    int io_threads;      /* reader and writer threads (each); 0 = 8 per GPU (capped at 64) */
+    int io_threads;      /* reader and writer threads (each); 0 = 8 per GPU, at most half the
+                            CPUs the process may use (affinity, cgroup quota), at least 2 (capped at 64) */
     int nslots;          /* slabs in flight per device (2..8) */
     int ndevices;        /* GPUs device .. device+ndevices-1 (mod the visible count),
                             batches round-robin (0 = 1) */

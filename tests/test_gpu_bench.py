@@ -94,6 +94,7 @@ def test_bench_gpus_n_launches_its_own_ranks(bcp, n):
     assert cpu["legs"][0]["threads"] == 1 and "quota_cpus" in cpu
     e2e = line["e2e"]
     assert e2e["ranks"] == n and len(e2e["per_rank"]) == n
+    assert 2 <= e2e["io_threads_per_rank"] <= 8  # the ranks share the host's CPU quota
     assert e2e["gen"]["verified"] is True and e2e["rebuild"]["verified"] is True
     assert e2e["gen"]["GiBps"] > 0 and e2e["rebuild"]["GiBps"] > 0
     assert e2e["gen"]["bytes_read"] == sum(r["bytes_read"] for r in e2e["per_rank"])
