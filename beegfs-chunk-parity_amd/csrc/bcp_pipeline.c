@@ -1341,8 +1341,10 @@ static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, 
             (rc = bcp_queue_wait_event(L->qd, S->ev_k)) ||
             (rc = bcp_d2h_async(L->qd, S->h_out, S->d_out, (size_t)out_used)) ||
             (rc = bcp_event_record(S->ev_d, L->qd))) {
-            if (batch_map) /* never submitted: nothing on the device reads it */
+            if (batch_map) { /* its copy may have been queued before the failing call */
+                bcp_queue_sync(L->qh);
                 map_release(batch_map);
+            }
             break;
         }
         /* writers start once the batch's D2H is done (completion thread);
