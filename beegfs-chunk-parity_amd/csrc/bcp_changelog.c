@@ -463,17 +463,26 @@ int bcp_plan_rounds(const bcp_eventset *s, int ntargets, const int *cum_weight, 
         free(eater);
         return -ENOMEM;
     }
-    for (size_t i = 0; i < s->n; i++)
+    /* bucket by eater in one pass (arrival order kept inside each bucket) */
+    size_t start[MAX_STORAGE_TARGETS + 1] = {0};
+    for (size_t i = 0; i < s->n; i++) {
         eater[i] = bcp_path_hash(s->e[i].path, strlen(s->e[i].path)) % (uint32_t)ntargets;
+        start[eater[i] + 1]++;
+    }
+    for (int k = 0; k < ntargets; k++)
+        start[k + 1] += start[k];
+    {
+        size_t fill[MAX_STORAGE_TARGETS];
+        memcpy(fill, start, sizeof(fill));
+        for (size_t i = 0; i < s->n; i++)
+            order[fill[eater[i]]++] = (size_index){s->e[i].size, i};
+    }
     size_t j = 0;
     for (int k = 0; k < ntargets; k++) {
         if (round_start)
             round_start[k] = j;
-        size_t m = 0;
+        const size_t m = start[k + 1] - start[k];
         size_index *mine = order + j;
-        for (size_t i = 0; i < s->n; i++)
-            if (eater[i] == (uint32_t)k)
-                mine[m++] = (size_index){s->e[i].size, i};
         /* shuffle (gen/main.c:373-386, a fresh fixed-seed generator per
          * eater) then sort by total size */
         if (m > 1) {
