@@ -6,7 +6,11 @@
 // flavour): plain / nt stores keep the line in the XCD's L2, sc1 / sc0 sc1
 // drop it; nt / sc1 loads bypass L1.  Variants, same tile body otherwise:
 //   LD 0 nt, 1 plain;  ST 0 nt, 1 plain, 2 sc1, 3 sc0 sc1, 4 nt sc1
-// (ST >= 2 through inline `global_store_dwordx4 ... off <bits>`, vector stores).
+// (ST >= 2 through inline `global_store_dwordx4 ... off <bits>`, vector stores.
+// Measured r4af: those three wrote WRONG bytes -- the compiler does not track
+// the store-data hazard of an inline-asm store, so a following VALU may
+// overwrite the data VGPRs before the store reads them; their times are not
+// evidence.  The compiler-generated variants (nt / plain) are exact.)
 //
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -Ibeegfs-chunk-parity_amd/csrc -Iinclude \
 //         tools/exp/xor_exp7.hip -o tools/exp/xor_exp7
@@ -163,6 +167,7 @@ int main(int argc, char **argv) {
       const int v = r % 2 ? nv - 1 - i : i;  // alternate the order round by round
       if (r == 0) {
         CK(hipMemsetAsync(dst, 0, out_bytes, st));
+        CK(hipMemsetAsync(dcount, 0, 8, st));  // (launch_compare accumulates)
         launch(v, dst);
         CK(bcp::launch_compare(st, grid, dst, ref, out_bytes, dcount));
         unsigned long long h;
