@@ -19,8 +19,8 @@
  *         --procs: the same with one process per target, as under mpirun.
  *       --fold picks the protocol P role's GPU fold: pipelined (default) or
  *       batched; --read the pipeline's read path (bcp_pipeline_opts.read_mode):
- *       copy (default), map, or direct (O_DIRECT: for disk-backed stores whose
- *       chunks are not in the page cache).  A --complete over an existing state needs --force and first
+ *       auto (default: copy for stores in memory, direct for a cold store on a
+ *       disk), copy, map, or direct (O_DIRECT into the pinned slabs).  A --complete over an existing state needs --force and first
  *       deletes the old parity data and DBs (the script's clean_old,
  *       :94-108, :120-126).  On success <root>/last-gen-timestamp.
  *   bcp parity-rebuild [--pipeline|--protocol|--procs] [--fold MODE] [--read PATH] [--lanes N]
@@ -56,7 +56,8 @@ static int usage(void)
           "       engine: --pipeline (default: batched pipeline on every GPU) | --protocol (per-rank\n"
           "               process_task, ranks as threads) | --procs (ranks as processes)\n"
           "       MODE (protocol P-role fold): pipelined (default) | batched\n"
-          "       PATH (pipeline read path): copy (default) | map | direct (O_DIRECT, cold disk stores)\n",
+          "       PATH (pipeline read path): auto (default: copy in memory, direct for cold disk stores) | copy |\n"
+          "            map | direct (O_DIRECT)\n",
           stderr);
     return 1;
 }
@@ -65,6 +66,8 @@ static int g_read_mode = BCP_READ_AUTO;
 
 static int read_mode_arg(const char *s)
 {
+    if (!strcmp(s, "auto"))
+        return BCP_READ_AUTO;
     if (!strcmp(s, "copy"))
         return BCP_READ_COPY;
     if (!strcmp(s, "map"))

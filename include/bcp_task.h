@@ -506,7 +506,11 @@ typedef struct {
  *     read through the page cache instead, piece by piece.  O_DIRECT reads
  *     bypass the page cache: for a store whose chunks are cached (just
  *     written, or on tmpfs) COPY is the faster choice.
- *   AUTO (0): COPY; env BCP_PIPELINE_READ=copy|map|direct overrides AUTO. */
+ *   AUTO (0): chosen per run between COPY and DIRECT -- COPY on tmpfs / ramfs
+ *     or when a sample of the run's chunks (mincore over the first 16 MiB of
+ *     one source in each of up to 64 tasks) is mostly in the page cache,
+ *     DIRECT otherwise (a cold store on a disk); bcp_pipeline_timing.read_mode
+ *     says which.  Env BCP_PIPELINE_READ=copy|map|direct names a mode instead. */
 #define BCP_READ_AUTO 0
 #define BCP_READ_COPY 1
 #define BCP_READ_MAP 2

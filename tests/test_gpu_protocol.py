@@ -819,6 +819,87 @@ def test_pipeline_direct_reads_fall_back_piece_by_piece(bcp, oracle, tmp_path, m
         pl.close()
 
 
+def _resident_fraction(paths):
+    """Page-cache residency of files: mincore over a read-only mapping of each
+    (mapping does not fault the pages in)."""
+    import ctypes
+    libc = ctypes.CDLL(None, use_errno=True)
+    libc.mmap.restype = ctypes.c_void_p
+    libc.mmap.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_long]
+    libc.munmap.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+    libc.mincore.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_char_p]
+    PROT_READ, MAP_SHARED = 1, 1
+    pages = resident = 0
+    for p in paths:
+        n = os.path.getsize(p)
+        if not n:
+            continue
+        fd = os.open(p, os.O_RDONLY)
+        addr = libc.mmap(None, n, PROT_READ, MAP_SHARED, fd, 0)
+        os.close(fd)
+        if addr in (None, ctypes.c_void_p(-1).value):
+            continue
+        np_ = (n + 4095) // 4096
+        vec = ctypes.create_string_buffer(np_)
+        if libc.mincore(addr, n, vec) == 0:
+            pages += np_
+            resident += sum(b & 1 for b in vec.raw[:np_])
+        libc.munmap(addr, n)
+    return resident / pages if pages else 1.0
+
+
+def test_pipeline_auto_read_path_follows_the_page_cache(bcp, oracle, tmp_path, monkeypatch):
+    """read_mode AUTO picks per run: COPY while the chunks are in the page
+    cache (just written) or on tmpfs, DIRECT once they are not (written back
+    and dropped: a cold store on a disk) -- the same parity files either way
+    (bcp_pipeline_timing.read_mode says which path ran)."""
+    monkeypatch.delenv("BCP_PIPELINE_READ", raising=False)
+    rng = np.random.default_rng(5)
+    nt = 9
+    files = []
+    for i in range(24):
+        holders, p = S.random_layout(rng, nt, 8)
+        files.append((f"a/{i % 3}/c{i}", holders, p, [int(x) for x in rng.integers(1, 2 * MiB, size=8)]))
+    stores = {"disk": str(tmp_path / "store")}
+    if os.path.isdir("/dev/shm"):
+        stores["shm"] = f"/dev/shm/bcp_auto_{os.getpid()}"
+    pl = bcp.Pipeline(slab_bytes=16 << 20, io_threads=4, nslots=3)
+    try:
+        for kind, root in stores.items():
+            items, contents = S.populate(root, nt, files, seed=8)
+            chunks = [S.chunk_path(root, h, path) for path, holders, _, _ in files for h in holders]
+            for cold in (False, True):
+                if cold:
+                    for c in chunks:
+                        fd = os.open(c, os.O_RDONLY)
+                        os.fsync(fd)
+                        os.posix_fadvise(fd, 0, 0, os.POSIX_FADV_DONTNEED)
+                        os.close(fd)
+                frac = _resident_fraction(chunks)
+                st = pl.run(root, nt, items)
+                tm = pl.last_timing()
+                assert st.errors == 0 and st.tasks == len(files)
+                for path, holders, p, lens in files:
+                    assert S.read_file(S.parity_path(root, p, path)) == oracle.gen_parity_file(contents[path])
+                if kind == "shm":
+                    assert tm["read_mode"] == bcp.READ_COPY, (kind, cold, frac, tm)
+                elif frac > 0.9:  # (a filesystem that keeps the pages, e.g. tmpfs: COPY;
+                    # the decision samples a subset: clear cases only)
+                    assert tm["read_mode"] == bcp.READ_COPY, (kind, cold, frac, tm)
+                elif frac < 0.1:
+                    assert tm["read_mode"] == bcp.READ_DIRECT, (kind, cold, frac, tm)
+                    assert tm["direct_bytes"] > 0 or tm["direct_fallbacks"] > 0, tm
+                assert tm["read_mode"] in (bcp.READ_COPY, bcp.READ_DIRECT)
+            if kind == "shm":
+                import shutil
+                shutil.rmtree(root, ignore_errors=True)
+    finally:
+        pl.close()
+        if "shm" in stores:
+            import shutil
+            shutil.rmtree(stores["shm"], ignore_errors=True)
+
+
 @pytest.mark.usefixtures("read_path")
 def test_pipeline_overwrites_shorter_parity_files_exactly(bcp, oracle, tmp_path):
     """Parity files are overwritten in place and cut to their new length: a
