@@ -878,6 +878,7 @@ def test_pipeline_auto_read_path_follows_the_page_cache(bcp, oracle, tmp_path, m
                 frac = _resident_fraction(chunks)
                 st = pl.run(root, nt, items)
                 tm = pl.last_timing()
+                print(f"auto read path: {kind} cold={cold} resident={frac:.2f} -> mode {tm['read_mode']}")
                 assert st.errors == 0 and st.tasks == len(files)
                 for path, holders, p, lens in files:
                     assert S.read_file(S.parity_path(root, p, path)) == oracle.gen_parity_file(contents[path])
