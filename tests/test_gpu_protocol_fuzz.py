@@ -89,6 +89,16 @@ def fuzz_rounds(bcp, oracle, tmp_path, budget, seed, engines):
             read_mode = int(rng.choice([bcp.READ_AUTO, bcp.READ_COPY, bcp.READ_MAP, bcp.READ_DIRECT]))  # the pipeline's read path
             if how == "pipeline":
                 what += f" read_mode {read_mode}"
+                if rng.random() < 0.3:  # a cold store: written back and dropped (AUTO then reads with O_DIRECT)
+                    what += " cold"
+                    for path, holders, _, _ in files:
+                        for h in holders:
+                            c = S.chunk_path(root, h, path)
+                            if os.path.exists(c):
+                                fd = os.open(c, os.O_RDONLY)
+                                os.fsync(fd)
+                                os.posix_fadvise(fd, 0, 0, os.POSIX_FADV_DONTNEED)
+                                os.close(fd)
                 st = bcp.pipeline_gen(root, ntargets, items, slab_bytes=int(rng.choice([1, 8, 64])) << 20,
                                       io_threads=int(rng.integers(1, 9)), nslots=int(rng.integers(2, 5)),
                                       read_mode=read_mode)
@@ -124,6 +134,8 @@ def fuzz_rounds(bcp, oracle, tmp_path, budget, seed, engines):
             seen.add((how, rb))
             rounds += 1
             files_done += len(files)
+            if rounds % 100 == 0:
+                print(f"protocol fuzz: {rounds} rounds ...", flush=True)  # progress for long soaks
             shutil.rmtree(root, ignore_errors=True)
     finally:
         bcp.set_fold_mode(prev[0])
