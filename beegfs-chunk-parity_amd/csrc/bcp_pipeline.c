@@ -78,6 +78,7 @@ typedef struct {
     pthread_mutex_t lock;
     pthread_cond_t cv;
     job *head, *tail;
+    job *hhead, *htail;   /* taken first (pool_push_hi) */
     int stop;
     int nthreads;
     pthread_t *th;
@@ -88,16 +89,22 @@ static void *pool_main(void *p)
     pool *P = p;
     for (;;) {
         pthread_mutex_lock(&P->lock);
-        while (!P->head && !P->stop)
+        while (!P->head && !P->hhead && !P->stop)
             pthread_cond_wait(&P->cv, &P->lock);
-        job *j = P->head;
+        job *j = P->hhead ? P->hhead : P->head;
         if (!j) {
             pthread_mutex_unlock(&P->lock);
             return NULL;
         }
-        P->head = j->next;
-        if (!P->head)
-            P->tail = NULL;
+        if (j == P->hhead) {
+            P->hhead = j->next;
+            if (!P->hhead)
+                P->htail = NULL;
+        } else {
+            P->head = j->next;
+            if (!P->head)
+                P->tail = NULL;
+        }
         pthread_mutex_unlock(&P->lock);
         j->fn(j);
     }
@@ -137,6 +144,21 @@ static void pool_push(pool *P, job *j, void (*fn)(job *))
     else
         P->head = j;
     P->tail = j;
+    pthread_cond_signal(&P->cv);
+    pthread_mutex_unlock(&P->lock);
+}
+
+/* The same, ahead of every job pushed with pool_push. */
+static void pool_push_hi(pool *P, job *j, void (*fn)(job *))
+{
+    j->fn = fn;
+    j->next = NULL;
+    pthread_mutex_lock(&P->lock);
+    if (P->htail)
+        P->htail->next = j;
+    else
+        P->hhead = j;
+    P->htail = j;
     pthread_cond_signal(&P->cv);
     pthread_mutex_unlock(&P->lock);
 }
@@ -308,6 +330,7 @@ typedef struct {
     int *errors;
     int *dev_rc;
     int prealloc;
+    int hi;               /* writers share the readers' pool: writes go ahead of reads */
 } complete_arg;
 
 static pthread_mutex_t g_stat_lock = PTHREAD_MUTEX_INITIALIZER;
@@ -580,7 +603,10 @@ static void do_complete(job *p)
             write_arg *w = &a.wa[i];
             *w = (write_arg){{0}, a.root, &a.tasks[i], a.S->h_out + a.tasks[i].out_off, &a.S->writes, a.log, a.errors,
                              a.prealloc};
-            pool_push(a.writers, &w->j, do_write);
+            if (a.hi)
+                pool_push_hi(a.writers, &w->j, do_write);
+            else
+                pool_push(a.writers, &w->j, do_write);
         }
     }
 }
@@ -647,6 +673,7 @@ struct bcp_pipeline {
     int ndev;
     dev_lane *dev;
     pool readers, writers, completer;
+    int shared_io;      /* one pool of 2 x io_threads for reads and writes (writes first) */
     int pools;
     size_t in_cap, out_cap;
     bcp_stripe *st;
@@ -838,12 +865,18 @@ int bcp_pipeline_create(const bcp_pipeline_opts *opts_in, bcp_pipeline **out)
             (rc = bcp_queue_create(L->eng, &L->qk)) || (rc = bcp_queue_create(L->eng, &L->qd)))
             goto fail;
     }
-    if ((rc = pool_start(&pl->readers, o.io_threads)))
+    {
+        const char *sh = getenv("BCP_PIPELINE_SHARED_IO");
+        pl->shared_io = sh && atoi(sh) != 0;
+    }
+    if ((rc = pool_start(&pl->readers, pl->shared_io ? 2 * o.io_threads : o.io_threads)))
         goto fail;
     pl->pools |= 1;
-    if ((rc = pool_start(&pl->writers, o.io_threads)))
-        goto fail;
-    pl->pools |= 2;
+    if (!pl->shared_io) {
+        if ((rc = pool_start(&pl->writers, o.io_threads)))
+            goto fail;
+        pl->pools |= 2;
+    }
     if ((rc = pool_start(&pl->completer, 1)))
         goto fail;
     pl->pools |= 4;
@@ -1401,8 +1434,9 @@ static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, 
         latch_init(&S->writes, (long)(last - first));
         S->busy = 1;
         complete_arg *ca = &cargs[b];
-        *ca = (complete_arg){{0}, S, batch_map, &pl->releaser, store_root, tasks, wa, first, last, &pl->writers, log,
-                             &errors, &dev_rc, prealloc};
+        *ca = (complete_arg){{0}, S, batch_map, &pl->releaser, store_root, tasks, wa, first, last,
+                             pl->shared_io ? &pl->readers : &pl->writers, log,
+                             &errors, &dev_rc, prealloc, pl->shared_io};
         pool_push(&pl->completer, &ca->j, do_complete);
         for (size_t i = first; i < last; i++)
             bytes_written += (tasks[i].rebuild ? 0 : 8u * (uint64_t)tasks[i].n) + tasks[i].out_len;
