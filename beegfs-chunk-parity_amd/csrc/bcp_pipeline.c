@@ -673,7 +673,8 @@ struct bcp_pipeline {
     int ndev;
     dev_lane *dev;
     pool readers, writers, completer;
-    int shared_io;      /* one pool of 2 x io_threads for reads and writes (writes first) */
+    int shared_io;      /* one pool of 2 x io_threads for reads and writes (writes first);
+                           env BCP_PIPELINE_SHARED_IO=0: separate reader and writer pools */
     int pools;
     size_t in_cap, out_cap;
     bcp_stripe *st;
@@ -865,9 +866,15 @@ int bcp_pipeline_create(const bcp_pipeline_opts *opts_in, bcp_pipeline **out)
             (rc = bcp_queue_create(L->eng, &L->qk)) || (rc = bcp_queue_create(L->eng, &L->qd)))
             goto fail;
     }
+    /* Readers and writers share one pool of 2 x io_threads threads that
+     * takes parity writes before chunk reads: the run is bound by the host
+     * CPU time of those copies, and a thread of either kind that would idle
+     * carries the other's jobs -- 1.3-1.6x on the 2 GiB config-5 and the
+     * config-1 stores against 8 + 8 separate threads, every one of 10
+     * interleaved rounds (profiles/r04/pipeline/shared_io_ab_r4al.jsonl). */
     {
         const char *sh = getenv("BCP_PIPELINE_SHARED_IO");
-        pl->shared_io = sh && atoi(sh) != 0;
+        pl->shared_io = !sh || atoi(sh) != 0;
     }
     if ((rc = pool_start(&pl->readers, pl->shared_io ? 2 * o.io_threads : o.io_threads)))
         goto fail;

@@ -478,8 +478,9 @@ int bcp_gen_round_procs(const char *store_root, int ntargets, const bcp_eventset
 typedef struct {
     int device;          /* HIP device */
     size_t slab_bytes;   /* pinned / device slab per slot (grown to the largest stripe) */
-    int io_threads;      /* reader and writer threads (each); 0 = 8 per GPU, at most half the
-                            CPUs the process may use (affinity, cgroup quota), at least 2 (capped at 64) */
+    int io_threads;      /* io threads = 2 x this (reads and writes share them); 0 = 8 per GPU, at
+                            most half the CPUs the process may use (affinity, cgroup quota), at least 2
+                            (capped at 64) */
     int nslots;          /* slabs in flight per device (2..8) */
     int ndevices;        /* GPUs device .. device+ndevices-1 (mod the visible count),
                             batches round-robin (0 = 1) */
@@ -527,9 +528,11 @@ typedef struct {
  * Footprint per device: nslots x (input + output slab) of pinned host memory
  * and the same of HBM -- 4 x 2 x 256 MiB = 2 GiB pinned + 2 GiB HBM by
  * default, 16 GiB pinned over 8 GPUs (slabs grow to the largest stripe's
- * inputs) -- plus io_threads readers and as many writers (8 + 8 per GPU by
- * default, each pool capped at 64 threads); MAP mode adds a reserved (not
- * committed) address range of the input slab's size per slot. */
+ * inputs) -- plus 2 x io_threads io threads (16 per GPU by default, within
+ * the CPUs the process may use): one pool that reads chunks and writes
+ * parity files, taking writes first (env BCP_PIPELINE_SHARED_IO=0: a reader
+ * and a writer pool of io_threads each, as before r04); MAP mode adds a
+ * reserved (not committed) address range of the input slab's size per slot. */
 int bcp_pipeline_gen(const char *store_root, int ntargets, const bcp_work_item *items, size_t nitems,
                      const bcp_pipeline_opts *opts, FILE *log, bcp_run_stats *stats);
 /* The same as a long-lived object: engine, queues, io threads and pinned /

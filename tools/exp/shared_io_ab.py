@@ -4,8 +4,9 @@ block is bound by host CPU time (8 readers need ~41 ms
 of the 50 ms run, 8 writers ~35 ms), so idle threads of one kind could carry
 the other's jobs.  Two pipelines in one process, interleaved run by run over
 the same in-memory stores: separate pools (8 readers + 8 writers, the
-default) and one pool of 16 threads taking writes before reads
-(BCP_PIPELINE_SHARED_IO=1 at creation).  Config-5 shapes (2 GiB, as the
+default before r4al) and one pool of 16 threads taking writes before reads
+(BCP_PIPELINE_SHARED_IO=1 at creation; the default since r4al, =0 gives the
+separate pools).  Config-5 shapes (2 GiB, as the
 bench's e2e block) and config-1 shapes (4 targets, 3-wide, 512 KiB).
 
     python tools/exp/shared_io_ab.py --rounds 8
@@ -54,10 +55,7 @@ def main():
         work[name] = (root, nt, items, rd + wr)
     pls = {}
     for kind in ("separate", "shared"):
-        if kind == "shared":
-            os.environ["BCP_PIPELINE_SHARED_IO"] = "1"
-        else:
-            os.environ.pop("BCP_PIPELINE_SHARED_IO", None)
+        os.environ["BCP_PIPELINE_SHARED_IO"] = "1" if kind == "shared" else "0"
         pls[kind] = bcp.Pipeline(read_mode=bcp.READ_COPY)
     os.environ.pop("BCP_PIPELINE_SHARED_IO", None)
     res = {}
