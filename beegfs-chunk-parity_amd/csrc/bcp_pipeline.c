@@ -673,8 +673,9 @@ struct bcp_pipeline {
     int ndev;
     dev_lane *dev;
     pool readers, writers, completer;
-    int shared_io;      /* one pool of 2 x io_threads for reads and writes (writes first);
-                           env BCP_PIPELINE_SHARED_IO=0: separate reader and writer pools */
+    int shared_io;      /* one pool of 2 x io_threads for reads and writes: 1 writes first,
+                           2 in push order, 3 reads first; 0 (env BCP_PIPELINE_SHARED_IO=0):
+                           separate reader and writer pools */
     int pools;
     size_t in_cap, out_cap;
     bcp_stripe *st;
@@ -874,7 +875,7 @@ int bcp_pipeline_create(const bcp_pipeline_opts *opts_in, bcp_pipeline **out)
      * interleaved rounds (profiles/r04/pipeline/shared_io_ab_r4al.jsonl). */
     {
         const char *sh = getenv("BCP_PIPELINE_SHARED_IO");
-        pl->shared_io = !sh || atoi(sh) != 0;
+        pl->shared_io = !sh ? 1 : atoi(sh) >= 0 && atoi(sh) <= 3 ? atoi(sh) : 1;
     }
     if ((rc = pool_start(&pl->readers, pl->shared_io ? 2 * o.io_threads : o.io_threads)))
         goto fail;
@@ -1278,7 +1279,10 @@ static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, 
                     const uint64_t l_ = e_ - o_ < PIECE ? e_ - o_ : PIECE;                                 \
                     *a_ = (read_arg){{0}, store_root, &tasks[i_], k_, o_, l_, d_ + o_, rd,                 \
                                      &(B)->S->reads, dir};                                                 \
-                    pool_push(&pl->readers, &a_->j, do_read);                                              \
+                    if (pl->shared_io == 3)                                                                \
+                        pool_push_hi(&pl->readers, &a_->j, do_read);                                       \
+                    else                                                                                   \
+                        pool_push(&pl->readers, &a_->j, do_read);                                          \
                 }                                                                                          \
             }
     int started = 0; /* batches whose reads are queued */
@@ -1443,7 +1447,7 @@ static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, 
         complete_arg *ca = &cargs[b];
         *ca = (complete_arg){{0}, S, batch_map, &pl->releaser, store_root, tasks, wa, first, last,
                              pl->shared_io ? &pl->readers : &pl->writers, log,
-                             &errors, &dev_rc, prealloc, pl->shared_io};
+                             &errors, &dev_rc, prealloc, pl->shared_io == 1};
         pool_push(&pl->completer, &ca->j, do_complete);
         for (size_t i = first; i < last; i++)
             bytes_written += (tasks[i].rebuild ? 0 : 8u * (uint64_t)tasks[i].n) + tasks[i].out_len;

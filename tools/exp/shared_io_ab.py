@@ -5,8 +5,8 @@ of the 50 ms run, 8 writers ~35 ms), so idle threads of one kind could carry
 the other's jobs.  Two pipelines in one process, interleaved run by run over
 the same in-memory stores: separate pools (8 readers + 8 writers, the
 default before r4al) and one pool of 16 threads taking writes before reads
-(BCP_PIPELINE_SHARED_IO=1 at creation; the default since r4al, =0 gives the
-separate pools).  Config-5 shapes (2 GiB, as the
+(BCP_PIPELINE_SHARED_IO=1 at creation; =2 the same pool in push order, =3
+reads first, =0 the separate pools).  Config-5 shapes (2 GiB, as the
 bench's e2e block) and config-1 shapes (4 targets, 3-wide, 512 KiB).
 
     python tools/exp/shared_io_ab.py --rounds 8
@@ -54,8 +54,9 @@ def main():
         wr = sum(8 * len(f[3]) + max(f[3]) for f in files)
         work[name] = (root, nt, items, rd + wr)
     pls = {}
-    for kind in ("separate", "shared"):
-        os.environ["BCP_PIPELINE_SHARED_IO"] = "1" if kind == "shared" else "0"
+    kinds = {"separate": "0", "shared_writes_first": "1", "shared_fifo": "2", "shared_reads_first": "3"}
+    for kind, v in kinds.items():
+        os.environ["BCP_PIPELINE_SHARED_IO"] = v
         pls[kind] = bcp.Pipeline(read_mode=bcp.READ_COPY)
     os.environ.pop("BCP_PIPELINE_SHARED_IO", None)
     res = {}
@@ -64,7 +65,7 @@ def main():
             for kind in pls:  # warm both once
                 pls[kind].run(root, nt, items)
             for r in range(a.rounds):
-                order = ("separate", "shared") if r % 2 == 0 else ("shared", "separate")
+                order = list(kinds) if r % 2 == 0 else list(kinds)[::-1]
                 for kind in order:
                     t0 = time.perf_counter()
                     st = pls[kind].run(root, nt, items)
