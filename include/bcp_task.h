@@ -530,7 +530,7 @@ typedef struct {
  * default, 16 GiB pinned over 8 GPUs (slabs grow to the largest stripe's
  * inputs) -- plus 2 x io_threads io threads (16 per GPU by default, within
  * the CPUs the process may use): one pool that reads chunks and writes
- * parity files, taking writes first (env BCP_PIPELINE_SHARED_IO=0: a reader
+ * parity files, taking reads first (env BCP_PIPELINE_SHARED_IO=0: a reader
  * and a writer pool of io_threads each, as before r04); MAP mode adds a
  * reserved (not committed) address range of the input slab's size per slot. */
 int bcp_pipeline_gen(const char *store_root, int ntargets, const bcp_work_item *items, size_t nitems,
