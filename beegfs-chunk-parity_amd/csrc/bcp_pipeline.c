@@ -672,7 +672,7 @@ struct bcp_pipeline {
     pool releaser;      /* MAP: releases the ranges (one thread) */
     int ndev;
     dev_lane *dev;
-    pool readers, writers, completer;
+    pool readers, writers, completer; /* readers: the io pool (reads and writes unless shared_io == 0) */
     int shared_io;      /* one pool of 2 x io_threads for reads and writes: 1 writes first,
                            2 in push order, 3 reads first; 0 (env BCP_PIPELINE_SHARED_IO=0):
                            separate reader and writer pools */
@@ -819,12 +819,13 @@ int bcp_pipeline_create(const bcp_pipeline_opts *opts_in, bcp_pipeline **out)
     }
     if (o.ndevices < 1)
         o.ndevices = 1;
-    /* io threads 0 = auto: 8 readers and 8 writers per GPU.  One GPU's PCIe
-     * link takes what ~8 threads copy out of the page cache (8 beat 16 on a
-     * 16-CPU share, profiles/r02/protocol/pipeline_io_threads_ab_r2e4.jsonl),
-     * and every further GPU brings its own link and its own CPU share -- but
-     * never more readers (and writers) than half the CPUs this process may
-     * run on: beyond that the threads only measure oversubscription. */
+    /* io threads 0 = auto: 8 per GPU, and the io pool twice that (reads and
+     * writes share it, below).  One GPU's PCIe link takes what ~8 threads
+     * copy out of the page cache (8 + 8 beat 16 + 16 on a 16-CPU share,
+     * profiles/r02/protocol/pipeline_io_threads_ab_r2e4.jsonl), and every
+     * further GPU brings its own link and its own CPU share -- but never more
+     * than half the CPUs this process may run on, so the pool has no more
+     * threads than CPUs: beyond that they only measure oversubscription. */
     if (o.io_threads == 0) {
         const int half = usable_cpus() / 2;
         o.io_threads = 8 * o.ndevices;
