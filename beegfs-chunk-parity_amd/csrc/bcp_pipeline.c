@@ -7,11 +7,11 @@
  * device does one descriptor-kernel launch per batch (SURVEY.md §7 "hard
  * parts": batching vs the per-task interface).
  *
- *   readers (io thread pool)  chunk files -> pinned input slab   [slot s]
+ *   io pool (reads first)     chunk files -> pinned input slab   [slot s]
  *   h2d queue                 pinned -> device slab, event H
  *   compute queue             wait H, xor_desc over the batch, event K
  *   d2h queue                 wait K, parity bodies -> pinned output slab, event D
- *   writers (io thread pool)  wait D, parity files = u64 sizes[n] + body
+ *   io pool (the same)        wait D, parity files = u64 sizes[n] + body
  *
  * Slots are recycled round-robin, so batch b+1 is read while batch b is on
  * the device and batch b-1 is being written; H2D and D2H run on their own
