@@ -819,6 +819,40 @@ def test_pipeline_direct_reads_fall_back_piece_by_piece(bcp, oracle, tmp_path, m
         pl.close()
 
 
+@pytest.mark.parametrize("shared_io", ["0", "1", "2", "3"])
+def test_pipeline_io_pool_orders_same_files(bcp, oracle, tmp_path, monkeypatch, shared_io):
+    """Every io pool arrangement (BCP_PIPELINE_SHARED_IO: separate reader and
+    writer pools, or one pool taking writes first, in push order, or reads
+    first -- the default) writes the same parity files and rebuilt chunks,
+    with few threads and small slabs so jobs of both kinds queue up."""
+    monkeypatch.setenv("BCP_PIPELINE_SHARED_IO", shared_io)
+    rng = np.random.default_rng(17)
+    nt = 9
+    files = []
+    for i in range(60):
+        holders, p = S.random_layout(rng, nt, int(rng.integers(2, 9)))
+        files.append((f"p/{i % 4}/c{i}", holders, p, [int(x) for x in rng.integers(1, 1 * MiB, size=len(holders))]))
+    root = str(tmp_path)
+    items, contents = S.populate(root, nt, files, seed=19)
+    pl = bcp.Pipeline(slab_bytes=4 << 20, io_threads=2, nslots=2)
+    try:
+        st = pl.run(root, nt, items)
+        assert st.errors == 0 and st.tasks == len(files)
+        for path, holders, p, lens in files:
+            assert S.read_file(S.parity_path(root, p, path)) == oracle.gen_parity_file(contents[path]), path
+        victim = 3
+        lost = {path: S.read_file(S.chunk_path(root, victim, path)) for path, holders, _, _ in files
+                if victim in holders}
+        for path in lost:
+            os.remove(S.chunk_path(root, victim, path))
+        st = pl.rebuild(root, nt, victim, sorted(items, key=lambda x: x[0].encode()))
+        assert st.errors == 0 and st.tasks == len(lost)
+        for path, data in lost.items():
+            assert S.read_file(S.chunk_path(root, victim, path)) == data, path
+    finally:
+        pl.close()
+
+
 def _resident_fraction(paths):
     """Page-cache residency of files: mincore over a read-only mapping of each
     (mapping does not fault the pages in)."""
