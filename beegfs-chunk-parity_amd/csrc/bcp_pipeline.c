@@ -872,13 +872,14 @@ int bcp_pipeline_create(const bcp_pipeline_opts *opts_in, bcp_pipeline **out)
      * takes chunk reads (which feed the link) before parity writes (which
      * only gate a slot's reuse, four batches later): where the host's CPU
      * time bounds the run, a thread that would idle in one pool carries the
-     * other's jobs.  Interleaved A/Bs on six boxes, 2 GiB config-5 and
-     * config-1 stores (profiles/r04/pipeline/shared_io_ab*.jsonl): shared
-     * pools 1.3-1.6x on the one CPU-starved box; over the four boxes that
-     * timed every order, config 5 56.2 GiB/s reads first / 52.6 push order /
-     * 51.5 writes first / 50.4 separate, config 1 53.8 / 54.6 / 52.7 / 54.9
-     * -- the sign differs from box to box, so env BCP_PIPELINE_SHARED_IO
-     * (0 separate, 1 writes first, 2 push order, 3 reads first) stays. */
+     * other's jobs.  Interleaved A/Bs on eight boxes, 2 GiB config-5 and
+     * config-1 stores (profiles/r04/pipeline/shared_io_ab*.jsonl): a shared
+     * pool 1.3-1.6x on the one CPU-starved box; over the six boxes that
+     * timed every order, config 5 54.0 GiB/s reads first / 51.7 writes
+     * first / 49.9 push order / 51.6 separate, config 1 54.4 / 54.0 / 52.7 /
+     * 56.4 -- within the box-to-box spread elsewhere, so env
+     * BCP_PIPELINE_SHARED_IO (0 separate, 1 writes first, 2 push order, 3
+     * reads first) stays. */
     {
         const char *sh = getenv("BCP_PIPELINE_SHARED_IO");
         pl->shared_io = !sh ? 3 : atoi(sh) >= 0 && atoi(sh) <= 3 ? atoi(sh) : 3;
