@@ -48,8 +48,7 @@ class RunStats(ctypes.Structure):
 class PipelineTiming(ctypes.Structure):
     _fields_ = [("stat", ctypes.c_double), ("read_wait", ctypes.c_double), ("slot_wait", ctypes.c_double),
                 ("submit", ctypes.c_double), ("drain", ctypes.c_double), ("batches", ctypes.c_uint32),
-                ("read_jobs", ctypes.c_uint32), ("map", ctypes.c_double), ("mapped_bytes", ctypes.c_uint64),
-                ("map_fallbacks", ctypes.c_uint32), ("read_mode", ctypes.c_int),
+                ("read_jobs", ctypes.c_uint32), ("read_mode", ctypes.c_int),
                 ("direct_bytes", ctypes.c_uint64), ("direct_fallbacks", ctypes.c_uint32)]
 
 
@@ -58,7 +57,7 @@ class PipelineOpts(ctypes.Structure):
                 ("nslots", ctypes.c_int), ("ndevices", ctypes.c_int), ("read_mode", ctypes.c_int)]
 
 
-READ_AUTO, READ_COPY, READ_MAP, READ_DIRECT = 0, 1, 2, 3
+READ_AUTO, READ_COPY, READ_DIRECT = 0, 1, 3  # 2 was MAP (removed in ABI 3)
 
 
 XOR_HOOK = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t,
@@ -104,7 +103,6 @@ _SIGS = {
     "bcp_host_alloc_mapped": ([_V, ctypes.c_size_t, ctypes.POINTER(_V)], ctypes.c_int),
     "bcp_host_free": ([_V, _V], ctypes.c_int),
     "bcp_host_register": ([_V, _V, ctypes.c_size_t], ctypes.c_int),
-    "bcp_host_register_dma_src": ([_V, _V, ctypes.c_size_t], ctypes.c_int),
     "bcp_host_unregister": ([_V, _V], ctypes.c_int),
     "bcp_h2d_async": ([_V, _V, _V, ctypes.c_size_t], ctypes.c_int),
     "bcp_d2h_async": ([_V, _V, _V, ctypes.c_size_t], ctypes.c_int),

@@ -648,20 +648,6 @@ extern "C" int bcp_host_register(bcp_engine *eng, void *hptr, size_t bytes) {
   return 0;
 }
 
-// Read-only registration for copies OUT of caller memory the CPU may not
-// write (e.g. PROT_READ file mappings): pins the pages for the DMA engine,
-// nothing maps them for kernels.
-extern "C" int bcp_host_register_dma_src(bcp_engine *eng, const void *hptr, size_t bytes) {
-  if (!eng || !hptr || !bytes) return -EINVAL;
-  int rc = set_device(eng);
-  if (rc) return rc;
-  if (hipHostRegister(const_cast<void *>(hptr), bytes, hipHostRegisterReadOnly) != hipSuccess) {
-    (void)hipGetLastError();
-    return -EIO;
-  }
-  return 0;
-}
-
 extern "C" int bcp_host_unregister(bcp_engine *eng, void *hptr) {
   if (!eng || !hptr) return -EINVAL;
   int rc = set_device(eng);

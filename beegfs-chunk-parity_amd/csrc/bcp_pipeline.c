@@ -227,11 +227,13 @@ typedef struct {
     uint64_t src_off[MAX_STORAGE_TARGETS];/* file offset of the source data (parity body: 8n) */
     uint64_t max_cs;
     uint64_t out_len;                    /* gen: max_cs; rebuild: header[victim index] */
-    uint64_t in_off[MAX_STORAGE_TARGETS];/* offsets in the input slab (page layout, MAP and
-                                            DIRECT: of the file's first byte, page-aligned;
-                                            the data then starts src_off further) */
+    uint64_t in_off[MAX_STORAGE_TARGETS];/* offsets in the input slab (page layout, DIRECT:
+                                            of the file's first byte, page-aligned; the data
+                                            then starts src_off further) */
     uint64_t out_off;                    /* offset in the output slab */
     int batch;
+    int prealloc;                        /* posix_fallocate the output first (not where the
+                                            output target's directory is tmpfs: do_write) */
 } task;
 
 typedef struct {
@@ -298,39 +300,17 @@ typedef struct {
     int prealloc;         /* posix_fallocate first (not on tmpfs: see do_write) */
 } write_arg;
 
-/* MAP read mode: one batch's mapped tail -- a range of its own holding the
- * chunk files (MAP_FIXED, read-only) and registered for the DMA engine.
- * hipHostUnregister waits for ALL work on the device (74.6 ms behind a 4 GiB
- * copy against 0.001 ms for a register, profiles/r04/probe/unreg.jsonl) but
- * blocks only its caller (unreg_thread.jsonl): so a range is released by the
- * pipeline's releaser thread once its batch's copies are done, never by the
- * thread that submits. */
-typedef struct {
-    job j;                /* first: the releaser pool's link */
-    bcp_engine *eng;
-    uint8_t *va;
-    size_t len;
-    uint64_t nfiles;
-    uint64_t *out;        /* the run's outstanding {bytes, mappings}, decremented on release */
-    int registered;
-    int released;         /* set by whoever released it */
-} map_range;
-
 typedef struct {
     job j;
     slot *S;
-    map_range *map;       /* MAP: the batch's mapped range, or NULL */
-    pool *releaser;
     const char *root;
     task *tasks;
     write_arg *wa;        /* one per task of the run */
     size_t first, last;
-    pool *writers;
+    pool *io;
     FILE *log;
     int *errors;
     int *dev_rc;
-    int prealloc;
-    int hi;               /* writers share the readers' pool: writes go ahead of reads */
 } complete_arg;
 
 static pthread_mutex_t g_stat_lock = PTHREAD_MUTEX_INITIALIZER;
@@ -575,14 +555,7 @@ static void do_write(job *p)
 }
 
 /* Completion stage (one thread, batches in order): wait for the batch's D2H,
- * then hand its parity files to the writer pool. */
-static void map_release(map_range *r);
-
-static void do_release(job *p)
-{
-    map_release((map_range *)p);
-}
-
+ * then hand its parity files to the io pool (behind every queued read). */
 static void do_complete(job *p)
 {
     /* The run frees its job arrays once every write of the batch has counted
@@ -590,8 +563,6 @@ static void do_complete(job *p)
      * and touch neither `a` nor a pushed write job after handing it over. */
     const complete_arg a = *(complete_arg *)p;
     int rc = bcp_event_sync(a.S->ev_d);
-    if (a.map) /* its H2D is done: the releaser may unregister and unmap it */
-        pool_push(a.releaser, &a.map->j, do_release);
     if (rc) {
         pthread_mutex_lock(&g_stat_lock);
         *a.dev_rc = rc;
@@ -602,11 +573,8 @@ static void do_complete(job *p)
         for (size_t i = a.first; i < a.last; i++) {
             write_arg *w = &a.wa[i];
             *w = (write_arg){{0}, a.root, &a.tasks[i], a.S->h_out + a.tasks[i].out_off, &a.S->writes, a.log, a.errors,
-                             a.prealloc};
-            if (a.hi)
-                pool_push_hi(a.writers, &w->j, do_write);
-            else
-                pool_push(a.writers, &w->j, do_write);
+                             a.tasks[i].prealloc};
+            pool_push(a.io, &w->j, do_write);
         }
     }
 }
@@ -623,25 +591,6 @@ static int slot_alloc(bcp_engine *e, slot *s, size_t in_cap, size_t out_cap)
     s->in_cap = in_cap;
     s->out_cap = out_cap;
     return 0;
-}
-
-/* The device no longer reads r (its queues were synchronised). */
-static void map_release(map_range *r)
-{
-    if (r->released)
-        return;
-    if (r->registered)
-        bcp_host_unregister(r->eng, r->va);
-    if (r->va)
-        munmap(r->va, r->len);
-    if (r->out) {
-        __atomic_sub_fetch(&r->out[0], (uint64_t)r->len, __ATOMIC_RELAXED);
-        __atomic_sub_fetch(&r->out[1], r->nfiles, __ATOMIC_RELAXED);
-    }
-    r->registered = 0;
-    r->va = NULL;
-    r->out = NULL;
-    r->released = 1;
 }
 
 static void slot_free(bcp_engine *e, slot *s)
@@ -667,15 +616,10 @@ typedef struct {
 
 struct bcp_pipeline {
     bcp_pipeline_opts o;
-    int read_mode;      /* resolved: BCP_READ_COPY / MAP / DIRECT */
-    double map_share;   /* MAP: share of a batch's input bytes mapped (adapted per batch) */
-    pool releaser;      /* MAP: releases the ranges (one thread) */
+    int read_mode;      /* BCP_READ_AUTO (decided per run), COPY or DIRECT */
     int ndev;
     dev_lane *dev;
-    pool readers, writers, completer; /* readers: the io pool (reads and writes unless shared_io == 0) */
-    int shared_io;      /* one pool of 2 x io_threads for reads and writes: 1 writes first,
-                           2 in push order, 3 reads first; 0 (env BCP_PIPELINE_SHARED_IO=0):
-                           separate reader and writer pools */
+    pool io, completer; /* io: 2 x io_threads threads, chunk reads ahead of parity writes */
     int pools;
     size_t in_cap, out_cap;
     bcp_stripe *st;
@@ -710,14 +654,10 @@ int bcp_pipeline_destroy(bcp_pipeline *pl)
     if (!pl)
         return -EINVAL;
     /* only the pools that started (pool_start is all or nothing) */
-    if (pl->pools & 1)
-        pool_stop(&pl->readers);
-    if (pl->pools & 4)
-        pool_stop(&pl->completer);
-    if (pl->pools & 8)
-        pool_stop(&pl->releaser);
     if (pl->pools & 2)
-        pool_stop(&pl->writers);
+        pool_stop(&pl->completer);
+    if (pl->pools & 1)
+        pool_stop(&pl->io);
     if (pl->dev) {
         /* queues first (each synchronises its streams): no copy or kernel may
          * still use a slot when its memory goes */
@@ -807,13 +747,14 @@ int bcp_pipeline_create(const bcp_pipeline_opts *opts_in, bcp_pipeline **out)
     bcp_pipeline_opts o = {0, 256u << 20, 0, 4, 1, BCP_READ_AUTO};
     if (opts_in)
         o = *opts_in;
-    if (o.read_mode < BCP_READ_AUTO || o.read_mode > BCP_READ_DIRECT)
+    /* 2 was the MAP read mode (ABI 2), removed in ABI 3: never chosen by
+     * AUTO and level with or behind COPY */
+    if (o.read_mode != BCP_READ_AUTO && o.read_mode != BCP_READ_COPY && o.read_mode != BCP_READ_DIRECT)
         return -EINVAL;
     if (o.read_mode == BCP_READ_AUTO) { /* stays AUTO (decided per run) unless the env names a mode */
         const char *env = getenv("BCP_PIPELINE_READ");
         o.read_mode = !env                     ? BCP_READ_AUTO
                       : !strcmp(env, "copy")   ? BCP_READ_COPY
-                      : !strcmp(env, "map")    ? BCP_READ_MAP
                       : !strcmp(env, "direct") ? BCP_READ_DIRECT
                                                : BCP_READ_AUTO;
     }
@@ -851,7 +792,6 @@ int bcp_pipeline_create(const bcp_pipeline_opts *opts_in, bcp_pipeline **out)
         return -ENOMEM;
     pl->o = o;
     pl->read_mode = o.read_mode; /* AUTO: COPY or DIRECT, chosen per run (auto_read_mode) */
-    pl->map_share = 0.3;
     int rc = 0;
     pl->dev = calloc((size_t)o.ndevices, sizeof(dev_lane));
     if (!pl->dev) {
@@ -868,38 +808,19 @@ int bcp_pipeline_create(const bcp_pipeline_opts *opts_in, bcp_pipeline **out)
             (rc = bcp_queue_create(L->eng, &L->qk)) || (rc = bcp_queue_create(L->eng, &L->qd)))
             goto fail;
     }
-    /* Readers and writers share one pool of 2 x io_threads threads that
-     * takes chunk reads (which feed the link) before parity writes (which
-     * only gate a slot's reuse, four batches later): where the host's CPU
-     * time bounds the run, a thread that would idle in one pool carries the
-     * other's jobs.  Interleaved A/Bs on eight boxes, 2 GiB config-5 and
-     * config-1 stores (profiles/r04/pipeline/shared_io_ab*.jsonl): a shared
-     * pool 1.3-1.6x on the one CPU-starved box; over the six boxes that
-     * timed every order, config 5 54.0 GiB/s reads first / 51.7 writes
-     * first / 49.9 push order / 51.6 separate, config 1 54.4 / 54.0 / 52.7 /
-     * 56.4 -- within the box-to-box spread elsewhere, so env
-     * BCP_PIPELINE_SHARED_IO (0 separate, 1 writes first, 2 push order, 3
-     * reads first) stays. */
-    {
-        const char *sh = getenv("BCP_PIPELINE_SHARED_IO");
-        pl->shared_io = !sh ? 3 : atoi(sh) >= 0 && atoi(sh) <= 3 ? atoi(sh) : 3;
-    }
-    if ((rc = pool_start(&pl->readers, pl->shared_io ? 2 * o.io_threads : o.io_threads)))
+    /* One io pool of 2 x io_threads threads reads chunks and writes parity
+     * files, reads first: the reads feed the link, a batch's writes only gate
+     * its slot's reuse four batches later, and where the host's CPU time
+     * bounds the run a thread never idles in one pool while the other has
+     * work.  (Separate pools, writes first and push order measured within the
+     * box-to-box spread of this order on six boxes and were removed in r05:
+     * profiles/r04/pipeline/shared_io_ab*.jsonl) */
+    if ((rc = pool_start(&pl->io, 2 * o.io_threads)))
         goto fail;
     pl->pools |= 1;
-    if (!pl->shared_io) {
-        if ((rc = pool_start(&pl->writers, o.io_threads)))
-            goto fail;
-        pl->pools |= 2;
-    }
     if ((rc = pool_start(&pl->completer, 1)))
         goto fail;
-    pl->pools |= 4;
-    if (pl->read_mode == BCP_READ_MAP) {
-        if ((rc = pool_start(&pl->releaser, 1)))
-            goto fail;
-        pl->pools |= 8;
-    }
+    pl->pools |= 2;
     if ((rc = ensure_slots(pl, o.slab_bytes, o.slab_bytes)))
         goto fail;
     *out = pl;
@@ -913,48 +834,20 @@ static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, 
                          FILE *log, bcp_run_stats *stats, double t0);
 
 /* Bytes source k of t takes in the input slab: its data at 256-byte pitch
- * (COPY), or the whole file prefix up to the data's end at page pitch (MAP and
- * DIRECT: files are mapped / read from offset 0, the rebuild parity body sits
- * 8n in). */
-static uint64_t span_of(const task *t, int k, int map_layout)
+ * (COPY), or the whole file prefix up to the data's end at page pitch (DIRECT:
+ * files are read from offset 0 into page-aligned slab offsets, the rebuild
+ * parity body sits 8n in). */
+static uint64_t span_of(const task *t, int k, int page_layout)
 {
-    if (!map_layout)
+    if (!page_layout)
         return RUP(t->size[k]);
     return t->size[k] ? RUP_PAGE(t->src_off[k] + t->size[k]) : 0;
 }
 
 /* Where source k's data starts, relative to the slab. */
-static uint64_t data_off(const task *t, int k, int map_layout)
+static uint64_t data_off(const task *t, int k, int page_layout)
 {
-    return t->in_off[k] + (map_layout ? t->src_off[k] : 0);
-}
-
-/* MAP mode: place every source of tasks [a, b) in va (file offset 0 at
- * in_off - base, read-only, populated).  Returns 0, or -errno when a file
- * could not be opened or mapped (the caller reads those tasks instead). */
-static int map_tasks(uint8_t *va, uint64_t base, const char *root, task *tasks, size_t a, size_t b)
-{
-    char fn[4352];
-    for (size_t i = a; i < b; i++) {
-        task *t = &tasks[i];
-        for (int k = 0; k < t->n; k++) {
-            const uint64_t len = span_of(t, k, 1);
-            if (!len)
-                continue;
-            const int is_parity = t->rebuild && k == t->parity_src;
-            chunk_file(fn, sizeof(fn), root, t->holders[k], is_parity ? "parity" : "chunks", t->path);
-            int fd = open(fn, O_RDONLY);
-            if (fd < 0)
-                return -errno;
-            void *m = mmap(va + (t->in_off[k] - base), (size_t)len, PROT_READ, MAP_SHARED | MAP_FIXED | MAP_POPULATE,
-                           fd, 0);
-            const int e = errno;
-            close(fd);
-            if (m == MAP_FAILED)
-                return -e;
-        }
-    }
-    return 0;
+    return t->in_off[k] + (page_layout ? t->src_off[k] : 0);
 }
 
 int bcp_pipeline_run(bcp_pipeline *pl, const char *store_root, int ntargets, const bcp_work_item *items,
@@ -1009,41 +902,10 @@ int bcp_pipeline_run(bcp_pipeline *pl, const char *store_root, int ntargets, con
     return rc;
 }
 
-/* MAP mode's caps on what is mapped at once: registered ranges pin their
- * page-cache pages until the releaser gets to them, and each chunk file is a
- * mapping of its own (vm.max_map_count is 65530 by default); at either cap a
- * batch is read instead. */
-#define MAP_OUT_BYTES_MAX ((uint64_t)16 << 30)
-#define MAP_OUT_FILES_MAX ((uint64_t)24576)
-
-/* Wait until every release pushed so far has run (the pool is FIFO, one
- * thread). */
-typedef struct {
-    job j;
-    latch *l;
-} mark_job;
-
-static void do_mark(job *p)
-{
-    latch_down(((mark_job *)p)->l);
-}
-
-static void releaser_drain(pool *P)
-{
-    latch l;
-    latch_init(&l, 1);
-    mark_job m = {{0}, &l};
-    pool_push(P, &m.j, do_mark);
-    latch_wait(&l);
-    latch_destroy(&l);
-}
-
 /* One batch between queueing its reads and submitting it. */
 typedef struct {
-    size_t first, last, split; /* tasks; [split, last) mapped (MAP) */
-    uint64_t in_used, reg_lo;  /* input bytes; where the mapped tail starts */
-    double tw;                 /* reads queued at */
-    int need_map;
+    size_t first, last;        /* tasks */
+    uint64_t in_used;          /* input bytes */
     int reads_live;            /* S->reads initialised and not yet waited for */
     dev_lane *L;
     slot *S;
@@ -1056,10 +918,39 @@ typedef struct {
  * copy (1.1-1.4x).  The sample: the first 16 MiB of one
  * source in each of up to 64 tasks spread over the run, mincore() on a
  * mapping of it. */
-static int auto_read_mode(const char *root, const task *tasks, size_t nt)
+/* Filesystem of every storage target's directory a run touches, looked up
+ * once per run: <root>/st<k>/{chunks,parity} are often separate mounts, so
+ * the choices below are made per target, never from the store root. */
+typedef struct {
+    signed char mem[MAX_STORAGE_TARGETS][2]; /* [k][0 chunks, 1 parity]: 1 tmpfs / ramfs, 0 not, -1 unknown yet */
+} fs_kinds;
+
+static int dir_in_memory(fs_kinds *fk, const char *root, int k, int parity)
 {
-    struct statfs sf;
-    if (statfs(root, &sf) == 0 && (sf.f_type == TMPFS_MAGIC || sf.f_type == RAMFS_MAGIC))
+    signed char *m = &fk->mem[k][parity];
+    if (*m < 0) {
+        char dn[4352];
+        snprintf(dn, sizeof(dn), "%s/st%d/%s", root, k, parity ? "parity" : "chunks");
+        struct statfs sf;
+        *m = statfs(dn, &sf) == 0 && (sf.f_type == TMPFS_MAGIC || sf.f_type == RAMFS_MAGIC);
+    }
+    return *m;
+}
+
+/* AUTO's read path for one run: COPY where the chunks are in memory anyway
+ * (every source directory of the run on tmpfs / ramfs, or a sample of the
+ * run's sources mostly resident in the page cache -- just written, or read
+ * before), DIRECT for a cold store on a disk, where O_DIRECT lets the storage
+ * device fill the slabs without a CPU copy (1.1-1.4x).
+ * The sample: the first 16 MiB of one source in each of up to 64 tasks spread
+ * over the run, mincore() on a mapping of it. */
+static int auto_read_mode(const char *root, const task *tasks, size_t nt, fs_kinds *fk)
+{
+    int all_mem = 1;
+    for (size_t i = 0; i < nt && all_mem; i++)
+        for (int k = 0; k < tasks[i].n && all_mem; k++)
+            all_mem = dir_in_memory(fk, root, tasks[i].holders[k], tasks[i].rebuild && k == tasks[i].parity_src);
+    if (all_mem)
         return BCP_READ_COPY;
     const uint64_t cap = (uint64_t)16 << 20;
     unsigned char *vec = malloc(cap / PAGE);
@@ -1096,18 +987,13 @@ static int auto_read_mode(const char *root, const task *tasks, size_t nt)
     return pages && resident * 2 < pages ? BCP_READ_DIRECT : BCP_READ_COPY;
 }
 
-/* Stat, batch and stream the tasks through the slots (every read path).
+/* Stat, batch and stream the tasks through the slots (both read paths).
  * Takes no ownership of tasks. */
 static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, size_t nt, int corrupt_fd,
                          FILE *log, bcp_run_stats *stats, double t0)
 {
-    uint64_t map_out[2] = {0, 0}; /* outstanding mapped bytes, mappings (the releaser decrements) */
-    int prealloc = 1;
-    {
-        struct statfs sf;
-        if (statfs(store_root, &sf) == 0 && sf.f_type == TMPFS_MAGIC)
-            prealloc = 0;
-    }
+    fs_kinds fk;
+    memset(&fk, -1, sizeof(fk));
     const int nslots = pl->o.nslots;
     int rc = 0, errors = 0, dev_rc = 0;
     uint64_t rd[3] = {0, 0, 0}, bytes_written = 0, ntasks = 0; /* rd: see read_arg.bytes */
@@ -1125,23 +1011,26 @@ static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, 
         }
         for (size_t i = 0; i < nt; i++) {
             args[i] = (stat_arg){{0}, store_root, &tasks[i], &l, corrupt_fd};
-            pool_push(&pl->readers, &args[i].j, do_stat);
+            pool_push(&pl->io, &args[i].j, do_stat);
         }
         latch_wait(&l);
         latch_destroy(&l);
         free(args);
     }
+    /* the reference reserves every output's space first (task_processing.c:186),
+     * except where that output's directory is tmpfs / ramfs (do_write) */
+    for (size_t i = 0; i < nt; i++)
+        tasks[i].prealloc = !dir_in_memory(&fk, store_root, tasks[i].p, !tasks[i].rebuild);
 
-    /* 2. plan batches: inputs at 256-byte pitch (MAP: page pitch), outputs
+    /* 2. plan batches: inputs at 256-byte pitch (DIRECT: page pitch), outputs
      * at 256 */
-    const int mode = pl->read_mode == BCP_READ_AUTO ? auto_read_mode(store_root, tasks, nt) : pl->read_mode;
-    const int mapm = mode == BCP_READ_MAP, dir = mode == BCP_READ_DIRECT;
-    const int ml = mapm || dir; /* page layout */
+    const int mode = pl->read_mode == BCP_READ_AUTO ? auto_read_mode(store_root, tasks, nt, &fk) : pl->read_mode;
+    const int dir = mode == BCP_READ_DIRECT; /* page layout */
     size_t in_cap = pl->in_cap, out_cap = pl->out_cap;
     for (size_t i = 0; i < nt; i++) {
         uint64_t in = 0;
         for (int k = 0; k < tasks[i].n; k++)
-            in += span_of(&tasks[i], k, ml);
+            in += span_of(&tasks[i], k, dir);
         if (in > in_cap)
             in_cap = (size_t)in;
         if (RUP(tasks[i].out_len) > out_cap)
@@ -1165,7 +1054,7 @@ static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, 
         for (size_t i = 0; i < nt; i++) {
             uint64_t in = 0;
             for (int k = 0; k < tasks[i].n; k++)
-                in += span_of(&tasks[i], k, ml);
+                in += span_of(&tasks[i], k, dir);
             total_in += in;
             max_in = in > max_in ? in : max_in;
         }
@@ -1187,7 +1076,7 @@ static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, 
     uint64_t total_in_all = 0;
     for (size_t i = 0; i < nt; i++)
         for (int k = 0; k < tasks[i].n; k++)
-            total_in_all += span_of(&tasks[i], k, ml);
+            total_in_all += span_of(&tasks[i], k, dir);
     int nbatches = 0;
     {
         uint64_t in_used = 0, out_used = 0, consumed = 0, limit = plan_in;
@@ -1195,7 +1084,7 @@ static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, 
             task *t = &tasks[i];
             uint64_t in = 0;
             for (int k = 0; k < t->n; k++)
-                in += span_of(t, k, ml);
+                in += span_of(t, k, dir);
             if (i == 0 || in_used + in > limit || out_used + RUP(t->out_len) > out_cap) {
                 nbatches++;
                 consumed += in_used;
@@ -1209,7 +1098,7 @@ static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, 
             t->batch = nbatches - 1;
             for (int k = 0; k < t->n; k++) {
                 t->in_off[k] = in_used;
-                in_used += span_of(t, k, ml);
+                in_used += span_of(t, k, dir);
             }
             t->out_off = out_used;
             out_used += RUP(t->out_len);
@@ -1228,9 +1117,7 @@ static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, 
     bcp_stripe *st = pl->st;
     bcp_source *so = pl->so;
     /* every job of the run, before the first one is queued: a read job per
-     * piece of every source (read into the slab or, after a failed mapping,
-     * instead of it -- never both), a write job per task, a completion per
-     * batch */
+     * piece of every source, a write job per task, a completion per batch */
     size_t nreads_all = 0;
     for (size_t i = 0; i < nt; i++)
         for (int k = 0; k < tasks[i].n; k++)
@@ -1238,15 +1125,14 @@ static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, 
     read_arg *ra = calloc(nreads_all ? nreads_all : 1, sizeof(read_arg));
     write_arg *wa = calloc(nt ? nt : 1, sizeof(write_arg));
     complete_arg *cargs = calloc(nbatches ? (size_t)nbatches : 1, sizeof(complete_arg));
-    map_range *maps = mapm ? calloc(nbatches ? (size_t)nbatches : 1, sizeof(map_range)) : NULL;
-    if (!ra || !wa || !cargs || (mapm && !maps)) {
+    bstate *bs = calloc(nbatches ? (size_t)nbatches : 1, sizeof(bstate));
+    if (!ra || !wa || !cargs || !bs) {
         free(ra);
         free(wa);
         free(cargs);
-        free(maps);
+        free(bs);
         return -ENOMEM;
     }
-    size_t nmaps = 0;
     size_t rnext = 0;
     bcp_pipeline_timing tm = {0};
     tm.stat = now_s() - t_stat;
@@ -1257,14 +1143,6 @@ static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, 
      * one batch to the next without idling at a batch's last chunks; b is on
      * the device meanwhile and earlier batches are being written (4 slots by
      * default: a slot's parity writes gate its reuse). */
-    bstate *bs = calloc(nbatches ? (size_t)nbatches : 1, sizeof(bstate));
-    if (!bs) {
-        free(ra);
-        free(wa);
-        free(cargs);
-        free(maps);
-        return -ENOMEM;
-    }
     {
         size_t first = 0;
         for (int b = 0; b < nbatches; b++) {
@@ -1274,26 +1152,10 @@ static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, 
             bs[b].last = first;
         }
     }
-    /* queue batch b's reads into its slot (after the slot's previous batch
-     * has been written); MAP mode: decide the mapped tail */
-    #define PUSH_READS(B, A, Z)                                                                          \
-        for (size_t i_ = (A); i_ < (Z); i_++)                                                              \
-            for (int k_ = 0; k_ < tasks[i_].n; k_++) {                                                     \
-                const uint64_t e_ = read_extent(&tasks[i_], k_, dir);                                      \
-                uint8_t *d_ = (B)->S->h_in + (dir ? tasks[i_].in_off[k_] : data_off(&tasks[i_], k_, ml));  \
-                for (uint64_t o_ = 0; o_ < e_; o_ += PIECE) {                                              \
-                    read_arg *a_ = &ra[rnext++];                                                           \
-                    const uint64_t l_ = e_ - o_ < PIECE ? e_ - o_ : PIECE;                                 \
-                    *a_ = (read_arg){{0}, store_root, &tasks[i_], k_, o_, l_, d_ + o_, rd,                 \
-                                     &(B)->S->reads, dir};                                                 \
-                    if (pl->shared_io == 3)                                                                \
-                        pool_push_hi(&pl->readers, &a_->j, do_read);                                       \
-                    else                                                                                   \
-                        pool_push(&pl->readers, &a_->j, do_read);                                          \
-                }                                                                                          \
-            }
     int started = 0; /* batches whose reads are queued */
     for (int b = 0; b < nbatches && !rc; b++) {
+        /* queue batch b+1's reads into its slot (after the slot's previous
+         * batch has been written), ahead of every queued parity write */
         for (; started < nbatches && started <= b + 1; started++) {
             bstate *B = &bs[started];
             B->L = &pl->dev[started % pl->ndev];
@@ -1306,118 +1168,41 @@ static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, 
             }
             tm.slot_wait += now_s() - tw;
             uint64_t in_used = 0;
+            long nreads = 0;
             for (size_t i = B->first; i < B->last; i++)
                 for (int k = 0; k < tasks[i].n; k++) {
-                    const uint64_t end = tasks[i].in_off[k] + span_of(&tasks[i], k, ml);
+                    const uint64_t end = tasks[i].in_off[k] + span_of(&tasks[i], k, dir);
                     if (end > in_used)
                         in_used = end;
+                    nreads += (long)pieces_of(read_extent(&tasks[i], k, dir));
                 }
             B->in_used = in_used;
-            /* MAP: the batch's tail tasks [split, last), about map_share of
-             * its input bytes, are mapped by this thread while the io
-             * threads read the head (within the caps on what is mapped at
-             * once) */
-            B->split = B->last;
-            if (mapm && B->last > B->first && __atomic_load_n(&map_out[0], __ATOMIC_RELAXED) < MAP_OUT_BYTES_MAX &&
-                __atomic_load_n(&map_out[1], __ATOMIC_RELAXED) < MAP_OUT_FILES_MAX) {
-                const uint64_t from = in_used - (uint64_t)(pl->map_share * (double)in_used);
-                B->split = B->first;
-                while (B->split < B->last && tasks[B->split].in_off[0] < from)
-                    B->split++;
-            }
-            B->reg_lo = B->split < B->last ? tasks[B->split].in_off[0] : in_used;
-            long nreads = 0;
-            for (size_t i = B->first; i < B->split; i++)
-                for (int k = 0; k < tasks[i].n; k++)
-                    nreads += (long)pieces_of(read_extent(&tasks[i], k, dir));
-            B->tw = now_s();
             latch_init(&B->S->reads, nreads);
             B->reads_live = 1;
-            PUSH_READS(B, B->first, B->split);
+            for (size_t i = B->first; i < B->last; i++)
+                for (int k = 0; k < tasks[i].n; k++) {
+                    const uint64_t e = read_extent(&tasks[i], k, dir);
+                    uint8_t *d = B->S->h_in + (dir ? tasks[i].in_off[k] : data_off(&tasks[i], k, dir));
+                    for (uint64_t o = 0; o < e; o += PIECE) {
+                        read_arg *a = &ra[rnext++];
+                        *a = (read_arg){{0}, store_root, &tasks[i], k, o, e - o < PIECE ? e - o : PIECE, d + o, rd,
+                                        &B->S->reads, dir};
+                        pool_push_hi(&pl->io, &a->j, do_read);
+                    }
+                }
             tm.read_jobs += (uint32_t)nreads;
-            B->need_map = B->split < B->last;
         }
         bstate *B = &bs[b];
         dev_lane *L = B->L;
         slot *S = B->S;
-        const uint64_t in_used = B->in_used, reg_lo = B->reg_lo;
-        const size_t first = B->first, last = B->last, split = B->split;
-        const double tw = B->tw;
-        /* MAP: this batch's tail, mapped now (batch b+1's reads are queued) */
-        double map_s = 0;
-        int mapped_ok = 0;
-        uint8_t *map_va = NULL;
-        map_range *batch_map = NULL;
-        if (B->need_map) {
-            const double tm0 = now_s();
-            const size_t map_len = (size_t)(in_used - reg_lo);
-            map_range *R = &maps[nmaps];
-            int mrc = 0;
-            void *va = mmap(NULL, map_len, PROT_NONE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
-            if (va == MAP_FAILED) {
-                mrc = -errno;
-            } else {
-                uint64_t nf = 0;
-                for (size_t i = split; i < last; i++)
-                    nf += (uint64_t)tasks[i].n;
-                *R = (map_range){{0}, L->eng, va, map_len, nf, map_out, 0, 0};
-                __atomic_add_fetch(&map_out[0], (uint64_t)map_len, __ATOMIC_RELAXED);
-                __atomic_add_fetch(&map_out[1], nf, __ATOMIC_RELAXED);
-                nmaps++;
-                mrc = map_tasks(va, reg_lo, store_root, tasks, split, last);
-                if (!mrc)
-                    mrc = bcp_host_register_dma_src(L->eng, va, map_len);
-                if (!mrc) {
-                    R->registered = 1;
-                    map_va = va;
-                    batch_map = R;
-                } else { /* nothing registered: releasing it waits for nothing */
-                    map_release(R);
-                }
-            }
-            map_s = now_s() - tm0;
-            tm.map += map_s;
-            mapped_ok = !mrc;
-            if (!mapped_ok)
-                tm.map_fallbacks++;
-        }
+        const uint64_t in_used = B->in_used;
+        const size_t first = B->first, last = B->last;
         const double t_wait0 = now_s();
         latch_wait(&S->reads);
-        const double t_read_end = S->reads.t_zero;
         latch_destroy(&S->reads);
         B->reads_live = 0;
-        if (split < last && !mapped_ok) { /* read what could not be mapped */
-            long n2 = 0;
-            for (size_t i = split; i < last; i++)
-                for (int k = 0; k < tasks[i].n; k++)
-                    n2 += (long)pieces_of(read_extent(&tasks[i], k, dir));
-            latch_init(&S->reads, n2);
-            PUSH_READS(B, split, last);
-            tm.read_jobs += (uint32_t)n2;
-            latch_wait(&S->reads);
-            latch_destroy(&S->reads);
-        }
-        if (split < last && mapped_ok) {
-            uint64_t got = 0;
-            for (size_t i = split; i < last; i++)
-                for (int k = 0; k < tasks[i].n; k++)
-                    got += tasks[i].size[k];
-            pthread_mutex_lock(&g_stat_lock);
-            rd[0] += got;
-            pthread_mutex_unlock(&g_stat_lock);
-            tm.mapped_bytes += in_used - reg_lo;
-            /* next share: the two paths' rates in this batch, balanced so
-             * both finish together (smoothed; a batch with nothing read
-             * gives no reader rate) */
-            const double rd_s = t_read_end - tw;
-            if (split > first && rd_s > 0 && map_s > 0) {
-                const double rr = (double)reg_lo / rd_s, rm = (double)(in_used - reg_lo) / map_s;
-                double f = 0.5 * pl->map_share + 0.5 * rm / (rm + rr);
-                pl->map_share = f < 0.05 ? 0.05 : f > 0.95 ? 0.95 : f;
-            }
-        }
         const double ts = now_s();
-        tm.read_wait += ts - t_wait0; /* blocked on this batch's reads (its fallback reads included) */
+        tm.read_wait += ts - t_wait0; /* blocked on this batch's reads */
         uint32_t ns = 0, nsrc = 0;
         uint64_t out_used = 0;
         for (size_t i = first; i < last; i++) {
@@ -1425,43 +1210,31 @@ static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, 
             st[ns] = (bcp_stripe){(uint64_t)S->d_out + t->out_off, t->out_len, nsrc, (uint32_t)t->n,
                                   t->max_cs > WINDOW ? WINDOW : 0};
             for (int k = 0; k < t->n; k++)
-                so[nsrc++] = (bcp_source){(uint64_t)S->d_in + data_off(t, k, ml), t->size[k]};
+                so[nsrc++] = (bcp_source){(uint64_t)S->d_in + data_off(t, k, dir), t->size[k]};
             ns++;
             if (t->out_off + RUP(t->out_len) > out_used)
                 out_used = t->out_off + RUP(t->out_len);
         }
-        /* device: H2D (side queue; the slab's part, then the mapped part
-         * straight out of the page cache) -> kernel -> D2H (side queue) */
-        const uint8_t *tail_src = mapped_ok ? map_va : S->h_in + reg_lo;
-        if ((reg_lo && (rc = bcp_h2d_async(L->qh, S->d_in, S->h_in, (size_t)reg_lo))) ||
-            (in_used > reg_lo &&
-             (rc = bcp_h2d_async(L->qh, (uint8_t *)S->d_in + reg_lo, tail_src, (size_t)(in_used - reg_lo)))) ||
+        /* device: H2D (side queue) -> kernel -> D2H (side queue) */
+        if ((in_used && (rc = bcp_h2d_async(L->qh, S->d_in, S->h_in, (size_t)in_used))) ||
             (rc = bcp_event_record(S->ev_h, L->qh)) || (rc = bcp_queue_wait_event(L->qk, S->ev_h)) ||
             (rc = bcp_xor_stripes_async(L->qk, st, ns, so, nsrc)) || (rc = bcp_event_record(S->ev_k, L->qk)) ||
             (rc = bcp_queue_wait_event(L->qd, S->ev_k)) ||
             (rc = bcp_d2h_async(L->qd, S->h_out, S->d_out, (size_t)out_used)) ||
-            (rc = bcp_event_record(S->ev_d, L->qd))) {
-            if (batch_map) { /* its copy may have been queued before the failing call */
-                bcp_queue_sync(L->qh);
-                map_release(batch_map);
-            }
+            (rc = bcp_event_record(S->ev_d, L->qd)))
             break;
-        }
-        /* writers start once the batch's D2H is done (completion thread);
-         * the host moves on to batch b+1 meanwhile */
+        /* writes start once the batch's D2H is done (completion thread); the
+         * host moves on to batch b+1 meanwhile */
         latch_init(&S->writes, (long)(last - first));
         S->busy = 1;
         complete_arg *ca = &cargs[b];
-        *ca = (complete_arg){{0}, S, batch_map, &pl->releaser, store_root, tasks, wa, first, last,
-                             pl->shared_io ? &pl->readers : &pl->writers, log,
-                             &errors, &dev_rc, prealloc, pl->shared_io == 1};
+        *ca = (complete_arg){{0}, S, store_root, tasks, wa, first, last, &pl->io, log, &errors, &dev_rc};
         pool_push(&pl->completer, &ca->j, do_complete);
         for (size_t i = first; i < last; i++)
             bytes_written += (tasks[i].rebuild ? 0 : 8u * (uint64_t)tasks[i].n) + tasks[i].out_len;
         ntasks += last - first;
         tm.submit += now_s() - ts;
     }
-    #undef PUSH_READS
     /* a failed submission leaves batch b+1's reads queued: let them finish
      * before the slab and the jobs go away */
     for (int b = 0; b < started; b++)
@@ -1489,19 +1262,10 @@ static int pipeline_exec(bcp_pipeline *pl, const char *store_root, task *tasks, 
         if (!rc && !dev_rc)
             dev_rc = s1 ? s1 : s2 ? s2 : s3;
     }
-    /* no mapping outlives the run: the releaser's queue first (the
-     * completions that pushed to it have all run: their writes latched
-     * above), then whatever a failed submission left (the queues are idle) */
-    if (mapm) {
-        releaser_drain(&pl->releaser);
-        for (size_t i = 0; i < nmaps; i++)
-            map_release(&maps[i]);
-    }
     /* every job has run: the writes latched above, the completions before them */
     free(ra);
     free(wa);
     free(cargs);
-    free(maps);
     tm.drain = now_s() - td;
     tm.read_mode = mode;
     tm.direct_bytes = rd[1];

@@ -153,9 +153,16 @@ int bcp_eventset_scan(bcp_eventset *s, int st, const char *chunks_dir, uint64_t 
 
 #define RUN_MAGIC "BCPRUN01"
 
+/* Stamp of the run_data file's format (the reference's Target.version =
+ * GIT_VERSION, checked at gen/main.c:500-502).  The format has not changed
+ * since it was introduced (1); the r04 build stamped its struct ABI version 2
+ * instead, so 2 reads as the same format and is rewritten as 1. */
+#define RUN_DATA_VERSION 1u
+#define RUN_DATA_VERSION_R04 2u
+
 typedef struct {
     char magic[8];
-    uint32_t version;    /* GIT_VERSION stamp of the writer: BCP_ABI_VERSION here */
+    uint32_t version;    /* RUN_DATA_VERSION */
     uint32_t ntargets;
     int32_t ids[MAX_STORAGE_TARGETS];
 } run_data;
@@ -189,7 +196,7 @@ int bcp_check_targets(const char *store_root, int ntargets, const char *run_data
     run_data cur;
     memset(&cur, 0, sizeof(cur));
     memcpy(cur.magic, RUN_MAGIC, 8);
-    cur.version = BCP_TASK_ABI_VERSION;
+    cur.version = RUN_DATA_VERSION;
     cur.ntargets = (uint32_t)ntargets;
     for (int k = 0; k < ntargets; k++) {
         int rc = read_target_id(store_root, k, &cur.ids[k]);
@@ -209,7 +216,7 @@ int bcp_check_targets(const char *store_root, int ntargets, const char *run_data
         return -errno;
     ssize_t got = read(fd, &last, sizeof(last));
     if (got == (ssize_t)sizeof(last) && !memcmp(last.magic, RUN_MAGIC, 8)) {
-        if (last.version != cur.version) {
+        if (last.version != RUN_DATA_VERSION && last.version != RUN_DATA_VERSION_R04) {
             if (log)
                 fprintf(log, "Version mismatch\n");
             close(fd);

@@ -20,7 +20,10 @@
  *       --fold picks the protocol P role's GPU fold: pipelined (default) or
  *       batched; --read the pipeline's read path (bcp_pipeline_opts.read_mode):
  *       auto (default: copy for stores in memory, direct for a cold store on a
- *       disk), copy, map, or direct (O_DIRECT into the pinned slabs).  A --complete over an existing state needs --force and first
+ *       disk), copy, or direct (O_DIRECT into the pinned slabs); --read with
+ *       --protocol / --procs and --fold with the pipeline are refused (usage):
+ *       each names a path the other engines do not have.  A --complete over
+ *       an existing state needs --force and first
  *       deletes the old parity data and DBs (the script's clean_old,
  *       :94-108, :120-126).  On success <root>/last-gen-timestamp.
  *   bcp parity-rebuild [--pipeline|--protocol|--procs] [--fold MODE] [--read PATH] [--lanes N]
@@ -57,7 +60,8 @@ static int usage(void)
           "               process_task, ranks as threads) | --procs (ranks as processes)\n"
           "       MODE (protocol P-role fold): pipelined (default) | batched\n"
           "       PATH (pipeline read path): auto (default: copy in memory, direct for cold disk stores) | copy |\n"
-          "            map | direct (O_DIRECT)\n",
+          "            direct (O_DIRECT)\n"
+          "       --read applies to the pipeline only, --fold to --protocol / --procs only\n",
           stderr);
     return 1;
 }
@@ -70,8 +74,6 @@ static int read_mode_arg(const char *s)
         return BCP_READ_AUTO;
     if (!strcmp(s, "copy"))
         return BCP_READ_COPY;
-    if (!strcmp(s, "map"))
-        return BCP_READ_MAP;
     if (!strcmp(s, "direct"))
         return BCP_READ_DIRECT;
     return -1;
@@ -137,7 +139,7 @@ static double now_s(void)
 static int cmd_gen(int argc, char **argv)
 {
     const double t_start = now_s();
-    int complete = -1, engines = 0, use_pipeline = 1, use_procs = 0, lanes = 12, force = 0;
+    int complete = -1, engines = 0, use_pipeline = 1, use_procs = 0, lanes = 12, force = 0, read_arg = 0, fold_arg = 0;
     const char *changelog = NULL;
     int i = 0;
     for (; i < argc && argv[i][0] == '-'; i++) {
@@ -152,10 +154,12 @@ static int cmd_gen(int argc, char **argv)
         else if (!strcmp(argv[i], "--procs"))
             engines++, use_pipeline = 0, use_procs = 1;
         else if (!strcmp(argv[i], "--fold") && i + 1 < argc) {
+            fold_arg = 1;
             if (fold_mode_arg(argv[++i]) < 0 || bcp_task_set_fold_mode(fold_mode_arg(argv[i])) < 0)
                 return usage();
         }
         else if (!strcmp(argv[i], "--read") && i + 1 < argc) {
+            read_arg = 1;
             if ((g_read_mode = read_mode_arg(argv[++i])) < 0)
                 return usage();
         }
@@ -168,7 +172,7 @@ static int cmd_gen(int argc, char **argv)
         else
             return usage();
     }
-    if (complete < 0 || argc - i != 2 || engines > 1)
+    if (complete < 0 || argc - i != 2 || engines > 1 || (read_arg && !use_pipeline) || (fold_arg && use_pipeline))
         return usage();
     const char *root = argv[i];
     const int ntargets = atoi(argv[i + 1]);
@@ -270,7 +274,7 @@ static int cmd_gen(int argc, char **argv)
 static int cmd_rebuild(int argc, char **argv)
 {
     const char *db = NULL, *corrupt = NULL;
-    int engines = 0, use_pipeline = 1, use_procs = 0;
+    int engines = 0, use_pipeline = 1, use_procs = 0, read_arg = 0, fold_arg = 0;
     int i = 0;
     for (; i < argc && argv[i][0] == '-'; i++) {
         if (!strcmp(argv[i], "--db") && i + 1 < argc)
@@ -284,9 +288,11 @@ static int cmd_rebuild(int argc, char **argv)
         else if (!strcmp(argv[i], "--procs"))
             engines++, use_pipeline = 0, use_procs = 1;
         else if (!strcmp(argv[i], "--fold") && i + 1 < argc) {
+            fold_arg = 1;
             if (fold_mode_arg(argv[++i]) < 0 || bcp_task_set_fold_mode(fold_mode_arg(argv[i])) < 0)
                 return usage();
         } else if (!strcmp(argv[i], "--read") && i + 1 < argc) {
+            read_arg = 1;
             if ((g_read_mode = read_mode_arg(argv[++i])) < 0)
                 return usage();
         } else if (!strcmp(argv[i], "--lanes") && i + 1 < argc) {
@@ -295,7 +301,7 @@ static int cmd_rebuild(int argc, char **argv)
         } else
             return usage();
     }
-    if (argc - i != 3 || engines > 1)
+    if (argc - i != 3 || engines > 1 || (read_arg && !use_pipeline) || (fold_arg && use_pipeline))
         return usage();
     const char *root = argv[i];
     const int ntargets = atoi(argv[i + 1]), target = atoi(argv[i + 2]);

@@ -41,13 +41,15 @@
 extern "C" {
 #endif
 
-/* 2 (r04): bcp_task.h's bcp_run_stats gained `refused`, bcp_pipeline_opts
+/* 3 (r05): the pipeline's MAP read mode (BCP_READ_MAP), its
+ * bcp_pipeline_timing fields and bcp_host_register_dma_src removed.
+ * 2 (r04): bcp_task.h's bcp_run_stats gained `refused`, bcp_pipeline_opts
  * `read_mode`, bcp_pipeline_timing the MAP fields; bcp_host_register_dma_src
  * added.  Since 1 (r03): fold modes ZERO_COPY, STAGED, STREAMED and
  * DEVICE_ROWS, bcp_dev_alloc_hostwrite and the engine keys they used were
  * removed, and the default window padding became BCP_PAD_AUTO
  * ("ABI history"). */
-#define BCP_ABI_VERSION 2
+#define BCP_ABI_VERSION 3
 #define BCP_MAX_SOURCES 56                  /* MAX_STORAGE_TARGETS, common.h:18 */
 #define BCP_WINDOW_BYTES (10u * 1024u * 1024u) /* FILE_TRANSFER_BUFFER_SIZE, task_processing.c:20 */
 
@@ -131,12 +133,6 @@ int bcp_host_free(bcp_engine *eng, void *hptr);
  * bcp_host_alloc_mapped memory; -EIO if the device cannot address it at its
  * host address.  Unregister before the memory is unmapped or reused. */
 int bcp_host_register(bcp_engine *eng, void *hptr, size_t bytes);
-/* Register caller memory only as the SOURCE of bcp_h2d_async copies (pages
- * pinned read-only; kernels do not address it): e.g. a PROT_READ mapping of
- * chunk files, copied to the device straight out of the page cache.  -EIO if
- * the pages cannot be pinned (a file truncated under its mapping).
- * Unregister with bcp_host_unregister before unmapping. */
-int bcp_host_register_dma_src(bcp_engine *eng, const void *hptr, size_t bytes);
 int bcp_host_unregister(bcp_engine *eng, void *hptr);
 /* Async copies, in order on q. */
 int bcp_h2d_async(bcp_queue *q, void *dst, const void *src, size_t bytes);

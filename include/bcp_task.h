@@ -457,8 +457,9 @@ int bcp_eventset_scan(bcp_eventset *s, int st, const char *chunks_dir, uint64_t 
 /* Storage-target bookkeeping of gen/main.c:472-551 over <root>/st<k>: ids
  * from st<k>/targetNumID (k+1 when absent), checked against and saved to
  * run_data_path.  -EEXIST duplicate id, -ENODEV fewer targets or a target
- * whose id changed ("Storage target missing!"), -EPROTO version stamp. */
-#define BCP_TASK_ABI_VERSION 2
+ * whose id changed ("Storage target missing!"), -EPROTO version stamp (the
+ * file's own format stamp, 1; not the struct ABI: BCP_ABI_VERSION). */
+#define BCP_TASK_ABI_VERSION 3 /* = BCP_ABI_VERSION (include/bcp.h) */
 int bcp_check_targets(const char *store_root, int ntargets, const char *run_data_path, FILE *log);
 
 /* Cumulative store weights st_weight (gen/main.c:485, 528-536) of
@@ -489,32 +490,24 @@ typedef struct {
 /* Read paths of the pipeline's input:
  *   COPY: io threads read() each chunk into the slot's pinned slab, one H2D
  *     per batch (page cache -> slab -> device: the CPU copies every byte);
- *   MAP:  a share of every batch is mmap'ed (MAP_FIXED into a range of its
- *     own), registered read-only (bcp_host_register_dma_src) and copied to the
- *     device straight out of the page cache, while the io threads read the
- *     rest; the share follows the measured rates of the two (mapping and
- *     pinning is serial per process).  A releaser thread unregisters and
- *     unmaps each batch's range once its copy is done (unregistering waits
- *     for the whole device, so the submitting thread never does it); at most
- *     16 GiB / 24,576 files are mapped at once, beyond which batches are read.
- *     A batch whose mapping cannot be registered (a file truncated meanwhile)
- *     is read instead.
- *     Input offsets are page-aligned in this mode.
  *   DIRECT: the io threads read each chunk file with O_DIRECT straight into
- *     the pinned slab (page layout as MAP): on a disk-backed store the
+ *     the pinned slab (page layout: every file from offset 0 at a page-aligned
+ *     slab offset): on a disk-backed store the
  *     storage device's DMA fills the slab and no CPU copies the bytes.  A
  *     file the filesystem will not read that way (open or read refused) is
  *     read through the page cache instead, piece by piece.  O_DIRECT reads
  *     bypass the page cache: for a store whose chunks are cached (just
  *     written, or on tmpfs) COPY is the faster choice.
- *   AUTO (0): chosen per run between COPY and DIRECT -- COPY on tmpfs / ramfs
+ *   AUTO (0): chosen per run between COPY and DIRECT -- COPY when every
+ *     source directory of the run (<root>/st<k>/chunks, parity) is tmpfs / ramfs,
  *     or when a sample of the run's chunks (mincore over the first 16 MiB of
  *     one source in each of up to 64 tasks) is mostly in the page cache,
  *     DIRECT otherwise (a cold store on a disk); bcp_pipeline_timing.read_mode
- *     says which.  Env BCP_PIPELINE_READ=copy|map|direct names a mode instead. */
+ *     says which.  Env BCP_PIPELINE_READ=copy|direct names a mode instead.
+ * (2 was MAP -- mmap + read-only registration of the chunk files -- removed
+ * in ABI 3: AUTO never chose it; bcp_pipeline_create returns -EINVAL for it.) */
 #define BCP_READ_AUTO 0
 #define BCP_READ_COPY 1
-#define BCP_READ_MAP 2
 #define BCP_READ_DIRECT 3
 
 /* Parity generation for local stores without per-task messaging: chunk
@@ -530,9 +523,9 @@ typedef struct {
  * default, 16 GiB pinned over 8 GPUs (slabs grow to the largest stripe's
  * inputs) -- plus 2 x io_threads io threads (16 per GPU by default, within
  * the CPUs the process may use): one pool that reads chunks and writes
- * parity files, taking reads first (env BCP_PIPELINE_SHARED_IO=0: a reader
- * and a writer pool of io_threads each, as before r04); MAP mode adds a
- * reserved (not committed) address range of the input slab's size per slot. */
+ * parity files, taking reads first.  posix_fallocate of each output (as
+ * task_processing.c:186) is skipped where that output's directory is tmpfs /
+ * ramfs (it would zero every page the write fills again). */
 int bcp_pipeline_gen(const char *store_root, int ntargets, const bcp_work_item *items, size_t nitems,
                      const bcp_pipeline_opts *opts, FILE *log, bcp_run_stats *stats);
 /* The same as a long-lived object: engine, queues, io threads and pinned /
@@ -547,18 +540,14 @@ int bcp_pipeline_destroy(bcp_pipeline *pl);
  * (seconds; for tools): stat phase, blocked on a batch's reads (the next
  * batch's reads are already queued then), waiting for a slot's previous
  * batch to be written before queueing reads into it, building and submitting
- * batches, and the drain after the last submission; MAP mode: the host
- * thread's mapping + registering time, the bytes copied out of mappings, and
- * batches that fell back to reading; DIRECT mode: the data bytes read with
- * O_DIRECT and the pieces read through the page cache instead. */
+ * batches, and the drain after the last submission; DIRECT mode: the data
+ * bytes read with O_DIRECT and the pieces read through the page cache
+ * instead.  (ABI 3 removed the MAP fields map / mapped_bytes / map_fallbacks.) */
 typedef struct {
     double stat, read_wait, slot_wait, submit, drain;
     uint32_t batches;    /* device batches */
     uint32_t read_jobs;  /* io read jobs (one per 1 MiB piece of a chunk read into a slab) */
-    double map;
-    uint64_t mapped_bytes;
-    uint32_t map_fallbacks;
-    int read_mode;       /* the mode the run used (BCP_READ_COPY / MAP / DIRECT) */
+    int read_mode;       /* the mode the run used (BCP_READ_COPY / DIRECT) */
     uint64_t direct_bytes;
     uint32_t direct_fallbacks;
 } bcp_pipeline_timing;

@@ -45,7 +45,7 @@ def test_library_exports_every_declared_symbol(bcp):
 
 
 def test_abi_version(bcp):
-    assert bcp.lib().bcp_abi_version() == 2
+    assert bcp.lib().bcp_abi_version() == 3
 
 
 def test_headers_compile_as_c_and_cxx(tmp_path):

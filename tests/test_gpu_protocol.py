@@ -24,12 +24,11 @@ def gpu_fold(bcp, engine):
     bcp.task_shutdown()
 
 
-@pytest.fixture(params=["copy", "map", "direct"])
+@pytest.fixture(params=["copy", "direct"])
 def read_path(request, monkeypatch):
-    """Every read path of the batched pipeline (bcp_pipeline_opts.read_mode
+    """Both read paths of the batched pipeline (bcp_pipeline_opts.read_mode
     AUTO resolves through BCP_PIPELINE_READ): chunks read into pinned slabs,
-    a share of every batch mapped and copied from the page cache, or chunks
-    read with O_DIRECT into the slabs."""
+    or chunks read with O_DIRECT into the slabs."""
     monkeypatch.setenv("BCP_PIPELINE_READ", request.param)
     return request.param
 
@@ -229,14 +228,11 @@ def test_pipeline_object_reuse_and_growth(bcp, oracle, tmp_path):
             for (path, holders, p, lens) in files:
                 assert S.read_file(S.parity_path(root, p, path)) == oracle.gen_parity_file(contents[path]), path
             # one io read job per 1 MiB piece of every chunk read into a slab
-            # (bcp_pipeline_last_timing); MAP mode reads only the unmapped ones;
-            # DIRECT reads the page-rounded file, the same pieces for a gen
+            # (bcp_pipeline_last_timing); DIRECT reads the page-rounded file,
+            # the same pieces for a gen
             tm = pl.last_timing()
             pieces = sum((n + MiB - 1) // MiB for f in files for n in f[3])
-            if os.environ.get("BCP_PIPELINE_READ") == "map":
-                assert tm["read_jobs"] <= pieces and (tm["read_jobs"] < pieces or tm["mapped_bytes"] == 0), tm
-            else:
-                assert tm["read_jobs"] == pieces, tm
+            assert tm["read_jobs"] == pieces, tm
             assert 1 <= tm["batches"] <= len(files) and min(tm[k] for k in ("stat", "read_wait", "submit")) >= 0
     finally:
         pl.close()
@@ -442,7 +438,7 @@ def test_rank_pool_on_device(tmp_path, mode):
     assert r.returncode == 0 and "pool ok" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]
 
 
-@pytest.mark.parametrize("engine_kind", ["default", "protocol", "pipeline", "pipeline_map", "pipeline_direct", "procs",
+@pytest.mark.parametrize("engine_kind", ["default", "protocol", "pipeline", "pipeline_direct", "procs",
                                          "procs_batched"])
 def test_cli_complete_partial_rebuild(bcp, oracle, tmp_path, engine_kind):
     """bin/bcp end to end on the device: --complete (scan of every target),
@@ -467,7 +463,7 @@ def test_cli_complete_partial_rebuild(bcp, oracle, tmp_path, engine_kind):
             arrs.append(d)
         files[path], contents[path] = holders, arrs
     flags = {"default": [], "protocol": ["--protocol"], "pipeline": ["--pipeline"],
-             "pipeline_map": ["--pipeline", "--read", "map"], "pipeline_direct": ["--read", "direct"],
+             "pipeline_direct": ["--read", "direct"],
              "procs": ["--procs"], "procs_batched": ["--procs", "--fold", "batched"]}[engine_kind]
     r = subprocess.run([bcp.BIN_PATH, "parity-gen", "--complete", *flags, root, str(nt)], capture_output=True)
     assert r.returncode == 0, r.stderr
@@ -702,15 +698,13 @@ def test_caller_transport_table_on_device(bcp, oracle, tmp_path, foreign_ops_add
         bcp.set_transport(None)
 
 
-@pytest.mark.parametrize("mode", ["map", "copy", "direct"])
+@pytest.mark.parametrize("mode", ["copy", "direct"])
 def test_pipeline_read_modes_byte_identical_and_fallback(bcp, oracle, tmp_path, mode):
-    """read_mode MAP: part of every batch goes to the device straight out of
-    mapped chunk files (timing.mapped_bytes), the output is the COPY path's
-    byte for byte; a chunk that cannot be opened (mode 000: stat works, open
-    does not) makes its batch fall back to reading, with the same result --
-    the source counts as unreadable (zeros) exactly as in COPY mode.  DIRECT:
-    every chunk is read with O_DIRECT (timing.direct_bytes), or through the
-    page cache where the filesystem refuses it, with the same output."""
+    """Both read paths write the same parity files; a chunk that cannot be
+    opened (mode 000: stat works, open does not) counts as unreadable (zeros)
+    in either.  DIRECT: every chunk is read with O_DIRECT
+    (timing.direct_bytes), or through the page cache where the filesystem
+    refuses it, with the same output."""
     rng = np.random.default_rng(4242)
     nt = 9
     files = []
@@ -721,7 +715,7 @@ def test_pipeline_read_modes_byte_identical_and_fallback(bcp, oracle, tmp_path, 
     root = str(tmp_path / "store")
     items, contents = S.populate(root, nt, files, seed=17)
     bad = S.chunk_path(root, files[40][1][2], files[40][0])
-    want_mode = {"map": bcp.READ_MAP, "copy": bcp.READ_COPY, "direct": bcp.READ_DIRECT}[mode]
+    want_mode = {"copy": bcp.READ_COPY, "direct": bcp.READ_DIRECT}[mode]
     outs = {}
     for locked in (False, True):
         if locked:
@@ -737,12 +731,6 @@ def test_pipeline_read_modes_byte_identical_and_fallback(bcp, oracle, tmp_path, 
             os.chmod(bad, 0o600)
         assert st.errors == 0 and st.tasks == len(files)
         assert tm["read_mode"] == want_mode and tm["batches"] > 4
-        if mode == "map":
-            assert tm["mapped_bytes"] > 0 and tm["map"] > 0
-            if not locked:  # (locked: the bad chunk's batch falls back if that task was to be mapped)
-                assert tm["map_fallbacks"] == 0
-        else:
-            assert tm["mapped_bytes"] == 0 and tm["map_fallbacks"] == 0
         if mode == "direct":
             total = sum(sum(f[3]) for f in files)
             # all of it with O_DIRECT, or pieces through the page cache (a
@@ -819,13 +807,15 @@ def test_pipeline_direct_reads_fall_back_piece_by_piece(bcp, oracle, tmp_path, m
         pl.close()
 
 
-@pytest.mark.parametrize("shared_io", ["0", "1", "2", "3"])
-def test_pipeline_io_pool_orders_same_files(bcp, oracle, tmp_path, monkeypatch, shared_io):
-    """Every io pool arrangement (BCP_PIPELINE_SHARED_IO: separate reader and
-    writer pools, or one pool taking writes first, in push order, or reads
-    first -- the default) writes the same parity files and rebuilt chunks,
-    with few threads and small slabs so jobs of both kinds queue up."""
-    monkeypatch.setenv("BCP_PIPELINE_SHARED_IO", shared_io)
+@pytest.mark.parametrize("mode", ["copy", "direct"])
+def test_pipeline_small_pool_and_odd_holder_counts(bcp, oracle, tmp_path, mode):
+    """The io pool (reads ahead of writes) with few threads and small slabs,
+    so jobs of both kinds queue up: the same parity files and rebuilt chunks.
+    Holder counts 2..8 give rebuild stripes of every source count n, so for
+    odd n the parity body starts 8n bytes into its file -- an 8-byte-aligned
+    source in the slab's page layout under DIRECT, 256-byte
+    aligned under COPY -- and the rebuilt chunks must still match byte for
+    byte."""
     rng = np.random.default_rng(17)
     nt = 9
     files = []
@@ -834,19 +824,23 @@ def test_pipeline_io_pool_orders_same_files(bcp, oracle, tmp_path, monkeypatch, 
         files.append((f"p/{i % 4}/c{i}", holders, p, [int(x) for x in rng.integers(1, 1 * MiB, size=len(holders))]))
     root = str(tmp_path)
     items, contents = S.populate(root, nt, files, seed=19)
-    pl = bcp.Pipeline(slab_bytes=4 << 20, io_threads=2, nslots=2)
+    want_mode = {"copy": bcp.READ_COPY, "direct": bcp.READ_DIRECT}[mode]
+    victim = 3
+    ns = {len(h) for _, h, _, _ in files if victim in h}   # rebuild sources: survivors + parity body
+    assert {3, 5, 7} <= ns, ns
+    pl = bcp.Pipeline(slab_bytes=4 << 20, io_threads=2, nslots=2, read_mode=want_mode)
     try:
         st = pl.run(root, nt, items)
         assert st.errors == 0 and st.tasks == len(files)
         for path, holders, p, lens in files:
             assert S.read_file(S.parity_path(root, p, path)) == oracle.gen_parity_file(contents[path]), path
-        victim = 3
         lost = {path: S.read_file(S.chunk_path(root, victim, path)) for path, holders, _, _ in files
                 if victim in holders}
         for path in lost:
             os.remove(S.chunk_path(root, victim, path))
         st = pl.rebuild(root, nt, victim, sorted(items, key=lambda x: x[0].encode()))
         assert st.errors == 0 and st.tasks == len(lost)
+        assert pl.last_timing()["read_mode"] == want_mode
         for path, data in lost.items():
             assert S.read_file(S.chunk_path(root, victim, path)) == data, path
     finally:

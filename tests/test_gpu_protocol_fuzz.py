@@ -86,7 +86,7 @@ def fuzz_rounds(bcp, oracle, tmp_path, budget, seed, engines):
             bcp.set_explicit_padding(pad)
             bcp.set_fold_inflight(int(rng.choice([1, 1, 2, 4])))
             what = f"seed {seed} round {rounds} {how} pad {pad}"
-            read_mode = int(rng.choice([bcp.READ_AUTO, bcp.READ_COPY, bcp.READ_MAP, bcp.READ_DIRECT]))  # the pipeline's read path
+            read_mode = int(rng.choice([bcp.READ_AUTO, bcp.READ_COPY, bcp.READ_DIRECT]))  # the pipeline's read path
             if how == "pipeline":
                 what += f" read_mode {read_mode}"
                 if rng.random() < 0.3:  # a cold store: written back and dropped (AUTO then reads with O_DIRECT)

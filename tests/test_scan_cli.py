@@ -82,6 +82,50 @@ def test_check_targets_bookkeeping(bcp, tmp_path):
         bcp.check_targets(root, 4, str(tmp_path / "other"))
 
 
+def test_run_data_stamp_is_the_file_format_not_the_abi(bcp, tmp_path):
+    """run_data carries its own format stamp (1), independent of
+    the struct ABI; a store the r04 build stamped 2 still passes (the format
+    is the same) and is rewritten as 1; any other stamp is refused."""
+    import struct
+    root, rd = str(tmp_path), tmp_path / "run_data"
+    S.make_store(root, 3)
+    bcp.check_targets(root, 3, str(rd))
+    raw = bytearray(rd.read_bytes())
+    assert raw[:8] == b"BCPRUN01" and struct.unpack_from("<I", raw, 8)[0] == 1
+    struct.pack_into("<I", raw, 8, 2)                # as the r04 build wrote it
+    rd.write_bytes(bytes(raw))
+    bcp.check_targets(root, 3, str(rd))
+    assert struct.unpack_from("<I", rd.read_bytes(), 8)[0] == 1
+    struct.pack_into("<I", raw, 8, 7)
+    rd.write_bytes(bytes(raw))
+    with pytest.raises(bcp.BcpError):                # "Version mismatch"
+        bcp.check_targets(root, 3, str(rd))
+
+
+def test_read_and_fold_flags_only_with_their_engine(bcp, tmp_path):
+    """--read names a pipeline read path, --fold a protocol P-role
+    fold; given to the other engine they would be ignored, so they are refused."""
+    S.make_store(str(tmp_path), 3)
+    for cmd in (["parity-gen", "--complete", "--protocol", "--read", "copy", str(tmp_path), "3"],
+                ["parity-gen", "--complete", "--procs", "--read", "direct", str(tmp_path), "3"],
+                ["parity-gen", "--complete", "--fold", "batched", str(tmp_path), "3"],
+                ["parity-rebuild", "--protocol", "--read", "copy", str(tmp_path), "3", "1"],
+                ["parity-rebuild", "--pipeline", "--fold", "batched", str(tmp_path), "3", "1"],
+                ["parity-gen", "--complete", "--read", "map", str(tmp_path), "3"]):   # MAP: removed in ABI 3
+        r = subprocess.run([bcp.BIN_PATH, *cmd], capture_output=True)
+        assert r.returncode == 1 and b"usage" in r.stderr, cmd
+    assert not os.path.exists(tmp_path / "run_data")  # refused before touching the store
+
+
+def test_pipeline_refuses_the_removed_map_read_mode(bcp):
+    """read_mode 2 (MAP, ABI 2) is rejected before any device is touched."""
+    import ctypes
+    opts = bcp.PipelineOpts(0, 1 << 20, 1, 2, 1, 2)
+    pl = ctypes.c_void_p()
+    assert bcp.lib().bcp_pipeline_create(ctypes.byref(opts), ctypes.byref(pl)) == -22
+    assert not pl.value
+
+
 def test_cli_usage_and_loud_failure_without_gpu(bcp, tmp_path):
     r = subprocess.run([bcp.BIN_PATH], capture_output=True)
     assert r.returncode == 1 and b"usage" in r.stderr

@@ -11,7 +11,7 @@ against the originals.  Rates: (chunk bytes read + bytes written) / wall
 time; the host-to-device link's bound beside them (tools/box_probe.py).
 One JSON line per measurement.
 
---modes copy,map,direct: the pipeline's read paths (bcp_pipeline_opts.read_mode),
+--modes copy,direct: the pipeline's read paths (bcp_pipeline_opts.read_mode),
 interleaved run by run; --contend 0,16: with N host threads memcpy'ing
 64 MiB buffers meanwhile (host memory bandwidth taken, as by the other GPUs'
 pipelines of one node), also interleaved.
@@ -61,7 +61,7 @@ def main():
     ap.add_argument("--contend", default="0")
     ap.add_argument("--evict", action="store_true")
     a = ap.parse_args()
-    modes = {"copy": bcp.READ_COPY, "map": bcp.READ_MAP, "direct": bcp.READ_DIRECT}
+    modes = {"copy": bcp.READ_COPY, "direct": bcp.READ_DIRECT}
     mode_list = a.modes.split(",")
     contend_list = [int(x) for x in a.contend.split(",")]
     import box_probe
