@@ -181,6 +181,12 @@ _SIGS = {
     "bcp_plan_rounds": ([_V, ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(WorkItem), ctypes.c_size_t,
                          ctypes.POINTER(WorkItem), ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t),
                          ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
+    "bcp_plan_rounds_ordered": ([_V, ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
+                                 ctypes.POINTER(WorkItem), ctypes.c_size_t, ctypes.POINTER(WorkItem), ctypes.c_size_t,
+                                 ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
+    "bcp_map_targets": ([ctypes.POINTER(ctypes.c_int32), ctypes.c_int, ctypes.POINTER(ctypes.c_int32), ctypes.c_int,
+                         ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
+    "bcp_store_round_order": ([ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
     "bcp_assign_lanes_rounds": ([ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(FileInfo),
                                  ctypes.POINTER(ctypes.c_int)], None),
     "bcp_lb_finalize": ([], ctypes.c_int),
@@ -866,9 +872,11 @@ class EventSet:
         """prev: iterable of (path, timestamp, locations); returns [(path, timestamp, locations)]."""
         return self.plan_rounds(ntargets, cum_weight, prev)[0]
 
-    def plan_rounds(self, ntargets: int, cum_weight, prev=()):
+    def plan_rounds(self, ntargets: int, cum_weight, prev=(), round_st=None):
         """bcp_plan_rounds: (worklist, round_start) -- the coordinators' rounds
-        back to back, round k = worklist[round_start[k]:round_start[k+1]]."""
+        back to back, round k = worklist[round_start[k]:round_start[k+1]];
+        round_st (bcp_plan_rounds_ordered): the target whose eater broadcasts
+        round r, in MPI rank order (None = target order)."""
         prev = sorted(prev, key=lambda x: x[0].encode())
         parr, keep = _items(prev)
         cw = (ctypes.c_int * ntargets)(*cum_weight)
@@ -876,7 +884,11 @@ class EventSet:
         call("bcp_plan_worklist", self.h, ntargets, cw, parr, len(prev), None, 0, ctypes.byref(n))
         out = (WorkItem * max(n.value, 1))()
         rs = (ctypes.c_size_t * (ntargets + 1))()
-        call("bcp_plan_rounds", self.h, ntargets, cw, parr, len(prev), out, n.value, ctypes.byref(n), rs)
+        if round_st is None:
+            call("bcp_plan_rounds", self.h, ntargets, cw, parr, len(prev), out, n.value, ctypes.byref(n), rs)
+        else:
+            call("bcp_plan_rounds_ordered", self.h, ntargets, cw, (ctypes.c_int * ntargets)(*round_st), parr,
+                 len(prev), out, n.value, ctypes.byref(n), rs)
         del keep
         return ([(out[i].path.decode(), out[i].fi.timestamp, out[i].fi.locations) for i in range(n.value)],
                 list(rs))
@@ -892,6 +904,24 @@ BIN_PATH = os.path.join(PKG_DIR, "bin", "bcp")
 
 def check_targets(store_root: str, ntargets: int, run_data: str):
     call("bcp_check_targets", store_root.encode(), ntargets, run_data.encode(), None)
+
+
+def map_targets(prev_ids, rank_ids):
+    """bcp_map_targets (gen/main.c:498-499, 506-541): (st_ids, round_st), or
+    BcpError (-EEXIST duplicate, -ENODEV fewer / missing)."""
+    n = len(rank_ids)
+    st = (ctypes.c_int32 * max(n, 1))()
+    rs = (ctypes.c_int * max(n, 1))()
+    call("bcp_map_targets", (ctypes.c_int32 * max(len(prev_ids), 1))(*prev_ids), len(prev_ids),
+         (ctypes.c_int32 * max(n, 1))(*rank_ids), n, st, rs)
+    return list(st)[:n], list(rs)[:n]
+
+
+def store_round_order(store_root: str, ntargets: int) -> list:
+    """bcp_store_round_order: the target of every round from <root>/rank_order."""
+    rs = (ctypes.c_int * ntargets)()
+    call("bcp_store_round_order", store_root.encode(), ntargets, rs)
+    return list(rs)
 
 
 def path_hash(path: str) -> int:

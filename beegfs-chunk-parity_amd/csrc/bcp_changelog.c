@@ -433,21 +433,34 @@ static int cmp_size(const void *a, const void *b)
 
 /*
  * Phase 2's worklist as the reference's coordinators produce it.  Phase 1
- * sends every path to eater simple_hash(path) % ntargets (gen/main.c:310);
- * each eater keeps its paths in arrival order, shuffles them with the
- * fixed-seed PCG32 and sorts them by total size (:710-711); then the eaters
- * broadcast their lists one round at a time, in rank order (:758-797), and
- * every round is planned item by item against the DB (:772-788) and given
- * its own lanes (:823).  Here eater k = storage target k and arrival order =
- * the event set's first-seen order (targets fed 0, 1, ...: the reference's
- * interleaving of several feeders is not deterministic).  round_start[k] is
- * where round k begins in out; round_start[ntargets] = *nout.
+ * sends every path to the eater of storage target simple_hash(path) %
+ * ntargets (gen/main.c:310, eater_rank_from_st :77-80); each eater keeps its
+ * paths in arrival order, shuffles them with the fixed-seed PCG32 and sorts
+ * them by total size (:710-711); then the eaters broadcast their lists one
+ * round at a time, in MPI rank order (:758-797: communicator rank i is world
+ * rank 2i-1, the eater of storage target rank2st[2i-1]), and every round is
+ * planned item by item against the DB (:772-788) and given its own lanes
+ * (:823).  round_st[r] = the storage target whose eater broadcasts round r
+ * (bcp_map_targets derives it as :506-541 does; NULL = target order, the
+ * order of every first run).  Arrival order = the event set's first-seen
+ * order (targets fed 0, 1, ...: the reference's interleaving of several
+ * feeders is not deterministic).  round_start[r] is where round r begins in
+ * out; round_start[ntargets] = *nout.
  */
-int bcp_plan_rounds(const bcp_eventset *s, int ntargets, const int *cum_weight, const bcp_work_item *prev,
-                    size_t nprev, bcp_work_item *out, size_t out_cap, size_t *nout, size_t *round_start)
+int bcp_plan_rounds_ordered(const bcp_eventset *s, int ntargets, const int *cum_weight, const int *round_st,
+                            const bcp_work_item *prev, size_t nprev, bcp_work_item *out, size_t out_cap,
+                            size_t *nout, size_t *round_start)
 {
     if (!s || ntargets < 1 || ntargets > MAX_STORAGE_TARGETS || !cum_weight || (nprev && !prev) || !nout)
         return -EINVAL;
+    if (round_st) { /* a permutation of the targets */
+        uint64_t seen = 0;
+        for (int r = 0; r < ntargets; r++) {
+            if (round_st[r] < 0 || round_st[r] >= ntargets || (seen >> round_st[r] & 1))
+                return -EINVAL;
+            seen |= UINT64_C(1) << round_st[r];
+        }
+    }
     if (cum_weight[ntargets - 1] <= 0)
         return -EINVAL;
     for (size_t i = 1; i < nprev; i++)
@@ -477,12 +490,22 @@ int bcp_plan_rounds(const bcp_eventset *s, int ntargets, const int *cum_weight, 
         for (size_t i = 0; i < s->n; i++)
             order[fill[eater[i]]++] = (size_index){s->e[i].size, i};
     }
+    /* the eaters' buckets in place (target order), then copied round by round */
+    size_index *rounds = round_st ? malloc((s->n ? s->n : 1) * sizeof(size_index)) : order;
+    if (!rounds) {
+        free(order);
+        free(eater);
+        return -ENOMEM;
+    }
     size_t j = 0;
-    for (int k = 0; k < ntargets; k++) {
+    for (int r = 0; r < ntargets; r++) {
+        const int k = round_st ? round_st[r] : r;
         if (round_start)
-            round_start[k] = j;
+            round_start[r] = j;
         const size_t m = start[k + 1] - start[k];
-        size_index *mine = order + j;
+        size_index *mine = rounds + j;
+        if (round_st)
+            memcpy(mine, order + start[k], m * sizeof(size_index));
         /* shuffle (gen/main.c:373-386, a fresh fixed-seed generator per
          * eater) then sort by total size */
         if (m > 1) {
@@ -517,9 +540,17 @@ int bcp_plan_rounds(const bcp_eventset *s, int ntargets, const int *cum_weight, 
     }
     if (round_start)
         round_start[ntargets] = j;
+    if (rounds != order)
+        free(rounds);
     free(order);
     free(eater);
     return 0;
+}
+
+int bcp_plan_rounds(const bcp_eventset *s, int ntargets, const int *cum_weight, const bcp_work_item *prev,
+                    size_t nprev, bcp_work_item *out, size_t out_cap, size_t *nout, size_t *round_start)
+{
+    return bcp_plan_rounds_ordered(s, ntargets, cum_weight, NULL, prev, nprev, out, out_cap, nout, round_start);
 }
 
 int bcp_plan_worklist(const bcp_eventset *s, int ntargets, const int *cum_weight, const bcp_work_item *prev,

@@ -667,10 +667,14 @@ static int round_impl(bcp_pipeline *pl, int procs, const char *store_root, int n
     size_t n = 0, round_start[MAX_STORAGE_TARGETS + 1];
     bcp_work_item *work = NULL;
     int *lanes = NULL;
-    rc = bcp_plan_worklist(events, ntargets, cw, prev, nprev, NULL, 0, &n);
+    int round_st[MAX_STORAGE_TARGETS];
+    rc = bcp_store_round_order(store_root, ntargets, round_st); /* the eaters' rounds in MPI rank order */
+    if (!rc)
+        rc = bcp_plan_worklist(events, ntargets, cw, prev, nprev, NULL, 0, &n);
     if (!rc) {
         work = malloc((n ? n : 1) * sizeof(bcp_work_item));
-        rc = work ? bcp_plan_rounds(events, ntargets, cw, prev, nprev, work, n, &n, round_start) : -ENOMEM;
+        rc = work ? bcp_plan_rounds_ordered(events, ntargets, cw, round_st, prev, nprev, work, n, &n, round_start)
+                  : -ENOMEM;
     }
     if (!rc && !pl) {
         /* lanes per coordinator round (gen/main.c:823); the lanes walk the

@@ -189,6 +189,101 @@ static int read_target_id(const char *root, int k, int32_t *id)
     return 0;
 }
 
+/* gen/main.c:498-499, 506-541 on the coordinator after the Gathers: every
+ * target found in the previous run's list keeps its storage-target index
+ * (a second rank with an id already placed: "Duplicate targetNumID"),
+ * targets not in it are appended in rank order, and an index left without a
+ * rank is "Storage target missing!"; st2rank[i] = the rank of target i, and
+ * round r (communicator rank r+1 = world rank 2r+1, :570-574, :758) is
+ * broadcast by the eater of target rank2st[2r+1]. */
+int bcp_map_targets(const int32_t *prev_ids, int nprev, const int32_t *rank_ids, int ntargets, int32_t *st_ids,
+                    int *round_st)
+{
+    if (ntargets < 1 || ntargets > MAX_STORAGE_TARGETS || nprev < 0 || nprev > MAX_STORAGE_TARGETS ||
+        (nprev && !prev_ids) || !rank_ids || !st_ids || !round_st)
+        return -EINVAL;
+    if (ntargets < nprev)
+        return -ENODEV; /* "Fewer targets than last run, something is wrong!" */
+    int32_t ids[2 * MAX_STORAGE_TARGETS];
+    int rank_of[2 * MAX_STORAGE_TARGETS];
+    for (int j = 0; j < nprev; j++) {
+        ids[j] = prev_ids[j];
+        rank_of[j] = -1;
+    }
+    int k = nprev;
+    for (int r = 0; r < ntargets; r++) {
+        int found = 0;
+        for (int j = 0; j < nprev; j++)
+            if (ids[j] == rank_ids[r]) {
+                if (rank_of[j] != -1)
+                    return -EEXIST; /* "Duplicate targetNumID = %d" */
+                rank_of[j] = r;
+                found = 1;
+                break;
+            }
+        if (!found) {
+            ids[k] = rank_ids[r];
+            rank_of[k++] = r;
+        }
+    }
+    for (int i = 0; i < ntargets; i++)
+        if (rank_of[i] == -1)
+            return -ENODEV; /* "Storage target missing! targetNumID = %d" */
+    for (int i = 0; i < ntargets; i++) {
+        st_ids[i] = ids[i];
+        round_st[rank_of[i]] = i;
+    }
+    return 0;
+}
+
+/* <root>/rank_order: the targetNumID of every storage target's eater rank in
+ * MPI rank order -- the order of the hosts in the hostfile the parity-gen
+ * script builds from etc/hosts (src/beegfs-parity-gen:114-117), whitespace
+ * separated.  Absent: target order.  -ENOENT absent, -EPROTO malformed. */
+static int read_rank_order(const char *root, int ntargets, int32_t *rank_ids)
+{
+    char p[4096];
+    int n = snprintf(p, sizeof(p), "%s/rank_order", root);
+    if (n < 0 || (size_t)n >= sizeof(p))
+        return -ENAMETOOLONG;
+    FILE *f = fopen(p, "r");
+    if (!f)
+        return errno == ENOENT ? -ENOENT : -errno;
+    int got = 0, rc = 0;
+    long v;
+    while (fscanf(f, "%ld", &v) == 1) {
+        if (got >= ntargets || v < INT32_MIN || v > INT32_MAX) {
+            rc = -EPROTO;
+            break;
+        }
+        rank_ids[got++] = (int32_t)v;
+    }
+    if (!rc && (!feof(f) || got != ntargets))
+        rc = -EPROTO;
+    fclose(f);
+    return rc;
+}
+
+int bcp_store_round_order(const char *store_root, int ntargets, int *round_st)
+{
+    if (!store_root || !round_st || ntargets < 1 || ntargets > MAX_STORAGE_TARGETS)
+        return -EINVAL;
+    int32_t cur[MAX_STORAGE_TARGETS], rank_ids[MAX_STORAGE_TARGETS], st_ids[MAX_STORAGE_TARGETS];
+    int rc = read_rank_order(store_root, ntargets, rank_ids);
+    if (rc == -ENOENT) {
+        for (int r = 0; r < ntargets; r++)
+            round_st[r] = r;
+        return 0;
+    }
+    if (rc)
+        return rc;
+    for (int k = 0; k < ntargets; k++)
+        if ((rc = read_target_id(store_root, k, &cur[k])))
+            return rc;
+    /* the directories are the persisted index order (bcp_check_targets) */
+    return bcp_map_targets(cur, ntargets, rank_ids, ntargets, st_ids, round_st);
+}
+
 int bcp_check_targets(const char *store_root, int ntargets, const char *run_data_path, FILE *log)
 {
     if (!store_root || !run_data_path || ntargets < 1 || ntargets > MAX_STORAGE_TARGETS)
@@ -241,6 +336,34 @@ int bcp_check_targets(const char *store_root, int ntargets, const char *run_data
     } else if (got != 0) {
         close(fd);
         return -EPROTO;
+    }
+    /* the rank order (<root>/rank_order) against the index order the
+     * reference would derive from the previous run's list (gen/main.c:506-541;
+     * a first run: the directories' order): targets added since must be
+     * numbered st<k> in the order the reference appends them, rank order */
+    {
+        int32_t rank_ids[MAX_STORAGE_TARGETS], st_ids[MAX_STORAGE_TARGETS];
+        int round_st[MAX_STORAGE_TARGETS];
+        int rc = read_rank_order(store_root, ntargets, rank_ids);
+        if (rc != -ENOENT) {
+            const int first = !(got == (ssize_t)sizeof(last));
+            if (!rc)
+                rc = bcp_map_targets(first ? cur.ids : last.ids, first ? ntargets : (int)last.ntargets, rank_ids,
+                                     ntargets, st_ids, round_st);
+            for (int k = 0; k < ntargets && !rc; k++)
+                if (st_ids[k] != cur.ids[k]) {
+                    if (log)
+                        fprintf(log, "st%d holds targetNumID %d, but the rank order appends %d there\n", k,
+                                cur.ids[k], st_ids[k]);
+                    rc = -EPROTO;
+                }
+            if (rc) {
+                if (log && rc != -EPROTO)
+                    fprintf(log, "rank_order: %s\n", strerror(-rc));
+                close(fd);
+                return rc;
+            }
+        }
     }
     int rc = 0;
     if (pwrite(fd, &cur, sizeof(cur), 0) != (ssize_t)sizeof(cur))

@@ -24,10 +24,13 @@ any HIP call) and relays rank 0's line and the exit code; it refuses when the
 ranks would share GPUs unless --allow-shared.
 
 roofline.achieved / frac (= frac_event) use the kernel's HIP-event time on the
-stream it runs on; frac_rocprof and traffic come from a live profile on this
-box (rank 0, after the timing: the same workload under rocprofv3 in child
-processes -- kernel trace + stats, then --pmc FETCH_SIZE and --pmc WRITE_SIZE
-in runs of their own; roofline.live_profile, same_box true), or, with
+stream it runs on (an event pair at every step boundary: kernel_ms is the
+average, kernel_ms_median / min / max / steps the per-launch spread);
+frac_rocprof and traffic come from a live profile on this box (rank 0, after
+the timing: the same workload under rocprofv3 in child processes -- kernel
+trace + stats over the parent's warm-up and steps, of which the timed
+dispatches alone are averaged, then --pmc FETCH_SIZE and --pmc WRITE_SIZE in
+runs of their own; roofline.live_profile, same_box true), or, with
 --no-prof or when a child run fails, from the committed profile set of the
 same workload (profiles/CURRENT_SET, profiles/**/*pmc*.json,
 tools/pmc_summary.py), reported beside it as roofline.committed_set.
@@ -47,7 +50,14 @@ own GPU over its own store of chunk files in /dev/shm (config-5 shapes, about
 --e2e-gib GiB per rank, created and removed by the rank): gen (cold + warm
 runs) and the rebuild of one lost target, all ranks at once, sampled parity
 files and rebuilt chunks checked with numpy; rates against the H2D link each
-rank measures over pinned memory at the same time.
+rank measures over pinned memory at the same time; then config 5's
+changelog-driven partial update on the same store (e2e.partial).
+configs (BASELINE configs[0] and [4] as BASELINE states them): config1 -- rank
+0 runs config 1 end to end (4 loopback storage-target ranks, 3-wide stripes,
+1,333 x 512 KiB files) through the per-task protocol with the reference's own
+xor_parity as the P-role fold (the cpu_baseline leg's library, kind
+"reference"), with the GPU fold, and through the pipeline, gen and rebuild, on
+one store in one process; config5_partial -- the e2e block's partial round.
 The output is verified after timing: cleared, one more step, then fold
 conservation plus sampled stripes compared byte for byte with numpy.
 """
@@ -97,12 +107,14 @@ def parse():
     ap.add_argument("--e2e-reps", type=int, default=3, help="warm end-to-end gen runs (after one cold run)")
     ap.add_argument("--e2e-dir", default="/dev/shm", help="where the end-to-end stores are created")
     ap.add_argument("--e2e-max-s", type=float, default=150.0, help="wall-time cap of the end-to-end leg")
-    ap.add_argument("--e2e-modes", default="copy,map,direct",
+    ap.add_argument("--e2e-modes", default="copy,direct",
                     help="pipeline read paths timed end to end, interleaved; the first is the headline")
     ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--no-configs", action="store_true", help="skip the config-1 protocol leg (rank 0)")
+    ap.add_argument("--c1-files", type=int, default=1333, help="config 1: files (3 chunks of 512 KiB each)")
+    ap.add_argument("--c1-reps", type=int, default=3, help="config 1: warm rounds per leg (after one cold round)")
     ap.add_argument("--no-prof", action="store_true",
                     help="skip the live rocprofv3 kernel-trace and PMC passes of this workload on this box")
-    ap.add_argument("--prof-steps", type=int, default=5, help="steps of each profiled child run")
     ap.add_argument("--allow-shared", action="store_true",
                     help="run N ranks even when fewer than N distinct GPUs exist (rehearsal; "
                          "the line then says shared_gpu true and counts distinct GPUs)")
@@ -249,9 +261,14 @@ def live_profile(a, stripes_arg: int, kernel_tag: str, bytes_per_step: int) -> d
     (FETCH_SIZE, WRITE_SIZE: counters in runs of their own, as
     MI355X_MICROARCH.md's HBM recipe prescribes), each a child process
     `rocprofv3 ... -- python3 bench.py <same workload> --no-e2e --no-cpu
-    --no-prof` under its own time limit; HBM bytes per launch with the gfx950
-    corrections of tools/pmc_summary.py (FETCH_SIZE x2, KiB).  So the line's
-    frac_rocprof and traffic come from the machine its frac_event does."""
+    --no-prof --no-configs` under its own time limit; HBM bytes per launch with
+    the gfx950 corrections of tools/pmc_summary.py (FETCH_SIZE x2, KiB).  So
+    the line's frac_rocprof and traffic come from the machine its frac_event
+    does.  The kernel-trace child runs the parent's --warmup and --steps; its
+    timed launches -- the dispatches after the warm-up ones, before the
+    verification one -- are the rocprof figure, and the child's own per-step
+    HIP events time those SAME launches (child_event_ms), so the two clocks
+    are compared on one launch set in one process."""
     import csv
     import shutil
     import signal
@@ -265,7 +282,7 @@ def live_profile(a, stripes_arg: int, kernel_tag: str, bytes_per_step: int) -> d
     out = tempfile.mkdtemp(prefix="bcp_bench_prof_")
     child = [sys.executable, os.path.abspath(__file__), "--gpus", "1", "--mode", a.mode, "--stripes", str(stripes_arg),
              "--nsrc", str(a.nsrc), "--chunk", str(a.chunk), "--rebuild-layout", a.rebuild_layout,
-             "--warmup", "1", "--no-cpu", "--no-e2e", "--no-prof"]
+             "--no-cpu", "--no-e2e", "--no-prof", "--no-configs"]
     for flag, val in (("--blocks-per-cu", a.blocks_per_cu), ("--vecs", a.vecs), ("--grid", a.grid)):
         if val:
             child += [flag, str(val)]
@@ -277,19 +294,25 @@ def live_profile(a, stripes_arg: int, kernel_tag: str, bytes_per_step: int) -> d
            if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK",
                         "MASTER_ADDR", "MASTER_PORT") and not k.startswith("TORCHELASTIC")}
 
-    def run(tag, args, steps):
+    child_line = {}
+
+    def run(tag, args, steps, warmup):
         d_ = os.path.join(out, tag)
-        cmd = [exe] + args + ["-d", d_, "-o", "run", "--output-format", "csv", "--"] + child + ["--steps", str(steps)]
-        p = subprocess.Popen(cmd, env=env, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True,
+        cmd = [exe] + args + ["-d", d_, "-o", "run", "--output-format", "csv", "--"] + child + \
+            ["--steps", str(steps), "--warmup", str(warmup)]
+        p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
                              start_new_session=True)
         try:
-            _, err = p.communicate(timeout=150)
+            so, err = p.communicate(timeout=150)
         except subprocess.TimeoutExpired:
             os.killpg(p.pid, signal.SIGKILL)
             p.wait()
             raise RuntimeError(f"rocprofv3 {tag}: time limit")
         if p.returncode:
             raise RuntimeError(f"rocprofv3 {tag}: exit {p.returncode}: {err[-300:]}")
+        lines = [x for x in so.splitlines() if x.startswith("{")]
+        if lines:
+            child_line[tag] = json.loads(lines[-1])
         return d_
 
     def one(d_, pattern):
@@ -306,15 +329,35 @@ def live_profile(a, stripes_arg: int, kernel_tag: str, bytes_per_step: int) -> d
         return statistics.median(vals), len(vals)
 
     try:
-        stats = one(run("trace", ["--kernel-trace", "--stats"], a.prof_steps), "*kernel_stats.csv")
+        steps = max(1, min(a.steps, 63))
+        d_trace = run("trace", ["--kernel-trace", "--stats"], steps, a.warmup)
+        stats = one(d_trace, "*kernel_stats.csv")
         row = next((r for r in csv.DictReader(open(stats)) if kernel_tag in r["Name"]), None)
         if row is None:
             raise RuntimeError(f"{kernel_tag} not in the kernel statistics")
-        fetch, nf = counter(one(run("pmc_fetch", ["--pmc", "FETCH_SIZE"], 3), "*counter_collection.csv"), "FETCH_SIZE")
-        write, nw = counter(one(run("pmc_write", ["--pmc", "WRITE_SIZE"], 3), "*counter_collection.csv"), "WRITE_SIZE")
+        # the timed dispatches: after the warm-up ones, before the verification one
+        durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+                for r in sorted(csv.DictReader(open(one(d_trace, "*kernel_trace.csv"))), key=lambda r: int(r["Dispatch_Id"]))
+                if kernel_tag in r["Kernel_Name"]]
+        timed = durs[a.warmup:a.warmup + steps]
+        if len(timed) != steps or len(durs) != a.warmup + steps + 1:
+            raise RuntimeError(f"{len(durs)} dispatches of {kernel_tag}, expected {a.warmup} + {steps} + 1")
+        cl = child_line.get("trace", {}).get("roofline", {})
+        ev = cl.get("kernel_ms_steps")
+        fetch, nf = counter(one(run("pmc_fetch", ["--pmc", "FETCH_SIZE"], 3, 1), "*counter_collection.csv"), "FETCH_SIZE")
+        write, nw = counter(one(run("pmc_write", ["--pmc", "WRITE_SIZE"], 3, 1), "*counter_collection.csv"), "WRITE_SIZE")
         traffic = fetch * 1024 * 2 + write * 1024
-        return {"rocprof_avg_ns": float(row["AverageNs"]), "rocprof_calls": int(row["Calls"]),
-                "rocprof_min_ns": float(row["MinNs"]), "traffic": round(traffic),
+        avg_t = statistics.fmean(timed)
+        return {"rocprof_avg_ns": round(avg_t, 1), "rocprof_median_ns": float(statistics.median(timed)),
+                "rocprof_min_ns": float(min(timed)), "rocprof_max_ns": float(max(timed)),
+                "rocprof_timed_launches": len(timed),
+                "rocprof_all_dispatches": {"calls": int(row["Calls"]), "avg_ns": float(row["AverageNs"])},
+                "child_event_ms_median": (round(statistics.median(ev), 4) if ev else None),
+                "child_event_over_rocprof": (round(statistics.median(ev) * 1e6 / statistics.median(timed), 4)
+                                             if ev else None),
+                "child_event_ms_steps": ev,
+                "rocprof_timed_ms_steps": [round(x / 1e6, 4) for x in timed],
+                "traffic": round(traffic),
                 "traffic_over_algorithmic": round(traffic / bytes_per_step, 5),
                 "dispatches": {"fetch": nf, "write": nw},
                 "source": "live: rocprofv3 --kernel-trace --stats, then --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate "
@@ -373,6 +416,213 @@ def cpu_baseline(a, N: int, C: int, lens_all) -> dict:
             "quota_cpus": None if quota is None else round(quota, 2), "cpu_model": model}
 
 
+def default_stripes(world: int, rank: int) -> int:
+    """Stripes per GPU without --stripes: config 2's 12,500 (100k chunks per
+    GPU) up to 4 GPUs; at 8 GPUs config 4 -- 1,000,000 chunks = 125,000
+    stripes sharded contiguously, 15,625 per GPU (bcp_dist.shard_range)."""
+    if world == 8:
+        lo, hi = shard_range(125_000, world, rank)
+        return hi - lo
+    return 12_500
+
+
+def gen_config_label(world: int, stripes: int) -> str:
+    """The BASELINE config a gen line measures: config 4 exactly when 8 ranks
+    each run config 4's 15,625-stripe shard, else config 2."""
+    return "config4" if world == 8 and stripes == 15_625 else "config2"
+
+
+def config1_leg(a) -> dict:
+    """BASELINE config 1 (configs[0]): beegfs-parity-gen --complete over 4
+    loopback storage-target ranks, ~1000 x 512 KiB chunk files per rank --
+    files -> per-task protocol -> XOR -> parity files, timed end to end in this
+    process on rank 0 (after cpu_baseline; the other ranks wait).  SURVEY
+    section 8(d): 4 targets, 3-wide stripes with P rotating over the target
+    left out, --c1-files files round-robin over the 4 rotations.  Over the same
+    store, interleaved in rotating order (one cold round, then --c1-reps warm):
+      reference_fold  bcp_gen_run (process_task, 12 lanes per rank, the MPI
+                      subset on loopback threads) with the P role folding every
+                      window with the reference's OWN xor_parity
+                      (task_processing.c:96-109 compiled unchanged, oracle/_ref,
+                      the cpu_baseline leg's library; the restatement where
+                      _ref is absent -- `kind` says which) on the reference's
+                      zero-padded wire (task_processing.c:302-303), as
+                      parity_generator folds (:203-226): kind "reference";
+      gpu_fold        the same protocol, the P role folding on the GPU (the
+                      product's default fold);
+      pipeline        bcp_pipeline_run, the batched engine.
+    Then target 2 is lost and rebuilt by each (protocol: one lane, tag 0, as
+    rebuild/main.c:63).  Sampled parity files and rebuilt chunks are checked
+    with numpy.  Rate = (chunk bytes read + parity bytes written) / warm run.
+    The protocol around the reference fold is libbcp's: the reference program
+    itself needs MPI."""
+    import concurrent.futures as cf
+    import shutil
+
+    import numpy as np
+    import bcp_store as BS
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # cpu_baseline leg only: the reference's xor_parity as the P-role fold
+    t_start = time.perf_counter()
+    NT, C, VICTIM = 4, 512 * KiB, 2
+    nfiles = a.c1_files
+    need = nfiles * 3 * C
+    want = int(need * 1.4)  # chunks + parity (1/3 of them) + slack
+    base, room, reason = e2e_store_dir([a.e2e_dir], 1, want)
+    if reason or room < want:
+        return {"skipped": reason or f"{base}: room for {room / GiB:.2f} GiB, config 1 needs {want / GiB:.2f}"}
+    root = os.path.join(base, f"bcp_bench_c1_{os.getpid()}")
+    rng = np.random.default_rng(1)
+    block = rng.integers(0, 256, size=8 << 20, dtype=np.uint8)
+    files = []
+    for i in range(nfiles):
+        p = i % NT
+        files.append((f"u0/{i % 64:02X}/chunk{i}", [t for t in range(NT) if t != p], p))
+
+    def chunk_of(i, k):
+        off = ((i * 3 + k) * 40961) % ((8 << 20) - C)
+        return block[off:off + C]
+    items = [(path, 2 ** 40, BS.with_p(sum(1 << h for h in hs), p)) for path, hs, p in files]
+    rd, wr = nfiles * 3 * C, nfiles * (3 * 8 + C)
+    lost = [i for i in range(nfiles) if VICTIM in files[i][1]]
+    rb_rd = len(lost) * 3 * C + len(lost) * 3 * 8  # 2 survivors + the parity file (header + body)
+    rb_wr = len(lost) * C
+    vr = np.random.default_rng(13)
+    sample = sorted({0, nfiles - 1} | {int(x) for x in vr.integers(0, nfiles, 10)})
+    rsample = sorted({lost[0], lost[-1]} | {lost[int(x)] for x in vr.integers(0, len(lost), 8)})
+    ref_fold, ref_name = oracle.cpu_fold_hook()
+    kind = "reference" if ref_name == "ref_xor_parity" else "port"
+    errors = []
+
+    def parity_ok(i):
+        body = np.zeros(C, dtype=np.uint8)
+        for k in range(3):
+            body ^= chunk_of(i, k)
+        want = np.full(3, C, dtype="<u8").tobytes() + body.tobytes()
+        return BS.read_file(BS.parity_path(root, files[i][2], files[i][0])) == want
+
+    def rebuilt_ok(i):
+        return BS.read_file(BS.chunk_path(root, VICTIM, files[i][0])) == \
+            chunk_of(i, files[i][1].index(VICTIM)).tobytes()
+
+    def reset_parity():
+        for k in range(NT):
+            shutil.rmtree(os.path.join(root, f"st{k}", "parity"), ignore_errors=True)
+            os.makedirs(os.path.join(root, f"st{k}", "parity"))
+
+    def drop_victim():
+        for i in lost:
+            try:
+                os.remove(BS.chunk_path(root, VICTIM, files[i][0]))
+            except FileNotFoundError:
+                pass
+
+    def with_fold(leg, fn):
+        """fn under the leg's P-role fold (reference: the batched fold service
+        handing whole windows to the hook, senders padding as the reference's)."""
+        if leg != "reference_fold":
+            return fn()
+        prev = bcp.set_fold_mode(bcp.FOLD_BATCHED)
+        bcp.set_xor_hook(ref_fold)
+        prev_pad = bcp.set_explicit_padding(True)
+        try:
+            return fn()
+        finally:
+            bcp.set_explicit_padding(prev_pad)
+            bcp.set_xor_hook(None)
+            bcp.set_fold_mode(prev)
+
+    legs = ["reference_fold", "gpu_fold", "pipeline"]
+    gen_t = {x: [] for x in legs}
+    reb_t = {x: [] for x in legs}
+    ok = {x: True for x in legs}
+    rok = {x: True for x in legs}
+    pl = None
+    try:
+        BS.make_store(root, NT)
+
+        def write_file(i):
+            path, holders, _ = files[i]
+            for k, h in enumerate(holders):
+                fn = BS.chunk_path(root, h, path)
+                os.makedirs(os.path.dirname(fn), exist_ok=True)
+                with open(fn, "wb") as f:
+                    f.write(memoryview(chunk_of(i, k)))
+        t0 = time.perf_counter()
+        with cf.ThreadPoolExecutor(8) as ex:
+            list(ex.map(write_file, range(nfiles)))
+        t_store = time.perf_counter() - t0
+        pl = bcp.Pipeline()
+        runs = 1 + max(1, a.c1_reps)
+        for r in range(runs):
+            for leg in legs[r % 3:] + legs[:r % 3]:
+                reset_parity()
+                t0 = time.perf_counter()
+                if leg == "pipeline":
+                    st = pl.run(root, NT, items)
+                else:
+                    st = with_fold(leg, lambda: bcp.gen_run(root, NT, items, nlanes=12))
+                gen_t[leg].append(time.perf_counter() - t0)
+                good = st.errors == 0 and st.tasks == (nfiles if leg == "pipeline" else 4 * nfiles)
+                if r == runs - 1:
+                    good = good and all(parity_ok(i) for i in sample)
+                ok[leg] = ok[leg] and good
+        # rebuild of target VICTIM (protocol: one lane, tag 0, as rebuild/main.c)
+        ordered = sorted(items, key=lambda x: x[0].encode())
+        prev_lanes = bcp.set_rebuild_lanes(1)
+        try:
+            for r in range(runs):
+                for leg in legs[r % 3:] + legs[:r % 3]:
+                    drop_victim()
+                    t0 = time.perf_counter()
+                    if leg == "pipeline":
+                        st = pl.rebuild(root, NT, VICTIM, ordered)
+                    else:
+                        st = with_fold(leg, lambda: bcp.rebuild_run(root, NT, VICTIM, ordered))
+                    reb_t[leg].append(time.perf_counter() - t0)
+                    good = st.errors == 0
+                    if r == runs - 1:
+                        good = good and all(rebuilt_ok(i) for i in rsample)
+                    rok[leg] = rok[leg] and good
+        finally:
+            bcp.set_rebuild_lanes(prev_lanes)
+    except Exception as e:  # reported in the block, never raised: the device line stands
+        errors.append(f"{type(e).__name__}: {e}")
+    finally:
+        if pl is not None:
+            pl.close()
+        bcp.task_shutdown()
+        shutil.rmtree(root, ignore_errors=True)
+    if errors:
+        return {"error": errors[0], "wall_s": round(time.perf_counter() - t_start, 1)}
+    import statistics
+
+    def summary(t, b, good):
+        warm = statistics.median(t[1:])
+        return {"cold_s": round(t[0], 4), "warm_s": round(warm, 4), "runs_s": [round(x, 4) for x in t],
+                "GiBps": round(b / warm / GiB, 2), "verified": good}
+    gen = {leg: summary(gen_t[leg], rd + wr, ok[leg]) for leg in legs}
+    reb = {leg: summary(reb_t[leg], rb_rd + rb_wr, rok[leg]) for leg in legs}
+    gen["reference_fold"]["kind"] = reb["reference_fold"]["kind"] = kind
+    return {
+        "workload": f"config1: beegfs-parity-gen --complete, {NT} loopback storage-target ranks, {nfiles} files x 3 "
+                    f"x {C // KiB} KiB chunks ({nfiles * 3 // NT} per rank), P rotating over the target left out",
+        "store": {"dir": base, "chunk_GiB": round(rd / GiB, 3), "write_s": round(t_store, 2)},
+        "gen": gen,
+        "rebuild": {"target": VICTIM, "files": len(lost), **reb},
+        "gpu_fold_over_reference_fold": round(gen["gpu_fold"]["GiBps"] / gen["reference_fold"]["GiBps"], 3),
+        "pipeline_over_reference_fold": round(gen["pipeline"]["GiBps"] / gen["reference_fold"]["GiBps"], 3),
+        "rebuild_gpu_fold_over_reference_fold": round(reb["gpu_fold"]["GiBps"] / reb["reference_fold"]["GiBps"], 3),
+        "bytes": {"gen_read": rd, "gen_written": wr, "rebuild_read": rb_rd, "rebuild_written": rb_wr},
+        "legs_note": "reference_fold: bcp_gen_run / bcp_rebuild_run (process_task over loopback threads, 12 lanes "
+                     "per rank for gen, 1 for rebuild) with the P role's fold = the reference's own xor_parity "
+                     f"({ref_name}) over whole windows on the reference's zero-padded wire; gpu_fold: the same "
+                     "protocol, GPU fold; pipeline: bcp_pipeline_run / _rebuild. Interleaved in rotating order, "
+                     "one cold round then warm ones (median); GiBps = (bytes read + written) / warm run",
+        "wall_s": round(time.perf_counter() - t_start, 1),
+    }
+
+
 def e2e_store_dir(dirs, world: int, want: int):
     """(directory, bytes per rank, reason or None) for the ranks' end-to-end
     stores: the first of dirs, then the temp dir, with room for every rank's
@@ -421,7 +671,7 @@ def e2e_leg(a, d, device: int, bus_id: str):
     import bcp_store as BS
     t_start = time.perf_counter()
     NT, W, VICTIM = 9, 8, 4
-    modes = [m for m in a.e2e_modes.split(",") if m in ("copy", "map", "direct")] or ["copy"]
+    modes = [m for m in a.e2e_modes.split(",") if m in ("copy", "direct")] or ["copy"]
     base, want, reason = e2e_store_dir([a.e2e_dir], d.world, int(a.e2e_gib * GiB))
     rank_root = os.path.join(base, f"bcp_bench_e2e_{os.getppid()}_{d.rank}")
     # every rank agrees to run (or not): a rank that skipped would leave the
@@ -529,6 +779,95 @@ def e2e_leg(a, d, device: int, bus_id: str):
         with cf.ThreadPoolExecutor(8) as ex:
             list(ex.map(lambda i: os.remove(BS.chunk_path(rank_root, VICTIM, files[i][0])), lost))
 
+    def partial_round(pl):
+        """A seeded 10 % of the stripes is rewritten (new chunk contents, same
+        lengths, outside the timing); their chunk events go out as one binary
+        record stream per target ({i64 ts, u64 size, u64 'm', u64 len, path},
+        bp-find-all-chunks/main.c:25-33); every target's DB replica holds the
+        full generation's state (seeded outside the timing, as the full run's
+        process_list updates leave it, gen/main.c:146-149).  Timed, every rank
+        at once: bcp_gen_round_pipeline -- records parsed into the event set
+        (gen/main.c:286-336), the worklist planned against the DB (merge, P
+        kept, NO_P when unchanged: :772-788; bcp_plan_rounds), only the subset
+        recomputed through the pipeline, the replicas updated.  One cold and
+        two warm rounds (the replicas re-seeded between them, so each plans the
+        same subset); checked: the plan is exactly the subset with each
+        stripe's P kept, and sampled parity files against numpy.  Every rank
+        makes the same barrier calls whatever fails (failures are reported)."""
+        prng = np.random.default_rng(17 + d.rank)
+        sub = sorted(int(x) for x in prng.choice(nst, size=max(1, nst // 10), replace=False))
+        ts1 = ts + 3600
+        new_off = {}
+
+        def prepare():
+            streams = {t: [] for t in range(NT)}
+            for i in sub:
+                path, holders, _ = files[i]
+                for k, h in enumerate(holders):
+                    off = ((i * W + k) * 65537 + 12345) % (8 << 20)
+                    new_off[(i, k)] = off
+                    with open(BS.chunk_path(rank_root, h, path), "wb") as f:
+                        f.write(memoryview(block[off:off + int(lens[i][k])]))
+                    streams[h].append((ts1, int(lens[i][k]), "m", path))
+            return {t: bcp.pack_records(recs) for t, recs in streams.items()}
+
+        def seed_dbs():
+            for k in range(NT):
+                dbdir = os.path.join(rank_root, f"st{k}", "db")
+                shutil.rmtree(dbdir, ignore_errors=True)
+                db = bcp.PDB(dbdir)
+                for path, t_, loc in items:
+                    db.set(path, t_, loc)
+                db.close()
+
+        def one_round():
+            t0 = time.perf_counter()
+            es = bcp.EventSet()
+            try:
+                for t, data in packed.items():
+                    es.feed(t, data)
+                st, nplanned = pl.round(rank_root, NT, es, cum_weight=[1000 * (k + 1) for k in range(NT)])
+            finally:
+                es.close()
+            return time.perf_counter() - t0, st.seconds, nplanned == len(sub) and st.errors == 0 and st.tasks == len(sub)
+
+        packed = guard("partial: rewriting the subset", prepare) if pl is not None else None
+        runs_p = []
+        for r in range(3):
+            if packed is not None:
+                guard("partial: seeding the DB replicas", seed_dbs)
+            d.barrier()
+            if packed is not None:
+                res = guard("partial round", one_round)
+                if res is not None:
+                    runs_p.append(res)
+
+        def check():
+            db = bcp.PDB(os.path.join(rank_root, "st0", "db"))
+            state = {k.decode(): (t_, loc) for k, t_, loc in db.items()}
+            db.close()
+            plan_ok = all(x[2] for x in runs_p) and all(state[files[i][0]] == (ts1, items[i][2]) for i in sub)
+
+            def sub_parity_ok(i):
+                ch = [block[new_off[(i, k)]:new_off[(i, k)] + int(lens[i][k])] for k in range(W)]
+                m = max(len(c) for c in ch)
+                body = np.zeros(m, dtype=np.uint8)
+                for c in ch:
+                    body[:len(c)] ^= c
+                return BS.read_file(BS.parity_path(rank_root, files[i][2], files[i][0])) == \
+                    np.asarray([len(c) for c in ch], dtype="<u8").tobytes() + body.tobytes()
+            ssample = sorted({sub[0], sub[-1]} | {sub[int(x)] for x in prng.integers(0, len(sub), 6)})
+            return plan_ok, plan_ok and all(sub_parity_ok(i) for i in ssample)
+        if len(runs_p) != 3:
+            return None
+        plan_ok, verified = guard("partial: checking", check, (False, False))
+        times = [x[0] for x in runs_p]
+        return {"stripes": len(sub), "bytes_read": sum(int(lens[i].sum()) for i in sub),
+                "bytes_written": sum(8 * W + int(lens[i].max()) for i in sub),
+                "own_runs_s": [round(x, 4) for x in times], "own_warm_s": round(float(np.median(times[1:])), 4),
+                "own_pipeline_warm_s": round(float(np.median([x[1] for x in runs_p][1:])), 4),
+                "plan_ok": bool(plan_ok), "verified": bool(verified)}
+
     pls = {}
     runs = {m: [] for m in modes}
     rruns = {m: [] for m in modes}
@@ -556,6 +895,7 @@ def e2e_leg(a, d, device: int, bus_id: str):
     # half of the rank's part of it, 2..8 (the library's own rule for one
     # process, which cannot see its sibling ranks)
     io_threads = max(2, min(8, usable_cpus()[0] // (2 * d.world)))
+    partial = None
     try:
         t_store = guard("writing the store", write_store, 0.0)
         d.barrier()
@@ -563,7 +903,7 @@ def e2e_leg(a, d, device: int, bus_id: str):
         for m in modes:
             pl = guard(f"pipeline ({m})", lambda: bcp.Pipeline(
                 device=device, io_threads=io_threads,
-                read_mode={"copy": bcp.READ_COPY, "map": bcp.READ_MAP, "direct": bcp.READ_DIRECT}[m]))
+                read_mode={"copy": bcp.READ_COPY, "direct": bcp.READ_DIRECT}[m]))
             if pl is not None:
                 pls[m] = pl
         # ---- gen: one cold run, then warm runs, the read paths interleaved
@@ -587,6 +927,8 @@ def e2e_leg(a, d, device: int, bus_id: str):
                 if r == 1:
                     rok[m] = rok[m] and bool(guard("checking rebuilt chunks",
                                                    lambda: all(rebuilt_ok(i) for i in rsample)))
+        # ---- config 5's changelog-driven partial update (BASELINE configs[4])
+        partial = partial_round(pls.get(modes[0]))
     finally:
         for p_ in pls.values():
             guard("closing a pipeline", p_.close)
@@ -610,6 +952,7 @@ def e2e_leg(a, d, device: int, bus_id: str):
             "rebuild_bytes_read": rd3, "rebuild_bytes_written": wr3, "rebuild_own_warm_s": reb["own_warm_s"],
             "gen_verified": all(ok.values()), "rebuild_verified": all(rok.values()),
             "store_write_s": round(t_store, 2),
+            "partial": partial or None,
             "own_warm_s_by_mode": {m: [per_mode[m][0]["own_warm_s"], per_mode[m][1]["own_warm_s"]] for m in modes},
             "errors": errors or None}
     ranks = d.gather(mine)
@@ -638,9 +981,25 @@ def e2e_leg(a, d, device: int, bus_id: str):
                  "verified": all(r["rebuild_verified"] for r in ranks) and not all_errors})
     by_mode = {m: rates(m) for m in modes}
     gen, reb = by_mode[modes[0]]
+
+    def partial_summary(rs):
+        ps = [r.get("partial") for r in rs]
+        if not all(ps):
+            return {"error": "a rank did not finish its partial round", "ranks": ps}
+        slow_warm = max(p["own_warm_s"] for p in ps)  # every rank at once behind a barrier: the slowest bounds
+        b = sum(p["bytes_read"] + p["bytes_written"] for p in ps)
+        return {"what": "config 5 changelog-driven partial update: record streams of a seeded 10 % of the "
+                        "stripes (rewritten) -> bcp_gen_round_pipeline (parse, plan vs the DB replicas with "
+                        "bcp_plan_rounds, pipeline over the subset, replicas updated), every rank at once",
+                "stripes": sum(p["stripes"] for p in ps), "bytes_read": sum(p["bytes_read"] for p in ps),
+                "bytes_written": sum(p["bytes_written"] for p in ps), "warm_s": slow_warm,
+                "GiBps": round(b / slow_warm / GiB, 2),
+                "pipeline_warm_s_rank0": ps[0]["own_pipeline_warm_s"],
+                "runs_s_rank0": ps[0]["own_runs_s"],
+                "plan_ok": all(p["plan_ok"] for p in ps), "verified": all(p["verified"] for p in ps)}
     return {
         "path": ("bcp_pipeline_run / bcp_pipeline_rebuild on every rank's own GPU: chunk files (tmpfs) -> "
-                 "pinned slabs (io threads; read_mode map: part of every batch straight from the page cache; direct: O_DIRECT reads) -> "
+                 "pinned slabs (io threads; read_mode direct: O_DIRECT reads) -> "
                  "H2D on a side queue -> xor_desc -> D2H on a side queue -> parity files / rebuilt chunks"),
         "store": {"dir": os.path.dirname(rank_root), "shapes": "config 5: 8-wide stripes, chunks log-uniform "
                                                                "64 KiB-4 MiB, 9 targets, P rotating",
@@ -653,9 +1012,9 @@ def e2e_leg(a, d, device: int, bus_id: str):
         "by_read_mode": {m: {"gen_GiBps": by_mode[m][0]["GiBps"], "gen_input_over_link": by_mode[m][0]["input_over_link"],
                              "gen_warm_s": by_mode[m][0]["warm_s"], "rebuild_GiBps": by_mode[m][1]["GiBps"],
                              "rebuild_warm_s": by_mode[m][1]["warm_s"],
-                             "mapped_bytes_last_gen": by_mode[m][0]["timing"].get("mapped_bytes"),
                              "gen_timing": by_mode[m][0]["timing"]}
                          for m in modes},
+        "partial": partial_summary(ranks),
         "link_h2d_GBps_sum": round(h2d_all / 1e9, 2),
         "errors": all_errors or None,
         "rate_note": "GiBps = (chunk bytes read + parity bytes written) of all ranks / the slowest rank's warm "
@@ -708,8 +1067,7 @@ def main():
     # config 2 (100k chunks per GPU) up to 4 GPUs; at 8 GPUs config 4: 1,000,000
     # chunks = 125,000 stripes sharded 15,625 per GPU (bcp_dist.shard_range)
     if not a.stripes:
-        lo, hi = shard_range(125_000, d.world, d.rank)
-        a.stripes = hi - lo if d.world == 8 else 12_500
+        a.stripes = default_stripes(d.world, d.rank)
     stripes_arg = a.stripes
     S, N, C = a.stripes, a.nsrc, a.chunk
     chk = eng.alloc(64)
@@ -765,7 +1123,7 @@ def main():
         bytes_per_step = S * (N + 1) * C
         kernel = "xor_stream<{N},{U},strided>"
         kernel_tag = "xor_stream<{N}, {U}, 0, "
-        cfg = "config4" if d.world == 8 and S == 15_625 else "config2"
+        cfg = gen_config_label(d.world, S)
         workload = f"{cfg}: parity gen, {S} stripes x {N} x {C // KiB} KiB device-resident per GPU"
     else:
         # config 3: parity first, then rebuild source index 3 from the other
@@ -812,18 +1170,25 @@ def main():
         step()
     q.sync()
 
+    # one HIP event per step boundary on the kernel's stream (BCP_TIMER_SLOTS
+    # = 64 slots: beyond 63 steps, boundaries every g steps), so the line
+    # carries the per-launch spread, not only the block's average
+    g = -(-a.steps // 63)
+    bounds = list(range(0, a.steps, g)) + [a.steps]
     d.barrier()
     q.sync()
     t0 = time.perf_counter()
     q.mark(0)
-    for _ in range(a.steps):
+    for i in range(a.steps):
         step()
-    q.mark(1)
+        if (i + 1) in bounds:
+            q.mark(bounds.index(i + 1))
     q.sync()
     t1 = time.perf_counter()
     d.barrier()
     wall = t1 - t0
-    kern_ms = q.elapsed_ms(0, 1) / a.steps  # avg launch duration on the kernel's stream
+    seg_ms = [q.elapsed_ms(j, j + 1) / (bounds[j + 1] - bounds[j]) for j in range(len(bounds) - 1)]
+    kern_ms = q.elapsed_ms(0, len(bounds) - 1) / a.steps  # avg launch duration on the kernel's stream
     if a.mode == "mixed":  # the descriptor kernel's form and tile size of the timed launches
         U = eng.option("last_desc_vecs")
         pipe = 5 if U >= 8 else 0  # the rolling-window form at U = 8 and 16 (launch_xor_desc)
@@ -902,7 +1267,11 @@ def main():
     kern_ms_max = d.max(kern_ms)
     # every rank's own figures (per-GPU rates of the N-GPU line): bus id, HIP-event
     # kernel time, its share of the wall clock
+    import statistics
+    seg_med = statistics.median(seg_ms)
     per_rank = d.gather({"rank": d.rank, "pci_bus_id": bus_ids[d.rank], "kernel_ms": round(kern_ms, 4),
+                         "kernel_ms_median": round(seg_med, 4), "kernel_ms_min": round(min(seg_ms), 4),
+                         "kernel_ms_max": round(max(seg_ms), 4),
                          "GiBps": round(bytes_per_step * a.steps / wall / GiB, 2),
                          "pct_hbm_peak": round(100.0 * bytes_per_step / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 2),
                          "verified": bool(verified)})
@@ -920,6 +1289,14 @@ def main():
             cpu = cpu_baseline(a, N, C, lens_all if a.mode == "mixed" else None)
         except Exception as e:  # a reported baseline: never worth the device line
             cpu = {"error": f"{type(e).__name__}: {e}"}
+    # BASELINE config 1 end to end (rank 0; the reference's xor_parity as the
+    # P-role fold beside the GPU fold and the pipeline, same store)
+    c1 = None
+    if d.rank == 0 and not a.no_configs:
+        try:
+            c1 = config1_leg(a)
+        except Exception as e:  # reported, never worth the device line
+            c1 = {"error": f"{type(e).__name__}: {e}"}
     # rocprofv3 on this box: rank 0's device, child processes (the device
     # buffers of this run are released first)
     live = None
@@ -987,6 +1364,13 @@ def main():
                 "frac_event": round(achieved / HBM_PEAK_GBS, 4),
                 "frac_rocprof": frac_rocprof,
                 "kernel_ms": round(kern_ms_max, 4),
+                # rank 0's per-launch spread (HIP event pairs at every step boundary)
+                "kernel_ms_median": round(seg_med, 4),
+                "kernel_ms_min": round(min(seg_ms), 4),
+                "kernel_ms_max": round(max(seg_ms), 4),
+                "kernel_ms_steps": [round(x, 4) for x in seg_ms],
+                "steps_per_event_pair": g,
+                "frac_event_median": round(bytes_per_step / (seg_med * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                 "traffic": (live["traffic"] if live_ok else pmc["hbm_bytes_per_launch"] if pmc else None),
                 "traffic_source": (live["source"] if live_ok else pmc["source"] if pmc else None),
                 "live_profile": live,
@@ -1000,15 +1384,23 @@ def main():
                                                          HBM_PEAK_GBS, 4) if pmc.get("rocprof_avg_ns") else None,
                                    "traffic": pmc.get("hbm_bytes_per_launch"), "box": pmc.get("box")}
                                   if pmc else None),
-                "frac_note": "frac = frac_event: algorithmic bytes / HIP-event kernel time in this run (run_box); "
-                             "frac_rocprof and traffic: the same bytes / the rocprofv3 kernel-trace average and the "
-                             "PMC passes of this workload -- live child runs on this box after the timing "
-                             "(live_profile; same_box) or, where those failed or --no-prof, the committed profile "
-                             "set (profile_files, measured on profile_box)",
+                "frac_note": "frac = frac_event: algorithmic bytes / the average HIP-event time of the timed "
+                             "launches in this run (run_box; the slowest rank's); frac_event_median and "
+                             "kernel_ms_median/min/max/steps: rank 0's event pair per step; frac_rocprof: the same "
+                             "bytes / the rocprofv3 kernel-trace average over the timed launches only (warm-up and "
+                             "verification dispatches excluded) of a live child run of this workload with this "
+                             "run's --warmup/--steps on this box, whose own per-step events over those same "
+                             "launches are live_profile.child_event_ms_*; traffic: the PMC passes of that child "
+                             "workload -- or, where those failed or --no-prof, the committed profile set "
+                             "(profile_files, measured on profile_box)",
             },
             "cpu_baseline": cpu,
             "per_rank": per_rank,
             "e2e": e2e,
+            # BASELINE configs[0] and configs[4] as BASELINE states them (rank 0's config-1 protocol
+            # leg; the config-5 changelog subset of every rank's e2e store)
+            "configs": {"config1": c1,
+                        "config5_partial": (e2e or {}).get("partial") if isinstance(e2e, dict) else None},
         }
         print(json.dumps(line), flush=True)
     q.close()

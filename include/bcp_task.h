@@ -441,6 +441,29 @@ int bcp_store_weight(int dirfd);
  * per round (:823). */
 int bcp_plan_rounds(const bcp_eventset *s, int ntargets, const int *cum_weight, const bcp_work_item *prev,
                     size_t nprev, bcp_work_item *out, size_t out_cap, size_t *nout, size_t *round_start);
+/* The same with the rounds in MPI rank order: round r is broadcast by the
+ * eater of storage target round_st[r] (a permutation of 0..ntargets-1, as
+ * bcp_map_targets derives it; NULL = target order).  bcp_plan_rounds is this
+ * with NULL. */
+int bcp_plan_rounds_ordered(const bcp_eventset *s, int ntargets, const int *cum_weight, const int *round_st,
+                            const bcp_work_item *prev, size_t nprev, bcp_work_item *out, size_t out_cap,
+                            size_t *nout, size_t *round_start);
+/* Storage-target index and round order of gen/main.c:498-499, 506-541:
+ * prev_ids[nprev] = the previous run's targetNumIDs in index order (RunData),
+ * rank_ids[ntargets] = the targetNumID of each eater rank in MPI rank order.
+ * Targets found in prev keep their index, new ones are appended in rank
+ * order; out st_ids[ntargets] (the new index order) and round_st[ntargets]
+ * (the target whose eater broadcasts round r).  -EEXIST a rank repeats an id
+ * already placed ("Duplicate targetNumID"), -ENODEV fewer targets than prev
+ * or a previous target without a rank ("Storage target missing!"). */
+int bcp_map_targets(const int32_t *prev_ids, int nprev, const int32_t *rank_ids, int ntargets, int32_t *st_ids,
+                    int *round_st);
+/* The round order of a store: <root>/rank_order (the targetNumID of every
+ * target's eater in MPI rank order, whitespace separated -- the hostfile's
+ * order, src/beegfs-parity-gen:114-117) mapped onto the st<k> directories
+ * (their ids: st<k>/targetNumID, k+1 when absent); identity when the file is
+ * absent.  Used by bcp_gen_round*. */
+int bcp_store_round_order(const char *store_root, int ntargets, int *round_st);
 /* The same without the round boundaries. */
 int bcp_plan_worklist(const bcp_eventset *s, int ntargets, const int *cum_weight, const bcp_work_item *prev,
                       size_t nprev, bcp_work_item *out, size_t out_cap, size_t *nout);
@@ -458,7 +481,11 @@ int bcp_eventset_scan(bcp_eventset *s, int st, const char *chunks_dir, uint64_t 
  * from st<k>/targetNumID (k+1 when absent), checked against and saved to
  * run_data_path.  -EEXIST duplicate id, -ENODEV fewer targets or a target
  * whose id changed ("Storage target missing!"), -EPROTO version stamp (the
- * file's own format stamp, 1; not the struct ABI: BCP_ABI_VERSION). */
+ * file's own format stamp, 1; not the struct ABI: BCP_ABI_VERSION).  With a
+ * <root>/rank_order (bcp_store_round_order) also its mapping as the reference
+ * derives it from the previous run's list (bcp_map_targets; a first run: the
+ * directories' order): -EPROTO when targets added since are not numbered in
+ * the order the reference appends them (rank order). */
 #define BCP_TASK_ABI_VERSION 3 /* = BCP_ABI_VERSION (include/bcp.h) */
 int bcp_check_targets(const char *store_root, int ntargets, const char *run_data_path, FILE *log);
 

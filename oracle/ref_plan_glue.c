@@ -18,10 +18,11 @@
  *   gen/assign_lanes.c:7-46          assign_lanes
  *
  * and exports them as ref_* for tests/golden/make_ref_plan_golden.py and the
- * CPU tests.  Only two pieces below are glue of mine, each a few lines that
- * sequence reference functions exactly as the reference's caller does (the
- * caller itself needs MPI / LevelDB and is not compiled): ref_sort_order
- * (gen/main.c:710-711) and ref_plan_item (gen/main.c:772-788 around pdb_get).
+ * CPU tests.  The pieces below that are glue of mine are a few lines each
+ * that sequence reference functions exactly as the reference's caller does
+ * (the caller itself needs MPI / LevelDB and is not compiled): ref_sort_order
+ * (gen/main.c:710-711), ref_round_order[_ranked] (:310, :710-711, :758) and
+ * ref_plan_item (gen/main.c:772-788 around pdb_get).
  * Output: oracle/_ref/libref_plan.so (git-ignored).
  */
 
@@ -158,4 +159,32 @@ uint64_t ref_plan_item(const char *s, int64_t timestamp, uint64_t modified, uint
 int ref_store_weight(int dirfd)
 {
     return get_store_weight(dirfd);
+}
+
+/* The same rounds with the eaters in MPI rank order (gen/main.c:758: round
+ * r is broadcast by communicator rank r+1 = world rank 2r+1, the eater of
+ * storage target round_st[r] = rank2st[2r+1] as ref_map_targets prints it,
+ * gen/main.c:506-541); round_st NULL = target order (ref_round_order). */
+void ref_round_order_ranked(const char *const *paths, const uint64_t *sizes, size_t n, unsigned ntargets,
+                            const int *round_st, uint64_t *idx, size_t *round_start)
+{
+    SizeIndex *a = malloc((n ? n : 1) * sizeof(SizeIndex));
+    size_t j = 0;
+    for (unsigned r = 0; r < ntargets; r++) {
+        const unsigned k = round_st ? (unsigned)round_st[r] : r;
+        round_start[r] = j;
+        size_t m = 0;
+        for (size_t i = 0; i < n; i++)
+            if (simple_hash(paths[i], (int)strlen(paths[i])) % ntargets == k) {
+                a[m].size = sizes[i];
+                a[m].idx = i;
+                m++;
+            }
+        shuffle(a, m);
+        qsort(a, m, sizeof(SizeIndex), cmp_entries);
+        for (size_t t = 0; t < m; t++)
+            idx[j++] = a[t].idx;
+    }
+    round_start[ntargets] = j;
+    free(a);
 }

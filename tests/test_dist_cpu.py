@@ -185,3 +185,17 @@ def test_e2e_store_dir_fits_every_rank(tmp_path, monkeypatch):
     free["/shm"] = free["/tmpdir"] = 16 << 20
     assert bench.e2e_store_dir(["/shm"], 8, 2 * GiB)[2] is not None
     assert bench.e2e_store_dir(["/absent"], 1, GiB)[0] == "/tmpdir"
+
+
+def test_bench_default_shard_and_label_per_world():
+    """The driver's N = 8 run takes the config-4 branch: 125,000 stripes over 8
+    ranks = 15,625 each, labelled config4; every other N runs config 2's
+    12,500 per GPU; an explicit stripe count is never labelled config 4."""
+    import bench
+    for world in (1, 2, 4):
+        assert all(bench.default_stripes(world, r) == 12_500 for r in range(world))
+        assert bench.gen_config_label(world, 12_500) == "config2"
+    shards = [bench.default_stripes(8, r) for r in range(8)]
+    assert shards == [15_625] * 8 and sum(shards) * 8 == 1_000_000  # config 4: 1M chunks
+    assert bench.gen_config_label(8, 15_625) == "config4"
+    assert bench.gen_config_label(8, 64) == "config2" and bench.gen_config_label(4, 15_625) == "config2"

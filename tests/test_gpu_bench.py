@@ -38,11 +38,17 @@ def _run(cmd, timeout):
 @pytest.mark.timeout(400)
 @pytest.mark.parametrize("mode", ["gen", "rebuild", "mixed"])
 def test_bench_one_rank_small(bcp, mode):
-    line = _run([sys.executable, "bench.py", "--stripes", "64", "--steps", "2", "--warmup", "1", "--no-cpu",
-                 "--no-e2e", "--no-prof", "--mode", mode], 300)
+    line = _run([sys.executable, "bench.py", "--stripes", "64", "--steps", "5", "--warmup", "1", "--no-cpu",
+                 "--no-e2e", "--no-prof", "--no-configs", "--mode", mode], 300)
     assert line["config"]["verified_on_device"] is True
     assert line["n_gpus"] == 1 and line["config"]["ranks"] == 1 and line["config"]["shared_gpu"] is False
-    assert line["roofline"]["frac"] == line["roofline"]["frac_event"] > 0
+    rf = line["roofline"]
+    assert rf["frac"] == rf["frac_event"] > 0
+    # the per-launch spread: one event pair per step, the average in between
+    assert len(rf["kernel_ms_steps"]) == 5 and rf["steps_per_event_pair"] == 1
+    assert rf["kernel_ms_min"] <= rf["kernel_ms_median"] <= rf["kernel_ms_max"]
+    assert rf["kernel_ms_min"] <= rf["kernel_ms"] * 1.0001 and rf["kernel_ms"] <= rf["kernel_ms_max"] * 1.0001
+    assert line["configs"]["config1"] is None
 
 
 @pytest.mark.timeout(500)
@@ -51,7 +57,7 @@ def test_bench_torchrun_two_ranks_labels(bcp):
     line = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                  "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
                  "bench.py", "--gpus", "2", "--stripes", "64", "--steps", "2", "--warmup", "1", "--no-cpu",
-                 "--no-e2e", "--no-prof", "--allow-shared"], 420)
+                 "--no-e2e", "--no-prof", "--no-configs", "--allow-shared"], 420)
     assert line["config"]["verified_on_device"] is True
     assert line["config"]["ranks"] == 2
     distinct = min(ndev, 2)  # bench maps local rank r to device r % ndev
@@ -60,18 +66,22 @@ def test_bench_torchrun_two_ranks_labels(bcp):
     assert line["roofline"]["run_box"]["pci_bus_id"] in line["config"]["pci_bus_ids"]
 
 
-@pytest.mark.timeout(500)
-@pytest.mark.parametrize("n", [2, 4])
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("n", [2, 4, 8])
 def test_bench_gpus_n_launches_its_own_ranks(bcp, n):
     """The driver's form, `python3 bench.py --gpus N` with no launcher: bench.py
     starts N ranks itself.  With fewer GPUs than N it refuses (non-zero exit,
-    no line) unless --allow-shared, which reports the ranks and the distinct GPUs."""
+    no line) unless --allow-shared, which reports the ranks and the distinct GPUs.
+    N = 8 rehearses every branch of the driver's 8-GPU run on one device (an
+    explicit --stripes: the config-4 default shard is 68.6 GiB per rank; the
+    default itself is pinned on CPU, tests/test_dist_cpu.py)."""
     ndev = bcp.device_count()
     env = dict(os.environ, MASTER_ADDR="127.0.0.1")
     env.pop("WORLD_SIZE", None)
     args = [sys.executable, "bench.py", "--gpus", str(n), "--stripes", "64", "--steps", "2", "--warmup", "1",
-            "--cpu-seconds", "1", "--cpu-stripes", "16", "--e2e-gib", "0.25", "--e2e-reps", "1"]
-    args += ["--prof-steps", "2"] if n == 2 else ["--no-prof"]  # the live profile from rank 0 of an N-rank job
+            "--cpu-seconds", "1", "--cpu-stripes", "16", "--e2e-gib", "0.1" if n == 8 else "0.25", "--e2e-reps", "1",
+            "--c1-files", "48", "--c1-reps", "1"]
+    args += [] if n == 2 else ["--no-prof"]  # the live profile from rank 0 of an N-rank job
     if ndev < n:
         r = subprocess.run(args, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
         assert r.returncode == 4, (r.returncode, r.stdout[-2000:], r.stderr[-2000:])
@@ -98,13 +108,21 @@ def test_bench_gpus_n_launches_its_own_ranks(bcp, n):
     assert e2e["gen"]["verified"] is True and e2e["rebuild"]["verified"] is True
     assert e2e["gen"]["GiBps"] > 0 and e2e["rebuild"]["GiBps"] > 0
     assert e2e["gen"]["bytes_read"] == sum(r["bytes_read"] for r in e2e["per_rank"])
-    assert set(e2e["by_read_mode"]) == {"copy", "map", "direct"} and e2e["read_mode"] == "copy"
-    assert e2e["by_read_mode"]["map"]["mapped_bytes_last_gen"] > 0
+    assert set(e2e["by_read_mode"]) == {"copy", "direct"} and e2e["read_mode"] == "copy"
     dt = e2e["by_read_mode"]["direct"]["gen_timing"]
     assert dt["read_mode"] == 3 and (dt["direct_bytes"] > 0 or dt["direct_fallbacks"] > 0), dt
+    # the config-5 changelog subset on every rank, the config-1 protocol leg on rank 0
+    part = line["configs"]["config5_partial"]
+    assert part == e2e["partial"] and part["verified"] is True and part["plan_ok"] is True, part
+    assert part["stripes"] == sum(r["partial"]["stripes"] for r in e2e["per_rank"]) > 0
+    c1 = line["configs"]["config1"]
+    assert "gen" in c1 and all(c1["gen"][k]["verified"] for k in ("reference_fold", "gpu_fold", "pipeline")), c1
+    assert c1["gen"]["reference_fold"]["kind"] == "reference"
     if n == 2:
         live = line["roofline"]["live_profile"]
         assert live and "error" not in live and line["roofline"]["same_box"] is True, live
+    if n == 8:
+        assert "config2" in line["config"]["workload"]  # an explicit --stripes is never labelled config 4
     assert line["config"]["bytes_per_step_per_gpu"] * n * line["steps"] / 2**30 / (line["ms_per_step"] *
                                                                                    line["steps"] * 1e-3) == \
         pytest.approx(line["value"], rel=5e-3)  # value = the whole job's bytes / the slowest rank's time
@@ -115,11 +133,34 @@ def test_bench_mixed_line_carries_cpu_baseline_and_e2e(bcp):
     """Mixed mode (config-5 shapes): the reference's fold timed over the same
     zero-padded stripe shapes, and the end-to-end leg, in the one-rank line."""
     line = _run([sys.executable, "bench.py", "--mode", "mixed", "--stripes", "64", "--steps", "2", "--warmup", "1",
-                 "--cpu-seconds", "1", "--e2e-gib", "0.25", "--e2e-reps", "1", "--no-prof"], 300)
+                 "--cpu-seconds", "1", "--e2e-gib", "0.25", "--e2e-reps", "1", "--no-prof", "--no-configs"], 300)
     cpu = line["cpu_baseline"]
     assert cpu["kind"] == "reference" and cpu["value"] > 0 and "stripe_shapes" in cpu["legs"][0]
     assert line["e2e"]["gen"]["verified"] is True and line["e2e"]["rebuild"]["verified"] is True
     assert line["per_rank"][0]["verified"] is True
+
+
+@pytest.mark.timeout(400)
+def test_bench_configs_block_one_rank(bcp):
+    """BASELINE configs 1 and 5 in the driver's line: config 1 (4 loopback
+    ranks, 3-wide stripes, P rotating) through the per-task protocol with the
+    reference's own xor_parity as the P-role fold, with the GPU fold and
+    through the pipeline, gen and rebuild, all verified; config 5's changelog
+    subset planned against the DB and recomputed, verified."""
+    line = _run([sys.executable, "bench.py", "--stripes", "64", "--steps", "2", "--warmup", "1", "--no-prof",
+                 "--cpu-seconds", "1", "--e2e-gib", "0.25", "--e2e-reps", "1", "--c1-files", "96",
+                 "--c1-reps", "1"], 360)
+    c1 = line["configs"]["config1"]
+    assert "error" not in c1 and "skipped" not in c1, c1
+    for what in ("gen", "rebuild"):
+        for leg in ("reference_fold", "gpu_fold", "pipeline"):
+            x = c1[what][leg]
+            assert x["verified"] is True and x["GiBps"] > 0 and len(x["runs_s"]) == 2, (what, leg, x)
+    assert c1["gen"]["reference_fold"]["kind"] == "reference" and c1["rebuild"]["files"] == 72
+    assert c1["bytes"]["gen_read"] == 96 * 3 * 512 * 1024
+    part = line["configs"]["config5_partial"]
+    assert part["verified"] is True and part["plan_ok"] is True and part["GiBps"] > 0, part
+    assert part["stripes"] == max(1, line["e2e"]["per_rank"][0]["stripes"] // 10)
 
 
 @pytest.mark.timeout(400)
@@ -130,7 +171,7 @@ def test_bench_line_survives_an_e2e_failure_on_one_rank(bcp):
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", BCP_BENCH_E2E_FAIL_RANK="1")
     env.pop("WORLD_SIZE", None)
     r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--allow-shared", "--stripes", "64", "--steps", "2",
-                        "--warmup", "1", "--no-cpu", "--e2e-gib", "0.25", "--e2e-reps", "1", "--no-prof"],
+                        "--warmup", "1", "--no-cpu", "--e2e-gib", "0.25", "--e2e-reps", "1", "--no-prof", "--no-configs"],
                        cwd=ROOT, env=env, capture_output=True, text=True, timeout=360)
     assert r.returncode == 0, (r.returncode, r.stdout[-2000:], r.stderr[-4000:])
     line = _last_json(r.stdout)
@@ -138,6 +179,7 @@ def test_bench_line_survives_an_e2e_failure_on_one_rank(bcp):
     e2e = line["e2e"]
     assert list(e2e["errors"]) in (["1"], [1]) and "injected" in str(e2e["errors"])
     assert e2e["gen"]["verified"] is False and e2e["per_rank"][0]["errors"] is None
+    assert "error" in e2e["partial"]  # the failed rank's partial round is reported, rank 0's line stands
 
 
 @pytest.mark.timeout(500)
@@ -146,12 +188,17 @@ def test_bench_live_profile_on_its_own_box(bcp, mode):
     """The roofline's rocprof figures come from this box: the same workload
     under rocprofv3 in child processes (kernel trace, then the two PMC passes),
     traffic within 1 % of the algorithmic bytes, same_box set."""
-    line = _run([sys.executable, "bench.py", "--mode", mode, "--stripes", "256", "--steps", "3", "--warmup", "1",
-                 "--no-cpu", "--no-e2e", "--prof-steps", "3"], 450)
+    line = _run([sys.executable, "bench.py", "--mode", mode, "--stripes", "256", "--steps", "4", "--warmup", "2",
+                 "--no-cpu", "--no-e2e", "--no-configs"], 450)
     rf = line["roofline"]
     live = rf["live_profile"]
     assert live and "error" not in live, live
-    assert live["rocprof_calls"] >= 3 and live["rocprof_avg_ns"] > 0
+    # the timed launches only (warm-up and verification dispatches excluded),
+    # and the child's own events over those same launches
+    assert live["rocprof_timed_launches"] == 4 and len(live["rocprof_timed_ms_steps"]) == 4
+    assert live["rocprof_all_dispatches"]["calls"] == 2 + 4 + 1
+    assert len(live["child_event_ms_steps"]) == 4 and 0.8 < live["child_event_over_rocprof"] < 1.25, live
+    assert live["rocprof_min_ns"] <= live["rocprof_median_ns"] <= live["rocprof_max_ns"]
     assert 0.99 < live["traffic_over_algorithmic"] < 1.02, live
     assert rf["same_box"] is True and rf["traffic"] == live["traffic"]
     assert rf["frac_rocprof"] > 0 and rf["profile_box"] == rf["run_box"]
