@@ -298,8 +298,8 @@ def live_profile(a, stripes_arg: int, kernel_tag: str, bytes_per_step: int) -> d
 
     def run(tag, args, steps, warmup):
         d_ = os.path.join(out, tag)
-        cmd = [exe] + args + ["-d", d_, "-o", "run", "--output-format", "csv", "--"] + child + \
-            ["--steps", str(steps), "--warmup", str(warmup)]
+        cmd = ([exe] + args + ["-d", d_, "-o", "run", "--output-format", "csv", "--"] if args is not None else []) + \
+            child + ["--steps", str(steps), "--warmup", str(warmup)]
         p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
                              start_new_session=True)
         try:
@@ -344,6 +344,10 @@ def live_profile(a, stripes_arg: int, kernel_tag: str, bytes_per_step: int) -> d
             raise RuntimeError(f"{len(durs)} dispatches of {kernel_tag}, expected {a.warmup} + {steps} + 1")
         cl = child_line.get("trace", {}).get("roofline", {})
         ev = cl.get("kernel_ms_steps")
+        # the same child without the profiler: whether a process-to-process
+        # difference or the profiler sets the gap to the parent's events
+        run("plain", None, steps, a.warmup)
+        plain = child_line.get("plain", {}).get("roofline", {}).get("kernel_ms_median")
         fetch, nf = counter(one(run("pmc_fetch", ["--pmc", "FETCH_SIZE"], 3, 1), "*counter_collection.csv"), "FETCH_SIZE")
         write, nw = counter(one(run("pmc_write", ["--pmc", "WRITE_SIZE"], 3, 1), "*counter_collection.csv"), "WRITE_SIZE")
         traffic = fetch * 1024 * 2 + write * 1024
@@ -356,6 +360,7 @@ def live_profile(a, stripes_arg: int, kernel_tag: str, bytes_per_step: int) -> d
                 "child_event_over_rocprof": (round(statistics.median(ev) * 1e6 / statistics.median(timed), 4)
                                              if ev else None),
                 "child_event_ms_steps": ev,
+                "plain_child_event_ms_median": plain,
                 "rocprof_timed_ms_steps": [round(x / 1e6, 4) for x in timed],
                 "traffic": round(traffic),
                 "traffic_over_algorithmic": round(traffic / bytes_per_step, 5),
@@ -533,6 +538,7 @@ def config1_leg(a) -> dict:
             bcp.set_fold_mode(prev)
 
     legs = ["reference_fold", "gpu_fold", "pipeline"]
+    pl_timing = {}
     gen_t = {x: [] for x in legs}
     reb_t = {x: [] for x in legs}
     ok = {x: True for x in legs}
@@ -560,6 +566,7 @@ def config1_leg(a) -> dict:
                 t0 = time.perf_counter()
                 if leg == "pipeline":
                     st = pl.run(root, NT, items)
+                    pl_timing["gen"] = pl.last_timing()
                 else:
                     st = with_fold(leg, lambda: bcp.gen_run(root, NT, items, nlanes=12))
                 gen_t[leg].append(time.perf_counter() - t0)
@@ -577,6 +584,7 @@ def config1_leg(a) -> dict:
                     t0 = time.perf_counter()
                     if leg == "pipeline":
                         st = pl.rebuild(root, NT, VICTIM, ordered)
+                        pl_timing["rebuild"] = pl.last_timing()
                     else:
                         st = with_fold(leg, lambda: bcp.rebuild_run(root, NT, VICTIM, ordered))
                     reb_t[leg].append(time.perf_counter() - t0)
@@ -604,6 +612,8 @@ def config1_leg(a) -> dict:
     gen = {leg: summary(gen_t[leg], rd + wr, ok[leg]) for leg in legs}
     reb = {leg: summary(reb_t[leg], rb_rd + rb_wr, rok[leg]) for leg in legs}
     gen["reference_fold"]["kind"] = reb["reference_fold"]["kind"] = kind
+    gen["pipeline"]["last_run_timing"] = pl_timing.get("gen")
+    reb["pipeline"]["last_run_timing"] = pl_timing.get("rebuild")
     return {
         "workload": f"config1: beegfs-parity-gen --complete, {NT} loopback storage-target ranks, {nfiles} files x 3 "
                     f"x {C // KiB} KiB chunks ({nfiles * 3 // NT} per rank), P rotating over the target left out",
