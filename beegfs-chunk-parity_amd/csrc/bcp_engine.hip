@@ -13,6 +13,7 @@
 //    both kernels take tiles from a per-queue device work queue (monotone
 //    counter, base advanced on the host per launch).
 #include <errno.h>
+#include <pthread.h>
 #include <stdio.h>
 #include <sys/mman.h>
 #include <stdlib.h>
@@ -556,6 +557,46 @@ struct RegAlloc {
 pthread_mutex_t g_reg_lock = PTHREAD_MUTEX_INITIALIZER;
 RegAlloc *g_reg = nullptr;
 
+// First touch of a fresh allocation, split over up to 8 threads for big ones:
+// zeroing the pages is the cost of a pinned slab (a pipeline's 8 x 256 MiB
+// took 0.25-0.38 s of a config-1 CLI run on one thread,
+// profiles/r05/pipeline/c1_cli_r5e.jsonl); faults of one process scale
+// across threads.
+struct TouchArg {
+  char *p;
+  size_t n;
+};
+void *touch_range(void *a) {
+  TouchArg *t = (TouchArg *)a;
+  memset(t->p, 0, t->n);
+  return nullptr;
+}
+void first_touch(void *p, size_t n) {
+  const size_t piece = (size_t)32 << 20;
+  int nt = (int)std::min<size_t>(8, n / piece);
+  if (nt < 2) {
+    memset(p, 0, n);
+    return;
+  }
+  pthread_t th[8];
+  TouchArg args[8];
+  const size_t huge = (size_t)2 << 20;
+  const size_t per = (n / nt + huge - 1) / huge * huge;
+  int started = 0;
+  for (int i = 0; i < nt; i++) {
+    const size_t off = (size_t)i * per;
+    args[i] = {(char *)p + off, off >= n ? 0 : std::min(per, n - off)};
+    if (i == 0 || pthread_create(&th[i], nullptr, touch_range, &args[i]) != 0) {
+      touch_range(&args[i]);  // this thread's share, or one a thread could not take
+      th[i] = pthread_t();
+      continue;
+    }
+    started |= 1 << i;
+  }
+  for (int i = 1; i < nt; i++)
+    if (started >> i & 1) pthread_join(th[i], nullptr);
+}
+
 // posix_memalign (2 MiB, MADV_HUGEPAGE) + first touch + hipHostRegister
 // (mapped): the CPU side stays normal write-back, huge-page-backed memory;
 // the device reads and writes it at the same address.
@@ -569,7 +610,7 @@ int alloc_registered(size_t bytes, void **out) {
     return -ENOMEM;
   }
   (void)madvise(p, n, MADV_HUGEPAGE);
-  memset(p, 0, n);  // fault the pages in here, not under the first copy
+  first_touch(p, n);  // fault the pages in here, not under the first copy
   void *dev = nullptr;
   if (hipHostRegister(p, n, hipHostRegisterMapped) != hipSuccess ||
       hipHostGetDevicePointer(&dev, p, 0) != hipSuccess || dev != p) {

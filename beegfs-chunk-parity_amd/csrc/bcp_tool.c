@@ -89,13 +89,41 @@ static int fold_mode_arg(const char *s)
 }
 
 /* The batched pipeline on every visible GPU (each brings its own PCIe link;
- * io threads scale with them). */
-static int pipeline_on_all_gpus(bcp_pipeline **pl)
+ * io threads scale with them).  job_bytes (0: unknown) sizes the slabs: the
+ * pipeline cuts a run into batches of at most job / (4 x slots x GPUs)
+ * anyway, so bigger slabs would only be pinned and zeroed for nothing -- the
+ * setup of a one-shot run (a config-1 --complete: 2 GiB of slabs, 0.25-0.38 s
+ * of a 0.6 s process, profiles/r05/pipeline/c1_cli_r5e.jsonl).  Slabs still
+ * grow to a stripe that does not fit. */
+static int pipeline_on_all_gpus(bcp_pipeline **pl, uint64_t job_bytes)
 {
     int ndev = 0;
     bcp_device_count(&ndev);
-    const bcp_pipeline_opts o = {0, (size_t)256 << 20, 0, 4, ndev > 0 ? ndev : 1, g_read_mode};
+    const uint64_t devs = ndev > 0 ? (uint64_t)ndev : 1, full = (uint64_t)256 << 20, least = (uint64_t)16 << 20;
+    uint64_t slab = full;
+    if (job_bytes) {
+        slab = job_bytes / (4 * 4 * devs) + 1;
+        slab = (slab + least - 1) / least * least;
+        slab = slab < least ? least : slab > full ? full : slab;
+    }
+    const bcp_pipeline_opts o = {0, (size_t)slab, 0, 4, (int)devs, g_read_mode};
     return bcp_pipeline_create(&o, pl);
+}
+
+/* Chunk bytes the event set's records announce (the sizes the scan or the
+ * changelog reported; a deleted chunk counts as what it was). */
+static uint64_t event_bytes(const bcp_eventset *es)
+{
+    uint64_t total = 0;
+    const size_t n = bcp_eventset_count(es);
+    for (size_t i = 0; i < n; i++) {
+        const char *p;
+        int64_t ts;
+        uint64_t m, d, sz = 0;
+        if (bcp_eventset_get(es, i, &p, &ts, &m, &d, &sz) == 0)
+            total += sz;
+    }
+    return total;
 }
 
 static int fail(const char *what, int rc)
@@ -233,7 +261,7 @@ static int cmd_gen(int argc, char **argv)
     size_t planned = 0;
     if (use_pipeline) {
         bcp_pipeline *pl = NULL;
-        rc = pipeline_on_all_gpus(&pl);
+        rc = pipeline_on_all_gpus(&pl, event_bytes(es));
         t_setup = now_s();
         if (!rc)
             rc = bcp_gen_round_pipeline(pl, root, ntargets, es, NULL, stderr, &st, &planned);
@@ -329,7 +357,7 @@ static int cmd_rebuild(int argc, char **argv)
             rc = bcp_rebuild_run_procs(root, ntargets, target, items, n, corrupt, stderr, &st);
         } else if (!rc) {
             bcp_pipeline *pl = NULL;
-            rc = pipeline_on_all_gpus(&pl);
+            rc = pipeline_on_all_gpus(&pl, 0);
             if (!rc)
                 rc = bcp_pipeline_rebuild(pl, root, ntargets, target, items, n, corrupt, stderr, &st);
             if (pl)

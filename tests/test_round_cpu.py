@@ -36,12 +36,20 @@ def test_gen_run_db_updates_every_replica(bcp, cpu_hook, tmp_path):
         assert replica_items(bcp, root, k) == want
 
 
+@pytest.mark.parametrize("ranked", [False, True])
 @pytest.mark.parametrize("seed", range(2))
-def test_round_plan_run_update_and_rebuild(bcp, oracle, cpu_hook, tmp_path, seed):
+def test_round_plan_run_update_and_rebuild(bcp, oracle, cpu_hook, tmp_path, seed, ranked):
+    """ranked: the store names a permuted MPI rank order (<root>/rank_order),
+    so the round plans its coordinators' rounds in that order -- the same
+    items, files and DB state, another schedule."""
     rng = np.random.default_rng(seed)
     root = str(tmp_path)
     ntargets = int(rng.integers(4, 10))
     S.make_store(root, ntargets)
+    if ranked:  # no targetNumID files: target k's id is k + 1
+        order = [int(x) for x in rng.permutation(ntargets)]
+        (tmp_path / "rank_order").write_text(" ".join(str(k + 1) for k in order))
+        assert bcp.store_round_order(root, ntargets) == order
     cw = list(np.cumsum([int(x) for x in rng.integers(500, 7000, size=ntargets)]))
     files, contents, ts0 = {}, {}, 1_700_000_000
     streams = {k: [] for k in range(ntargets)}
