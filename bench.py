@@ -1328,8 +1328,9 @@ def main():
         frac_rocprof = None
         if live_ok:
             frac_rocprof = round(bytes_per_step / (live["rocprof_avg_ns"] * 1e-9) / 1e9 / HBM_PEAK_GBS, 4)
-        elif pmc and pmc.get("rocprof_avg_ns"):
-            frac_rocprof = round(bytes_per_step / (pmc["rocprof_avg_ns"] * 1e-9) / 1e9 / HBM_PEAK_GBS, 4)
+        elif pmc and (pmc.get("rocprof_timed_avg_ns") or pmc.get("rocprof_avg_ns")):
+            frac_rocprof = round(bytes_per_step / ((pmc.get("rocprof_timed_avg_ns") or pmc["rocprof_avg_ns"]) * 1e-9)
+                                 / 1e9 / HBM_PEAK_GBS, 4)
         line = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -1390,8 +1391,10 @@ def main():
                 "profile_box": run_box if live_ok else (pmc.get("box") if pmc else None),
                 "same_box": live_ok or bool(pmc and pmc.get("box") and run_box["boot_id"]
                                             and pmc["box"].get("boot_id") == run_box["boot_id"]),
-                "committed_set": ({"frac_rocprof": round(bytes_per_step / (pmc["rocprof_avg_ns"] * 1e-9) / 1e9 /
+                "committed_set": ({"frac_rocprof": round(bytes_per_step / ((pmc.get("rocprof_timed_avg_ns") or
+                                                                            pmc["rocprof_avg_ns"]) * 1e-9) / 1e9 /
                                                          HBM_PEAK_GBS, 4) if pmc.get("rocprof_avg_ns") else None,
+                                   "timed_launches_only": bool(pmc.get("rocprof_timed_avg_ns")),
                                    "traffic": pmc.get("hbm_bytes_per_launch"), "box": pmc.get("box")}
                                   if pmc else None),
                 "frac_note": "frac = frac_event: algorithmic bytes / the average HIP-event time of the timed "

@@ -54,6 +54,8 @@ def main():
             shutil.copy(bench, os.path.join(a.dst, f"bench_{m}.json"))
         stats = os.path.join(a.dst, f"{m}_kernel_stats.csv")
         shutil.copy(one(os.path.join(d, "trace", "**", "*kernel_stats.csv")), stats)
+        trace = os.path.join(a.dst, f"{m}_kernel_trace.csv")
+        shutil.copy(one(os.path.join(d, "trace", "**", "*kernel_trace.csv")), trace)
         fetch = os.path.join(a.dst, f"{m}_pmc_fetch.csv")
         write = os.path.join(a.dst, f"{m}_pmc_write.csv")
         shutil.copy(one(os.path.join(d, "pmc_fetch", "**", "*counter_collection.csv")), fetch)
@@ -65,7 +67,8 @@ def main():
         rel = lambda p: os.path.relpath(p, ROOT)  # noqa: E731
         subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pmc_summary.py"), "--fetch", fetch, "--write", write,
                         "--kernel", tag, "--workload-key", wkey, "--algorithmic", str(cfg["bytes_per_step_per_gpu"]),
-                        "--stats", rel(stats), "--commit", a.commit, "--files", rel(fetch), rel(write),
+                        "--stats", rel(stats), "--trace", rel(trace), "--warmup", str(line["warmup"]),
+                        "--steps", str(line["steps"]), "--commit", a.commit, "--files", rel(fetch), rel(write),
                         rel(os.path.join(a.dst, f"bench_{m}.json")),  # the committed copy of the bench line
                         "--out", os.path.join(a.dst, f"pmc_{m}.json")], check=True)
         # the box the set was measured on (bench.py's run_box), for bench.py's profile_box

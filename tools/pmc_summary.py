@@ -36,6 +36,9 @@ def main():
     ap.add_argument("--algorithmic", type=float, required=True, help="algorithmic bytes per launch")
     ap.add_argument("--out", required=True)
     ap.add_argument("--stats", help="rocprofv3 --kernel-trace --stats kernel_stats.csv of the same command")
+    ap.add_argument("--trace", help="rocprofv3 kernel_trace.csv of the same command: the timed launches alone")
+    ap.add_argument("--warmup", type=int, default=3, help="warm-up launches of the traced bench command")
+    ap.add_argument("--steps", type=int, default=20, help="timed launches of the traced bench command")
     ap.add_argument("--commit", help="code commit the profiled tree was built from")
     ap.add_argument("--files", nargs="*", default=[], help="committed copies of the raw inputs (provenance)")
     a = ap.parse_args()
@@ -51,11 +54,22 @@ def main():
                 if a.kernel in row["Name"]:
                     avg_ns = float(row["AverageNs"])
                     break
+    timed = None
+    if a.trace:  # dispatches in order; drop the warm-up ones and the verification one after the timed steps
+        with open(a.trace) as f:
+            rows = sorted((r for r in csv.DictReader(f) if a.kernel in r["Kernel_Name"]),
+                          key=lambda r: int(r["Dispatch_Id"]))
+        durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows]
+        if len(durs) == a.warmup + a.steps + 1:
+            timed = durs[a.warmup:a.warmup + a.steps]
     doc = {
         "workload_key": a.workload_key,
         "code_commit": a.commit,
         "rocprof_avg_ns": avg_ns,
-        "files": {"stats": a.stats, "raw": a.files},
+        "rocprof_timed_avg_ns": round(statistics.fmean(timed), 1) if timed else None,
+        "rocprof_timed_median_ns": statistics.median(timed) if timed else None,
+        "rocprof_timed_launches": len(timed) if timed else None,
+        "files": {"stats": a.stats, "trace": a.trace, "raw": a.files},
         "kernel": next(iter(fe.values()))[1],
         "dispatches": {"fetch_pass": len(fe), "write_pass": len(wr)},
         "fetch_bytes_per_launch": round(fetch_b),
