@@ -1,0 +1,28 @@
+#!/bin/bash
+# ThreadSanitizer run of the batched pipeline's host code ON A GPU BOX
+# (tests/test_gpu_sanitize.py): the C sources are built with
+# -fsanitize=thread (gcc, host code only) and linked with the uninstrumented
+# HIP objects; tests/native/pipeline_driver.c runs parity gen through both
+# read paths and two device lanes, checks every parity file against its own
+# CPU XOR, then rebuilds a lost target.  Fails on any TSan report.
+set -euo pipefail
+R=$(cd "$(dirname "$0")/.." && pwd)
+P=$R/beegfs-chunk-parity_amd
+B=${TSAN_BUILD:-$P/build-tsan}
+mkdir -p $B
+CF="-std=gnu11 -O1 -g -fPIC -Wall -pthread -fsanitize=thread -fno-omit-frame-pointer -I$R/include -I$P/csrc"
+objs=""
+for c in $P/csrc/*.c; do
+  n=$(basename $c .c)
+  [ "$n" = bcp_tool ] && continue
+  gcc $CF -c $c -o $B/$n.o
+  objs="$objs $B/$n.o"
+done
+gcc $CF -c $R/tests/native/pipeline_driver.c -o $B/pipeline_driver.o
+gcc -fsanitize=thread -o $B/pipeline_driver $B/pipeline_driver.o $objs $P/build/bcp_kernels.o $P/build/bcp_engine.o \
+  -L/opt/rocm/lib -lamdhip64 -Wl,-rpath,/opt/rocm/lib -lstdc++ -lm -pthread
+if [ -n "${BUILD_ONLY:-}" ]; then exit 0; fi
+S=${TMPDIR:-/tmp}/bcp_tsan_pipeline_$$
+rm -rf $S
+TSAN_OPTIONS="halt_on_error=1 second_deadlock_stack=1" $B/pipeline_driver $S
+rm -rf $S
