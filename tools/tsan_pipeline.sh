@@ -24,5 +24,8 @@ gcc -fsanitize=thread -o $B/pipeline_driver $B/pipeline_driver.o $objs $P/build/
 if [ -n "${BUILD_ONLY:-}" ]; then exit 0; fi
 S=${TMPDIR:-/tmp}/bcp_tsan_pipeline_$$
 rm -rf $S
-TSAN_OPTIONS="halt_on_error=1 second_deadlock_stack=1" $B/pipeline_driver $S
+# setarch -R: no address-space randomisation (TSan's fixed shadow layout
+# refuses the high-entropy mmap bases of newer kernels: "unexpected memory
+# mapping"); the driver is exec'ed before anything touches the GPU
+TSAN_OPTIONS="halt_on_error=1 second_deadlock_stack=1" setarch "$(uname -m)" -R $B/pipeline_driver $S
 rm -rf $S
