@@ -27,5 +27,6 @@ rm -rf $S
 # setarch -R: no address-space randomisation (TSan's fixed shadow layout
 # refuses the high-entropy mmap bases of newer kernels: "unexpected memory
 # mapping"); the driver is exec'ed before anything touches the GPU
-TSAN_OPTIONS="halt_on_error=1 second_deadlock_stack=1" setarch "$(uname -m)" -R $B/pipeline_driver $S
+TSAN_OPTIONS="halt_on_error=1 second_deadlock_stack=1 suppressions=$R/tools/tsan_rocm.supp" \
+  setarch "$(uname -m)" -R $B/pipeline_driver $S
 rm -rf $S
