@@ -839,7 +839,8 @@ def e2e_leg(a, d, device: int, bus_id: str):
                 st, nplanned = pl.round(rank_root, NT, es, cum_weight=[1000 * (k + 1) for k in range(NT)])
             finally:
                 es.close()
-            return time.perf_counter() - t0, st.seconds, nplanned == len(sub) and st.errors == 0 and st.tasks == len(sub)
+            return (time.perf_counter() - t0, st.seconds, nplanned == len(sub) and st.errors == 0 and st.tasks == len(sub),
+                    pl.last_timing())
 
         packed = guard("partial: rewriting the subset", prepare) if pl is not None else None
         runs_p = []
@@ -876,6 +877,7 @@ def e2e_leg(a, d, device: int, bus_id: str):
                 "bytes_written": sum(8 * W + int(lens[i].max()) for i in sub),
                 "own_runs_s": [round(x, 4) for x in times], "own_warm_s": round(float(np.median(times[1:])), 4),
                 "own_pipeline_warm_s": round(float(np.median([x[1] for x in runs_p][1:])), 4),
+                "pipeline_timing_last": runs_p[-1][3],
                 "plan_ok": bool(plan_ok), "verified": bool(verified)}
 
     pls = {}
@@ -1005,6 +1007,7 @@ def e2e_leg(a, d, device: int, bus_id: str):
                 "bytes_written": sum(p["bytes_written"] for p in ps), "warm_s": slow_warm,
                 "GiBps": round(b / slow_warm / GiB, 2),
                 "pipeline_warm_s_rank0": ps[0]["own_pipeline_warm_s"],
+                "pipeline_timing_rank0": ps[0].get("pipeline_timing_last"),
                 "runs_s_rank0": ps[0]["own_runs_s"],
                 "plan_ok": all(p["plan_ok"] for p in ps), "verified": all(p["verified"] for p in ps)}
     return {
