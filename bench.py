@@ -112,7 +112,7 @@ def parse():
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-configs", action="store_true", help="skip the config-1 protocol leg (rank 0)")
     ap.add_argument("--c1-files", type=int, default=1333, help="config 1: files (3 chunks of 512 KiB each)")
-    ap.add_argument("--c1-reps", type=int, default=3, help="config 1: warm rounds per leg (after one cold round)")
+    ap.add_argument("--c1-reps", type=int, default=7, help="config 1: warm rounds per leg (after one cold round)")
     ap.add_argument("--no-prof", action="store_true",
                     help="skip the live rocprofv3 kernel-trace and PMC passes of this workload on this box")
     ap.add_argument("--allow-shared", action="store_true",
