@@ -439,19 +439,26 @@ def test_rank_pool_on_device(tmp_path, mode):
 
 
 @pytest.mark.parametrize("engine_kind", ["default", "protocol", "pipeline", "pipeline_direct", "procs",
-                                         "procs_batched"])
+                                         "procs_batched", "protocol_ranked", "default_ranked"])
 def test_cli_complete_partial_rebuild(bcp, oracle, tmp_path, engine_kind):
     """bin/bcp end to end on the device: --complete (scan of every target),
     --partial from changelog record files, then parity-rebuild from the DB --
     ranks as threads, the batched pipeline, or ranks as processes (--procs:
     one forked process per target on the socketpair transport, each with its
     the node fold server holding the GPU for all of them, in the default fold
-    mode or batched)."""
+    mode or batched).  *_ranked: the store states a permuted MPI rank order
+    (<root>/rank_order), so the coordinators' rounds run in that order -- the
+    same files and DB state."""
     import subprocess
     import planner as PL
     rng = np.random.default_rng(21)
     root, nt = str(tmp_path / "store"), 6
     S.make_store(root, nt)
+    if engine_kind.endswith("_ranked"):  # ids default to k + 1 (no targetNumID files)
+        with open(os.path.join(root, "rank_order"), "w") as f:
+            f.write("4 1 6 2 5 3\n")
+        assert bcp.store_round_order(root, nt) == [3, 0, 5, 1, 4, 2]
+        engine_kind = engine_kind[:-len("_ranked")]
     files, contents = {}, {}
     for i in range(20):
         path = f"u{i % 2}/{i:02X}/c{i}"
