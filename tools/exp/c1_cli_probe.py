@@ -32,6 +32,8 @@ def main():
     ap.add_argument("--runs", type=int, default=4)
     ap.add_argument("--dir", default="/dev/shm")
     ap.add_argument("--engines", default="pipeline,protocol")
+    ap.add_argument("--tools", default="", help="CLI builds to alternate (comma separated paths to bin/bcp; "
+                                                   "default: the in-tree one)")
     a = ap.parse_args()
     NT, C = 4, 512 * KiB
     root = os.path.join(a.dir, f"c1cli_{os.getpid()}")
@@ -48,22 +50,29 @@ def main():
                 f.write(memoryview(block[off:off + C]))
     with cf.ThreadPoolExecutor(8) as ex:
         list(ex.map(write_file, range(a.files)))
-    tool = os.path.join(ROOT, "beegfs-chunk-parity_amd", "bin", "bcp")
-    engines = a.engines.split(",")
-    res = {e: [] for e in engines}
+    tools = [os.path.abspath(t) for t in a.tools.split(",") if t] or \
+        [os.path.join(ROOT, "beegfs-chunk-parity_amd", "bin", "bcp")]
+    keys = [(t, e) for t in tools for e in a.engines.split(",")]
+    res = {k: [] for k in keys}
     for r in range(a.runs):
-        for e in engines:
+        for tool, e in keys[r % len(keys):] + keys[:r % len(keys)]:
             t0 = time.perf_counter()
             p = subprocess.run([tool, "parity-gen", "--complete", "--force", f"--{e}", root, str(NT)],
                                capture_output=True, text=True)
             wall = time.perf_counter() - t0
             line = next((ln for ln in p.stdout.splitlines() if ln.startswith("timings:")), "")
             stages = {k: float(v) for k, v in re.findall(r"([a-z0-9 ()]+?) ([0-9.]+) s", line.replace("timings: ", ""))}
-            res[e].append({"rc": p.returncode, "wall_s": round(wall, 4),
+            res[(tool, e)].append({"rc": p.returncode, "wall_s": round(wall, 4),
                            "stages": {k.strip(" ,()"): v for k, v in stages.items()},
                            "err": p.stderr[-300:] if p.returncode else None})
-    for e in engines:
-        print(json.dumps({"engine": e, "runs": res[e]}), flush=True)
+    import statistics
+    for (tool, e), runs in res.items():
+        warm = runs[1:] or runs
+        print(json.dumps({"tool": os.path.relpath(tool, ROOT), "engine": e,
+                          "wall_median_s": round(statistics.median(x["wall_s"] for x in warm), 4),
+                          "setup_median_s": round(statistics.median(x["stages"].get("engine setup", 0) for x in warm), 4),
+                          "total_median_s": round(statistics.median(x["stages"].get("total", 0) for x in warm), 4),
+                          "runs": runs}), flush=True)
     shutil.rmtree(root, ignore_errors=True)
 
 
