@@ -437,7 +437,7 @@ def gen_config_label(world: int, stripes: int) -> str:
     return "config4" if world == 8 and stripes == 15_625 else "config2"
 
 
-def config1_leg(a) -> dict:
+def config1_leg(a, device: int = 0) -> dict:
     """BASELINE config 1 (configs[0]): beegfs-parity-gen --complete over 4
     loopback storage-target ranks, ~1000 x 512 KiB chunk files per rank --
     files -> per-task protocol -> XOR -> parity files, timed end to end in this
@@ -460,7 +460,10 @@ def config1_leg(a) -> dict:
     rebuild/main.c:63).  Sampled parity files and rebuilt chunks are checked
     with numpy.  Rate = (chunk bytes read + parity bytes written) / warm run.
     The protocol around the reference fold is libbcp's: the reference program
-    itself needs MPI."""
+    itself needs MPI.  Every leg runs on this rank's GPU
+    (`device`): the P roles of all four targets are mapped to it
+    (bcp_task_set_device_map; by default target st would fold on GPU st %
+    count, other ranks' GPUs on a multi-GPU node)."""
     import concurrent.futures as cf
     import shutil
 
@@ -544,6 +547,8 @@ def config1_leg(a) -> dict:
     ok = {x: True for x in legs}
     rok = {x: True for x in legs}
     pl = None
+    import ctypes
+    bcp.lib().bcp_task_set_device_map((ctypes.c_int * NT)(*([device] * NT)), NT)
     try:
         BS.make_store(root, NT)
 
@@ -558,7 +563,7 @@ def config1_leg(a) -> dict:
         with cf.ThreadPoolExecutor(8) as ex:
             list(ex.map(write_file, range(nfiles)))
         t_store = time.perf_counter() - t0
-        pl = bcp.Pipeline()
+        pl = bcp.Pipeline(device=device)
         runs = 1 + max(1, a.c1_reps)
         for r in range(runs):
             for leg in legs[r % 3:] + legs[:r % 3]:
@@ -600,6 +605,7 @@ def config1_leg(a) -> dict:
         if pl is not None:
             pl.close()
         bcp.task_shutdown()
+        bcp.lib().bcp_task_set_device_map(None, 0)
         shutil.rmtree(root, ignore_errors=True)
     if errors:
         return {"error": errors[0], "wall_s": round(time.perf_counter() - t_start, 1)}
@@ -618,6 +624,7 @@ def config1_leg(a) -> dict:
         "workload": f"config1: beegfs-parity-gen --complete, {NT} loopback storage-target ranks, {nfiles} files x 3 "
                     f"x {C // KiB} KiB chunks ({nfiles * 3 // NT} per rank), P rotating over the target left out",
         "store": {"dir": base, "chunk_GiB": round(rd / GiB, 3), "write_s": round(t_store, 2)},
+        "device": device,
         "gen": gen,
         "rebuild": {"target": VICTIM, "files": len(lost), **reb},
         "gpu_fold_over_reference_fold": round(gen["gpu_fold"]["GiBps"] / gen["reference_fold"]["GiBps"], 3),
@@ -1307,7 +1314,7 @@ def main():
     c1 = None
     if d.rank == 0 and not a.no_configs:
         try:
-            c1 = config1_leg(a)
+            c1 = config1_leg(a, eng.device)
         except Exception as e:  # reported, never worth the device line
             c1 = {"error": f"{type(e).__name__}: {e}"}
     # rocprofv3 on this box: rank 0's device, child processes (the device
