@@ -437,6 +437,17 @@ def gen_config_label(world: int, stripes: int) -> str:
     return "config4" if world == 8 and stripes == 15_625 else "config2"
 
 
+def cpu_baseline_fold():
+    """The cpu_baseline leg's library as a P-role fold hook (bcp_xor_hook_fn):
+    the reference's own xor_parity, task_processing.c:96-109 compiled
+    unchanged into oracle/_ref (oracle.cpu_fold_hook; the restatement where
+    _ref was not built).  Only config1_leg's reference_fold leg uses it --
+    the reference CPU path timed beside the product, never the product."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # cpu_baseline leg only
+    return oracle.cpu_fold_hook()
+
+
 def config1_leg(a, device: int = 0) -> dict:
     """BASELINE config 1 (configs[0]): beegfs-parity-gen --complete over 4
     loopback storage-target ranks, ~1000 x 512 KiB chunk files per rank --
@@ -469,8 +480,6 @@ def config1_leg(a, device: int = 0) -> dict:
 
     import numpy as np
     import bcp_store as BS
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import oracle  # cpu_baseline leg only: the reference's xor_parity as the P-role fold
     t_start = time.perf_counter()
     NT, C, VICTIM = 4, 512 * KiB, 2
     nfiles = a.c1_files
@@ -498,7 +507,7 @@ def config1_leg(a, device: int = 0) -> dict:
     vr = np.random.default_rng(13)
     sample = sorted({0, nfiles - 1} | {int(x) for x in vr.integers(0, nfiles, 10)})
     rsample = sorted({lost[0], lost[-1]} | {lost[int(x)] for x in vr.integers(0, len(lost), 8)})
-    ref_fold, ref_name = oracle.cpu_fold_hook()
+    ref_fold, ref_name = cpu_baseline_fold()
     kind = "reference" if ref_name == "ref_xor_parity" else "port"
     errors = []
 
@@ -1417,7 +1426,11 @@ def main():
                              "workload -- or, where those failed or --no-prof, the committed profile set "
                              "(profile_files, measured on profile_box)",
             },
-            "cpu_baseline": cpu,
+            "cpu_baseline": (dict(cpu, config1_protocol_reference_fold=(
+                {"gen_GiBps": c1["gen"]["reference_fold"]["GiBps"],
+                 "rebuild_GiBps": c1["rebuild"]["reference_fold"]["GiBps"], "kind": c1["gen"]["reference_fold"]["kind"],
+                 "see": "configs.config1"} if isinstance(c1, dict) and "gen" in c1 else None))
+                             if isinstance(cpu, dict) else cpu),
             "per_rank": per_rank,
             "e2e": e2e,
             # BASELINE configs[0] and configs[4] as BASELINE states them (rank 0's config-1 protocol
