@@ -9,7 +9,7 @@ wire (implicit / the reference's) and the fold service width; every parity
 file must equal the oracle's (oracle.gen_parity_file, the reference's
 parity_generator restated).  Then a random target is lost and rebuilt by
 the protocol (1..4 rebuild lanes) or the pipeline (either read path, COPY or
-MAP); every lost chunk of a
+DIRECT); every lost chunk of a
 stripe without a missing chunk must come back byte for byte."""
 import os
 import shutil
