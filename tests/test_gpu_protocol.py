@@ -439,7 +439,7 @@ def test_rank_pool_on_device(tmp_path, mode):
 
 
 @pytest.mark.parametrize("engine_kind", ["default", "protocol", "pipeline", "pipeline_direct", "procs",
-                                         "procs_batched", "protocol_ranked", "default_ranked"])
+                                         "procs_batched", "protocol_ranked", "default_ranked", "procs_ranked"])
 def test_cli_complete_partial_rebuild(bcp, oracle, tmp_path, engine_kind):
     """bin/bcp end to end on the device: --complete (scan of every target),
     --partial from changelog record files, then parity-rebuild from the DB --
