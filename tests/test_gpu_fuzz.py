@@ -115,6 +115,8 @@ def test_random_batches_match_the_oracle(oracle, engine, queue):
             rounds += 1
             stripes_done += len(stripes)
             bytes_done += sum(len(r) for r in refs)
+            if rounds % 50 == 0:
+                print(f"fuzz: {rounds} batches ...", flush=True)  # progress for long soaks
     finally:
         for k, v in defaults.items():
             engine.option(k, v)
