@@ -448,6 +448,12 @@ def cpu_baseline_fold():
     return oracle.cpu_fold_hook()
 
 
+def proc_cpu_s() -> float:
+    import resource
+    ru = resource.getrusage(resource.RUSAGE_SELF)
+    return ru.ru_utime + ru.ru_stime
+
+
 def config1_leg(a, device: int = 0) -> dict:
     """BASELINE config 1 (configs[0]): beegfs-parity-gen --complete over 4
     loopback storage-target ranks, ~1000 x 512 KiB chunk files per rank --
@@ -553,6 +559,8 @@ def config1_leg(a, device: int = 0) -> dict:
     pl_timing = {}
     gen_t = {x: [] for x in legs}
     reb_t = {x: [] for x in legs}
+    gen_c = {x: [] for x in legs}  # this process's CPU seconds (all threads, user + system) per run
+    reb_c = {x: [] for x in legs}
     ok = {x: True for x in legs}
     rok = {x: True for x in legs}
     pl = None
@@ -577,6 +585,7 @@ def config1_leg(a, device: int = 0) -> dict:
         for r in range(runs):
             for leg in legs[r % 3:] + legs[:r % 3]:
                 reset_parity()
+                c0 = proc_cpu_s()
                 t0 = time.perf_counter()
                 if leg == "pipeline":
                     st = pl.run(root, NT, items)
@@ -584,6 +593,7 @@ def config1_leg(a, device: int = 0) -> dict:
                 else:
                     st = with_fold(leg, lambda: bcp.gen_run(root, NT, items, nlanes=12))
                 gen_t[leg].append(time.perf_counter() - t0)
+                gen_c[leg].append(proc_cpu_s() - c0)
                 good = st.errors == 0 and st.tasks == (nfiles if leg == "pipeline" else 4 * nfiles)
                 if r == runs - 1:
                     good = good and all(parity_ok(i) for i in sample)
@@ -595,6 +605,7 @@ def config1_leg(a, device: int = 0) -> dict:
             for r in range(runs):
                 for leg in legs[r % 3:] + legs[:r % 3]:
                     drop_victim()
+                    c0 = proc_cpu_s()
                     t0 = time.perf_counter()
                     if leg == "pipeline":
                         st = pl.rebuild(root, NT, VICTIM, ordered)
@@ -602,6 +613,7 @@ def config1_leg(a, device: int = 0) -> dict:
                     else:
                         st = with_fold(leg, lambda: bcp.rebuild_run(root, NT, VICTIM, ordered))
                     reb_t[leg].append(time.perf_counter() - t0)
+                    reb_c[leg].append(proc_cpu_s() - c0)
                     good = st.errors == 0
                     if r == runs - 1:
                         good = good and all(rebuilt_ok(i) for i in rsample)
@@ -620,12 +632,14 @@ def config1_leg(a, device: int = 0) -> dict:
         return {"error": errors[0], "wall_s": round(time.perf_counter() - t_start, 1)}
     import statistics
 
-    def summary(t, b, good):
+    def summary(t, c, b, good):
         warm = statistics.median(t[1:])
         return {"cold_s": round(t[0], 4), "warm_s": round(warm, 4), "runs_s": [round(x, 4) for x in t],
-                "GiBps": round(b / warm / GiB, 2), "verified": good}
-    gen = {leg: summary(gen_t[leg], rd + wr, ok[leg]) for leg in legs}
-    reb = {leg: summary(reb_t[leg], rb_rd + rb_wr, rok[leg]) for leg in legs}
+                "GiBps": round(b / warm / GiB, 2), "verified": good,
+                "cpu_s": round(statistics.median(c[1:]), 3),
+                "cores_busy": round(statistics.median(x / y for x, y in zip(c[1:], t[1:])), 1)}
+    gen = {leg: summary(gen_t[leg], gen_c[leg], rd + wr, ok[leg]) for leg in legs}
+    reb = {leg: summary(reb_t[leg], reb_c[leg], rb_rd + rb_wr, rok[leg]) for leg in legs}
     gen["reference_fold"]["kind"] = reb["reference_fold"]["kind"] = kind
     gen["pipeline"]["last_run_timing"] = pl_timing.get("gen")
     reb["pipeline"]["last_run_timing"] = pl_timing.get("rebuild")
@@ -640,6 +654,10 @@ def config1_leg(a, device: int = 0) -> dict:
         "pipeline_over_reference_fold": round(gen["pipeline"]["GiBps"] / gen["reference_fold"]["GiBps"], 3),
         "rebuild_gpu_fold_over_reference_fold": round(reb["gpu_fold"]["GiBps"] / reb["reference_fold"]["GiBps"], 3),
         "bytes": {"gen_read": rd, "gen_written": wr, "rebuild_read": rb_rd, "rebuild_written": rb_wr},
+        "cpu_quota": cpu_quota(),
+        "cpu_note": "cpu_s: this process's CPU seconds (all threads, user + system, getrusage) per warm run, median; "
+                    "cores_busy: cpu_s / wall per run, median -- against cpu_quota, the host CPU time bounds the "
+                    "protocol legs (tmpfs reads and parity writes are kernel copies)",
         "legs_note": "reference_fold: bcp_gen_run / bcp_rebuild_run (process_task over loopback threads, 12 lanes "
                      "per rank for gen, 1 for rebuild) with the P role's fold = the reference's own xor_parity "
                      f"({ref_name}) over whole windows on the reference's zero-padded wire; gpu_fold: the same "

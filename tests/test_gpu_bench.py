@@ -156,6 +156,7 @@ def test_bench_configs_block_one_rank(bcp):
         for leg in ("reference_fold", "gpu_fold", "pipeline"):
             x = c1[what][leg]
             assert x["verified"] is True and x["GiBps"] > 0 and len(x["runs_s"]) == 2, (what, leg, x)
+            assert x["cpu_s"] > 0 and x["cores_busy"] > 0, (what, leg, x)
     assert c1["gen"]["reference_fold"]["kind"] == "reference" and c1["rebuild"]["files"] == 72
     assert c1["bytes"]["gen_read"] == 96 * 3 * 512 * 1024
     part = line["configs"]["config5_partial"]

@@ -41,6 +41,7 @@ import argparse
 import ctypes
 import json
 import os
+import resource
 import shutil
 import subprocess
 import sys
@@ -74,6 +75,20 @@ def noop_hook():
     so = os.path.join(tmp, "libnoop.so")
     subprocess.run(["gcc", "-O2", "-shared", "-fPIC", "-o", so, src], check=True)
     return ctypes.CDLL(so)
+
+
+def cpu_now():
+    """(process CPU seconds over all threads, cgroup throttled periods, throttled us)."""
+    ru = resource.getrusage(resource.RUSAGE_SELF)
+    nr = us = 0
+    try:
+        for ln in open("/sys/fs/cgroup/cpu.stat"):
+            k, v = ln.split()
+            nr = int(v) if k == "nr_throttled" else nr
+            us = int(v) if k == "throttled_usec" else us
+    except OSError:
+        pass
+    return ru.ru_utime + ru.ru_stime, nr, us
 
 
 def fold_setup(fold, hooks):
@@ -112,6 +127,7 @@ def fold_setup(fold, hooks):
 
 def measure(name, folds, rounds, run_once, verify_fn, nbytes, hooks, extra=None, prepare=None):
     times = {f: [] for f in folds}
+    cpu = {f: [] for f in folds}  # (CPU seconds, throttled periods, throttled ms) per run
     batching = {}
     phases = {}
     for r in range(rounds + 1):
@@ -124,9 +140,12 @@ def measure(name, folds, rounds, run_once, verify_fn, nbytes, hooks, extra=None,
                 w0, l0 = bcp.fold_stats()
                 pw0, pr0 = bcp.pipe_stats()
                 bcp.phase_stats(reset=True)
+                c0 = cpu_now()
                 t0 = time.perf_counter()
                 st = run_once()
                 dt = time.perf_counter() - t0
+                c1 = cpu_now()
+                cpu[f].append((c1[0] - c0[0], c1[1] - c0[1], (c1[2] - c0[2]) / 1e3))
                 w1, l1 = bcp.fold_stats()
                 pw1, pr1 = bcp.pipe_stats()
                 ph = bcp.phase_stats()
@@ -156,7 +175,11 @@ def measure(name, folds, rounds, run_once, verify_fn, nbytes, hooks, extra=None,
         warm = float(np.median(times[f][1:]))
         res[f] = nbytes / warm / GiB
         line = dict(workload=name, fold=f, GiBps=round(res[f], 3), warm_median_s=round(warm, 4),
-                    runs_s=[round(x, 4) for x in times[f]], cold_s=round(times[f][0], 4))
+                    runs_s=[round(x, 4) for x in times[f]], cold_s=round(times[f][0], 4),
+                    cpu_s_median=round(float(np.median([c[0] for c in cpu[f][1:]])), 4),
+                    cores_busy_median=round(float(np.median([c[0] / t for c, t in zip(cpu[f][1:], times[f][1:])])), 2),
+                    throttled_periods=sum(c[1] for c in cpu[f][1:]),
+                    throttled_ms_runs=[round(c[2], 1) for c in cpu[f]])
         if f.startswith("gpu_pipelined") and batching.get(f, {}).get("windows"):
             line["range_folds_per_window"] = round(batching[f]["launches"] / batching[f]["windows"], 2)
         elif batching.get(f, {}).get("launches"):
