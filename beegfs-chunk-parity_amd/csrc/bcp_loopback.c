@@ -7,15 +7,18 @@
  * source and tag) for ranks that are threads of one process.
  *
  * Matching: every destination rank has an inbox of unmatched sends (FIFO by
- * arrival) and a list of posted receives (FIFO by posting).  An arriving send
- * takes the oldest posted receive with its (source, tag); a new receive takes
- * the oldest inbox entry with its (source, tag).  That gives MPI's
- * non-overtaking order per (source, destination, tag).
+ * arrival) and a list of posted receives (FIFO by posting), split into
+ * LB_SHARDS channels by tag, each with its own lock (the protocol's tag is the
+ * lane: the lanes of one rank do not contend for one lock).  An arriving send
+ * takes the oldest posted receive with its (source, tag) in its channel; a new
+ * receive takes the oldest inbox entry with its (source, tag).  That gives
+ * MPI's non-overtaking order per (source, destination, tag).
  *
- * Copies: blocking sends are rendezvous -- the receiver copies straight from
- * the sender's buffer (one memcpy, outside the lock) and then releases the
- * sender; non-blocking sends are eager (copied at post time; the protocol only
- * uses them for the 8-byte max_cs broadcast).  Fill sends (bcp_lb_send_fill)
+ * Copies: blocking sends above LB_EAGER_MAX are rendezvous -- the receiver
+ * copies straight from the sender's buffer (one memcpy, outside the lock) and
+ * then releases the sender; smaller blocking sends and all non-blocking sends
+ * are eager (copied at post time, the sender goes on: the protocol's 8-byte
+ * chunk sizes and max_cs broadcast, the rebuild's size table).  Fill sends (bcp_lb_send_fill)
  * copy nothing: once matched, the receiver's buffer is handed to the sending
  * thread, whose callback writes the payload into it (the chunk sender reads
  * its file straight into the P role's window row).
@@ -35,7 +38,7 @@ typedef struct lb_msg {
     int src, tag;
     const void *buf;     /* payload (sender's or eager copy) */
     size_t n;
-    int eager;           /* payload is owned by this record */
+    int eager;           /* payload is owned by this record (free_eager) */
     int done;            /* rendezvous: receiver finished copying */
     int fill;            /* fill send: payload produced by the sender into `target` */
     struct bcp_lb_req *target; /* fill send: the matched receive */
@@ -44,6 +47,7 @@ typedef struct lb_msg {
 
 struct bcp_lb_req {
     struct bcp_lb_req *next;
+    pthread_mutex_t *mu; /* the channel lock done / cv are guarded by */
     int is_recv;
     int src, tag;        /* recv: match key */
     void *buf;
@@ -54,30 +58,57 @@ struct bcp_lb_req {
     pthread_cond_t cv;
 };
 
+/* Channels per destination rank (a power of two; tags map by their low bits). */
+#define LB_SHARDS 64
+
 typedef struct {
+    pthread_mutex_t mu;
     lb_msg *inbox_head, *inbox_tail;
     bcp_lb_req *posted_head, *posted_tail;
-} lb_rank;
+} __attribute__((aligned(64))) lb_chan;
 
-static pthread_mutex_t g_lock = PTHREAD_MUTEX_INITIALIZER;
-static lb_rank *g_ranks = NULL;
+static pthread_mutex_t g_lock = PTHREAD_MUTEX_INITIALIZER; /* init / finalize */
+static lb_chan *g_chans = NULL;                            /* g_world x LB_SHARDS */
 static int g_world = 0;
 static __thread int t_rank = -1;
+
+static lb_chan *chan_of(int rank, int tag)
+{
+    return &g_chans[(size_t)rank * LB_SHARDS + ((unsigned)tag & (LB_SHARDS - 1))];
+}
+
+/* Blocking sends up to this size are buffered (eager): the protocol's 8-byte
+ * chunk sizes and the rebuild's size table need no rendezvous. */
+#define LB_EAGER_MAX 4096
+
+/* An eager inbox record: 1 = payload malloc'd apart (isend), 2 = inline (send). */
+static void free_eager(lb_msg *m)
+{
+    if (m->eager == 1) {
+        free((void *)m->buf);
+        pthread_cond_destroy(&m->cv);
+    }
+    free(m);
+}
 
 int bcp_lb_init(int world_size)
 {
     if (world_size <= 0)
         return -EINVAL;
     pthread_mutex_lock(&g_lock);
-    if (g_ranks) {
+    if (g_chans) {
         pthread_mutex_unlock(&g_lock);
         return -EBUSY;
     }
-    g_ranks = calloc((size_t)world_size, sizeof(lb_rank));
-    if (!g_ranks) {
+    lb_chan *c = aligned_alloc(64, (size_t)world_size * LB_SHARDS * sizeof(lb_chan));
+    if (!c) {
         pthread_mutex_unlock(&g_lock);
         return -ENOMEM;
     }
+    memset(c, 0, (size_t)world_size * LB_SHARDS * sizeof(lb_chan));
+    for (size_t i = 0; i < (size_t)world_size * LB_SHARDS; i++)
+        pthread_mutex_init(&c[i].mu, NULL);
+    g_chans = c;
     g_world = world_size;
     pthread_mutex_unlock(&g_lock);
     return 0;
@@ -87,22 +118,21 @@ int bcp_lb_finalize(void)
 {
     pthread_mutex_lock(&g_lock);
     int leftover = 0;
-    for (int r = 0; r < g_world; r++) {
-        for (lb_msg *m = g_ranks[r].inbox_head; m;) {
+    for (size_t i = 0; g_chans && i < (size_t)g_world * LB_SHARDS; i++) {
+        lb_chan *c = &g_chans[i];
+        for (lb_msg *m = c->inbox_head; m;) {
             lb_msg *nx = m->next;
             leftover++;
-            if (m->eager) {
-                free((void *)m->buf);
-                pthread_cond_destroy(&m->cv);
-                free(m);
-            }
+            if (m->eager)
+                free_eager(m);
             m = nx;
         }
-        if (g_ranks[r].posted_head)
+        if (c->posted_head)
             leftover++;
+        pthread_mutex_destroy(&c->mu);
     }
-    free(g_ranks);
-    g_ranks = NULL;
+    free(g_chans);
+    g_chans = NULL;
     g_world = 0;
     pthread_mutex_unlock(&g_lock);
     return leftover ? -EPIPE : 0;
@@ -114,7 +144,7 @@ int bcp_lb_rank(void) { return t_rank; }
 
 static int check_peer(int peer)
 {
-    if (!g_ranks || peer < 0 || peer >= g_world || t_rank < 0 || t_rank >= g_world)
+    if (!g_chans || peer < 0 || peer >= g_world || t_rank < 0 || t_rank >= g_world)
         return -EINVAL;
     return 0;
 }
@@ -129,8 +159,8 @@ static void deliver(bcp_lb_req *r, const void *buf, size_t n)
     r->status = n <= r->cap ? 0 : -EMSGSIZE;
 }
 
-/* Remove and return the oldest posted receive at `dst` matching (src, tag). */
-static bcp_lb_req *take_posted(lb_rank *d, int src, int tag)
+/* Remove and return the oldest posted receive in channel d matching (src, tag). */
+static bcp_lb_req *take_posted(lb_chan *d, int src, int tag)
 {
     bcp_lb_req *prev = NULL;
     for (bcp_lb_req *r = d->posted_head; r; prev = r, r = r->next) {
@@ -148,7 +178,7 @@ static bcp_lb_req *take_posted(lb_rank *d, int src, int tag)
     return NULL;
 }
 
-static lb_msg *take_inbox(lb_rank *d, int src, int tag)
+static lb_msg *take_inbox(lb_chan *d, int src, int tag)
 {
     lb_msg *prev = NULL;
     for (lb_msg *m = d->inbox_head; m; prev = m, m = m->next) {
@@ -166,7 +196,7 @@ static lb_msg *take_inbox(lb_rank *d, int src, int tag)
     return NULL;
 }
 
-static void push_inbox(lb_rank *d, lb_msg *m)
+static void push_inbox(lb_chan *d, lb_msg *m)
 {
     m->next = NULL;
     if (d->inbox_tail)
@@ -178,10 +208,11 @@ static void push_inbox(lb_rank *d, lb_msg *m)
 
 static void complete_req(bcp_lb_req *r)
 {
-    pthread_mutex_lock(&g_lock);
+    pthread_mutex_t *mu = r->mu;
+    pthread_mutex_lock(mu);
     r->done = 1;
     pthread_cond_signal(&r->cv);
-    pthread_mutex_unlock(&g_lock);
+    pthread_mutex_unlock(mu);
 }
 
 int bcp_lb_send(const void *buf, size_t n, int dst, int tag)
@@ -189,15 +220,34 @@ int bcp_lb_send(const void *buf, size_t n, int dst, int tag)
     int rc = check_peer(dst);
     if (rc)
         return rc;
-    pthread_mutex_lock(&g_lock);
-    lb_rank *d = &g_ranks[dst];
+    lb_chan *d = chan_of(dst, tag);
+    pthread_mutex_lock(&d->mu);
     bcp_lb_req *r = take_posted(d, t_rank, tag);
     if (r) {
-        pthread_mutex_unlock(&g_lock);
+        pthread_mutex_unlock(&d->mu);
         deliver(r, buf, n);
         int st = r->status; /* r belongs to the receiver once completed */
         complete_req(r);
         return st;
+    }
+    if (n <= LB_EAGER_MAX) {
+        /* small: buffered, the sender goes on (MPI_Send may buffer; shared-
+         * memory MPIs do below their eager limit) */
+        lb_msg *m = calloc(1, sizeof(*m) + (n ? n : 1));
+        if (!m) {
+            pthread_mutex_unlock(&d->mu);
+            return -ENOMEM;
+        }
+        if (n)
+            memcpy(m + 1, buf, n);
+        m->src = t_rank;
+        m->tag = tag;
+        m->buf = m + 1;
+        m->n = n;
+        m->eager = 2;
+        push_inbox(d, m);
+        pthread_mutex_unlock(&d->mu);
+        return 0;
     }
     lb_msg m = {0};
     m.src = t_rank;
@@ -207,8 +257,8 @@ int bcp_lb_send(const void *buf, size_t n, int dst, int tag)
     pthread_cond_init(&m.cv, NULL);
     push_inbox(d, &m);
     while (!m.done)
-        pthread_cond_wait(&m.cv, &g_lock);
-    pthread_mutex_unlock(&g_lock);
+        pthread_cond_wait(&m.cv, &d->mu);
+    pthread_mutex_unlock(&d->mu);
     pthread_cond_destroy(&m.cv);
     return 0;
 }
@@ -248,8 +298,8 @@ int bcp_lb_send_fill(bcp_lb_fill_fn fill, void *ctx, size_t n, int dst, int tag)
         return rc;
     if (!fill)
         return -EINVAL;
-    pthread_mutex_lock(&g_lock);
-    lb_rank *d = &g_ranks[dst];
+    lb_chan *d = chan_of(dst, tag);
+    pthread_mutex_lock(&d->mu);
     bcp_lb_req *r = take_posted(d, t_rank, tag);
     if (!r) {
         lb_msg m = {0};
@@ -260,12 +310,12 @@ int bcp_lb_send_fill(bcp_lb_fill_fn fill, void *ctx, size_t n, int dst, int tag)
         pthread_cond_init(&m.cv, NULL);
         push_inbox(d, &m);
         while (!m.target)
-            pthread_cond_wait(&m.cv, &g_lock);
+            pthread_cond_wait(&m.cv, &d->mu);
         r = m.target;
-        pthread_mutex_unlock(&g_lock);
+        pthread_mutex_unlock(&d->mu);
         pthread_cond_destroy(&m.cv);
     } else {
-        pthread_mutex_unlock(&g_lock);
+        pthread_mutex_unlock(&d->mu);
     }
     return fill_into(r, fill, ctx, n);
 }
@@ -280,18 +330,19 @@ int bcp_lb_isend(const void *buf, size_t n, int dst, int tag, bcp_lb_req **req)
         return -ENOMEM;
     pthread_cond_init(&s->cv, NULL);
     s->done = 1; /* eager: complete at post */
-    pthread_mutex_lock(&g_lock);
-    lb_rank *d = &g_ranks[dst];
+    s->mu = &chan_of(dst, tag)->mu;
+    lb_chan *d = chan_of(dst, tag);
+    pthread_mutex_lock(&d->mu);
     bcp_lb_req *r = take_posted(d, t_rank, tag);
     if (r) {
-        pthread_mutex_unlock(&g_lock);
+        pthread_mutex_unlock(&d->mu);
         deliver(r, buf, n);
         complete_req(r);
     } else {
         lb_msg *m = calloc(1, sizeof(*m));
         void *copy = malloc(n ? n : 1);
         if (!m || !copy) {
-            pthread_mutex_unlock(&g_lock);
+            pthread_mutex_unlock(&d->mu);
             free(m);
             free(copy);
             pthread_cond_destroy(&s->cv);
@@ -307,7 +358,7 @@ int bcp_lb_isend(const void *buf, size_t n, int dst, int tag, bcp_lb_req **req)
         m->eager = 1;
         pthread_cond_init(&m->cv, NULL);
         push_inbox(d, m);
-        pthread_mutex_unlock(&g_lock);
+        pthread_mutex_unlock(&d->mu);
     }
     if (req)
         *req = s;
@@ -334,28 +385,27 @@ int bcp_lb_irecv(void *buf, size_t n, int src, int tag, bcp_lb_req **req)
     r->tag = tag;
     r->buf = buf;
     r->cap = n;
-    pthread_mutex_lock(&g_lock);
-    lb_rank *me = &g_ranks[t_rank];
+    lb_chan *me = chan_of(t_rank, tag);
+    r->mu = &me->mu;
+    pthread_mutex_lock(&me->mu);
     lb_msg *m = take_inbox(me, src, tag);
     if (m && m->fill) {
         /* hand the buffer to the sending thread; it completes r */
         r->next = NULL;
         m->target = r;
         pthread_cond_signal(&m->cv);
-        pthread_mutex_unlock(&g_lock);
+        pthread_mutex_unlock(&me->mu);
     } else if (m) {
-        pthread_mutex_unlock(&g_lock);
+        pthread_mutex_unlock(&me->mu);
         deliver(r, m->buf, m->n);
         r->done = 1;
         if (m->eager) {
-            free((void *)m->buf);
-            pthread_cond_destroy(&m->cv);
-            free(m);
+            free_eager(m);
         } else {
-            pthread_mutex_lock(&g_lock);
+            pthread_mutex_lock(&me->mu);
             m->done = 1; /* m lives on the sender's stack: signal under the lock */
             pthread_cond_signal(&m->cv);
-            pthread_mutex_unlock(&g_lock);
+            pthread_mutex_unlock(&me->mu);
         }
     } else {
         r->next = NULL;
@@ -364,7 +414,7 @@ int bcp_lb_irecv(void *buf, size_t n, int src, int tag, bcp_lb_req **req)
         else
             me->posted_head = r;
         me->posted_tail = r;
-        pthread_mutex_unlock(&g_lock);
+        pthread_mutex_unlock(&me->mu);
     }
     *req = r;
     return 0;
@@ -374,10 +424,11 @@ int bcp_lb_wait(bcp_lb_req *r, size_t *received)
 {
     if (!r)
         return -EINVAL;
-    pthread_mutex_lock(&g_lock);
+    pthread_mutex_t *mu = r->mu;
+    pthread_mutex_lock(mu);
     while (!r->done)
-        pthread_cond_wait(&r->cv, &g_lock);
-    pthread_mutex_unlock(&g_lock);
+        pthread_cond_wait(&r->cv, mu);
+    pthread_mutex_unlock(mu);
     int st = r->status;
     if (received)
         *received = r->received;

@@ -1,7 +1,10 @@
 /* Loopback transport checks (CPU): bcp_lb_send_fill against posted and
  * unposted receives, ordering with plain sends on the same (source, tag),
- * truncation, and fill errors.  Two ranks as two threads. */
+ * truncation, fill errors, small blocking sends that do not wait for their
+ * receive (eager), and tags that share a matching channel (tag and tag + 64)
+ * kept apart and in order.  Two ranks as two threads. */
 #include <errno.h>
+#include <stdint.h>
 #include <pthread.h>
 #include <stdio.h>
 #include <string.h>
@@ -52,6 +55,16 @@ static void *sender(void *arg)
     int go = 0;
     CHECK(bcp_lb_recv(&go, sizeof go, 1, 11, NULL) == 0);
     CHECK(bcp_lb_send_fill(fill_pattern, &b1, 256, 1, 12) == 0);
+    /* 6: small blocking sends return before any receive is posted (the
+     * receiver waits on tag 21 first: a rendezvous here would deadlock) */
+    for (uint64_t v = 1; v <= 3; v++)
+        CHECK(bcp_lb_send(&v, sizeof v, 1, 20) == 0);
+    CHECK(bcp_lb_send(&go, sizeof go, 1, 21) == 0);
+    /* 7: tags 30 and 94 share a channel; interleaved, received out of order */
+    for (uint64_t v = 0; v < 4; v++)
+        CHECK(bcp_lb_send(&v, sizeof v, 1, v % 2 ? 94 : 30) == 0);
+    for (int t = 0; t < 200; t += 7) /* many tags, many channels */
+        CHECK(bcp_lb_send(&t, sizeof t, 1, 1000 + t) == 0);
     return NULL;
 }
 
@@ -87,7 +100,26 @@ int main(void)
     int go = 1;
     CHECK(bcp_lb_send(&go, sizeof go, 0, 11) == 0);
     CHECK(bcp_lb_wait(r, &got) == 0 && got == 256 && buf[255] == (unsigned char)(1 + 255));
+    /* 6 */
+    CHECK(bcp_lb_recv(&go, sizeof go, 0, 21, NULL) == 0);
+    for (uint64_t v = 1; v <= 3; v++) {
+        uint64_t x = 0;
+        CHECK(bcp_lb_recv(&x, sizeof x, 0, 20, &got) == 0 && got == 8 && x == v);
+    }
+    /* 7: tag 94 first (values 1, 3), then tag 30 (0, 2); then the 29 tags backwards */
     pthread_join(th, NULL);
+    for (uint64_t want = 1; want < 4; want += 2) {
+        uint64_t x = 99;
+        CHECK(bcp_lb_recv(&x, sizeof x, 0, 94, NULL) == 0 && x == want);
+    }
+    for (uint64_t want = 0; want < 4; want += 2) {
+        uint64_t x = 99;
+        CHECK(bcp_lb_recv(&x, sizeof x, 0, 30, NULL) == 0 && x == want);
+    }
+    for (int t = 196; t >= 0; t -= 7) {
+        int x = -1;
+        CHECK(bcp_lb_recv(&x, sizeof x, 0, 1000 + t, NULL) == 0 && x == t);
+    }
     CHECK(bcp_lb_finalize() == 0);
     printf("%s (%d failures)\n", failures ? "FAILED" : "OK", failures);
     return failures ? 1 : 0;
