@@ -448,6 +448,34 @@ def cpu_baseline_fold():
     return oracle.cpu_fold_hook()
 
 
+def link_rates(device: int) -> dict:
+    """This process's H2D / D2H over pinned memory on `device` (256 MiB, median of 5)."""
+    import numpy as np
+    eng = bcp.Engine(device)
+    q = eng.queue()
+    nb = 256 << 20
+    h = eng.host_alloc(nb)
+    dv = eng.alloc(nb)
+    out = {}
+    try:
+        for name, fn in (("h2d_GBps", lambda: q.h2d(dv, h, nb)), ("d2h_GBps", lambda: q.d2h(h, dv, nb))):
+            tt = []
+            for _ in range(5):
+                q.sync()
+                t0 = time.perf_counter()
+                fn()
+                q.sync()
+                tt.append(time.perf_counter() - t0)
+            out[name] = round(nb / float(np.median(tt)) / 1e9, 2)
+    finally:
+        q.sync()
+        eng.free(dv)
+        eng.host_free(h)
+        q.close()
+        eng.close()
+    return out
+
+
 def proc_cpu_s() -> float:
     import resource
     ru = resource.getrusage(resource.RUSAGE_SELF)
@@ -557,6 +585,7 @@ def config1_leg(a, device: int = 0) -> dict:
 
     legs = ["reference_fold", "gpu_fold", "pipeline"]
     pl_timing = {}
+    link = {}
     gen_t = {x: [] for x in legs}
     reb_t = {x: [] for x in legs}
     gen_c = {x: [] for x in legs}  # this process's CPU seconds (all threads, user + system) per run
@@ -580,6 +609,7 @@ def config1_leg(a, device: int = 0) -> dict:
         with cf.ThreadPoolExecutor(8) as ex:
             list(ex.map(write_file, range(nfiles)))
         t_store = time.perf_counter() - t0
+        link = link_rates(device)
         pl = bcp.Pipeline(device=device)
         runs = 1 + max(1, a.c1_reps)
         for r in range(runs):
@@ -653,6 +683,11 @@ def config1_leg(a, device: int = 0) -> dict:
         "gpu_fold_over_reference_fold": round(gen["gpu_fold"]["GiBps"] / gen["reference_fold"]["GiBps"], 3),
         "pipeline_over_reference_fold": round(gen["pipeline"]["GiBps"] / gen["reference_fold"]["GiBps"], 3),
         "rebuild_gpu_fold_over_reference_fold": round(reb["gpu_fold"]["GiBps"] / reb["reference_fold"]["GiBps"], 3),
+        # every chunk byte a GPU fold folds crosses the host-to-device link once (parity comes back
+        # on the other direction): the gen rate it cannot pass on this link
+        "link": link,
+        "gpu_fold_link_ceiling_GiBps": (round((rd + wr) / (rd / (link["h2d_GBps"] * 1e9)) / GiB, 2)
+                                        if link.get("h2d_GBps") else None),
         "bytes": {"gen_read": rd, "gen_written": wr, "rebuild_read": rb_rd, "rebuild_written": rb_wr},
         "cpu_quota": cpu_quota(),
         "cpu_note": "cpu_s: this process's CPU seconds (all threads, user + system, getrusage) per warm run, median; "
@@ -779,32 +814,6 @@ def e2e_leg(a, d, device: int, bus_id: str):
         with cf.ThreadPoolExecutor(8) as ex:
             list(ex.map(write_stripe, range(nst)))
         return time.perf_counter() - t0
-
-    def link_rates():
-        """This rank's H2D / D2H over pinned memory (every rank at once)."""
-        eng = bcp.Engine(device)
-        q = eng.queue()
-        nb = 256 << 20
-        h = eng.host_alloc(nb)
-        dv = eng.alloc(nb)
-        out = {}
-        try:
-            for name, fn in (("h2d_GBps", lambda: q.h2d(dv, h, nb)), ("d2h_GBps", lambda: q.d2h(h, dv, nb))):
-                tt = []
-                for _ in range(5):
-                    q.sync()
-                    t0 = time.perf_counter()
-                    fn()
-                    q.sync()
-                    tt.append(time.perf_counter() - t0)
-                out[name] = round(nb / float(np.median(tt)) / 1e9, 2)
-        finally:
-            q.sync()
-            eng.free(dv)
-            eng.host_free(h)
-            q.close()
-            eng.close()
-        return out
 
     def parity_ok(i):
         ch = [chunk_of(i, k) for k in range(W)]
@@ -945,7 +954,7 @@ def e2e_leg(a, d, device: int, bus_id: str):
     try:
         t_store = guard("writing the store", write_store, 0.0)
         d.barrier()
-        link = guard("link probe", link_rates, {}) or {}
+        link = guard("link probe", lambda: link_rates(device), {}) or {}
         for m in modes:
             pl = guard(f"pipeline ({m})", lambda: bcp.Pipeline(
                 device=device, io_threads=io_threads,
