@@ -15,6 +15,10 @@
  * with that (source, tag) if there is one, else into an unexpected-message
  * buffer that a later receive takes (the match is re-checked under the lock
  * after the payload is in, so a receive posted meanwhile is never missed).
+ * The other waiters on that socket sleep on their own request's condition
+ * variable in a per-(source, socket) queue: a completed request wakes only
+ * its owner, and a reader whose own request completes hands the reading to
+ * the oldest waiter left (no broadcast to every lane of the rank per frame).
  * Sends write the frame under a per-destination lock (the lanes of a rank
  * share its sockets).  Writes block only on a full socket buffer, which the
  * destination drains as soon as any of its threads waits on us -- the MPI
@@ -79,6 +83,9 @@ typedef struct sk_req {
     uint64_t cts_addr, cts_cap; /* fill-send side: the receiver's answer */
     int ctl;                    /* waits on the control socket (a fill send's CTS) */
     int busy;                   /* its payload is being read into buf by the socket's reader */
+    pthread_cond_t cv;          /* its owner sleeps here (progress_until) */
+    int queued;                 /* in the wait queue of (src, ctl) */
+    struct sk_req *wnext;
 } sk_req;
 
 struct bcp_sock_world {
@@ -86,7 +93,7 @@ struct bcp_sock_world {
     int *fds;             /* [world][world]: fds[a*world+b] = a's end towards b (-1 closed) */
     int *cfds;            /* the same for the control sockets (CTS) */
     pthread_mutex_t mu;
-    pthread_cond_t cv;
+    sk_req **wq;              /* per (peer, socket): [2 * peer + ctl], waiters of that socket, oldest first */
     pthread_mutex_t *send_mu; /* per peer */
     pthread_mutex_t *ctl_mu;  /* per peer: control-socket writes */
     int *reading;             /* per peer: a thread is reading that socket */
@@ -281,7 +288,8 @@ int bcp_sock_world_create(int world_size, bcp_sock_world **out)
     w->reading = calloc((size_t)world_size, sizeof(int));
     w->reading_ctl = calloc((size_t)world_size, sizeof(int));
     w->dead = calloc((size_t)world_size, sizeof(int));
-    if (!w->fds || !w->cfds || !w->send_mu || !w->ctl_mu || !w->reading || !w->reading_ctl || !w->dead) {
+    w->wq = calloc((size_t)world_size * 2, sizeof(sk_req *));
+    if (!w->fds || !w->cfds || !w->send_mu || !w->ctl_mu || !w->reading || !w->reading_ctl || !w->dead || !w->wq) {
         if (w->fds)
             for (int i = 0; i < world_size * world_size; i++)
                 w->fds[i] = -1;
@@ -307,7 +315,6 @@ int bcp_sock_world_create(int world_size, bcp_sock_world **out)
         }
     }
     pthread_mutex_init(&w->mu, NULL);
-    pthread_cond_init(&w->cv, NULL);
     for (int i = 0; i < world_size; i++) {
         pthread_mutex_init(&w->send_mu[i], NULL);
         pthread_mutex_init(&w->ctl_mu[i], NULL);
@@ -361,6 +368,7 @@ int bcp_sock_world_destroy(bcp_sock_world *w)
     free(w->reading);
     free(w->reading_ctl);
     free(w->dead);
+    free(w->wq);
     if (w->arena) {
         pthread_mutex_lock(&g_arena_mu);
         if (g_arena_lo == w->arena) {
@@ -537,6 +545,48 @@ static void deliver_msg(sk_req *r, sk_msg *m)
     free(m);
 }
 
+/* ---- waiters (under w->mu) ------------------------------------------------ */
+
+static void wq_push(bcp_sock_world *w, sk_req *r)
+{
+    if (r->queued)
+        return;
+    sk_req **pp = &w->wq[2 * r->src + r->ctl];
+    while (*pp)
+        pp = &(*pp)->wnext;
+    r->wnext = NULL;
+    *pp = r;
+    r->queued = 1;
+}
+
+static void wq_remove(bcp_sock_world *w, sk_req *r)
+{
+    if (!r->queued)
+        return;
+    for (sk_req **pp = &w->wq[2 * r->src + r->ctl]; *pp; pp = &(*pp)->wnext)
+        if (*pp == r) {
+            *pp = r->wnext;
+            break;
+        }
+    r->wnext = NULL;
+    r->queued = 0;
+}
+
+/* r changed (completed, or its peer failed): its owner looks again. */
+static void wake_req(bcp_sock_world *w, sk_req *r)
+{
+    wq_remove(w, r);
+    pthread_cond_signal(&r->cv);
+}
+
+/* Every waiter of peer s (its sockets failed). */
+static void wake_peer(bcp_sock_world *w, int s)
+{
+    for (int c = 0; c < 2; c++)
+        while (w->wq[2 * s + c])
+            wake_req(w, w->wq[2 * s + c]);
+}
+
 /* One frame {magic, tag, len} + payload to peer, under its send lock. */
 static int send_frame(bcp_sock_world *w, int peer, uint32_t magic, int tag, uint64_t len, const void *pl,
                       size_t pn)
@@ -591,6 +641,7 @@ static int read_ctl_one(bcp_sock_world *w, int src)
         r->cts_cap = f.pl[1];
         r->status = 0;
         r->done = 1;
+        wake_req(w, r);
     }
     pthread_mutex_unlock(&w->mu);
     return r ? 0 : -EPROTO;
@@ -654,6 +705,7 @@ static int read_control(bcp_sock_world *w, int src, const frame_hdr *h)
             r->received = n <= r->cap ? (size_t)n : r->cap;
             r->status = n <= r->cap ? 0 : -EMSGSIZE;
             r->done = 1;
+            wake_req(w, r);
         }
         pthread_mutex_unlock(&w->mu);
         return r ? 0 : -EPROTO;
@@ -687,6 +739,7 @@ static int read_one(bcp_sock_world *w, int src)
         r->status = rc ? rc : (h.len <= r->cap ? 0 : -EMSGSIZE);
         r->busy = 0;
         r->done = 1;
+        wake_req(w, r);
         pthread_mutex_unlock(&w->mu);
         return rc;
     }
@@ -709,9 +762,10 @@ static int read_one(bcp_sock_world *w, int src)
     m->data = data;
     pthread_mutex_lock(&w->mu);
     /* a receive may have been posted while the payload came in */
-    if ((r = take_posted(w, src, h.tag)))
+    if ((r = take_posted(w, src, h.tag))) {
         deliver_msg(r, m);
-    else {
+        wake_req(w, r);
+    } else {
         if (w->unexp_tail)
             w->unexp_tail->next = m;
         else
@@ -739,7 +793,10 @@ static int progress_until(bcp_sock_world *w, sk_req *r)
         }
         int *rd = r->ctl ? &w->reading_ctl[s] : &w->reading[s];
         if (*rd || r->busy) {
-            pthread_cond_wait(&w->cv, &w->mu);
+            /* another thread reads the socket (or r's payload): sleep until
+             * r completes or the reading is handed over */
+            wq_push(w, r);
+            pthread_cond_wait(&r->cv, &w->mu);
             continue;
         }
         *rd = 1;
@@ -747,10 +804,15 @@ static int progress_until(bcp_sock_world *w, sk_req *r)
         int rc = r->ctl ? read_ctl_one(w, s) : read_one(w, s);
         pthread_mutex_lock(&w->mu);
         *rd = 0;
-        if (rc && rc != -EMSGSIZE && rc != -ENOMEM)
+        if (rc && rc != -EMSGSIZE && rc != -ENOMEM) {
             w->dead[s] = -rc;
-        pthread_cond_broadcast(&w->cv);
+            wake_peer(w, s);
+        } else if (r->done && w->wq[2 * s + r->ctl]) {
+            /* leaving: the oldest waiter left becomes the reader */
+            wake_req(w, w->wq[2 * s + r->ctl]);
+        }
     }
+    wq_remove(w, r);
     pthread_mutex_unlock(&w->mu);
     return r->status;
 }
@@ -782,6 +844,7 @@ static int sk_irecv(void *ctx, void *buf, size_t n, int src, int tag, void **req
     sk_req *r = calloc(1, sizeof(*r));
     if (!r)
         return -ENOMEM;
+    pthread_cond_init(&r->cv, NULL);
     r->src = src;
     r->tag = tag;
     r->buf = buf;
@@ -813,7 +876,7 @@ static int sk_irecv(void *ctx, void *buf, size_t n, int src, int tag, void **req
             pthread_mutex_lock(&w->mu);
             if (!w->dead[src])
                 w->dead[src] = crc < 0 ? -crc : EIO;
-            pthread_cond_broadcast(&w->cv);
+            wake_peer(w, src);
             pthread_mutex_unlock(&w->mu);
         }
     }
@@ -846,6 +909,7 @@ static int sk_send_fill(void *ctx, bcp_lb_fill_fn fill, void *fctx, size_t n, in
     sk_req *r = calloc(1, sizeof(*r));
     if (!r)
         return -ENOMEM;
+    pthread_cond_init(&r->cv, NULL);
     r->src = dst;
     r->tag = tag;
     r->ctl = 1;
@@ -857,12 +921,14 @@ static int sk_send_fill(void *ctx, bcp_lb_fill_fn fill, void *fctx, size_t n, in
         pthread_mutex_lock(&w->mu);
         drop_list(&w->cts_wait, r);
         pthread_mutex_unlock(&w->mu);
+        pthread_cond_destroy(&r->cv);
         free(r);
         return rc;
     }
     rc = progress_until(w, r);
     uint8_t *addr = (uint8_t *)(uintptr_t)r->cts_addr;
     const size_t cap = (size_t)r->cts_cap;
+    pthread_cond_destroy(&r->cv);
     free(r);
     if (rc)
         return rc;
@@ -909,6 +975,7 @@ static int sk_wait(void *ctx, void *req)
         return 0;
     sk_req *r = req;
     int st = progress_until(w, r);
+    pthread_cond_destroy(&r->cv);
     free(r);
     return st;
 }

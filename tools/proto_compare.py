@@ -78,17 +78,20 @@ def noop_hook():
 
 
 def cpu_now():
-    """(process CPU seconds over all threads, cgroup throttled periods, throttled us)."""
+    """(process CPU seconds over all threads, cgroup throttled periods, throttled us,
+    cgroup CPU seconds: every process of the container, rank processes included)."""
     ru = resource.getrusage(resource.RUSAGE_SELF)
     nr = us = 0
+    cg = None
     try:
         for ln in open("/sys/fs/cgroup/cpu.stat"):
             k, v = ln.split()
             nr = int(v) if k == "nr_throttled" else nr
             us = int(v) if k == "throttled_usec" else us
+            cg = int(v) / 1e6 if k == "usage_usec" else cg
     except OSError:
         pass
-    return ru.ru_utime + ru.ru_stime, nr, us
+    return ru.ru_utime + ru.ru_stime, nr, us, cg
 
 
 def fold_setup(fold, hooks):
@@ -145,7 +148,8 @@ def measure(name, folds, rounds, run_once, verify_fn, nbytes, hooks, extra=None,
                 st = run_once()
                 dt = time.perf_counter() - t0
                 c1 = cpu_now()
-                cpu[f].append((c1[0] - c0[0], c1[1] - c0[1], (c1[2] - c0[2]) / 1e3))
+                cpu[f].append((c1[0] - c0[0], c1[1] - c0[1], (c1[2] - c0[2]) / 1e3,
+                               c1[3] - c0[3] if c0[3] is not None else None))
                 w1, l1 = bcp.fold_stats()
                 pw1, pr1 = bcp.pipe_stats()
                 ph = bcp.phase_stats()
@@ -178,6 +182,8 @@ def measure(name, folds, rounds, run_once, verify_fn, nbytes, hooks, extra=None,
                     runs_s=[round(x, 4) for x in times[f]], cold_s=round(times[f][0], 4),
                     cpu_s_median=round(float(np.median([c[0] for c in cpu[f][1:]])), 4),
                     cores_busy_median=round(float(np.median([c[0] / t for c, t in zip(cpu[f][1:], times[f][1:])])), 2),
+                    cgroup_cpu_s_median=(round(float(np.median([c[3] for c in cpu[f][1:]])), 4)
+                                         if cpu[f][1][3] is not None else None),
                     throttled_periods=sum(c[1] for c in cpu[f][1:]),
                     throttled_ms_runs=[round(c[2], 1) for c in cpu[f]])
         if f.startswith("gpu_pipelined") and batching.get(f, {}).get("windows"):
@@ -227,6 +233,7 @@ def main():
     ap.add_argument("--fold-server", action="store_true",
                     help="ranks as threads, every GPU fold through a node fold server process on a socket "
                          "(bcp_fold_server_connect: an MPI job's shape)")
+    ap.add_argument("--no-gpu", action="store_true", help="CPU folds only (cpu_*, noop): no link probe, runs without a GPU")
     a = ap.parse_args()
     server = None
     if a.fold_server:  # before this process touches the GPU: the server is the only HIP context
@@ -273,7 +280,7 @@ def main():
     wl = a.workloads.split(",")
     import box_probe
     box = box_probe.cpu_info()
-    if not (a.procs or a.procs_cold or a.fold_server):  # those keep the GPU out of this process
+    if not (a.procs or a.procs_cold or a.fold_server or a.no_gpu):  # those keep the GPU out of this process
         box.update(box_probe.pcie_rates(bcp))
     emit(box=box, cpu_reference_fold=ref_name)
     tr = {"transport": "socketpair rank processes, pooled" if a.procs else
