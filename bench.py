@@ -1259,9 +1259,9 @@ def main():
         budget = (N == 8 and U == 8) or (a.mode == "gen" and ((5 <= N <= 7 and U == 8) or
                                                               (N in (9, 10, 11, 12, 16) and U == 4)))
         if budget:
-            form, g = ("gather", 1) if a.mode == "rebuild" else ("strided", 0)
+            form, gather = ("gather", 1) if a.mode == "rebuild" else ("strided", 0)
             kernel = "xor_stream_w<{N},{U},%s,wpe6>" % form
-            kernel_tag = "xor_stream_w<{N}, {U}, %d, 0, 6>" % g
+            kernel_tag = "xor_stream_w<{N}, {U}, %d, 0, 6>" % gather
         NS = N if (1 <= N <= 12 or N == 16) else 0  # widths without a specialisation run xor_stream<0, ...>
         kernel, kernel_tag = kernel.format(N=NS, U=U), kernel_tag.format(N=NS, U=U)
 
