@@ -1,0 +1,98 @@
+#!/usr/bin/env python3
+"""How fast can the GPU fold stripes that live in pinned HOST memory? (r05:
+the per-task protocol's GPU fold reaches 62-80 % of config 1's link ceiling.)
+
+The protocol's P role hands its window rows (pinned host memory, filled by
+the senders' reads) to bcp_xor_stripes_async, whose kernel reads them across
+PCIe in place and writes the parity into a pinned host block.  Here, over
+the same shape (3 sources x 512 KiB per stripe, config 1):
+  zero_copy   kernel reads host rows, writes host output (the protocol's fold)
+  dma         hipMemcpyAsync rows H2D, kernel in HBM, output D2H, one queue
+for K stripes per launch and Q queues launching concurrently (the lanes),
+as GB/s of chunk bytes read (the link's H2D direction).  One JSON line per
+(mode, K, Q).
+
+  python tools/exp/zero_copy_probe.py
+"""
+import argparse
+import json
+import os
+import sys
+import threading
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.join(ROOT, "beegfs-chunk-parity_amd"))
+import bcp_ctypes as bcp  # noqa: E402
+
+KiB = 1024
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ks", default="1,4,16")
+    ap.add_argument("--qs", default="1,4,12")
+    ap.add_argument("--total-stripes", type=int, default=768)
+    ap.add_argument("--nsrc", type=int, default=3)
+    a = ap.parse_args()
+    C, N = 512 * KiB, a.nsrc
+    T = a.total_stripes
+    eng = bcp.Engine(0)
+    rows = eng.host_alloc(T * N * C)
+    outs = eng.host_alloc(T * C)
+    qmax = max(int(x) for x in a.qs.split(","))
+    kmax = max(int(x) for x in a.ks.split(","))
+    dev_rows = [eng.alloc(kmax * N * C) for _ in range(qmax)]
+    dev_out = [eng.alloc(kmax * C) for _ in range(qmax)]
+    queues = [eng.queue() for _ in range(qmax)]
+
+    def launch(q, qi, s0, k, mode):
+        if mode == "zero_copy":
+            q.xor_stripes([(outs + (s0 + i) * C, C, i * N, N, 0) for i in range(k)],
+                          [(rows + ((s0 + i) * N + j) * C, C) for i in range(k) for j in range(N)])
+        else:
+            q.h2d(dev_rows[qi], rows + s0 * N * C, k * N * C)
+            q.xor_stripes([(dev_out[qi] + i * C, C, i * N, N, 0) for i in range(k)],
+                          [(dev_rows[qi] + (i * N + j) * C, C) for i in range(k) for j in range(N)])
+            q.d2h(outs + s0 * C, dev_out[qi], k * C)
+
+    def run(mode, k, nq):
+        # each queue owns a contiguous range of stripes, k per launch, then one sync
+        per_q = T // nq // k * k
+
+        def worker(qi):
+            q = queues[qi]
+            base = qi * per_q
+            for s0 in range(base, base + per_q, k):
+                launch(q, qi, s0, k, mode)
+                q.sync()  # the protocol's P lane waits for every window
+
+        ths = [threading.Thread(target=worker, args=(i,)) for i in range(nq)]
+        t0 = time.perf_counter()
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join()
+        dt = time.perf_counter() - t0
+        return per_q * nq, dt
+
+    for mode in ("zero_copy", "dma"):
+        for k in (int(x) for x in a.ks.split(",")):
+            for nq in (int(x) for x in a.qs.split(",")):
+                run(mode, k, nq)  # warm
+                res = [run(mode, k, nq) for _ in range(3)]
+                st, dt = min(res, key=lambda x: x[1])
+                print(json.dumps({"mode": mode, "stripes_per_launch": k, "queues": nq, "stripes": st,
+                                  "best_s": round(dt, 4), "read_GBps": round(st * N * C / dt / 1e9, 2),
+                                  "read_plus_write_GiBps": round(st * (N + 1) * C / dt / 2 ** 30, 2)}), flush=True)
+    for q in queues:
+        q.close()
+    for p in dev_rows + dev_out:
+        eng.free(p)
+    eng.host_free(rows)
+    eng.host_free(outs)
+    eng.close()
+
+
+if __name__ == "__main__":
+    main()
