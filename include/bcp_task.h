@@ -255,9 +255,11 @@ int bcp_sock_world_destroy(bcp_sock_world *w);
 /* ---- loopback rank transport (replaces the MPI subset of §2) ----------- */
 /* A world of `world_size` ranks inside this process.  Every thread acting
  * for rank r calls bcp_lb_set_rank(r) first.  Semantics follow MPI
- * point-to-point: blocking send (rendezvous: returns once a receiver has the
+ * point-to-point: blocking send (up to 4 KiB buffered and returning at once,
+ * as an MPI eager send; larger ones rendezvous: return once a receiver has the
  * data), non-blocking send (eager copy), posted receives matched in order by
- * (source, tag), non-overtaking per (source, destination, tag). */
+ * (source, tag), non-overtaking per (source, destination, tag).  A program
+ * correct under MPI_Send's rules does not depend on which one happens. */
 typedef struct bcp_lb_req bcp_lb_req;
 int bcp_lb_init(int world_size);
 int bcp_lb_finalize(void);

@@ -102,6 +102,9 @@ def fuzz_rounds(bcp, oracle, tmp_path, budget, seed, engines):
                 st = bcp.pipeline_gen(root, ntargets, items, slab_bytes=int(rng.choice([1, 8, 64])) << 20,
                                       io_threads=int(rng.integers(1, 9)), nslots=int(rng.integers(2, 5)),
                                       read_mode=read_mode)
+            elif how == "procs":  # every rank its own process (socketpair transport), P roles fold pipelined
+                bcp.set_fold_mode(bcp.FOLD_PIPELINED)
+                st = bcp.gen_run_procs(root, ntargets, items, nlanes=int(rng.integers(1, 13)))
             else:
                 bcp.set_fold_mode(bcp.FOLD_PIPELINED if how == "pipelined" else bcp.FOLD_BATCHED)
                 st = bcp.gen_run(root, ntargets, items, nlanes=int(rng.integers(1, 13)))
@@ -125,9 +128,9 @@ def fuzz_rounds(bcp, oracle, tmp_path, budget, seed, engines):
                 rb = "pipeline"
             else:
                 bcp.set_rebuild_lanes(int(rng.integers(1, 5)))
-                st = bcp.rebuild_run(root, ntargets, victim, ordered)
+                st = (bcp.rebuild_run_procs if how == "procs" else bcp.rebuild_run)(root, ntargets, victim, ordered)
                 bcp.set_rebuild_lanes(1)
-                rb = "protocol"
+                rb = "procs" if how == "procs" else "protocol"
             assert st.errors == 0, (what, rb)
             for path, data in lost.items():
                 assert S.read_file(S.chunk_path(root, victim, path)) == data, (what, rb, path)
