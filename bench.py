@@ -476,6 +476,50 @@ def link_rates(device: int) -> dict:
     return out
 
 
+def zero_copy_fold_rate(device: int, lanes: int = 12, stripes: int = 768, nsrc: int = 3,
+                        chunk: int = 512 * KiB) -> dict:
+    """The config-1 protocol's GPU fold shape with nothing else: `lanes` queues
+    (threads), each launching one stripe of `nsrc` x `chunk` bytes that lives
+    in pinned HOST memory and waiting for it (bcp_xor_stripes_async reads the
+    rows in place across PCIe and writes the parity into pinned host memory,
+    as the P role's fold does).  Returns the chunk bytes read per second and
+    (read + written) GiB/s (tools/exp/zero_copy_probe.py has the sweep)."""
+    import threading
+    eng = bcp.Engine(device)
+    rows = eng.host_alloc(stripes * nsrc * chunk)
+    outs = eng.host_alloc(stripes * chunk)
+    qs = [eng.queue() for _ in range(lanes)]
+    per = stripes // lanes
+
+    def lane(i):
+        q = qs[i]
+        for s in range(i * per, (i + 1) * per):
+            q.xor_stripes([(outs + s * chunk, chunk, 0, nsrc, 0)],
+                          [(rows + (s * nsrc + j) * chunk, chunk) for j in range(nsrc)])
+            q.sync()
+
+    try:
+        best = None
+        for _ in range(3):
+            ths = [threading.Thread(target=lane, args=(i,)) for i in range(lanes)]
+            t0 = time.perf_counter()
+            for t in ths:
+                t.start()
+            for t in ths:
+                t.join()
+            dt = time.perf_counter() - t0
+            best = dt if best is None else min(best, dt)
+    finally:
+        for q in qs:
+            q.close()
+        eng.host_free(rows)
+        eng.host_free(outs)
+        eng.close()
+    n = per * lanes
+    return {"read_GBps": round(n * nsrc * chunk / best / 1e9, 2),
+            "GiBps": round(n * (nsrc + 1) * chunk / best / GiB, 2), "lanes": lanes, "stripes": n}
+
+
 def proc_cpu_s() -> float:
     import resource
     ru = resource.getrusage(resource.RUSAGE_SELF)
@@ -585,7 +629,7 @@ def config1_leg(a, device: int = 0) -> dict:
 
     legs = ["reference_fold", "gpu_fold", "pipeline"]
     pl_timing = {}
-    link = {}
+    link, zc = {}, {}
     gen_t = {x: [] for x in legs}
     reb_t = {x: [] for x in legs}
     gen_c = {x: [] for x in legs}  # this process's CPU seconds (all threads, user + system) per run
@@ -610,6 +654,7 @@ def config1_leg(a, device: int = 0) -> dict:
             list(ex.map(write_file, range(nfiles)))
         t_store = time.perf_counter() - t0
         link = link_rates(device)
+        zc = zero_copy_fold_rate(device)
         pl = bcp.Pipeline(device=device)
         runs = 1 + max(1, a.c1_reps)
         for r in range(runs):
@@ -688,6 +733,9 @@ def config1_leg(a, device: int = 0) -> dict:
         "link": link,
         "gpu_fold_link_ceiling_GiBps": (round((rd + wr) / (rd / (link["h2d_GBps"] * 1e9)) / GiB, 2)
                                         if link.get("h2d_GBps") else None),
+        # ... and what the device folds of rows in pinned host memory reach in the protocol's shape
+        # (12 lanes, one stripe per launch, read in place), the fold alone: the GPU fold's own bound
+        "gpu_fold_in_place_bound": zc,
         "bytes": {"gen_read": rd, "gen_written": wr, "rebuild_read": rb_rd, "rebuild_written": rb_wr},
         "cpu_quota": cpu_quota(),
         "cpu_note": "cpu_s: this process's CPU seconds (all threads, user + system, getrusage) per warm run, median; "

@@ -160,6 +160,7 @@ def test_bench_configs_block_one_rank(bcp):
     assert c1["gen"]["reference_fold"]["kind"] == "reference" and c1["rebuild"]["files"] == 72
     assert c1["bytes"]["gen_read"] == 96 * 3 * 512 * 1024
     assert c1["link"]["h2d_GBps"] > 0 and c1["gpu_fold_link_ceiling_GiBps"] > 0, c1
+    assert c1["gpu_fold_in_place_bound"]["GiBps"] > 0 and c1["gpu_fold_in_place_bound"]["lanes"] == 12, c1
     part = line["configs"]["config5_partial"]
     assert part["verified"] is True and part["plan_ok"] is True and part["GiBps"] > 0, part
     assert part["stripes"] == max(1, line["e2e"]["per_rank"][0]["stripes"] // 10)
