@@ -653,8 +653,12 @@ def config1_leg(a, device: int = 0) -> dict:
         with cf.ThreadPoolExecutor(8) as ex:
             list(ex.map(write_file, range(nfiles)))
         t_store = time.perf_counter() - t0
-        link = link_rates(device)
-        zc = zero_copy_fold_rate(device)
+        # diagnostics beside the legs: a failure here is reported, never costs the legs
+        try:
+            link = link_rates(device)
+            zc = zero_copy_fold_rate(device)
+        except Exception as e:
+            link, zc = {"error": f"{type(e).__name__}: {e}"}, {}
         pl = bcp.Pipeline(device=device)
         runs = 1 + max(1, a.c1_reps)
         for r in range(runs):

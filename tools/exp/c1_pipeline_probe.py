@@ -7,7 +7,9 @@ the pipeline at 0.75x the protocol with the reference's fold).
 Each setting: --rounds interleaved warm runs after one cold run; per run the
 wall time and bcp_pipeline_last_timing (stat, read_wait, slot_wait, submit,
 drain, batches).  Settings: io threads per pool half (io_threads), slots,
-slab size, and the protocol (GPU fold) beside them.  One JSON line each.
+slab size, the protocol (GPU fold), and `copies` (the same file reads and
+parity writes from 16 C threads, nothing else) beside them; CPU seconds per
+run.  One JSON line each.
 
   python tools/exp/c1_pipeline_probe.py --rounds 5
 """
@@ -15,6 +17,7 @@ import argparse
 import concurrent.futures as cf
 import json
 import os
+import resource
 import shutil
 import statistics
 import sys
@@ -63,6 +66,11 @@ def main():
             os.makedirs(os.path.join(root, f"st{k}", "parity"))
 
     settings = a.settings.split(",")
+    floor = None
+    if "copies" in settings:  # the kernel-copy floor of the same files (tools/exp/c1_cpu_cost.py)
+        sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+        import c1_cpu_cost
+        floor = c1_cpu_cost.copy_floor_lib()
     pls = {}
     for s in settings:
         kw = {}
@@ -72,26 +80,35 @@ def main():
             kw["nslots"] = int(s[5:])
         elif s.startswith("slab"):
             kw["slab_bytes"] = int(s[4:]) << 20
-        if s != "protocol":
+        if s not in ("protocol", "copies"):
             pls[s] = bcp.Pipeline(**kw)
     times = {s: [] for s in settings}
     timing = {s: [] for s in settings}
+    cpu = {s: [] for s in settings}  # (CPU seconds, voluntary context switches) per run
     for r in range(1 + a.rounds):
         for s in settings[r % len(settings):] + settings[:r % len(settings)]:
             reset()
+            ru0 = resource.getrusage(resource.RUSAGE_SELF)
             t0 = time.perf_counter()
             if s == "protocol":
                 st = bcp.gen_run(root, NT, items, nlanes=12)
+            elif s == "copies":
+                assert floor.c1_copies(root.encode(), a.files, NT, C, 16) == 0
+                st = None
             else:
                 st = pls[s].run(root, NT, items)
             times[s].append(time.perf_counter() - t0)
-            assert st.errors == 0
-            if s != "protocol":
+            ru1 = resource.getrusage(resource.RUSAGE_SELF)
+            cpu[s].append((ru1.ru_utime + ru1.ru_stime - ru0.ru_utime - ru0.ru_stime, ru1.ru_nvcsw - ru0.ru_nvcsw))
+            assert st is None or st.errors == 0
+            if s not in ("protocol", "copies"):
                 timing[s].append(pls[s].last_timing())
     for s in settings:
         warm = times[s][1:]
         med = statistics.median(warm)
         out = {"setting": s, "warm_median_s": round(med, 4), "GiBps": round((rd + wr) / med / GiB, 2),
+               "cpu_s": round(statistics.median(c[0] for c in cpu[s][1:]), 4),
+               "vol_ctxsw": int(statistics.median(c[1] for c in cpu[s][1:])),
                "runs_s": [round(x, 4) for x in times[s]]}
         if timing[s]:
             keys = ("stat", "read_wait", "slot_wait", "submit", "drain")
