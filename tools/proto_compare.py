@@ -183,7 +183,7 @@ def measure(name, folds, rounds, run_once, verify_fn, nbytes, hooks, extra=None,
                     cpu_s_median=round(float(np.median([c[0] for c in cpu[f][1:]])), 4),
                     cores_busy_median=round(float(np.median([c[0] / t for c, t in zip(cpu[f][1:], times[f][1:])])), 2),
                     cgroup_cpu_s_median=(round(float(np.median([c[3] for c in cpu[f][1:]])), 4)
-                                         if cpu[f][1][3] is not None else None),
+                                         if cpu[f][-1][3] is not None else None),
                     throttled_periods=sum(c[1] for c in cpu[f][1:]),
                     throttled_ms_runs=[round(c[2], 1) for c in cpu[f]])
         if f.startswith("gpu_pipelined") and batching.get(f, {}).get("windows"):
