@@ -30,7 +30,8 @@ int st2rank[MAX_STORAGE_TARGETS]; /* the caller's own, as gen/main.c:48 */
 
 #define NT 5      /* storage targets */
 #define NRANKS 16 /* world: ranks 10..14 are the targets, the rest idle */
-#define NLANES 3
+#define MAX_LANES 12
+static int NLANES = 3; /* lanes per rank; BCP_CALLER_LANES=1..12 (tools/tsan_host.sh runs 3 and 12) */
 #define NFILES 24
 
 #define CHECK(c)                                                           \
@@ -101,8 +102,8 @@ static void rank_main(bcp_sock_world *w, const char *root, int st, const worklis
     hs.write_dir = open(d, O_DIRECTORY | O_RDONLY);
     hs.read_parity_dir = -1;
     CHECK(hs.read_chunk_dir > 0 && hs.write_dir > 0);
-    pthread_t th[NLANES];
-    lane_params lp[NLANES];
+    pthread_t th[MAX_LANES];
+    lane_params lp[MAX_LANES];
     for (int l = 0; l < NLANES; l++) {
         lp[l] = (lane_params){&hs, wl, l, PROGRESS_SAMPLE_INIT};
         CHECK(pthread_create(&th[l], NULL, process_list, &lp[l]) == 0);
@@ -131,6 +132,9 @@ int main(int argc, char **argv)
           offsetof(HostState, log) == 48);
 
     const char *root = argv[1];
+    if (getenv("BCP_CALLER_LANES"))
+        NLANES = atoi(getenv("BCP_CALLER_LANES"));
+    CHECK(NLANES >= 1 && NLANES <= MAX_LANES);
     char d[4096];
     mkdir(root, 0700);
     for (int st = 0; st < NT; st++) {

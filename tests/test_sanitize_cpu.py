@@ -3,7 +3,7 @@ parity gen over 6 loopback ranks x 12 lanes and a rebuild (CPU test-double
 fold), a run where one rank's parity writes fail from many lanes at
 once (the sticky error is raised once, race-free; the reference writes it
 unlocked), and the C caller test with one forked process per
-rank on the socketpair transport (3 lanes per rank share its sockets).  Fails
+rank on the socketpair transport (3, then 12 lanes per rank share its sockets).  Fails
 on any TSan report."""
 import os
 import subprocess

@@ -38,3 +38,6 @@ gcc -fsanitize=thread -o $B/caller_test $B/caller.o $objs $P/build/bcp_kernels.o
 rm -rf /tmp/bcp_tsan_caller
 TSAN_OPTIONS="halt_on_error=1 second_deadlock_stack=1" $B/caller_test /tmp/bcp_tsan_caller
 rm -rf /tmp/bcp_tsan_caller
+# 12 lanes per rank: the socket readers hand over and wake per request
+BCP_CALLER_LANES=12 TSAN_OPTIONS="halt_on_error=1 second_deadlock_stack=1" $B/caller_test /tmp/bcp_tsan_caller
+rm -rf /tmp/bcp_tsan_caller
