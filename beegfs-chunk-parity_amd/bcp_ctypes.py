@@ -116,6 +116,13 @@ _SIGS = {
     "bcp_xor_stripes_async": ([_V, ctypes.POINTER(Stripe), ctypes.c_uint32, ctypes.POINTER(Source), ctypes.c_uint32],
                               ctypes.c_int),
     "bcp_xor_parity": ([_V, ctypes.c_size_t, _V, ctypes.c_int], ctypes.c_int),
+    "bcp_ring_create": ([_V, ctypes.c_int, ctypes.c_int, ctypes.POINTER(_V)], ctypes.c_int),
+    "bcp_ring_submit": ([_V, ctypes.POINTER(Stripe), ctypes.POINTER(Source), ctypes.POINTER(ctypes.c_uint64)],
+                        ctypes.c_int),
+    "bcp_ring_wait": ([_V, ctypes.c_uint64], ctypes.c_int),
+    "bcp_ring_query": ([_V, ctypes.c_uint64], ctypes.c_int),
+    "bcp_ring_destroy": ([_V], ctypes.c_int),
+    "bcp_ring_stats": ([_V, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)], ctypes.c_int),
     "bcp_dev_fill_synthetic_async": ([_V, _V, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64], ctypes.c_int),
     "bcp_dev_xor_fold_async": ([_V, _V, ctypes.c_uint64, _V], ctypes.c_int),
     "bcp_dev_compare_async": ([_V, _V, _V, ctypes.c_uint64, _V], ctypes.c_int),
@@ -133,6 +140,8 @@ _SIGS = {
     "bcp_task_pipe_stats": ([ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)], ctypes.c_int),
     "bcp_task_set_fold_inflight": ([ctypes.c_int], ctypes.c_int),
     "bcp_task_fold_stats": ([ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)], ctypes.c_int),
+    "bcp_task_set_fold_ring": ([ctypes.c_int], ctypes.c_int),
+    "bcp_task_ring_stats": ([ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)], ctypes.c_int),
     "bcp_task_inject_failure": ([ctypes.c_int, ctypes.c_int, ctypes.c_int], ctypes.c_int),
     "bcp_task_phase_stats": ([ctypes.POINTER(ctypes.c_double), ctypes.c_int, ctypes.c_int], ctypes.c_int),
     "bcp_task_set_transport": ([_V], ctypes.c_int),
@@ -401,6 +410,45 @@ class Queue:
     def close(self):
         if self.h:
             call("bcp_queue_destroy", self.h)
+            self.h = None
+
+
+class Ring:
+    """Resident fold ring (bcp_ring_create): one launch that folds stripes
+    published from any thread, no launch or sync per stripe."""
+
+    def __init__(self, eng: Engine, workers: int = 0, idle_us: int = 0):
+        h = _V()
+        call("bcp_ring_create", eng.h, workers, idle_us, ctypes.byref(h))
+        self.h = h
+        self.eng = eng
+
+    def submit(self, dst: int, out_len: int, sources) -> int:
+        """sources: list of (ptr, len); returns the handle."""
+        st = Stripe(dst, out_len, 0, len(sources), 0)
+        so = (Source * max(len(sources), 1))(*[Source(*s) for s in sources])
+        hnd = ctypes.c_uint64(0)
+        call("bcp_ring_submit", self.h, ctypes.byref(st), so, ctypes.byref(hnd))
+        return hnd.value
+
+    def wait(self, handle: int):
+        call("bcp_ring_wait", self.h, handle)
+
+    def query(self, handle: int) -> bool:
+        rc = lib().bcp_ring_query(self.h, handle)
+        if rc == -11:  # -EAGAIN
+            return False
+        check("bcp_ring_query", rc)
+        return True
+
+    def stats(self) -> tuple[int, int]:
+        p, n = ctypes.c_uint64(0), ctypes.c_uint64(0)
+        call("bcp_ring_stats", self.h, ctypes.byref(p), ctypes.byref(n))
+        return p.value, n.value
+
+    def close(self):
+        if self.h:
+            call("bcp_ring_destroy", self.h)
             self.h = None
 
 
@@ -788,6 +836,21 @@ def set_fold_inflight(k: int) -> int:
     if rc < 0:
         raise BcpError("bcp_task_set_fold_inflight", rc)
     return rc
+
+
+def set_fold_ring(on: bool) -> bool:
+    """PIPELINED folds through the device's resident fold ring (default on);
+    returns the previous setting."""
+    prev = lib().bcp_task_set_fold_ring(1 if on else 0)
+    check("bcp_task_set_fold_ring", min(prev, 0))
+    return bool(prev)
+
+
+def ring_stats() -> tuple[int, int]:
+    """(pieces published to the fold rings, launches of them) since start."""
+    p, n = ctypes.c_uint64(0), ctypes.c_uint64(0)
+    call("bcp_task_ring_stats", ctypes.byref(p), ctypes.byref(n))
+    return p.value, n.value
 
 
 def fold_stats() -> tuple[int, int]:

@@ -1090,6 +1090,277 @@ extern "C" int bcp_xor_uniform_async(bcp_queue *q, void *dst, const void *src, u
 }
 
 // ---------------------------------------------------------------------------
+// resident fold ring (RingArgs in bcp_internal.h, kernel fold_ring)
+// ---------------------------------------------------------------------------
+namespace {
+constexpr uint32_t kRingEntries = 512;        // tickets in flight (12 lanes x 4 ranks x <= 5 ranges fit)
+constexpr unsigned long long kRingLive = ~0ull;  // RingCtl::closed while a launch is live
+constexpr uint64_t kRingMaxPieces = 255;      // a handle carries the piece count in 8 bits
+}  // namespace
+
+struct bcp_ring {
+  bcp_engine *eng = nullptr;
+  hipStream_t stream = nullptr;
+  hipEvent_t ended = nullptr;     // recorded after each launch
+  bool launched = false;
+  RingEntry *host = nullptr;      // [K] pinned, coherent
+  RingCtl *ctl = nullptr;         // pinned, coherent: closed, stop, done[]
+  unsigned long long *done = nullptr;
+  char *dev = nullptr;            // RingState | cnt[K] | copy[K]
+  int workers = 64;
+  unsigned long long idle_ticks = 0, hard_ticks = 0;
+  pthread_mutex_t mu = PTHREAD_MUTEX_INITIALIZER;  // publication and launches
+  uint64_t next = 0;              // next ticket
+  std::atomic<int> broken{0};
+  std::atomic<uint64_t> launches{0};
+};
+
+static size_t ring_dev_bytes() {
+  return sizeof(RingState) + kRingEntries * sizeof(unsigned long long) + kRingEntries * sizeof(RingEntry);
+}
+
+static unsigned long long ring_load(const unsigned long long *p) { return __atomic_load_n(p, __ATOMIC_ACQUIRE); }
+
+static void ring_free(bcp_ring *r) {
+  if (r->ended) (void)hipEventDestroy(r->ended);
+  if (r->stream) (void)hipStreamDestroy(r->stream);
+  if (r->dev) (void)hipFree(r->dev);
+  if (r->host) (void)hipHostFree(r->host);
+  if (r->ctl) (void)hipHostFree(r->ctl);
+  pthread_mutex_destroy(&r->mu);
+  delete r;
+}
+
+extern "C" int bcp_ring_create(bcp_engine *eng, int workers, int idle_us, bcp_ring **out) {
+  if (!eng || !out || workers < 0 || workers > 4096 || idle_us < 0 || idle_us > 10000000) return -EINVAL;
+  *out = nullptr;
+  int rc = set_device(eng);
+  if (rc) return rc;
+  bcp_ring *r = new (std::nothrow) bcp_ring();
+  if (!r) return -ENOMEM;
+  r->eng = eng;
+  r->workers = workers ? workers : 64;
+  int khz = 0;  // s_memrealtime rate
+  if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, eng->device) != hipSuccess || khz <= 0)
+    khz = 100000;
+  const unsigned long long idle = idle_us ? (unsigned long long)idle_us : 5000ull;
+  r->idle_ticks = idle * (unsigned long long)khz / 1000ull;
+  r->hard_ticks = 4 * r->idle_ticks + 100ull * (unsigned long long)khz;  // + 100 ms
+  const size_t ctl_bytes = sizeof(RingCtl) + (size_t)kRingEntries * kRingDoneStride * sizeof(unsigned long long);
+  hipError_t e = hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&r->ended, hipEventDisableTiming);
+  if (e == hipSuccess)
+    e = hipHostMalloc((void **)&r->host, kRingEntries * sizeof(RingEntry), hipHostMallocMapped | hipHostMallocCoherent);
+  if (e == hipSuccess) e = hipHostMalloc((void **)&r->ctl, ctl_bytes, hipHostMallocMapped | hipHostMallocCoherent);
+  if (e == hipSuccess) e = hipMalloc((void **)&r->dev, ring_dev_bytes());
+  if (e == hipSuccess) e = hipMemsetAsync(r->dev, 0, ring_dev_bytes(), r->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(r->stream);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    ring_free(r);
+    return hip_to_errno(e);
+  }
+  memset(r->host, 0, kRingEntries * sizeof(RingEntry));
+  memset(r->ctl, 0, ctl_bytes);
+  r->done = (unsigned long long *)(r->ctl + 1);
+  __atomic_store_n(&r->ctl->closed, 0ull, __ATOMIC_RELEASE);  // no launch yet; the first starts at ticket 0
+  *out = r;
+  return 0;
+}
+
+// Under r->mu: make sure a launch will take the tickets published so far.  A
+// closed launch (the watcher wrote the first ticket it did not take) is
+// drained, then a new one starts from that ticket.  Tickets below it were
+// all folded; none at or above it was touched (fold_ring), so nothing is
+// folded twice.
+static int ring_live_locked(bcp_ring *r) {
+  const unsigned long long c = ring_load(&r->ctl->closed);
+  if (c == kRingLive) return 0;
+  if (r->broken.load(std::memory_order_relaxed)) return -EIO;
+  int rc = set_device(r->eng);
+  if (rc) return rc;
+  hipError_t e = hipSuccess;
+  if (r->launched) e = hipEventSynchronize(r->ended);  // the closed launch drains within microseconds
+  __atomic_store_n(&r->ctl->closed, kRingLive, __ATOMIC_RELEASE);
+  if (e == hipSuccess) e = hipMemsetAsync(r->dev, 0, sizeof(RingState), r->stream);
+  if (e == hipSuccess) {
+    RingArgs a;
+    a.host = r->host;
+    a.done = r->done;
+    a.closed = &r->ctl->closed;
+    a.stop = &r->ctl->stop;
+    a.state = (RingState *)r->dev;
+    a.cnt = (unsigned long long *)(r->dev + sizeof(RingState));
+    a.copy = (RingEntry *)(r->dev + sizeof(RingState) + kRingEntries * sizeof(unsigned long long));
+    a.base = c;
+    a.idle_ticks = r->idle_ticks;
+    a.hard_ticks = r->hard_ticks;
+    a.kmask = kRingEntries - 1;
+    a.kshift = (uint32_t)__builtin_ctz(kRingEntries);
+    (void)hipGetLastError();
+    e = launch_fold_ring(r->stream, r->workers, a);
+  }
+  if (e == hipSuccess) e = hipEventRecord(r->ended, r->stream);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    r->broken.store(1, std::memory_order_relaxed);
+    __atomic_store_n(&r->ctl->closed, c, __ATOMIC_RELEASE);  // no launch: waiters see it and fail
+    return hip_to_errno(e);
+  }
+  r->launched = true;
+  r->launches.fetch_add(1, std::memory_order_relaxed);
+  return 0;
+}
+
+static inline void cpu_relax() { __builtin_ia32_pause(); }
+
+// Ticket t is folded (its done word reached t + 1: done words only grow).
+static bool ring_ticket_done(const bcp_ring *r, uint64_t t) {
+  return ring_load(&r->done[(size_t)(t & (kRingEntries - 1)) * kRingDoneStride]) >= t + 1;
+}
+
+// Wait for ticket t; relaunch when the live launch closed before taking it.
+// Spins with pause for a short while (a piece folds in tens of microseconds),
+// then yields the CPU between looks.
+static int ring_wait_ticket(bcp_ring *r, uint64_t t) {
+  for (uint32_t spin = 0;; spin++) {
+    if (ring_ticket_done(r, t)) return 0;
+    if (r->broken.load(std::memory_order_relaxed)) return -EIO;
+    if (ring_load(&r->ctl->closed) != kRingLive) {
+      pthread_mutex_lock(&r->mu);
+      const int rc = ring_live_locked(r);
+      pthread_mutex_unlock(&r->mu);
+      if (rc) return rc;
+      continue;
+    }
+    if ((spin & 4095u) == 4095u) {
+      // a launch that ended without closing (a fault) never completes t
+      pthread_mutex_lock(&r->mu);
+      const hipError_t q = r->launched ? hipEventQuery(r->ended) : hipErrorNotReady;
+      const bool dead = q != hipErrorNotReady && ring_load(&r->ctl->closed) == kRingLive && !ring_ticket_done(r, t);
+      if (q != hipSuccess && q != hipErrorNotReady) (void)hipGetLastError();
+      if (dead) r->broken.store(1, std::memory_order_relaxed);
+      pthread_mutex_unlock(&r->mu);
+      if (dead) return -EIO;
+    }
+    if (spin < 512) {
+      for (int i = 0; i < 16; i++) cpu_relax();
+    } else {
+      sched_yield();
+    }
+  }
+}
+
+extern "C" int bcp_ring_submit(bcp_ring *r, const bcp_stripe *stripe, const bcp_source *sources, uint64_t *handle) {
+  if (!r || !stripe || !handle || (stripe->nsrc && !sources)) return -EINVAL;
+  const bcp_stripe s = *stripe;
+  if (s.window != 0 || s.nsrc > BCP_MAX_SOURCES || (s.out_len && !s.dst)) return -EINVAL;
+  for (uint32_t k = 0; k < s.nsrc; k++)
+    if (sources[k].len && !sources[k].ptr) return -EINVAL;
+  const uint64_t pieces = (s.out_len + kRingPieceMax - 1) / kRingPieceMax;
+  if (pieces > kRingMaxPieces) return -EINVAL;
+  *handle = 0;
+  if (!pieces) return 0;
+  // Reserve the tickets; each is then this caller's alone.  The watcher takes
+  // tickets in order, so a later caller's published tickets wait for ours.
+  pthread_mutex_lock(&r->mu);
+  if (r->broken.load(std::memory_order_relaxed)) {
+    pthread_mutex_unlock(&r->mu);
+    return -EIO;
+  }
+  const uint64_t first = r->next;
+  r->next += pieces;
+  pthread_mutex_unlock(&r->mu);
+  int rc = 0;
+  for (uint64_t i = 0; i < pieces && !rc; i++) {
+    const uint64_t t = first + i;
+    RingEntry *E = r->host + (t & (kRingEntries - 1));
+    // the entry's previous ticket must be folded before it is reused (it
+    // is earlier in ticket order, so it never waits for ours)
+    if (t >= kRingEntries && (rc = ring_wait_ticket(r, t - kRingEntries))) break;
+    const uint64_t p0 = i * kRingPieceMax;
+    const uint64_t plen = std::min<uint64_t>(kRingPieceMax, s.out_len - p0);
+    E->dst = s.dst + p0;
+    E->out_len = plen;
+    E->nsrc = s.nsrc;
+    for (uint32_t k = 0; k < s.nsrc; k++) {
+      const uint64_t len = sources[k].len > p0 ? std::min<uint64_t>(sources[k].len - p0, plen) : 0;
+      E->src[k].ptr = len ? sources[k].ptr + p0 : 0;
+      E->src[k].len = len;
+    }
+    __atomic_store_n(&E->seq, (unsigned long long)(t + 1), __ATOMIC_RELEASE);
+  }
+  if (rc) {
+    // reserved tickets that were never published would stall every later
+    // one: the ring is unusable from here on
+    r->broken.store(1, std::memory_order_relaxed);
+    return rc;
+  }
+  if (ring_load(&r->ctl->closed) != kRingLive) {
+    // no live launch (or it just closed): start one.  A launch that closes
+    // after this look is caught by the waiters (ring_wait_ticket).
+    pthread_mutex_lock(&r->mu);
+    rc = ring_live_locked(r);
+    pthread_mutex_unlock(&r->mu);
+    if (rc) return rc;
+  }
+  *handle = (first << 8) | pieces;
+  return 0;
+}
+
+extern "C" int bcp_ring_wait(bcp_ring *r, uint64_t handle) {
+  if (!r) return -EINVAL;
+  const uint64_t first = handle >> 8, n = handle & 0xFF;
+  for (uint64_t t = first; t < first + n; t++) {
+    const int rc = ring_wait_ticket(r, t);
+    if (rc) return rc;
+  }
+  return 0;
+}
+
+extern "C" int bcp_ring_query(bcp_ring *r, uint64_t handle) {
+  if (!r) return -EINVAL;
+  const uint64_t first = handle >> 8, n = handle & 0xFF;
+  for (uint64_t t = first; t < first + n; t++)
+    if (!ring_ticket_done(r, t)) {
+      if (r->broken.load(std::memory_order_relaxed)) return -EIO;
+      if (ring_load(&r->ctl->closed) != kRingLive) {
+        pthread_mutex_lock(&r->mu);
+        const int rc = ring_live_locked(r);
+        pthread_mutex_unlock(&r->mu);
+        if (rc) return rc;
+      }
+      return -EAGAIN;
+    }
+  return 0;
+}
+
+extern "C" int bcp_ring_stats(bcp_ring *r, uint64_t *pieces, uint64_t *launches) {
+  if (!r) return -EINVAL;
+  pthread_mutex_lock(&r->mu);
+  if (pieces) *pieces = r->next;
+  pthread_mutex_unlock(&r->mu);
+  if (launches) *launches = r->launches.load(std::memory_order_relaxed);
+  return 0;
+}
+
+extern "C" int bcp_ring_destroy(bcp_ring *r) {
+  if (!r) return -EINVAL;
+  set_device(r->eng);
+  pthread_mutex_lock(&r->mu);
+  __atomic_store_n(&r->ctl->stop, 1u, __ATOMIC_RELEASE);
+  int rc = 0;
+  if (r->launched && hipEventSynchronize(r->ended) != hipSuccess) {
+    (void)hipGetLastError();
+    rc = -EIO;
+  }
+  pthread_mutex_unlock(&r->mu);
+  (void)hipStreamSynchronize(r->stream);
+  ring_free(r);
+  return rc;
+}
+
+// ---------------------------------------------------------------------------
 // verification / synthetic data
 // ---------------------------------------------------------------------------
 extern "C" int bcp_dev_fill_synthetic_async(bcp_queue *q, void *dst, uint64_t bytes, uint64_t seed,

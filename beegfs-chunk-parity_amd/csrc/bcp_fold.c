@@ -19,6 +19,12 @@
  *              the fold service.
  * Both read the rows in place over PCIe (pinned, device-mapped host memory;
  * data bytes only -- the zero padding of a gen window is the kernel's).
+ * Under PIPELINED the folds go to the device's resident fold ring
+ * (bcp_ring_*, default; bcp_task_set_fold_ring): every range and window is
+ * one publication into a launch that stays on the device, and the P lane
+ * waits for its own pieces -- no launch and no stream sync per window.  With
+ * the ring off, ranges launch on the P lane's queue and windows go to the
+ * fold service as before.
  *
  * Resources are pooled: rows and output blocks stay pinned from task to
  * task (and run to run in a rank pool); engines are per device.
@@ -84,6 +90,95 @@ bcp_engine *bcpf_any_engine(void)
         e = g_engines[d];
     pthread_mutex_unlock(&g_mu);
     return e;
+}
+
+/* ---- resident fold rings (one per device) ---------------------------------
+ * Made on first use, destroyed by bcp_task_shutdown.  Workers: 16 worker
+ * workgroups read host rows at the link's rate in the protocol's shape (3 x
+ * 512 KiB stripes, 4-12 lanes: 56.6-57.0 GB/s, against 46.1 for one launch
+ * per stripe and 47-48 with 64-128 workers; tools/exp/zero_copy_probe.py,
+ * profiles/r06/protocol/zc_ring_r6a.jsonl). */
+static bcp_ring *g_ring[BCPF_MAX_DEVICES];
+static int g_ring_rc[BCPF_MAX_DEVICES];
+static int g_fold_ring = 1;
+static uint64_t g_ring_pieces, g_ring_launches; /* of rings already destroyed */
+#define RING_WORKERS 16
+
+int bcp_task_set_fold_ring(int on)
+{
+    if (on != 0 && on != 1)
+        return -EINVAL;
+    pthread_mutex_lock(&g_mu);
+    const int prev = g_fold_ring;
+    g_fold_ring = on;
+    pthread_mutex_unlock(&g_mu);
+    return prev;
+}
+
+int bcpi_fold_ring(void)
+{
+    pthread_mutex_lock(&g_mu);
+    const int on = g_fold_ring;
+    pthread_mutex_unlock(&g_mu);
+    return on;
+}
+
+bcp_ring *bcpf_ring_for(int dev, bcp_engine *e)
+{
+    if (dev < 0 || dev >= BCPF_MAX_DEVICES || !e)
+        return NULL;
+    pthread_mutex_lock(&g_mu);
+    if (!g_ring[dev] && !g_ring_rc[dev])
+        g_ring_rc[dev] = bcp_ring_create(e, RING_WORKERS, 0, &g_ring[dev]);
+    bcp_ring *r = g_ring[dev];
+    pthread_mutex_unlock(&g_mu);
+    return r;
+}
+
+int bcp_task_ring_stats(uint64_t *pieces, uint64_t *launches)
+{
+    uint64_t p = 0, l = 0;
+    pthread_mutex_lock(&g_mu);
+    p = g_ring_pieces;
+    l = g_ring_launches;
+    for (int d = 0; d < BCPF_MAX_DEVICES; d++)
+        if (g_ring[d]) {
+            uint64_t a = 0, b = 0;
+            (void)bcp_ring_stats(g_ring[d], &a, &b);
+            p += a;
+            l += b;
+        }
+    pthread_mutex_unlock(&g_mu);
+    if (pieces)
+        *pieces = p;
+    if (launches)
+        *launches = l;
+    return 0;
+}
+
+/* One stripe through the ring: n rows at `pitch`, row j's first valid[j]
+ * bytes, into out[0, nbytes); returns once it is on the host. */
+static int ring_fold(bcp_ring *r, const uint8_t *rows, size_t pitch, const size_t *valid, size_t nbytes, int n,
+                     uint8_t *out)
+{
+    bcp_stripe st = {(uint64_t)(uintptr_t)out, nbytes, 0, (uint32_t)n, 0};
+    bcp_source so[MAX_STORAGE_TARGETS];
+    for (int j = 0; j < n; j++)
+        so[j] = (bcp_source){(uint64_t)(uintptr_t)(rows + (size_t)j * pitch), MIN_(valid[j], nbytes)};
+    uint64_t h = 0;
+    int rc = bcp_ring_submit(r, &st, so, &h);
+    return rc ? rc : bcp_ring_wait(r, h);
+}
+
+int bcpf_fold_device(int dev, bcp_engine *e, int use_ring, const uint8_t *rows, size_t pitch, const size_t *valid,
+                     size_t nbytes, int n, uint8_t *out)
+{
+    bcp_ring *r = use_ring ? bcpf_ring_for(dev, e) : NULL;
+    if (r)
+        return ring_fold(r, rows, pitch, valid, nbytes, n, out);
+    fold_svc *S = NULL;
+    int rc = bcpf_svc_get(dev, e, &S);
+    return rc ? rc : bcpf_fold_batched(S, rows, pitch, valid, nbytes, n, out);
 }
 
 /* ---- fold service ----------------------------------------------------------
@@ -437,8 +532,8 @@ int bcpf_res_acquire(int st, int use_gpu, size_t rows_bytes, size_t nbytes, uint
     return 0;
 }
 
-int bcpf_fold_window(fold_res *R, HostState *hs, int tag, bcp_xor_hook_fn hook, void *ctx, const uint8_t *rows,
-                     size_t pitch, const size_t *valid, size_t nbytes, int n, uint8_t *out)
+int bcpf_fold_window(fold_res *R, HostState *hs, int tag, bcp_xor_hook_fn hook, void *ctx, int use_ring,
+                     const uint8_t *rows, size_t pitch, const size_t *valid, size_t nbytes, int n, uint8_t *out)
 {
     void *ab;
     size_t az;
@@ -454,9 +549,7 @@ int bcpf_fold_window(fold_res *R, HostState *hs, int tag, bcp_xor_hook_fn hook, 
         }
         return hook(out, nbytes, rows, pitch, n, ctx);
     }
-    fold_svc *S = NULL;
-    int rc = bcpf_svc_get(R->device, R->eng, &S);
-    return rc ? rc : bcpf_fold_batched(S, rows, pitch, valid, nbytes, n, out);
+    return bcpf_fold_device(R->device, R->eng, use_ring, rows, pitch, valid, nbytes, n, out);
 }
 
 /* ---- pipelined fold: row watches -------------------------------------------
@@ -564,7 +657,7 @@ row_watch *bcpf_watch_find(const void *row, int *j)
  * (under the test hook: the hook, at once, over whole rows whose padding the
  * P role zeroed before the receives).  Callers hold w->mu: the queue is one
  * lane's, and launches on it must not interleave. */
-static int launch_range(const row_watch *w, size_t lo, size_t hi)
+static int launch_range(row_watch *w, size_t lo, size_t hi)
 {
     __atomic_fetch_add(&g_pipe_ranges, 1, __ATOMIC_RELAXED);
     if (w->hook)
@@ -575,7 +668,22 @@ static int launch_range(const row_watch *w, size_t lo, size_t hi)
         const size_t len = w->valid[j] > lo ? MIN_(w->valid[j], hi) - lo : 0;
         so[j] = (bcp_source){(uint64_t)(uintptr_t)(w->rows + (size_t)j * w->pitch + lo), len};
     }
-    return bcp_xor_stripes_async(w->R->q, &st, 1, so, (uint32_t)w->n);
+    if (!w->ring)
+        return bcp_xor_stripes_async(w->R->q, &st, 1, so, (uint32_t)w->n);
+    if (w->nh == BCPF_WATCH_HANDLES) {
+        /* (ranges are at least a quarter window: never more than ~5) */
+        for (int i = 0; i < w->nh; i++) {
+            const int rc = bcp_ring_wait(w->ring, w->hnd[i]);
+            if (rc)
+                return rc;
+        }
+        w->nh = 0;
+    }
+    uint64_t h = 0;
+    const int rc = bcp_ring_submit(w->ring, &st, so, &h);
+    if (!rc)
+        w->hnd[w->nh++] = h;
+    return rc;
 }
 
 /* Under w->mu: launch every range all rows have delivered past w->lo. */
@@ -609,10 +717,12 @@ void bcpf_watch_publish(row_watch *w, int j, size_t bytes, int redo)
     pthread_mutex_unlock(&w->mu);
 }
 
-int bcpf_watch_rows(row_watch *W, fold_res *R, bcp_xor_hook_fn hook, void *hook_ctx, const uint8_t *rows,
-                    size_t pitch, const size_t *valid, int n, size_t nbytes, uint8_t *out)
+int bcpf_watch_rows(row_watch *W, fold_res *R, bcp_ring *ring, bcp_xor_hook_fn hook, void *hook_ctx,
+                    const uint8_t *rows, size_t pitch, const size_t *valid, int n, size_t nbytes, uint8_t *out)
 {
     pthread_mutex_init(&W->mu, NULL);
+    W->ring = hook ? NULL : ring;
+    W->nh = 0;
     memset(W->prog, 0, sizeof(W->prog));
     W->redo = W->err = 0;
     W->R = R;
@@ -648,8 +758,17 @@ int bcpf_finish_rows(row_watch *W, int fold)
     __atomic_fetch_add(&g_pipe_windows, 1, __ATOMIC_RELAXED);
     if (fold && !rc && lo < W->nbytes)
         rc = launch_range(W, lo, W->nbytes);
-    /* the one sync -- also after an error: ranges may be in flight */
-    const int src = W->hook ? 0 : bcp_queue_sync(W->R->q);
+    /* the one wait -- also after an error: ranges may be in flight */
+    int src = 0;
+    if (W->ring) {
+        for (int i = 0; i < W->nh; i++) {
+            const int e = bcp_ring_wait(W->ring, W->hnd[i]);
+            src = src ? src : e;
+        }
+        W->nh = 0;
+    } else if (!W->hook) {
+        src = bcp_queue_sync(W->R->q);
+    }
     pthread_mutex_destroy(&W->mu);
     return rc ? rc : src;
 }
@@ -672,9 +791,24 @@ int bcp_task_shutdown(void)
     }
     fold_res *R = g_pool;
     g_pool = NULL;
+    bcp_ring *ring[BCPF_MAX_DEVICES];
+    for (int d = 0; d < BCPF_MAX_DEVICES; d++) {
+        ring[d] = g_ring[d];
+        g_ring[d] = NULL;
+        g_ring_rc[d] = 0;
+        if (ring[d]) {
+            uint64_t a = 0, b = 0;
+            (void)bcp_ring_stats(ring[d], &a, &b);
+            g_ring_pieces += a;
+            g_ring_launches += b;
+        }
+    }
     pthread_mutex_unlock(&g_mu);
     for (int d = 0; d < BCPF_MAX_DEVICES; d++)
         svc_destroy(svc[d]);
+    for (int d = 0; d < BCPF_MAX_DEVICES; d++)
+        if (ring[d])
+            (void)bcp_ring_destroy(ring[d]); /* every lane has returned: nothing pending */
     while (R) {
         fold_res *nx = R->next;
         res_destroy(R);

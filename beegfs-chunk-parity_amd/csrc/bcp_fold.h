@@ -29,6 +29,14 @@ int bcpf_engine_for_target(int st, bcp_engine **out, int *device);
 /* Any live engine (for unregistering host memory), or NULL. */
 bcp_engine *bcpf_any_engine(void);
 
+/* ---- resident fold rings (bcp_ring_*, one per device) ----------------------- */
+/* The device's ring (made on first use), or NULL if it cannot be made. */
+bcp_ring *bcpf_ring_for(int dev, bcp_engine *e);
+/* One window's fold on device dev: through its ring when use_ring (and the
+ * ring exists), else the fold service; returns once it is on the host. */
+int bcpf_fold_device(int dev, bcp_engine *e, int use_ring, const uint8_t *rows, size_t pitch, const size_t *valid,
+                     size_t nbytes, int n, uint8_t *out);
+
 /* ---- fold service ----------------------------------------------------------- */
 typedef struct fold_svc fold_svc;
 int bcpf_svc_get(int dev, bcp_engine *e, fold_svc **out);
@@ -56,8 +64,8 @@ void bcpf_res_release(fold_res *R);
 /* One window's fold (replaces xor_parity at task_processing.c:211): by the
  * node fold server when the rows are in its arena, by the test hook when one
  * is set, else through the device's fold service.  tag: the lane's MPI tag. */
-int bcpf_fold_window(fold_res *R, HostState *hs, int tag, bcp_xor_hook_fn hook, void *ctx, const uint8_t *rows,
-                     size_t pitch, const size_t *valid, size_t nbytes, int n, uint8_t *out);
+int bcpf_fold_window(fold_res *R, HostState *hs, int tag, bcp_xor_hook_fn hook, void *ctx, int use_ring,
+                     const uint8_t *rows, size_t pitch, const size_t *valid, size_t nbytes, int n, uint8_t *out);
 
 /* ---- pipelined fold: row watches ------------------------------------------ */
 typedef struct row_watch {
@@ -74,15 +82,20 @@ typedef struct row_watch {
     uint8_t *out;
     size_t step; /* smallest range folded before the window is complete */
     int n;
+    bcp_ring *ring; /* ranges go to the resident fold ring (else R->q) */
+    uint64_t hnd[8];
+    int nh;
 } row_watch;
+#define BCPF_WATCH_HANDLES 8
 
 /* Bytes a source reads between two publishes of its row's final prefix. */
 #define BCPF_WATCH_PIECE ((size_t)256 << 10)
 
 /* Register the window's n rows (1), or 0 when the table is full (fold it
- * whole).  R->q must exist unless hook is set. */
-int bcpf_watch_rows(row_watch *W, fold_res *R, bcp_xor_hook_fn hook, void *hook_ctx, const uint8_t *rows,
-                    size_t pitch, const size_t *valid, int n, size_t nbytes, uint8_t *out);
+ * whole).  The ranges go to `ring` when it is given, else R->q must exist
+ * (unless hook is set). */
+int bcpf_watch_rows(row_watch *W, fold_res *R, bcp_ring *ring, bcp_xor_hook_fn hook, void *hook_ctx,
+                    const uint8_t *rows, size_t pitch, const size_t *valid, int n, size_t nbytes, uint8_t *out);
 /* After the receives: unregister, fold the rest (fold = 0: only wait for the
  * ranges in flight), sync once.  0 or the first error. */
 int bcpf_finish_rows(row_watch *W, int fold);

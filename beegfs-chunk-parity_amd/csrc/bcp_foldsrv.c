@@ -231,6 +231,16 @@ static void fs_map_put(fs_map *m)
     free(m);
 }
 
+/* The server folds through its device's resident ring when its own
+ * settings say so (PIPELINED with the ring on), else through the fold
+ * service. */
+static int srv_use_ring(void)
+{
+    bcpi_settings s;
+    bcpi_settings_get(&s);
+    return s.fold_mode == BCP_FOLD_PIPELINED && s.fold_ring;
+}
+
 static void fs_serve_conn(fs_conn *c)
 {
     const int fd = c->fd;
@@ -260,7 +270,6 @@ static void fs_serve_conn(fs_conn *c)
         q.rows_base += (uint64_t)c->delta;
         q.out_base += (uint64_t)c->delta;
         bcp_engine *e = NULL;
-        fold_svc *S = NULL;
         int dev = -1;
         bcp_xor_hook_fn hook = NULL;
         void *hctx = NULL;
@@ -275,9 +284,11 @@ static void fs_serve_conn(fs_conn *c)
                                (size_t)q.pitch, q.n, hctx)
                         : -ENOSYS;
         else if (!(r.rc = bcpf_engine_for_target(q.st, &e, &dev)) && !(r.rc = fs_register(e, q.rows_base, q.rows_size)) &&
-                 !(r.rc = fs_register(e, q.out_base, q.out_size)) && !(r.rc = bcpf_svc_get(dev, e, &S)))
-            r.rc = bcpf_fold_batched(S, (const uint8_t *)(uintptr_t)q.rows, (size_t)q.pitch, valid, (size_t)q.nbytes,
-                                     q.n, (uint8_t *)(uintptr_t)q.out);
+                 !(r.rc = fs_register(e, q.out_base, q.out_size)))
+            /* the server's own settings: the ring when PIPELINED with the
+             * ring on, else the fold service */
+            r.rc = bcpf_fold_device(dev, e, srv_use_ring(), (const uint8_t *)(uintptr_t)q.rows, (size_t)q.pitch, valid,
+                                    (size_t)q.nbytes, q.n, (uint8_t *)(uintptr_t)q.out);
         if (fs_io(fd, &r, sizeof(r), 1))
             break;
     }

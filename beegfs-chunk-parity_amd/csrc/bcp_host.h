@@ -15,7 +15,7 @@ int bcpi_hip_touched(void);
  * hook, window padding): a rank pool (bcp_pool.c) hands the caller's
  * settings to its rank processes with every run. */
 typedef struct {
-    int fold_mode, fold_inflight, explicit_pad;
+    int fold_mode, fold_inflight, explicit_pad, fold_ring;
     bcp_xor_hook_fn hook;
     void *hook_ctx;
 } bcpi_settings;
@@ -56,6 +56,8 @@ uint64_t bcpi_foldsrv_folds(void);
 int bcpi_sock_transport_is(const bcp_transport_ops *ops);
 /* The fold service's width (bcp_task_set_fold_inflight). */
 int bcpi_fold_inflight(void);
+/* PIPELINED folds through the resident fold ring (bcp_task_set_fold_ring). */
+int bcpi_fold_ring(void);
 /* Make [base, base + bytes) this process's arena slice (a memfd shared with
  * a node fold server, bcp_fold_server_connect). */
 void bcpi_arena_set(void *base, size_t bytes);

@@ -202,6 +202,70 @@ struct DescArgs {
     unsigned long long base;
 };
 
+// ---------------------------------------------------------------------------
+// Resident fold ring (bcp_ring_*, include/bcp.h).  One launch stays on the
+// device and folds stripes that callers publish into a ring of descriptors
+// in pinned host memory: no launch and no stream sync per stripe (the P
+// role's protocol folds one window at a time, task_processing.c:203-226).
+//   ticket  one piece of a stripe (<= kRingPieceMax output bytes), numbered
+//           from 0 in publication order; entry = ticket % K
+//   tile    1/kRingParts of a ticket's output (a multiple of 4 KiB, <= 32
+//           KiB), the unit a worker workgroup claims from the device cursor
+// Host: writes the entry, then seq = ticket + 1 (release).  Device: one
+// watcher wave polls seq in ticket order, copies the entry to HBM and
+// advances `pub`; workers claim tiles in order, fold those of tickets below
+// `pub`, and the last tile of a ticket writes done[entry] = ticket + 1 to host
+// memory.  After idle_ticks without a new ticket (or on stop) the watcher
+// writes the first ticket it did not take to *closed and the launch drains:
+// every ticket below it was folded, none at or above it was touched, and the
+// host relaunches from there (bcp_engine.hip, ring_live_locked).
+// ---------------------------------------------------------------------------
+constexpr int kRingParts = 16;
+constexpr uint64_t kRingPieceMax = (uint64_t)512 << 10;
+struct RingEntry {
+    unsigned long long seq;  // ticket + 1 once published (written last)
+    uint64_t dst;            // output of this piece
+    uint64_t out_len;        // <= kRingPieceMax
+    uint32_t nsrc, rsv0;
+    uint64_t rsv[4];
+    bcp_source src[BCP_MAX_SOURCES];  // offset to the piece, len clamped to it
+    uint64_t pad[8];
+};
+static_assert(sizeof(RingEntry) == 1024, "one 16-byte load per lane of one wave copies an entry");
+// Host-side control words the device writes or reads (pinned, coherent).
+struct RingCtl {
+    unsigned long long closed;  // first ticket the last launch did not take; ~0 while a launch is live
+    unsigned long long pad0[15];
+    unsigned int stop;          // host: drain and exit once idle
+    unsigned int pad1[31];
+    // then done[K * kRingDoneStride]
+};
+constexpr int kRingDoneStride = 8;  // one 64-byte line per entry's done word
+// Device-side state (HBM): claim cursor, announced tickets, quit flag, each
+// on its own 128-byte line; then cnt[K] (tiles folded per entry, monotone
+// over the ring's life) and the entries' copies.
+struct RingState {
+    unsigned long long cursor;  // tiles claimed in this launch
+    unsigned long long pad0[15];
+    unsigned long long pub;     // tickets announced (absolute; 0 at launch)
+    unsigned long long pad1[15];
+    unsigned int quit;          // the watcher closed this launch
+    unsigned int pad2[31];
+};
+struct RingArgs {
+    const RingEntry *host;           // [K] pinned host memory
+    unsigned long long *done;        // host, [K * kRingDoneStride]
+    unsigned long long *closed;      // host (RingCtl::closed)
+    const unsigned int *stop;        // host (RingCtl::stop)
+    RingState *state;                // HBM
+    unsigned long long *cnt;         // HBM [K]
+    RingEntry *copy;                 // HBM [K]
+    unsigned long long base;         // first ticket of this launch
+    unsigned long long idle_ticks;   // watcher: close after this long without a ticket (s_memrealtime ticks)
+    unsigned long long hard_ticks;   // worker: give up waiting after this long (no watcher)
+    uint32_t kmask, kshift;          // K - 1, log2 K
+};
+
 // Kernel launchers (bcp_kernels.hip).  All return hipError_t.
 // Streaming fold.  Consumes ceil(ntiles / grab) + grid counts of a.ctr; the
 // caller clamps grid to [1, ntiles].
@@ -214,6 +278,8 @@ hipError_t launch_desc_tiles(hipStream_t st, const DescBatch &b);
 hipError_t launch_xor_desc(hipStream_t st, int grid, int vecs, const DescBatch &b);
 // Small batch in the arguments; same work-queue accounting (ntiles + grid).
 hipError_t launch_xor_desc_args(hipStream_t st, int grid, int vecs, const DescArgs &a);
+// Resident fold ring: 1 watcher workgroup + `workers`.
+hipError_t launch_fold_ring(hipStream_t st, int workers, const RingArgs &a);
 hipError_t launch_fill_synthetic(hipStream_t st, int grid, char *dst,
                                  uint64_t bytes, uint64_t seed,
                                  uint64_t byte_offset);

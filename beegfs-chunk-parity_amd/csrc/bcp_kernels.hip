@@ -802,6 +802,176 @@ __global__ __launch_bounds__(kBlock) void desc_tiles(DescBatch b) {
 }
 
 // ---------------------------------------------------------------------------
+// Resident fold ring (RingArgs, bcp_internal.h).  Workgroup 0's first wave is
+// the watcher, every other workgroup a worker.  Exit conditions every wave
+// reaches: the watcher closes after idle_ticks without a new ticket or once
+// the host sets stop while nothing is pending; a worker leaves when the
+// watcher has closed and its claimed tile lies at or past the last announced
+// ticket, or after hard_ticks of waiting (no watcher: never in a healthy
+// launch, where the watcher's close comes first).
+// Memory ordering: host rows and the entry are read after a system-scope
+// acquire; a tile's stores go out behind every wave's vmcnt(0) wait, a
+// barrier and a system-scope release by lane 0 before it counts the tile;
+// the last tile of a ticket acquires and releases again before its done
+// word (system scope: the reader is the host).  The explicit vmcnt(0) after
+// each release fence keeps the flag behind the write-back whatever the
+// compiler proves about the scoreboard (MI355X_MICROARCH.md, compiler hazard).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ unsigned long long now_ticks() { return __builtin_amdgcn_s_memrealtime(); }
+
+__device__ __forceinline__ void ring_watch(const RingArgs &a) {
+  const uint32_t lane = threadIdx.x;  // one wave
+  unsigned long long pub = a.base;
+  unsigned long long last = now_ticks();
+  for (;;) {
+    const uint32_t e = (uint32_t)(pub & a.kmask);
+    const unsigned long long s = __hip_atomic_load(&a.host[e].seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (s == pub + 1) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // the entry's body, written before seq
+      const glob<v4u> *src = gp<v4u>((uint64_t)(uintptr_t)(a.host + e));
+      glob<v4u> *dst = gp<v4u>((uint64_t)(uintptr_t)(a.copy + e));
+      dst[lane] = src[lane];
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0) __hip_atomic_store(&a.state->pub, pub + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      pub++;
+      last = now_ticks();
+      continue;
+    }
+    if (__hip_atomic_load(a.stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) break;
+    if (now_ticks() - last > a.idle_ticks) break;
+    __builtin_amdgcn_s_sleep(4);
+  }
+  if (lane == 0) {
+    __hip_atomic_store(a.closed, pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // pub before quit
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(&a.state->quit, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// One tile: bytes [lo, lo + tb) of the ticket's piece, lane l owning vectors
+// l + 256 u (u < tb / 4 KiB <= 8).  Sources that cover the tile are folded
+// four at a time with every load first; a source ending inside it takes the
+// masked path (load_src_tail); zero padding is never read.
+__device__ __forceinline__ void ring_tile(const RingEntry &E, uint32_t part) {
+  const uint64_t out_len = E.out_len;
+  uint64_t tb = (out_len + kRingParts - 1) / kRingParts;
+  tb = (tb + 4095u) & ~(uint64_t)4095u;
+  const uint64_t lo = (uint64_t)part * tb;
+  if (lo >= out_len) return;
+  const uint32_t nv = (uint32_t)(tb >> 12);  // 1..8
+  const uint64_t hi = lo + tb;
+  const uint32_t nsrc = E.nsrc;
+  const uint32_t lane_off = threadIdx.x * 16u;
+  v4u acc[8];
+#pragma unroll
+  for (int u = 0; u < 8; u++) acc[u] = zero4();
+  for (uint32_t k0 = 0; k0 < nsrc; k0 += 4) {
+    v4u x[4][8];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const uint32_t k = k0 + i;
+      const bool full = k < nsrc && E.src[k].len >= hi;
+      gbyte *p = gp<const unsigned char>(full ? E.src[k].ptr + lo + lane_off : 0);
+#pragma unroll
+      for (int u = 0; u < 8; u++) x[i][u] = full && (uint32_t)u < nv ? ld16(p + u * 4096) : zero4();
+    }
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+#pragma unroll
+      for (int u = 0; u < 8; u++) acc[u] ^= x[i][u];
+  }
+  for (uint32_t k = 0; k < nsrc; k++) {
+    const uint64_t len = E.src[k].len;
+    if (len <= lo || len >= hi) continue;
+    gbyte *p = gp<const unsigned char>(E.src[k].ptr);
+#pragma unroll
+    for (int u = 0; u < 8; u++)
+      if ((uint32_t)u < nv) acc[u] ^= load_src_tail(p, len, lo + lane_off + u * 4096u);
+  }
+  glob<unsigned char> *d = gp<unsigned char>(E.dst);
+#pragma unroll
+  for (int u = 0; u < 8; u++)
+    if ((uint32_t)u < nv) store_tail(d, out_len, lo + lane_off + u * 4096u, acc[u]);
+}
+
+__device__ __forceinline__ void ring_work(const RingArgs &a) {
+  __shared__ unsigned long long s_g[2];
+  __shared__ int s_go[2];
+  __shared__ RingEntry s_e;
+  int slot = 0;
+  for (;;) {
+    if (threadIdx.x == 0) {
+      const unsigned long long g = atomicAdd(&a.state->cursor, 1ull);
+      const unsigned long long t = a.base + g / kRingParts;
+      const unsigned long long t0 = now_ticks();
+      int go = 1;
+      for (;;) {
+        if (t < __hip_atomic_load(&a.state->pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
+        if (__hip_atomic_load(&a.state->quit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+          // quit is stored after the last pub: one more look decides
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          go = t < __hip_atomic_load(&a.state->pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+        if (now_ticks() - t0 > a.hard_ticks) {
+          go = 0;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+      s_g[slot] = g;
+      s_go[slot] = go;
+    }
+    __syncthreads();
+    const int go = __builtin_amdgcn_readfirstlane(s_go[slot]);
+    const unsigned long long g = s_g[slot];
+    slot ^= 1;
+    if (!go) return;
+    const unsigned long long t = a.base + g / kRingParts;
+    const uint32_t part = (uint32_t)(g % kRingParts);
+    const uint32_t e = (uint32_t)(t & a.kmask);
+    // the entry's copy (HBM, written by the watcher) and the host rows: fresh
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    if (threadIdx.x < 64) {
+      const unsigned long long *q = (const unsigned long long *)(a.copy + e) + 2 * threadIdx.x;
+      unsigned long long *w = (unsigned long long *)&s_e + 2 * threadIdx.x;
+      w[0] = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      w[1] = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    ring_tile(s_e, part);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // every wave's stores done; s_e free for the next tile
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const unsigned long long use = t >> a.kshift;
+      const unsigned long long old =
+          __hip_atomic_fetch_add(&a.cnt[e], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (old == (use + 1) * kRingParts - 1) {
+        // the ticket's last tile: the other tiles' stores were released
+        // before their counts; order them before the done word
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(&a.done[(size_t)e * kRingDoneStride], t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void fold_ring(RingArgs a) {
+  if (blockIdx.x == 0) {
+    if (threadIdx.x < 64) ring_watch(a);
+    return;
+  }
+  ring_work(a);
+}
+
+// ---------------------------------------------------------------------------
 // Synthetic data: byte b of the stream = byte (b & 7) of splitmix64(seed + b/8)
 // (same stream as oracle_fill_synthetic).
 // ---------------------------------------------------------------------------
@@ -1016,6 +1186,12 @@ hipError_t launch_xor_desc_args(hipStream_t st, int grid, int vecs, const DescAr
     case 8: hipLaunchKernelGGL((xor_desc_args<8>), dim3(grid), dim3(kBlock), 0, st, a); break;
     default: hipLaunchKernelGGL((xor_desc_args<2>), dim3(grid), dim3(kBlock), 0, st, a); break;
   }
+  return hipGetLastError();
+}
+
+hipError_t launch_fold_ring(hipStream_t st, int workers, const RingArgs &a) {
+  if (workers < 1) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(fold_ring, dim3(1 + workers), dim3(kBlock), 0, st, a);
   return hipGetLastError();
 }
 

@@ -124,6 +124,7 @@ typedef struct {
     bcp_xor_hook_fn hook;
     void *hook_ctx;
     int fold_mode;
+    int fold_ring;    /* PIPELINED folds through the device's resident ring */
     int implicit_pad; /* sources may send a one-window gen chunk's bytes only */
 } task_settings;
 
@@ -148,6 +149,7 @@ static void settings_now(task_settings *s)
     const int pad = g_pad;
     pthread_mutex_unlock(&g_lock);
     s->implicit_pad = pad == BCP_PAD_AUTO ? own_transport(&s->T) : pad == 0;
+    s->fold_ring = s->fold_mode == BCP_FOLD_PIPELINED && bcpi_fold_ring();
 }
 
 /* ---- failure injection (tests) ------------------------------------------ */
@@ -525,7 +527,11 @@ static void parity_generator(const task_settings *ts, const char *path, const Fi
     const int remote_fold = !res_rc && L && L->device < 0 && remote && bcpi_arena_block(L->h_win[0], &rb_, &rz_);
     int pipelined = ts->fold_mode == BCP_FOLD_PIPELINED && !res_rc && expected_messages == 1 && T->send_fill &&
                     T->send_fill == bcp_lb_transport()->send_fill && !remote_fold;
-    if (pipelined && !hook && !L->q && bcp_queue_create(L->eng, &L->q))
+    /* the resident fold ring of the P role's device (PIPELINED; the fold
+     * service and lane queues otherwise) */
+    bcp_ring *const ring = ts->fold_ring && !res_rc && L && L->device >= 0 && !hook ? bcpf_ring_for(L->device, L->eng)
+                                                                                     : NULL;
+    if (pipelined && !hook && !ring && !L->q && bcp_queue_create(L->eng, &L->q))
         pipelined = 0;
     phase_add(BCP_PHASE_P_OPEN, &tph);
     if (res_rc) {
@@ -556,7 +562,7 @@ static void parity_generator(const task_settings *ts, const char *path, const Fi
                     if (valid[j] < buffer_size)
                         memset(win_a + (size_t)j * pitch + valid[j], 0, buffer_size - valid[j]);
             watched = pipelined && !have_had_error &&
-                      bcpf_watch_rows(&W, L, hook, hook_ctx, win_a, pitch, valid, n, buffer_size, pblk);
+                      bcpf_watch_rows(&W, L, ring, hook, hook_ctx, win_a, pitch, valid, n, buffer_size, pblk);
             trc = post_recvs(T, req, n, win_a, pitch, buffer_size, ranks, ti.tag);
             open_parity_chunk(hs, path, final_size, open_parity, &P_fd, &opened, &have_had_error,
                               ti.is_rebuilding ? NULL : chunk_sizes, n);
@@ -575,8 +581,8 @@ static void parity_generator(const task_settings *ts, const char *path, const Fi
         /* fold window msg_i on the GPU while the senders fill win_b */
         if (!have_had_error) {
             int frc = watched ? bcpf_finish_rows(&W, 1)
-                              : bcpf_fold_window(L, hs, ti.tag, hook, hook_ctx, win_a, pitch, valid, buffer_size, n,
-                                                 pblk);
+                              : bcpf_fold_window(L, hs, ti.tag, hook, hook_ctx, ring != NULL, win_a, pitch, valid,
+                                                 buffer_size, n, pblk);
             if (frc) {
                 have_had_error = EIO;
                 LOGERR("GPU fold of '%s' failed: %s\n", path, bcp_strerror(frc));
@@ -888,6 +894,7 @@ void bcpi_settings_get(bcpi_settings *s)
     s->explicit_pad = g_pad;
     pthread_mutex_unlock(&g_lock);
     s->fold_inflight = bcpi_fold_inflight();
+    s->fold_ring = bcpi_fold_ring();
 }
 
 int bcpi_settings_apply(const bcpi_settings *s)
@@ -895,6 +902,8 @@ int bcpi_settings_apply(const bcpi_settings *s)
     int rc = bcp_task_set_fold_mode(s->fold_mode);
     if (rc >= 0)
         rc = bcp_task_set_fold_inflight(s->fold_inflight);
+    if (rc >= 0)
+        rc = bcp_task_set_fold_ring(s->fold_ring);
     if (rc >= 0 && bcp_task_set_explicit_padding(s->explicit_pad) == -EINVAL) /* (returns BCP_PAD_AUTO = -1 too) */
         rc = -EINVAL;
     if (rc < 0)

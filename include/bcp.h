@@ -41,7 +41,9 @@
 extern "C" {
 #endif
 
-/* 3 (r05): the pipeline's MAP read mode (BCP_READ_MAP), its
+/* 4 (r06): the resident fold ring (bcp_ring_*) and the P role's fold
+ * through it (bcp_task.h, bcp_task_set_fold_ring) added.
+ * 3 (r05): the pipeline's MAP read mode (BCP_READ_MAP), its
  * bcp_pipeline_timing fields and bcp_host_register_dma_src removed.
  * 2 (r04): bcp_task.h's bcp_run_stats gained `refused`, bcp_pipeline_opts
  * `read_mode`, bcp_pipeline_timing the MAP fields; bcp_host_register_dma_src
@@ -49,7 +51,7 @@ extern "C" {
  * DEVICE_ROWS, bcp_dev_alloc_hostwrite and the engine keys they used were
  * removed, and the default window padding became BCP_PAD_AUTO
  * ("ABI history"). */
-#define BCP_ABI_VERSION 3
+#define BCP_ABI_VERSION 4
 #define BCP_MAX_SOURCES 56                  /* MAX_STORAGE_TARGETS, common.h:18 */
 #define BCP_WINDOW_BYTES (10u * 1024u * 1024u) /* FILE_TRANSFER_BUFFER_SIZE, task_processing.c:20 */
 
@@ -161,6 +163,44 @@ int bcp_xor_strided_async(bcp_queue *q, void *dst, uint64_t dst_stride,
 int bcp_xor_stripes_async(bcp_queue *q, const bcp_stripe *stripes,
                           uint32_t nstripes, const bcp_source *sources,
                           uint32_t nsources);
+
+/* ---- resident fold ring ------------------------------------------------ */
+/* One kernel launch that stays on the device and folds stripes published
+ * into a ring of descriptors in pinned host memory: no launch and no stream
+ * sync per stripe.  For callers that fold one small stripe at a time from
+ * many threads -- the P role's windows, task_processing.c:203-226, 12 lanes
+ * per rank (gen/main.c:821-889) -- where a launch + sync per window is the
+ * bound.  Same semantics as bcp_xor_stripes_async for one stripe with
+ * window 0 (sources and output anywhere the device can address: pinned
+ * mapped host memory or device memory; any alignment and length).
+ *
+ * The launch starts on the first submission and ends by itself after
+ * idle_us without one (it is relaunched on the next); bcp_ring_destroy ends
+ * it at once.  While it is live it holds 1 + `workers` workgroups of the
+ * device, and HIP calls that wait for the whole device (hipFree,
+ * hipHostUnregister, device synchronisation) wait until it idles out.
+ * A ring is thread-safe: any thread may submit and wait. */
+typedef struct bcp_ring bcp_ring;
+/* workers: worker workgroups (0 = default 64, at most 4096); idle_us: idle
+ * time before the launch ends (0 = default 5000, at most 10 s). */
+int bcp_ring_create(bcp_engine *eng, int workers, int idle_us, bcp_ring **out);
+/* Publish stripe (window must be 0; nsrc <= BCP_MAX_SOURCES; out_len <=
+ * 255 x 512 KiB) with its sources[0 .. nsrc) (stripe->first_src is ignored).
+ * Returns at once with a handle for bcp_ring_wait / _query; blocks only while
+ * the ring is full.  The caller keeps sources and output untouched until the
+ * handle completes. */
+int bcp_ring_submit(bcp_ring *r, const bcp_stripe *stripe, const bcp_source *sources, uint64_t *handle);
+/* Block until the stripe behind handle is folded and visible to the host;
+ * -EIO if the ring's launch failed. */
+int bcp_ring_wait(bcp_ring *r, uint64_t handle);
+/* 0 done, -EAGAIN pending, -EIO failed. */
+int bcp_ring_query(bcp_ring *r, uint64_t handle);
+/* Stops the launch (pending stripes are folded first) and frees the ring;
+ * every handle must have been waited for. */
+int bcp_ring_destroy(bcp_ring *r);
+/* Pieces published (a stripe is cut into 512 KiB pieces) and launches made
+ * since the ring was created. */
+int bcp_ring_stats(bcp_ring *r, uint64_t *pieces, uint64_t *launches);
 
 /* ---- drop-in for xor_parity (task_processing.c:96-109) ----------------- */
 /* Host pointers, synchronous, same contract as the reference: dst gets

@@ -112,8 +112,9 @@ int bcp_task_set_device_map(const int *devices, int ntargets);
  * transport's send_fill) reads its chunk in 256 KiB pieces and publishes
  * each final prefix; the source whose piece completes a byte range of every
  * row (at least 128 KiB and a quarter window) launches its fold on the lane's
- * queue (no sync), so the rows' PCIe reads overlap the file reads; after the
- * receives, the rest and one sync.  Windows it cannot follow (multi-window
+ * queue (no sync) -- or publishes it to the device's fold ring
+ * (bcp_task_set_fold_ring) -- so the rows' PCIe reads overlap the file
+ * reads; after the receives, the rest and one wait.  Windows it cannot follow (multi-window
  * tasks, other transports, folds by a node fold server) go to the fold
  * service as in BATCHED.
  * Returns the previous mode, or -EINVAL. */
@@ -154,6 +155,19 @@ int bcp_task_set_fold_inflight(int k);
 /* Fold-service counters since the last shutdown: windows
  * folded and launches issued (windows / launches = the batching achieved). */
 int bcp_task_fold_stats(uint64_t *windows, uint64_t *launches);
+/* PIPELINED folds through the device's resident fold ring (bcp_ring_*,
+ * include/bcp.h): 1 (default) -- every range fold and every whole-window fold
+ * of a PIPELINED P role (and of a node fold server) is one publication into a
+ * launch that stays on the device, and the lane waits for its own pieces:
+ * no launch and no stream sync per window; 0 -- range folds launch on the
+ * lane's queue and whole windows go to the fold service.  BATCHED mode
+ * always uses the fold service.  The ring of a device lives until
+ * bcp_task_shutdown; its launch ends by itself 5 ms after the last fold.
+ * Returns the previous value or -EINVAL. */
+int bcp_task_set_fold_ring(int on);
+/* Pieces (<= 512 KiB of parity each) published to the fold rings and
+ * launches of them since the process started. */
+int bcp_task_ring_stats(uint64_t *pieces, uint64_t *launches);
 /* Wall time spent per protocol phase, summed over every task of every lane
  * since the last reset (seconds[i] for i < nphases; the last two entries are
  * task COUNTS, not seconds).  Returns BCP_PHASES.  P role: size exchange,

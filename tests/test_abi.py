@@ -45,7 +45,7 @@ def test_library_exports_every_declared_symbol(bcp):
 
 
 def test_abi_version(bcp):
-    assert bcp.lib().bcp_abi_version() == 3
+    assert bcp.lib().bcp_abi_version() == 4
 
 
 def test_headers_compile_as_c_and_cxx(tmp_path):
@@ -79,6 +79,12 @@ def test_argument_validation_without_device(bcp):
     t = bcp.PipelineTiming()
     assert L.bcp_pipeline_last_timing(None, ctypes.byref(t)) == -errno.EINVAL
     assert L.bcp_pipeline_destroy(None) == -errno.EINVAL
+    r = ctypes.c_void_p()
+    assert L.bcp_ring_create(None, 0, 0, ctypes.byref(r)) == -errno.EINVAL
+    assert L.bcp_ring_wait(None, 0) == -errno.EINVAL
+    assert L.bcp_ring_query(None, 0) == -errno.EINVAL
+    assert L.bcp_ring_destroy(None) == -errno.EINVAL
+    assert L.bcp_ring_submit(None, None, None, None) == -errno.EINVAL
 
 
 def test_host_buffer_bounds_checked(bcp):

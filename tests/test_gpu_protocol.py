@@ -33,13 +33,22 @@ def read_path(request, monkeypatch):
     return request.param
 
 
-@pytest.fixture(params=["pipelined", "batched"])
+@pytest.fixture(params=["pipelined", "pipelined_queues", "batched"])
 def fold_mode(request, bcp):
-    """Both forms of the P role's GPU fold (bcp_task_set_fold_mode)."""
-    mode = {"batched": bcp.FOLD_BATCHED, "pipelined": bcp.FOLD_PIPELINED}[request.param]
+    """Every form of the P role's GPU fold (bcp_task_set_fold_mode): PIPELINED
+    through the device's resident fold ring (the default), PIPELINED with
+    range launches on the lanes' queues and the fold service for whole
+    windows (bcp_task_set_fold_ring(0)), BATCHED."""
+    mode = {"batched": bcp.FOLD_BATCHED, "pipelined": bcp.FOLD_PIPELINED,
+            "pipelined_queues": bcp.FOLD_PIPELINED}[request.param]
     prev = bcp.set_fold_mode(mode)
+    prev_ring = bcp.set_fold_ring(request.param != "pipelined_queues")
+    p0 = bcp.ring_stats()[0]
     yield request.param
+    used = bcp.ring_stats()[0] - p0
+    bcp.set_fold_ring(prev_ring)
     bcp.set_fold_mode(prev)
+    assert (used > 0) == (request.param == "pipelined"), (request.param, used)
 
 
 @pytest.mark.parametrize("name", ["KAT-2", "KAT-3", "KAT-4"])
@@ -106,6 +115,70 @@ def test_config1_shape_small(bcp, oracle, tmp_path):
     st = bcp.gen_run(root, 4, items)
     assert st.errors == 0 and st.tasks == 48 * 4
     for (path, holders, p, lens) in files:
+        assert S.read_file(S.parity_path(root, p, path)) == oracle.gen_parity_file(contents[path])
+
+
+def test_fold_ring_and_lane_queues_write_the_same_files(bcp, oracle, tmp_path):
+    """Config 1's shape through the resident fold ring and through the lane
+    queues: identical parity files and rebuilt chunks, every window of the
+    ring run published to the ring (one piece per range at least)."""
+    root = str(tmp_path)
+    files = []
+    for i in range(36):
+        p = i % 4
+        holders = [t for t in range(4) if t != p]
+        lens = [512 * KiB, 512 * KiB - 17 * (i % 3), 300 * KiB + i]
+        files.append((f"c1/f{i}", holders, p, lens))
+    items, contents = S.populate(root, 4, files, seed=21)
+    prev = bcp.set_fold_ring(True)
+    try:
+        results = {}
+        for ring in (True, False, True):
+            bcp.set_fold_ring(ring)
+            p0, _ = bcp.ring_stats()
+            st = bcp.gen_run(root, 4, items)
+            pieces = bcp.ring_stats()[0] - p0
+            assert st.errors == 0
+            assert (pieces >= len(files)) if ring else pieces == 0, (ring, pieces)
+            got = {path: S.read_file(S.parity_path(root, p, path)) for path, _, p, _ in files}
+            for path, _, p, _ in files:
+                assert got[path] == oracle.gen_parity_file(contents[path]), (ring, path)
+            results.setdefault(ring, got)
+            victim = 1
+            for path, holders, p, lens in files:
+                if victim in holders:
+                    os.remove(S.chunk_path(root, victim, path))
+            st = bcp.rebuild_run(root, 4, victim, items)
+            assert st.errors == 0
+            for path, holders, p, lens in files:
+                if victim in holders:
+                    k = holders.index(victim)
+                    assert S.read_file(S.chunk_path(root, victim, path)) == bytes(contents[path][k]), (ring, path)
+        assert results[True] == results[False]
+    finally:
+        bcp.set_fold_ring(prev)
+
+
+def test_fold_ring_idles_out_between_runs_and_shuts_down_live(bcp, oracle, tmp_path):
+    """The ring's launch ends 5 ms after the last fold and the next run
+    relaunches it; bcp_task_shutdown right after a run (launch still live)
+    stops it at once; the next run makes a new ring."""
+    import time
+    root = str(tmp_path)
+    files = [(f"r/f{i}", [t for t in range(5) if t != i % 5][:3], i % 5, [200 * KiB] * 3) for i in range(20)]
+    items, contents = S.populate(root, 5, files, seed=4)
+    _, l0 = bcp.ring_stats()
+    for _ in range(3):
+        assert bcp.gen_run(root, 5, items).errors == 0
+        time.sleep(0.05)
+    _, l1 = bcp.ring_stats()
+    assert l1 - l0 >= 3
+    assert bcp.gen_run(root, 5, items).errors == 0
+    t0 = time.perf_counter()
+    bcp.task_shutdown()  # the launch is live (idle limit 5 ms)
+    assert time.perf_counter() - t0 < 1.0
+    assert bcp.gen_run(root, 5, items).errors == 0
+    for path, holders, p, lens in files:
         assert S.read_file(S.parity_path(root, p, path)) == oracle.gen_parity_file(contents[path])
 
 

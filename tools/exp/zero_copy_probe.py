@@ -8,6 +8,8 @@ PCIe in place and writes the parity into a pinned host block.  Here, over
 the same shape (3 sources x 512 KiB per stripe, config 1):
   zero_copy   kernel reads host rows, writes host output (the protocol's fold)
   dma         hipMemcpyAsync rows H2D, kernel in HBM, output D2H, one queue
+  ring        (r06) the resident fold ring (bcp_ring_*): each lane publishes
+              its K stripes and waits for them, no launch and no stream sync
 for K stripes per launch and Q queues launching concurrently (the lanes),
 as GB/s of chunk bytes read (the link's H2D direction).  One JSON line per
 (mode, K, Q).
@@ -34,6 +36,8 @@ def main():
     ap.add_argument("--qs", default="1,4,12")
     ap.add_argument("--total-stripes", type=int, default=768)
     ap.add_argument("--nsrc", type=int, default=3)
+    ap.add_argument("--modes", default="zero_copy,dma,ring")
+    ap.add_argument("--ring-workers", default="64")
     a = ap.parse_args()
     C, N = 512 * KiB, a.nsrc
     T = a.total_stripes
@@ -45,8 +49,27 @@ def main():
     dev_rows = [eng.alloc(kmax * N * C) for _ in range(qmax)]
     dev_out = [eng.alloc(kmax * C) for _ in range(qmax)]
     queues = [eng.queue() for _ in range(qmax)]
+    import ctypes
+    L = bcp.lib()
+    # ring submissions prebuilt (ctypes argument building is not what is measured)
+    ring_args = []
+    for s in range(T):
+        st = bcp.Stripe(outs + s * C, C, 0, N, 0)
+        so = (bcp.Source * N)(*[bcp.Source(rows + (s * N + j) * C, C) for j in range(N)])
+        ring_args.append((st, so))
+    ring = None
 
     def launch(q, qi, s0, k, mode):
+        if mode == "ring":
+            hs = []
+            for i in range(k):
+                st, so = ring_args[s0 + i]
+                h = ctypes.c_uint64(0)
+                bcp.check("bcp_ring_submit", L.bcp_ring_submit(ring.h, ctypes.byref(st), so, ctypes.byref(h)))
+                hs.append(h.value)
+            for h in hs:
+                bcp.check("bcp_ring_wait", L.bcp_ring_wait(ring.h, h))
+            return
         if mode == "zero_copy":
             q.xor_stripes([(outs + (s0 + i) * C, C, i * N, N, 0) for i in range(k)],
                           [(rows + ((s0 + i) * N + j) * C, C) for i in range(k) for j in range(N)])
@@ -65,7 +88,8 @@ def main():
             base = qi * per_q
             for s0 in range(base, base + per_q, k):
                 launch(q, qi, s0, k, mode)
-                q.sync()  # the protocol's P lane waits for every window
+                if mode != "ring":
+                    q.sync()  # the protocol's P lane waits for every window
 
         ths = [threading.Thread(target=worker, args=(i,)) for i in range(nq)]
         t0 = time.perf_counter()
@@ -76,15 +100,22 @@ def main():
         dt = time.perf_counter() - t0
         return per_q * nq, dt
 
-    for mode in ("zero_copy", "dma"):
-        for k in (int(x) for x in a.ks.split(",")):
+    for mode in a.modes.split(","):
+        for w in ([int(x) for x in a.ring_workers.split(",")] if mode == "ring" else [0]):
+          if mode == "ring":
+            if ring is not None:
+                ring.close()
+            ring = bcp.Ring(eng, workers=w)
+          for k in (int(x) for x in a.ks.split(",")):
             for nq in (int(x) for x in a.qs.split(",")):
                 run(mode, k, nq)  # warm
                 res = [run(mode, k, nq) for _ in range(3)]
                 st, dt = min(res, key=lambda x: x[1])
-                print(json.dumps({"mode": mode, "stripes_per_launch": k, "queues": nq, "stripes": st,
+                print(json.dumps({"mode": mode, "ring_workers": w, "stripes_per_launch": k, "queues": nq, "stripes": st,
                                   "best_s": round(dt, 4), "read_GBps": round(st * N * C / dt / 1e9, 2),
                                   "read_plus_write_GiBps": round(st * (N + 1) * C / dt / 2 ** 30, 2)}), flush=True)
+    if ring is not None:
+        ring.close()
     for q in queues:
         q.close()
     for p in dev_rows + dev_out:

@@ -5,7 +5,9 @@ interleaved in ONE run on ONE box:
   gpu_pipelined  BCP_FOLD_PIPELINED (default): the fold follows the senders'
                  reads -- each range all rows have delivered is folded (by
                  the source that completed it) while the rest is read; the P
-                 role folds the tail and syncs
+                 role folds the tail and waits.  Since r06 through the
+                 device's resident fold ring (= gpu_ring); gpu_queues: the
+                 same with range launches on the lanes' queues (ring off)
   gpu_batched[K] BCP_FOLD_BATCHED: the device's fold service batches the
                  pending windows of every lane into one launch (K batches in
                  flight, default 4)
@@ -106,9 +108,17 @@ def fold_setup(fold, hooks):
             bcp.set_fold_mode(prev)
             bcp.set_fold_inflight(prev_k)
         return restore
-    if fold == "gpu_pipelined":
+    if fold in ("gpu_pipelined", "gpu_ring", "gpu_queues"):
+        # gpu_ring / gpu_pipelined: PIPELINED through the resident fold ring
+        # (the default since r06); gpu_queues: range launches on the lanes'
+        # queues, whole windows by the fold service (bcp_task_set_fold_ring(0))
         prev = bcp.set_fold_mode(bcp.FOLD_PIPELINED)
-        return lambda: bcp.set_fold_mode(prev)
+        prev_ring = bcp.set_fold_ring(fold != "gpu_queues")
+
+        def restore_pipe():
+            bcp.set_fold_ring(prev_ring)
+            bcp.set_fold_mode(prev)
+        return restore_pipe
     if fold == "cpu_reference":
         prev = bcp.set_fold_mode(bcp.FOLD_BATCHED)  # the hook folds whole windows after every row arrived
         prev_pad = bcp.set_explicit_padding(True)  # the reference's wire
@@ -166,7 +176,7 @@ def measure(name, folds, rounds, run_once, verify_fn, nbytes, hooks, extra=None,
                 b = batching.setdefault(f, {"windows": 0, "launches": 0})
                 b["windows"] += w1 - w0
                 b["launches"] += l1 - l0
-            if f.startswith("gpu_pipelined") and r > 0:
+            if f in ("gpu_pipelined", "gpu_ring", "gpu_queues") and r > 0:
                 b = batching.setdefault(f, {"windows": 0, "launches": 0})
                 b["windows"] += pw1 - pw0
                 b["launches"] += pr1 - pr0
@@ -186,7 +196,7 @@ def measure(name, folds, rounds, run_once, verify_fn, nbytes, hooks, extra=None,
                                          if cpu[f][-1][3] is not None else None),
                     throttled_periods=sum(c[1] for c in cpu[f][1:]),
                     throttled_ms_runs=[round(c[2], 1) for c in cpu[f]])
-        if f.startswith("gpu_pipelined") and batching.get(f, {}).get("windows"):
+        if f in ("gpu_pipelined", "gpu_ring", "gpu_queues") and batching.get(f, {}).get("windows"):
             line["range_folds_per_window"] = round(batching[f]["launches"] / batching[f]["windows"], 2)
         elif batching.get(f, {}).get("launches"):
             line["windows_per_launch"] = round(batching[f]["windows"] / batching[f]["launches"], 2)
