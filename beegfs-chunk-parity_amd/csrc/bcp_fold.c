@@ -161,12 +161,8 @@ int bcp_task_ring_stats(uint64_t *pieces, uint64_t *launches)
 static int ring_fold(bcp_ring *r, const uint8_t *rows, size_t pitch, const size_t *valid, size_t nbytes, int n,
                      uint8_t *out)
 {
-    bcp_stripe st = {(uint64_t)(uintptr_t)out, nbytes, 0, (uint32_t)n, 0};
-    bcp_source so[MAX_STORAGE_TARGETS];
-    for (int j = 0; j < n; j++)
-        so[j] = (bcp_source){(uint64_t)(uintptr_t)(rows + (size_t)j * pitch), MIN_(valid[j], nbytes)};
     uint64_t h = 0;
-    int rc = bcp_ring_submit(r, &st, so, &h);
+    int rc = bcpf_ring_submit_window(r, rows, pitch, valid, nbytes, n, out, &h);
     return rc ? rc : bcp_ring_wait(r, h);
 }
 
@@ -749,28 +745,77 @@ int bcpf_watch_rows(row_watch *W, fold_res *R, bcp_ring *ring, bcp_xor_hook_fn h
 /* (Writing the ranges folded so far while the last one folds, behind an
  * event the launching source records, measured slower on every workload --
  * config 5 by a quarter, r2bh / r2bi -- and is gone.) */
-int bcpf_finish_rows(row_watch *W, int fold)
+/* Wait for every range of W in the ring (0 or the first error). */
+static int ring_wait_all(row_watch *W)
+{
+    int rc = 0;
+    for (int i = 0; i < W->nh; i++) {
+        const int e = bcp_ring_wait(W->ring, W->hnd[i]);
+        rc = rc ? rc : e;
+    }
+    W->nh = 0;
+    return rc;
+}
+
+/* Unregister the rows and launch what is left to fold (fold = 0: nothing).
+ * A redo (a source replaced published bytes with zeros) refolds the whole
+ * window -- in the ring only after the ranges in flight have landed: ring
+ * pieces run side by side, so an earlier range could otherwise overwrite
+ * the refold's output with what it read before the zeros. */
+static int finish_launch(row_watch *W, int fold, int *wait_rc)
 {
     for (int j = 0; j < W->n; j++)
         watch_del(W->rows + (size_t)j * W->pitch);
     int rc = W->err;
     const size_t lo = W->redo ? 0 : W->lo;
     __atomic_fetch_add(&g_pipe_windows, 1, __ATOMIC_RELAXED);
+    *wait_rc = 0;
+    if (W->ring && W->redo)
+        *wait_rc = ring_wait_all(W);
     if (fold && !rc && lo < W->nbytes)
         rc = launch_range(W, lo, W->nbytes);
+    return rc;
+}
+
+int bcpf_finish_rows(row_watch *W, int fold)
+{
+    int wrc = 0;
+    const int rc = finish_launch(W, fold, &wrc);
     /* the one wait -- also after an error: ranges may be in flight */
-    int src = 0;
+    int src = wrc;
     if (W->ring) {
-        for (int i = 0; i < W->nh; i++) {
-            const int e = bcp_ring_wait(W->ring, W->hnd[i]);
-            src = src ? src : e;
-        }
-        W->nh = 0;
+        const int e = ring_wait_all(W);
+        src = src ? src : e;
     } else if (!W->hook) {
         src = bcp_queue_sync(W->R->q);
     }
     pthread_mutex_destroy(&W->mu);
     return rc ? rc : src;
+}
+
+int bcpf_finish_rows_submit(row_watch *W, uint64_t *hnd, int *nh)
+{
+    int wrc = 0;
+    int rc = finish_launch(W, 1, &wrc);
+    rc = rc ? rc : wrc;
+    if (rc) /* nothing is handed over: every range in flight lands first */
+        (void)ring_wait_all(W);
+    for (int i = 0; i < W->nh; i++)
+        hnd[i] = W->hnd[i];
+    *nh = W->nh;
+    W->nh = 0;
+    pthread_mutex_destroy(&W->mu);
+    return rc;
+}
+
+int bcpf_ring_submit_window(bcp_ring *r, const uint8_t *rows, size_t pitch, const size_t *valid, size_t nbytes,
+                            int n, uint8_t *out, uint64_t *hnd)
+{
+    bcp_stripe st = {(uint64_t)(uintptr_t)out, nbytes, 0, (uint32_t)n, 0};
+    bcp_source so[MAX_STORAGE_TARGETS];
+    for (int j = 0; j < n; j++)
+        so[j] = (bcp_source){(uint64_t)(uintptr_t)(rows + (size_t)j * pitch), MIN_(valid[j], nbytes)};
+    return bcp_ring_submit(r, &st, so, hnd);
 }
 
 /* ---- shutdown -------------------------------------------------------------- */

@@ -99,6 +99,15 @@ int bcpf_watch_rows(row_watch *W, fold_res *R, bcp_ring *ring, bcp_xor_hook_fn h
 /* After the receives: unregister, fold the rest (fold = 0: only wait for the
  * ranges in flight), sync once.  0 or the first error. */
 int bcpf_finish_rows(row_watch *W, int fold);
+/* The same for a ring watch, without waiting: the rest is published and the
+ * ring handles of every range in flight are handed to the caller (hnd has
+ * room for BCPF_WATCH_HANDLES + 1), who waits for them before the rows or
+ * the output are touched.  On an error every range has landed and nothing
+ * is handed over. */
+int bcpf_finish_rows_submit(row_watch *W, uint64_t *hnd, int *nh);
+/* One whole window into the ring without waiting (*hnd for bcp_ring_wait). */
+int bcpf_ring_submit_window(bcp_ring *r, const uint8_t *rows, size_t pitch, const size_t *valid, size_t nbytes,
+                            int n, uint8_t *out, uint64_t *hnd);
 /* The watch of the row being filled at `row` (row j of it), or NULL. */
 row_watch *bcpf_watch_find(const void *row, int *j);
 /* A source's new final prefix of row j; folds every range it completes. */

@@ -215,6 +215,9 @@ void *bcpr_gen_lane(void *p)
     if (!bcpr_gate_pass(a->gate))
         return NULL;
     bcp_lb_set_rank(a->rank);
+    /* a lane without a DB lets its P tasks' writes trail by one task (a DB
+     * entry must not precede its parity file) */
+    (void)bcp_task_set_lane_deferral(a->db == NULL);
     TaskInfo ti = {a->hs->read_chunk_dir, 0, -1, a->lane, &a->sample};
     for (size_t i = 0; i < a->nitems; i++) {
         if (a->lanes[i] != a->lane)
@@ -238,7 +241,8 @@ void *bcpr_gen_lane(void *p)
             a->tasks++;
         }
     }
-    bcp_task_thread_release();
+    bcp_task_thread_release(); /* (completes a deferred P task first) */
+    (void)bcp_task_set_lane_deferral(0);
     return NULL;
 }
 
@@ -418,6 +422,7 @@ void *bcpr_rebuild_rank(void *p)
     if (a->gate && !bcpr_gate_pass(a->gate))
         return NULL;
     bcp_lb_set_rank(a->rank);
+    (void)bcp_task_set_lane_deferral(1);
     const int my_st = a->hs->storage_target;
     const int victim = a->rebuild_target;
     const int nl = a->nlanes > 1 ? a->nlanes : 1;
@@ -442,7 +447,8 @@ void *bcpr_rebuild_rank(void *p)
             a->tasks++;
         }
     }
-    bcp_task_thread_release();
+    bcp_task_thread_release(); /* (completes a deferred P task first) */
+    (void)bcp_task_set_lane_deferral(0);
     return NULL;
 }
 

@@ -209,8 +209,89 @@ typedef struct {
 
 static __thread lane_res t_res;
 
+/* ---- deferred P-role completion (lane deferral) ---------------------------
+ * A lane that opted in (bcp_task_set_lane_deferral: libbcp's own runners,
+ * for lanes that keep no DB) lets a single-window P task return once its
+ * fold is published to the device's resident ring: the wait for the fold,
+ * the parity write, the rebuild's truncation and the file's close happen
+ * when this lane's next task has published its own fold or finished
+ * sending (or at bcp_task_flush / bcp_task_thread_release).  So a lane's
+ * next task overlaps the previous one's fold and write, as two buffers of
+ * parity_generator's own window loop overlap receive and fold
+ * (task_processing.c:203-226).  Same bytes, same files; an error of the
+ * deferred part becomes sticky when it completes. */
+typedef struct {
+    int active;
+    HostState *hs;
+    char *path;
+    fold_res *L;
+    bcp_ring *ring;
+    uint64_t hnd[BCPF_WATCH_HANDLES + 1];
+    int nh;
+    int fd;
+    uint8_t *pblk;
+    size_t wsize;
+    int rebuilding;
+    uint64_t final_size; /* rebuild: the rebuilt chunk's size */
+    uint64_t final_total;
+} deferred_p;
+
+static __thread deferred_p t_def;
+static __thread int t_defer_on;
+
+int bcp_task_set_lane_deferral(int on)
+{
+    if (on != 0 && on != 1)
+        return -EINVAL;
+    const int prev = t_defer_on;
+    t_defer_on = on;
+    return prev;
+}
+
+static int raise_sticky_error(HostState *hs, int err, const char *path);
+static uint64_t mono_ns(void);
+static void phase_add(int ph, uint64_t *t);
+
+static void deferred_complete(deferred_p *d)
+{
+    if (!d->active)
+        return;
+    d->active = 0;
+    HostState *hs = d->hs;
+    uint64_t tph = mono_ns();
+    int err = 0;
+    for (int i = 0; i < d->nh; i++) {
+        const int rc = bcp_ring_wait(d->ring, d->hnd[i]);
+        if (rc && !err) {
+            err = EIO;
+            LOGERR("GPU fold of '%s' failed: %s\n", d->path, bcp_strerror(rc));
+        }
+    }
+    if (!err) {
+        ssize_t wr = write(d->fd, d->pblk, d->wsize);
+        if (wr <= 0) {
+            err = errno;
+            LOGERR("write of '%s' failed with %d (%s) after %llu bytes\n", d->path, errno, strerror(errno),
+                   (unsigned long long)(d->final_total - d->wsize));
+        }
+    }
+    if (d->rebuilding && d->fd != hs->fd_null)
+        if (ftruncate(d->fd, (off_t)d->final_size) != 0 && !err)
+            err = errno;
+    if (err && raise_sticky_error(hs, err, d->path))
+        LOGERR("error on '%s' is now sticky for st %d\n", d->path, hs->storage_target);
+    bcpf_res_release(d->L);
+    if (d->fd != hs->fd_null)
+        close(d->fd);
+    free(d->path);
+    phase_add(BCP_PHASE_P_WRITE, &tph);
+}
+
+void bcp_task_flush(void) { deferred_complete(&t_def); }
+
 void bcp_task_thread_release(void)
 {
+    deferred_complete(&t_def);
     free(t_res.send_buf);
     t_res.send_buf = NULL;
     t_res.send_cap = 0;
@@ -547,6 +628,10 @@ static void parity_generator(const task_settings *ts, const char *path, const Fi
         open_parity_chunk(hs, path, final_size, open_parity, &P_fd, &opened, &have_had_error,
                           ti.is_rebuilding ? NULL : chunk_sizes, n);
 
+    /* lane deferral: a single-window task whose fold goes to the ring returns
+     * once the fold is published (deferred_p) */
+    const int defer = t_defer_on && ring && expected_messages == 1;
+    int deferred = 0;
     uint8_t *win_a = L ? L->h_win[0] : NULL, *win_b = L ? L->h_win[1] : NULL, *pblk = L ? L->h_par : NULL;
     for (int j = 0; j < n; j++)
         req[j] = NULL;
@@ -579,7 +664,43 @@ static void parity_generator(const task_settings *ts, const char *path, const Fi
             LOGERR("windows of '%s' not received: %s\n", path, strerror(have_had_error));
         }
         /* fold window msg_i on the GPU while the senders fill win_b */
-        if (!have_had_error) {
+        if (!have_had_error && defer) {
+            deferred_p d = {0};
+            int frc = watched ? bcpf_finish_rows_submit(&W, d.hnd, &d.nh)
+                              : bcpf_ring_submit_window(ring, win_a, pitch, valid, buffer_size, n, pblk, &d.hnd[d.nh++]);
+            if (frc) {
+                if (!watched)
+                    d.nh = 0; /* (a failed submission hands nothing over) */
+                have_had_error = EIO;
+                LOGERR("GPU fold of '%s' failed: %s\n", path, bcp_strerror(frc));
+            } else {
+                d.active = 1;
+                d.hs = hs;
+                d.path = strdup(path);
+                d.L = L;
+                d.ring = ring;
+                d.fd = P_fd;
+                d.pblk = pblk;
+                d.wsize = (size_t)MIN_((uint64_t)buffer_size, data_left);
+                d.rebuilding = ti.is_rebuilding;
+                d.final_size = final_parity_chunk_size;
+                d.final_total = final_size;
+                if (!d.path) { /* no memory for the record: complete it here */
+                    d.path = (char *)path;
+                    deferred_complete(&d);
+                    d.path = NULL;
+                } else {
+                    /* this fold is on the device: now the previous task's part */
+                    deferred_complete(&t_def);
+                    t_def = d;
+                }
+                deferred = 1;
+                if (ti.sample)
+                    ti.sample->bytes_written += buffer_size;
+                phase_add(BCP_PHASE_P_FOLD, &tph);
+                break;
+            }
+        } else if (!have_had_error) {
             int frc = watched ? bcpf_finish_rows(&W, 1)
                               : bcpf_fold_window(L, hs, ti.tag, hook, hook_ctx, ring != NULL, win_a, pitch, valid,
                                                  buffer_size, n, pblk);
@@ -609,6 +730,11 @@ static void parity_generator(const task_settings *ts, const char *path, const Fi
         win_b = t;
     }
 
+    if (deferred) {
+        /* the record owns the resources, the file and its error */
+        __atomic_fetch_add(&g_phase_ns[BCP_PHASE_P_TASKS], 1, __ATOMIC_RELAXED);
+        return;
+    }
     if (ti.is_rebuilding && P_fd != hs->fd_null)
         if (ftruncate(P_fd, (off_t)final_parity_chunk_size) != 0 && !have_had_error)
             have_had_error = errno;
@@ -858,6 +984,8 @@ done:
         close(fd);
     phase_add(BCP_PHASE_S_SEND, &tph);
     __atomic_fetch_add(&g_phase_ns[BCP_PHASE_S_TASKS], 1, __ATOMIC_RELAXED);
+    /* this lane's deferred P task (its fold had the sends' time to land) */
+    deferred_complete(&t_def);
 }
 
 int process_task(HostState *hs, const char *path, const FileInfo *fi, TaskInfo ti)

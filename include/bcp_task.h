@@ -168,6 +168,21 @@ int bcp_task_set_fold_ring(int on);
 /* Pieces (<= 512 KiB of parity each) published to the fold rings and
  * launches of them since the process started. */
 int bcp_task_ring_stats(uint64_t *pieces, uint64_t *launches);
+/* Lane deferral, for the CALLING THREAD (a lane): 1 -- a single-window P task
+ * whose fold goes to the fold ring returns once the fold is published; the
+ * wait for it, the parity write (the rebuild's truncation) and the close
+ * happen when this thread's next task has published its own fold or sent
+ * its windows, or at bcp_task_flush / bcp_task_thread_release.  The lane's
+ * next task then overlaps the previous one's fold and write.  Files, bytes
+ * and sticky errors are the same; an error of the deferred part becomes
+ * sticky when it completes.  0 (default): process_task returns with the
+ * parity written, as the reference's does.  libbcp's runners turn it on for
+ * lanes that write no DB entries (a DB entry must not precede its file).
+ * Returns the previous value or -EINVAL. */
+int bcp_task_set_lane_deferral(int on);
+/* Complete the calling thread's deferred P task, if any (a lane calls it
+ * before its list's end is reported: MPI barrier, DB sync, exit). */
+void bcp_task_flush(void);
 /* Wall time spent per protocol phase, summed over every task of every lane
  * since the last reset (seconds[i] for i < nphases; the last two entries are
  * task COUNTS, not seconds).  Returns BCP_PHASES.  P role: size exchange,

@@ -38,6 +38,10 @@ def main():
     ap.add_argument("--nsrc", type=int, default=3)
     ap.add_argument("--modes", default="zero_copy,dma,ring")
     ap.add_argument("--ring-workers", default="64")
+    ap.add_argument("--dirty", default="none",
+                    help="comma list of row states before each fold: none (rows untouched since the first fill), "
+                         "copy (each lane memcpy's its stripe's rows first, as the sources' read() does), "
+                         "copy_only (the copies alone, no fold: their own cost)")
     a = ap.parse_args()
     C, N = 512 * KiB, a.nsrc
     T = a.total_stripes
@@ -59,7 +63,22 @@ def main():
         ring_args.append((st, so))
     ring = None
 
+    import numpy as np
+    pool = np.random.default_rng(1).integers(0, 256, size=64 << 20, dtype=np.uint8)
+    pool_addr = pool.ctypes.data
+    dirty_state = {"mode": "none"}
+
+    def dirty(s0, k):
+        if dirty_state["mode"] == "none":
+            return
+        for i in range(k):
+            s_ = s0 + i
+            ctypes.memmove(rows + s_ * N * C, pool_addr + (s_ * 7919 * 4096) % ((64 << 20) - N * C), N * C)
+
     def launch(q, qi, s0, k, mode):
+        dirty(s0, k)
+        if dirty_state["mode"] == "copy_only":
+            return
         if mode == "ring":
             hs = []
             for i in range(k):
@@ -88,7 +107,7 @@ def main():
             base = qi * per_q
             for s0 in range(base, base + per_q, k):
                 launch(q, qi, s0, k, mode)
-                if mode != "ring":
+                if mode != "ring" and dirty_state["mode"] != "copy_only":
                     q.sync()  # the protocol's P lane waits for every window
 
         ths = [threading.Thread(target=worker, args=(i,)) for i in range(nq)]
@@ -100,7 +119,9 @@ def main():
         dt = time.perf_counter() - t0
         return per_q * nq, dt
 
-    for mode in a.modes.split(","):
+    for dm in a.dirty.split(","):
+      dirty_state["mode"] = dm
+      for mode in a.modes.split(","):
         for w in ([int(x) for x in a.ring_workers.split(",")] if mode == "ring" else [0]):
           if mode == "ring":
             if ring is not None:
@@ -111,7 +132,7 @@ def main():
                 run(mode, k, nq)  # warm
                 res = [run(mode, k, nq) for _ in range(3)]
                 st, dt = min(res, key=lambda x: x[1])
-                print(json.dumps({"mode": mode, "ring_workers": w, "stripes_per_launch": k, "queues": nq, "stripes": st,
+                print(json.dumps({"dirty": dm, "mode": mode, "ring_workers": w, "stripes_per_launch": k, "queues": nq, "stripes": st,
                                   "best_s": round(dt, 4), "read_GBps": round(st * N * C / dt / 1e9, 2),
                                   "read_plus_write_GiBps": round(st * (N + 1) * C / dt / 2 ** 30, 2)}), flush=True)
     if ring is not None:
