@@ -141,6 +141,7 @@ _SIGS = {
     "bcp_task_set_fold_inflight": ([ctypes.c_int], ctypes.c_int),
     "bcp_task_fold_stats": ([ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)], ctypes.c_int),
     "bcp_task_set_fold_ring": ([ctypes.c_int], ctypes.c_int),
+    "bcp_gen_round_timing": ([ctypes.POINTER(ctypes.c_double), ctypes.c_int], ctypes.c_int),
     "bcp_task_ring_stats": ([ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)], ctypes.c_int),
     "bcp_task_inject_failure": ([ctypes.c_int, ctypes.c_int, ctypes.c_int], ctypes.c_int),
     "bcp_task_phase_stats": ([ctypes.POINTER(ctypes.c_double), ctypes.c_int, ctypes.c_int], ctypes.c_int),
@@ -836,6 +837,14 @@ def set_fold_inflight(k: int) -> int:
     if rc < 0:
         raise BcpError("bcp_task_set_fold_inflight", rc)
     return rc
+
+
+def round_timing() -> dict:
+    """Stage times of this process's latest changelog round (bcp_gen_round_timing)."""
+    t = (ctypes.c_double * 4)()
+    n = lib().bcp_gen_round_timing(t, 4)
+    check("bcp_gen_round_timing", min(n, 0))
+    return {"db_read_s": round(t[0], 5), "plan_s": round(t[1], 5), "run_s": round(t[2], 5), "replicas_s": round(t[3], 5)}
 
 
 def set_fold_ring(on: bool) -> bool:

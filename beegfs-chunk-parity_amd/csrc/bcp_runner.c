@@ -645,9 +645,26 @@ static int update_replicas(const char *root, int ntargets, const bcp_work_item *
     return rc;
 }
 
+/* Stage times of the latest round in this process (bcp_gen_round_timing). */
+static double g_round_t[BCP_ROUND_STAGES];
+static pthread_mutex_t g_round_mu = PTHREAD_MUTEX_INITIALIZER;
+
+int bcp_gen_round_timing(double *seconds, int nstages)
+{
+    if (nstages < 0 || (nstages && !seconds))
+        return -EINVAL;
+    pthread_mutex_lock(&g_round_mu);
+    for (int i = 0; i < nstages && i < BCP_ROUND_STAGES; i++)
+        seconds[i] = g_round_t[i];
+    pthread_mutex_unlock(&g_round_mu);
+    return BCP_ROUND_STAGES;
+}
+
 static int round_impl(bcp_pipeline *pl, int procs, const char *store_root, int ntargets, const bcp_eventset *events,
                       const int *cum_weight_in, int nlanes, FILE *log, bcp_run_stats *stats, size_t *nplanned)
 {
+    double tt[BCP_ROUND_STAGES] = {0};
+    double tmark = bcpr_now_s();
     if (!store_root || !events || ntargets < 1 || ntargets > MAX_STORAGE_TARGETS)
         return -EINVAL;
     int cw[MAX_STORAGE_TARGETS];
@@ -670,6 +687,8 @@ static int round_impl(bcp_pipeline *pl, int procs, const char *store_root, int n
     bcp_pdb_close(db);
     if (rc)
         return rc;
+    tt[BCP_ROUND_DB_READ] = bcpr_now_s() - tmark;
+    tmark = bcpr_now_s();
     size_t n = 0, round_start[MAX_STORAGE_TARGETS + 1];
     bcp_work_item *work = NULL;
     int *lanes = NULL;
@@ -697,6 +716,8 @@ static int round_impl(bcp_pipeline *pl, int procs, const char *store_root, int n
         }
         free(fis);
     }
+    tt[BCP_ROUND_PLAN] = bcpr_now_s() - tmark;
+    tmark = bcpr_now_s();
     if (!rc && !pl && !procs)
         rc = bcp_gen_run_db(store_root, ntargets, work, n, nlanes, lanes, log, stats);
     if (!rc && (pl || procs)) {
@@ -704,11 +725,19 @@ static int round_impl(bcp_pipeline *pl, int procs, const char *store_root, int n
         memset(&st, 0, sizeof(st));
         rc = pl ? bcp_pipeline_run(pl, store_root, ntargets, work, n, log, &st)
                 : bcp_gen_run_procs(store_root, ntargets, work, n, nlanes, lanes, log, &st);
+        tt[BCP_ROUND_RUN] = bcpr_now_s() - tmark;
+        tmark = bcpr_now_s();
         if (!rc && st.errors == 0)
             rc = update_replicas(store_root, ntargets, work, n); /* only after the parity is on disk */
+        tt[BCP_ROUND_REPLICAS] = bcpr_now_s() - tmark;
         if (stats)
             *stats = st;
+    } else {
+        tt[BCP_ROUND_RUN] = bcpr_now_s() - tmark; /* (the DB runner updates its replicas as it goes) */
     }
+    pthread_mutex_lock(&g_round_mu);
+    memcpy(g_round_t, tt, sizeof(tt));
+    pthread_mutex_unlock(&g_round_mu);
     if (nplanned)
         *nplanned = n;
     free(lanes);

@@ -623,6 +623,17 @@ int bcp_pipeline_rebuild(bcp_pipeline *pl, const char *store_root, int ntargets,
  * updated after the run, only when it finished without errors. */
 int bcp_gen_round_pipeline(bcp_pipeline *pl, const char *store_root, int ntargets, const bcp_eventset *events,
                            const int *cum_weight, FILE *log, bcp_run_stats *stats, size_t *nplanned);
+/* Stage times (seconds) of this process's latest round (bcp_gen_round*):
+ * reading the previous state from replica 0, planning (event set -> rounds
+ * -> worklist against that state), the run over the planned items, and the
+ * replicas' update (pipeline and rank-process rounds; the DB runner updates
+ * its replicas inside the run).  Returns BCP_ROUND_STAGES. */
+#define BCP_ROUND_DB_READ 0
+#define BCP_ROUND_PLAN 1
+#define BCP_ROUND_RUN 2
+#define BCP_ROUND_REPLICAS 3
+#define BCP_ROUND_STAGES 4
+int bcp_gen_round_timing(double *seconds, int nstages);
 
 #ifdef __cplusplus
 }

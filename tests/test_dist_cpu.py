@@ -134,15 +134,16 @@ def test_kfd_gpus_counts_usable_gpu_nodes_without_hip(tmp_path):
 def test_cpu_quota_caps_the_cpu_baseline_threads(tmp_path, monkeypatch):
     sys.path.insert(0, ROOT)
     import bench
+    import bench_legs
     (tmp_path / "cpu.max").write_text("1600000 100000\n")
     assert bench.cpu_quota(str(tmp_path)) == 16.0
     (tmp_path / "cpu.max").write_text("max 100000\n")
     assert bench.cpu_quota(str(tmp_path)) is None
     assert bench.cpu_quota(str(tmp_path / "none")) is None
-    monkeypatch.setattr(bench, "cpu_quota", lambda: 16.0)
+    monkeypatch.setattr(bench_legs, "cpu_quota", lambda: 16.0)
     monkeypatch.setattr(os, "sched_getaffinity", lambda pid: set(range(256)))
     assert bench.usable_cpus() == (16, 256, 16.0)
-    monkeypatch.setattr(bench, "cpu_quota", lambda: None)
+    monkeypatch.setattr(bench_legs, "cpu_quota", lambda: None)
     monkeypatch.setattr(os, "sched_getaffinity", lambda pid: set(range(8)))
     assert bench.usable_cpus() == (8, 8, None)
 

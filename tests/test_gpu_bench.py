@@ -80,7 +80,7 @@ def test_bench_gpus_n_launches_its_own_ranks(bcp, n):
     env.pop("WORLD_SIZE", None)
     args = [sys.executable, "bench.py", "--gpus", str(n), "--stripes", "64", "--steps", "2", "--warmup", "1",
             "--cpu-seconds", "1", "--cpu-stripes", "16", "--e2e-gib", "0.1" if n == 8 else "0.25", "--e2e-reps", "1",
-            "--c1-files", "48", "--c1-reps", "1"]
+            "--c1-files", "48", "--c1-reps", "1", "--c5-reps", "1"]
     args += [] if n == 2 else ["--no-prof"]  # the live profile from rank 0 of an N-rank job
     if ndev < n:
         r = subprocess.run(args, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
@@ -118,9 +118,11 @@ def test_bench_gpus_n_launches_its_own_ranks(bcp, n):
     c1 = line["configs"]["config1"]
     assert "gen" in c1 and all(c1["gen"][k]["verified"] for k in ("reference_fold", "gpu_fold", "pipeline")), c1
     assert c1["gen"]["reference_fold"]["kind"] == "reference"
+    assert "error" not in line["configs"]["config5_protocol"], line["configs"]["config5_protocol"]
     if n == 2:
         live = line["roofline"]["live_profile"]
         assert live and "error" not in live and line["roofline"]["same_box"] is True, live
+        assert line["roofline"]["profiled_in_process"] is True
     if n == 8:
         assert "config2" in line["config"]["workload"]  # an explicit --stripes is never labelled config 4
     assert line["config"]["bytes_per_step_per_gpu"] * n * line["steps"] / 2**30 / (line["ms_per_step"] *
@@ -149,7 +151,7 @@ def test_bench_configs_block_one_rank(bcp):
     subset planned against the DB and recomputed, verified."""
     line = _run([sys.executable, "bench.py", "--stripes", "64", "--steps", "2", "--warmup", "1", "--no-prof",
                  "--cpu-seconds", "1", "--e2e-gib", "0.25", "--e2e-reps", "1", "--c1-files", "96",
-                 "--c1-reps", "1"], 360)
+                 "--c1-reps", "1", "--c5-reps", "1"], 360)
     c1 = line["configs"]["config1"]
     assert "error" not in c1 and "skipped" not in c1, c1
     for what in ("gen", "rebuild"):
@@ -164,6 +166,17 @@ def test_bench_configs_block_one_rank(bcp):
     part = line["configs"]["config5_partial"]
     assert part["verified"] is True and part["plan_ok"] is True and part["GiBps"] > 0, part
     assert part["stripes"] == max(1, line["e2e"]["per_rank"][0]["stripes"] // 10)
+    st = part["stages_warm_s_rank0"]
+    assert set(st) == {"parse_s", "db_read_s", "plan_s", "run_s", "replicas_s"} and st["run_s"] > 0, st
+    c5 = line["configs"]["config5_protocol"]
+    assert "error" not in c5, c5
+    for what in ("gen", "rebuild"):
+        for leg in ("reference_fold", "gpu_fold"):
+            x = c5[what][leg]
+            assert x["verified"] is True and x["GiBps"] > 0 and len(x["runs_s"]) == 2, (what, leg, x)
+    assert c5["gen"]["reference_fold"]["kind"] == "reference" and c5["ring"]["pieces"] > 0, c5
+    ib = c1["gpu_fold_in_place_bound"]
+    assert ib["per_launch"]["GiBps"] > 0 and "ring" in ib["shape"], ib
 
 
 @pytest.mark.timeout(400)
@@ -188,20 +201,42 @@ def test_bench_line_survives_an_e2e_failure_on_one_rank(bcp):
 @pytest.mark.timeout(500)
 @pytest.mark.parametrize("mode", ["gen", "mixed"])
 def test_bench_live_profile_on_its_own_box(bcp, mode):
-    """The roofline's rocprof figures come from this box: the same workload
-    under rocprofv3 in child processes (kernel trace, then the two PMC passes),
-    traffic within 1 % of the algorithmic bytes, same_box set."""
+    """The roofline's rocprof figures come from the line's own launches: the
+    rank runs under rocprofv3 --kernel-trace as a child of bench.py, the
+    trace's timed dispatches (warm-up and verification excluded) are averaged
+    and compared with the same process's HIP events over the same launches;
+    then the two PMC passes of the workload (traffic within 1 % of the
+    algorithmic bytes), same_box set."""
     line = _run([sys.executable, "bench.py", "--mode", mode, "--stripes", "256", "--steps", "4", "--warmup", "2",
                  "--no-cpu", "--no-e2e", "--no-configs"], 450)
     rf = line["roofline"]
     live = rf["live_profile"]
-    assert live and "error" not in live, live
-    # the timed launches only (warm-up and verification dispatches excluded),
-    # and the child's own events over those same launches
+    assert live and "error" not in live and "pmc_error" not in live, live
+    assert rf["profiled_in_process"] is True and live["in_process"] is True
     assert live["rocprof_timed_launches"] == 4 and len(live["rocprof_timed_ms_steps"]) == 4
-    assert live["rocprof_all_dispatches"]["calls"] == 2 + 4 + 1
-    assert len(live["child_event_ms_steps"]) == 4 and 0.8 < live["child_event_over_rocprof"] < 1.25, live
+    assert live["tagged_dispatches"] == 2 + 4 + 1
+    assert 0.9 < live["event_over_rocprof"] < 1.1, live
     assert live["rocprof_min_ns"] <= live["rocprof_median_ns"] <= live["rocprof_max_ns"]
     assert 0.99 < live["traffic_over_algorithmic"] < 1.02, live
     assert rf["same_box"] is True and rf["traffic"] == live["traffic"]
     assert rf["frac_rocprof"] > 0 and rf["profile_box"] == rf["run_box"]
+    assert abs(rf["frac_event_over_rocprof"] - live["event_over_rocprof"]) < 1e-3
+
+
+@pytest.mark.timeout(500)
+def test_bench_line_survives_failed_legs(bcp):
+    """Every leg beside the device timing fails (injected): the CPU baseline,
+    config 1, config 5 through the protocol -- the line is printed, verified,
+    with each failure in its own block and the e2e block intact."""
+    env = dict(os.environ, BCP_BENCH_FAIL_LEG="cpu_baseline,config1,config5_protocol")
+    r = subprocess.run([sys.executable, "bench.py", "--stripes", "64", "--steps", "2", "--warmup", "1", "--no-prof",
+                        "--cpu-seconds", "1", "--e2e-gib", "0.25", "--e2e-reps", "1"], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=420)
+    assert r.returncode == 0, (r.returncode, r.stdout[-2000:], r.stderr[-4000:])
+    line = _last_json(r.stdout)
+    assert line["config"]["verified_on_device"] is True and line["value"] > 0
+    assert "injected" in line["cpu_baseline"]["error"]
+    assert "injected" in line["configs"]["config1"]["error"]
+    assert "injected" in line["configs"]["config5_protocol"]["error"]
+    assert line["e2e"]["gen"]["verified"] is True and line["e2e"]["errors"] is None
+    assert line["configs"]["config5_partial"]["verified"] is True
