@@ -122,6 +122,8 @@ _SIGS = {
     "bcp_ring_wait": ([_V, ctypes.c_uint64], ctypes.c_int),
     "bcp_ring_query": ([_V, ctypes.c_uint64], ctypes.c_int),
     "bcp_ring_destroy": ([_V], ctypes.c_int),
+    "bcp_ring_set_wait": ([_V, ctypes.c_int, ctypes.c_int], ctypes.c_int),
+    "bcp_task_set_ring_wait": ([ctypes.c_int, ctypes.c_int], ctypes.c_int),
     "bcp_ring_stats": ([_V, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)], ctypes.c_int),
     "bcp_dev_fill_synthetic_async": ([_V, _V, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64], ctypes.c_int),
     "bcp_dev_xor_fold_async": ([_V, _V, ctypes.c_uint64, _V], ctypes.c_int),

@@ -16,6 +16,8 @@
 #include <pthread.h>
 #include <stdio.h>
 #include <sys/mman.h>
+#include <sys/prctl.h>
+#include <time.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -333,6 +335,8 @@ extern "C" int bcp_set_option(bcp_engine *eng, const char *key, int value) {
   else if (!strcmp(key, "desc_reuse_records") && (value == 0 || value == 1)) eng->tuning.desc_reuse_records = value;
   else if (!strcmp(key, "desc_table_host_max") && value >= 0 && value <= (1 << 24))
     eng->tuning.desc_table_host_max = value;
+  else if (!strcmp(key, "ring_spin_us") && value >= 0 && value <= 1000000) eng->tuning.ring_spin_us = value;
+  else if (!strcmp(key, "ring_sleep_us") && value >= 0 && value <= 100000) eng->tuning.ring_sleep_us = value;
   else rc = -EINVAL;
   pthread_mutex_unlock(&eng->lock);
   return rc;
@@ -355,6 +359,8 @@ extern "C" int bcp_get_option(bcp_engine *eng, const char *key, int *value) {
   else if (!strcmp(key, "host_registered")) *value = t.host_registered;
   else if (!strcmp(key, "desc_reuse_records")) *value = t.desc_reuse_records;
   else if (!strcmp(key, "desc_table_host_max")) *value = t.desc_table_host_max;
+  else if (!strcmp(key, "ring_spin_us")) *value = t.ring_spin_us;
+  else if (!strcmp(key, "ring_sleep_us")) *value = t.ring_sleep_us;
   else if (!strcmp(key, "last_stream_vecs")) *value = eng->last_stream_vecs.load(std::memory_order_relaxed);
   else if (!strcmp(key, "last_desc_vecs")) *value = eng->last_desc_vecs.load(std::memory_order_relaxed);
   else if (!strcmp(key, "last_desc_form")) *value = eng->last_desc_form.load(std::memory_order_relaxed);
@@ -1113,6 +1119,7 @@ struct bcp_ring {
   uint64_t next = 0;              // next ticket
   std::atomic<int> broken{0};
   std::atomic<uint64_t> launches{0};
+  std::atomic<int> spin_us{4}, sleep_us{10};  // waits (bcp_ring_set_wait; from the engine's options)
 };
 
 static size_t ring_dev_bytes() {
@@ -1140,6 +1147,8 @@ extern "C" int bcp_ring_create(bcp_engine *eng, int workers, int idle_us, bcp_ri
   if (!r) return -ENOMEM;
   r->eng = eng;
   r->workers = workers ? workers : 64;
+  r->spin_us.store(eng->tuning.ring_spin_us, std::memory_order_relaxed);
+  r->sleep_us.store(eng->tuning.ring_sleep_us, std::memory_order_relaxed);
   int khz = 0;  // s_memrealtime rate
   if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, eng->device) != hipSuccess || khz <= 0)
     khz = 100000;
@@ -1219,11 +1228,24 @@ static bool ring_ticket_done(const bcp_ring *r, uint64_t t) {
   return ring_load(&r->done[(size_t)(t & (kRingEntries - 1)) * kRingDoneStride]) >= t + 1;
 }
 
+static uint64_t mono_ns() {
+  struct timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
+}
+
 // Wait for ticket t; relaunch when the live launch closed before taking it.
-// Spins with pause for a short while (a piece folds in tens of microseconds),
-// then yields the CPU between looks.
+// Spins with pause for ring_spin_us, then sleeps ring_sleep_us between looks
+// (engine options): the waiters are the protocol's P lanes, dozens per
+// process, and a spinning one takes the CPU the source lanes copy chunks
+// with (config 1 is CPU-bound on a 16-CPU share).  The thread's timer slack
+// is set to 1 us once, so the sleeps are as short as asked.
 static int ring_wait_ticket(bcp_ring *r, uint64_t t) {
-  for (uint32_t spin = 0;; spin++) {
+  static thread_local bool slack_set = false;
+  const uint64_t spin_ns = (uint64_t)r->spin_us.load(std::memory_order_relaxed) * 1000u;
+  const long sleep_ns = (long)r->sleep_us.load(std::memory_order_relaxed) * 1000L;
+  uint64_t t0 = 0, last_query = 0;
+  for (;;) {
     if (ring_ticket_done(r, t)) return 0;
     if (r->broken.load(std::memory_order_relaxed)) return -EIO;
     if (ring_load(&r->ctl->closed) != kRingLive) {
@@ -1233,8 +1255,11 @@ static int ring_wait_ticket(bcp_ring *r, uint64_t t) {
       if (rc) return rc;
       continue;
     }
-    if ((spin & 4095u) == 4095u) {
+    const uint64_t now = mono_ns();
+    if (!t0) t0 = last_query = now;
+    if (now - last_query > 1000000u) {
       // a launch that ended without closing (a fault) never completes t
+      last_query = now;
       pthread_mutex_lock(&r->mu);
       const hipError_t q = r->launched ? hipEventQuery(r->ended) : hipErrorNotReady;
       const bool dead = q != hipErrorNotReady && ring_load(&r->ctl->closed) == kRingLive && !ring_ticket_done(r, t);
@@ -1243,8 +1268,15 @@ static int ring_wait_ticket(bcp_ring *r, uint64_t t) {
       pthread_mutex_unlock(&r->mu);
       if (dead) return -EIO;
     }
-    if (spin < 512) {
+    if (now - t0 < spin_ns) {
       for (int i = 0; i < 16; i++) cpu_relax();
+    } else if (sleep_ns > 0) {
+      if (!slack_set) {
+        (void)prctl(PR_SET_TIMERSLACK, 1000UL, 0, 0, 0);
+        slack_set = true;
+      }
+      const struct timespec ts = {0, sleep_ns};
+      nanosleep(&ts, nullptr);
     } else {
       sched_yield();
     }
@@ -1332,6 +1364,13 @@ extern "C" int bcp_ring_query(bcp_ring *r, uint64_t handle) {
       }
       return -EAGAIN;
     }
+  return 0;
+}
+
+extern "C" int bcp_ring_set_wait(bcp_ring *r, int spin_us, int sleep_us) {
+  if (!r || spin_us < 0 || spin_us > 1000000 || sleep_us < 0 || sleep_us > 100000) return -EINVAL;
+  r->spin_us.store(spin_us, std::memory_order_relaxed);
+  r->sleep_us.store(sleep_us, std::memory_order_relaxed);
   return 0;
 }
 

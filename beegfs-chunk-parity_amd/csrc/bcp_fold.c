@@ -102,6 +102,7 @@ static bcp_ring *g_ring[BCPF_MAX_DEVICES];
 static int g_ring_rc[BCPF_MAX_DEVICES];
 static int g_fold_ring = 1;
 static uint64_t g_ring_pieces, g_ring_launches; /* of rings already destroyed */
+static int g_ring_spin_us = -1, g_ring_sleep_us = -1; /* bcp_task_set_ring_wait; -1: the engine's */
 #define RING_WORKERS 16
 
 int bcp_task_set_fold_ring(int on)
@@ -128,11 +129,28 @@ bcp_ring *bcpf_ring_for(int dev, bcp_engine *e)
     if (dev < 0 || dev >= BCPF_MAX_DEVICES || !e)
         return NULL;
     pthread_mutex_lock(&g_mu);
-    if (!g_ring[dev] && !g_ring_rc[dev])
+    if (!g_ring[dev] && !g_ring_rc[dev]) {
         g_ring_rc[dev] = bcp_ring_create(e, RING_WORKERS, 0, &g_ring[dev]);
+        if (!g_ring_rc[dev] && g_ring_spin_us >= 0)
+            (void)bcp_ring_set_wait(g_ring[dev], g_ring_spin_us, g_ring_sleep_us);
+    }
     bcp_ring *r = g_ring[dev];
     pthread_mutex_unlock(&g_mu);
     return r;
+}
+
+int bcp_task_set_ring_wait(int spin_us, int sleep_us)
+{
+    if (spin_us < 0 || spin_us > 1000000 || sleep_us < 0 || sleep_us > 100000)
+        return -EINVAL;
+    pthread_mutex_lock(&g_mu);
+    g_ring_spin_us = spin_us;
+    g_ring_sleep_us = sleep_us;
+    for (int d = 0; d < BCPF_MAX_DEVICES; d++)
+        if (g_ring[d])
+            (void)bcp_ring_set_wait(g_ring[d], spin_us, sleep_us);
+    pthread_mutex_unlock(&g_mu);
+    return 0;
 }
 
 int bcp_task_ring_stats(uint64_t *pieces, uint64_t *launches)

@@ -47,6 +47,10 @@ struct Tuning {
     // tables reuses that slot's tile records (no table upload, no desc_tiles):
     // the A/B of desc_tiles' concurrent HBM traffic (tools/exp/desc_records_ab.py).
     int desc_reuse_records = 0;
+    // Resident fold ring waits (bcp_ring_wait): spin this long, then sleep
+    // this long between looks (0: sched_yield instead).
+    int ring_spin_us = 4;
+    int ring_sleep_us = 10;
 };
 
 // Arguments of the streaming kernel (xor_stream).

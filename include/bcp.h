@@ -198,6 +198,10 @@ int bcp_ring_query(bcp_ring *r, uint64_t handle);
 /* Stops the launch (pending stripes are folded first) and frees the ring;
  * every handle must have been waited for. */
 int bcp_ring_destroy(bcp_ring *r);
+/* How waiters wait: spin spin_us, then sleep sleep_us between looks (0:
+ * sched_yield); defaults from the engine options ring_spin_us /
+ * ring_sleep_us (4 / 10). */
+int bcp_ring_set_wait(bcp_ring *r, int spin_us, int sleep_us);
 /* Pieces published (a stripe is cut into 512 KiB pieces) and launches made
  * since the ring was created. */
 int bcp_ring_stats(bcp_ring *r, uint64_t *pieces, uint64_t *launches);
@@ -249,6 +253,9 @@ int bcp_set_tuning(bcp_engine *eng, int blocks_per_cu, int vecs_per_thread);
  *   default 131072), "desc_reuse_records" (1: a batch resubmitted on a ring
  *   slot with byte-identical staged tables reuses that slot's tile records;
  *   default 0, an A/B knob);
+ *  resident fold ring: "ring_spin_us" (a waiter spins this long, default 4)
+ *   and "ring_sleep_us" (then sleeps this long between looks, default 10;
+ *   0 = sched_yield instead);
  *  memory: "contiguous_alloc" (1: bcp_dev_alloc requests physically
  *   contiguous memory for buffers of 64 MiB and more; default 0),
  *   "host_registered" (bcp_host_alloc / bcp_host_alloc_mapped: 1 = ordinary

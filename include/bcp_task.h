@@ -165,6 +165,9 @@ int bcp_task_fold_stats(uint64_t *windows, uint64_t *launches);
  * bcp_task_shutdown; its launch ends by itself 5 ms after the last fold.
  * Returns the previous value or -EINVAL. */
 int bcp_task_set_fold_ring(int on);
+/* How the P lanes wait for their folds in the ring (bcp_ring_set_wait) --
+ * for the rings now and those made later; tools and A/B runs. */
+int bcp_task_set_ring_wait(int spin_us, int sleep_us);
 /* Pieces (<= 512 KiB of parity each) published to the fold rings and
  * launches of them since the process started. */
 int bcp_task_ring_stats(uint64_t *pieces, uint64_t *launches);

@@ -108,6 +108,19 @@ def fold_setup(fold, hooks):
             bcp.set_fold_mode(prev)
             bcp.set_fold_inflight(prev_k)
         return restore
+    if fold.startswith("gpu_ring_w"):
+        # gpu_ring_w<spin>_<sleep>: the ring with waiters spinning <spin> us,
+        # then sleeping <sleep> us between looks (0: sched_yield)
+        spin, sleep = (int(x) for x in fold[len("gpu_ring_w"):].split("_"))
+        prev = bcp.set_fold_mode(bcp.FOLD_PIPELINED)
+        prev_ring = bcp.set_fold_ring(True)
+        bcp.call("bcp_task_set_ring_wait", spin, sleep)
+
+        def restore_w():
+            bcp.call("bcp_task_set_ring_wait", 4, 10)
+            bcp.set_fold_ring(prev_ring)
+            bcp.set_fold_mode(prev)
+        return restore_w
     if fold in ("gpu_pipelined", "gpu_ring", "gpu_queues"):
         # gpu_ring / gpu_pipelined: PIPELINED through the resident fold ring
         # (the default since r06); gpu_queues: range launches on the lanes'
@@ -176,7 +189,7 @@ def measure(name, folds, rounds, run_once, verify_fn, nbytes, hooks, extra=None,
                 b = batching.setdefault(f, {"windows": 0, "launches": 0})
                 b["windows"] += w1 - w0
                 b["launches"] += l1 - l0
-            if f in ("gpu_pipelined", "gpu_ring", "gpu_queues") and r > 0:
+            if (f in ("gpu_pipelined", "gpu_ring", "gpu_queues") or f.startswith("gpu_ring_w")) and r > 0:
                 b = batching.setdefault(f, {"windows": 0, "launches": 0})
                 b["windows"] += pw1 - pw0
                 b["launches"] += pr1 - pr0
@@ -196,7 +209,8 @@ def measure(name, folds, rounds, run_once, verify_fn, nbytes, hooks, extra=None,
                                          if cpu[f][-1][3] is not None else None),
                     throttled_periods=sum(c[1] for c in cpu[f][1:]),
                     throttled_ms_runs=[round(c[2], 1) for c in cpu[f]])
-        if f in ("gpu_pipelined", "gpu_ring", "gpu_queues") and batching.get(f, {}).get("windows"):
+        if (f in ("gpu_pipelined", "gpu_ring", "gpu_queues") or f.startswith("gpu_ring_w")) and \
+                batching.get(f, {}).get("windows"):
             line["range_folds_per_window"] = round(batching[f]["launches"] / batching[f]["windows"], 2)
         elif batching.get(f, {}).get("launches"):
             line["windows_per_launch"] = round(batching[f]["windows"] / batching[f]["launches"], 2)
