@@ -110,10 +110,15 @@ static int pipeline_on_all_gpus(bcp_pipeline **pl, uint64_t job_bytes)
     return bcp_pipeline_create(&o, pl);
 }
 
-/* Chunk bytes the event set's records announce (the sizes the scan or the
- * changelog reported; a deleted chunk counts as what it was). */
-static uint64_t event_bytes(const bcp_eventset *es)
+/* Bytes a --complete run stages: the chunk bytes the scan's records announce
+ * plus a page per chunk (DIRECT reads place every source at page pitch).
+ * Only a --complete run's records are its whole input: a --partial run reads
+ * every holder's chunk of each changed stripe, which the changelog's records
+ * do not list, so it keeps the library's default slabs (0). */
+static uint64_t job_bytes_of(const bcp_eventset *es, int complete)
 {
+    if (!complete)
+        return 0;
     uint64_t total = 0;
     const size_t n = bcp_eventset_count(es);
     for (size_t i = 0; i < n; i++) {
@@ -121,7 +126,7 @@ static uint64_t event_bytes(const bcp_eventset *es)
         int64_t ts;
         uint64_t m, d, sz = 0;
         if (bcp_eventset_get(es, i, &p, &ts, &m, &d, &sz) == 0)
-            total += sz;
+            total += sz + 4096;
     }
     return total;
 }
@@ -261,7 +266,7 @@ static int cmd_gen(int argc, char **argv)
     size_t planned = 0;
     if (use_pipeline) {
         bcp_pipeline *pl = NULL;
-        rc = pipeline_on_all_gpus(&pl, event_bytes(es));
+        rc = pipeline_on_all_gpus(&pl, job_bytes_of(es, complete == 1));
         t_setup = now_s();
         if (!rc)
             rc = bcp_gen_round_pipeline(pl, root, ntargets, es, NULL, stderr, &st, &planned);

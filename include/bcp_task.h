@@ -517,10 +517,18 @@ int bcp_eventset_scan(bcp_eventset *s, int st, const char *chunks_dir, uint64_t 
  * whose id changed ("Storage target missing!"), -EPROTO version stamp (the
  * file's own format stamp, 1; not the struct ABI: BCP_ABI_VERSION).  With a
  * <root>/rank_order (bcp_store_round_order) also its mapping as the reference
- * derives it from the previous run's list (bcp_map_targets; a first run: the
- * directories' order): -EPROTO when targets added since are not numbered in
- * the order the reference appends them (rank order). */
-#define BCP_TASK_ABI_VERSION 3 /* = BCP_ABI_VERSION (include/bcp.h) */
+ * derives it from the previous run's list (bcp_map_targets): -EPROTO when
+ * targets added since are not numbered in the order the reference appends
+ * them (rank order).
+ * First run (no previous list), a DELIBERATE DEVIATION: the reference numbers
+ * the targets in rank order there (gen/main.c:508-527: every rank's id
+ * appended in rank order, so index i is the i-th rank); here the st<k>
+ * directories exist before any run and keep their index k, and rank_order
+ * only orders the rounds.  With a rank_order that differs from the
+ * directories' order, a first run's target indices -- and so select_P's
+ * placements -- differ from the reference's; stores whose directories are
+ * created in rank order (bcp_store.make_store, the CLI) are unaffected. */
+#define BCP_TASK_ABI_VERSION 4 /* = BCP_ABI_VERSION (include/bcp.h) */
 int bcp_check_targets(const char *store_root, int ntargets, const char *run_data_path, FILE *log);
 
 /* Cumulative store weights st_weight (gen/main.c:485, 528-536) of
