@@ -24,6 +24,7 @@
 #include <algorithm>
 #include <atomic>
 #include <new>
+#include <thread>
 #include <vector>
 
 #include "bcp_internal.h"
@@ -792,6 +793,33 @@ static int desc_vecs_for(const bcp_engine *e, uint64_t tiles8) {
   return 8;
 }
 
+// fn(lo, hi) over [0, n): on this thread, or split over up to 8 threads when
+// there are at least 2 * per items (thread start-up costs ~10-20 us each).
+template <typename F>
+static void par_for(uint32_t n, uint32_t per, F fn) {
+  const uint32_t want = n / (per ? per : 1);
+  const uint32_t nt = std::min<uint32_t>(8, want);
+  if (nt < 2) {
+    fn(0, n);
+    return;
+  }
+  std::thread th[8];
+  bool started[8] = {};
+  const uint32_t chunk = (n + nt - 1) / nt;
+  for (uint32_t t = 1; t < nt; t++) {
+    const uint32_t lo = std::min(n, t * chunk), hi = std::min(n, lo + chunk);
+    try {
+      th[t] = std::thread(fn, lo, hi);
+      started[t] = true;
+    } catch (...) {
+      fn(lo, hi);  // no thread: on this one
+    }
+  }
+  fn(0, std::min(n, chunk));
+  for (uint32_t t = 1; t < nt; t++)
+    if (started[t]) th[t].join();
+}
+
 // Small batches (engine option desc_args_max, default kArgStripes stripes):
 // the whole descriptor in the kernel arguments, one launch (xor_desc_args).
 // Returns 1 if the batch does not qualify (caller takes the general path).
@@ -924,31 +952,45 @@ static int submit_desc(bcp_queue *q, const bcp_stripe *stripes, uint32_t nstripe
   char *h = (char *)slot->host;
   bcp_stripe *hs = (bcp_stripe *)h;
   bcp_source *hso = (bcp_source *)(h + off_src);
-  uint32_t next_src = 0;
-  for (uint32_t i = 0; i < nstripes; i++) {
-    hs[i] = stripes[i];
-    hs[i].first_src = next_src;
-    bcp_source *run = hso + next_src;
-    for (uint32_t k = 0; k < stripes[i].nsrc; k++) {
-      // insertion sort, descending len (runs are short: <= BCP_MAX_SOURCES)
-      const bcp_source x = sources[stripes[i].first_src + k];
-      uint32_t m = k;
-      while (m > 0 && run[m - 1].len < x.len) {
-        run[m] = run[m - 1];
-        m--;
-      }
-      run[m] = x;
-    }
-    next_src += stripes[i].nsrc;
-  }
-  // tiles per stripe (sub_class / tile_starts; desc_tiles repeats the cut)
   uint32_t *ts = (uint32_t *)(h + off_tiles);
+  {
+    uint32_t next_src = 0;
+    for (uint32_t i = 0; i < nstripes; i++) {
+      hs[i].first_src = next_src;  // (the rest of hs[i] is staged below)
+      next_src += stripes[i].nsrc;
+    }
+  }
+  // Per stripe: its run sorted by length and its tile count (sub_class /
+  // tile_starts; desc_tiles repeats the cut).  Large batches are staged by
+  // several threads: this host work runs before the kernel can start
+  // whenever the queue is idle (a block's first launch: config-5 shapes,
+  // 6,600 stripes, tools/exp/submit_cost.py).
+  par_for(nstripes, 1024, [&](uint32_t lo, uint32_t hi) {
+    for (uint32_t i = lo; i < hi; i++) {
+      const uint32_t first = hs[i].first_src;
+      hs[i] = stripes[i];
+      hs[i].first_src = first;
+      bcp_source *run = hso + first;
+      for (uint32_t k = 0; k < stripes[i].nsrc; k++) {
+        // insertion sort, descending len (runs are short: <= BCP_MAX_SOURCES)
+        const bcp_source x = sources[stripes[i].first_src + k];
+        uint32_t m = k;
+        while (m > 0 && run[m - 1].len < x.len) {
+          run[m] = run[m - 1];
+          m--;
+        }
+        run[m] = x;
+      }
+      const uint64_t c = count_tiles([run](uint32_t k) { return run[k].len; }, hs[i].nsrc, hs[i].out_len,
+                                     tile_bytes, hs[i].window != 0);
+      ts[i] = c > 0xFFFFFFF0ull ? 0xFFFFFFF1u : (uint32_t)c;
+    }
+  });
   uint64_t acc64 = 0;
   for (uint32_t i = 0; i < nstripes; i++) {
+    const uint64_t c = ts[i];
     ts[i] = (uint32_t)acc64;
-    const bcp_stripe &st = hs[i];
-    const bcp_source *run = hso + st.first_src;
-    acc64 += count_tiles([run](uint32_t k) { return run[k].len; }, st.nsrc, st.out_len, tile_bytes, st.window != 0);
+    acc64 += c;
     if (acc64 > 0xFFFFFFF0ull) return -EINVAL;
   }
   const uint32_t acc = (uint32_t)acc64;
