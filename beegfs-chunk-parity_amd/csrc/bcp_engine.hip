@@ -1165,7 +1165,7 @@ struct bcp_ring {
 };
 
 static size_t ring_dev_bytes() {
-  return sizeof(RingState) + kRingEntries * sizeof(unsigned long long) + kRingEntries * sizeof(RingEntry);
+  return sizeof(RingState) + 2 * kRingEntries * sizeof(unsigned long long) + kRingEntries * sizeof(RingEntry);
 }
 
 static unsigned long long ring_load(const unsigned long long *p) { return __atomic_load_n(p, __ATOMIC_ACQUIRE); }
@@ -1241,8 +1241,9 @@ static int ring_live_locked(bcp_ring *r) {
     a.closed = &r->ctl->closed;
     a.stop = &r->ctl->stop;
     a.state = (RingState *)r->dev;
-    a.cnt = (unsigned long long *)(r->dev + sizeof(RingState));
-    a.copy = (RingEntry *)(r->dev + sizeof(RingState) + kRingEntries * sizeof(unsigned long long));
+    a.claim = (unsigned long long *)(r->dev + sizeof(RingState));
+    a.cnt = a.claim + kRingEntries;
+    a.copy = (RingEntry *)(r->dev + sizeof(RingState) + 2 * kRingEntries * sizeof(unsigned long long));
     a.base = c;
     a.idle_ticks = r->idle_ticks;
     a.hard_ticks = r->hard_ticks;
@@ -1357,6 +1358,7 @@ extern "C" int bcp_ring_submit(bcp_ring *r, const bcp_stripe *stripe, const bcp_
     E->dst = s.dst + p0;
     E->out_len = plen;
     E->nsrc = s.nsrc;
+    E->parts = (uint32_t)((plen + kRingTileBytes - 1) / kRingTileBytes);  // 1..16 (plen <= kRingPieceMax)
     for (uint32_t k = 0; k < s.nsrc; k++) {
       const uint64_t len = sources[k].len > p0 ? std::min<uint64_t>(sources[k].len - p0, plen) : 0;
       E->src[k].ptr = len ? sources[k].ptr + p0 : 0;

@@ -213,29 +213,31 @@ struct DescArgs {
 // role's protocol folds one window at a time, task_processing.c:203-226).
 //   ticket  one piece of a stripe (<= kRingPieceMax output bytes), numbered
 //           from 0 in publication order; entry = ticket % K
-//   tile    1/kRingParts of a ticket's output (a multiple of 4 KiB, <= 32
-//           KiB), the unit a worker workgroup claims from the device cursor
+//   tile    one of a ticket's `parts` (its output / parts, rounded up to
+//           4 KiB, <= 32 KiB), the unit a worker workgroup claims
 // Host: writes the entry, then seq = ticket + 1 (release).  Device: one
 // watcher wave polls seq in ticket order, copies the entry to HBM and
-// advances `pub`; workers claim tiles in order, fold those of tickets below
-// `pub`, and the last tile of a ticket writes done[entry] = ticket + 1 to host
-// memory.  After idle_ticks without a new ticket (or on stop) the watcher
+// advances `pub`; workers claim the parts of the tickets below `pub` in
+// ticket order (fold_ring, bcp_kernels.hip), and the last tile of a ticket
+// writes done[entry] = ticket + 1 to host memory.  After idle_ticks without a new ticket (or on stop) the watcher
 // writes the first ticket it did not take to *closed and the launch drains:
 // every ticket below it was folded, none at or above it was touched, and the
 // host relaunches from there (bcp_engine.hip, ring_live_locked).
 // ---------------------------------------------------------------------------
-constexpr int kRingParts = 16;
-constexpr uint64_t kRingPieceMax = (uint64_t)512 << 10;
+constexpr int kRingMaxParts = 16;                       // tiles per ticket, at most
+constexpr uint64_t kRingTileBytes = (uint64_t)32 << 10;  // a tile's output, at most
+constexpr uint64_t kRingPieceMax = kRingMaxParts * kRingTileBytes;
 struct RingEntry {
     unsigned long long seq;  // ticket + 1 once published (written last)
     uint64_t dst;            // output of this piece
     uint64_t out_len;        // <= kRingPieceMax
-    uint32_t nsrc, rsv0;
+    uint32_t nsrc, parts;    // parts: tiles of this piece, ceil(out_len / 32 KiB) (1..16)
     uint64_t rsv[4];
     bcp_source src[BCP_MAX_SOURCES];  // offset to the piece, len clamped to it
     uint64_t pad[8];
 };
 static_assert(sizeof(RingEntry) == 1024, "one 16-byte load per lane of one wave copies an entry");
+static_assert(offsetof(RingEntry, parts) == 28, "the watcher reads parts from lane 1's word, dword 3");
 // Host-side control words the device writes or reads (pinned, coherent).
 struct RingCtl {
     unsigned long long closed;  // first ticket the last launch did not take; ~0 while a launch is live
@@ -245,11 +247,12 @@ struct RingCtl {
     // then done[K * kRingDoneStride]
 };
 constexpr int kRingDoneStride = 8;  // one 64-byte line per entry's done word
-// Device-side state (HBM): claim cursor, announced tickets, quit flag, each
-// on its own 128-byte line; then cnt[K] (tiles folded per entry, monotone
-// over the ring's life) and the entries' copies.
+// Device-side state (HBM): the ticket being claimed, announced tickets, quit flag, each
+// on its own 128-byte line; then claim[K] and cnt[K] (per entry: ticket <<
+// 16 | parts << 8 | parts claimed, and ticket << 16 | tiles folded; set by
+// the watcher when it announces the entry's ticket) and the entries' copies.
 struct RingState {
-    unsigned long long cursor;  // tiles claimed in this launch
+    unsigned long long cur;     // the ticket being claimed, relative to the launch's base
     unsigned long long pad0[15];
     unsigned long long pub;     // tickets announced (absolute; 0 at launch)
     unsigned long long pad1[15];
@@ -262,6 +265,7 @@ struct RingArgs {
     unsigned long long *closed;      // host (RingCtl::closed)
     const unsigned int *stop;        // host (RingCtl::stop)
     RingState *state;                // HBM
+    unsigned long long *claim;       // HBM [K]
     unsigned long long *cnt;         // HBM [K]
     RingEntry *copy;                 // HBM [K]
     unsigned long long base;         // first ticket of this launch

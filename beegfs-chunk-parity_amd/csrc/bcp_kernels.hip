@@ -803,12 +803,22 @@ __global__ __launch_bounds__(kBlock) void desc_tiles(DescBatch b) {
 
 // ---------------------------------------------------------------------------
 // Resident fold ring (RingArgs, bcp_internal.h).  Workgroup 0's first wave is
-// the watcher, every other workgroup a worker.  Exit conditions every wave
-// reaches: the watcher closes after idle_ticks without a new ticket or once
-// the host sets stop while nothing is pending; a worker leaves when the
-// watcher has closed and its claimed tile lies at or past the last announced
-// ticket, or after hard_ticks of waiting (no watcher: never in a healthy
-// launch, where the watcher's close comes first).
+// the watcher, every other workgroup a worker.
+// Tickets and parts: the host cuts each piece into `parts` tiles (a field of
+// its entry; ~32 KiB of output each, 1..16).  Announcing ticket t at
+// entry e, the watcher sets claim[e] = t << 16 | parts << 8 (claimed 0) and
+// done_cnt[e] = t << 16 before it advances `pub`.  A worker reads `cur` (the
+// ticket being claimed, relative to base), and while t = base + cur < pub it
+// claims part n of t by a CAS on claim[e] -- the word carries the ticket, so
+// a stale claimer can never take a part of the entry's next ticket -- or,
+// when every part is claimed, moves `cur` on by a CAS.  The tile's last
+// finisher (done_cnt[e]'s low byte reaching parts - 1) writes done[e].
+// Exit conditions every wave reaches: the watcher closes after idle_ticks
+// without a new ticket or once the host sets stop while nothing is pending;
+// a worker leaves when the watcher has closed and `cur` has reached the last
+// announced ticket (every part of every announced ticket claimed, and the
+// claimed ones are folded before their claimers look again), or after
+// hard_ticks of waiting (no watcher: never in a healthy launch).
 // Memory ordering: host rows and the entry are read after a system-scope
 // acquire; a tile's stores go out behind every wave's vmcnt(0) wait, a
 // barrier and a system-scope release by lane 0 before it counts the tile;
@@ -818,6 +828,11 @@ __global__ __launch_bounds__(kBlock) void desc_tiles(DescBatch b) {
 // compiler proves about the scoreboard (MI355X_MICROARCH.md, compiler hazard).
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ unsigned long long now_ticks() { return __builtin_amdgcn_s_memrealtime(); }
+
+template <typename T>
+__device__ __forceinline__ T ld_agent(const T *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 __device__ __forceinline__ void ring_watch(const RingArgs &a) {
   const uint32_t lane = threadIdx.x;  // one wave
@@ -830,7 +845,13 @@ __device__ __forceinline__ void ring_watch(const RingArgs &a) {
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // the entry's body, written before seq
       const glob<v4u> *src = gp<v4u>((uint64_t)(uintptr_t)(a.host + e));
       glob<v4u> *dst = gp<v4u>((uint64_t)(uintptr_t)(a.copy + e));
-      dst[lane] = src[lane];
+      const v4u body = src[lane];
+      dst[lane] = body;
+      if (lane == 1) {  // bytes 16..31: out_len, nsrc, parts
+        const unsigned long long parts = body[3] & 0xFFu;
+        __hip_atomic_store(&a.claim[e], pub << 16 | parts << 8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&a.cnt[e], pub << 16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -855,13 +876,13 @@ __device__ __forceinline__ void ring_watch(const RingArgs &a) {
 // l + 256 u (u < tb / 4 KiB <= 8).  Sources that cover the tile are folded
 // four at a time with every load first; a source ending inside it takes the
 // masked path (load_src_tail); zero padding is never read.
-__device__ __forceinline__ void ring_tile(const RingEntry &E, uint32_t part) {
+__device__ __forceinline__ void ring_tile(const RingEntry &E, uint32_t parts, uint32_t part) {
   const uint64_t out_len = E.out_len;
-  uint64_t tb = (out_len + kRingParts - 1) / kRingParts;
+  uint64_t tb = (out_len + parts - 1) / parts;
   tb = (tb + 4095u) & ~(uint64_t)4095u;
   const uint64_t lo = (uint64_t)part * tb;
   if (lo >= out_len) return;
-  const uint32_t nv = (uint32_t)(tb >> 12);  // 1..8
+  const uint32_t nv = (uint32_t)(tb >> 12);  // 1..8 (the host keeps tb <= 32 KiB)
   const uint64_t hi = lo + tb;
   const uint32_t nsrc = E.nsrc;
   const uint32_t lane_off = threadIdx.x * 16u;
@@ -897,61 +918,72 @@ __device__ __forceinline__ void ring_tile(const RingEntry &E, uint32_t part) {
     if ((uint32_t)u < nv) store_tail(d, out_len, lo + lane_off + u * 4096u, acc[u]);
 }
 
+// Thread 0: the next (ticket, part) to fold, packed t << 16 | parts << 8 |
+// part, or ~0 when the launch is over for this workgroup.
+__device__ __forceinline__ unsigned long long ring_claim(const RingArgs &a) {
+  const unsigned long long t0 = now_ticks();
+  for (;;) {
+    const unsigned long long c = ld_agent(&a.state->cur);
+    const unsigned long long t = a.base + c;
+    if (t >= ld_agent(&a.state->pub)) {
+      if (ld_agent(&a.state->quit)) {
+        // quit is stored after the last pub: one more look decides
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        if (a.base + ld_agent(&a.state->cur) >= ld_agent(&a.state->pub)) return ~0ull;
+        continue;
+      }
+      if (now_ticks() - t0 > a.hard_ticks) return ~0ull;
+      __builtin_amdgcn_s_sleep(2);
+      continue;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the watcher's claim word for t
+    const uint32_t e = (uint32_t)(t & a.kmask);
+    unsigned long long v = ld_agent(&a.claim[e]);
+    if ((v >> 16) != t) continue;  // cur moved on meanwhile: look again
+    const uint32_t parts = (uint32_t)(v >> 8) & 0xFFu, n = (uint32_t)v & 0xFFu;
+    if (n >= parts) {  // every part of t is taken: on to t + 1
+      unsigned long long cc = c;
+      __hip_atomic_compare_exchange_strong(&a.state->cur, &cc, c + 1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+      continue;
+    }
+    if (__hip_atomic_compare_exchange_strong(&a.claim[e], &v, v + 1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT))
+      return t << 16 | (unsigned long long)parts << 8 | n;
+  }
+}
+
 __device__ __forceinline__ void ring_work(const RingArgs &a) {
   __shared__ unsigned long long s_g[2];
-  __shared__ int s_go[2];
   __shared__ RingEntry s_e;
   int slot = 0;
   for (;;) {
-    if (threadIdx.x == 0) {
-      const unsigned long long g = atomicAdd(&a.state->cursor, 1ull);
-      const unsigned long long t = a.base + g / kRingParts;
-      const unsigned long long t0 = now_ticks();
-      int go = 1;
-      for (;;) {
-        if (t < __hip_atomic_load(&a.state->pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
-        if (__hip_atomic_load(&a.state->quit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-          // quit is stored after the last pub: one more look decides
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-          go = t < __hip_atomic_load(&a.state->pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          break;
-        }
-        if (now_ticks() - t0 > a.hard_ticks) {
-          go = 0;
-          break;
-        }
-        __builtin_amdgcn_s_sleep(2);
-      }
-      s_g[slot] = g;
-      s_go[slot] = go;
-    }
+    if (threadIdx.x == 0) s_g[slot] = ring_claim(a);
     __syncthreads();
-    const int go = __builtin_amdgcn_readfirstlane(s_go[slot]);
     const unsigned long long g = s_g[slot];
     slot ^= 1;
-    if (!go) return;
-    const unsigned long long t = a.base + g / kRingParts;
-    const uint32_t part = (uint32_t)(g % kRingParts);
+    if (g == ~0ull) return;
+    const unsigned long long t = g >> 16;
+    const uint32_t parts = (uint32_t)(g >> 8) & 0xFFu, part = (uint32_t)g & 0xFFu;
     const uint32_t e = (uint32_t)(t & a.kmask);
     // the entry's copy (HBM, written by the watcher) and the host rows: fresh
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
     if (threadIdx.x < 64) {
       const unsigned long long *q = (const unsigned long long *)(a.copy + e) + 2 * threadIdx.x;
       unsigned long long *w = (unsigned long long *)&s_e + 2 * threadIdx.x;
-      w[0] = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      w[1] = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      w[0] = ld_agent(q);
+      w[1] = ld_agent(q + 1);
     }
     __syncthreads();
-    ring_tile(s_e, part);
+    ring_tile(s_e, parts, part);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();  // every wave's stores done; s_e free for the next tile
     if (threadIdx.x == 0) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      const unsigned long long use = t >> a.kshift;
       const unsigned long long old =
           __hip_atomic_fetch_add(&a.cnt[e], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      if (old == (use + 1) * kRingParts - 1) {
+      if (old == (t << 16 | (unsigned long long)(parts - 1))) {
         // the ticket's last tile: the other tiles' stores were released
         // before their counts; order them before the done word
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");

@@ -36,14 +36,16 @@ def main():
     ap.add_argument("--qs", default="1,4,12")
     ap.add_argument("--total-stripes", type=int, default=768)
     ap.add_argument("--nsrc", type=int, default=3)
+    ap.add_argument("--chunk-kib", type=int, default=512, help="bytes per row (the protocol's range folds: 128)")
     ap.add_argument("--modes", default="zero_copy,dma,ring")
     ap.add_argument("--ring-workers", default="64")
     ap.add_argument("--dirty", default="none",
                     help="comma list of row states before each fold: none (rows untouched since the first fill), "
                          "copy (each lane memcpy's its stripe's rows first, as the sources' read() does), "
+                         "copy_elsewhere (the same copies into a scratch buffer: the rows stay clean), "
                          "copy_only (the copies alone, no fold: their own cost)")
     a = ap.parse_args()
-    C, N = 512 * KiB, a.nsrc
+    C, N = a.chunk_kib * KiB, a.nsrc
     T = a.total_stripes
     eng = bcp.Engine(0)
     rows = eng.host_alloc(T * N * C)
@@ -68,12 +70,19 @@ def main():
     pool_addr = pool.ctypes.data
     dirty_state = {"mode": "none"}
 
+    scratch = np.empty(qmax * N * C, dtype=np.uint8)
+
     def dirty(s0, k):
         if dirty_state["mode"] == "none":
             return
         for i in range(k):
             s_ = s0 + i
-            ctypes.memmove(rows + s_ * N * C, pool_addr + (s_ * 7919 * 4096) % ((64 << 20) - N * C), N * C)
+            src_ = pool_addr + (s_ * 7919 * 4096) % ((64 << 20) - N * C)
+            if dirty_state["mode"] == "copy_elsewhere":  # the same copies, into a lane's scratch: rows stay clean
+                lane = threading.get_ident() % qmax
+                ctypes.memmove(scratch.ctypes.data + lane * N * C, src_, N * C)
+            else:
+                ctypes.memmove(rows + s_ * N * C, src_, N * C)
 
     def launch(q, qi, s0, k, mode):
         dirty(s0, k)
@@ -132,7 +141,7 @@ def main():
                 run(mode, k, nq)  # warm
                 res = [run(mode, k, nq) for _ in range(3)]
                 st, dt = min(res, key=lambda x: x[1])
-                print(json.dumps({"dirty": dm, "mode": mode, "ring_workers": w, "stripes_per_launch": k, "queues": nq, "stripes": st,
+                print(json.dumps({"chunk_kib": a.chunk_kib, "dirty": dm, "mode": mode, "ring_workers": w, "stripes_per_launch": k, "queues": nq, "stripes": st,
                                   "best_s": round(dt, 4), "read_GBps": round(st * N * C / dt / 1e9, 2),
                                   "read_plus_write_GiBps": round(st * (N + 1) * C / dt / 2 ** 30, 2)}), flush=True)
     if ring is not None:

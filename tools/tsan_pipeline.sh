@@ -35,7 +35,9 @@ if [ "$SAN" = address ]; then
   ASAN_OPTIONS="detect_leaks=0:halt_on_error=1:protect_shadow_gap=0" UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1" \
     $B/pipeline_driver $S
 else
-  TSAN_OPTIONS="halt_on_error=1 second_deadlock_stack=1 suppressions=$R/tools/tsan_rocm.supp" \
+  # TSAN_SUPP / TSAN_HALT: another suppression file (e.g. /dev/null) and
+  # halt_on_error=0 -- to list the ROCm-runtime reports the file suppresses
+  TSAN_OPTIONS="halt_on_error=${TSAN_HALT:-1} second_deadlock_stack=1 suppressions=${TSAN_SUPP:-$R/tools/tsan_rocm.supp}" \
     setarch "$(uname -m)" -R $B/pipeline_driver $S
 fi
 rm -rf $S
