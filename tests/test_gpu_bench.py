@@ -215,7 +215,10 @@ def test_bench_live_profile_on_its_own_box(bcp, mode):
     assert rf["profiled_in_process"] is True and live["in_process"] is True
     assert live["rocprof_timed_launches"] == 4 and len(live["rocprof_timed_ms_steps"]) == 4
     assert live["tagged_dispatches"] == 2 + 4 + 1
-    assert 0.9 < live["event_over_rocprof"] < 1.1, live
+    # the events of a step bracket the fold alone in gen; in mixed mode also the
+    # step's desc_tiles and, on an idle queue, its host staging (tiny steps here)
+    hi = 1.1 if mode == "gen" else 1.3
+    assert 0.9 < live["event_over_rocprof"] < hi and 0.9 < live["event_over_rocprof_median"] < hi, live
     assert live["rocprof_min_ns"] <= live["rocprof_median_ns"] <= live["rocprof_max_ns"]
     assert 0.99 < live["traffic_over_algorithmic"] < 1.02, live
     assert rf["same_box"] is True and rf["traffic"] == live["traffic"]
