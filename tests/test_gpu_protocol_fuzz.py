@@ -4,7 +4,8 @@ same test with a larger budget is a soak).  Each round draws a store (3..16
 targets), a worklist (widths 1..15, chunk lengths from 0 B to 4 MiB, now and
 then past the 10 MiB transfer window so sources replay their last window,
 quirk A3-q1; a chunk file missing after planning), the P-role fold
-(pipelined or batched) or the pipeline, the lanes, the padding rule on the
+(pipelined through the fold ring, pipelined on the lanes' queues, or
+batched) or the pipeline, the lanes, the padding rule on the
 wire (implicit / the reference's) and the fold service width; every parity
 file must equal the oracle's (oracle.gen_parity_file, the reference's
 parity_generator restated).  Then a random target is lost and rebuilt by
@@ -58,13 +59,13 @@ def _worklist(rng, ntargets):
 
 def test_random_rounds_match_the_oracle(bcp, oracle, tmp_path):
     fuzz_rounds(bcp, oracle, tmp_path, float(os.environ.get("BCP_FUZZ_SECONDS", "8")),
-                int(os.environ.get("BCP_FUZZ_SEED", "3")), ("pipelined", "batched", "pipeline"))
+                int(os.environ.get("BCP_FUZZ_SEED", "3")), ("pipelined", "pipelined_queues", "batched", "pipeline"))
 
 
 def fuzz_rounds(bcp, oracle, tmp_path, budget, seed, engines):
     rng = np.random.default_rng(seed)
     prev = (bcp.set_fold_mode(bcp.FOLD_PIPELINED), bcp.set_rebuild_lanes(1), bcp.set_explicit_padding(bcp.PAD_AUTO),
-            bcp.set_fold_inflight(1))
+            bcp.set_fold_inflight(1), bcp.set_fold_ring(True))
     t_end = time.monotonic() + budget
     rounds = files_done = 0
     seen = set()
@@ -106,7 +107,10 @@ def fuzz_rounds(bcp, oracle, tmp_path, budget, seed, engines):
                 bcp.set_fold_mode(bcp.FOLD_PIPELINED)
                 st = bcp.gen_run_procs(root, ntargets, items, nlanes=int(rng.integers(1, 13)))
             else:
-                bcp.set_fold_mode(bcp.FOLD_PIPELINED if how == "pipelined" else bcp.FOLD_BATCHED)
+                # pipelined: through the device's fold ring (lane deferral in the runner's lanes);
+                # pipelined_queues: range launches on the lanes' queues
+                bcp.set_fold_mode(bcp.FOLD_BATCHED if how == "batched" else bcp.FOLD_PIPELINED)
+                bcp.set_fold_ring(how != "pipelined_queues")
                 st = bcp.gen_run(root, ntargets, items, nlanes=int(rng.integers(1, 13)))
             assert st.errors == 0, what
             for (path, holders, p, lens) in files:
@@ -145,5 +149,6 @@ def fuzz_rounds(bcp, oracle, tmp_path, budget, seed, engines):
         bcp.set_rebuild_lanes(prev[1])
         bcp.set_explicit_padding(prev[2])
         bcp.set_fold_inflight(prev[3])
+        bcp.set_fold_ring(prev[4])
     print(f"protocol fuzz: {rounds} rounds, {files_done} stripes, engines {sorted(seen)}")
     assert rounds >= 2
