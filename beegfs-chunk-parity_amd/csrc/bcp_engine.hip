@@ -24,6 +24,9 @@
 #include <algorithm>
 #include <atomic>
 #include <new>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -793,31 +796,86 @@ static int desc_vecs_for(const bcp_engine *e, uint64_t tiles8) {
   return 8;
 }
 
-// fn(lo, hi) over [0, n): on this thread, or split over up to 8 threads when
-// there are at least 2 * per items (thread start-up costs ~10-20 us each).
+// Host staging threads: a small pool made on first use (7 threads that sleep
+// between jobs), so a large batch's staging does not pay thread start-ups
+// (~15 us each) on the path to its kernel.  One job at a time; a caller that
+// finds the pool busy stages on its own thread.
+namespace {
+struct StagePool {
+  std::mutex run;  // one job at a time (try_lock)
+  std::mutex mu;
+  std::condition_variable go, fin;
+  const std::function<void(uint32_t)> *job = nullptr;
+  uint32_t nparts = 0, claimed = 0, done = 0;
+  uint64_t gen = 0;
+  int nthreads = 0;
+
+  void work_on(std::unique_lock<std::mutex> &lk) {  // with mu held: take parts until none is left
+    while (claimed < nparts) {
+      const uint32_t i = claimed++;
+      const std::function<void(uint32_t)> *j = job;
+      lk.unlock();
+      (*j)(i);
+      lk.lock();
+      if (++done == nparts) fin.notify_all();
+    }
+  }
+  void loop() {
+    uint64_t seen = 0;
+    std::unique_lock<std::mutex> lk(mu);
+    for (;;) {
+      go.wait(lk, [&] { return gen != seen; });
+      seen = gen;
+      work_on(lk);
+    }
+  }
+};
+
+StagePool *stage_pool() {
+  static StagePool *P = [] {
+    StagePool *p = new StagePool();  // never freed: its threads live as long as the process
+    for (int t = 0; t < 7; t++) {
+      try {
+        std::thread(&StagePool::loop, p).detach();
+        p->nthreads++;
+      } catch (...) {
+        break;
+      }
+    }
+    return p;
+  }();
+  return P;
+}
+}  // namespace
+
+// fn(lo, hi) over [0, n): on this thread, or split over the staging pool and
+// this thread when there are at least 2 * per items.
 template <typename F>
 static void par_for(uint32_t n, uint32_t per, F fn) {
-  const uint32_t want = n / (per ? per : 1);
-  const uint32_t nt = std::min<uint32_t>(8, want);
-  if (nt < 2) {
+  uint32_t nt = std::min<uint32_t>(8, n / (per ? per : 1));
+  StagePool *P = nt >= 2 ? stage_pool() : nullptr;
+  if (P) nt = std::min<uint32_t>(nt, (uint32_t)P->nthreads + 1);
+  if (nt < 2 || !P->run.try_lock()) {
     fn(0, n);
     return;
   }
-  std::thread th[8];
-  bool started[8] = {};
   const uint32_t chunk = (n + nt - 1) / nt;
-  for (uint32_t t = 1; t < nt; t++) {
-    const uint32_t lo = std::min(n, t * chunk), hi = std::min(n, lo + chunk);
-    try {
-      th[t] = std::thread(fn, lo, hi);
-      started[t] = true;
-    } catch (...) {
-      fn(lo, hi);  // no thread: on this one
-    }
+  const std::function<void(uint32_t)> job = [&](uint32_t i) {
+    const uint32_t lo = std::min(n, i * chunk), hi = std::min(n, lo + chunk);
+    if (lo < hi) fn(lo, hi);
+  };
+  {
+    std::unique_lock<std::mutex> lk(P->mu);
+    P->job = &job;
+    P->nparts = nt;
+    P->claimed = P->done = 0;
+    P->gen++;
+    P->go.notify_all();
+    P->work_on(lk);  // this thread takes parts too
+    P->fin.wait(lk, [&] { return P->done == P->nparts; });
+    P->job = nullptr;
   }
-  fn(0, std::min(n, chunk));
-  for (uint32_t t = 1; t < nt; t++)
-    if (started[t]) th[t].join();
+  P->run.unlock();
 }
 
 // Small batches (engine option desc_args_max, default kArgStripes stripes):
