@@ -124,6 +124,7 @@ _SIGS = {
     "bcp_ring_destroy": ([_V], ctypes.c_int),
     "bcp_ring_set_wait": ([_V, ctypes.c_int, ctypes.c_int], ctypes.c_int),
     "bcp_task_set_ring_wait": ([ctypes.c_int, ctypes.c_int], ctypes.c_int),
+    "bcp_task_set_fold_tuning": ([ctypes.c_char_p, ctypes.c_int], ctypes.c_int),
     "bcp_ring_stats": ([_V, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)], ctypes.c_int),
     "bcp_dev_fill_synthetic_async": ([_V, _V, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64], ctypes.c_int),
     "bcp_dev_xor_fold_async": ([_V, _V, ctypes.c_uint64, _V], ctypes.c_int),
@@ -839,6 +840,13 @@ def set_fold_inflight(k: int) -> int:
     if rc < 0:
         raise BcpError("bcp_task_set_fold_inflight", rc)
     return rc
+
+
+def set_fold_tuning(key: str, value: int) -> int:
+    """The P role's fold shape for tools / A/B runs (bcp_task_set_fold_tuning); returns the previous value."""
+    prev = lib().bcp_task_set_fold_tuning(key.encode(), value)
+    check("bcp_task_set_fold_tuning", min(prev, 0))
+    return prev
 
 
 def round_timing() -> dict:

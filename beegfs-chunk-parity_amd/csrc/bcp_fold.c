@@ -103,7 +103,41 @@ static int g_ring_rc[BCPF_MAX_DEVICES];
 static int g_fold_ring = 1;
 static uint64_t g_ring_pieces, g_ring_launches; /* of rings already destroyed */
 static int g_ring_spin_us = -1, g_ring_sleep_us = -1; /* bcp_task_set_ring_wait; -1: the engine's */
-#define RING_WORKERS 16
+static int g_ring_workers = 16;
+/* The pipelined fold's shape (bcp_task_set_fold_tuning): a source publishes
+ * its row after every g_pipe_piece bytes read; a range is folded once every
+ * row has at least max(g_pipe_step, window / 4) more bytes. */
+static size_t g_pipe_piece = (size_t)256 << 10;
+static size_t g_pipe_step = (size_t)128 << 10;
+static int g_defer_depth = 1;
+
+size_t bcpf_watch_piece(void) { return __atomic_load_n(&g_pipe_piece, __ATOMIC_RELAXED); }
+int bcpi_defer_depth(void) { return __atomic_load_n(&g_defer_depth, __ATOMIC_RELAXED); }
+
+int bcp_task_set_fold_tuning(const char *key, int value)
+{
+    if (!key)
+        return -EINVAL;
+    int prev;
+    pthread_mutex_lock(&g_mu);
+    if (!strcmp(key, "ring_workers") && value >= 1 && value <= 1024) {
+        prev = g_ring_workers;
+        g_ring_workers = value; /* rings made from now on (bcp_task_shutdown ends the current ones) */
+    } else if (!strcmp(key, "pipe_piece_kib") && value >= 4 && value <= 10240) {
+        prev = (int)(g_pipe_piece >> 10);
+        __atomic_store_n(&g_pipe_piece, (size_t)value << 10, __ATOMIC_RELAXED);
+    } else if (!strcmp(key, "pipe_step_kib") && value >= 4 && value <= 10240) {
+        prev = (int)(g_pipe_step >> 10);
+        g_pipe_step = (size_t)value << 10;
+    } else if (!strcmp(key, "defer_depth") && value >= 0 && value <= BCP_DEFER_MAX) {
+        prev = g_defer_depth;
+        __atomic_store_n(&g_defer_depth, value, __ATOMIC_RELAXED);
+    } else {
+        prev = -EINVAL;
+    }
+    pthread_mutex_unlock(&g_mu);
+    return prev;
+}
 
 int bcp_task_set_fold_ring(int on)
 {
@@ -130,7 +164,7 @@ bcp_ring *bcpf_ring_for(int dev, bcp_engine *e)
         return NULL;
     pthread_mutex_lock(&g_mu);
     if (!g_ring[dev] && !g_ring_rc[dev]) {
-        g_ring_rc[dev] = bcp_ring_create(e, RING_WORKERS, 0, &g_ring[dev]);
+        g_ring_rc[dev] = bcp_ring_create(e, g_ring_workers, 0, &g_ring[dev]);
         if (!g_ring_rc[dev] && g_ring_spin_us >= 0)
             (void)bcp_ring_set_wait(g_ring[dev], g_ring_spin_us, g_ring_sleep_us);
     }
@@ -576,7 +610,6 @@ int bcpf_fold_window(fold_res *R, HostState *hs, int tag, bcp_xor_hook_fn hook, 
  * around the receives, and every fill into the rows has returned before the
  * receives complete, so no publish can reach a watch after its window. */
 #define WATCH_SLOTS 4096u
-#define PIPE_STEP ((size_t)128 << 10) /* smallest range worth a launch (also >= a quarter window) */
 #define PIPE_ALIGN ((size_t)4096)     /* range boundaries */
 
 typedef struct {
@@ -748,7 +781,10 @@ int bcpf_watch_rows(row_watch *W, fold_res *R, bcp_ring *ring, bcp_xor_hook_fn h
     W->lo = 0;
     W->valid = valid;
     W->out = out;
-    W->step = MAX_(PIPE_STEP, nbytes / 4); /* at most ~5 launches per window */
+    pthread_mutex_lock(&g_mu);
+    const size_t step = g_pipe_step;
+    pthread_mutex_unlock(&g_mu);
+    W->step = MAX_(step, nbytes / 4); /* at most ~5 ranges per window */
     W->n = n;
     for (int j = 0; j < n; j++)
         if (watch_add(rows + (size_t)j * pitch, W, j)) {

@@ -88,8 +88,10 @@ typedef struct row_watch {
 } row_watch;
 #define BCPF_WATCH_HANDLES 8
 
-/* Bytes a source reads between two publishes of its row's final prefix. */
-#define BCPF_WATCH_PIECE ((size_t)256 << 10)
+/* Bytes a source reads between two publishes of its row's final prefix
+ * (256 KiB; bcp_task_set_fold_tuning "pipe_piece_kib"). */
+size_t bcpf_watch_piece(void);
+
 
 /* Register the window's n rows (1), or 0 when the table is full (fold it
  * whole).  The ranges go to `ring` when it is given, else R->q must exist

@@ -217,7 +217,7 @@ void *bcpr_gen_lane(void *p)
     bcp_lb_set_rank(a->rank);
     /* a lane without a DB lets its P tasks' writes trail by one task (a DB
      * entry must not precede its parity file) */
-    (void)bcp_task_set_lane_deferral(a->db == NULL);
+    (void)bcp_task_set_lane_deferral(a->db == NULL ? bcpi_defer_depth() : 0);
     TaskInfo ti = {a->hs->read_chunk_dir, 0, -1, a->lane, &a->sample};
     for (size_t i = 0; i < a->nitems; i++) {
         if (a->lanes[i] != a->lane)
@@ -422,7 +422,7 @@ void *bcpr_rebuild_rank(void *p)
     if (a->gate && !bcpr_gate_pass(a->gate))
         return NULL;
     bcp_lb_set_rank(a->rank);
-    (void)bcp_task_set_lane_deferral(1);
+    (void)bcp_task_set_lane_deferral(bcpi_defer_depth());
     const int my_st = a->hs->storage_target;
     const int victim = a->rebuild_target;
     const int nl = a->nlanes > 1 ? a->nlanes : 1;

@@ -236,12 +236,14 @@ typedef struct {
     uint64_t final_total;
 } deferred_p;
 
-static __thread deferred_p t_def;
+/* This lane's deferred P tasks, oldest first (at most t_defer_on). */
+static __thread deferred_p t_def[BCP_DEFER_MAX];
+static __thread int t_ndef;
 static __thread int t_defer_on;
 
 int bcp_task_set_lane_deferral(int on)
 {
-    if (on != 0 && on != 1)
+    if (on < 0 || on > BCP_DEFER_MAX)
         return -EINVAL;
     const int prev = t_defer_on;
     t_defer_on = on;
@@ -287,11 +289,22 @@ static void deferred_complete(deferred_p *d)
     phase_add(BCP_PHASE_P_WRITE, &tph);
 }
 
-void bcp_task_flush(void) { deferred_complete(&t_def); }
+/* Complete this lane's oldest deferred tasks until at most `keep` remain. */
+static void deferred_trim(int keep)
+{
+    while (t_ndef > keep) {
+        deferred_complete(&t_def[0]);
+        for (int i = 1; i < t_ndef; i++)
+            t_def[i - 1] = t_def[i];
+        t_ndef--;
+    }
+}
+
+void bcp_task_flush(void) { deferred_trim(0); }
 
 void bcp_task_thread_release(void)
 {
-    deferred_complete(&t_def);
+    deferred_trim(0);
     free(t_res.send_buf);
     t_res.send_buf = NULL;
     t_res.send_cap = 0;
@@ -690,9 +703,10 @@ static void parity_generator(const task_settings *ts, const char *path, const Fi
                     deferred_complete(&d);
                     d.path = NULL;
                 } else {
-                    /* this fold is on the device: now the previous task's part */
-                    deferred_complete(&t_def);
-                    t_def = d;
+                    /* this fold is on the device: now the oldest tasks' parts
+                     * beyond the lane's depth */
+                    deferred_trim(t_defer_on - 1);
+                    t_def[t_ndef++] = d;
                 }
                 deferred = 1;
                 if (ti.sample)
@@ -812,7 +826,7 @@ static void fill_bytes(window_fill *w, uint8_t *data, size_t n)
         while (got < want) {
             ssize_t k = got && bcpi_inject_hit(BCP_INJECT_READ)
                             ? (errno = EIO, -1)
-                            : read(w->fd, data + got, MIN_(BCPF_WATCH_PIECE, want - got));
+                            : read(w->fd, data + got, MIN_(bcpf_watch_piece(), want - got));
             if (k <= 0) {
                 r = k < 0 ? k : (ssize_t)got;
                 break;
@@ -984,8 +998,9 @@ done:
         close(fd);
     phase_add(BCP_PHASE_S_SEND, &tph);
     __atomic_fetch_add(&g_phase_ns[BCP_PHASE_S_TASKS], 1, __ATOMIC_RELAXED);
-    /* this lane's deferred P task (its fold had the sends' time to land) */
-    deferred_complete(&t_def);
+    /* this lane's deferred P tasks but the newest depth - 1 (their folds had
+     * the sends' time to land) */
+    deferred_trim(t_defer_on > 0 ? t_defer_on - 1 : 0);
 }
 
 int process_task(HostState *hs, const char *path, const FileInfo *fi, TaskInfo ti)

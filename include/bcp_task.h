@@ -171,21 +171,29 @@ int bcp_task_set_ring_wait(int spin_us, int sleep_us);
 /* Pieces (<= 512 KiB of parity each) published to the fold rings and
  * launches of them since the process started. */
 int bcp_task_ring_stats(uint64_t *pieces, uint64_t *launches);
-/* Lane deferral, for the CALLING THREAD (a lane): 1 -- a single-window P task
+/* Lane deferral, for the CALLING THREAD (a lane): d = 1..4 -- a single-window P task
  * whose fold goes to the fold ring returns once the fold is published; the
  * wait for it, the parity write (the rebuild's truncation) and the close
  * happen when this thread's next task has published its own fold or sent
- * its windows, or at bcp_task_flush / bcp_task_thread_release.  The lane's
- * next task then overlaps the previous one's fold and write.  Files, bytes
+ * its windows (the oldest beyond d - 1 of them), or at bcp_task_flush /
+ * bcp_task_thread_release.  The lane's next tasks then overlap the previous
+ * ones' folds and writes.  Files, bytes
  * and sticky errors are the same; an error of the deferred part becomes
  * sticky when it completes.  0 (default): process_task returns with the
  * parity written, as the reference's does.  libbcp's runners turn it on for
  * lanes that write no DB entries (a DB entry must not precede its file).
  * Returns the previous value or -EINVAL. */
 int bcp_task_set_lane_deferral(int on);
-/* Complete the calling thread's deferred P task, if any (a lane calls it
+/* Complete the calling thread's deferred P tasks, if any (a lane calls it
  * before its list's end is reported: MPI barrier, DB sync, exit). */
 void bcp_task_flush(void);
+/* Tools and A/B runs: the P role's fold shape.  "ring_workers" (16: worker
+ * workgroups of rings made from now on), "pipe_piece_kib" (256: bytes a
+ * source reads between two publishes of its row), "pipe_step_kib" (128: the
+ * smallest range folded before the window is complete, at least a quarter
+ * window), "defer_depth" (1: lane deferral depth of libbcp's runners,
+ * 0..4).  Returns the previous value or -EINVAL. */
+int bcp_task_set_fold_tuning(const char *key, int value);
 /* Wall time spent per protocol phase, summed over every task of every lane
  * since the last reset (seconds[i] for i < nphases; the last two entries are
  * task COUNTS, not seconds).  Returns BCP_PHASES.  P role: size exchange,

@@ -108,6 +108,23 @@ def fold_setup(fold, hooks):
             bcp.set_fold_mode(prev)
             bcp.set_fold_inflight(prev_k)
         return restore
+    if fold.startswith("gpu_ring@"):
+        # gpu_ring@piece=K,step=K,depth=D: the ring with another pipelined shape
+        # (bcp_task_set_fold_tuning: KiB per publish, smallest range, lane deferral depth)
+        keys = {"piece": "pipe_piece_kib", "step": "pipe_step_kib", "depth": "defer_depth"}
+        prev = bcp.set_fold_mode(bcp.FOLD_PIPELINED)
+        prev_ring = bcp.set_fold_ring(True)
+        olds = []
+        for kv in fold.split("@", 1)[1].split(","):
+            k, v = kv.split("=")
+            olds.append((keys[k], bcp.set_fold_tuning(keys[k], int(v))))
+
+        def restore_t():
+            for k, v in reversed(olds):
+                bcp.set_fold_tuning(k, v)
+            bcp.set_fold_ring(prev_ring)
+            bcp.set_fold_mode(prev)
+        return restore_t
     if fold.startswith("gpu_ring_w"):
         # gpu_ring_w<spin>_<sleep>: the ring with waiters spinning <spin> us,
         # then sleeping <sleep> us between looks (0: sched_yield)
@@ -189,7 +206,8 @@ def measure(name, folds, rounds, run_once, verify_fn, nbytes, hooks, extra=None,
                 b = batching.setdefault(f, {"windows": 0, "launches": 0})
                 b["windows"] += w1 - w0
                 b["launches"] += l1 - l0
-            if (f in ("gpu_pipelined", "gpu_ring", "gpu_queues") or f.startswith("gpu_ring_w")) and r > 0:
+            if (f in ("gpu_pipelined", "gpu_ring", "gpu_queues") or f.startswith("gpu_ring_w") or f.startswith("gpu_ring@")) \
+                    and r > 0:
                 b = batching.setdefault(f, {"windows": 0, "launches": 0})
                 b["windows"] += pw1 - pw0
                 b["launches"] += pr1 - pr0
@@ -209,7 +227,7 @@ def measure(name, folds, rounds, run_once, verify_fn, nbytes, hooks, extra=None,
                                          if cpu[f][-1][3] is not None else None),
                     throttled_periods=sum(c[1] for c in cpu[f][1:]),
                     throttled_ms_runs=[round(c[2], 1) for c in cpu[f]])
-        if (f in ("gpu_pipelined", "gpu_ring", "gpu_queues") or f.startswith("gpu_ring_w")) and \
+        if (f in ("gpu_pipelined", "gpu_ring", "gpu_queues") or f.startswith(("gpu_ring_w", "gpu_ring@"))) and \
                 batching.get(f, {}).get("windows"):
             line["range_folds_per_window"] = round(batching[f]["launches"] / batching[f]["windows"], 2)
         elif batching.get(f, {}).get("launches"):
