@@ -120,6 +120,9 @@ def parse():
                     help="config 5 through the protocol (rank 0, the e2e store): warm gen rounds per leg")
     ap.add_argument("--no-prof", action="store_true",
                     help="skip the live rocprofv3 kernel-trace and PMC passes of this workload on this box")
+    ap.add_argument("--profile-dir", default=None,
+                    help="keep rank 0's kernel trace (<dir>/trace) and the PMC passes (<dir>/pmc_fetch, pmc_write) "
+                         "there (tools/gpu_profiles.sh, the committed profile sets)")
     ap.add_argument("--allow-shared", action="store_true",
                     help="run N ranks even when fewer than N distinct GPUs exist (rehearsal; "
                          "the line then says shared_gpu true and counts distinct GPUs)")
@@ -277,7 +280,12 @@ def profiled_rank(a) -> int:
     import subprocess
     import tempfile
     exe = rocprof_exe()
-    out = tempfile.mkdtemp(prefix="bcp_bench_trace_")
+    keep = a.profile_dir is not None
+    if keep:
+        out = os.path.join(os.path.abspath(a.profile_dir), "trace")
+        os.makedirs(out, exist_ok=True)
+    else:
+        out = tempfile.mkdtemp(prefix="bcp_bench_trace_")
     env = dict(os.environ, **{PROFILED_ENV: "1"})
     me = [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]
     t0 = time.perf_counter()
@@ -292,7 +300,8 @@ def profiled_rank(a) -> int:
         line = _last_json(p.stdout)
     if line is None:
         import shutil
-        shutil.rmtree(out, ignore_errors=True)
+        if not keep:
+            shutil.rmtree(out, ignore_errors=True)
         return p.returncode or 1
     rf = line["roofline"]
     cfg = line["config"]
@@ -307,11 +316,13 @@ def profiled_rank(a) -> int:
         tr = {"error": f"trace: {type(e).__name__}: {e}"}
     finally:
         import shutil
-        shutil.rmtree(out, ignore_errors=True)
+        if not keep:
+            shutil.rmtree(out, ignore_errors=True)
     penv = {k: v for k, v in os.environ.items()
             if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK",
                          "MASTER_ADDR", "MASTER_PORT", PROFILED_ENV) and not k.startswith("TORCHELASTIC")}
-    pm = pmc_passes(workload_cmd(a), penv, rf["kernel_tag"], bps)
+    pm = pmc_passes(workload_cmd(a), penv, rf["kernel_tag"], bps,
+                    keep_dir=os.path.abspath(a.profile_dir) if keep else None)
     live = dict(tr)
     for k, v in pm.items():
         live[{"error": "pmc_error", "wall_s": "pmc_wall_s", "skipped": "pmc_skipped"}.get(k, k)] = v

@@ -1062,7 +1062,8 @@ def trace_figures(out_dir: str, kernel_tag: str, warmup: int, steps: int, bytes_
     return out
 
 
-def pmc_passes(child_cmd: list, env: dict, kernel_tag: str, bytes_per_step: int, timeout_s: float = 150) -> dict:
+def pmc_passes(child_cmd: list, env: dict, kernel_tag: str, bytes_per_step: int, timeout_s: float = 150,
+               keep_dir=None) -> dict:
     """HBM bytes per launch of the same workload on this box: `--pmc
     FETCH_SIZE` and `--pmc WRITE_SIZE` in child runs of their own (counters
     in separate passes, MI355X_MICROARCH.md's HBM recipe), FETCH_SIZE x2 (the
@@ -1078,11 +1079,11 @@ def pmc_passes(child_cmd: list, env: dict, kernel_tag: str, bytes_per_step: int,
     if not exe:
         return {"skipped": "rocprofv3 not on PATH"}
     t0 = time.perf_counter()
-    out = tempfile.mkdtemp(prefix="bcp_bench_pmc_")
+    out = keep_dir or tempfile.mkdtemp(prefix="bcp_bench_pmc_")
     try:
         vals = {}
         for name in ("FETCH_SIZE", "WRITE_SIZE"):
-            d_ = os.path.join(out, name)
+            d_ = os.path.join(out, {"FETCH_SIZE": "pmc_fetch", "WRITE_SIZE": "pmc_write"}[name])
             cmd = [exe, "--pmc", name, "-d", d_, "-o", "run", "--output-format", "csv", "--"] + child_cmd
             p = subprocess.Popen(cmd, env=env, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True,
                                  start_new_session=True)
@@ -1108,4 +1109,5 @@ def pmc_passes(child_cmd: list, env: dict, kernel_tag: str, bytes_per_step: int,
     except Exception as e:  # reported, never fatal: the committed set stands in
         return {"error": f"{type(e).__name__}: {e}", "wall_s": round(time.perf_counter() - t0, 1)}
     finally:
-        shutil.rmtree(out, ignore_errors=True)
+        if not keep_dir:
+            shutil.rmtree(out, ignore_errors=True)
