@@ -1,11 +1,18 @@
-/* Batched-pipeline driver for host-code sanitizer runs on a GPU box
- * (tools/tsan_pipeline.sh): a loopback store of mixed chunk sizes, parity gen
- * through bcp_pipeline_run with both read paths (COPY, DIRECT) and two
- * device lanes wrapping onto the visible GPUs (small slabs, few io threads,
- * so batches, slot reuse and the io pool's two job kinds all interleave),
- * every parity file checked against a CPU XOR written here; then one target
- * lost and rebuilt by bcp_pipeline_rebuild, compared with the lost chunks.
- * The host layer is built with -fsanitize=thread; the HIP objects are not. */
+/* Host-code sanitizer driver on a GPU box (tools/tsan_pipeline.sh): a
+ * loopback store of mixed chunk sizes.
+ *  1. The batched pipeline: parity gen through bcp_pipeline_run with both
+ *     read paths (COPY, DIRECT) and two device lanes wrapping onto the
+ *     visible GPUs (small slabs, few io threads, so batches, slot reuse and
+ *     the io pool's two job kinds all interleave); then one target lost and
+ *     rebuilt by bcp_pipeline_rebuild.
+ *  2. The per-task protocol over loopback ranks (bcp_gen_run, 3 lanes per
+ *     rank; bcp_rebuild_run), once through the resident fold ring with lane
+ *     deferral (the default) and once through the lane queues: ring
+ *     submission and waits from every P lane at once, deferred completions,
+ *     relaunches after the ring idles out between runs.
+ * Every parity file is checked against a CPU XOR written here and every
+ * rebuilt chunk against the lost one.  The C host layer and the engine's
+ * host code are built with -fsanitize=thread (clang); device code is not. */
 #define _GNU_SOURCE
 #include <errno.h>
 #include <fcntl.h>
@@ -71,14 +78,91 @@ static uint64_t rnd(void)
     return rng_state;
 }
 
+static const char *root;
+static bcp_work_item *items;
+static char (*names)[64];
+static uint8_t *chunk[NFILES][NT];
+static size_t len[NFILES][NT];
+
+/* every parity file = u64 sizes (ascending holders) + zero-padded XOR */
+static int check_parity(const char *what)
+{
+    char path[512];
+    int bad = 0;
+    for (int i = 0; i < NFILES; i++) {
+        const uint64_t loc = items[i].fi.locations;
+        const int p = (int)(loc >> 56);
+        size_t maxn = 0;
+        int n = 0;
+        for (int t = 0; t < NT; t++)
+            if (loc >> t & 1) {
+                n++;
+                maxn = len[i][t] > maxn ? len[i][t] : maxn;
+            }
+        uint8_t *want = calloc(8 * (size_t)n + maxn + 1, 1);
+        int k = 0;
+        for (int t = 0; t < NT; t++)
+            if (loc >> t & 1) {
+                memcpy(want + 8 * k++, &len[i][t], 8);
+                for (size_t j = 0; j < len[i][t]; j++)
+                    want[8 * (size_t)n + j] ^= chunk[i][t][j];
+            }
+        snprintf(path, sizeof path, "%s/st%d/parity/%s", root, p, names[i]);
+        size_t got_n = 0;
+        uint8_t *got = read_file(path, &got_n);
+        if (!got || got_n != 8 * (size_t)n + maxn || memcmp(got, want, got_n)) {
+            fprintf(stderr, "parity mismatch: %s file %s\n", what, names[i]);
+            bad++;
+        }
+        free(got);
+        free(want);
+    }
+    return bad;
+}
+
+static void remove_parity(void)
+{
+    char path[512];
+    for (int i = 0; i < NFILES; i++) {
+        snprintf(path, sizeof path, "%s/st%d/parity/%s", root, (int)(items[i].fi.locations >> 56), names[i]);
+        unlink(path);
+    }
+}
+
+static void lose_victim(void)
+{
+    char path[512];
+    for (int i = 0; i < NFILES; i++)
+        if (items[i].fi.locations >> VICTIM & 1) {
+            snprintf(path, sizeof path, "%s/st%d/chunks/%s", root, VICTIM, names[i]);
+            unlink(path);
+        }
+}
+
+static int check_victim(const char *what)
+{
+    char path[512];
+    int bad = 0;
+    for (int i = 0; i < NFILES; i++)
+        if (items[i].fi.locations >> VICTIM & 1) {
+            snprintf(path, sizeof path, "%s/st%d/chunks/%s", root, VICTIM, names[i]);
+            size_t got_n = 0;
+            uint8_t *got = read_file(path, &got_n);
+            if (!got || got_n != len[i][VICTIM] || memcmp(got, chunk[i][VICTIM], got_n)) {
+                fprintf(stderr, "rebuilt chunk mismatch: %s file %s\n", what, names[i]);
+                bad++;
+            }
+            free(got);
+        }
+    return bad;
+}
+
 int main(int argc, char **argv)
 {
-    const char *root = argc > 1 ? argv[1] : "/tmp/bcp_tsan_pipeline";
+    root = argc > 1 ? argv[1] : "/tmp/bcp_tsan_pipeline";
     char path[512];
-    bcp_work_item *items = calloc(NFILES, sizeof *items);
-    char (*names)[64] = calloc(NFILES, 64);
-    uint8_t *chunk[NFILES][NT] = {{0}};
-    size_t len[NFILES][NT] = {{0}};
+    items = calloc(NFILES, sizeof *items);
+    names = calloc(NFILES, 64);
     for (int i = 0; i < NFILES; i++) {
         const int p = i % NT;
         uint64_t loc = 0;
@@ -130,59 +214,39 @@ int main(int argc, char **argv)
             fprintf(stderr, "pipeline_run mode %d: rc=%d errors=%d\n", modes[m], rc, st.errors);
             return 1;
         }
-        /* every parity file = u64 sizes (ascending holders) + zero-padded XOR */
-        for (int i = 0; i < NFILES; i++) {
-            const uint64_t loc = items[i].fi.locations;
-            const int p = (int)(loc >> 56);
-            size_t maxn = 0;
-            int n = 0;
-            for (int t = 0; t < NT; t++)
-                if (loc >> t & 1) {
-                    n++;
-                    maxn = len[i][t] > maxn ? len[i][t] : maxn;
-                }
-            uint8_t *want = calloc(8 * (size_t)n + maxn + 1, 1);
-            int k = 0;
-            for (int t = 0; t < NT; t++)
-                if (loc >> t & 1) {
-                    memcpy(want + 8 * k++, &len[i][t], 8);
-                    for (size_t j = 0; j < len[i][t]; j++)
-                        want[8 * (size_t)n + j] ^= chunk[i][t][j];
-                }
-            snprintf(path, sizeof path, "%s/st%d/parity/%s", root, p, names[i]);
-            size_t got_n = 0;
-            uint8_t *got = read_file(path, &got_n);
-            if (!got || got_n != 8 * (size_t)n + maxn || memcmp(got, want, got_n)) {
-                fprintf(stderr, "parity mismatch: mode %d file %s\n", modes[m], names[i]);
-                bad++;
-            }
-            free(got);
-            free(want);
-        }
+        char what[32];
+        snprintf(what, sizeof what, "pipeline mode %d", modes[m]);
+        bad += check_parity(what);
         /* lose VICTIM, rebuild it (DB key order does not matter for the bytes) */
-        for (int i = 0; i < NFILES; i++)
-            if (items[i].fi.locations >> VICTIM & 1) {
-                snprintf(path, sizeof path, "%s/st%d/chunks/%s", root, VICTIM, names[i]);
-                unlink(path);
-            }
+        lose_victim();
         rc = bcp_pipeline_rebuild(pl, root, NT, VICTIM, items, NFILES, NULL, NULL, &st);
         if (rc || st.errors) {
             fprintf(stderr, "pipeline_rebuild mode %d: rc=%d errors=%d\n", modes[m], rc, st.errors);
             return 1;
         }
-        for (int i = 0; i < NFILES; i++)
-            if (items[i].fi.locations >> VICTIM & 1) {
-                snprintf(path, sizeof path, "%s/st%d/chunks/%s", root, VICTIM, names[i]);
-                size_t got_n = 0;
-                uint8_t *got = read_file(path, &got_n);
-                if (!got || got_n != len[i][VICTIM] || memcmp(got, chunk[i][VICTIM], got_n)) {
-                    fprintf(stderr, "rebuilt chunk mismatch: mode %d file %s\n", modes[m], names[i]);
-                    bad++;
-                }
-                free(got);
-            }
+        bad += check_victim(what);
         bcp_pipeline_destroy(pl);
     }
+    for (int ring = 1; ring >= 0; ring--) {
+        const char *what = ring ? "protocol, fold ring" : "protocol, lane queues";
+        bcp_task_set_fold_ring(ring);
+        remove_parity();
+        bcp_run_stats st;
+        int rc = bcp_gen_run(root, NT, items, NFILES, 3, NULL, NULL, &st);
+        if (rc || st.errors) {
+            fprintf(stderr, "gen_run %s: rc=%d errors=%d\n", what, rc, st.errors);
+            return 1;
+        }
+        bad += check_parity(what);
+        lose_victim();
+        rc = bcp_rebuild_run(root, NT, VICTIM, items, NFILES, NULL, NULL, &st);
+        if (rc || st.errors) {
+            fprintf(stderr, "rebuild_run %s: rc=%d errors=%d\n", what, rc, st.errors);
+            return 1;
+        }
+        bad += check_victim(what);
+    }
+    bcp_task_shutdown();
     printf("%s: %d problems\n", bad ? "FAILED" : "OK", bad);
     return bad ? 1 : 0;
 }

@@ -1,11 +1,13 @@
-"""Sanitizer runs of the batched pipeline's host code on the device
-(tools/tsan_pipeline.sh): the C host layer built with -fsanitize=thread
-(host code only; the HIP objects uninstrumented), tests/native/
-pipeline_driver.c running parity gen through both read paths and two device
-lanes with small slabs and few io threads -- batches, slot reuse, reads and
-parity writes interleaving in the one io pool -- every parity file checked
-against the driver's own CPU XOR, then a lost target rebuilt and compared.
-ThreadSanitizer, then AddressSanitizer + UBSan; fails on any report."""
+"""Sanitizer runs of libbcp's host code on the device (tools/tsan_pipeline.sh):
+tests/native/pipeline_driver.c runs parity gen and a rebuild through the
+batched pipeline (both read paths, two device lanes, small slabs and few io
+threads -- batches, slot reuse, reads and parity writes interleaving in the one
+io pool) and through the per-task protocol over loopback ranks (the resident
+fold ring with lane deferral, then the lane queues), every parity file checked
+against the driver's own CPU XOR and every rebuilt chunk against the lost one.
+ThreadSanitizer (the C host layer and the engine's host code instrumented,
+device code not), then AddressSanitizer + UBSan (the C host layer); fails on
+any report."""
 import os
 import subprocess
 
