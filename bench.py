@@ -123,6 +123,8 @@ def parse():
     ap.add_argument("--profile-dir", default=None,
                     help="keep rank 0's kernel trace (<dir>/trace) and the PMC passes (<dir>/pmc_fetch, pmc_write) "
                          "there (tools/gpu_profiles.sh, the committed profile sets)")
+    ap.add_argument("--device-helper", default=None, metavar="RANK,WORLD,LOCAL_RANK",
+                    help=argparse.SUPPRESS)  # internal: profiled_rank's device helper under rocprofv3
     ap.add_argument("--allow-shared", action="store_true",
                     help="run N ranks even when fewer than N distinct GPUs exist (rehearsal; "
                          "the line then says shared_gpu true and counts distinct GPUs)")
@@ -258,7 +260,8 @@ def run_leg(name: str, fn, *args):
         return {"error": f"{name}: {type(e).__name__}: {e}"}
 
 
-PROFILED_ENV = "BCP_BENCH_PROFILED"  # set in the rank process that runs under rocprofv3
+PROFILED_ENV = "BCP_BENCH_PROFILED"  # set in the device helper that runs under rocprofv3
+HELPER_TAG = "BCPDEV "  # the device helper's messages on its stdout
 
 
 def _last_json(text: str):
@@ -266,17 +269,87 @@ def _last_json(text: str):
     return json.loads(lines[-1]) if lines else None
 
 
-def profiled_rank(a) -> int:
-    """Rank 0 (or the one rank) runs as a CHILD process under `rocprofv3
-    --kernel-trace --stats` (started before this process touches HIP; never
-    an exec): the child is the rank -- it joins the job, times the steps,
-    runs every leg and prints the line -- and its own timed launches are in
-    the trace.  After it exits, this parent reads the trace (the rocprof
-    average of exactly the launches the line's HIP events timed, in the same
-    process), runs the two PMC passes of the same workload, puts both in the
-    line's roofline and prints it.  A child that cannot start under the
-    profiler (an exit status, no line) is run once more without it; a child
-    killed by a signal is not."""
+class DistCoord:
+    """device_phase's two collectives, in the rank process itself."""
+
+    def __init__(self, d):
+        self.d = d
+
+    def gather_bus(self, bus: str) -> list:
+        return self.d.gather(bus)
+
+    def barrier(self):
+        self.d.barrier()
+
+
+class PipeCoord:
+    """device_phase's collectives from the profiled device helper: each is a
+    message to the rank process (the helper's parent, the job's member), which
+    runs it in the job and answers on the helper's stdin."""
+
+    def _send(self, obj):
+        sys.stdout.write(HELPER_TAG + json.dumps(obj) + "\n")
+        sys.stdout.flush()
+
+    def _recv(self) -> dict:
+        line = sys.stdin.readline()
+        if not line:
+            raise SystemExit(5)  # the rank process is gone
+        return json.loads(line)
+
+    def gather_bus(self, bus: str) -> list:
+        self._send({"op": "gather_bus", "bus": bus})
+        return self._recv()["bus_ids"]
+
+    def barrier(self):
+        self._send({"op": "barrier"})
+        self._recv()
+
+    def done(self, dev: dict):
+        self._send({"op": "device", "dev": dev})
+
+
+def serve_helper(p, d) -> tuple:
+    """The rank process's side of PipeCoord: answer the helper's collectives in
+    the job until it exits; (its device figures or None, whether it got as far
+    as a collective, its exit status)."""
+    dev, started = None, False
+    for line in p.stdout:
+        if not line.startswith(HELPER_TAG):
+            sys.stderr.write(line)  # the helper's own output, kept off the line's stdout
+            continue
+        m = json.loads(line[len(HELPER_TAG):])
+        started = True
+        if m["op"] == "gather_bus":
+            reply = {"bus_ids": d.gather(m["bus"])}
+        elif m["op"] == "barrier":
+            d.barrier()
+            reply = {}
+        else:
+            dev = m["dev"]
+            continue
+        p.stdin.write(json.dumps(reply) + "\n")
+        p.stdin.flush()
+    p.stdin.close()
+    return dev, started, p.wait()
+
+
+def profiled_rank(a, d) -> int:
+    """Rank 0 (or the one rank): the device timing runs in a CHILD process
+    under `rocprofv3 --kernel-trace --stats` (this process has not touched HIP;
+    never an exec) -- the device helper, which sets up the stripes, times the
+    steps and verifies them, and sends its figures back; the helper's two
+    collectives (the bus-id gather, the barriers around the timed region) go
+    through this process, the job's member (PipeCoord / serve_helper).  So the
+    trace holds exactly the launches the line's HIP events time, and only the
+    device timing runs under the profiler: this process then runs the legs
+    (e2e, cpu_baseline, configs) itself, reads the trace (the rocprof average
+    of the timed launches), runs the two PMC passes of the same workload, puts
+    both in the line's roofline and prints it.  A helper that fails before its
+    first collective (or at one rank, any time) is replaced by the same device
+    phase in this process, without the profiler; one that fails later in an
+    N-rank job fails the rank."""
+    import shutil
     import subprocess
     import tempfile
     exe = rocprof_exe()
@@ -286,23 +359,32 @@ def profiled_rank(a) -> int:
         os.makedirs(out, exist_ok=True)
     else:
         out = tempfile.mkdtemp(prefix="bcp_bench_trace_")
-    env = dict(os.environ, **{PROFILED_ENV: "1"})
-    me = [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]
+    env = {k: v for k, v in os.environ.items() if k not in DIST_ENV and not k.startswith("TORCHELASTIC")}
+    env[PROFILED_ENV] = "1"
+    me = [sys.executable, os.path.abspath(__file__)] + sys.argv[1:] + [
+        "--device-helper", f"{d.rank},{d.world},{d.local_rank}"]
     t0 = time.perf_counter()
-    p = subprocess.run([exe, "--kernel-trace", "--stats", "-d", out, "-o", "run", "--output-format", "csv", "--"] + me,
-                       env=env, stdout=subprocess.PIPE, text=True)
-    line = _last_json(p.stdout)
+    p = subprocess.Popen([exe, "--kernel-trace", "--stats", "-d", out, "-o", "run", "--output-format", "csv", "--"]
+                         + me, env=env, stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True)
+    dev, started, rc = serve_helper(p, d)
     note = None
-    if line is None and p.returncode > 0:
-        note = f"the profiled run exited {p.returncode} without a line; run again without the profiler"
+    if dev is None:
+        if started and d.world > 1:  # the other ranks are inside a collective with it
+            print(f"bench.py: the profiled device helper exited {rc} in the middle of the run", file=sys.stderr)
+            if not keep:
+                shutil.rmtree(out, ignore_errors=True)
+            return rc or 1
+        note = f"the profiled device helper exited {rc} without its figures; timed without the profiler"
         print(f"bench.py: {note}", file=sys.stderr)
-        p = subprocess.run(me + ["--no-prof"], env=env, stdout=subprocess.PIPE, text=True)
-        line = _last_json(p.stdout)
+        dev = device_phase(a, d.rank, d.world, d.local_rank, DistCoord(d))
+    if dev.get("refused"):
+        return dev["refused"]
+    dev["profiled"] = note is None
+    line, rc2 = finish(a, d, dev)
     if line is None:
-        import shutil
         if not keep:
             shutil.rmtree(out, ignore_errors=True)
-        return p.returncode or 1
+        return rc2 or 1
     rf = line["roofline"]
     cfg = line["config"]
     bps = cfg["bytes_per_step_per_gpu"]
@@ -315,12 +397,10 @@ def profiled_rank(a) -> int:
     except Exception as e:
         tr = {"error": f"trace: {type(e).__name__}: {e}"}
     finally:
-        import shutil
         if not keep:
             shutil.rmtree(out, ignore_errors=True)
     penv = {k: v for k, v in os.environ.items()
-            if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK",
-                         "MASTER_ADDR", "MASTER_PORT", PROFILED_ENV) and not k.startswith("TORCHELASTIC")}
+            if k not in DIST_ENV and k != PROFILED_ENV and not k.startswith("TORCHELASTIC")}
     pm = pmc_passes(workload_cmd(a), penv, rf["kernel_tag"], bps,
                     keep_dir=os.path.abspath(a.profile_dir) if keep else None)
     live = dict(tr)
@@ -338,7 +418,11 @@ def profiled_rank(a) -> int:
         rf["profile_box"] = rf["run_box"]
         rf["same_box"] = True
     print(json.dumps(line), flush=True)
-    return p.returncode
+    return rc2
+
+
+DIST_ENV = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK", "MASTER_ADDR",
+            "MASTER_PORT")
 
 
 def workload_cmd(a) -> list:
@@ -357,36 +441,40 @@ def workload_cmd(a) -> list:
     return cmd
 
 
-def main():
-    a = parse()
-    if a.gpus < 1:
-        sys.exit("bench.py: --gpus must be >= 1")
-    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
-        sys.exit(launch_ranks(a))
-    # rank 0 runs under the profiler as a child (this process has not touched HIP)
-    if (not a.no_prof and PROFILED_ENV not in os.environ and int(os.environ.get("RANK", "0")) == 0
-            and rocprof_exe()):
-        if not a.stripes:
-            a.stripes = default_stripes(int(os.environ.get("WORLD_SIZE", "1")), 0)
-        sys.exit(profiled_rank(a))
-    d = Dist()
-    if d.world != a.gpus and d.rank == 0:
-        print(f"bench.py: note: launched with {d.world} ranks for --gpus {a.gpus}; "
-              f"the line reports the ranks and distinct GPUs actually used", file=sys.stderr)
+def mixed_lengths(stripes: int, N: int, C: int, rank: int) -> list:
+    """--mode mixed's stripe shapes (seeded per rank): log-uniform chunk
+    lengths in [64 KiB, 4 MiB], as many 8-wide stripes as fit config 2's input
+    volume (stripes x N x C)."""
+    import numpy as np
+    rng = np.random.default_rng(3 + rank)
+    budget = stripes * N * C
+    lens_all, tot = [], 0
+    while tot < budget:
+        ls = np.exp(rng.uniform(np.log(64 * KiB), np.log(4 * 1024 * KiB), size=N)).astype(np.int64)
+        lens_all.append(ls)
+        tot += int(ls.sum())
+    return lens_all
+
+
+def device_phase(a, rank: int, world: int, local_rank: int, coord) -> dict:
+    """The device timing of one rank: stripes set up in HBM, warm-up, the
+    timed steps between two barriers (coord: DistCoord in the rank process,
+    PipeCoord in the profiled device helper), one more step verified on the
+    device and against numpy.  Returns the figures finish() needs (JSON), or
+    {"refused": 4} when ranks share a GPU without --allow-shared."""
     ndev = bcp.device_count()
     assert ndev > 0, "bench.py needs a HIP device (there is no CPU path)"
-    eng = bcp.Engine(d.local_rank % ndev)
+    eng = bcp.Engine(local_rank % ndev)
     # physical GPUs in the job: ranks that map to the same device share it
-    bus_ids = d.gather(eng.pci_bus_id())
+    bus_ids = coord.gather_bus(eng.pci_bus_id())
     n_devices = len(set(bus_ids))
-    shared_gpu = n_devices < d.world
+    shared_gpu = n_devices < world
     if shared_gpu and not a.allow_shared:
-        if d.rank == 0:
-            print(f"bench.py: {d.world} ranks but only {n_devices} distinct GPU(s) (PCI bus ids "
+        if rank == 0:
+            print(f"bench.py: {world} ranks but only {n_devices} distinct GPU(s) (PCI bus ids "
                   f"{sorted(set(bus_ids))}); refusing (pass --allow-shared to rehearse)", file=sys.stderr)
         eng.close()
-        d.close()
-        sys.exit(4)
+        return {"refused": 4}
     if a.mode == "mixed":  # the timed kernel is the descriptor kernel
         if a.blocks_per_cu:
             eng.option("desc_blocks_per_cu", a.blocks_per_cu)
@@ -406,20 +494,12 @@ def main():
     # config 2 (100k chunks per GPU) up to 4 GPUs; at 8 GPUs config 4: 1,000,000
     # chunks = 125,000 stripes sharded 15,625 per GPU (bcp_dist.shard_range)
     if not a.stripes:
-        a.stripes = default_stripes(d.world, d.rank)
+        a.stripes = default_stripes(world, rank)
     S, N, C = a.stripes, a.nsrc, a.chunk
     chk = eng.alloc(64)
     lens_all = None
     if a.mode == "mixed":
-        import numpy as np
-        rng = np.random.default_rng(3 + d.rank)
-        # log-uniform lengths; as many stripes as fit the config-2 input volume
-        budget = S * N * C
-        lens_all, tot = [], 0
-        while tot < budget:
-            ls = np.exp(rng.uniform(np.log(64 * KiB), np.log(4 * 1024 * KiB), size=N)).astype(np.int64)
-            lens_all.append(ls)
-            tot += int(ls.sum())
+        lens_all = mixed_lengths(S, N, C, rank)
         align = lambda x: (x + 255) & ~255
         src_bytes = sum(int(sum(align(int(x)) for x in ls)) for ls in lens_all)
         out_bytes = sum(align(int(ls.max())) for ls in lens_all)
@@ -429,7 +509,7 @@ def main():
         src = eng.alloc(S * N * C)
         out = eng.alloc(S * C)
         src_bytes = S * N * C
-    q.fill_synthetic(src, src_bytes, seed=1 + d.rank)
+    q.fill_synthetic(src, src_bytes, seed=1 + rank)
 
     if a.mode == "mixed":
         stripes, sources, so_off, do_off = [], [], 0, 0
@@ -461,7 +541,7 @@ def main():
         bytes_per_step = S * (N + 1) * C
         kernel = "xor_stream<{N},{U},strided>"
         kernel_tag = "xor_stream<{N}, {U}, 0, "
-        cfg = gen_config_label(d.world, S)
+        cfg = gen_config_label(world, S)
         workload = f"{cfg}: parity gen, {S} stripes x {N} x {C // KiB} KiB device-resident per GPU"
     else:
         # config 3: parity first, then rebuild source index 3 from the other
@@ -513,7 +593,7 @@ def main():
     # carries the per-launch spread, not only the block's average
     g = -(-a.steps // 63)
     bounds = list(range(0, a.steps, g)) + [a.steps]
-    d.barrier()
+    coord.barrier()
     q.sync()
     t0 = time.perf_counter()
     q.mark(0)
@@ -523,7 +603,7 @@ def main():
             q.mark(bounds.index(i + 1))
     q.sync()
     t1 = time.perf_counter()
-    d.barrier()
+    coord.barrier()
     wall = t1 - t0
     seg_ms = [q.elapsed_ms(j, j + 1) / (bounds[j + 1] - bounds[j]) for j in range(len(bounds) - 1)]
     kern_ms = q.elapsed_ms(0, len(bounds) - 1) / a.steps  # avg launch duration on the kernel's stream
@@ -554,7 +634,7 @@ def main():
     q.memset(out, 0xA5, out_bytes if a.mode == "mixed" else S * C)
     step()
     q.sync()
-    rng = np.random.default_rng(7 + d.rank)
+    rng = np.random.default_rng(7 + rank)
 
     def sampled(idx, fetch_inputs, out_ptr, out_len):
         ok = True
@@ -599,6 +679,27 @@ def main():
         verified = int(f.view("<u8")[0]) == 0 and sampled(
             idx, lambda i: [dget(src + (i * N + victim) * C, C)], lambda i: out + i * C, C)
 
+    device = eng.device
+    q.close()
+    eng.close()
+    return {"rank": rank, "world": world, "device": device, "bus_ids": bus_ids, "n_devices": n_devices,
+            "shared_gpu": shared_gpu, "cus": cus, "devname": devname, "S": S, "N": N, "C": C, "U": U,
+            "kernel": kernel, "kernel_tag": kernel_tag, "workload": workload, "bytes_per_step": bytes_per_step,
+            "wall": wall, "kern_ms": kern_ms, "seg_ms": seg_ms, "g": g, "verified": bool(verified)}
+
+
+def finish(a, d, dev: dict) -> tuple:
+    """After the device phase (dev: device_phase's figures, this rank's): the
+    max-over-ranks reductions, the legs (bench_legs, each behind run_leg; they
+    run in the rank process, never under the profiler) and, on rank 0, the
+    line.  Returns (the line or None, exit status)."""
+    S, N, C, U = dev["S"], dev["N"], dev["C"], dev["U"]
+    kernel, kernel_tag, workload = dev["kernel"], dev["kernel_tag"], dev["workload"]
+    bytes_per_step, wall, kern_ms, seg_ms, g = (dev["bytes_per_step"], dev["wall"], dev["kern_ms"], dev["seg_ms"],
+                                                dev["g"])
+    verified, bus_ids, n_devices, shared_gpu = dev["verified"], dev["bus_ids"], dev["n_devices"], dev["shared_gpu"]
+    cus, devname = dev["cus"], dev["devname"]
+    lens_all = mixed_lengths(a.stripes, N, C, d.rank) if a.mode == "mixed" and not a.no_cpu and d.rank == 0 else None
     wall_max = d.max(wall)
     total_bytes = d.sum(float(bytes_per_step * a.steps))
     ok_all = d.sum(1.0 if verified else 0.0) == d.world
@@ -618,15 +719,14 @@ def main():
     # e2e_leg keeps every rank's collective calls in step whatever fails)
     e2e = None
     if not a.no_e2e:
-        q.sync()
-        e2e = e2e_leg(a, d, eng.device, bus_ids[d.rank])
+        e2e = e2e_leg(a, d, dev["device"], bus_ids[d.rank])
     # the reference CPU path, rank 0 only, after every device figure; the
     # other ranks wait at the barrier
     cpu = run_leg("cpu_baseline", cpu_baseline, a, N, C, lens_all if a.mode == "mixed" else None) \
         if d.rank == 0 and not a.no_cpu else None
     # BASELINE config 1 end to end (rank 0; the reference's xor_parity as the
     # P-role fold beside the GPU fold and the pipeline, same store)
-    c1 = run_leg("config1", config1_leg, a, eng.device) if d.rank == 0 and not a.no_configs else None
+    c1 = run_leg("config1", config1_leg, a, dev["device"]) if d.rank == 0 and not a.no_configs else None
     d.barrier()
 
     if d.rank == 0:
@@ -697,7 +797,8 @@ def main():
                 "traffic": pmc["hbm_bytes_per_launch"] if pmc else None,
                 "traffic_source": pmc["source"] if pmc else None,
                 "live_profile": None,
-                "profiled_in_process": PROFILED_ENV in os.environ,
+                # the timed launches ran in the device helper under rocprofv3 (profiled_rank); the legs not
+                "profiled_in_process": bool(dev.get("profiled")),
                 "profile_files": pmc.get("files") if pmc else None,
                 "profile_commit": pmc.get("code_commit") if pmc else None,
                 "run_box": run_box,
@@ -723,12 +824,41 @@ def main():
             **leg_blocks(cpu, c1, e2e),
             "per_rank": per_rank,
         }
-        print(json.dumps(line), flush=True)
-    q.close()
-    eng.close()
+    else:
+        line = None
     d.close()
-    if not ok_all:
-        sys.exit(3)
+    return line, (0 if ok_all else 3)
+
+
+def main():
+    a = parse()
+    if a.gpus < 1:
+        sys.exit("bench.py: --gpus must be >= 1")
+    if a.device_helper:  # the profiled device helper (profiled_rank's child)
+        rank, world, local_rank = (int(x) for x in a.device_helper.split(","))
+        pc = PipeCoord()
+        dev = device_phase(a, rank, world, local_rank, pc)
+        pc.done(dev)
+        sys.exit(0)
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        sys.exit(launch_ranks(a))
+    d = Dist()
+    if d.world != a.gpus and d.rank == 0:
+        print(f"bench.py: note: launched with {d.world} ranks for --gpus {a.gpus}; "
+              f"the line reports the ranks and distinct GPUs actually used", file=sys.stderr)
+    if not a.stripes:
+        a.stripes = default_stripes(d.world, d.rank)
+    # rank 0's device timing runs in a child under the profiler (this process has not touched HIP)
+    if not a.no_prof and d.rank == 0 and rocprof_exe():
+        sys.exit(profiled_rank(a, d))
+    dev = device_phase(a, d.rank, d.world, d.local_rank, DistCoord(d))
+    if dev.get("refused"):
+        d.close()
+        sys.exit(dev["refused"])
+    line, rc = finish(a, d, dev)
+    if line is not None:
+        print(json.dumps(line), flush=True)
+    sys.exit(rc)
 
 
 if __name__ == "__main__":

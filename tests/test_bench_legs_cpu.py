@@ -91,7 +91,7 @@ def test_trace_figures_average_the_timed_launches_only(tmp_path):
 FAKE_ROCPROF = textwrap.dedent('''\
     #!{py}
     """Stand-in rocprofv3: writes the csv files the real one writes and, for a
-    kernel trace, prints the line the profiled bench child would print."""
+    kernel trace, plays the device helper (bench.PipeCoord's messages)."""
     import json, os, sys
     args = sys.argv[1:]
     d = args[args.index("-d") + 1]
@@ -101,18 +101,31 @@ FAKE_ROCPROF = textwrap.dedent('''\
     if "--kernel-trace" in args:
         if mode == "fail":
             sys.exit(3)
-        assert os.environ.get("BCP_BENCH_PROFILED") == "1"
+        assert os.environ.get("BCP_BENCH_PROFILED") == "1" and "RANK" not in os.environ
+        assert "--device-helper" in args
+
+        def send(obj):
+            print("BCPDEV " + json.dumps(obj), flush=True)
+
+        def recv():
+            return json.loads(sys.stdin.readline())
+        print("noise before the messages", flush=True)
+        send({{"op": "gather_bus", "bus": "0000:00:00.0"}})
+        assert recv()["bus_ids"] == ["0000:00:00.0"]
+        send({{"op": "barrier"}})
+        recv()
+        send({{"op": "barrier"}})
+        recv()
         with open(os.path.join(d, "run_kernel_trace.csv"), "w") as f:
             f.write("Dispatch_Id,Kernel_Name,Start_Timestamp,End_Timestamp\\n")
             for i, dur in enumerate([9000000, 8400000, 8400000, 8400000, 7000000]):
                 f.write(f"{{i + 1}},\\"{{tag}}\\",{{i * 20000000}},{{i * 20000000 + dur}}\\n")
-        line = {{"warmup": 1, "steps": 3, "config": {{"bytes_per_step_per_gpu": 58982400000,
-                                                     "per_rank": [{{"kernel_ms": 8.4}}]}},
-                 "roofline": {{"kernel_tag": tag, "frac_event": 0.8778, "kernel_ms_steps": [8.4, 8.4, 8.4],
-                               "steps_per_event_pair": 1, "run_box": {{"boot_id": "b"}}, "frac_rocprof": None,
-                               "traffic": None, "same_box": False}}}}
-        print("noise before the line")
-        print(json.dumps(line))
+        send({{"op": "device", "dev": {{
+            "rank": 0, "world": 1, "device": 0, "bus_ids": ["0000:00:00.0"], "n_devices": 1, "shared_gpu": False,
+            "cus": 256, "devname": "fake", "S": 12500, "N": 8, "C": 524288, "U": 8,
+            "kernel": "xor_stream_w<8,8,strided,wpe6>", "kernel_tag": tag, "workload": "config2: fake",
+            "bytes_per_step": 58982400000, "wall": 0.0252, "kern_ms": 8.4, "seg_ms": [8.4, 8.4, 8.4], "g": 1,
+            "verified": True}}}})
         sys.exit(0)
     name = args[args.index("--pmc") + 1]
     assert "BCP_BENCH_PROFILED" not in os.environ and "RANK" not in os.environ
@@ -136,17 +149,25 @@ def fake_rocprof(tmp_path, monkeypatch):
     return exe
 
 
-def test_profiled_rank_patches_the_childs_line(fake_rocprof, monkeypatch, capsys):
-    """The parent relays the child's line with the rocprof figures of the
-    child's own timed launches and the PMC traffic of the same workload."""
+def test_profiled_rank_patches_the_line(fake_rocprof, monkeypatch, capsys):
+    """The device timing runs in the helper under the profiler, its collectives
+    answered by the rank process; the rank process makes the line (legs off
+    here) with the rocprof figures of the helper's own timed launches and the
+    PMC traffic of the same workload, and says the timed launches were
+    profiled."""
     import bench
-    monkeypatch.setattr(sys, "argv", ["bench.py", "--steps", "3", "--warmup", "1"])
+    from bcp_dist import Dist
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--steps", "3", "--warmup", "1", "--no-e2e", "--no-cpu",
+                                      "--no-configs"])
     a = bench.parse()
     a.stripes = 12_500
-    assert bench.profiled_rank(a) == 0
-    line = json.loads([x for x in capsys.readouterr().out.splitlines() if x.startswith("{")][-1])
+    assert bench.profiled_rank(a, Dist()) == 0
+    out, err = capsys.readouterr()
+    assert "noise before the messages" in err and "BCPDEV" not in out
+    line = json.loads([x for x in out.splitlines() if x.startswith("{")][-1])
     rf = line["roofline"]
     live = rf["live_profile"]
+    assert rf["profiled_in_process"] is True and line["config"]["verified_on_device"] is True
     assert live["in_process"] is True and live["rocprof_timed_launches"] == 3 and live["tagged_dispatches"] == 5
     assert live["rocprof_avg_ns"] == 8_400_000 and live["event_over_rocprof"] == 1.0
     assert rf["frac_rocprof"] == round(58982400000 / 8.4e-3 / 1e9 / 8000.0, 4)
@@ -154,18 +175,22 @@ def test_profiled_rank_patches_the_childs_line(fake_rocprof, monkeypatch, capsys
     assert rf["traffic"] == 25600000 * 1024 * 2 + 6400000 * 1024 and rf["same_box"] is True
     assert rf["profile_box"] == rf["run_box"]
     assert 0.99 < live["traffic_over_algorithmic"] < 1.01
+    assert line["value"] == round(58982400000 * 3 / 0.0252 / 1024 ** 3, 2)
 
 
-def test_profiled_rank_without_a_line_reruns_without_the_profiler(fake_rocprof, monkeypatch, capsys):
-    """rocprofv3 exits with a status and no line: one plain run follows (here
-    it cannot run either: no GPU), and no line is made up."""
+def test_profiled_rank_without_figures_times_in_process(fake_rocprof, monkeypatch, capsys):
+    """rocprofv3 exits with a status and no figures: the device phase runs in
+    the rank process without the profiler (here it cannot: no GPU, so it
+    fails loudly), and no line is made up."""
     import bench
+    from bcp_dist import Dist
     monkeypatch.setenv("FAKE_ROCPROF_MODE", "fail")
     monkeypatch.setattr(sys, "argv", ["bench.py", "--steps", "3", "--warmup", "1", "--no-e2e", "--no-cpu",
                                       "--no-configs"])
     a = bench.parse()
     a.stripes = 64
-    rc = bench.profiled_rank(a)
+    with pytest.raises(AssertionError, match="needs a HIP device"):
+        bench.profiled_rank(a, Dist())
     out, err = capsys.readouterr()
-    assert rc != 0 and not [x for x in out.splitlines() if x.startswith("{")]
+    assert not [x for x in out.splitlines() if x.startswith("{")]
     assert "without the profiler" in err
