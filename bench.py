@@ -25,13 +25,15 @@ ranks would share GPUs unless --allow-shared.
 
 roofline.achieved / frac (= frac_event) use the kernel's HIP-event time on the
 stream it runs on (an event pair at every step boundary: kernel_ms is the
-average, kernel_ms_median / min / max / steps the per-launch spread).  Rank 0
-runs as a child of its own process under `rocprofv3 --kernel-trace --stats`
-(profiled_rank: started before anything touches HIP, never an exec), so
-frac_rocprof is the rocprof average of the SAME timed launches in the same
-process (roofline.live_profile: event_over_rocprof); the parent then runs the
-PMC passes (FETCH_SIZE, WRITE_SIZE, runs of their own) of the same workload
-for traffic.  With --no-prof, or when a pass fails, the committed profile set
+average, kernel_ms_median / min / max / steps the per-launch spread).  Rank
+0's device timing runs in a child of the rank process under `rocprofv3
+--kernel-trace --stats` (profiled_rank: the device helper, started before
+anything touches HIP, never an exec; its barriers go through the rank
+process, which stays the job's member), so frac_rocprof is the rocprof
+average of the SAME timed launches (roofline.live_profile:
+event_over_rocprof), and nothing else runs under the profiler: the rank
+process then runs the legs itself and the PMC passes (FETCH_SIZE,
+WRITE_SIZE, runs of their own) of the same workload for traffic.  With --no-prof, or when a pass fails, the committed profile set
 of the workload (profiles/CURRENT_SET, profiles/**/*pmc*.json,
 tools/pmc_summary.py) stands in, reported as roofline.committed_set.
 The legs beside the device timing are bench_legs.py's, each behind run_leg.
