@@ -110,9 +110,11 @@ static int g_ring_workers = 16;
 static size_t g_pipe_piece = (size_t)256 << 10;
 static size_t g_pipe_step = (size_t)128 << 10;
 static int g_defer_depth = 1;
+static int g_completion_threads = 4;
 
 size_t bcpf_watch_piece(void) { return __atomic_load_n(&g_pipe_piece, __ATOMIC_RELAXED); }
 int bcpi_defer_depth(void) { return __atomic_load_n(&g_defer_depth, __ATOMIC_RELAXED); }
+int bcpi_completion_threads(void) { return __atomic_load_n(&g_completion_threads, __ATOMIC_RELAXED); }
 
 int bcp_task_set_fold_tuning(const char *key, int value)
 {
@@ -132,6 +134,9 @@ int bcp_task_set_fold_tuning(const char *key, int value)
     } else if (!strcmp(key, "defer_depth") && value >= 0 && value <= BCP_DEFER_MAX) {
         prev = g_defer_depth;
         __atomic_store_n(&g_defer_depth, value, __ATOMIC_RELAXED);
+    } else if (!strcmp(key, "completion_threads") && value >= 0 && value <= BCP_COMPLETION_MAX) {
+        prev = g_completion_threads; /* more start on next use; fewer after bcp_task_shutdown */
+        __atomic_store_n(&g_completion_threads, value, __ATOMIC_RELAXED);
     } else {
         prev = -EINVAL;
     }
@@ -876,6 +881,7 @@ int bcpf_ring_submit_window(bcp_ring *r, const uint8_t *rows, size_t pitch, cons
 int bcp_task_shutdown(void)
 {
     bcp_task_thread_release();
+    bcpt_completion_stop(); /* every lane has returned: the queue drains */
     /* fold services first: they hold queues on the engines (all lanes have
      * returned, so no batch is in flight) */
     pthread_mutex_lock(&g_mu);

@@ -62,6 +62,12 @@ int bcpi_fold_ring(void);
  * "defer_depth"). */
 int bcpi_defer_depth(void);
 #define BCP_DEFER_MAX 4
+/* Completion threads for deferred P tasks (4; bcp_task_set_fold_tuning
+ * "completion_threads", 0 = each lane completes its own). */
+#define BCP_COMPLETION_MAX 16
+int bcpi_completion_threads(void);
+/* Drain the deferred-completion queue and join its threads (bcp_task_shutdown). */
+void bcpt_completion_stop(void);
 /* Make [base, base + bytes) this process's arena slice (a memfd shared with
  * a node fold server, bcp_fold_server_connect). */
 void bcpi_arena_set(void *base, size_t bytes);

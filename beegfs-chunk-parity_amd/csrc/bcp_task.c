@@ -300,11 +300,139 @@ static void deferred_trim(int keep)
     }
 }
 
-void bcp_task_flush(void) { deferred_trim(0); }
+/* ---- completion threads ---------------------------------------------------
+ * The deferred part of a lane's tasks (fold wait, write, truncation, close)
+ * runs on a few threads of this process (bcp_task_set_fold_tuning
+ * "completion_threads", default 4), so the lane goes straight on to its next
+ * task; with 0 the lane completes its own, oldest first, when it next
+ * publishes (deferred_trim).  Either way a lane holds at most `depth`
+ * deferred tasks -- their rows stay reserved until they complete -- and
+ * bcp_task_flush waits for its own.  A lane thread that ends without a flush
+ * is flushed by its key's destructor.  bcp_task_shutdown drains the queue
+ * and joins the threads (bcpt_completion_stop). */
+typedef struct cq_item {
+    struct cq_item *next;
+    deferred_p d;
+    int *pending; /* the submitting lane's count */
+} cq_item;
+
+static pthread_mutex_t cq_mu = PTHREAD_MUTEX_INITIALIZER;
+static pthread_cond_t cq_work = PTHREAD_COND_INITIALIZER;
+static pthread_cond_t cq_done = PTHREAD_COND_INITIALIZER;
+static cq_item *cq_head, *cq_tail;
+static int cq_nthreads, cq_quit;
+static pthread_t cq_tid[BCP_COMPLETION_MAX];
+static __thread int t_pending; /* this lane's items in the queue or being completed */
+static pthread_key_t cq_key;
+static pthread_once_t cq_key_once = PTHREAD_ONCE_INIT;
+
+static void *cq_main(void *arg)
+{
+    (void)arg;
+    pthread_mutex_lock(&cq_mu);
+    for (;;) {
+        while (!cq_head && !cq_quit)
+            pthread_cond_wait(&cq_work, &cq_mu);
+        cq_item *it = cq_head;
+        if (!it)
+            break; /* stopping, and nothing is left */
+        cq_head = it->next;
+        if (!cq_head)
+            cq_tail = NULL;
+        pthread_mutex_unlock(&cq_mu);
+        deferred_complete(&it->d);
+        pthread_mutex_lock(&cq_mu);
+        (*it->pending)--;
+        pthread_cond_broadcast(&cq_done);
+        free(it);
+    }
+    pthread_mutex_unlock(&cq_mu);
+    return NULL;
+}
+
+static void cq_wait_own(int below)
+{
+    pthread_mutex_lock(&cq_mu);
+    while (t_pending > below)
+        pthread_cond_wait(&cq_done, &cq_mu);
+    pthread_mutex_unlock(&cq_mu);
+}
+
+static void cq_thread_end(void *v)
+{
+    (void)v;
+    deferred_trim(0);
+    cq_wait_own(0);
+}
+
+static void cq_make_key(void) { (void)pthread_key_create(&cq_key, cq_thread_end); }
+
+/* The completion threads wanted now, started on first use; 0 = none. */
+static int cq_threads(void)
+{
+    const int want = bcpi_completion_threads();
+    if (want <= 0)
+        return 0;
+    pthread_mutex_lock(&cq_mu);
+    while (cq_nthreads < want && !cq_quit && pthread_create(&cq_tid[cq_nthreads], NULL, cq_main, NULL) == 0)
+        cq_nthreads++;
+    const int n = cq_quit ? 0 : cq_nthreads;
+    pthread_mutex_unlock(&cq_mu);
+    return n;
+}
+
+/* Hand a published task's deferred part over: to the completion threads, or
+ * keep it on this lane (completing the oldest beyond depth - 1 first). */
+static void deferred_add(const deferred_p *d)
+{
+    cq_item *it = cq_threads() > 0 ? malloc(sizeof *it) : NULL;
+    if (!it) {
+        deferred_trim(t_defer_on - 1);
+        t_def[t_ndef++] = *d;
+        return;
+    }
+    (void)pthread_once(&cq_key_once, cq_make_key);
+    (void)pthread_setspecific(cq_key, (void *)1); /* flushed at thread end */
+    it->next = NULL;
+    it->d = *d;
+    it->pending = &t_pending;
+    pthread_mutex_lock(&cq_mu);
+    while (t_pending >= t_defer_on)
+        pthread_cond_wait(&cq_done, &cq_mu);
+    t_pending++;
+    if (cq_tail)
+        cq_tail->next = it;
+    else
+        cq_head = it;
+    cq_tail = it;
+    pthread_cond_signal(&cq_work);
+    pthread_mutex_unlock(&cq_mu);
+}
+
+void bcpt_completion_stop(void)
+{
+    pthread_mutex_lock(&cq_mu);
+    cq_quit = 1;
+    pthread_cond_broadcast(&cq_work);
+    const int n = cq_nthreads;
+    pthread_mutex_unlock(&cq_mu);
+    for (int i = 0; i < n; i++)
+        pthread_join(cq_tid[i], NULL);
+    pthread_mutex_lock(&cq_mu);
+    cq_nthreads = 0;
+    cq_quit = 0;
+    pthread_mutex_unlock(&cq_mu);
+}
+
+void bcp_task_flush(void)
+{
+    deferred_trim(0);
+    cq_wait_own(0);
+}
 
 void bcp_task_thread_release(void)
 {
-    deferred_trim(0);
+    bcp_task_flush();
     free(t_res.send_buf);
     t_res.send_buf = NULL;
     t_res.send_cap = 0;
@@ -703,10 +831,9 @@ static void parity_generator(const task_settings *ts, const char *path, const Fi
                     deferred_complete(&d);
                     d.path = NULL;
                 } else {
-                    /* this fold is on the device: now the oldest tasks' parts
-                     * beyond the lane's depth */
-                    deferred_trim(t_defer_on - 1);
-                    t_def[t_ndef++] = d;
+                    /* this fold is on the device: its completion goes to the
+                     * completion threads, or waits on this lane */
+                    deferred_add(&d);
                 }
                 deferred = 1;
                 if (ti.sample)

@@ -174,9 +174,12 @@ int bcp_task_ring_stats(uint64_t *pieces, uint64_t *launches);
 /* Lane deferral, for the CALLING THREAD (a lane): d = 1..4 -- a single-window P task
  * whose fold goes to the fold ring returns once the fold is published; the
  * wait for it, the parity write (the rebuild's truncation) and the close
- * happen when this thread's next task has published its own fold or sent
- * its windows (the oldest beyond d - 1 of them), or at bcp_task_flush /
- * bcp_task_thread_release.  The lane's next tasks then overlap the previous
+ * happen on the process's completion threads (bcp_task_set_fold_tuning
+ * "completion_threads"; with 0, on this thread when its next task has
+ * published its own fold or sent its windows, the oldest beyond d - 1 of
+ * them).  The thread holds at most d such tasks (its next publication waits
+ * for the oldest); bcp_task_flush / bcp_task_thread_release (or the thread's
+ * end) wait for all of them.  The lane's next tasks then overlap the previous
  * ones' folds and writes.  Files, bytes
  * and sticky errors are the same; an error of the deferred part becomes
  * sticky when it completes.  0 (default): process_task returns with the
@@ -192,7 +195,8 @@ void bcp_task_flush(void);
  * source reads between two publishes of its row), "pipe_step_kib" (128: the
  * smallest range folded before the window is complete, at least a quarter
  * window), "defer_depth" (1: lane deferral depth of libbcp's runners,
- * 0..4).  Returns the previous value or -EINVAL. */
+ * 0..4), "completion_threads" (4: threads completing deferred P tasks,
+ * 0..16; 0 = each lane completes its own).  Returns the previous value or -EINVAL. */
 int bcp_task_set_fold_tuning(const char *key, int value);
 /* Wall time spent per protocol phase, summed over every task of every lane
  * since the last reset (seconds[i] for i < nphases; the last two entries are

@@ -118,10 +118,23 @@ def test_config1_shape_small(bcp, oracle, tmp_path):
         assert S.read_file(S.parity_path(root, p, path)) == oracle.gen_parity_file(contents[path])
 
 
-def test_fold_ring_and_lane_queues_write_the_same_files(bcp, oracle, tmp_path):
+@pytest.mark.parametrize("completion,depth", [(4, 1), (0, 1), (2, 3)])
+def test_fold_ring_and_lane_queues_write_the_same_files(bcp, oracle, tmp_path, completion, depth):
     """Config 1's shape through the resident fold ring and through the lane
     queues: identical parity files and rebuilt chunks, every window of the
-    ring run published to the ring (one piece per range at least)."""
+    ring run published to the ring (one piece per range at least).  The
+    ring's deferred completions on the completion threads (default 4, and 2
+    with depth 3) and on the lanes themselves (0)."""
+    old_c = bcp.set_fold_tuning("completion_threads", completion)
+    old_d = bcp.set_fold_tuning("defer_depth", depth)
+    try:
+        _ring_vs_queues(bcp, oracle, tmp_path)
+    finally:
+        bcp.set_fold_tuning("completion_threads", old_c)
+        bcp.set_fold_tuning("defer_depth", old_d)
+
+
+def _ring_vs_queues(bcp, oracle, tmp_path):
     root = str(tmp_path)
     files = []
     for i in range(36):

@@ -109,9 +109,11 @@ def fold_setup(fold, hooks):
             bcp.set_fold_inflight(prev_k)
         return restore
     if fold.startswith("gpu_ring@"):
-        # gpu_ring@piece=K+step=K+depth=D: the ring with another pipelined shape
-        # (bcp_task_set_fold_tuning: KiB per publish, smallest range, lane deferral depth)
-        keys = {"piece": "pipe_piece_kib", "step": "pipe_step_kib", "depth": "defer_depth"}
+        # gpu_ring@piece=K+step=K+depth=D+completion=T: the ring with another pipelined shape
+        # (bcp_task_set_fold_tuning: KiB per publish, smallest range, lane deferral depth,
+        # completion threads)
+        keys = {"piece": "pipe_piece_kib", "step": "pipe_step_kib", "depth": "defer_depth",
+                "completion": "completion_threads"}
         prev = bcp.set_fold_mode(bcp.FOLD_PIPELINED)
         prev_ring = bcp.set_fold_ring(True)
         olds = []
