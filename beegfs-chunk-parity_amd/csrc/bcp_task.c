@@ -310,19 +310,26 @@ static void deferred_trim(int keep)
  * bcp_task_flush waits for its own.  A lane thread that ends without a flush
  * is flushed by its key's destructor.  bcp_task_shutdown drains the queue
  * and joins the threads (bcpt_completion_stop). */
+typedef struct {
+    int pending; /* this lane's items in the queue or being completed */
+    int init;
+    pthread_cond_t done; /* signalled (under cq_mu) when one of them completes */
+} cq_lane;
+
 typedef struct cq_item {
     struct cq_item *next;
     deferred_p d;
-    int *pending; /* the submitting lane's count */
+    cq_lane *lane; /* the submitting lane's */
 } cq_item;
 
 static pthread_mutex_t cq_mu = PTHREAD_MUTEX_INITIALIZER;
 static pthread_cond_t cq_work = PTHREAD_COND_INITIALIZER;
-static pthread_cond_t cq_done = PTHREAD_COND_INITIALIZER;
 static cq_item *cq_head, *cq_tail;
 static int cq_nthreads, cq_quit;
 static pthread_t cq_tid[BCP_COMPLETION_MAX];
-static __thread int t_pending; /* this lane's items in the queue or being completed */
+/* each lane waits on its own condition: a completion wakes its lane only,
+ * not every lane at its depth limit */
+static __thread cq_lane t_cq;
 static pthread_key_t cq_key;
 static pthread_once_t cq_key_once = PTHREAD_ONCE_INIT;
 
@@ -342,8 +349,8 @@ static void *cq_main(void *arg)
         pthread_mutex_unlock(&cq_mu);
         deferred_complete(&it->d);
         pthread_mutex_lock(&cq_mu);
-        (*it->pending)--;
-        pthread_cond_broadcast(&cq_done);
+        it->lane->pending--;
+        pthread_cond_signal(&it->lane->done);
         free(it);
     }
     pthread_mutex_unlock(&cq_mu);
@@ -352,9 +359,11 @@ static void *cq_main(void *arg)
 
 static void cq_wait_own(int below)
 {
+    if (!t_cq.init)
+        return; /* this thread never handed a task over */
     pthread_mutex_lock(&cq_mu);
-    while (t_pending > below)
-        pthread_cond_wait(&cq_done, &cq_mu);
+    while (t_cq.pending > below)
+        pthread_cond_wait(&t_cq.done, &cq_mu);
     pthread_mutex_unlock(&cq_mu);
 }
 
@@ -363,6 +372,10 @@ static void cq_thread_end(void *v)
     (void)v;
     deferred_trim(0);
     cq_wait_own(0);
+    if (t_cq.init) {
+        pthread_cond_destroy(&t_cq.done);
+        t_cq.init = 0;
+    }
 }
 
 static void cq_make_key(void) { (void)pthread_key_create(&cq_key, cq_thread_end); }
@@ -391,15 +404,19 @@ static void deferred_add(const deferred_p *d)
         t_def[t_ndef++] = *d;
         return;
     }
-    (void)pthread_once(&cq_key_once, cq_make_key);
-    (void)pthread_setspecific(cq_key, (void *)1); /* flushed at thread end */
+    if (!t_cq.init) {
+        (void)pthread_once(&cq_key_once, cq_make_key);
+        (void)pthread_setspecific(cq_key, (void *)1); /* flushed at thread end */
+        pthread_cond_init(&t_cq.done, NULL);
+        t_cq.init = 1;
+    }
     it->next = NULL;
     it->d = *d;
-    it->pending = &t_pending;
+    it->lane = &t_cq;
     pthread_mutex_lock(&cq_mu);
-    while (t_pending >= t_defer_on)
-        pthread_cond_wait(&cq_done, &cq_mu);
-    t_pending++;
+    while (t_cq.pending >= t_defer_on)
+        pthread_cond_wait(&t_cq.done, &cq_mu);
+    t_cq.pending++;
     if (cq_tail)
         cq_tail->next = it;
     else
