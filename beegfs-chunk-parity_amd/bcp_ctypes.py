@@ -774,7 +774,7 @@ def set_xor_hook(fn_addr: int | None, ctx: int | None = None):
 FOLD_BATCHED, FOLD_PIPELINED = 2, 5
 PAD_AUTO = -1
 INJECT_FOLD_RES, INJECT_DRAIN_ROW, INJECT_SEND_BUF, INJECT_THREAD, INJECT_READ = 1, 2, 4, 8, 16
-INJECT_FOLD_SERVER, INJECT_DIRECT_READ = 32, 64
+INJECT_FOLD_SERVER, INJECT_DIRECT_READ, INJECT_PARITY_WRITE = 32, 64, 128
 
 
 def set_fold_mode(mode: int) -> int:

@@ -153,7 +153,7 @@ static void settings_now(task_settings *s)
 }
 
 /* ---- failure injection (tests) ------------------------------------------ */
-#define NSITES 7
+#define NSITES 8
 static int g_inj_after[NSITES], g_inj_count[NSITES];
 
 static int site_index(int site)
@@ -166,6 +166,7 @@ static int site_index(int site)
     case BCP_INJECT_READ: return 4;
     case BCP_INJECT_FOLD_SERVER: return 5;
     case BCP_INJECT_DIRECT_READ: return 6;
+    case BCP_INJECT_PARITY_WRITE: return 7;
     default: return -1;
     }
 }
@@ -270,7 +271,7 @@ static void deferred_complete(deferred_p *d)
         }
     }
     if (!err) {
-        ssize_t wr = write(d->fd, d->pblk, d->wsize);
+        ssize_t wr = bcpi_inject_hit(BCP_INJECT_PARITY_WRITE) ? (errno = ENOSPC, -1) : write(d->fd, d->pblk, d->wsize);
         if (wr <= 0) {
             err = errno;
             LOGERR("write of '%s' failed with %d (%s) after %llu bytes\n", d->path, errno, strerror(errno),
@@ -872,7 +873,7 @@ static void parity_generator(const task_settings *ts, const char *path, const Fi
         phase_add(BCP_PHASE_P_FOLD, &tph);
         if (!have_had_error) {
             size_t wsize = (size_t)MIN_((uint64_t)buffer_size, data_left);
-            ssize_t wr = write(P_fd, pblk, wsize);
+            ssize_t wr = bcpi_inject_hit(BCP_INJECT_PARITY_WRITE) ? (errno = ENOSPC, -1) : write(P_fd, pblk, wsize);
             if (wr <= 0) {
                 have_had_error = errno;
                 LOGERR("write of '%s' failed with %d (%s) after %llu bytes\n", path, errno, strerror(errno),

@@ -241,8 +241,9 @@ void bcp_task_set_xor_hook(bcp_xor_hook_fn fn, void *ctx);
  * connection instead of answering a fold (the server process takes the
  * setting when a rank pool forks it), and the pipeline's O_DIRECT read of a
  * piece ending short before the end of its file (DIRECT read mode: the rest
- * of the piece is then read through the page cache).  count 0 clears the
- * site. */
+ * of the piece is then read through the page cache), and the P role's write
+ * of a parity window or rebuilt chunk (as ENOSPC; on the lane or on a
+ * completion thread).  count 0 clears the site. */
 #define BCP_INJECT_FOLD_RES 1
 #define BCP_INJECT_DRAIN_ROW 2
 #define BCP_INJECT_SEND_BUF 4
@@ -250,6 +251,7 @@ void bcp_task_set_xor_hook(bcp_xor_hook_fn fn, void *ctx);
 #define BCP_INJECT_READ 16
 #define BCP_INJECT_FOLD_SERVER 32
 #define BCP_INJECT_DIRECT_READ 64
+#define BCP_INJECT_PARITY_WRITE 128
 int bcp_task_inject_failure(int site, int after, int count);
 
 /* ---- transport seam (the MPI subset process_task speaks) ---------------- */

@@ -172,6 +172,34 @@ def _ring_vs_queues(bcp, oracle, tmp_path):
         bcp.set_fold_ring(prev)
 
 
+@pytest.mark.parametrize("completion", [4, 0])
+def test_deferred_parity_write_failure_is_sticky(bcp, oracle, tmp_path, completion):
+    """Through the fold ring with lane deferral, a parity write fails (ENOSPC,
+    injected) in a deferred completion -- on a completion thread (4) or on
+    the lane (0): exactly that rank's error is sticky, every other rank's
+    parity files are exact, rebuilds of a clean rerun are exact."""
+    root = str(tmp_path)
+    files = [(f"d/f{i}", [t for t in range(4) if t != i % 4], i % 4, [512 * KiB - 3 * i, 512 * KiB, 200 * KiB])
+             for i in range(24)]
+    items, contents = S.populate(root, 4, files, seed=31)
+    old_c = bcp.set_fold_tuning("completion_threads", completion)
+    bcp.inject_failure(bcp.INJECT_PARITY_WRITE, 5, 1)
+    try:
+        st = bcp.gen_run(root, 4, items)
+    finally:
+        bcp.inject_failure(bcp.INJECT_PARITY_WRITE, 0, 0)
+    try:
+        assert st.errors == 1
+        good = sum(1 for (path, _, p, _) in files if os.path.exists(S.parity_path(root, p, path))
+                   and S.read_file(S.parity_path(root, p, path)) == oracle.gen_parity_file(contents[path]))
+        assert 18 <= good < len(files)  # one rank of four failed: at most its 6 files
+        assert bcp.gen_run(root, 4, items).errors == 0
+        for (path, _, p, _) in files:
+            assert S.read_file(S.parity_path(root, p, path)) == oracle.gen_parity_file(contents[path]), path
+    finally:
+        bcp.set_fold_tuning("completion_threads", old_c)
+
+
 def test_fold_ring_idles_out_between_runs_and_shuts_down_live(bcp, oracle, tmp_path):
     """The ring's launch ends 5 ms after the last fold and the next run
     relaunches it; bcp_task_shutdown right after a run (launch still live)

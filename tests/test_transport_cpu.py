@@ -30,7 +30,7 @@ KiB, MiB = 1024, 1024 * 1024
 def _clean(bcp):
     yield
     for site in (bcp.INJECT_FOLD_RES, bcp.INJECT_DRAIN_ROW, bcp.INJECT_SEND_BUF, bcp.INJECT_THREAD,
-                 bcp.INJECT_FOLD_SERVER):
+                 bcp.INJECT_FOLD_SERVER, bcp.INJECT_PARITY_WRITE):
         bcp.inject_failure(site, 0, 0)
     bcp.set_transport(None)
 
@@ -244,6 +244,25 @@ def test_p_role_without_resources_drains_and_raises(bcp, oracle, cpu_hook, tmp_p
     # the failing rank's parity files (that task and its later ones) are missing;
     # every other rank's are exact
     assert 1 <= bad < len(files)
+
+
+@pytest.mark.timeout(120)
+def test_parity_write_failure_is_sticky_on_its_rank(bcp, oracle, cpu_hook, tmp_path):
+    """The P role's parity write fails (ENOSPC, injected) on one task: its
+    rank's error is sticky (that rank's later parity files go to the null
+    device), every other rank's files are exact, and the next run is clean."""
+    root, files, items, contents = _config(tmp_path)
+    bcp.inject_failure(bcp.INJECT_PARITY_WRITE, 3, 1)
+    st = bcp.gen_run(root, 6, items, nlanes=4)
+    assert st.errors == 1
+    good = sum(1 for (path, holders, p, lens) in files
+               if os.path.exists(S.parity_path(root, p, path))
+               and S.read_file(S.parity_path(root, p, path)) == oracle.gen_parity_file(contents[path]))
+    assert 1 <= len(files) - good < len(files)
+    bcp.inject_failure(bcp.INJECT_PARITY_WRITE, 0, 0)
+    assert bcp.gen_run(root, 6, items, nlanes=4).errors == 0
+    for (path, holders, p, lens) in files:
+        assert S.read_file(S.parity_path(root, p, path)) == oracle.gen_parity_file(contents[path]), path
 
 
 @pytest.mark.timeout(120)
