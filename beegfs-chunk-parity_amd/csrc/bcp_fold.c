@@ -134,6 +134,8 @@ int bcp_task_set_fold_tuning(const char *key, int value)
     } else if (!strcmp(key, "defer_depth") && value >= 0 && value <= BCP_DEFER_MAX) {
         prev = g_defer_depth;
         __atomic_store_n(&g_defer_depth, value, __ATOMIC_RELAXED);
+    } else if (!strcmp(key, "lb_spin_us") && value >= 0 && value <= 1000) {
+        prev = bcpi_lb_spin_us(value);
     } else if (!strcmp(key, "completion_threads") && value >= 0 && value <= BCP_COMPLETION_MAX) {
         prev = g_completion_threads; /* more start on next use; fewer after bcp_task_shutdown */
         __atomic_store_n(&g_completion_threads, value, __ATOMIC_RELAXED);

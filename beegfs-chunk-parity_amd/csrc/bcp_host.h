@@ -66,6 +66,10 @@ int bcpi_defer_depth(void);
  * "completion_threads", 0 = each lane completes its own). */
 #define BCP_COMPLETION_MAX 16
 int bcpi_completion_threads(void);
+/* The loopback transport's spin before a blocked wait sleeps, in us (0;
+ * bcp_task_set_fold_tuning "lb_spin_us"); us < 0 only reads.  Returns the
+ * previous value. */
+int bcpi_lb_spin_us(int us);
 /* Drain the deferred-completion queue and join its threads (bcp_task_shutdown). */
 void bcpt_completion_stop(void);
 /* Make [base, base + bytes) this process's arena slice (a memfd shared with

@@ -28,8 +28,51 @@
 #include <pthread.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
+#include "bcp_host.h"
 #include "bcp_task.h"
+
+/* Waiting: a blocked receive (and a fill send whose receive is not posted
+ * yet) first watches its flag for up to lb_spin_us (bcp_task_set_fold_tuning
+ * "lb_spin_us"), as MPI's shared-memory transports poll, then sleeps on its
+ * condition.  Completers set the flag with a release store under the channel
+ * lock; a waiter that saw it while spinning takes that lock once before it
+ * frees the request, so the completer's signal has returned. */
+static int g_lb_spin_ns;
+
+int bcpi_lb_spin_us(int us)
+{
+    const int prev = __atomic_load_n(&g_lb_spin_ns, __ATOMIC_RELAXED) / 1000;
+    if (us >= 0)
+        __atomic_store_n(&g_lb_spin_ns, us * 1000, __ATOMIC_RELAXED);
+    return prev;
+}
+
+static uint64_t lb_now_ns(void)
+{
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return (uint64_t)t.tv_sec * 1000000000u + (uint64_t)t.tv_nsec;
+}
+
+/* spin until *flag is non-zero or the budget is spent; 1 if it was seen */
+static int lb_spin_int(const int *flag)
+{
+    const int budget = __atomic_load_n(&g_lb_spin_ns, __ATOMIC_RELAXED);
+    if (budget <= 0)
+        return 0;
+    const uint64_t t0 = lb_now_ns();
+    for (;;) {
+        for (int i = 0; i < 64; i++) {
+            if (__atomic_load_n(flag, __ATOMIC_ACQUIRE))
+                return 1;
+            __builtin_ia32_pause();
+        }
+        if (lb_now_ns() - t0 >= (uint64_t)budget)
+            return 0;
+    }
+}
 
 struct bcp_lb_req;
 
@@ -42,6 +85,7 @@ typedef struct lb_msg {
     int done;            /* rendezvous: receiver finished copying */
     int fill;            /* fill send: payload produced by the sender into `target` */
     struct bcp_lb_req *target; /* fill send: the matched receive */
+    int target_set;      /* fill send: target is set (release store; spinning senders) */
     pthread_cond_t cv;   /* rendezvous sender waits here */
 } lb_msg;
 
@@ -210,7 +254,7 @@ static void complete_req(bcp_lb_req *r)
 {
     pthread_mutex_t *mu = r->mu;
     pthread_mutex_lock(mu);
-    r->done = 1;
+    __atomic_store_n(&r->done, 1, __ATOMIC_RELEASE);
     pthread_cond_signal(&r->cv);
     pthread_mutex_unlock(mu);
 }
@@ -309,6 +353,11 @@ int bcp_lb_send_fill(bcp_lb_fill_fn fill, void *ctx, size_t n, int dst, int tag)
         m.fill = 1;
         pthread_cond_init(&m.cv, NULL);
         push_inbox(d, &m);
+        if (__atomic_load_n(&g_lb_spin_ns, __ATOMIC_RELAXED) > 0) {
+            pthread_mutex_unlock(&d->mu);
+            (void)lb_spin_int((const int *)&m.target_set);
+            pthread_mutex_lock(&d->mu);
+        }
         while (!m.target)
             pthread_cond_wait(&m.cv, &d->mu);
         r = m.target;
@@ -393,6 +442,7 @@ int bcp_lb_irecv(void *buf, size_t n, int src, int tag, bcp_lb_req **req)
         /* hand the buffer to the sending thread; it completes r */
         r->next = NULL;
         m->target = r;
+        __atomic_store_n(&m->target_set, 1, __ATOMIC_RELEASE);
         pthread_cond_signal(&m->cv);
         pthread_mutex_unlock(&me->mu);
     } else if (m) {
@@ -425,7 +475,8 @@ int bcp_lb_wait(bcp_lb_req *r, size_t *received)
     if (!r)
         return -EINVAL;
     pthread_mutex_t *mu = r->mu;
-    pthread_mutex_lock(mu);
+    (void)lb_spin_int(&r->done);
+    pthread_mutex_lock(mu); /* also: the completer's signal has returned */
     while (!r->done)
         pthread_cond_wait(&r->cv, mu);
     pthread_mutex_unlock(mu);

@@ -196,7 +196,8 @@ void bcp_task_flush(void);
  * smallest range folded before the window is complete, at least a quarter
  * window), "defer_depth" (1: lane deferral depth of libbcp's runners,
  * 0..4), "completion_threads" (4: threads completing deferred P tasks,
- * 0..16; 0 = each lane completes its own).  Returns the previous value or -EINVAL. */
+ * 0..16; 0 = each lane completes its own), "lb_spin_us" (0: how long a
+ * blocked loopback receive or fill send polls before it sleeps, 0..1000).  Returns the previous value or -EINVAL. */
 int bcp_task_set_fold_tuning(const char *key, int value);
 /* Wall time spent per protocol phase, summed over every task of every lane
  * since the last reset (seconds[i] for i < nphases; the last two entries are

@@ -7,9 +7,10 @@
  *     rebuilt by bcp_pipeline_rebuild.
  *  2. The per-task protocol over loopback ranks (bcp_gen_run, 3 lanes per
  *     rank; bcp_rebuild_run), once through the resident fold ring with lane
- *     deferral (the default) and once through the lane queues: ring
- *     submission and waits from every P lane at once, deferred completions,
- *     relaunches after the ring idles out between runs.
+ *     deferral (the default; the loopback transport polling 20 us before it
+ *     sleeps) and once through the lane queues: ring submission and waits
+ *     from every P lane at once, deferred completions on the completion
+ *     threads, relaunches after the ring idles out between runs.
  * Every parity file is checked against a CPU XOR written here and every
  * rebuilt chunk against the lost one.  The C host layer and the engine's
  * host code are built with -fsanitize=thread (clang); device code is not. */
@@ -230,6 +231,8 @@ int main(int argc, char **argv)
     for (int ring = 1; ring >= 0; ring--) {
         const char *what = ring ? "protocol, fold ring" : "protocol, lane queues";
         bcp_task_set_fold_ring(ring);
+        /* the ring pass with the transport's spin-before-sleep waits */
+        bcp_task_set_fold_tuning("lb_spin_us", ring ? 20 : 0);
         remove_parity();
         bcp_run_stats st;
         int rc = bcp_gen_run(root, NT, items, NFILES, 3, NULL, NULL, &st);

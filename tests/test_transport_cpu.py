@@ -226,6 +226,34 @@ def _config(tmp_path, seed=5, nfiles=24):
     return root, files, items, contents
 
 
+@pytest.mark.timeout(200)
+@pytest.mark.parametrize("spin_us", [0, 3, 200])
+def test_loopback_spin_waits_give_the_same_files(bcp, oracle, cpu_hook, tmp_path, spin_us):
+    """The loopback transport's receives and fill sends poll for spin_us
+    before they sleep (lb_spin_us): gen (12 lanes, mixed sizes, multi-window
+    stripes) and a rebuild give the oracle's files whatever the budget."""
+    rng = np.random.default_rng(41)
+    files = _random_files(rng, 6, 30, 300_000)
+    files.append(("w/big", [0, 2], 4, [10 * MiB + 7, 3 * MiB]))  # two windows, the second replays
+    root = str(tmp_path)
+    items, contents = S.populate(root, 6, files, seed=41)
+    old = bcp.set_fold_tuning("lb_spin_us", spin_us)
+    try:
+        assert bcp.gen_run(root, 6, items, nlanes=12).errors == 0
+        for (path, holders, p, lens) in files:
+            assert S.read_file(S.parity_path(root, p, path)) == oracle.gen_parity_file(contents[path]), path
+        victim = 2
+        for (path, holders, p, lens) in files:
+            if victim in holders:
+                os.remove(S.chunk_path(root, victim, path))
+        assert bcp.rebuild_run(root, 6, victim, items).errors == 0
+        for (path, holders, p, lens) in files:
+            if victim in holders:
+                assert S.read_file(S.chunk_path(root, victim, path)) == bytes(contents[path][holders.index(victim)])
+    finally:
+        bcp.set_fold_tuning("lb_spin_us", old)
+
+
 @pytest.mark.timeout(120)
 @pytest.mark.parametrize("drain_row", [True, False], ids=["one-row-drain", "16KiB-truncating-drain"])
 def test_p_role_without_resources_drains_and_raises(bcp, oracle, cpu_hook, tmp_path, drain_row):

@@ -96,8 +96,25 @@ def cpu_now():
     return ru.ru_utime + ru.ru_stime, nr, us, cg
 
 
+TUNING_KEYS = {"piece": "pipe_piece_kib", "step": "pipe_step_kib", "depth": "defer_depth",
+               "completion": "completion_threads", "spin": "lb_spin_us"}
+
+
 def fold_setup(fold, hooks):
-    """Returns a context restore callable."""
+    """Returns a context restore callable.  <fold>%k=v+k=v: any fold with
+    protocol tuning (bcp_task_set_fold_tuning, TUNING_KEYS) around it, e.g.
+    cpu_reference%spin=20."""
+    if "%" in fold:
+        base, tun = fold.split("%", 1)
+        olds = [(TUNING_KEYS[k], bcp.set_fold_tuning(TUNING_KEYS[k], int(v)))
+                for k, v in (kv.split("=") for kv in tun.split("+"))]
+        inner = fold_setup(base, hooks)
+
+        def restore_pct():
+            inner()
+            for k, v in reversed(olds):
+                bcp.set_fold_tuning(k, v)
+        return restore_pct
     if fold.startswith("gpu_batched"):
         # gpu_batched[K]: K concurrent batches (bcp_task_set_fold_inflight)
         k = int(fold[len("gpu_batched"):] or 4)
@@ -112,8 +129,7 @@ def fold_setup(fold, hooks):
         # gpu_ring@piece=K+step=K+depth=D+completion=T: the ring with another pipelined shape
         # (bcp_task_set_fold_tuning: KiB per publish, smallest range, lane deferral depth,
         # completion threads)
-        keys = {"piece": "pipe_piece_kib", "step": "pipe_step_kib", "depth": "defer_depth",
-                "completion": "completion_threads"}
+        keys = TUNING_KEYS
         prev = bcp.set_fold_mode(bcp.FOLD_PIPELINED)
         prev_ring = bcp.set_fold_ring(True)
         olds = []
@@ -208,7 +224,7 @@ def measure(name, folds, rounds, run_once, verify_fn, nbytes, hooks, extra=None,
                 b = batching.setdefault(f, {"windows": 0, "launches": 0})
                 b["windows"] += w1 - w0
                 b["launches"] += l1 - l0
-            if (f in ("gpu_pipelined", "gpu_ring", "gpu_queues") or f.startswith("gpu_ring_w") or f.startswith("gpu_ring@")) \
+            if (f.split("%")[0] in ("gpu_pipelined", "gpu_ring", "gpu_queues") or f.startswith(("gpu_ring_w", "gpu_ring@"))) \
                     and r > 0:
                 b = batching.setdefault(f, {"windows": 0, "launches": 0})
                 b["windows"] += pw1 - pw0
@@ -229,8 +245,8 @@ def measure(name, folds, rounds, run_once, verify_fn, nbytes, hooks, extra=None,
                                          if cpu[f][-1][3] is not None else None),
                     throttled_periods=sum(c[1] for c in cpu[f][1:]),
                     throttled_ms_runs=[round(c[2], 1) for c in cpu[f]])
-        if (f in ("gpu_pipelined", "gpu_ring", "gpu_queues") or f.startswith(("gpu_ring_w", "gpu_ring@"))) and \
-                batching.get(f, {}).get("windows"):
+        if (f.split("%")[0] in ("gpu_pipelined", "gpu_ring", "gpu_queues") or f.startswith(("gpu_ring_w", "gpu_ring@"))) \
+                and batching.get(f, {}).get("windows"):
             line["range_folds_per_window"] = round(batching[f]["launches"] / batching[f]["windows"], 2)
         elif batching.get(f, {}).get("launches"):
             line["windows_per_launch"] = round(batching[f]["windows"] / batching[f]["launches"], 2)
