@@ -4,8 +4,9 @@ same test with a larger budget is a soak).  Each round draws a store (3..16
 targets), a worklist (widths 1..15, chunk lengths from 0 B to 4 MiB, now and
 then past the 10 MiB transfer window so sources replay their last window,
 quirk A3-q1; a chunk file missing after planning), the P-role fold
-(pipelined through the fold ring, pipelined on the lanes' queues, or
-batched) or the pipeline, the lanes, the padding rule on the
+(pipelined through the fold ring -- with a random deferral depth, number of
+completion threads, transport spin and range shape -- pipelined on the
+lanes' queues, or batched) or the pipeline, the lanes, the padding rule on the
 wire (implicit / the reference's) and the fold service width; every parity
 file must equal the oracle's (oracle.gen_parity_file, the reference's
 parity_generator restated).  Then a random target is lost and rebuilt by
@@ -66,6 +67,11 @@ def fuzz_rounds(bcp, oracle, tmp_path, budget, seed, engines):
     rng = np.random.default_rng(seed)
     prev = (bcp.set_fold_mode(bcp.FOLD_PIPELINED), bcp.set_rebuild_lanes(1), bcp.set_explicit_padding(bcp.PAD_AUTO),
             bcp.set_fold_inflight(1), bcp.set_fold_ring(True))
+    prev_tuning = {}
+    for k, probe in (("defer_depth", 1), ("completion_threads", 4), ("lb_spin_us", 0), ("pipe_piece_kib", 256),
+                     ("pipe_step_kib", 128)):
+        prev_tuning[k] = bcp.set_fold_tuning(k, probe)  # (read by setting; restored below)
+        bcp.set_fold_tuning(k, prev_tuning[k])
     t_end = time.monotonic() + budget
     rounds = files_done = 0
     seen = set()
@@ -87,6 +93,13 @@ def fuzz_rounds(bcp, oracle, tmp_path, budget, seed, engines):
             bcp.set_explicit_padding(pad)
             bcp.set_fold_inflight(int(rng.choice([1, 1, 2, 4])))
             what = f"seed {seed} round {rounds} {how} pad {pad}"
+            if how in ("pipelined", "procs"):  # the ring's deferral, completion threads, transport waits, range shape
+                tn = {"defer_depth": int(rng.integers(1, 5)), "completion_threads": int(rng.choice([0, 1, 4])),
+                      "lb_spin_us": int(rng.choice([0, 0, 20])), "pipe_piece_kib": int(rng.choice([64, 256, 1024])),
+                      "pipe_step_kib": int(rng.choice([32, 128]))}
+                for k, v in tn.items():
+                    bcp.set_fold_tuning(k, v)
+                what += f" {tn}"
             read_mode = int(rng.choice([bcp.READ_AUTO, bcp.READ_COPY, bcp.READ_DIRECT]))  # the pipeline's read path
             if how == "pipeline":
                 what += f" read_mode {read_mode}"
@@ -145,6 +158,8 @@ def fuzz_rounds(bcp, oracle, tmp_path, budget, seed, engines):
                 print(f"protocol fuzz: {rounds} rounds ...", flush=True)  # progress for long soaks
             shutil.rmtree(root, ignore_errors=True)
     finally:
+        for k, v in prev_tuning.items():
+            bcp.set_fold_tuning(k, v)
         bcp.set_fold_mode(prev[0])
         bcp.set_rebuild_lanes(prev[1])
         bcp.set_explicit_padding(prev[2])
