@@ -463,6 +463,10 @@ def config1_leg(a, device: int = 0) -> dict:
         # ... and what the device folds of rows in pinned host memory reach in the protocol's shape
         # (12 lanes, one stripe per launch, read in place), the fold alone: the GPU fold's own bound
         "gpu_fold_in_place_bound": zc,
+        "gpu_fold_over_link_ceiling": (round(gen["gpu_fold"]["GiBps"] / ((rd + wr) / (rd / (link["h2d_GBps"] * 1e9))
+                                                                         / GiB), 3) if link.get("h2d_GBps") else None),
+        "gpu_fold_over_in_place_bound": (round(gen["gpu_fold"]["GiBps"] / zc["GiBps"], 3)
+                                         if isinstance(zc, dict) and zc.get("GiBps") else None),
         "bytes": {"gen_read": rd, "gen_written": wr, "rebuild_read": rb_rd, "rebuild_written": rb_wr},
         "cpu_quota": cpu_quota(),
         "cpu_note": "cpu_s: this process's CPU seconds (all threads, user + system, getrusage) per warm run, median; "

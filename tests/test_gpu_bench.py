@@ -163,6 +163,10 @@ def test_bench_configs_block_one_rank(bcp):
     assert c1["bytes"]["gen_read"] == 96 * 3 * 512 * 1024
     assert c1["link"]["h2d_GBps"] > 0 and c1["gpu_fold_link_ceiling_GiBps"] > 0, c1
     assert c1["gpu_fold_in_place_bound"]["GiBps"] > 0 and c1["gpu_fold_in_place_bound"]["lanes"] == 12, c1
+    assert c1["gpu_fold_over_link_ceiling"] == round(
+        c1["gen"]["gpu_fold"]["GiBps"] / ((c1["bytes"]["gen_read"] + c1["bytes"]["gen_written"]) /
+                                          (c1["bytes"]["gen_read"] / (c1["link"]["h2d_GBps"] * 1e9)) / 1024 ** 3), 3)
+    assert c1["gpu_fold_over_in_place_bound"] > 0, c1
     part = line["configs"]["config5_partial"]
     assert part["verified"] is True and part["plan_ok"] is True and part["GiBps"] > 0, part
     assert part["stripes"] == max(1, line["e2e"]["per_rank"][0]["stripes"] // 10)
