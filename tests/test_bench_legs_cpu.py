@@ -112,6 +112,8 @@ FAKE_ROCPROF = textwrap.dedent('''\
         print("noise before the messages", flush=True)
         send({{"op": "gather_bus", "bus": "0000:00:00.0"}})
         assert recv()["bus_ids"] == ["0000:00:00.0"]
+        if mode == "midway":
+            sys.exit(3)
         send({{"op": "barrier"}})
         recv()
         send({{"op": "barrier"}})
@@ -178,13 +180,15 @@ def test_profiled_rank_patches_the_line(fake_rocprof, monkeypatch, capsys):
     assert line["value"] == round(58982400000 * 3 / 0.0252 / 1024 ** 3, 2)
 
 
-def test_profiled_rank_without_figures_times_in_process(fake_rocprof, monkeypatch, capsys):
-    """rocprofv3 exits with a status and no figures: the device phase runs in
-    the rank process without the profiler (here it cannot: no GPU, so it
-    fails loudly), and no line is made up."""
+@pytest.mark.parametrize("mode", ["fail", "midway"])
+def test_profiled_rank_without_figures_times_in_process(fake_rocprof, monkeypatch, capsys, mode):
+    """rocprofv3 exits with a status and no figures (before any message, or
+    after its first collective -- at one rank both can be retried): the
+    device phase runs in the rank process without the profiler (here it
+    cannot: no GPU, so it fails loudly), and no line is made up."""
     import bench
     from bcp_dist import Dist
-    monkeypatch.setenv("FAKE_ROCPROF_MODE", "fail")
+    monkeypatch.setenv("FAKE_ROCPROF_MODE", mode)  # no message at all / gone after its first collective
     monkeypatch.setattr(sys, "argv", ["bench.py", "--steps", "3", "--warmup", "1", "--no-e2e", "--no-cpu",
                                       "--no-configs"])
     a = bench.parse()
@@ -194,3 +198,31 @@ def test_profiled_rank_without_figures_times_in_process(fake_rocprof, monkeypatc
     out, err = capsys.readouterr()
     assert not [x for x in out.splitlines() if x.startswith("{")]
     assert "without the profiler" in err
+
+
+def test_profiled_rank_helper_lost_midway_fails_an_n_rank_job(fake_rocprof, monkeypatch, capsys):
+    """In an N-rank job a helper gone after its first collective cannot be
+    replaced (the other ranks are inside the job's collectives with it): the
+    rank returns the helper's status, no line, no in-process retry."""
+    import bench
+
+    class TwoRanks:
+        world, rank, local_rank = 2, 0, 0
+
+        def gather(self, x):
+            return [x, "0000:01:00.0"]
+
+        def barrier(self):
+            pass
+
+        def close(self):
+            pass
+    monkeypatch.setenv("FAKE_ROCPROF_MODE", "midway")
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--steps", "3", "--warmup", "1", "--no-e2e", "--no-cpu",
+                                      "--no-configs"])
+    a = bench.parse()
+    a.stripes = 64
+    assert bench.profiled_rank(a, TwoRanks()) == 3
+    out, err = capsys.readouterr()
+    assert not [x for x in out.splitlines() if x.startswith("{")]
+    assert "in the middle of the run" in err
