@@ -97,7 +97,9 @@ def cpu_now():
 
 
 TUNING_KEYS = {"piece": "pipe_piece_kib", "step": "pipe_step_kib", "depth": "defer_depth",
-               "completion": "completion_threads", "spin": "lb_spin_us"}
+               "completion": "completion_threads", "spin": "lb_spin_us", "workers": "ring_workers"}
+# keys that take effect on rings made from now on: the current rings end (bcp_task_shutdown)
+RING_REMAKE = {"ring_workers"}
 
 
 def fold_setup(fold, hooks):
@@ -136,10 +138,14 @@ def fold_setup(fold, hooks):
         for kv in fold.split("@", 1)[1].split("+"):
             k, v = kv.split("=")
             olds.append((keys[k], bcp.set_fold_tuning(keys[k], int(v))))
+        if any(k in RING_REMAKE for k, _ in olds):
+            bcp.task_shutdown()
 
         def restore_t():
             for k, v in reversed(olds):
                 bcp.set_fold_tuning(k, v)
+            if any(k in RING_REMAKE for k, _ in olds):
+                bcp.task_shutdown()
             bcp.set_fold_ring(prev_ring)
             bcp.set_fold_mode(prev)
         return restore_t
