@@ -203,6 +203,12 @@ def measure(name, folds, rounds, run_once, verify_fn, nbytes, hooks, extra=None,
             if prepare:
                 prepare()  # outside the timed region (removing old parity files)
             restore = fold_setup(f, hooks)
+            if any(TUNING_KEYS.get(kv.split("=")[0]) in RING_REMAKE
+                   for kv in (f.split("@", 1)[1].split("+") if "@" in f else [])):
+                # the rings (and with them the P roles' pooled rows) were remade: one untimed run first
+                run_once()
+                if prepare:
+                    prepare()
             try:
                 w0, l0 = bcp.fold_stats()
                 pw0, pr0 = bcp.pipe_stats()
