@@ -124,7 +124,7 @@ int bcp_task_set_fold_tuning(const char *key, int value)
     pthread_mutex_lock(&g_mu);
     if (!strcmp(key, "ring_workers") && value >= 1 && value <= 1024) {
         prev = g_ring_workers;
-        g_ring_workers = value; /* rings made from now on (bcp_task_shutdown ends the current ones) */
+        g_ring_workers = value; /* rings made from now on: the current ones end below */
     } else if (!strcmp(key, "pipe_piece_kib") && value >= 4 && value <= 10240) {
         prev = (int)(g_pipe_piece >> 10);
         __atomic_store_n(&g_pipe_piece, (size_t)value << 10, __ATOMIC_RELAXED);
@@ -142,7 +142,25 @@ int bcp_task_set_fold_tuning(const char *key, int value)
     } else {
         prev = -EINVAL;
     }
+    /* a new worker count: the devices' rings end now (no fold may be in
+     * flight: between runs), the next fold makes them anew */
+    bcp_ring *old_ring[BCPF_MAX_DEVICES] = {0};
+    if (!strcmp(key, "ring_workers") && prev >= 0 && prev != value)
+        for (int d = 0; d < BCPF_MAX_DEVICES; d++) {
+            old_ring[d] = g_ring[d];
+            g_ring[d] = NULL;
+            g_ring_rc[d] = 0;
+            if (old_ring[d]) {
+                uint64_t a = 0, b = 0;
+                (void)bcp_ring_stats(old_ring[d], &a, &b);
+                g_ring_pieces += a;
+                g_ring_launches += b;
+            }
+        }
     pthread_mutex_unlock(&g_mu);
+    for (int d = 0; d < BCPF_MAX_DEVICES; d++)
+        if (old_ring[d])
+            (void)bcp_ring_destroy(old_ring[d]);
     return prev;
 }
 

@@ -191,7 +191,8 @@ int bcp_task_set_lane_deferral(int on);
  * before its list's end is reported: MPI barrier, DB sync, exit). */
 void bcp_task_flush(void);
 /* Tools and A/B runs: the P role's fold shape.  "ring_workers" (16: worker
- * workgroups of rings made from now on), "pipe_piece_kib" (256: bytes a
+ * workgroups of the rings; a new value ends the current rings -- call it
+ * between runs -- and the next fold makes new ones), "pipe_piece_kib" (256: bytes a
  * source reads between two publishes of its row), "pipe_step_kib" (128: the
  * smallest range folded before the window is complete, at least a quarter
  * window), "defer_depth" (1: lane deferral depth of libbcp's runners,

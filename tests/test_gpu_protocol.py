@@ -172,6 +172,28 @@ def _ring_vs_queues(bcp, oracle, tmp_path):
         bcp.set_fold_ring(prev)
 
 
+def test_ring_worker_count_change_remakes_the_rings(bcp, oracle, tmp_path):
+    """bcp_task_set_fold_tuning("ring_workers") between runs ends the current
+    rings; the next fold makes new ones with that many workers (1, 8, 40,
+    then the default): every run's parity files exact."""
+    root = str(tmp_path)
+    files = [(f"w/f{i}", [t for t in range(4) if t != i % 4], i % 4, [400 * KiB + 7 * i, 512 * KiB, 64 * KiB])
+             for i in range(16)]
+    items, contents = S.populate(root, 4, files, seed=12)
+    old = bcp.set_fold_tuning("ring_workers", 16)
+    try:
+        for w in (1, 8, 40, old):
+            bcp.set_fold_tuning("ring_workers", w)
+            p0, l0 = bcp.ring_stats()
+            assert bcp.gen_run(root, 4, items).errors == 0, w
+            p1, l1 = bcp.ring_stats()
+            assert p1 > p0 and l1 > l0, (w, p0, p1, l0, l1)
+            for (path, _, p, _) in files:
+                assert S.read_file(S.parity_path(root, p, path)) == oracle.gen_parity_file(contents[path]), (w, path)
+    finally:
+        bcp.set_fold_tuning("ring_workers", old)
+
+
 @pytest.mark.parametrize("completion", [4, 0])
 def test_deferred_parity_write_failure_is_sticky(bcp, oracle, tmp_path, completion):
     """Through the fold ring with lane deferral, a parity write fails (ENOSPC,

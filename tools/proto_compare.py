@@ -98,7 +98,7 @@ def cpu_now():
 
 TUNING_KEYS = {"piece": "pipe_piece_kib", "step": "pipe_step_kib", "depth": "defer_depth",
                "completion": "completion_threads", "spin": "lb_spin_us", "workers": "ring_workers"}
-# keys that take effect on rings made from now on: the current rings end (bcp_task_shutdown)
+# keys whose new value ends the current rings (the next fold makes new ones)
 RING_REMAKE = {"ring_workers"}
 
 
@@ -138,14 +138,10 @@ def fold_setup(fold, hooks):
         for kv in fold.split("@", 1)[1].split("+"):
             k, v = kv.split("=")
             olds.append((keys[k], bcp.set_fold_tuning(keys[k], int(v))))
-        if any(k in RING_REMAKE for k, _ in olds):
-            bcp.task_shutdown()
 
         def restore_t():
             for k, v in reversed(olds):
                 bcp.set_fold_tuning(k, v)
-            if any(k in RING_REMAKE for k, _ in olds):
-                bcp.task_shutdown()
             bcp.set_fold_ring(prev_ring)
             bcp.set_fold_mode(prev)
         return restore_t
@@ -203,9 +199,9 @@ def measure(name, folds, rounds, run_once, verify_fn, nbytes, hooks, extra=None,
             if prepare:
                 prepare()  # outside the timed region (removing old parity files)
             restore = fold_setup(f, hooks)
-            if any(TUNING_KEYS.get(kv.split("=")[0]) in RING_REMAKE
-                   for kv in (f.split("@", 1)[1].split("+") if "@" in f else [])):
-                # the rings (and with them the P roles' pooled rows) were remade: one untimed run first
+            remake = any(TUNING_KEYS.get(kv.split("=")[0]) in RING_REMAKE
+                         for kv in (f.split("@", 1)[1].split("+") if "@" in f else []))
+            if remake:  # a new ring: made and launched by one untimed run
                 run_once()
                 if prepare:
                     prepare()
@@ -229,6 +225,13 @@ def measure(name, folds, rounds, run_once, verify_fn, nbytes, hooks, extra=None,
                         acc[k] = acc.get(k, 0) + v
             finally:
                 restore()
+            if remake:  # the default ring again, made outside the next fold's timing
+                if prepare:
+                    prepare()
+                bcp.set_fold_ring(True)
+                prev_mode = bcp.set_fold_mode(bcp.FOLD_PIPELINED)
+                run_once()
+                bcp.set_fold_mode(prev_mode)
             if st.errors:
                 raise RuntimeError(f"{name}/{f}: {st.errors} rank errors")
             times[f].append(dt)
