@@ -109,7 +109,7 @@ static int g_ring_workers = 16;
  * row has at least max(g_pipe_step, window / 4) more bytes. */
 static size_t g_pipe_piece = (size_t)256 << 10;
 static size_t g_pipe_step = (size_t)128 << 10;
-static int g_defer_depth = 1;
+static int g_defer_depth = 2;
 static int g_completion_threads = 4;
 
 size_t bcpf_watch_piece(void) { return __atomic_load_n(&g_pipe_piece, __ATOMIC_RELAXED); }

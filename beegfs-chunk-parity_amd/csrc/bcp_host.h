@@ -58,7 +58,7 @@ int bcpi_sock_transport_is(const bcp_transport_ops *ops);
 int bcpi_fold_inflight(void);
 /* PIPELINED folds through the resident fold ring (bcp_task_set_fold_ring). */
 int bcpi_fold_ring(void);
-/* Lane deferral depth of libbcp's runners (1; bcp_task_set_fold_tuning
+/* Lane deferral depth of libbcp's runners (2; bcp_task_set_fold_tuning
  * "defer_depth"). */
 int bcpi_defer_depth(void);
 #define BCP_DEFER_MAX 4

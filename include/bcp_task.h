@@ -195,7 +195,7 @@ void bcp_task_flush(void);
  * between runs -- and the next fold makes new ones), "pipe_piece_kib" (256: bytes a
  * source reads between two publishes of its row), "pipe_step_kib" (128: the
  * smallest range folded before the window is complete, at least a quarter
- * window), "defer_depth" (1: lane deferral depth of libbcp's runners,
+ * window), "defer_depth" (2: lane deferral depth of libbcp's runners,
  * 0..4), "completion_threads" (4: threads completing deferred P tasks,
  * 0..16; 0 = each lane completes its own), "lb_spin_us" (0: how long a
  * blocked loopback receive or fill send polls before it sleeps, 0..1000).  Returns the previous value or -EINVAL. */
