@@ -116,6 +116,8 @@ def parse():
                     help="pipeline read paths timed end to end, interleaved; the first is the headline")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-configs", action="store_true", help="skip the config-1 protocol leg (rank 0)")
+    ap.add_argument("--c1-first", action=argparse.BooleanOptionalAction, default=False,
+                    help="run the config-1 protocol leg before the e2e and CPU-baseline legs")
     ap.add_argument("--c1-files", type=int, default=1333, help="config 1: files (3 chunks of 512 KiB each)")
     ap.add_argument("--c1-reps", type=int, default=7, help="config 1: warm rounds per leg (after one cold round)")
     ap.add_argument("--c5-reps", type=int, default=3,
@@ -717,6 +719,14 @@ def finish(a, d, dev: dict) -> tuple:
                          "pct_hbm_peak": round(100.0 * bytes_per_step / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 2),
                          "verified": bool(verified)})
 
+    # BASELINE config 1 end to end (rank 0; the reference's xor_parity as the
+    # P-role fold beside the GPU fold and the pipeline, same store); first
+    # with --c1-first, before the e2e store's churn and the CPU baseline's
+    # all-core run (the other ranks wait at the barrier)
+    c1 = None
+    if a.c1_first:
+        c1 = run_leg("config1", config1_leg, a, dev["device"]) if d.rank == 0 and not a.no_configs else None
+        d.barrier()
     # end to end from chunk files (every rank on its own GPU, all at once;
     # e2e_leg keeps every rank's collective calls in step whatever fails)
     e2e = None
@@ -726,9 +736,8 @@ def finish(a, d, dev: dict) -> tuple:
     # other ranks wait at the barrier
     cpu = run_leg("cpu_baseline", cpu_baseline, a, N, C, lens_all if a.mode == "mixed" else None) \
         if d.rank == 0 and not a.no_cpu else None
-    # BASELINE config 1 end to end (rank 0; the reference's xor_parity as the
-    # P-role fold beside the GPU fold and the pipeline, same store)
-    c1 = run_leg("config1", config1_leg, a, dev["device"]) if d.rank == 0 and not a.no_configs else None
+    if not a.c1_first:
+        c1 = run_leg("config1", config1_leg, a, dev["device"]) if d.rank == 0 and not a.no_configs else None
     d.barrier()
 
     if d.rank == 0:
