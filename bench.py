@@ -33,9 +33,10 @@ process, which stays the job's member), so frac_rocprof is the rocprof
 average of the SAME timed launches (roofline.live_profile:
 event_over_rocprof), and nothing else runs under the profiler: the rank
 process then runs the legs itself and the PMC passes (FETCH_SIZE,
-WRITE_SIZE, runs of their own) of the same workload for traffic.  With --no-prof, or when a pass fails, the committed profile set
-of the workload (profiles/CURRENT_SET, profiles/**/*pmc*.json,
-tools/pmc_summary.py) stands in, reported as roofline.committed_set.
+WRITE_SIZE, runs of their own) of the same workload for traffic.  With
+--no-prof, or when a pass fails, the committed profile set of the workload
+(profiles/CURRENT_SET, profiles/**/*pmc*.json, tools/pmc_summary.py) stands
+in, reported as roofline.committed_set.
 The legs beside the device timing are bench_legs.py's, each behind run_leg.
 n_gpus counts DISTINCT devices (PCI bus ids gathered over gloo): ranks that
 share a GPU are flagged shared_gpu instead of being reported as more GPUs.
