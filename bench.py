@@ -119,6 +119,8 @@ def parse():
     ap.add_argument("--no-configs", action="store_true", help="skip the config-1 protocol leg (rank 0)")
     ap.add_argument("--c1-first", action=argparse.BooleanOptionalAction, default=False,
                     help="run the config-1 protocol leg before the e2e and CPU-baseline legs")
+    ap.add_argument("--c1-legs", default="reference_fold,gpu_fold,pipeline",
+                    help="config-1 legs (the two folds always run; the pipeline can be left out for A/B runs)")
     ap.add_argument("--c1-files", type=int, default=1333, help="config 1: files (3 chunks of 512 KiB each)")
     ap.add_argument("--c1-reps", type=int, default=7, help="config 1: warm rounds per leg (after one cold round)")
     ap.add_argument("--c5-reps", type=int, default=3,

@@ -350,7 +350,8 @@ def config1_leg(a, device: int = 0) -> dict:
             bcp.set_xor_hook(None)
             bcp.set_fold_mode(prev)
 
-    legs = ["reference_fold", "gpu_fold", "pipeline"]
+    # the two folds always; the pipeline unless --c1-legs leaves it out (A/B)
+    legs = ["reference_fold", "gpu_fold"] + (["pipeline"] if "pipeline" in a.c1_legs.split(",") else [])
     pl_timing = {}
     link, zc = {}, {}
     gen_t = {x: [] for x in legs}
@@ -382,10 +383,10 @@ def config1_leg(a, device: int = 0) -> dict:
             zc = zero_copy_fold_rate(device)
         except Exception as e:
             link, zc = {"error": f"{type(e).__name__}: {e}"}, {}
-        pl = bcp.Pipeline(device=device)
+        pl = bcp.Pipeline(device=device) if "pipeline" in legs else None
         runs = 1 + max(1, a.c1_reps)
         for r in range(runs):
-            for leg in legs[r % 3:] + legs[:r % 3]:
+            for leg in legs[r % len(legs):] + legs[:r % len(legs)]:
                 reset_parity()
                 c0 = proc_cpu_s()
                 t0 = time.perf_counter()
@@ -405,7 +406,7 @@ def config1_leg(a, device: int = 0) -> dict:
         prev_lanes = bcp.set_rebuild_lanes(1)
         try:
             for r in range(runs):
-                for leg in legs[r % 3:] + legs[:r % 3]:
+                for leg in legs[r % len(legs):] + legs[:r % len(legs)]:
                     drop_victim()
                     c0 = proc_cpu_s()
                     t0 = time.perf_counter()
@@ -443,8 +444,9 @@ def config1_leg(a, device: int = 0) -> dict:
     gen = {leg: summary(gen_t[leg], gen_c[leg], rd + wr, ok[leg]) for leg in legs}
     reb = {leg: summary(reb_t[leg], reb_c[leg], rb_rd + rb_wr, rok[leg]) for leg in legs}
     gen["reference_fold"]["kind"] = reb["reference_fold"]["kind"] = kind
-    gen["pipeline"]["last_run_timing"] = pl_timing.get("gen")
-    reb["pipeline"]["last_run_timing"] = pl_timing.get("rebuild")
+    if "pipeline" in legs:
+        gen["pipeline"]["last_run_timing"] = pl_timing.get("gen")
+        reb["pipeline"]["last_run_timing"] = pl_timing.get("rebuild")
     return {
         "workload": f"config1: beegfs-parity-gen --complete, {NT} loopback storage-target ranks, {nfiles} files x 3 "
                     f"x {C // KiB} KiB chunks ({nfiles * 3 // NT} per rank), P rotating over the target left out",
@@ -453,7 +455,8 @@ def config1_leg(a, device: int = 0) -> dict:
         "gen": gen,
         "rebuild": {"target": VICTIM, "files": len(lost), **reb},
         "gpu_fold_over_reference_fold": round(gen["gpu_fold"]["GiBps"] / gen["reference_fold"]["GiBps"], 3),
-        "pipeline_over_reference_fold": round(gen["pipeline"]["GiBps"] / gen["reference_fold"]["GiBps"], 3),
+        "pipeline_over_reference_fold": (round(gen["pipeline"]["GiBps"] / gen["reference_fold"]["GiBps"], 3)
+                                         if "pipeline" in gen else None),
         "rebuild_gpu_fold_over_reference_fold": round(reb["gpu_fold"]["GiBps"] / reb["reference_fold"]["GiBps"], 3),
         # every chunk byte a GPU fold folds crosses the host-to-device link once (parity comes back
         # on the other direction): the gen rate it cannot pass on this link
