@@ -970,8 +970,21 @@ static int submit_desc(bcp_queue *q, const bcp_stripe *stripes, uint32_t nstripe
     int rc = ring_acquire(q, bytes, &slot);
     if (rc) return rc;
     slot->rec_ok = false;  // its tables and records are about to be overwritten
-    memcpy(slot->host, stripes, (size_t)nstripes * sizeof(bcp_stripe));
-    memcpy((char *)slot->host + off_src, sources, (size_t)nsources * sizeof(bcp_source));
+    // (large tables -- config 3's 100,000 sources, 2 MB -- copied by the
+    // staging pool: this runs before the kernel whenever the queue is idle)
+    char *const hs = (char *)slot->host;
+    const size_t sb = (size_t)nstripes * sizeof(bcp_stripe), ob = (size_t)nsources * sizeof(bcp_source);
+    const uint32_t pieces = (uint32_t)((sb + ob) >> 16) + 1;  // 64 KiB pieces
+    par_for(pieces, 8, [&](uint32_t lo, uint32_t hi) {
+      for (uint32_t i = lo; i < hi; i++) {
+        const size_t a = (size_t)i << 16, b = std::min(sb + ob, a + ((size_t)1 << 16));
+        if (a < sb) memcpy(hs + a, (const char *)stripes + a, std::min(b, sb) - a);
+        if (b > sb) {
+          const size_t a2 = std::max(a, sb);
+          memcpy(hs + off_src + (a2 - sb), (const char *)sources + (a2 - sb), b - a2);
+        }
+      }
+    });
     char *d = nullptr;
     if ((rc = stage_tables(q, slot, bytes, (size_t)e->tuning.table_host_max, &d))) return rc;
     StreamArgs a{};
