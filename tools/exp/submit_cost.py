@@ -28,12 +28,16 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--stripes", type=int, default=12500, help="config-2 volume budget as bench.py computes it")
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--uniform", action="store_true",
+                    help="bench.py --mode rebuild's batch instead: --stripes x 8 x 512 KiB, one pointer table")
     a = ap.parse_args()
     N, C = 8, 512 * KiB
     rng = np.random.default_rng(3)
     budget = a.stripes * N * C
     lens_all, tot = [], 0
-    while tot < budget:
+    if a.uniform:
+        lens_all = [np.full(N, C, dtype=np.int64) for _ in range(a.stripes)]
+    while tot < budget and not a.uniform:
         ls = np.exp(rng.uniform(np.log(64 * KiB), np.log(4 * 1024 * KiB), size=N)).astype(np.int64)
         lens_all.append(ls)
         tot += int(ls.sum())
@@ -73,7 +77,7 @@ def main():
         q.sync()
         first_ev.append(q.elapsed_ms(0, 1))
         next_ev.append(q.elapsed_ms(1, 2))
-    print(json.dumps({"stripes": len(stripes), "sources": len(sources),
+    print(json.dumps({"uniform": a.uniform, "stripes": len(stripes), "sources": len(sources),
                       "submit_ms_queue_idle": [round(x * 1e3, 3) for x in idle],
                       "submit_ms_kernel_in_flight": [round(x * 1e3, 3) for x in busy],
                       "event_ms_first_after_idle": [round(x, 3) for x in first_ev],
