@@ -199,22 +199,41 @@ static int desc_vecs_for(const bcp_engine *e, uint64_t tiles8);
 
 static bool aligned16(uint64_t x) { return (x & 15u) == 0; }
 
+// A slot none of whose kernels is still running.
+static bool slot_idle(DescSlot *s) { return !s->used || hipEventQuery(s->done) == hipSuccess; }
+
+// Grow an idle slot's tables to at least `bytes`.
+static int slot_grow(DescSlot *s, size_t bytes) {
+  s->rec_ok = false;
+  if (s->host) HIP_RC(hipHostFree(s->host));
+  if (s->dev) HIP_RC(hipFree(s->dev));
+  s->host = s->dev = nullptr;
+  s->cap = 0;
+  size_t cap = 64 * 1024;
+  while (cap < bytes) cap *= 2;
+  HIP_RC(hipHostMalloc(&s->host, cap, hipHostMallocDefault));
+  HIP_RC(hipMalloc(&s->dev, cap));
+  s->cap = cap;
+  return 0;
+}
+
 // Reserve a ring slot of at least `bytes`; waits only if that slot's
-// previous kernel has not finished (kRingSlots submissions ago).
+// previous kernel has not finished (kRingSlots submissions ago).  A slot
+// that must grow grows the queue's other idle slots with it: a queue's
+// batches are alike, and a slot first reached later (the fourth submission:
+// a block's first timed launch after three warm-up ones) would otherwise
+// allocate on the path to its kernel.
 static int ring_acquire(bcp_queue *q, size_t bytes, DescSlot **out) {
   DescSlot *s = &q->ring[q->next_slot];
   q->next_slot = (q->next_slot + 1) % kRingSlots;
   if (s->used) HIP_RC(hipEventSynchronize(s->done));
   if (s->cap < bytes) {
-    s->rec_ok = false;
-    if (s->host) HIP_RC(hipHostFree(s->host));
-    if (s->dev) HIP_RC(hipFree(s->dev));
-    s->host = s->dev = nullptr;
-    size_t cap = 64 * 1024;
-    while (cap < bytes) cap *= 2;
-    HIP_RC(hipHostMalloc(&s->host, cap, hipHostMallocDefault));
-    HIP_RC(hipMalloc(&s->dev, cap));
-    s->cap = cap;
+    int rc = slot_grow(s, bytes);
+    if (rc) return rc;
+    for (int j = 0; j < kRingSlots; j++) {
+      DescSlot *o = &q->ring[j];
+      if (o != s && o->cap < bytes && slot_idle(o) && (rc = slot_grow(o, bytes))) return rc;
+    }
   }
   if (!s->done) HIP_RC(hipEventCreateWithFlags(&s->done, hipEventDisableTiming));
   if (!s->copied) HIP_RC(hipEventCreateWithFlags(&s->copied, hipEventDisableTiming));
@@ -1079,13 +1098,19 @@ static int submit_desc(bcp_queue *q, const bcp_stripe *stripes, uint32_t nstripe
                      slot->rec_len == bytes && slot->tiles_cap >= acc && memcmp(slot->rec_copy, h, bytes) == 0;
   slot->rec_ok = false;
   if (slot->tiles_cap < acc) {
-    // the slot's previous kernels have finished (ring_acquire waited)
-    if (slot->tiles) HIP_RC(hipFree(slot->tiles));
-    slot->tiles = nullptr;
-    slot->tiles_cap = 0;
+    // the slot's previous kernels have finished (ring_acquire waited); the
+    // queue's other idle slots grow with it (as ring_acquire grows tables)
     const size_t cap = std::max<size_t>(acc + acc / 4, 1u << 12);
-    HIP_RC(hipMalloc((void **)&slot->tiles, cap * sizeof(DescTile)));
-    slot->tiles_cap = cap;
+    for (int j = 0; j < kRingSlots; j++) {
+      DescSlot *o = &q->ring[j];
+      if (o != slot && (o->tiles_cap >= acc || !slot_idle(o))) continue;
+      o->rec_ok = false;
+      if (o->tiles) HIP_RC(hipFree(o->tiles));
+      o->tiles = nullptr;
+      o->tiles_cap = 0;
+      HIP_RC(hipMalloc((void **)&o->tiles, cap * sizeof(DescTile)));
+      o->tiles_cap = cap;
+    }
   }
   int grid = desc_grid_for(e);
   if ((uint32_t)grid > acc) grid = (int)acc;
